@@ -1,0 +1,1036 @@
+// oracle.cpp -- CPU restatement of the reference pattern/sequence engine.
+//
+// TEST INFRASTRUCTURE ONLY (the parity checker for libsiddhi_hip.so): only tests/,
+// __graft_entry__.smoke() and bench.py's cpu_baseline may load this library.
+//
+// Pinned by the reference's own known-answer tests, transcribed into tests/golden/*.json by
+// tests/golden/extract_reference_tests.py (EveryPatternTestCase, WithinPatternTestCase,
+// CountPatternTestCase, LogicalPatternTestCase, ComplexPatternTestCase, SequenceTestCase,
+// PatternPartitionTestCase, SequencePartitionTestCase). The Java engine itself cannot run in this
+// image (no JDK), so no outputs of the reference were generated here.
+//
+// Abbreviation: state/ = modules/siddhi-core/src/main/java/org/wso2/siddhi/core/query/input/stream/state/
+//
+// The object model is restated literally: StateEvent objects shared between pending lists,
+// shallow every-clones (state/../event/state/StateEventCloner.java:46-58), StreamEvent chains for
+// count slots (event/state/StateEvent.java:208-236), two-phase newAndEvery -> pending promotion.
+// Garbage is reclaimed by a mark/sweep over all pending lists (the JVM's job in the reference).
+#include "oracle.h"
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <list>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+using i64 = int64_t;
+
+// ------------------------------------------------------------------------------------------
+// IR (siddhi_amd/ir.py)
+// ------------------------------------------------------------------------------------------
+enum { T_INT, T_LONG, T_FLOAT, T_DOUBLE, T_BOOL, T_STRING };
+enum { OP_CONST = 1, OP_ATTR, OP_IS_NULL, OP_STREAM_IS_NULL, OP_CMP, OP_AND, OP_OR, OP_NOT, OP_ARITH };
+enum { CMP_EQ, CMP_NE, CMP_GT, CMP_GE, CMP_LT, CMP_LE };
+enum { AR_ADD, AR_SUB, AR_MUL, AR_DIV, AR_MOD };
+enum { K_STREAM, K_COUNT, K_LOGICAL };
+enum { L_AND, L_OR };
+enum { Q_PATTERN, Q_SEQUENCE };
+enum { R_SINGLE, R_MULTI };
+enum { N_STREAM, N_NEXT, N_EVERY, N_LOGICAL, N_COUNT };
+
+struct Insn {
+  int op, lt, rt, res;
+  i64 a, b, imm;
+};
+using Code = std::vector<Insn>;
+
+struct StateDef {
+  int kind, stream, is_start, min, max, ltype, partner, next_pre, next_every, within_every,
+      callback, this_last, has_selector;
+  std::vector<Code> filters;
+};
+struct RecvDef {
+  int stream, kind;
+  std::vector<int> procs;
+};
+struct NodeDef {
+  int type, a, b, pre;
+};
+struct QueryDef {
+  int type;
+  i64 within;
+  int partition;
+  std::vector<StateDef> states;
+  std::vector<int> start_ids;
+  std::vector<RecvDef> recvs;
+  std::vector<NodeDef> nodes;
+};
+struct PartKey {
+  int stream;
+  Code code;
+};
+struct PartDef {
+  std::vector<PartKey> keys;
+  std::vector<int> queries;
+};
+struct Program {
+  std::vector<std::vector<int>> stream_types;
+  std::vector<QueryDef> queries;
+  std::vector<PartDef> parts;
+};
+
+struct Reader {
+  const i64* w;
+  size_t n, i = 0;
+  i64 next() {
+    if (i >= n) throw std::runtime_error("IR blob truncated");
+    return w[i++];
+  }
+};
+
+Code read_code(Reader& r) {
+  Code c(r.next());
+  for (auto& ins : c) {
+    i64 w0 = r.next();
+    ins.op = w0 & 0xff;
+    ins.lt = (w0 >> 8) & 0xff;
+    ins.rt = (w0 >> 16) & 0xff;
+    ins.res = (w0 >> 24) & 0xff;
+    ins.a = r.next();
+    ins.b = r.next();
+    ins.imm = r.next();
+  }
+  return c;
+}
+
+Program parse_ir(const void* blob, size_t len) {
+  if (len < 16 || std::memcmp(blob, "SDHIR001", 8) != 0) throw std::runtime_error("bad IR magic");
+  Reader r{reinterpret_cast<const i64*>(static_cast<const char*>(blob) + 8), (len - 8) / 8};
+  Program p;
+  if (r.next() != 1) throw std::runtime_error("unsupported IR version");
+  p.stream_types.resize(r.next());
+  for (auto& st : p.stream_types) {
+    st.resize(r.next());
+    for (auto& t : st) t = (int)r.next();
+  }
+  i64 nstr = r.next();
+  for (i64 k = 0; k < nstr; ++k) {
+    i64 nb = r.next();
+    for (i64 j = 0; j < (nb + 7) / 8; ++j) r.next();
+  }
+  p.queries.resize(r.next());
+  for (auto& q : p.queries) {
+    q.type = (int)r.next();
+    q.within = r.next();
+    q.states.resize(r.next());
+    q.partition = (int)r.next();
+    r.next();  // selector present
+    for (auto& s : q.states) {
+      s.kind = (int)r.next(); s.stream = (int)r.next(); s.is_start = (int)r.next();
+      s.min = (int)r.next(); s.max = (int)r.next(); s.ltype = (int)r.next();
+      s.partner = (int)r.next(); s.next_pre = (int)r.next(); s.next_every = (int)r.next();
+      s.within_every = (int)r.next(); s.callback = (int)r.next(); s.this_last = (int)r.next();
+      s.has_selector = (int)r.next();
+      s.filters.resize(r.next());
+      for (auto& f : s.filters) f = read_code(r);
+    }
+    q.start_ids.resize(r.next());
+    for (auto& x : q.start_ids) x = (int)r.next();
+    q.recvs.resize(r.next());
+    for (auto& rv : q.recvs) {
+      rv.stream = (int)r.next(); rv.kind = (int)r.next();
+      rv.procs.resize(r.next());
+      for (auto& x : rv.procs) x = (int)r.next();
+    }
+    q.nodes.resize(r.next());
+    for (auto& n : q.nodes) {
+      n.type = (int)r.next(); n.a = (int)r.next(); n.b = (int)r.next(); n.pre = (int)r.next();
+    }
+    i64 nout = r.next();
+    for (i64 k = 0; k < nout; ++k) read_code(r);
+  }
+  p.parts.resize(r.next());
+  for (auto& pd : p.parts) {
+    pd.keys.resize(r.next());
+    for (auto& k : pd.keys) {
+      k.stream = (int)r.next();
+      k.code = read_code(r);
+    }
+    pd.queries.resize(r.next());
+    for (auto& x : pd.queries) x = (int)r.next();
+  }
+  return p;
+}
+
+// ------------------------------------------------------------------------------------------
+// Event model (event/stream/StreamEvent.java, event/state/StateEvent.java)
+// ------------------------------------------------------------------------------------------
+struct InEvent {     // an input event (values live here; StreamEvents are per-use copies)
+  int stream;
+  i64 ts;
+  std::vector<i64> vals;
+  std::vector<uint8_t> nulls;
+};
+
+struct StreamEvent {  // copyStreamEvent result: same values, own `next` link
+  i64 seq;
+  i64 ts;
+  StreamEvent* next = nullptr;
+  bool mark = false;
+};
+
+struct StateEvent {
+  std::vector<StreamEvent*> slots;
+  i64 ts = -1;
+  bool mark = false;
+};
+
+struct Heap {
+  std::vector<StreamEvent*> sev;
+  std::vector<StateEvent*> stev;
+  size_t last_live = 0;
+  ~Heap() {
+    for (auto* p : sev) delete p;
+    for (auto* p : stev) delete p;
+  }
+  StreamEvent* copy(i64 seq, i64 ts) {
+    auto* e = new StreamEvent{seq, ts};
+    sev.push_back(e);
+    return e;
+  }
+  StateEvent* state(size_t n) {
+    auto* s = new StateEvent;
+    s->slots.assign(n, nullptr);
+    stev.push_back(s);
+    return s;
+  }
+};
+
+// Java semantics helpers ----------------------------------------------------------------------
+struct Value {
+  int type = T_INT;
+  bool null = true;
+  i64 i = 0;     // int/long/bool/string-id
+  float f = 0;
+  double d = 0;
+};
+
+Value mk_null() { return Value(); }
+
+float as_f(const Value& v) {  // Number.floatValue() / binary numeric promotion to float
+  switch (v.type) {
+    case T_INT: return (float)(int32_t)v.i;
+    case T_LONG: return (float)v.i;
+    case T_FLOAT: return v.f;
+    default: return (float)v.d;
+  }
+}
+double as_d(const Value& v) {
+  switch (v.type) {
+    case T_INT: return (double)(int32_t)v.i;
+    case T_LONG: return (double)v.i;
+    case T_FLOAT: return (double)v.f;
+    default: return v.d;
+  }
+}
+i64 as_l(const Value& v) { return v.i; }  // only int/long reach here
+
+template <class T>
+bool cmp_op(int op, T a, T b) {
+  switch (op) {
+    case CMP_EQ: return a == b;
+    case CMP_NE: return a != b;
+    case CMP_GT: return a > b;
+    case CMP_GE: return a >= b;
+    case CMP_LT: return a < b;
+    default: return a <= b;
+  }
+}
+
+// The typed compare table of executor/condition/compare/** (execute() bodies at lines 33-38):
+// ordering compares use Java binary numeric promotion; ==/!= follow each executor's explicit
+// conversion, which differs only for Long x Float / Float x Long (both sides .doubleValue()).
+bool typed_compare(int op, const Value& l, const Value& r) {
+  int lt = l.type, rt = r.type;
+  if (lt == T_STRING || lt == T_BOOL) {
+    bool eq = l.i == r.i;  // String.equals on dictionary ids / boolean ==
+    return op == CMP_EQ ? eq : !eq;
+  }
+  bool is_eq = (op == CMP_EQ || op == CMP_NE);
+  if (lt == T_DOUBLE || rt == T_DOUBLE) return cmp_op(op, as_d(l), as_d(r));
+  if (lt == T_FLOAT || rt == T_FLOAT) {
+    if (is_eq && (lt == T_LONG || rt == T_LONG))  // EqualCompare...LongFloat.java:36 / FloatLong.java:37
+      return cmp_op(op, as_d(l), as_d(r));
+    return cmp_op(op, as_f(l), as_f(r));
+  }
+  if (lt == T_LONG || rt == T_LONG) return cmp_op(op, as_l(l), as_l(r));
+  return cmp_op(op, (int32_t)l.i, (int32_t)r.i);
+}
+
+// executor/math/{add,subtract,multiply,divide,mod}/*.java: null in -> null; /0 and %0 -> null
+// for every type (incl. 0.0f / -0.0); integer ops wrap like the JVM.
+Value arith(int op, int res, const Value& l, const Value& r) {
+  Value v;
+  v.type = res;
+  if (l.null || r.null) return mk_null();
+  v.null = false;
+  if (res == T_INT) {
+    int32_t a = (int32_t)l.i, b = (int32_t)r.i;
+    uint32_t ua = (uint32_t)a, ub = (uint32_t)b;
+    switch (op) {
+      case AR_ADD: v.i = (int32_t)(ua + ub); break;
+      case AR_SUB: v.i = (int32_t)(ua - ub); break;
+      case AR_MUL: v.i = (int32_t)(ua * ub); break;
+      case AR_DIV:
+        if (b == 0) return mk_null();
+        v.i = (a == INT32_MIN && b == -1) ? INT32_MIN : a / b;
+        break;
+      default:
+        if (b == 0) return mk_null();
+        v.i = (b == -1) ? 0 : a % b;
+    }
+  } else if (res == T_LONG) {
+    i64 a = l.i, b = r.i;
+    uint64_t ua = (uint64_t)a, ub = (uint64_t)b;
+    switch (op) {
+      case AR_ADD: v.i = (i64)(ua + ub); break;
+      case AR_SUB: v.i = (i64)(ua - ub); break;
+      case AR_MUL: v.i = (i64)(ua * ub); break;
+      case AR_DIV:
+        if (b == 0) return mk_null();
+        v.i = (a == INT64_MIN && b == -1) ? INT64_MIN : a / b;
+        break;
+      default:
+        if (b == 0) return mk_null();
+        v.i = (b == -1) ? 0 : a % b;
+    }
+  } else if (res == T_FLOAT) {
+    volatile float a = as_f(l), b = as_f(r);
+    switch (op) {
+      case AR_ADD: v.f = a + b; break;
+      case AR_SUB: v.f = a - b; break;
+      case AR_MUL: v.f = a * b; break;
+      case AR_DIV: if (b == 0.0f) return mk_null(); v.f = a / b; break;
+      default: if (b == 0.0f) return mk_null(); v.f = std::fmod((float)a, (float)b);
+    }
+  } else {
+    volatile double a = as_d(l), b = as_d(r);
+    switch (op) {
+      case AR_ADD: v.d = a + b; break;
+      case AR_SUB: v.d = a - b; break;
+      case AR_MUL: v.d = a * b; break;
+      case AR_DIV: if (b == 0.0) return mk_null(); v.d = a / b; break;
+      default: if (b == 0.0) return mk_null(); v.d = std::fmod((double)a, (double)b);
+    }
+  }
+  return v;
+}
+
+// StateEvent.getStreamEvent(int[] position), StateEvent.java:138-182
+StreamEvent* chain_at(StreamEvent* head, i64 idx) {
+  if (!head) return nullptr;
+  if (idx >= 0) {
+    StreamEvent* e = head;
+    for (i64 k = 1; k <= idx; ++k) {
+      e = e->next;
+      if (!e) return nullptr;
+    }
+    return e;
+  }
+  if (idx == -1) {  // CURRENT
+    StreamEvent* e = head;
+    while (e->next) e = e->next;
+    return e;
+  }
+  if (idx == -2) {  // LAST
+    if (!head->next) return nullptr;
+    StreamEvent* e = head;
+    while (e->next->next) e = e->next;
+    return e;
+  }
+  std::vector<StreamEvent*> v;
+  for (StreamEvent* e = head; e; e = e->next) v.push_back(e);
+  i64 k = (i64)v.size() + idx;
+  if (k < 0) return nullptr;
+  return v[k];
+}
+
+struct Engine;
+
+struct EvalCtx {
+  const std::vector<InEvent>* log;
+  const std::vector<std::vector<int>>* stream_types;
+};
+
+Value load_attr(const EvalCtx& cx, StreamEvent* ev, int attr, int type) {
+  if (!ev) return mk_null();
+  const InEvent& in = (*cx.log)[ev->seq];
+  if (in.nulls[attr]) return mk_null();
+  Value v;
+  v.type = type;
+  v.null = false;
+  i64 raw = in.vals[attr];
+  switch (type) {
+    case T_INT: v.i = (int32_t)raw; break;
+    case T_FLOAT: { uint32_t b = (uint32_t)raw; std::memcpy(&v.f, &b, 4); break; }
+    case T_DOUBLE: std::memcpy(&v.d, &raw, 8); break;
+    default: v.i = raw;
+  }
+  return v;
+}
+
+Value run_code(const EvalCtx& cx, const Code& code, const std::vector<StreamEvent*>& slots) {
+  std::vector<Value> st;
+  st.reserve(16);
+  for (const Insn& in : code) {
+    switch (in.op) {
+      case OP_CONST: {
+        Value v;
+        v.type = in.res;
+        v.null = false;
+        if (in.res == T_FLOAT) { uint32_t b = (uint32_t)in.imm; std::memcpy(&v.f, &b, 4); }
+        else if (in.res == T_DOUBLE) std::memcpy(&v.d, &in.imm, 8);
+        else if (in.res == T_INT) v.i = (int32_t)in.imm;
+        else v.i = in.imm;
+        st.push_back(v);
+        break;
+      }
+      case OP_ATTR:
+        st.push_back(load_attr(cx, chain_at(slots[in.a], in.b), (int)in.imm, in.res));
+        break;
+      case OP_STREAM_IS_NULL: {  // IsNullStreamConditionExpressionExecutor
+        Value v; v.type = T_BOOL; v.null = false;
+        v.i = chain_at(slots[in.a], in.b) == nullptr;
+        st.push_back(v);
+        break;
+      }
+      case OP_IS_NULL: {
+        Value x = st.back(); st.pop_back();
+        Value v; v.type = T_BOOL; v.null = false; v.i = x.null;
+        st.push_back(v);
+        break;
+      }
+      case OP_NOT: {  // NotConditionExpressionExecutor: only TRUE -> FALSE
+        Value x = st.back(); st.pop_back();
+        Value v; v.type = T_BOOL; v.null = false;
+        v.i = !(!x.null && x.i);
+        st.push_back(v);
+        break;
+      }
+      case OP_AND:
+      case OP_OR: {  // And/OrConditionExpressionExecutor: null is false
+        Value r = st.back(); st.pop_back();
+        Value l = st.back(); st.pop_back();
+        bool lb = !l.null && l.i, rb = !r.null && r.i;
+        Value v; v.type = T_BOOL; v.null = false;
+        v.i = in.op == OP_AND ? (lb && rb) : (lb || rb);
+        st.push_back(v);
+        break;
+      }
+      case OP_CMP: {  // CompareConditionExpressionExecutor.java:39-43
+        Value r = st.back(); st.pop_back();
+        Value l = st.back(); st.pop_back();
+        Value v; v.type = T_BOOL; v.null = false;
+        v.i = (!l.null && !r.null) && typed_compare((int)in.imm, l, r);
+        st.push_back(v);
+        break;
+      }
+      case OP_ARITH: {
+        Value r = st.back(); st.pop_back();
+        Value l = st.back(); st.pop_back();
+        st.push_back(arith((int)in.imm, in.res, l, r));
+        break;
+      }
+      default: throw std::runtime_error("bad opcode");
+    }
+  }
+  if (st.size() != 1) throw std::runtime_error("malformed bytecode");
+  return st.back();
+}
+
+// ------------------------------------------------------------------------------------------
+// One query runtime (one StateStreamRuntime, or one per-key clone of it)
+// ------------------------------------------------------------------------------------------
+struct Match {
+  int query;
+  i64 key;
+  i64 ts;
+  std::vector<std::vector<i64>> slots;
+};
+
+struct Runtime;
+
+struct Pre {
+  // StreamPreStateProcessor / CountPreStateProcessor / LogicalPreStateProcessor state
+  std::list<StateEvent*> pending, newAndEvery;
+  bool stateChanged = false, initialized = false;
+  bool successCondition = false, startStateReset = false;  // CountPreStateProcessor
+  bool iterating = false;
+};
+struct Post {
+  bool isEventReturned = false;
+};
+
+struct Runtime {
+  Engine* eng;
+  int qi;
+  i64 key;
+  const QueryDef* q;
+  std::vector<Pre> pres;
+  std::vector<Post> posts;
+
+  Runtime(Engine* e, int qi_, i64 key_, const QueryDef* qd)
+      : eng(e), qi(qi_), key(key_), q(qd), pres(qd->states.size()), posts(qd->states.size()) {}
+
+  size_t nslots() const { return q->states.size(); }
+  const StateDef& S(int i) const { return q->states[i]; }
+
+  // ---- pre processors -----------------------------------------------------------------------
+  // StreamPreStateProcessor.init():157-166
+  void init_pre(int i) {
+    const StateDef& s = S(i);
+    Pre& p = pres[i];
+    if (s.is_start && (!p.initialized || s.next_every >= 0)) {
+      StateEvent* se = new_state();
+      addState(i, se);
+      p.initialized = true;
+    }
+  }
+  StateEvent* new_state();
+
+  // StreamPreStateProcessor.addState:203-216 / CountPreStateProcessor.addState:109-132 /
+  // LogicalPreStateProcessor.addState:57-76
+  void addState(int i, StateEvent* se) {
+    const StateDef& s = S(i);
+    Pre& p = pres[i];
+    if (s.kind == K_LOGICAL) {
+      Pre& pp = pres[s.partner];
+      if (s.is_start || q->type == Q_SEQUENCE) {
+        if (p.newAndEvery.empty()) p.newAndEvery.push_back(se);
+        if (pp.newAndEvery.empty()) pp.newAndEvery.push_back(se);
+      } else {
+        p.newAndEvery.push_back(se);
+        pp.newAndEvery.push_back(se);
+      }
+      return;
+    }
+    if (q->type == Q_SEQUENCE) {
+      if (p.newAndEvery.empty()) p.newAndEvery.push_back(se);
+    } else {
+      p.newAndEvery.push_back(se);
+    }
+    if (s.kind == K_COUNT && s.min == 0 && se->slots[i] == nullptr) processMinCountReached(i, se);
+  }
+
+  // StreamPreStateProcessor.addEveryState:218-227 (slot NOT cleared) /
+  // LogicalPreStateProcessor.addEveryState:78-92 (own and partner slots cleared)
+  void addEveryState(int i, StateEvent* se) {
+    const StateDef& s = S(i);
+    StateEvent* c = clone(se);
+    if (s.kind == K_LOGICAL) {
+      c->slots[i] = nullptr;
+      pres[i].newAndEvery.push_back(c);
+      c->slots[s.partner] = nullptr;
+      pres[s.partner].newAndEvery.push_back(c);
+      return;
+    }
+    pres[i].newAndEvery.push_back(c);
+  }
+
+  StateEvent* clone(StateEvent* se);  // StateEventCloner.copyStateEvent:46-58 (shallow)
+
+  void promote(int i) {
+    Pre& p = pres[i];
+    if (p.iterating && !p.newAndEvery.empty())  // Java LinkedList iterator -> CME on next()
+      throw std::runtime_error("ConcurrentModificationException (reference engine would throw)");
+    p.pending.splice(p.pending.end(), p.newAndEvery);
+  }
+
+  // updateState: StreamPre:281-289, CountPre:149-156, LogicalPre:118-130
+  void updateState(int i) {
+    const StateDef& s = S(i);
+    if (s.kind == K_COUNT && pres[i].startStateReset) {
+      pres[i].startStateReset = false;
+      init_pre(i);
+    }
+    promote(i);
+    if (s.kind == K_LOGICAL) promote(s.partner);
+  }
+
+  // resetState: StreamPre:262-278, LogicalPre:94-116
+  void resetState(int i) {
+    const StateDef& s = S(i);
+    Pre& p = pres[i];
+    if (s.kind == K_LOGICAL) {
+      Pre& pp = pres[s.partner];
+      if (s.ltype == L_OR || p.pending.size() == pp.pending.size()) {
+        p.pending.clear();
+        pp.pending.clear();
+        if (s.is_start && p.newAndEvery.empty()) {
+          if (q->type == Q_SEQUENCE && s.next_every < 0 && next_pending_nonempty(i)) return;
+          init_pre(i);
+        }
+      }
+      return;
+    }
+    p.pending.clear();
+    if (s.is_start && p.newAndEvery.empty()) {
+      if (q->type == Q_SEQUENCE && s.next_every < 0 && next_pending_nonempty(i)) return;
+      init_pre(i);
+    }
+  }
+  bool next_pending_nonempty(int i) {
+    int n = S(i).next_pre;
+    if (n < 0) throw std::runtime_error("NullPointerException in resetState (no next state)");
+    return !pres[n].pending.empty();
+  }
+
+  // CountPreStateProcessor.startStateReset:142-147
+  void startStateReset(int i) {
+    if (S(i).kind != K_COUNT) throw std::runtime_error("callback target is not a count state");
+    pres[i].startStateReset = true;
+    if (S(i).callback >= 0) throw std::runtime_error("StackOverflowError in startStateReset (reference)");
+  }
+
+  bool isExpired(int i, StateEvent* se, i64 ts) {  // StreamPreStateProcessor.isExpired:102-113
+    const StateDef& s = S(i);
+    if (!s.is_start && q->within >= 0) {
+      for (int sid : q->start_ids) {
+        StreamEvent* ev = se->slots[sid];
+        if (ev) {
+          uint64_t d = (uint64_t)ev->ts - (uint64_t)ts;
+          i64 sd = (i64)d;
+          i64 a = sd < 0 ? (i64)(0 - (uint64_t)sd) : sd;  // Math.abs(long), MIN stays MIN
+          if (a > q->within) return true;
+        }
+      }
+    }
+    return false;
+  }
+
+  // StreamPreStateProcessor.process(StateEvent):115-121 -> FilterProcessor chain -> post
+  void process(int i, StateEvent* se);
+  bool filters_pass(int i, StateEvent* se);
+
+  // ---- post processors ------------------------------------------------------------------------
+  // StreamPostStateProcessor.process:53-72
+  void streamPost(int i, StateEvent* se) {
+    const StateDef& s = S(i);
+    pres[i].stateChanged = true;
+    se->ts = se->slots[i]->ts;
+    if (s.has_selector) posts[i].isEventReturned = true;
+    if (s.next_pre >= 0) addState(s.next_pre, se);
+    if (s.next_every >= 0) addEveryState(s.next_every, se);
+    if (s.callback >= 0) startStateReset(s.callback);
+  }
+  // CountPostStateProcessor.processMinCountReached:73-85
+  void processMinCountReached(int i, StateEvent* se) {
+    const StateDef& s = S(i);
+    if (s.has_selector) {
+      pres[i].stateChanged = true;
+      posts[i].isEventReturned = true;
+    }
+    if (s.next_pre >= 0) addState(s.next_pre, se);
+    if (s.next_every >= 0) addEveryState(s.next_every, se);
+  }
+  // CountPostStateProcessor.process:45-71
+  void countPost(int i, StateEvent* se) {
+    const StateDef& s = S(i);
+    StreamEvent* e = se->slots[i];
+    i64 n = 1;
+    while (e->next) { ++n; e = e->next; }
+    pres[i].successCondition = true;
+    se->ts = e->ts;
+    if (n >= s.min) {
+      if (q->type == Q_SEQUENCE) {
+        if (s.next_pre >= 0) addState(s.next_pre, se);
+        if (n != s.max) addState(i, se);
+      } else if (n == s.min) {
+        processMinCountReached(i, se);
+      }
+      if (n == s.max) pres[i].stateChanged = true;
+    }
+  }
+  // LogicalPostStateProcessor.process:59-87
+  void logicalPost(int i, StateEvent* se) {
+    const StateDef& s = S(i);
+    if (s.ltype == L_AND) {
+      if (se->slots[s.partner] != nullptr) streamPost(i, se);
+      else pres[i].stateChanged = true;
+    } else {
+      streamPost(i, se);
+      // 'from A or B select' case: thisStatePreProcessor.thisLastProcessor == partner post
+      if (S(s.partner).has_selector && s.this_last == s.partner) posts[s.partner].isEventReturned = true;
+    }
+  }
+
+  // ---- processAndReturn -----------------------------------------------------------------------
+  std::vector<StateEvent*> processAndReturn(int i, i64 seq, i64 ts);
+
+  // ---- inner state runtime tree (state/runtime/*InnerStateRuntime.java) ---------------------
+  void node_init(int n) {
+    const NodeDef& d = q->nodes[n];
+    switch (d.type) {
+      case N_STREAM: case N_COUNT: init_pre(d.pre); break;
+      case N_NEXT: node_init(d.a); node_init(d.b); break;
+      case N_EVERY: node_init(d.a); break;
+      case N_LOGICAL: node_init(d.b); node_init(d.a); break;
+    }
+  }
+  void node_reset(int n) {
+    const NodeDef& d = q->nodes[n];
+    switch (d.type) {
+      case N_STREAM: case N_COUNT: case N_EVERY: resetState(d.pre); break;
+      case N_NEXT: node_reset(d.b); node_reset(d.a); break;
+      case N_LOGICAL: node_reset(d.b); break;
+    }
+  }
+  void node_update(int n) {
+    const NodeDef& d = q->nodes[n];
+    switch (d.type) {
+      case N_STREAM: case N_COUNT: case N_EVERY: updateState(d.pre); break;
+      case N_NEXT: node_update(d.a); node_update(d.b); break;
+      case N_LOGICAL: node_update(d.b); break;
+    }
+  }
+
+  void receive(int stream, i64 seq, i64 ts);
+  void mark_roots();
+};
+
+struct Engine {
+  Program prog;
+  std::vector<InEvent> log;
+  Heap heap;
+  std::vector<std::unique_ptr<Runtime>> top;        // unpartitioned queries (index = query)
+  // per partition: key -> instance runtimes (one per partition query)
+  std::vector<std::map<i64, std::vector<std::unique_ptr<Runtime>>>> part_inst;
+  std::vector<std::vector<i64>> key_order;          // creation order per partition
+  std::vector<Match> matches;
+  std::vector<std::pair<Runtime*, StateEvent*>> deferred;  // single-receiver chunk deferral
+  std::string err;
+  size_t gc_threshold = 1 << 20;
+
+  void emit(Runtime* rt, StateEvent* se) {
+    Match m;
+    m.query = rt->qi;
+    m.key = rt->key;
+    m.ts = se->ts;
+    m.slots.resize(se->slots.size());
+    for (size_t k = 0; k < se->slots.size(); ++k)
+      for (StreamEvent* e = se->slots[k]; e; e = e->next) m.slots[k].push_back(e->seq);
+    matches.push_back(std::move(m));
+  }
+
+  void gc() {
+    size_t live_before = heap.sev.size() + heap.stev.size();
+    if (live_before < gc_threshold) return;
+    for (auto& r : top) if (r) r->mark_roots();
+    for (auto& pr : deferred) {
+      pr.second->mark = true;
+      for (StreamEvent* ev : pr.second->slots)
+        for (; ev && !ev->mark; ev = ev->next) ev->mark = true;
+    }
+    for (auto& pm : part_inst)
+      for (auto& kv : pm)
+        for (auto& r : kv.second) r->mark_roots();
+    size_t w = 0;
+    for (auto* s : heap.stev) {
+      if (s->mark) { s->mark = false; heap.stev[w++] = s; } else delete s;
+    }
+    heap.stev.resize(w);
+    w = 0;
+    for (auto* e : heap.sev) {
+      if (e->mark) { e->mark = false; heap.sev[w++] = e; } else delete e;
+    }
+    heap.sev.resize(w);
+    size_t live = heap.sev.size() + heap.stev.size();
+    gc_threshold = std::max<size_t>(1 << 20, live * 2);
+  }
+};
+
+StateEvent* Runtime::new_state() { return eng->heap.state(nslots()); }
+
+StateEvent* Runtime::clone(StateEvent* se) {
+  StateEvent* c = eng->heap.state(nslots());
+  c->slots = se->slots;
+  c->ts = se->ts;
+  return c;
+}
+
+bool Runtime::filters_pass(int i, StateEvent* se) {
+  EvalCtx cx{&eng->log, &eng->prog.stream_types};
+  for (const Code& f : S(i).filters) {
+    Value v = run_code(cx, f, se->slots);
+    if (v.null || !v.i) return false;  // FilterProcessor.process:55-66
+  }
+  return true;
+}
+
+void Runtime::process(int i, StateEvent* se) {
+  pres[i].stateChanged = false;
+  if (!filters_pass(i, se)) return;
+  switch (S(i).kind) {
+    case K_STREAM: streamPost(i, se); break;
+    case K_COUNT: countPost(i, se); break;
+    default: logicalPost(i, se); break;
+  }
+}
+
+std::vector<StateEvent*> Runtime::processAndReturn(int i, i64 seq, i64 ts) {
+  std::vector<StateEvent*> ret;
+  const StateDef& s = S(i);
+  Pre& p = pres[i];
+  p.iterating = true;
+  for (auto it = p.pending.begin(); it != p.pending.end();) {
+    StateEvent* se = *it;
+    if (s.kind == K_COUNT) {
+      // CountPreStateProcessor.processAndReturn:53-93 (no within check, R9)
+      if ((int)nslots() > i + 1 && se->slots[i + 1] != nullptr) { it = p.pending.erase(it); continue; }
+      if ((int)nslots() > i + 2 && se->slots[i + 2] != nullptr) { it = p.pending.erase(it); continue; }
+      StreamEvent* ev = eng->heap.copy(seq, ts);
+      if (!se->slots[i]) se->slots[i] = ev;        // StateEvent.addEvent:212-222
+      else { StreamEvent* t = se->slots[i]; while (t->next) t = t->next; t->next = ev; }
+      p.successCondition = false;
+      process(i, se);
+      if (posts[s.this_last].isEventReturned) {
+        posts[s.this_last].isEventReturned = false;
+        ret.push_back(se);
+      }
+      bool removed = false;
+      if (p.stateChanged) { it = p.pending.erase(it); removed = true; }
+      if (!p.successCondition) {
+        // StateEvent.removeLastEvent:224-236
+        StreamEvent* a = se->slots[i];
+        if (a) {
+          bool done = false;
+          while (a->next) {
+            if (!a->next->next) { a->next = nullptr; done = true; break; }
+            a = a->next;
+          }
+          if (!done) se->slots[i] = nullptr;
+        }
+        if (q->type == Q_SEQUENCE) {
+          if (removed) throw std::runtime_error("IllegalStateException (double iterator.remove)");
+          it = p.pending.erase(it);
+          removed = true;
+        }
+      }
+      if (!removed) ++it;
+      continue;
+    }
+    // StreamPreStateProcessor.processAndReturn:292-337 / LogicalPreStateProcessor:133-178
+    if (isExpired(i, se, ts)) {
+      it = p.pending.erase(it);
+      if (s.within_every >= 0) {
+        addEveryState(s.within_every, se);
+        updateState(s.within_every);
+      }
+      continue;
+    }
+    if (s.kind == K_LOGICAL && s.ltype == L_OR && se->slots[s.partner] != nullptr) {
+      it = p.pending.erase(it);
+      continue;
+    }
+    se->slots[i] = eng->heap.copy(seq, ts);
+    process(i, se);
+    if (posts[s.this_last].isEventReturned) {
+      posts[s.this_last].isEventReturned = false;
+      ret.push_back(se);
+    }
+    if (p.stateChanged) {
+      it = p.pending.erase(it);
+    } else {
+      se->slots[i] = nullptr;
+      if (q->type == Q_SEQUENCE) {
+        it = p.pending.erase(it);
+        if (s.kind == K_STREAM && s.callback >= 0) startStateReset(s.callback);
+      } else {
+        ++it;
+      }
+    }
+  }
+  p.iterating = false;
+  return ret;
+}
+
+void Runtime::receive(int stream, i64 seq, i64 ts) {
+  const RecvDef* rv = nullptr;
+  for (auto& r : q->recvs)
+    if (r.stream == stream) rv = &r;
+  if (!rv) return;
+  if (rv->kind == R_SINGLE) {
+    // SingleProcessStreamReceiver.processAndClear:57-80 (selector deferred to chunk end)
+    if (q->type == Q_SEQUENCE) { node_reset(0); node_update(0); }   // StateStreamRuntime.resetAndUpdate
+    else updateState(rv->procs[0]);                                  // PatternSingle.stabilizeStates
+    for (StateEvent* se : processAndReturn(rv->procs[0], seq, ts)) eng->deferred.push_back({this, se});
+  } else {
+    // MultiProcessStreamReceiver.receive:268-279 + StateMultiProcessStreamReceiver.processAndClear:53-74
+    if (q->type == Q_SEQUENCE) { node_reset(0); node_update(0); }
+    else for (int p : rv->procs) updateState(p);                     // PatternMulti.stabilizeStates
+    for (int k = (int)rv->procs.size() - 1; k >= 0; --k)             // reverse registration order
+      for (StateEvent* se : processAndReturn(rv->procs[k], seq, ts)) eng->emit(this, se);
+  }
+}
+
+void Runtime::mark_roots() {
+  auto mark_state = [](StateEvent* s) {
+    s->mark = true;
+    for (StreamEvent* e : s->slots)
+      for (; e && !e->mark; e = e->next) e->mark = true;
+  };
+  for (Pre& p : pres) {
+    for (StateEvent* s : p.pending) mark_state(s);
+    for (StateEvent* s : p.newAndEvery) mark_state(s);
+  }
+}
+
+i64 key_of(const Value& v) {
+  // PartitionKey = String.valueOf(value) (ValuePartitionExecutor.java:34-40); the planner
+  // restricts a partition's keys to one type class so raw-value identity equals string identity.
+  switch (v.type) {
+    case T_FLOAT: { float f = v.f; if (std::isnan(f)) return 0x7fc00000; uint32_t b; std::memcpy(&b, &f, 4); return b; }
+    case T_DOUBLE: { double d = v.d; if (std::isnan(d)) return 0x7ff8000000000000LL; i64 b; std::memcpy(&b, &d, 8); return b; }
+    default: return v.i;
+  }
+}
+
+void deliver_deferred(Engine* e) {
+  for (auto& pr : e->deferred) e->emit(pr.first, pr.second);
+  e->deferred.clear();
+}
+
+void send_one(Engine* e, int stream, i64 seq, i64 ts) {
+  const Program& P = e->prog;
+  // top-level queries and partitions in app order: queries carry their partition index
+  std::vector<char> part_done(P.parts.size(), 0);
+  for (size_t qi = 0; qi < P.queries.size(); ++qi) {
+    const QueryDef& q = P.queries[qi];
+    if (q.partition < 0) {
+      e->top[qi]->receive(stream, seq, ts);
+      continue;
+    }
+    int pi = q.partition;
+    if (part_done[pi]) continue;
+    part_done[pi] = 1;
+    const PartDef& pd = P.parts[pi];
+    for (const PartKey& k : pd.keys) {
+      if (k.stream != stream) continue;
+      EvalCtx cx{&e->log, &P.stream_types};
+      std::vector<StreamEvent*> slots(1);
+      StreamEvent tmp{seq, ts};
+      slots[0] = &tmp;
+      Value kv = run_code(cx, k.code, slots);
+      if (kv.null) continue;  // PartitionStreamReceiver.send: null key drops the event
+      i64 key = key_of(kv);
+      auto& inst = e->part_inst[pi];
+      auto it = inst.find(key);
+      if (it == inst.end()) {
+        // PartitionRuntime.clonePartition:263-306 -> per-key QueryRuntime clones, seeded at init
+        std::vector<std::unique_ptr<Runtime>> rts;
+        for (int pq : pd.queries) {
+          rts.emplace_back(new Runtime(e, pq, key, &P.queries[pq]));
+          rts.back()->node_init(0);
+        }
+        it = inst.emplace(key, std::move(rts)).first;
+        e->key_order[pi].push_back(key);
+      }
+      for (auto& rt : it->second) rt->receive(stream, seq, ts);
+    }
+  }
+}
+
+}  // namespace
+
+struct OracleEngine : Engine {};
+
+extern "C" {
+
+int oracle_create(const void* blob, size_t len, OracleEngine** out) {
+  try {
+    auto* e = new OracleEngine;
+    e->prog = parse_ir(blob, len);
+    e->top.resize(e->prog.queries.size());
+    for (size_t qi = 0; qi < e->prog.queries.size(); ++qi) {
+      if (e->prog.queries[qi].partition >= 0) continue;
+      e->top[qi].reset(new Runtime(e, (int)qi, -1, &e->prog.queries[qi]));
+      e->top[qi]->node_init(0);  // QueryRuntime.init -> StateStreamRuntime.setCommonProcessor
+    }
+    e->part_inst.resize(e->prog.parts.size());
+    e->key_order.resize(e->prog.parts.size());
+    *out = e;
+    return 0;
+  } catch (const std::exception& ex) {
+    *out = nullptr;
+    return -1;
+  }
+}
+
+int oracle_send(OracleEngine* e, int32_t stream, int64_t n, const int64_t* ts, const int64_t* vals,
+                const uint8_t* nulls, int as_chunk) {
+  try {
+    if (stream < 0 || stream >= (int)e->prog.stream_types.size()) throw std::runtime_error("bad stream");
+    size_t na = e->prog.stream_types[stream].size();
+    for (int64_t k = 0; k < n; ++k) {
+      InEvent ev;
+      ev.stream = stream;
+      ev.ts = ts[k];
+      ev.vals.assign(vals + k * na, vals + (k + 1) * na);
+      if (nulls) ev.nulls.assign(nulls + k * na, nulls + (k + 1) * na);
+      else ev.nulls.assign(na, 0);
+      i64 seq = (i64)e->log.size();
+      e->log.push_back(std::move(ev));
+      send_one(e, stream, seq, ts[k]);
+      if (!as_chunk) deliver_deferred(e);
+      e->gc();
+    }
+    deliver_deferred(e);
+    return 0;
+  } catch (const std::exception& ex) {
+    e->err = ex.what();
+    e->deferred.clear();
+    return -1;
+  }
+}
+
+int64_t oracle_num_matches(const OracleEngine* e) { return (int64_t)e->matches.size(); }
+
+int64_t oracle_match_words(const OracleEngine* e) {
+  int64_t w = 0;
+  for (auto& m : e->matches)
+    for (auto& s : m.slots) w += 1 + (int64_t)s.size();
+  return w;
+}
+
+int oracle_get_matches(const OracleEngine* e, int64_t* query, int64_t* key, int64_t* ts,
+                       int64_t* off, int64_t* words) {
+  int64_t w = 0;
+  for (size_t i = 0; i < e->matches.size(); ++i) {
+    const Match& m = e->matches[i];
+    query[i] = m.query;
+    key[i] = m.key;
+    ts[i] = m.ts;
+    off[i] = w;
+    for (auto& s : m.slots) {
+      words[w++] = (int64_t)s.size();
+      for (i64 q : s) words[w++] = q;
+    }
+  }
+  off[e->matches.size()] = w;
+  return 0;
+}
+
+void oracle_clear_matches(OracleEngine* e) { e->matches.clear(); }
+
+const char* oracle_error(const OracleEngine* e) { return e->err.c_str(); }
+
+void oracle_destroy(OracleEngine* e) { delete e; }
+
+}  // extern "C"
