@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""NFA-step throughput benchmark (BASELINE.json metric: events/s x active patterns).
+
+Workload (BASELINE.json configs[1]): P = 1,000 concurrent 2-state patterns
+    every e1=StockStream[price > T_p] -> e2=StockStream[price > e1.price] within W_p
+over the seeded synthetic StockStream (20 B/event SoA), one MI355X per rank. One step = one
+NFA-step pass (one sdh_engine_push) over a batch of B events already resident in HBM; the
+matches it produces stay in HBM (per-wave output segments, counted on the host).
+
+Multi-GPU (torchrun, one process per GPU): weak scaling by pattern set -- every rank runs its
+own P patterns (rank r uses patterns r*P .. r*P+P-1 of the family) over the same event stream;
+there is no data-path collective. Timing: barrier + device sync on both sides of the K timed
+steps, max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--patterns", type=int, default=1000)
+    ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--partials", type=int, default=128)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def c2_app_for_rank(rank, P):
+    from siddhi_amd.workloads import STOCK_STREAM, c2_threshold_text, c2_within_sec
+    qs = [STOCK_STREAM]
+    for k in range(P):
+        p = rank * P + k
+        qs.append(f"@info(name='p{p}') from every e1=StockStream[price > {c2_threshold_text(p)}] -> "
+                  f"e2=StockStream[price > e1.price] within {c2_within_sec(p)} sec "
+                  f"select e1.price as p1, e2.price as p2 insert into OutStream;")
+    return " ".join(qs)
+
+
+def cpu_baseline(app_src, budget_s):
+    """Reference-semantics CPU engine (the oracle, single thread) on a bounded sample of the
+    same workload: the first 32 patterns over consecutive batches of the same stream until the
+    time budget is spent."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from harness import App
+    from siddhi_amd.workloads import c2_app, stock_events
+    P = 32
+    app = App(c2_app(P))
+    done, t0, start = 0, time.perf_counter(), 0
+    n = 20000
+    while time.perf_counter() - t0 < budget_s:
+        ts, sym, price, vol = stock_events(start, n)
+        vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64),
+                         vol.astype(np.int64)], 1)
+        app.engine.send(0, ts, vals, None)
+        app.engine.take_matches(lambda q: 2)
+        start += n
+        done += n
+    dt = time.perf_counter() - t0
+    return {"value": done * P / dt, "unit": "pattern-events/s", "cores": 1, "kind": "port",
+            "sample": f"{P} C2 patterns x {done} events (oracle/liboracle.so, 1 thread, "
+                      f"{dt:.1f} s)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from siddhi_amd import ql
+    from siddhi_amd.engine import HipEngine
+    from siddhi_amd.planner import plan
+    from siddhi_amd.workloads import stock_events
+
+    P = args.patterns
+    ir = plan(ql.parse(c2_app_for_rank(rank, P)))
+    eng = HipEngine(ir.serialize(), device=local, partials=args.partials)
+
+    B = args.batch
+    n_batches = args.warmup + args.steps
+    # synthetic batches resident in HBM before the timed region
+    batches = []
+    for s in range(n_batches):
+        ts, sym, price, vol = stock_events(s * B, B)
+        batches.append((torch.from_numpy(ts).to(dev), torch.from_numpy(sym).to(dev),
+                        torch.from_numpy(price.view(np.int32)).to(dev), torch.from_numpy(vol).to(dev)))
+    torch.cuda.synchronize()
+
+    def step(i):
+        t, sy, pr, vo = batches[i]
+        eng.push_device(0, B, t.data_ptr(), [sy.data_ptr(), pr.data_ptr(), vo.data_ptr()])
+
+    for i in range(args.warmup):
+        step(i)
+    kern_ms, kern_bytes, matches = [], [], 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, n_batches):
+        step(i)
+        st = eng.stats()
+        kern_ms.append(st.last_kernel_ms)
+        kern_bytes.append(st.last_kernel_bytes)
+        matches += eng.pending_matches()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        mt = torch.tensor([matches], device=dev, dtype=torch.float64)
+        dist.all_reduce(mt)
+        matches = int(mt.item())
+
+    total_pe = float(B) * args.steps * P * world
+    value = total_pe / elapsed
+    avg_ms = float(np.mean(kern_ms))
+    avg_bytes = float(np.mean(kern_bytes))
+    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
+    peak = 8000.0
+    result = {
+        "metric": "events/sec x active patterns (whole node); achieved HBM GB/s",
+        "value": value,
+        "unit": "pattern-events/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded splitmix64 StockStream, SURVEY §8(d))",
+        "config": {"workload": "C2: 1K concurrent 2-state filter+reference patterns "
+                               "(every e1[price>T_p] -> e2[price>e1.price] within W_p)",
+                   "patterns_per_gpu": P, "events_per_step": B, "parallelism": f"pattern-set x{world}",
+                   "matches": matches},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                     "frac": achieved / peak, "traffic": None,
+                     "kernel": "nfa_chain_kernel", "kernel_ms": avg_ms},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(None, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

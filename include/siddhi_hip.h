@@ -1,0 +1,116 @@
+/*
+ * siddhi_hip.h -- C-ABI of libsiddhi_hip.so, the MI355X pattern/sequence (NFA) engine.
+ *
+ * This is the drop-in boundary for the reference's state-stream path
+ * (org.wso2.siddhi.core.query.input.stream.state). Each entry point replaces one seam of the
+ * reference (paths relative to modules/siddhi-core/src/main/java/org/wso2/siddhi/core/):
+ *
+ *   sdh_engine_create   <- util/parser/InputStreamParser.java:94-99 (state branch) +
+ *                          util/parser/StateInputStreamParser.java:77-143 (parseInputStream) +
+ *                          query/QueryRuntime.java:186-193 (init: seeds the start states)
+ *   sdh_engine_push     <- stream/StreamJunction.java:376-389 (Receiver.receive(Event[]) /
+ *                          receive(long, Object[])) -> query/input/ProcessStreamReceiver.java:105-183
+ *                          -> state/StreamPreStateProcessor.java:292-337 (processAndReturn)
+ *   sdh_engine_poll     <- query/input/SingleProcessStreamReceiver.java:75-79 and
+ *                          query/input/StateMultiProcessStreamReceiver.java:65-72 (hand-off of each
+ *                          completed StateEvent to QuerySelector.process)
+ *   sdh_engine_flush    <- (no reference equivalent: the reference is synchronous)
+ *   sdh_engine_snapshot / sdh_engine_restore
+ *                       <- state/StreamPreStateProcessor.java:352-367 (currentState/restoreState)
+ *   sdh_last_error      <- Java exceptions (SiddhiAppCreationException, OperationNotSupportedException)
+ *
+ * Conventions: plain C, no exceptions cross the ABI, every call returns 0 on success and a
+ * negative SDH_E* code on failure; sdh_last_error() then describes it. One producer thread per
+ * engine (the reference serialises receivers on a monitor, SingleProcessStreamReceiver.java:59).
+ * There is NO CPU fallback: an engine that cannot run a query on the GPU fails at create time.
+ */
+#ifndef SIDDHI_HIP_H
+#define SIDDHI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDH_OK 0
+#define SDH_E_INVALID (-1)     /* bad argument / malformed IR                               */
+#define SDH_E_UNSUPPORTED (-2) /* query shape not executable on the GPU path                */
+#define SDH_E_DEVICE (-3)      /* HIP runtime error                                          */
+#define SDH_E_CAPACITY (-4)    /* a partial-match table or match buffer overflowed           */
+#define SDH_E_REFERENCE (-5)   /* the reference engine would throw here (e.g. CME)           */
+
+typedef struct sdh_engine sdh_engine;
+
+typedef struct sdh_config {
+  int32_t device;            /* HIP device ordinal (one process per GPU)                      */
+  int32_t shard_rank;        /* pattern-set sharding: query q runs here iff q % shard_world   */
+  int32_t shard_world;       /*   == shard_rank (1/0 = unsharded)                             */
+  int32_t partials_per_inst; /* live partial-match capacity per query instance (mult. of 64) */
+  int64_t max_batch;         /* max events per push                                          */
+  int64_t match_capacity;    /* max matches held between polls (0 = sized automatically)     */
+  int32_t chunk_events;      /* target events per parallel chunk (0 = automatic)             */
+  int32_t flags;             /* reserved, 0                                                  */
+} sdh_config;
+
+/* One columnar (SoA) batch of events of one stream, in arrival order.
+ * cols[a] points to n elements of attribute a with the stream schema's native width:
+ *   INT -> int32, LONG -> int64, FLOAT -> float, DOUBLE -> double, BOOL -> uint8,
+ *   STRING -> int32 dictionary id (sdh_intern).
+ * nulls[a] (optional, may be NULL or have NULL entries) is a uint8 mask, 1 = null.
+ * on_device != 0: all pointers are HIP device pointers already resident in HBM; otherwise they
+ * are host pointers (pinned memory recommended) and are copied before sdh_engine_push returns. */
+typedef struct sdh_batch {
+  int64_t n;
+  const int64_t* ts;
+  const void* const* cols;
+  const uint8_t* const* nulls;
+  int32_t n_cols;
+  int32_t on_device;
+} sdh_batch;
+
+/* Matches, in the reference's delivery order (per input event; per query; per state processor
+ * in reverse registration order; per pending partial in insertion order -- SURVEY R18).
+ * Match i: query[i], key[i] (partition key id, -1 if unpartitioned), ts[i] (the StateEvent
+ * timestamp); words[off[i] .. off[i+1]) holds, per state slot, a count c followed by c global
+ * event sequence numbers (the slot's event chain when the selector would have run).
+ * Sequence numbers count pushed events from 0 across all streams in push order.
+ * Buffers are owned by the engine and valid until the next push/poll/destroy. */
+typedef struct sdh_matches {
+  int64_t n;
+  const int64_t* query;
+  const int64_t* key;
+  const int64_t* ts;
+  const int64_t* off;
+  const int64_t* words;
+} sdh_matches;
+
+typedef struct sdh_stats {
+  int64_t events;            /* events pushed                                                */
+  int64_t pattern_events;    /* sum over pushes of events x queries consuming that stream    */
+  int64_t matches;           /* matches produced                                             */
+  int64_t live_partials;     /* live partial matches after the last push                     */
+  double last_kernel_ms;     /* device time of the last NFA-step launch (HIP events)         */
+  double last_kernel_bytes;  /* algorithmic bytes of that launch (DESIGN.md roofline model)   */
+} sdh_stats;
+
+int sdh_engine_create(const void* ir_blob, size_t len, const sdh_config* cfg, sdh_engine** out);
+int sdh_engine_push(sdh_engine* e, int32_t stream, const sdh_batch* batch);
+int sdh_engine_flush(sdh_engine* e);
+int sdh_engine_poll(sdh_engine* e, sdh_matches* out);
+/* Device-resident match count of the last push (no host copy of the matches). */
+int sdh_engine_pending_matches(sdh_engine* e, int64_t* n);
+int sdh_engine_stats(sdh_engine* e, sdh_stats* out);
+int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len);
+int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len);
+void sdh_free(void* p);
+void sdh_engine_destroy(sdh_engine* e);
+const char* sdh_last_error(sdh_engine* e);
+/* Library version / build info string (static storage). */
+const char* sdh_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,799 @@
+// engine.hip -- host side of libsiddhi_hip.so: IR lowering, HBM state management, batching,
+// chunk planning, NFA-step launches and match hand-off. Implements include/siddhi_hip.h.
+//
+// The reference has no device boundary; this file is the GpuStateStreamRuntime half that replaces
+// StateInputStreamParser's object graph (core/util/parser/StateInputStreamParser.java:77-398) with
+// device tables, and the receiver loop (core/query/input/*ProcessStreamReceiver.java) with one
+// batched launch per pushed event batch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/siddhi_hip.h"
+#include "nfa_types.h"
+
+extern "C" hipError_t sdh_launch_chain(int k, const sdh::ChainLaunch* L, int n_blocks, size_t lds,
+                                       hipStream_t s);
+extern "C" hipError_t sdh_launch_compact(const int64_t* src, const int64_t* seg_off,
+                                         const int64_t* seg_count, const int64_t* dst_off,
+                                         int rec_words, int n_items, int64_t* dst, hipStream_t s);
+
+using namespace sdh;
+
+namespace {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+std::string fmt(const char* f, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(buf, sizeof buf, f, ap);
+  va_end(ap);
+  return buf;
+}
+
+#define HIPCHK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) throw Error(SDH_E_DEVICE, fmt("%s: %s", #x, hipGetErrorString(e_))); \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------
+// IR reader (format: siddhi_amd/ir.py)
+// ------------------------------------------------------------------------------------------
+enum { OP_CONST = 1, OP_ATTR, OP_IS_NULL, OP_STREAM_IS_NULL, OP_CMP, OP_AND, OP_OR, OP_NOT, OP_ARITH };
+enum { K_STREAM = 0, K_COUNT, K_LOGICAL };
+enum { Q_PATTERN = 0, Q_SEQUENCE };
+
+struct Insn {
+  int op, lt, rt, res;
+  int64_t a, b, imm;
+};
+struct IState {
+  int kind, stream, is_start, min, max, ltype, partner, next_pre, next_every, within_every, callback,
+      this_last, has_selector;
+  std::vector<std::vector<Insn>> filters;
+};
+struct IQuery {
+  int type, partition;
+  int64_t within;
+  std::vector<IState> st;
+};
+struct IProgram {
+  std::vector<std::vector<int>> stream_types;
+  std::vector<IQuery> q;
+};
+
+struct WordReader {
+  const int64_t* w;
+  size_t n, i = 0;
+  int64_t next() {
+    if (i >= n) throw Error(SDH_E_INVALID, "IR blob truncated");
+    return w[i++];
+  }
+};
+
+std::vector<Insn> read_code(WordReader& r) {
+  std::vector<Insn> c((size_t)r.next());
+  for (auto& x : c) {
+    int64_t w0 = r.next();
+    x.op = (int)(w0 & 0xff);
+    x.lt = (int)((w0 >> 8) & 0xff);
+    x.rt = (int)((w0 >> 16) & 0xff);
+    x.res = (int)((w0 >> 24) & 0xff);
+    x.a = r.next();
+    x.b = r.next();
+    x.imm = r.next();
+  }
+  return c;
+}
+
+IProgram read_ir(const void* blob, size_t len) {
+  if (!blob || len < 16 || memcmp(blob, "SDHIR001", 8) != 0) throw Error(SDH_E_INVALID, "bad IR magic");
+  WordReader r{reinterpret_cast<const int64_t*>(static_cast<const char*>(blob) + 8), (len - 8) / 8};
+  IProgram p;
+  if (r.next() != 1) throw Error(SDH_E_INVALID, "unsupported IR version");
+  p.stream_types.resize((size_t)r.next());
+  for (auto& s : p.stream_types) {
+    s.resize((size_t)r.next());
+    for (auto& t : s) t = (int)r.next();
+  }
+  int64_t ns = r.next();
+  for (int64_t k = 0; k < ns; ++k) {
+    int64_t nb = r.next();
+    for (int64_t j = 0; j < (nb + 7) / 8; ++j) r.next();
+  }
+  p.q.resize((size_t)r.next());
+  for (auto& q : p.q) {
+    q.type = (int)r.next();
+    q.within = r.next();
+    q.st.resize((size_t)r.next());
+    q.partition = (int)r.next();
+    r.next();
+    for (auto& s : q.st) {
+      s.kind = (int)r.next(); s.stream = (int)r.next(); s.is_start = (int)r.next();
+      s.min = (int)r.next(); s.max = (int)r.next(); s.ltype = (int)r.next();
+      s.partner = (int)r.next(); s.next_pre = (int)r.next(); s.next_every = (int)r.next();
+      s.within_every = (int)r.next(); s.callback = (int)r.next(); s.this_last = (int)r.next();
+      s.has_selector = (int)r.next();
+      s.filters.resize((size_t)r.next());
+      for (auto& f : s.filters) f = read_code(r);
+    }
+    int64_t n = r.next();
+    for (int64_t k = 0; k < n; ++k) r.next();           // start ids
+    n = r.next();
+    for (int64_t k = 0; k < n; ++k) {                    // receivers
+      r.next(); r.next();
+      int64_t np = r.next();
+      for (int64_t j = 0; j < np; ++j) r.next();
+    }
+    n = r.next();
+    for (int64_t k = 0; k < n * 4; ++k) r.next();        // runtime tree
+    n = r.next();
+    for (int64_t k = 0; k < n; ++k) read_code(r);        // selector outputs (host-side projection)
+  }
+  return p;  // partitions follow; partitioned queries are rejected by the lowering below
+}
+
+// ------------------------------------------------------------------------------------------
+// lowering: IR query -> ChainQuery (predicate atoms + captures)
+// ------------------------------------------------------------------------------------------
+// Compare domain of a typed compare (restates ExpressionParser.java:539-1220 + compare/**):
+// ordering compares promote like Java binary numeric promotion; ==/!= of Long x Float compare in
+// double (EqualCompareConditionExpressionExecutorLongFloat.java:36, ...FloatLong.java:37).
+int domain_of(int lt, int rt, int op) {
+  if (lt == T_STRING || lt == T_BOOL) return D_RAW;
+  if (lt == T_DOUBLE || rt == T_DOUBLE) return D_F64;
+  if (lt == T_FLOAT || rt == T_FLOAT) {
+    if ((op == CMP_EQ || op == CMP_NE) && (lt == T_LONG || rt == T_LONG)) return D_F64;
+    return D_F32;
+  }
+  if (lt == T_LONG || rt == T_LONG) return D_I64;
+  return D_I32;
+}
+
+struct Node {
+  int kind;  // 0 leaf operand, 1 cmp, 2 and, 3 other
+  Insn ins;
+  int l = -1, r = -1;
+};
+
+struct Lowered {
+  bool ok = false;
+  std::string why;
+  ChainQuery cq{};
+  std::vector<int> streams;
+};
+
+Lowered lower_query(const IProgram& P, int qi) {
+  Lowered L;
+  const IQuery& q = P.q[qi];
+  const int n = (int)q.st.size();
+  auto fail = [&](const std::string& w) { L.ok = false; L.why = fmt("query %d: %s", qi, w.c_str()); return L; };
+  if (q.partition >= 0) return fail("partitioned queries are not on the GPU path yet");
+  if (q.type != Q_PATTERN) return fail("sequences are not on the GPU path yet");
+  if (n < 1 || n > MAXS) return fail(fmt("%d states (chain kernel supports 1..%d)", n, MAXS));
+  ChainQuery& c = L.cq;
+  c.qid = qi;
+  c.n_states = n;
+  c.within = q.within;
+  for (int s = 0; s < n; ++s) {
+    const IState& st = q.st[s];
+    if (st.kind != K_STREAM) return fail("count/logical states are not on the GPU path yet");
+    if (st.is_start != (s == 0)) return fail("not a linear chain");
+    if (st.next_pre != (s + 1 < n ? s + 1 : -1)) return fail("not a linear chain");
+    if (s > 0 && st.next_every != -1) return fail("`every` inside the chain is not on the GPU path yet");
+    if (s == 0 && st.next_every != -1 && st.next_every != 0) return fail("every scope");
+    if (s > 0 && st.within_every != -1) return fail("within-every re-arm");
+    if (st.callback != -1) return fail("count callback");
+    if (st.has_selector != (s == n - 1)) return fail("selector placement");
+    c.state_stream[s] = st.stream;
+    if (std::find(L.streams.begin(), L.streams.end(), st.stream) == L.streams.end())
+      L.streams.push_back(st.stream);
+  }
+  c.every = q.st[0].next_every == 0;
+  c.n_attr = (int)P.stream_types[q.st[0].stream].size();
+  for (int s = 0; s < n; ++s)
+    if ((int)P.stream_types[q.st[s].stream].size() > MAXATTR) return fail("too many attributes");
+  // a single input stream and `every` make event-chunk warm-up exact
+  c.chunkable = (L.streams.size() == 1) && c.every && q.within >= 0 && n >= 2;
+
+  int na = 0;
+  for (int s = 0; s < n; ++s) {
+    c.atom_begin[s] = na;
+    for (const auto& code : q.st[s].filters) {
+      // postfix -> tree
+      std::vector<Node> nodes;
+      std::vector<int> stk;
+      for (const Insn& ins : code) {
+        Node nd;
+        nd.ins = ins;
+        if (ins.op == OP_CONST || ins.op == OP_ATTR) {
+          nd.kind = 0;
+        } else if (ins.op == OP_CMP || ins.op == OP_AND) {
+          nd.kind = ins.op == OP_CMP ? 1 : 2;
+          nd.r = stk.back(); stk.pop_back();
+          nd.l = stk.back(); stk.pop_back();
+        } else {
+          return fail("filter uses or/not/is-null/arithmetic (general predicate kernel pending)");
+        }
+        nodes.push_back(nd);
+        stk.push_back((int)nodes.size() - 1);
+      }
+      if (stk.size() != 1) return fail("malformed filter bytecode");
+      // flatten the conjunction into atoms
+      std::vector<int> todo{stk.back()};
+      std::vector<int> leaves;
+      while (!todo.empty()) {
+        int x = todo.back(); todo.pop_back();
+        if (nodes[x].kind == 2) { todo.push_back(nodes[x].r); todo.push_back(nodes[x].l); }
+        else leaves.push_back(x);
+      }
+      for (int x : leaves) {
+        if (na >= MAXATOM) return fail("too many predicate atoms");
+        Atom& A = c.atoms[na];
+        auto operand = [&](const Insn& in, int& k, int& idx, int& t, int64_t& cst) -> bool {
+          t = in.res;
+          if (in.op == OP_CONST) { k = OPK_CONST; cst = in.imm; idx = 0; return true; }
+          // ATTR: slot in.a, chain index in.b, attribute in.imm. Single-event slots: only
+          // CURRENT (-1) and 0 resolve to the event; other indices read null (StateEvent:138-182).
+          if (in.b != -1 && in.b != 0) { k = OPK_NULL; idx = 0; return true; }
+          if (in.a == s) { k = OPK_CUR; idx = (int)in.imm; return true; }
+          if (in.a > s) return false;
+          for (int cc = 0; cc < c.n_cap; ++cc)
+            if (c.cap_slot[cc] == in.a && c.cap_attr[cc] == in.imm) { k = OPK_CAP; idx = cc; return true; }
+          if (c.n_cap >= MAXCAP) return false;
+          c.cap_slot[c.n_cap] = (int)in.a;
+          c.cap_attr[c.n_cap] = (int)in.imm;
+          k = OPK_CAP;
+          idx = c.n_cap++;
+          return true;
+        };
+        const Node& nd = nodes[x];
+        if (nd.kind == 1) {
+          const Insn& li = nodes[nd.l].ins;
+          const Insn& ri = nodes[nd.r].ins;
+          if (nodes[nd.l].kind != 0 || nodes[nd.r].kind != 0)
+            return fail("compare of computed values (general predicate kernel pending)");
+          A.op = (int)nd.ins.imm;
+          if (!operand(li, A.lk, A.la, A.lt, A.lc) || !operand(ri, A.rk, A.ra, A.rt, A.rc))
+            return fail("operand not addressable");
+          A.dom = domain_of(A.lt, A.rt, A.op);
+        } else if (nd.kind == 0 && nd.ins.res == T_BOOL) {
+          // bare bool operand as a filter: FilterProcessor drops null and false
+          A.op = CMP_EQ;
+          if (!operand(nd.ins, A.lk, A.la, A.lt, A.lc)) return fail("operand not addressable");
+          A.rk = OPK_CONST; A.ra = 0; A.rt = T_BOOL; A.rc = 1;
+          A.dom = D_RAW;
+        } else {
+          return fail("unsupported filter form");
+        }
+        ++na;
+      }
+    }
+  }
+  c.atom_begin[n] = na;
+  for (int s = n + 1; s <= MAXS; ++s) c.atom_begin[s] = na;
+  L.ok = true;
+  return L;
+}
+
+int attr_width(int t) {
+  switch (t) {
+    case T_INT: case T_FLOAT: case T_STRING: return 4;
+    case T_BOOL: return 1;
+    default: return 8;
+  }
+}
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void ensure(size_t want) {
+    if (want <= n) return;
+    if (p) HIPCHK(hipFree(p));
+    p = nullptr;
+    n = 0;
+    size_t cap = std::max(want, n * 2);
+    HIPCHK(hipMalloc(&p, cap * sizeof(T)));
+    n = cap;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+struct HostMatch {
+  int64_t query, key, ts;
+  std::vector<int64_t> seqs;  // one event per slot (chain family)
+};
+
+}  // namespace
+
+struct sdh_engine {
+  sdh_config cfg{};
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  IProgram prog;
+  std::vector<Lowered> lq;           // local (this shard's) queries
+  int K = 1, pcap = 64, rec_words = 3;
+  DevBuf<ChainQuery> d_q;
+  DevBuf<InstHeader> d_hdr[2];
+  DevBuf<int64_t> d_part[2];
+  std::vector<int> cur;              // which buffer holds each local query's state
+  // batch staging for host-resident input
+  DevBuf<int64_t> d_ts;
+  std::vector<DevBuf<uint8_t>> d_col, d_nul;
+  std::vector<int64_t> prev_ts;      // per stream
+  int64_t seq = 0;
+  // last launch
+  DevBuf<WorkItem> d_work;
+  DevBuf<int64_t> d_seg_count, d_seg_off, d_dst_off, d_match, d_dense;
+  DevBuf<int32_t> d_err;
+  std::vector<WorkItem> work;
+  std::vector<int64_t> seg_count;
+  int64_t device_matches = 0;
+  bool device_unpolled = false;
+  std::vector<HostMatch> backlog;
+  // poll output
+  std::vector<int64_t> o_query, o_key, o_ts, o_off, o_words;
+  sdh_stats stats{};
+  std::string err;
+};
+
+namespace {
+
+void ensure_state(sdh_engine* e) {
+  const size_t nq = e->lq.size();
+  for (int b = 0; b < 2; ++b) {
+    e->d_hdr[b].ensure(std::max<size_t>(nq, 1));
+    e->d_part[b].ensure(std::max<size_t>(nq, 1) * NF * e->pcap);
+  }
+  // initial state: every query seeded (QueryRuntime.init -> StreamPreStateProcessor.init:157-166)
+  std::vector<InstHeader> h(nq);
+  for (auto& x : h) x = InstHeader{1, 0, 0, 0};
+  std::vector<int64_t> part(nq * NF * e->pcap, 0);
+  for (size_t q = 0; q < nq; ++q)
+    for (int l = 0; l < e->pcap; ++l) part[(q * NF + F_STATE) * e->pcap + l] = -1;
+  for (int b = 0; b < 2; ++b) {
+    if (nq) {
+      HIPCHK(hipMemcpy(e->d_hdr[b].p, h.data(), nq * sizeof(InstHeader), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(e->d_part[b].p, part.data(), part.size() * 8, hipMemcpyHostToDevice));
+    }
+  }
+  e->cur.assign(nq, 0);
+}
+
+void collect_device_matches(sdh_engine* e) {
+  if (!e->device_unpolled) return;
+  e->device_unpolled = false;
+  const int n_items = (int)e->work.size();
+  if (e->device_matches == 0 || n_items == 0) return;
+  std::vector<int64_t> seg_off(n_items), dst_off(n_items);
+  int64_t acc = 0;
+  for (int i = 0; i < n_items; ++i) {
+    seg_off[i] = e->work[i].seg_off;
+    dst_off[i] = acc;
+    acc += e->seg_count[i];
+  }
+  e->d_seg_off.ensure(n_items);
+  e->d_dst_off.ensure(n_items);
+  e->d_dense.ensure((size_t)acc * e->rec_words);
+  HIPCHK(hipMemcpyAsync(e->d_seg_off.p, seg_off.data(), n_items * 8, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemcpyAsync(e->d_dst_off.p, dst_off.data(), n_items * 8, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(sdh_launch_compact(e->d_match.p, e->d_seg_off.p, e->d_seg_count.p, e->d_dst_off.p,
+                            e->rec_words, n_items, e->d_dense.p, e->stream));
+  std::vector<int64_t> dense((size_t)acc * e->rec_words);
+  HIPCHK(hipMemcpyAsync(dense.data(), e->d_dense.p, dense.size() * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const size_t base = e->backlog.size();
+  e->backlog.resize(base + acc);
+  for (int64_t i = 0; i < acc; ++i) {
+    const int64_t* r = &dense[(size_t)i * e->rec_words];
+    HostMatch& m = e->backlog[base + i];
+    m.query = r[0];
+    m.key = -1;
+    m.ts = r[1];
+    const int S = (int)e->prog.q[m.query].st.size();
+    m.seqs.assign(r + 2, r + 2 + S);
+  }
+  e->device_matches = 0;
+}
+
+void d2h_sync(sdh_engine* e, void* dst, const void* src, size_t bytes) {
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+}
+
+void launch(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2],
+            const std::vector<int>& qs, bool allow_chunks, bool* unordered) {
+  const int64_t n = B.n;
+  // chunk planning: enough waves to fill 256 CUs, chunks >> the warm-up window
+  double ev_per_ms = 1.0;
+  if (n > 1) ev_per_ms = (double)n / (double)std::max<int64_t>(1, t01[1] - t01[0]);
+  const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : 8192;
+  const int64_t target_waves = 16384;
+  e->work.clear();
+  int64_t seg = 0;
+  int64_t per_query_target = std::max<int64_t>(1, target_waves / std::max<size_t>(1, qs.size()));
+  for (int li : qs) {
+    const ChainQuery& c = e->lq[li].cq;
+    int64_t C = 1;
+    if (allow_chunks && c.chunkable && n > 2 * min_chunk) {
+      const double warm = (double)c.within * ev_per_ms + 64.0;
+      const int64_t by_warm = (int64_t)((double)n / std::max(8.0 * warm, (double)min_chunk));
+      C = std::max<int64_t>(1, std::min<int64_t>(by_warm, per_query_target));
+      C = std::min<int64_t>(C, n / min_chunk);
+      C = std::max<int64_t>(C, 1);
+    }
+    for (int64_t ch = 0; ch < C; ++ch) {
+      WorkItem w{};
+      w.q = li;
+      w.chunk = (int)ch;
+      w.n_chunks = (int)C;
+      w.inb = e->cur[li];
+      w.c0 = n * ch / C;
+      w.c1 = n * (ch + 1) / C;
+      w.seg_off = seg;
+      w.seg_cap = (w.c1 - w.c0) + e->pcap + 1;
+      seg += w.seg_cap;
+      e->work.push_back(w);
+    }
+  }
+  const int n_items = (int)e->work.size();
+  e->d_work.ensure(n_items);
+  e->d_seg_count.ensure(n_items);
+  e->d_match.ensure((size_t)seg * e->rec_words);
+  e->d_err.ensure(4);
+  HIPCHK(hipMemcpyAsync(e->d_work.p, e->work.data(), n_items * sizeof(WorkItem), hipMemcpyHostToDevice,
+                        e->stream));
+  HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
+  ChainLaunch L{};
+  L.queries = e->d_q.p;
+  L.work = e->d_work.p;
+  L.n_work = n_items;
+  L.pcap = e->pcap;
+  L.b = B;
+  for (int b = 0; b < 2; ++b) {
+    L.hdr[b] = e->d_hdr[b].p;
+    L.part[b] = e->d_part[b].p;
+  }
+  L.match = e->d_match.p;
+  L.rec_words = e->rec_words;
+  L.seg_count = e->d_seg_count.p;
+  L.err = e->d_err.p;
+  const int blocks = (n_items + 3) / 4;
+  const size_t lds = (size_t)4 * WAVE * (B.n_attr + 2) * 8;
+  HIPCHK(hipEventRecord(e->ev0, e->stream));
+  HIPCHK(sdh_launch_chain(e->K, &L, blocks, lds, e->stream));
+  HIPCHK(hipEventRecord(e->ev1, e->stream));
+  int32_t errs[4];
+  e->seg_count.resize(n_items);
+  HIPCHK(hipMemcpyAsync(errs, e->d_err.p, 16, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(e->seg_count.data(), e->d_seg_count.p, n_items * 8, hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+  e->stats.last_kernel_ms = ms;
+  if (errs[0]) throw Error(SDH_E_CAPACITY, "partial-match table overflow: raise partials_per_inst");
+  if (errs[2]) throw Error(SDH_E_CAPACITY, "match segment overflow");
+  *unordered = errs[1] != 0;
+  // algorithmic bytes of this launch: every item streams its [w0, c1) events once
+  // (approximated by c1-c0 plus warm-up), reads and writes its partial table, writes its matches
+  int64_t ev_bytes = 8;
+  for (int a = 0; a < B.n_attr; ++a) ev_bytes += B.width[a];
+  double bytes = 0;
+  int64_t total_matches = 0;
+  for (int i = 0; i < n_items; ++i) {
+    const WorkItem& w = e->work[i];
+    const ChainQuery& c = e->lq[w.q].cq;
+    double warm = w.chunk > 0 ? std::min<double>((double)w.c0, (double)c.within * ev_per_ms) : 0.0;
+    bytes += ((double)(w.c1 - w.c0) + warm) * ev_bytes;
+    total_matches += e->seg_count[i];
+  }
+  bytes += (double)qs.size() * 2.0 * NF * e->pcap * 8;  // partial tables in + out
+  bytes += (double)total_matches * e->rec_words * 8;
+  e->stats.last_kernel_bytes = bytes;
+  e->device_matches = total_matches;
+}
+
+int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
+  if (!b || stream < 0 || stream >= (int)e->prog.stream_types.size())
+    throw Error(SDH_E_INVALID, "bad stream or batch");
+  const auto& types = e->prog.stream_types[stream];
+  const int na = (int)types.size();
+  if (b->n_cols != na) throw Error(SDH_E_INVALID, fmt("stream %d has %d attributes, batch has %d", stream, na, b->n_cols));
+  if (b->n < 0 || (e->cfg.max_batch > 0 && b->n > e->cfg.max_batch))
+    throw Error(SDH_E_INVALID, "batch larger than max_batch");
+  if (b->n == 0) return SDH_OK;
+  HIPCHK(hipSetDevice(e->dev));
+  // matches of the previous push that were not polled move to the host backlog
+  collect_device_matches(e);
+  StreamBatch B{};
+  B.n = b->n;
+  B.n_attr = na;
+  B.stream = stream;
+  B.seq_base = e->seq;
+  B.prev_ts = e->prev_ts[stream];
+  for (int a = 0; a < na; ++a) B.width[a] = attr_width(types[a]);
+  if (b->on_device) {
+    B.ts = b->ts;
+    for (int a = 0; a < na; ++a) {
+      B.col[a] = b->cols[a];
+      B.nul[a] = b->nulls ? b->nulls[a] : nullptr;
+    }
+  } else {
+    e->d_ts.ensure(b->n);
+    HIPCHK(hipMemcpyAsync(e->d_ts.p, b->ts, b->n * 8, hipMemcpyHostToDevice, e->stream));
+    B.ts = e->d_ts.p;
+    if ((int)e->d_col.size() < na) {
+      e->d_col.resize(na);
+      e->d_nul.resize(na);
+    }
+    for (int a = 0; a < na; ++a) {
+      e->d_col[a].ensure((size_t)b->n * B.width[a]);
+      HIPCHK(hipMemcpyAsync(e->d_col[a].p, b->cols[a], (size_t)b->n * B.width[a], hipMemcpyHostToDevice, e->stream));
+      B.col[a] = e->d_col[a].p;
+      B.nul[a] = nullptr;
+      if (b->nulls && b->nulls[a]) {
+        e->d_nul[a].ensure(b->n);
+        HIPCHK(hipMemcpyAsync(e->d_nul[a].p, b->nulls[a], b->n, hipMemcpyHostToDevice, e->stream));
+        B.nul[a] = e->d_nul[a].p;
+      }
+    }
+  }
+  std::vector<int> qs;
+  for (int li = 0; li < (int)e->lq.size(); ++li)
+    if (std::find(e->lq[li].streams.begin(), e->lq[li].streams.end(), stream) != e->lq[li].streams.end())
+      qs.push_back(li);
+  int64_t t01[2];
+  if (b->on_device) {
+    d2h_sync(e, &t01[0], B.ts, 8);
+    d2h_sync(e, &t01[1], B.ts + (b->n - 1), 8);
+  } else {
+    t01[0] = b->ts[0];
+    t01[1] = b->ts[b->n - 1];
+  }
+  if (!qs.empty()) {
+    bool unordered = false;
+    launch(e, stream, B, t01, qs, true, &unordered);
+    bool chunked = false;
+    for (auto& w : e->work) chunked |= w.n_chunks > 1;
+    if (unordered && chunked) launch(e, stream, B, t01, qs, false, &unordered);  // exact fallback
+    for (int li : qs) e->cur[li] ^= 1;
+    e->device_unpolled = true;
+    e->stats.pattern_events += b->n * (int64_t)qs.size();
+    e->stats.matches += e->device_matches;
+  }
+  e->prev_ts[stream] = t01[1];
+  e->seq += b->n;
+  e->stats.events += b->n;
+  return SDH_OK;
+}
+
+template <class F>
+int guard(sdh_engine* e, F f) {
+  try {
+    return f();
+  } catch (const Error& ex) {
+    if (e) e->err = ex.what();
+    return ex.code;
+  } catch (const std::exception& ex) {
+    if (e) e->err = ex.what();
+    return SDH_E_INVALID;
+  }
+}
+
+thread_local std::string g_create_error;
+
+}  // namespace
+
+extern "C" {
+
+const char* sdh_version(void) { return "libsiddhi_hip 0.1 (gfx950, chain NFA kernel)"; }
+
+int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_engine** out) {
+  if (!out) return SDH_E_INVALID;
+  *out = nullptr;
+  sdh_engine* e = new sdh_engine;
+  int rc = guard(e, [&]() {
+    if (cfg) e->cfg = *cfg;
+    if (e->cfg.shard_world <= 0) e->cfg.shard_world = 1;
+    e->dev = e->cfg.device;
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (ndev <= 0) throw Error(SDH_E_DEVICE, "no HIP device (the engine has no CPU fallback)");
+    HIPCHK(hipSetDevice(e->dev));
+    e->prog = read_ir(ir, len);
+    for (int qi = 0; qi < (int)e->prog.q.size(); ++qi) {
+      if (qi % e->cfg.shard_world != e->cfg.shard_rank) continue;
+      Lowered L = lower_query(e->prog, qi);
+      if (!L.ok) throw Error(SDH_E_UNSUPPORTED, L.why);
+      e->lq.push_back(L);
+    }
+    int want = e->cfg.partials_per_inst > 0 ? e->cfg.partials_per_inst : 128;
+    e->K = want <= 64 ? 1 : want <= 128 ? 2 : want <= 256 ? 4 : 8;
+    e->pcap = 64 * e->K;
+    int maxS = 1;
+    for (auto& L : e->lq) maxS = std::max(maxS, L.cq.n_states);
+    e->rec_words = 2 + maxS;
+    e->prev_ts.assign(e->prog.stream_types.size(), INT64_MIN);
+    HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&e->ev0));
+    HIPCHK(hipEventCreate(&e->ev1));
+    e->d_q.ensure(std::max<size_t>(1, e->lq.size()));
+    std::vector<ChainQuery> cqs;
+    for (auto& L : e->lq) cqs.push_back(L.cq);
+    if (!cqs.empty())
+      HIPCHK(hipMemcpy(e->d_q.p, cqs.data(), cqs.size() * sizeof(ChainQuery), hipMemcpyHostToDevice));
+    ensure_state(e);
+    return SDH_OK;
+  });
+  if (rc != SDH_OK) {
+    g_create_error = e->err;
+    delete e;
+    return rc;
+  }
+  *out = e;
+  return SDH_OK;
+}
+
+int sdh_engine_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
+  if (!e) return SDH_E_INVALID;
+  return guard(e, [&]() { return do_push(e, stream, b); });
+}
+
+int sdh_engine_flush(sdh_engine* e) {
+  if (!e) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return SDH_OK;
+  });
+}
+
+int sdh_engine_pending_matches(sdh_engine* e, int64_t* n) {
+  if (!e || !n) return SDH_E_INVALID;
+  *n = (int64_t)e->backlog.size() + (e->device_unpolled ? e->device_matches : 0);
+  return SDH_OK;
+}
+
+int sdh_engine_poll(sdh_engine* e, sdh_matches* out) {
+  if (!e || !out) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    collect_device_matches(e);
+    auto& v = e->backlog;
+    // reference delivery order (R18): per event, per query, per pending partial in insertion
+    // order -- for chain queries the pending list is ordered by the earlier slots' events
+    std::stable_sort(v.begin(), v.end(), [](const HostMatch& a, const HostMatch& b) {
+      if (a.seqs.back() != b.seqs.back()) return a.seqs.back() < b.seqs.back();
+      if (a.query != b.query) return a.query < b.query;
+      for (int k = (int)a.seqs.size() - 2; k >= 0; --k)
+        if (a.seqs[k] != b.seqs[k]) return a.seqs[k] < b.seqs[k];
+      return false;
+    });
+    const size_t n = v.size();
+    e->o_query.resize(n);
+    e->o_key.resize(n);
+    e->o_ts.resize(n);
+    e->o_off.resize(n + 1);
+    e->o_words.clear();
+    for (size_t i = 0; i < n; ++i) {
+      e->o_query[i] = v[i].query;
+      e->o_key[i] = v[i].key;
+      e->o_ts[i] = v[i].ts;
+      e->o_off[i] = (int64_t)e->o_words.size();
+      for (int64_t s : v[i].seqs) {
+        e->o_words.push_back(1);
+        e->o_words.push_back(s);
+      }
+    }
+    e->o_off[n] = (int64_t)e->o_words.size();
+    v.clear();
+    out->n = (int64_t)n;
+    out->query = e->o_query.data();
+    out->key = e->o_key.data();
+    out->ts = e->o_ts.data();
+    out->off = e->o_off.data();
+    out->words = e->o_words.data();
+    return SDH_OK;
+  });
+}
+
+int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
+  if (!e || !out) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    std::vector<InstHeader> h(e->lq.size());
+    int64_t live = 0;
+    for (size_t q = 0; q < e->lq.size(); ++q) {
+      HIPCHK(hipMemcpy(&h[q], e->d_hdr[e->cur[q]].p + q, sizeof(InstHeader), hipMemcpyDeviceToHost));
+      live += h[q].n_live;
+    }
+    e->stats.live_partials = live;
+    *out = e->stats;
+    return SDH_OK;
+  });
+}
+
+// snapshot: [magic][n_q][pcap][seq][n_streams][prev_ts...] then per query header + table
+int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
+  if (!e || !blob || !len) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const size_t nq = e->lq.size();
+    const size_t tbl = (size_t)NF * e->pcap;
+    std::vector<int64_t> w{0x5344485350415254LL, (int64_t)nq, e->pcap, e->seq, (int64_t)e->prev_ts.size()};
+    w.insert(w.end(), e->prev_ts.begin(), e->prev_ts.end());
+    for (size_t q = 0; q < nq; ++q) {
+      InstHeader h;
+      HIPCHK(hipMemcpy(&h, e->d_hdr[e->cur[q]].p + q, sizeof h, hipMemcpyDeviceToHost));
+      w.push_back(h.seed_alive);
+      w.push_back(h.n_live);
+      size_t o = w.size();
+      w.resize(o + tbl);
+      HIPCHK(hipMemcpy(&w[o], e->d_part[e->cur[q]].p + q * tbl, tbl * 8, hipMemcpyDeviceToHost));
+    }
+    *len = w.size() * 8;
+    *blob = malloc(*len);
+    memcpy(*blob, w.data(), *len);
+    return SDH_OK;
+  });
+}
+
+int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
+  if (!e || !blob) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    const int64_t* w = (const int64_t*)blob;
+    size_t nw = len / 8, i = 0;
+    auto nx = [&]() {
+      if (i >= nw) throw Error(SDH_E_INVALID, "snapshot truncated");
+      return w[i++];
+    };
+    if (nx() != 0x5344485350415254LL) throw Error(SDH_E_INVALID, "bad snapshot magic");
+    const size_t nq = (size_t)nx();
+    if (nq != e->lq.size() || nx() != e->pcap) throw Error(SDH_E_INVALID, "snapshot of a different program");
+    e->seq = nx();
+    const size_t ns = (size_t)nx();
+    if (ns != e->prev_ts.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
+    for (auto& t : e->prev_ts) t = nx();
+    const size_t tbl = (size_t)NF * e->pcap;
+    for (size_t q = 0; q < nq; ++q) {
+      InstHeader h{(int32_t)nx(), (int32_t)nx(), 0, 0};
+      if (i + tbl > nw) throw Error(SDH_E_INVALID, "snapshot truncated");
+      HIPCHK(hipMemcpy(e->d_hdr[e->cur[q]].p + q, &h, sizeof h, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(e->d_part[e->cur[q]].p + q * tbl, &w[i], tbl * 8, hipMemcpyHostToDevice));
+      i += tbl;
+    }
+    e->backlog.clear();
+    e->device_unpolled = false;
+    e->device_matches = 0;
+    return SDH_OK;
+  });
+}
+
+void sdh_free(void* p) { free(p); }
+
+void sdh_engine_destroy(sdh_engine* e) {
+  if (!e) return;
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+const char* sdh_last_error(sdh_engine* e) { return e ? e->err.c_str() : g_create_error.c_str(); }
+
+}  // extern "C"

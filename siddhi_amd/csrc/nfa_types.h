@@ -1,0 +1,96 @@
+// nfa_types.h -- device-visible program tables of the MI355X NFA engine (host + device).
+//
+// A query of the "chain" family (every? s0 -> s1 -> ... -> s{n-1} [within T], stream states
+// only) is lowered to a ChainQuery: per state its stream and a conjunction of compare atoms
+// (the predicate bytecode), plus the captured attribute values later filters read
+// (e.g. e1.price for `price > e1.price`). Device kernels read these tables through the scalar
+// cache (all fields are wave-uniform).
+#pragma once
+#include <stdint.h>
+
+namespace sdh {
+
+constexpr int MAXS = 4;      // states per chain query
+constexpr int MAXCAP = 4;    // captured attribute values per partial match
+constexpr int MAXATOM = 12;  // compare atoms per query (all states)
+constexpr int MAXATTR = 16;  // attributes per stream
+constexpr int WAVE = 64;
+
+enum AttrType { T_INT = 0, T_LONG, T_FLOAT, T_DOUBLE, T_BOOL, T_STRING };
+// compare domain = the precision Java evaluates the typed compare in
+enum Domain { D_I32 = 0, D_I64, D_F32, D_F64, D_RAW };
+// operand kinds
+enum OpKind { OPK_CUR = 0, OPK_CAP, OPK_CONST, OPK_NULL };
+enum CmpOp { CMP_EQ = 0, CMP_NE, CMP_GT, CMP_GE, CMP_LT, CMP_LE };
+
+struct Atom {
+  int32_t op, dom;
+  int32_t lk, la, lt;  // lhs kind, attr index (CUR) / capture index (CAP), attribute type
+  int32_t rk, ra, rt;
+  int64_t lc, rc;      // raw constant words (CONST)
+};
+
+struct ChainQuery {
+  int32_t qid;          // index of the query in the program
+  int32_t n_states;
+  int32_t every;        // 1: `every` on the start state
+  int32_t n_cap;
+  int64_t within;       // ms, -1 = no within
+  int32_t chunkable;    // planner proof that warm-up chunking is exact
+  int32_t n_attr;       // attributes of the (first) stream
+  int32_t state_stream[MAXS];
+  int32_t atom_begin[MAXS + 1];
+  int32_t cap_slot[MAXCAP], cap_attr[MAXCAP];
+  Atom atoms[MAXATOM];
+};
+
+// one wave of the NFA-step launch = one (query instance, event chunk)
+struct WorkItem {
+  int32_t q;            // index into the ChainQuery table
+  int32_t chunk, n_chunks;
+  int32_t inb;          // which of the two state buffers holds the instance's current state
+  int64_t c0, c1;       // events of the batch whose emissions this item owns
+  int64_t seg_off;      // first match record of this item's output segment
+  int64_t seg_cap;      // capacity of the segment (records)
+};
+
+// persisted partial-match table of one query instance: NF fields x PCAP lanes (SoA, int64)
+enum Field { F_STATE = 0, F_TS0, F_SEQ0, F_SEQ1, F_SEQ2, F_CAP0, F_CAP1, F_CAP2, F_CAP3, F_CAPNULL, NF };
+static_assert(F_SEQ0 + MAXS - 1 == F_CAP0, "seq fields");
+static_assert(F_CAP0 + MAXCAP == F_CAPNULL, "cap fields");
+
+struct InstHeader {
+  int32_t seed_alive;   // start state still holds its seed (non-every patterns consume it)
+  int32_t n_live;       // live partials
+  int32_t overflow;     // partial table overflowed
+  int32_t unordered;    // batch timestamps not monotone (chunked items must be re-run)
+};
+
+struct StreamBatch {
+  const int64_t* ts;
+  const void* col[MAXATTR];
+  const uint8_t* nul[MAXATTR];
+  int32_t width[MAXATTR];   // bytes per element (4 or 8; bool 1)
+  int32_t n_attr;
+  int32_t stream;
+  int64_t n;
+  int64_t seq_base;         // global sequence number of event 0
+  int64_t prev_ts;          // last timestamp of the previous batch of this stream (INT64_MIN: none)
+};
+
+struct ChainLaunch {
+  const ChainQuery* queries;
+  const WorkItem* work;
+  int32_t n_work;
+  int32_t pcap;             // partial capacity per instance (64 * K)
+  StreamBatch b;
+  InstHeader* hdr[2];       // double-buffered instance headers  [q]
+  int64_t* part[2];         // double-buffered partial tables     [q][NF][pcap]
+  int64_t* match;           // records of rec_words int64
+  int32_t rec_words;
+  int32_t pad;
+  int64_t* seg_count;       // per work item: matches written
+  int32_t* err;             // [0] overflow, [1] unordered, [2] segment overflow
+};
+
+}  // namespace sdh

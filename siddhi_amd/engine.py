@@ -1,0 +1,214 @@
+"""ctypes binding of libsiddhi_hip.so (include/siddhi_hip.h).
+
+This is the product path: it loads the in-tree HIP library and fails loudly when it is missing or
+when no GPU is visible -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .ir import T_BOOL, T_DOUBLE, T_FLOAT, T_INT, T_LONG, T_STRING
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsiddhi_hip.so")
+
+SDH_OK = 0
+ERRORS = {-1: "SDH_E_INVALID", -2: "SDH_E_UNSUPPORTED", -3: "SDH_E_DEVICE", -4: "SDH_E_CAPACITY",
+          -5: "SDH_E_REFERENCE"}
+
+
+class SdhConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("shard_rank", ctypes.c_int32),
+                ("shard_world", ctypes.c_int32), ("partials_per_inst", ctypes.c_int32),
+                ("max_batch", ctypes.c_int64), ("match_capacity", ctypes.c_int64),
+                ("chunk_events", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+class SdhBatch(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("ts", ctypes.c_void_p), ("cols", ctypes.POINTER(ctypes.c_void_p)),
+                ("nulls", ctypes.POINTER(ctypes.c_void_p)), ("n_cols", ctypes.c_int32),
+                ("on_device", ctypes.c_int32)]
+
+
+class SdhMatches(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("query", ctypes.POINTER(ctypes.c_int64)),
+                ("key", ctypes.POINTER(ctypes.c_int64)), ("ts", ctypes.POINTER(ctypes.c_int64)),
+                ("off", ctypes.POINTER(ctypes.c_int64)), ("words", ctypes.POINTER(ctypes.c_int64))]
+
+
+class SdhStats(ctypes.Structure):
+    _fields_ = [("events", ctypes.c_int64), ("pattern_events", ctypes.c_int64),
+                ("matches", ctypes.c_int64), ("live_partials", ctypes.c_int64),
+                ("last_kernel_ms", ctypes.c_double), ("last_kernel_bytes", ctypes.c_double)]
+
+
+EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engine_poll",
+           "sdh_engine_pending_matches", "sdh_engine_stats", "sdh_engine_snapshot",
+           "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version"]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libsiddhi_hip.so; raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                           "(the HIP engine has no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    lib.sdh_engine_create.argtypes = [P, ctypes.c_size_t, ctypes.POINTER(SdhConfig), ctypes.POINTER(P)]
+    lib.sdh_engine_push.argtypes = [P, ctypes.c_int32, ctypes.POINTER(SdhBatch)]
+    lib.sdh_engine_flush.argtypes = [P]
+    lib.sdh_engine_poll.argtypes = [P, ctypes.POINTER(SdhMatches)]
+    lib.sdh_engine_pending_matches.argtypes = [P, ctypes.POINTER(ctypes.c_int64)]
+    lib.sdh_engine_stats.argtypes = [P, ctypes.POINTER(SdhStats)]
+    lib.sdh_engine_snapshot.argtypes = [P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
+    lib.sdh_engine_restore.argtypes = [P, ctypes.c_void_p, ctypes.c_size_t]
+    lib.sdh_free.argtypes = [P]
+    lib.sdh_engine_destroy.argtypes = [P]
+    lib.sdh_last_error.argtypes = [P]
+    lib.sdh_last_error.restype = ctypes.c_char_p
+    lib.sdh_version.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+_NP_OF = {T_INT: np.int32, T_LONG: np.int64, T_FLOAT: np.uint32, T_DOUBLE: np.int64, T_BOOL: np.uint8,
+          T_STRING: np.int32}
+
+
+def columns_from_words(vals: np.ndarray, types: Sequence[int]) -> List[np.ndarray]:
+    """Raw 64-bit attribute words [n, a] -> native-width columns (see sdh_batch)."""
+    cols = []
+    for j, t in enumerate(types):
+        w = vals[:, j]
+        if t in (T_FLOAT,):
+            cols.append(np.ascontiguousarray((w & 0xFFFFFFFF).astype(np.uint32)))
+        elif t in (T_INT, T_STRING):
+            cols.append(np.ascontiguousarray(w.astype(np.int64).astype(np.int32)))
+        elif t == T_BOOL:
+            cols.append(np.ascontiguousarray(w.astype(np.uint8)))
+        else:
+            cols.append(np.ascontiguousarray(w.astype(np.int64)))
+    return cols
+
+
+class HipEngine:
+    """One engine instance on one GPU."""
+
+    def __init__(self, blob: bytes, device: int = 0, partials: int = 128, shard_rank: int = 0,
+                 shard_world: int = 1, chunk_events: int = 0, stream_types=None):
+        self.lib = load_library()
+        cfg = SdhConfig(device=device, shard_rank=shard_rank, shard_world=shard_world,
+                        partials_per_inst=partials, max_batch=0, match_capacity=0,
+                        chunk_events=chunk_events, flags=0)
+        self.h = ctypes.c_void_p()
+        self._blob = ctypes.create_string_buffer(blob, len(blob))
+        rc = self.lib.sdh_engine_create(self._blob, len(blob), ctypes.byref(cfg), ctypes.byref(self.h))
+        if rc != SDH_OK:
+            raise EngineError(rc, self.lib.sdh_last_error(None).decode())
+        self.stream_types = stream_types
+
+    def _check(self, rc):
+        if rc != SDH_OK:
+            raise EngineError(rc, self.lib.sdh_last_error(self.h).decode())
+
+    def push_columns(self, stream: int, ts: np.ndarray, cols: Sequence[np.ndarray],
+                     nulls: Optional[Sequence[Optional[np.ndarray]]] = None):
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        keep = [ts] + list(cols)
+        cp = (ctypes.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+        nptr = None
+        if nulls is not None:
+            nl = [None if x is None else np.ascontiguousarray(x, dtype=np.uint8) for x in nulls]
+            keep += [x for x in nl if x is not None]
+            nptr = (ctypes.c_void_p * len(cols))(*[0 if x is None else x.ctypes.data for x in nl])
+        b = SdhBatch(n=len(ts), ts=ts.ctypes.data, cols=cp, nulls=nptr, n_cols=len(cols), on_device=0)
+        self._check(self.lib.sdh_engine_push(self.h, stream, ctypes.byref(b)))
+        del keep
+
+    def push_device(self, stream: int, n: int, ts_ptr: int, col_ptrs: Sequence[int]):
+        """Push a batch whose columns are already resident in HBM (e.g. torch CUDA tensors)."""
+        cp = (ctypes.c_void_p * len(col_ptrs))(*col_ptrs)
+        b = SdhBatch(n=n, ts=ts_ptr, cols=cp, nulls=None, n_cols=len(col_ptrs), on_device=1)
+        self._check(self.lib.sdh_engine_push(self.h, stream, ctypes.byref(b)))
+
+    # interface used by tests/harness.App -------------------------------------------------------
+    def send(self, stream: int, ts, vals: np.ndarray, nulls: Optional[np.ndarray], as_chunk=False):
+        types = self.stream_types[stream]
+        cols = columns_from_words(np.asarray(vals, dtype=np.int64).reshape(len(ts), len(types)), types)
+        nl = None
+        if nulls is not None and np.any(nulls):
+            nl = [np.ascontiguousarray(nulls[:, j]) for j in range(len(types))]
+        self.push_columns(stream, np.asarray(ts, dtype=np.int64), cols, nl)
+
+    def poll(self):
+        m = SdhMatches()
+        self._check(self.lib.sdh_engine_poll(self.h, ctypes.byref(m)))
+        n = m.n
+        if n == 0:
+            return (np.zeros(0, np.int64),) * 4 + (np.zeros(0, np.int64),)
+        q = np.ctypeslib.as_array(m.query, shape=(n,)).copy()
+        k = np.ctypeslib.as_array(m.key, shape=(n,)).copy()
+        ts = np.ctypeslib.as_array(m.ts, shape=(n,)).copy()
+        off = np.ctypeslib.as_array(m.off, shape=(n + 1,)).copy()
+        words = np.ctypeslib.as_array(m.words, shape=(int(off[-1]),)).copy() if off[-1] else np.zeros(0, np.int64)
+        return q, k, ts, off, words
+
+    def take_matches(self, n_slots_of):
+        q, k, ts, off, words = self.poll()
+        out = []
+        for i in range(len(q)):
+            w = words[off[i]:off[i + 1]]
+            slots, j = [], 0
+            for _ in range(n_slots_of(int(q[i]))):
+                c = int(w[j])
+                slots.append(tuple(int(x) for x in w[j + 1:j + 1 + c]))
+                j += 1 + c
+            out.append((int(q[i]), int(k[i]), int(ts[i]), tuple(slots)))
+        return out
+
+    def pending_matches(self) -> int:
+        n = ctypes.c_int64()
+        self._check(self.lib.sdh_engine_pending_matches(self.h, ctypes.byref(n)))
+        return n.value
+
+    def stats(self) -> SdhStats:
+        s = SdhStats()
+        self._check(self.lib.sdh_engine_stats(self.h, ctypes.byref(s)))
+        return s
+
+    def snapshot(self) -> bytes:
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._check(self.lib.sdh_engine_snapshot(self.h, ctypes.byref(p), ctypes.byref(n)))
+        data = ctypes.string_at(p, n.value)
+        self.lib.sdh_free(p)
+        return data
+
+    def restore(self, blob: bytes):
+        buf = ctypes.create_string_buffer(blob, len(blob))
+        self._check(self.lib.sdh_engine_restore(self.h, buf, len(blob)))
+
+    def close(self):
+        if getattr(self, "h", None) and self.h:
+            self.lib.sdh_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

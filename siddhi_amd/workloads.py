@@ -1,0 +1,81 @@
+"""Seeded synthetic streams and pattern families of SURVEY.md §8(d) / BASELINE.json configs.
+
+Counter-based: h_j(i) = splitmix64(seed ^ (4*i + j)), so any shard can regenerate any range.
+
+* ts_i     = 1_700_000_000_000 + i                 (1 event / ms)
+* price_i  = (float)(h_1 % 10000) / 100.0f         in [0, 100)
+* volume_i = 1 + h_2 % 1000
+* sym_i    = h_3 % K                               (dictionary id of "SYM<k>")
+
+C1: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 10 sec
+C2: P patterns  every e1=StockStream[price > T_p] -> e2=StockStream[price > e1.price] within W_p
+    T_p = 20 + (p % 750) / 10.0 (a DOUBLE literal -> Float x Double compare),
+    W_p in {1, 10, 60} sec picked by splitmix64(7 ^ p) % 3.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+TS0 = 1_700_000_000_000
+EVENT_SEED = 42
+PATTERN_SEED = 7
+STOCK_STREAM = "define stream StockStream (symbol string, price float, volume int);"
+
+_M64 = (1 << 64) - 1
+
+
+def splitmix64_np(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def splitmix64(x: int) -> int:
+    z = (x + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def stock_events(start: int, n: int, n_symbols: int = 100, seed: int = EVENT_SEED):
+    """Events [start, start+n) of the seeded StockStream: (ts int64, sym int32, price float32,
+    volume int32)."""
+    i = np.arange(start, start + n, dtype=np.uint64)
+    s = np.uint64(seed)
+    h1 = splitmix64_np(s ^ (i * np.uint64(4) + np.uint64(1)))
+    h2 = splitmix64_np(s ^ (i * np.uint64(4) + np.uint64(2)))
+    h3 = splitmix64_np(s ^ (i * np.uint64(4) + np.uint64(3)))
+    ts = (np.int64(TS0) + i.astype(np.int64)).astype(np.int64)
+    price = (h1 % np.uint64(10000)).astype(np.float32) / np.float32(100.0)
+    volume = (np.uint64(1) + h2 % np.uint64(1000)).astype(np.int32)
+    sym = (h3 % np.uint64(n_symbols)).astype(np.int32)
+    return ts, sym, price.astype(np.float32), volume
+
+
+def c1_app() -> str:
+    return (STOCK_STREAM + " @info(name='q0') from every e1=StockStream[price>20] -> "
+            "e2=StockStream[price>e1.price] within 10 sec select e1.price as p1, e2.price as p2 "
+            "insert into OutStream;")
+
+
+def c2_threshold_text(p: int) -> str:
+    t10 = 200 + (p % 750)
+    return f"{t10 // 10}.{t10 % 10}"
+
+
+def c2_within_sec(p: int, seed: int = PATTERN_SEED) -> int:
+    return (1, 10, 60)[splitmix64(seed ^ p) % 3]
+
+
+def c2_app(n_patterns: int, within=None) -> str:
+    """1K concurrent 2-state filter+reference patterns (BASELINE.json configs[1])."""
+    qs = [STOCK_STREAM]
+    for p in range(n_patterns):
+        w = c2_within_sec(p) if within is None else within
+        qs.append(f"@info(name='p{p}') from every e1=StockStream[price > {c2_threshold_text(p)}] -> "
+                  f"e2=StockStream[price > e1.price] within {w} sec "
+                  f"select e1.price as p1, e2.price as p2 insert into OutStream;")
+    return " ".join(qs)
