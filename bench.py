@@ -87,13 +87,13 @@ def main():
     dev = torch.device("cuda", local)
 
     from siddhi_amd import ql
-    from siddhi_amd.engine import HipEngine
+    from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES, HipEngine
     from siddhi_amd.planner import plan
     from siddhi_amd.workloads import stock_events
 
     P = args.patterns
     ir = plan(ql.parse(c2_app_for_rank(rank, P)))
-    eng = HipEngine(ir.serialize(), device=local, partials=args.partials)
+    eng = HipEngine(ir.serialize(), device=local, partials=args.partials, flags=SDH_FLAG_DEVICE_MATCHES)
 
     B = args.batch
     n_batches = args.warmup + args.steps

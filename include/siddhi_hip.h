@@ -51,13 +51,18 @@ typedef struct sdh_config {
   int64_t max_batch;         /* max events per push                                          */
   int64_t match_capacity;    /* max matches held between polls (0 = sized automatically)     */
   int32_t chunk_events;      /* target events per parallel chunk (0 = automatic)             */
-  int32_t flags;             /* reserved, 0                                                  */
+  int32_t flags;             /* SDH_FLAG_*                                                   */
 } sdh_config;
+
+/* Matches of a push that are not polled before the next push are dropped instead of being copied
+ * to the host (they stay countable via sdh_engine_pending_matches until then). For consumers that
+ * read matches on the device, and for throughput benchmarking of the NFA step. */
+#define SDH_FLAG_DEVICE_MATCHES 1
 
 /* One columnar (SoA) batch of events of one stream, in arrival order.
  * cols[a] points to n elements of attribute a with the stream schema's native width:
  *   INT -> int32, LONG -> int64, FLOAT -> float, DOUBLE -> double, BOOL -> uint8,
- *   STRING -> int32 dictionary id (sdh_intern).
+ *   STRING -> int32 dictionary id (ids are assigned by the caller; equal strings, equal ids).
  * nulls[a] (optional, may be NULL or have NULL entries) is a uint8 mask, 1 = null.
  * on_device != 0: all pointers are HIP device pointers already resident in HBM; otherwise they
  * are host pointers (pinned memory recommended) and are copied before sdh_engine_push returns. */

@@ -314,10 +314,6 @@ struct DevBuf {
   }
 };
 
-struct HostMatch {
-  int64_t query, key, ts;
-  std::vector<int64_t> seqs;  // one event per slot (chain family)
-};
 
 }  // namespace
 
@@ -346,7 +342,7 @@ struct sdh_engine {
   std::vector<int64_t> seg_count;
   int64_t device_matches = 0;
   bool device_unpolled = false;
-  std::vector<HostMatch> backlog;
+  std::vector<int64_t> backlog;      // host-side match records (rec_words int64 each)
   // poll output
   std::vector<int64_t> o_query, o_key, o_ts, o_off, o_words;
   sdh_stats stats{};
@@ -376,9 +372,13 @@ void ensure_state(sdh_engine* e) {
   e->cur.assign(nq, 0);
 }
 
-void collect_device_matches(sdh_engine* e) {
+void collect_device_matches(sdh_engine* e, bool discard = false) {
   if (!e->device_unpolled) return;
   e->device_unpolled = false;
+  if (discard) {
+    e->device_matches = 0;
+    return;
+  }
   const int n_items = (int)e->work.size();
   if (e->device_matches == 0 || n_items == 0) return;
   std::vector<int64_t> seg_off(n_items), dst_off(n_items);
@@ -395,20 +395,11 @@ void collect_device_matches(sdh_engine* e) {
   HIPCHK(hipMemcpyAsync(e->d_dst_off.p, dst_off.data(), n_items * 8, hipMemcpyHostToDevice, e->stream));
   HIPCHK(sdh_launch_compact(e->d_match.p, e->d_seg_off.p, e->d_seg_count.p, e->d_dst_off.p,
                             e->rec_words, n_items, e->d_dense.p, e->stream));
-  std::vector<int64_t> dense((size_t)acc * e->rec_words);
-  HIPCHK(hipMemcpyAsync(dense.data(), e->d_dense.p, dense.size() * 8, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
   const size_t base = e->backlog.size();
-  e->backlog.resize(base + acc);
-  for (int64_t i = 0; i < acc; ++i) {
-    const int64_t* r = &dense[(size_t)i * e->rec_words];
-    HostMatch& m = e->backlog[base + i];
-    m.query = r[0];
-    m.key = -1;
-    m.ts = r[1];
-    const int S = (int)e->prog.q[m.query].st.size();
-    m.seqs.assign(r + 2, r + 2 + S);
-  }
+  e->backlog.resize(base + (size_t)acc * e->rec_words);
+  HIPCHK(hipMemcpyAsync(e->backlog.data() + base, e->d_dense.p, (size_t)acc * e->rec_words * 8,
+                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
   e->device_matches = 0;
 }
 
@@ -520,8 +511,9 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     throw Error(SDH_E_INVALID, "batch larger than max_batch");
   if (b->n == 0) return SDH_OK;
   HIPCHK(hipSetDevice(e->dev));
-  // matches of the previous push that were not polled move to the host backlog
-  collect_device_matches(e);
+  // matches of the previous push that were not polled move to the host backlog (or are dropped
+  // under SDH_FLAG_DEVICE_MATCHES)
+  collect_device_matches(e, (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) != 0);
   StreamBatch B{};
   B.n = b->n;
   B.n_attr = na;
@@ -666,7 +658,7 @@ int sdh_engine_flush(sdh_engine* e) {
 
 int sdh_engine_pending_matches(sdh_engine* e, int64_t* n) {
   if (!e || !n) return SDH_E_INVALID;
-  *n = (int64_t)e->backlog.size() + (e->device_unpolled ? e->device_matches : 0);
+  *n = (int64_t)(e->backlog.size() / e->rec_words) + (e->device_unpolled ? e->device_matches : 0);
   return SDH_OK;
 }
 
@@ -674,34 +666,40 @@ int sdh_engine_poll(sdh_engine* e, sdh_matches* out) {
   if (!e || !out) return SDH_E_INVALID;
   return guard(e, [&]() {
     collect_device_matches(e);
-    auto& v = e->backlog;
+    const int RW = e->rec_words;
+    const int64_t* v = e->backlog.data();
+    const size_t n = e->backlog.size() / RW;
+    auto S_of = [&](size_t i) { return (int)e->prog.q[v[i * RW]].st.size(); };
+    auto last = [&](size_t i) { return v[i * RW + 2 + S_of(i) - 1]; };
     // reference delivery order (R18): per event, per query, per pending partial in insertion
-    // order -- for chain queries the pending list is ordered by the earlier slots' events
-    std::stable_sort(v.begin(), v.end(), [](const HostMatch& a, const HostMatch& b) {
-      if (a.seqs.back() != b.seqs.back()) return a.seqs.back() < b.seqs.back();
-      if (a.query != b.query) return a.query < b.query;
-      for (int k = (int)a.seqs.size() - 2; k >= 0; --k)
-        if (a.seqs[k] != b.seqs[k]) return a.seqs[k] < b.seqs[k];
+    // order -- for chain queries a state's pending list is ordered by the earlier slots' events
+    std::vector<size_t> idx(n);
+    for (size_t i = 0; i < n; ++i) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
+      if (last(a) != last(b)) return last(a) < last(b);
+      if (v[a * RW] != v[b * RW]) return v[a * RW] < v[b * RW];
+      for (int k = S_of(a) - 2; k >= 0; --k)
+        if (v[a * RW + 2 + k] != v[b * RW + 2 + k]) return v[a * RW + 2 + k] < v[b * RW + 2 + k];
       return false;
     });
-    const size_t n = v.size();
     e->o_query.resize(n);
     e->o_key.resize(n);
     e->o_ts.resize(n);
     e->o_off.resize(n + 1);
     e->o_words.clear();
-    for (size_t i = 0; i < n; ++i) {
-      e->o_query[i] = v[i].query;
-      e->o_key[i] = v[i].key;
-      e->o_ts[i] = v[i].ts;
-      e->o_off[i] = (int64_t)e->o_words.size();
-      for (int64_t s : v[i].seqs) {
+    for (size_t j = 0; j < n; ++j) {
+      const size_t i = idx[j];
+      e->o_query[j] = v[i * RW];
+      e->o_key[j] = -1;
+      e->o_ts[j] = v[i * RW + 1];
+      e->o_off[j] = (int64_t)e->o_words.size();
+      for (int k = 0; k < S_of(i); ++k) {
         e->o_words.push_back(1);
-        e->o_words.push_back(s);
+        e->o_words.push_back(v[i * RW + 2 + k]);
       }
     }
     e->o_off[n] = (int64_t)e->o_words.size();
-    v.clear();
+    e->backlog.clear();
     out->n = (int64_t)n;
     out->query = e->o_query.data();
     out->key = e->o_key.data();
@@ -715,12 +713,14 @@ int sdh_engine_poll(sdh_engine* e, sdh_matches* out) {
 int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
   if (!e || !out) return SDH_E_INVALID;
   return guard(e, [&]() {
-    std::vector<InstHeader> h(e->lq.size());
+    const size_t nq = e->lq.size();
+    std::vector<InstHeader> h[2];
     int64_t live = 0;
-    for (size_t q = 0; q < e->lq.size(); ++q) {
-      HIPCHK(hipMemcpy(&h[q], e->d_hdr[e->cur[q]].p + q, sizeof(InstHeader), hipMemcpyDeviceToHost));
-      live += h[q].n_live;
+    for (int b = 0; b < 2 && nq; ++b) {
+      h[b].resize(nq);
+      d2h_sync(e, h[b].data(), e->d_hdr[b].p, nq * sizeof(InstHeader));
     }
+    for (size_t q = 0; q < nq; ++q) live += h[e->cur[q]][q].n_live;
     e->stats.live_partials = live;
     *out = e->stats;
     return SDH_OK;

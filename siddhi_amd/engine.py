@@ -16,6 +16,7 @@ from .ir import T_BOOL, T_DOUBLE, T_FLOAT, T_INT, T_LONG, T_STRING
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsiddhi_hip.so")
 
 SDH_OK = 0
+SDH_FLAG_DEVICE_MATCHES = 1
 ERRORS = {-1: "SDH_E_INVALID", -2: "SDH_E_UNSUPPORTED", -3: "SDH_E_DEVICE", -4: "SDH_E_CAPACITY",
           -5: "SDH_E_REFERENCE"}
 
@@ -109,11 +110,11 @@ class HipEngine:
     """One engine instance on one GPU."""
 
     def __init__(self, blob: bytes, device: int = 0, partials: int = 128, shard_rank: int = 0,
-                 shard_world: int = 1, chunk_events: int = 0, stream_types=None):
+                 shard_world: int = 1, chunk_events: int = 0, stream_types=None, flags: int = 0):
         self.lib = load_library()
         cfg = SdhConfig(device=device, shard_rank=shard_rank, shard_world=shard_world,
                         partials_per_inst=partials, max_batch=0, match_capacity=0,
-                        chunk_events=chunk_events, flags=0)
+                        chunk_events=chunk_events, flags=flags)
         self.h = ctypes.c_void_p()
         self._blob = ctypes.create_string_buffer(blob, len(blob))
         rc = self.lib.sdh_engine_create(self._blob, len(blob), ctypes.byref(cfg), ctypes.byref(self.h))
