@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -18,8 +19,8 @@
 #include "../../include/siddhi_hip.h"
 #include "nfa_types.h"
 
-extern "C" hipError_t sdh_launch_chain(int k, const sdh::ChainLaunch* L, int n_blocks, size_t lds,
-                                       hipStream_t s);
+extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaunch* L, int n_blocks,
+                                       size_t lds, hipStream_t s);
 extern "C" hipError_t sdh_launch_compact(const int64_t* src, const int64_t* seg_off,
                                          const int64_t* seg_count, const int64_t* dst_off,
                                          int rec_words, int n_items, int64_t* dst, hipStream_t s);
@@ -414,20 +415,29 @@ void launch(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2
   // chunk planning: enough waves to fill 256 CUs, chunks >> the warm-up window
   double ev_per_ms = 1.0;
   if (n > 1) ev_per_ms = (double)n / (double)std::max<int64_t>(1, t01[1] - t01[0]);
-  const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : 8192;
-  const int64_t target_waves = 16384;
-  e->work.clear();
-  int64_t seg = 0;
-  int64_t per_query_target = std::max<int64_t>(1, target_waves / std::max<size_t>(1, qs.size()));
+  const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : 4096;
+  const double target_waves = 16384.0;
+  // every wave replays (warm-up) + emits about the same number of events, so the launch has no
+  // serial tail: wave length T >= 2x the largest warm-up and ~ total work / target_waves
+  double max_warm = 0;
   for (int li : qs) {
     const ChainQuery& c = e->lq[li].cq;
+    if (c.chunkable) max_warm = std::max(max_warm, (double)c.within * ev_per_ms + 64.0);
+  }
+  const double T = std::max({2.0 * max_warm, (double)n * qs.size() / target_waves, 2.0 * min_chunk});
+  e->work.clear();
+  int64_t seg = 0;
+  // queries grouped by state count (one kernel instantiation per group)
+  std::vector<int> order(qs);
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int a, int b) { return e->lq[a].cq.n_states < e->lq[b].cq.n_states; });
+  for (int li : order) {
+    const ChainQuery& c = e->lq[li].cq;
     int64_t C = 1;
-    if (allow_chunks && c.chunkable && n > 2 * min_chunk) {
+    if (allow_chunks && c.chunkable) {
       const double warm = (double)c.within * ev_per_ms + 64.0;
-      const int64_t by_warm = (int64_t)((double)n / std::max(8.0 * warm, (double)min_chunk));
-      C = std::max<int64_t>(1, std::min<int64_t>(by_warm, per_query_target));
-      C = std::min<int64_t>(C, n / min_chunk);
-      C = std::max<int64_t>(C, 1);
+      const double emit_len = std::max((double)min_chunk, T - warm);
+      C = std::max<int64_t>(1, (int64_t)std::ceil((double)n / emit_len));
     }
     for (int64_t ch = 0; ch < C; ++ch) {
       WorkItem w{};
@@ -465,10 +475,19 @@ void launch(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2
   L.rec_words = e->rec_words;
   L.seg_count = e->d_seg_count.p;
   L.err = e->d_err.p;
-  const int blocks = (n_items + 3) / 4;
   const size_t lds = (size_t)4 * WAVE * (B.n_attr + 2) * 8;
   HIPCHK(hipEventRecord(e->ev0, e->stream));
-  HIPCHK(sdh_launch_chain(e->K, &L, blocks, lds, e->stream));
+  for (int i0 = 0; i0 < n_items;) {
+    const int S = e->lq[e->work[i0].q].cq.n_states;
+    int i1 = i0;
+    while (i1 < n_items && e->lq[e->work[i1].q].cq.n_states == S) ++i1;
+    ChainLaunch Ls = L;
+    Ls.work = e->d_work.p + i0;
+    Ls.seg_count = e->d_seg_count.p + i0;
+    Ls.n_work = i1 - i0;
+    HIPCHK(sdh_launch_chain(S, e->K, &Ls, (Ls.n_work + 3) / 4, lds, e->stream));
+    i0 = i1;
+  }
   HIPCHK(hipEventRecord(e->ev1, e->stream));
   int32_t errs[4];
   e->seg_count.resize(n_items);

@@ -162,7 +162,7 @@ __device__ int64_t lower_bound_ts(const int64_t* ts, int64_t c0, int64_t target,
   return lo;
 }
 
-template <int K>
+template <int S, int K>
 __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -170,19 +170,25 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
   const int wid = blockIdx.x * 4 + wv;
   if (wid >= L.n_work) return;
   const WorkItem W = L.work[wid];
-  const ChainQuery& Q = L.queries[W.q];
+  const ChainQuery* __restrict__ Qp = L.queries + W.q;
+  const ChainQuery& Q = *Qp;
+  // wave-uniform program fields kept in SGPRs for the whole chunk
+  const int64_t within = Q.within;
+  const int every = Q.every, n_cap = Q.n_cap, qid = Q.qid;
+  int sstream[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) sstream[s] = Q.state_stream[s];
   const int na = L.b.n_attr;
   uint64_t* t_attr = smem + (size_t)wv * WAVE * (na + 2);
   int64_t* t_ts = (int64_t*)(t_attr + WAVE * na);
   uint32_t* t_null = (uint32_t*)(t_attr + WAVE * (na + 1));
-  const int S = Q.n_states;
   const int stream = L.b.stream;
   const int pcap = L.pcap;
 
   // ---- start state: persisted table (chunk 0 / window reaching the batch start) or replay ----
   int64_t w0 = 0;
   if (W.chunk > 0) {
-    int64_t target = L.b.ts[W.c0 - 1] - Q.within;
+    int64_t target = L.b.ts[W.c0 - 1] - within;
     w0 = lower_bound_ts(L.b.ts, W.c0, target, lane);
   }
   PSet P[K];
@@ -256,14 +262,15 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
       const int64_t cseq = L.b.seq_base + j;
 
       // ---- non-start states, last to first (reverse registration order) ----
+#pragma unroll
       for (int s = S - 1; s >= 1; --s) {
-        if (Q.state_stream[s] != stream) continue;
+        if (sstream[s] != stream) continue;
         const bool last = (s == S - 1);
 #pragma unroll
         for (int kk = 0; kk < K; ++kk) {
           const bool in_s = P[kk].st == s;
           if (__ballot(in_s) == 0) continue;
-          const bool exp = in_s && Q.within >= 0 && expired(P[kk].ts0, cts, Q.within);
+          const bool exp = in_s && within >= 0 && expired(P[kk].ts0, cts, within);
           const bool pass = in_s && !exp && eval_state(Q, s, t_attr, t_null, k, P[kk]);
           if (last) {
             const uint64_t m = __ballot(pass);
@@ -273,7 +280,7 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
                 seg_over = true;
               } else if (pass) {
                 int64_t* r = seg + rank * RW;
-                r[0] = Q.qid;
+                r[0] = qid;
                 r[1] = cts;
 #pragma unroll
                 for (int q2 = 0; q2 < MAXS - 1; ++q2)
@@ -290,7 +297,7 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
 #pragma unroll
               for (int q2 = 1; q2 < MAXS - 1; ++q2)
                 if (q2 == s) P[kk].sq[q2] = cseq;
-              for (int c = 0; c < Q.n_cap; ++c) {
+              for (int c = 0; c < n_cap; ++c) {
                 if (Q.cap_slot[c] != s) continue;
                 const int at = Q.cap_attr[c];
                 const uint64_t v = t_attr[at * WAVE + k];
@@ -306,7 +313,7 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
       }
 
       // ---- start state: the seed (every re-arms it, otherwise one match consumes it) ----
-      if (seed_alive && Q.state_stream[0] == stream) {
+      if (seed_alive && sstream[0] == stream) {
         const bool p0 = eval_state(Q, 0, t_attr, t_null, k, P[0]);
         if (__ballot(p0) != 0) {  // uniform: the seed sees only the current event
           if (S == 1) {
@@ -315,7 +322,7 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
                 seg_over = true;
               } else if (lane == 0) {
                 int64_t* r = seg + nmatch * RW;
-                r[0] = Q.qid;
+                r[0] = qid;
                 r[1] = cts;
                 r[2] = cseq;
               }
@@ -335,7 +342,7 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
                 P[kk].ts0 = cts;
                 P[kk].sq[0] = cseq;
                 P[kk].cn = 0;
-                for (int c = 0; c < Q.n_cap; ++c) {
+                for (int c = 0; c < n_cap; ++c) {
                   if (Q.cap_slot[c] != 0) continue;
                   const int at = Q.cap_attr[c];
                   const uint64_t v = t_attr[at * WAVE + k];
@@ -349,7 +356,7 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
             }
             if (!placed) overflow = true;
           }
-          if (!Q.every) seed_alive = 0;
+          if (!every) seed_alive = 0;
         }
       }
     }
@@ -403,24 +410,32 @@ __global__ void compact_matches_kernel(const int64_t* __restrict__ src, const in
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) d[i] = s[i];
 }
 
-template __global__ void nfa_chain_kernel<1>(ChainLaunch);
-template __global__ void nfa_chain_kernel<2>(ChainLaunch);
-template __global__ void nfa_chain_kernel<4>(ChainLaunch);
-template __global__ void nfa_chain_kernel<8>(ChainLaunch);
-
 }  // namespace sdh
 
 // host-side launchers (C linkage inside the library)
-extern "C" hipError_t sdh_launch_chain(int k, const sdh::ChainLaunch* L, int n_blocks, size_t lds,
-                                       hipStream_t s) {
+template <int S>
+static hipError_t launch_s(int k, const sdh::ChainLaunch* L, int n_blocks, size_t lds, hipStream_t s) {
   switch (k) {
-    case 1: hipLaunchKernelGGL(sdh::nfa_chain_kernel<1>, dim3(n_blocks), dim3(256), lds, s, *L); break;
-    case 2: hipLaunchKernelGGL(sdh::nfa_chain_kernel<2>, dim3(n_blocks), dim3(256), lds, s, *L); break;
-    case 4: hipLaunchKernelGGL(sdh::nfa_chain_kernel<4>, dim3(n_blocks), dim3(256), lds, s, *L); break;
-    case 8: hipLaunchKernelGGL(sdh::nfa_chain_kernel<8>, dim3(n_blocks), dim3(256), lds, s, *L); break;
+    case 1: hipLaunchKernelGGL((sdh::nfa_chain_kernel<S, 1>), dim3(n_blocks), dim3(256), lds, s, *L); break;
+    case 2: hipLaunchKernelGGL((sdh::nfa_chain_kernel<S, 2>), dim3(n_blocks), dim3(256), lds, s, *L); break;
+    case 4: hipLaunchKernelGGL((sdh::nfa_chain_kernel<S, 4>), dim3(n_blocks), dim3(256), lds, s, *L); break;
+    case 8: hipLaunchKernelGGL((sdh::nfa_chain_kernel<S, 8>), dim3(n_blocks), dim3(256), lds, s, *L); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// host-side launchers (C linkage inside the library)
+extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaunch* L, int n_blocks,
+                                       size_t lds, hipStream_t s) {
+  if (n_blocks <= 0) return hipSuccess;
+  switch (n_states) {
+    case 1: return launch_s<1>(k, L, n_blocks, lds, s);
+    case 2: return launch_s<2>(k, L, n_blocks, lds, s);
+    case 3: return launch_s<3>(k, L, n_blocks, lds, s);
+    case 4: return launch_s<4>(k, L, n_blocks, lds, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 extern "C" hipError_t sdh_launch_compact(const int64_t* src, const int64_t* seg_off, const int64_t* seg_count,
