@@ -163,6 +163,45 @@ int domain_of(int lt, int rt, int op) {
   return D_I32;
 }
 
+// conversion of an operand of attribute type t into the key of domain d (enum Conv)
+int conv_of(int t, int d) {
+  switch (d) {
+    case D_I32:
+    case D_I64: return t == T_INT ? CV_I64_INT : CV_I64_LONG;
+    case D_F32: return t == T_INT ? CV_F32_INT : t == T_LONG ? CV_F32_LONG : CV_F32_FLOAT;
+    case D_F64:
+      return t == T_INT ? CV_F64_INT : t == T_LONG ? CV_F64_LONG : t == T_FLOAT ? CV_F64_FLOAT : CV_F64_DOUBLE;
+    default: return CV_RAW;
+  }
+}
+
+int64_t host_key(int64_t raw, int conv) {  // host twin of to_key() in nfa_chain.hip
+  auto dbits = [](double d) { int64_t b; memcpy(&b, &d, 8); return b; };
+  auto f_of = [](int64_t r) { uint32_t u = (uint32_t)r; float f; memcpy(&f, &u, 4); return f; };
+  switch (conv) {
+    case CV_I64_INT: return (int64_t)(int32_t)(uint32_t)raw;
+    case CV_I64_LONG: return raw;
+    case CV_F32_INT: return dbits((double)(float)(int32_t)(uint32_t)raw);
+    case CV_F32_LONG: return dbits((double)(float)raw);
+    case CV_F32_FLOAT:
+    case CV_F64_FLOAT: return dbits((double)f_of(raw));
+    case CV_F64_INT: return dbits((double)(int32_t)(uint32_t)raw);
+    case CV_F64_LONG: return dbits((double)raw);
+    default: return raw;
+  }
+}
+
+int mask_of(int op) {
+  switch (op) {
+    case CMP_EQ: return CM_EQ;
+    case CMP_NE: return CM_EQ | CM_NOT;
+    case CMP_GT: return CM_GT;
+    case CMP_GE: return CM_GT | CM_EQ;
+    case CMP_LT: return CM_LT;
+    default: return CM_LT | CM_EQ;
+  }
+}
+
 struct Node {
   int kind;  // 0 leaf operand, 1 cmp, 2 and, 3 other
   Insn ins;
@@ -203,7 +242,6 @@ Lowered lower_query(const IProgram& P, int qi) {
       L.streams.push_back(st.stream);
   }
   c.every = q.st[0].next_every == 0;
-  c.n_attr = (int)P.stream_types[q.st[0].stream].size();
   for (int s = 0; s < n; ++s)
     if ((int)P.stream_types[q.st[s].stream].size() > MAXATTR) return fail("too many attributes");
   // a single input stream and `every` make event-chunk warm-up exact
@@ -243,42 +281,58 @@ Lowered lower_query(const IProgram& P, int qi) {
       for (int x : leaves) {
         if (na >= MAXATOM) return fail("too many predicate atoms");
         Atom& A = c.atoms[na];
-        auto operand = [&](const Insn& in, int& k, int& idx, int& t, int64_t& cst) -> bool {
-          t = in.res;
-          if (in.op == OP_CONST) { k = OPK_CONST; cst = in.imm; idx = 0; return true; }
-          // ATTR: slot in.a, chain index in.b, attribute in.imm. Single-event slots: only
-          // CURRENT (-1) and 0 resolve to the event; other indices read null (StateEvent:138-182).
-          if (in.b != -1 && in.b != 0) { k = OPK_NULL; idx = 0; return true; }
-          if (in.a == s) { k = OPK_CUR; idx = (int)in.imm; return true; }
+        const Node& nd = nodes[x];
+        Insn li, ri;
+        int op;
+        if (nd.kind == 1) {
+          if (nodes[nd.l].kind != 0 || nodes[nd.r].kind != 0)
+            return fail("compare of computed values (general predicate kernel pending)");
+          li = nodes[nd.l].ins;
+          ri = nodes[nd.r].ins;
+          op = (int)nd.ins.imm;
+        } else if (nd.kind == 0 && nd.ins.res == T_BOOL) {
+          // bare bool operand as a filter: FilterProcessor drops null and false
+          li = nd.ins;
+          ri = Insn{OP_CONST, 0, 0, T_BOOL, 0, 0, 1};
+          op = CMP_EQ;
+        } else {
+          return fail("unsupported filter form");
+        }
+        const int dom = domain_of(li.res, ri.res, op);
+        A.mask = mask_of(op);
+        A.f64 = (dom == D_F32 || dom == D_F64) ? 1 : 0;
+        // operand -> (kind, index, const key); single-event slots resolve only chain index
+        // CURRENT (-1) and 0 (StateEvent.getStreamEvent:138-182), others read null
+        auto operand = [&](const Insn& in, int& k, int& idx, int64_t& cst) -> bool {
+          const int cv = conv_of(in.res, dom);
+          idx = 0;
+          cst = 0;
+          if (in.op == OP_CONST) { k = OPK_CONST; cst = host_key(in.imm, cv); return true; }
+          if (in.b != -1 && in.b != 0) { k = OPK_NULL; return true; }
           if (in.a > s) return false;
+          const int st_stream = q.st[in.a].stream;
+          int col = -1;
+          for (int cc = 0; cc < c.n_col; ++cc)
+            if (c.col_attr[cc] == in.imm && c.col_conv[cc] == cv && c.col_stream[cc] == st_stream) col = cc;
+          if (col < 0) {
+            if (c.n_col >= MAXCOL) return false;
+            col = c.n_col++;
+            c.col_attr[col] = (int)in.imm;
+            c.col_conv[col] = cv;
+            c.col_stream[col] = st_stream;
+          }
+          if (in.a == s) { k = OPK_CUR; idx = col; return true; }
           for (int cc = 0; cc < c.n_cap; ++cc)
-            if (c.cap_slot[cc] == in.a && c.cap_attr[cc] == in.imm) { k = OPK_CAP; idx = cc; return true; }
+            if (c.cap_slot[cc] == in.a && c.cap_col[cc] == col) { k = OPK_CAP; idx = cc; return true; }
           if (c.n_cap >= MAXCAP) return false;
           c.cap_slot[c.n_cap] = (int)in.a;
-          c.cap_attr[c.n_cap] = (int)in.imm;
+          c.cap_col[c.n_cap] = col;
           k = OPK_CAP;
           idx = c.n_cap++;
           return true;
         };
-        const Node& nd = nodes[x];
-        if (nd.kind == 1) {
-          const Insn& li = nodes[nd.l].ins;
-          const Insn& ri = nodes[nd.r].ins;
-          if (nodes[nd.l].kind != 0 || nodes[nd.r].kind != 0)
-            return fail("compare of computed values (general predicate kernel pending)");
-          A.op = (int)nd.ins.imm;
-          if (!operand(li, A.lk, A.la, A.lt, A.lc) || !operand(ri, A.rk, A.ra, A.rt, A.rc))
-            return fail("operand not addressable");
-          A.dom = domain_of(A.lt, A.rt, A.op);
-        } else if (nd.kind == 0 && nd.ins.res == T_BOOL) {
-          // bare bool operand as a filter: FilterProcessor drops null and false
-          A.op = CMP_EQ;
-          if (!operand(nd.ins, A.lk, A.la, A.lt, A.lc)) return fail("operand not addressable");
-          A.rk = OPK_CONST; A.ra = 0; A.rt = T_BOOL; A.rc = 1;
-          A.dom = D_RAW;
-        } else {
-          return fail("unsupported filter form");
-        }
+        if (!operand(li, A.lk, A.li, A.lc) || !operand(ri, A.rk, A.ri, A.rc))
+          return fail("operand not addressable (too many columns / captures)");
         ++na;
       }
     }
@@ -475,7 +529,7 @@ void launch(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2
   L.rec_words = e->rec_words;
   L.seg_count = e->d_seg_count.p;
   L.err = e->d_err.p;
-  const size_t lds = (size_t)4 * WAVE * (B.n_attr + 2) * 8;
+  const size_t lds = (size_t)4 * WAVE * (MAXCOL + 2) * 8;
   HIPCHK(hipEventRecord(e->ev0, e->stream));
   for (int i0 = 0; i0 < n_items;) {
     const int S = e->lq[e->work[i0].q].cq.n_states;

@@ -13,13 +13,16 @@
 //   * start state with `every` keeps its (stateless) seed forever (StreamPostStateProcessor:66-68
 //     re-arms a shallow clone); without `every` the seed is consumed by its first match (R3)
 //   * the last state emits (isEventReturned, :310-313) and drops the partial (stateChanged)
+//   * predicates: conjunctions of typed compares, null -> false (FilterProcessor:55-66,
+//     CompareConditionExpressionExecutor:39-43), evaluated in Java's promotion domain
 //
 // Mapping to CDNA4: one 64-lane wave owns one (query instance, event chunk); each lane holds one
-// partial match in registers (K register sets -> 64*K partials). The event stream is staged per
-// wave in LDS tiles of 64 events (one coalesced load per attribute column, then wave-uniform
-// broadcast reads); new partials take the first free lane (s_ff1 on the ballot of live lanes);
-// matches are compacted with ballot + mbcnt into the wave's contiguous output segment. No MFMA:
-// the step is compare/branch work.
+// partial match in registers (K register sets -> 64*K partials). Every 64 events the wave stages
+// a tile in its private LDS region: one coalesced load per attribute column, converted once per
+// event into compare-domain keys (f64 or i64), so the per-event predicate is a branch-free pair of
+// compares read by wave-uniform (broadcast) LDS loads. New partials take the first free lane
+// (ctz of the inverted live-lane ballot); matches are compacted with ballot + mbcnt into the
+// wave's contiguous output segment. No MFMA: the step is compare/branch work.
 //
 // Exactness of event-chunk parallelism: for chunkable queries (every on the start
 // state, within T, one input stream) chunk c > 0 re-derives its start state by replaying the
@@ -36,48 +39,43 @@ __device__ __forceinline__ int wave_mbcnt(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-template <class T>
-__device__ __forceinline__ bool cmpv(int op, T a, T b) {
-  switch (op) {
-    case CMP_EQ: return a == b;
-    case CMP_NE: return a != b;
-    case CMP_GT: return a > b;
-    case CMP_GE: return a >= b;
-    case CMP_LT: return a < b;
-    default: return a <= b;
+__device__ __forceinline__ int64_t rfl64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Number.floatValue()/doubleValue()/longValue() into the compare domain (see enum Conv)
+__device__ __forceinline__ int64_t to_key(uint64_t raw, int conv) {
+  switch (conv) {
+    case CV_I64_INT: return (int64_t)(int32_t)(uint32_t)raw;
+    case CV_I64_LONG: return (int64_t)raw;
+    case CV_F32_INT: return __double_as_longlong((double)(float)(int32_t)(uint32_t)raw);
+    case CV_F32_LONG: return __double_as_longlong((double)(float)(int64_t)raw);
+    case CV_F32_FLOAT:
+    case CV_F64_FLOAT: return __double_as_longlong((double)__uint_as_float((uint32_t)raw));
+    case CV_F64_INT: return __double_as_longlong((double)(int32_t)(uint32_t)raw);
+    case CV_F64_LONG: return __double_as_longlong((double)(int64_t)raw);
+    default: return (int64_t)raw;  // CV_F64_DOUBLE, CV_RAW
   }
 }
 
-// Number.floatValue()/doubleValue()/longValue() of a raw attribute word
-__device__ __forceinline__ float to_f32(uint64_t raw, int t) {
-  switch (t) {
-    case T_INT: return (float)(int32_t)(uint32_t)raw;
-    case T_LONG: return (float)(int64_t)raw;
-    case T_FLOAT: return __uint_as_float((uint32_t)raw);
-    default: return (float)__longlong_as_double((long long)raw);
+// typed compare of two keys: ((lt & b0) | (gt & b1) | (eq & b2)) ^ b3 -- IEEE semantics for f64
+// keys (NaN: only != holds), exactly Java's primitive compares
+__device__ __forceinline__ bool cmp_keys(int mask, int f64, int64_t l, int64_t r) {
+  bool lt, gt, eq;
+  if (f64) {
+    const double a = __longlong_as_double(l), b = __longlong_as_double(r);
+    lt = a < b;
+    gt = b < a;
+    eq = a == b;
+  } else {
+    lt = l < r;
+    gt = r < l;
+    eq = l == r;
   }
-}
-__device__ __forceinline__ double to_f64(uint64_t raw, int t) {
-  switch (t) {
-    case T_INT: return (double)(int32_t)(uint32_t)raw;
-    case T_LONG: return (double)(int64_t)raw;
-    case T_FLOAT: return (double)__uint_as_float((uint32_t)raw);
-    default: return __longlong_as_double((long long)raw);
-  }
-}
-__device__ __forceinline__ int64_t to_i64(uint64_t raw, int t) {
-  return t == T_INT ? (int64_t)(int32_t)(uint32_t)raw : (int64_t)raw;
-}
-
-// CompareConditionExpressionExecutor.execute:39-43 + the typed execute() of compare/**
-__device__ __forceinline__ bool atom_cmp(const Atom& A, uint64_t l, uint64_t r) {
-  switch (A.dom) {
-    case D_F32: return cmpv(A.op, to_f32(l, A.lt), to_f32(r, A.rt));
-    case D_F64: return cmpv(A.op, to_f64(l, A.lt), to_f64(r, A.rt));
-    case D_I64: return cmpv(A.op, to_i64(l, A.lt), to_i64(r, A.rt));
-    case D_I32: return cmpv(A.op, (int32_t)(uint32_t)l, (int32_t)(uint32_t)r);
-    default: return cmpv(A.op, l, r);  // BOOL / STRING (dictionary id) equality
-  }
+  const bool v = (lt && (mask & CM_LT)) || (gt && (mask & CM_GT)) || (eq && (mask & CM_EQ));
+  return v != ((mask & CM_NOT) != 0);
 }
 
 // Math.abs(a - b) > within with Java long wrap-around (Math.abs(Long.MIN_VALUE) < 0)
@@ -92,71 +90,65 @@ struct PSet {
   int st;                  // state id the partial is pending at, -1 = free lane
   int64_t ts0;             // timestamp of the start-state event (within reference)
   int64_t sq[MAXS - 1];    // event sequence number per filled slot
-  uint64_t cp[MAXCAP];     // captured raw attribute words read by later filters
+  int64_t cp[MAXCAP];      // captured operand keys read by later filters
   uint32_t cn;             // captured-null bits
 };
 
-__device__ __forceinline__ uint64_t cap_get(const PSet P, int idx) {
-  uint64_t v = P.cp[0];
+__device__ __forceinline__ int64_t cap_get(const PSet P, int idx) {
+  int64_t v = P.cp[0];
 #pragma unroll
   for (int c = 1; c < MAXCAP; ++c) v = (idx == c) ? P.cp[c] : v;
   return v;
 }
 
-// operand fetch; `k` indexes the event inside the wave's LDS tile
-__device__ __forceinline__ uint64_t fetch(int kind, int idx, int64_t c, const uint64_t* t_attr,
-                                          const uint32_t* t_null, int k, const PSet P, bool& nul) {
-  switch (kind) {
-    case OPK_CUR:
-      nul = (t_null[k] >> idx) & 1u;
-      return t_attr[idx * WAVE + k];
-    case OPK_CAP:
-      nul = (P.cn >> idx) & 1u;
-      return cap_get(P, idx);
-    case OPK_CONST:
-      nul = false;
-      return (uint64_t)c;
-    default:
-      nul = true;
-      return 0;
+// LDS tile of one wave: [n_col][64] keys, [64] ts, [64] null bits (per column)
+struct Tile {
+  const int64_t* key;
+  const int64_t* ts;
+  const uint32_t* nul;
+};
+
+__device__ __forceinline__ int64_t operand(int kind, int idx, int64_t c, const Tile T, int k,
+                                           const PSet P, bool& nul) {
+  if (kind == OPK_CUR) {
+    nul = (T.nul[k] >> idx) & 1u;
+    return T.key[idx * WAVE + k];
   }
+  if (kind == OPK_CAP) {
+    nul = (P.cn >> idx) & 1u;
+    return cap_get(P, idx);
+  }
+  nul = kind != OPK_CONST;
+  return c;
 }
 
 // conjunction of the atoms of state s (FilterProcessor chain, null -> false)
-__device__ __forceinline__ bool eval_state(const ChainQuery& Q, int s, const uint64_t* t_attr,
-                                           const uint32_t* t_null, int k, const PSet P) {
+__device__ __forceinline__ bool eval_state(const ChainQuery* __restrict__ Q, int a0, int a1,
+                                           const Tile T, int k, const PSet P) {
   bool ok = true;
-  const int a0 = Q.atom_begin[s], a1 = Q.atom_begin[s + 1];
   for (int a = a0; a < a1; ++a) {
-    const Atom& A = Q.atoms[a];
+    const Atom& A = Q->atoms[a];
     bool ln, rn;
-    uint64_t l = fetch(A.lk, A.la, A.lc, t_attr, t_null, k, P, ln);
-    uint64_t r = fetch(A.rk, A.ra, A.rc, t_attr, t_null, k, P, rn);
-    ok = ok && !ln && !rn && atom_cmp(A, l, r);
+    const int64_t l = operand(A.lk, A.li, A.lc, T, k, P, ln);
+    const int64_t r = operand(A.rk, A.ri, A.rc, T, k, P, rn);
+    ok = ok && !ln && !rn && cmp_keys(A.mask, A.f64, l, r);
   }
   return ok;
-}
-
-__device__ __forceinline__ int64_t rfl64(int64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 // first index i in [0, c0) with ts[i] >= target (64-ary search, all lanes cooperate)
 __device__ int64_t lower_bound_ts(const int64_t* ts, int64_t c0, int64_t target, int lane) {
   int64_t lo = 0, hi = c0;  // answer in [lo, hi]
   while (hi - lo > 1) {
-    int64_t span = hi - lo;
-    int64_t p = lo + (span * lane) / WAVE;   // probe positions, p < hi
-    bool below = ts[p] < target;
-    uint64_t m = __ballot(below);
-    int nb = __popcll(m);                    // ts is sorted: the first nb probes are below
-    int64_t nlo = nb == 0 ? lo : lo + (span * (nb - 1)) / WAVE + 1;
-    int64_t nhi = nb == WAVE ? hi : lo + (span * nb) / WAVE;
+    const int64_t span = hi - lo;
+    const int64_t p = lo + (span * lane) / WAVE;  // probe positions, p < hi
+    const uint64_t m = __ballot(ts[p] < target);
+    const int nb = __popcll(m);                   // ts is sorted: the first nb probes are below
+    const int64_t nlo = nb == 0 ? lo : lo + (span * (nb - 1)) / WAVE + 1;
+    const int64_t nhi = nb == WAVE ? hi : lo + (span * nb) / WAVE;
     lo = rfl64(nlo);
     hi = rfl64(nhi);
-    if (nlo == nhi) break;
+    if (lo == hi) break;
   }
   if (lo < c0 && ts[lo] < target) lo = lo + 1;
   return lo;
@@ -164,37 +156,36 @@ __device__ int64_t lower_bound_ts(const int64_t* ts, int64_t c0, int64_t target,
 
 template <int S, int K>
 __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  extern __shared__ __attribute__((aligned(16))) int64_t smem[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + wv;
   if (wid >= L.n_work) return;
   const WorkItem W = L.work[wid];
-  const ChainQuery* __restrict__ Qp = L.queries + W.q;
-  const ChainQuery& Q = *Qp;
-  // wave-uniform program fields kept in SGPRs for the whole chunk
-  const int64_t within = Q.within;
-  const int every = Q.every, n_cap = Q.n_cap, qid = Q.qid;
-  int sstream[S];
+  const ChainQuery* __restrict__ Q = L.queries + W.q;
+  // wave-uniform program fields, kept in SGPRs for the whole chunk
+  const int64_t within = Q->within;
+  const int every = Q->every, n_cap = Q->n_cap, qid = Q->qid, n_col = Q->n_col;
+  int sstream[S], abeg[S + 1];
 #pragma unroll
-  for (int s = 0; s < S; ++s) sstream[s] = Q.state_stream[s];
-  const int na = L.b.n_attr;
-  uint64_t* t_attr = smem + (size_t)wv * WAVE * (na + 2);
-  int64_t* t_ts = (int64_t*)(t_attr + WAVE * na);
-  uint32_t* t_null = (uint32_t*)(t_attr + WAVE * (na + 1));
+  for (int s = 0; s < S; ++s) sstream[s] = Q->state_stream[s];
+#pragma unroll
+  for (int s = 0; s <= S; ++s) abeg[s] = Q->atom_begin[s];
   const int stream = L.b.stream;
   const int pcap = L.pcap;
 
+  int64_t* t_key = smem + (size_t)wv * WAVE * (MAXCOL + 2);
+  int64_t* t_ts = t_key + WAVE * MAXCOL;
+  uint32_t* t_nul = (uint32_t*)(t_ts + WAVE);
+  const Tile T{t_key, t_ts, t_nul};
+
   // ---- start state: persisted table (chunk 0 / window reaching the batch start) or replay ----
   int64_t w0 = 0;
-  if (W.chunk > 0) {
-    int64_t target = L.b.ts[W.c0 - 1] - within;
-    w0 = lower_bound_ts(L.b.ts, W.c0, target, lane);
-  }
+  if (W.chunk > 0) w0 = lower_bound_ts(L.b.ts, W.c0, L.b.ts[W.c0 - 1] - within, lane);
   PSet P[K];
   int seed_alive = 1;
-  const int64_t* pin = L.part[W.inb] + (size_t)W.q * NF * pcap;
   if (w0 == 0) {
+    const int64_t* pin = L.part[W.inb] + (size_t)W.q * NF * pcap;
     seed_alive = L.hdr[W.inb][W.q].seed_alive;
 #pragma unroll
     for (int kk = 0; kk < K; ++kk) {
@@ -204,7 +195,7 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
 #pragma unroll
       for (int s = 0; s < MAXS - 1; ++s) P[kk].sq[s] = pin[(F_SEQ0 + s) * pcap + li];
 #pragma unroll
-      for (int c = 0; c < MAXCAP; ++c) P[kk].cp[c] = (uint64_t)pin[(F_CAP0 + c) * pcap + li];
+      for (int c = 0; c < MAXCAP; ++c) P[kk].cp[c] = pin[(F_CAP0 + c) * pcap + li];
       P[kk].cn = (uint32_t)pin[F_CAPNULL * pcap + li];
     }
   } else {
@@ -227,24 +218,26 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
   int64_t prev_tile_ts = (w0 == 0) ? L.b.prev_ts : L.b.ts[w0 - 1];
 
   for (int64_t t = w0; t < W.c1; t += WAVE) {
-    // ---- stage 64 events of the stream in this wave's LDS tile (coalesced column loads) ----
+    // ---- stage 64 events: coalesced column loads, converted once into compare-domain keys ----
     const int64_t e = t + lane;
     const bool live = e < W.c1;
-    int64_t ets = live ? L.b.ts[e] : INT64_MAX;
+    const int64_t ets = live ? L.b.ts[e] : INT64_MAX;
     uint32_t enull = 0;
-    for (int a = 0; a < na; ++a) {
-      uint64_t v = 0;
+    for (int c = 0; c < n_col; ++c) {
+      if (Q->col_stream[c] != stream) continue;  // columns of states fed by other streams
+      const int a = Q->col_attr[c];
+      uint64_t raw = 0;
       if (live) {
         const int wdt = L.b.width[a];
-        if (wdt == 8) v = ((const uint64_t*)L.b.col[a])[e];
-        else if (wdt == 4) v = ((const uint32_t*)L.b.col[a])[e];
-        else v = ((const uint8_t*)L.b.col[a])[e];
-        if (L.b.nul[a] && ((const uint8_t*)L.b.nul[a])[e]) enull |= 1u << a;
+        if (wdt == 8) raw = ((const uint64_t*)L.b.col[a])[e];
+        else if (wdt == 4) raw = ((const uint32_t*)L.b.col[a])[e];
+        else raw = ((const uint8_t*)L.b.col[a])[e];
+        if (L.b.nul[a] && ((const uint8_t*)L.b.nul[a])[e]) enull |= 1u << c;
       }
-      t_attr[a * WAVE + lane] = v;
+      t_key[c * WAVE + lane] = to_key(raw, Q->col_conv[c]);
     }
     t_ts[lane] = ets;
-    t_null[lane] = enull;
+    t_nul[lane] = enull;
     // timestamps must be non-decreasing for chunk warm-up to be exact
     int64_t pred = __shfl_up(ets, 1, WAVE);
     if (lane == 0) pred = prev_tile_ts;
@@ -271,7 +264,7 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
           const bool in_s = P[kk].st == s;
           if (__ballot(in_s) == 0) continue;
           const bool exp = in_s && within >= 0 && expired(P[kk].ts0, cts, within);
-          const bool pass = in_s && !exp && eval_state(Q, s, t_attr, t_null, k, P[kk]);
+          const bool pass = in_s && !exp && eval_state(Q, abeg[s], abeg[s + 1], T, k, P[kk]);
           if (last) {
             const uint64_t m = __ballot(pass);
             if (m && emit_ok) {
@@ -283,8 +276,7 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
                 r[0] = qid;
                 r[1] = cts;
 #pragma unroll
-                for (int q2 = 0; q2 < MAXS - 1; ++q2)
-                  if (q2 < S - 1) r[2 + q2] = P[kk].sq[q2];
+                for (int q2 = 0; q2 < S - 1; ++q2) r[2 + q2] = P[kk].sq[q2];
                 r[2 + S - 1] = cseq;
               }
               nmatch += __popcll(m);
@@ -298,10 +290,10 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
               for (int q2 = 1; q2 < MAXS - 1; ++q2)
                 if (q2 == s) P[kk].sq[q2] = cseq;
               for (int c = 0; c < n_cap; ++c) {
-                if (Q.cap_slot[c] != s) continue;
-                const int at = Q.cap_attr[c];
-                const uint64_t v = t_attr[at * WAVE + k];
-                const uint32_t nb = (t_null[k] >> at) & 1u;
+                if (Q->cap_slot[c] != s) continue;
+                const int col = Q->cap_col[c];
+                const int64_t v = t_key[col * WAVE + k];
+                const uint32_t nb = (t_nul[k] >> col) & 1u;
 #pragma unroll
                 for (int c2 = 0; c2 < MAXCAP; ++c2)
                   if (c2 == c) P[kk].cp[c2] = v;
@@ -314,8 +306,8 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
 
       // ---- start state: the seed (every re-arms it, otherwise one match consumes it) ----
       if (seed_alive && sstream[0] == stream) {
-        const bool p0 = eval_state(Q, 0, t_attr, t_null, k, P[0]);
-        if (__ballot(p0) != 0) {  // uniform: the seed sees only the current event
+        const bool p0 = eval_state(Q, abeg[0], abeg[1], T, k, P[0]);
+        if (__ballot(p0) != 0) {  // uniform: the seed only reads the current event
           if (S == 1) {
             if (emit_ok) {
               if (nmatch + 1 > W.seg_cap) {
@@ -336,21 +328,19 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
               const uint64_t freem = ~__ballot(P[kk].st >= 0);
               if (freem == 0) continue;
               placed = true;
-              const int fl = __builtin_ctzll(freem);
-              if (lane == fl) {
+              if (lane == __builtin_ctzll(freem)) {
                 P[kk].st = 1;
                 P[kk].ts0 = cts;
                 P[kk].sq[0] = cseq;
                 P[kk].cn = 0;
                 for (int c = 0; c < n_cap; ++c) {
-                  if (Q.cap_slot[c] != 0) continue;
-                  const int at = Q.cap_attr[c];
-                  const uint64_t v = t_attr[at * WAVE + k];
-                  const uint32_t nb = (t_null[k] >> at) & 1u;
+                  if (Q->cap_slot[c] != 0) continue;
+                  const int col = Q->cap_col[c];
+                  const int64_t v = t_key[col * WAVE + k];
 #pragma unroll
                   for (int c2 = 0; c2 < MAXCAP; ++c2)
                     if (c2 == c) P[kk].cp[c2] = v;
-                  P[kk].cn |= nb << c;
+                  P[kk].cn |= ((t_nul[k] >> col) & 1u) << c;
                 }
               }
             }
@@ -382,7 +372,7 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
 #pragma unroll
       for (int s = 0; s < MAXS - 1; ++s) pout[(F_SEQ0 + s) * pcap + li] = P[kk].sq[s];
 #pragma unroll
-      for (int c = 0; c < MAXCAP; ++c) pout[(F_CAP0 + c) * pcap + li] = (int64_t)P[kk].cp[c];
+      for (int c = 0; c < MAXCAP; ++c) pout[(F_CAP0 + c) * pcap + li] = P[kk].cp[c];
       pout[F_CAPNULL * pcap + li] = P[kk].cn;
       nlive += __popcll(__ballot(P[kk].st >= 0));
     }
@@ -412,7 +402,6 @@ __global__ void compact_matches_kernel(const int64_t* __restrict__ src, const in
 
 }  // namespace sdh
 
-// host-side launchers (C linkage inside the library)
 template <int S>
 static hipError_t launch_s(int k, const sdh::ChainLaunch* L, int n_blocks, size_t lds, hipStream_t s) {
   switch (k) {

@@ -11,8 +11,9 @@
 namespace sdh {
 
 constexpr int MAXS = 4;      // states per chain query
-constexpr int MAXCAP = 4;    // captured attribute values per partial match
+constexpr int MAXCAP = 4;    // captured operand keys per partial match
 constexpr int MAXATOM = 12;  // compare atoms per query (all states)
+constexpr int MAXCOL = 8;    // pre-keyed operand columns of the current event
 constexpr int MAXATTR = 16;  // attributes per stream
 constexpr int WAVE = 64;
 
@@ -23,11 +24,32 @@ enum Domain { D_I32 = 0, D_I64, D_F32, D_F64, D_RAW };
 enum OpKind { OPK_CUR = 0, OPK_CAP, OPK_CONST, OPK_NULL };
 enum CmpOp { CMP_EQ = 0, CMP_NE, CMP_GT, CMP_GE, CMP_LT, CMP_LE };
 
+// Key conversions: an attribute value is converted ONCE (per event, when its tile is staged, or
+// per capture) into the key of its compare domain, so that every compare is a plain f64 or i64
+// compare. F32-domain values are rounded to binary32 first and then widened exactly, so comparing
+// the f64 keys gives Java's float compare bit-for-bit (NaN included).
+enum Conv {
+  CV_I64_INT = 0,   // (long) int
+  CV_I64_LONG,      // long
+  CV_F32_INT,       // (double)(float) int
+  CV_F32_LONG,      // (double)(float) long
+  CV_F32_FLOAT,     // (double) float
+  CV_F64_INT,       // (double) int
+  CV_F64_LONG,      // (double) long
+  CV_F64_FLOAT,     // (double) float
+  CV_F64_DOUBLE,    // double
+  CV_RAW,           // bool / string id
+};
+
+// compare result = ((lt & b0) | (gt & b1) | (eq & b2)) ^ b3
+enum CmpMask { CM_LT = 1, CM_GT = 2, CM_EQ = 4, CM_NOT = 8 };
+
 struct Atom {
-  int32_t op, dom;
-  int32_t lk, la, lt;  // lhs kind, attr index (CUR) / capture index (CAP), attribute type
-  int32_t rk, ra, rt;
-  int64_t lc, rc;      // raw constant words (CONST)
+  int32_t mask;         // CmpMask bits
+  int32_t f64;          // 1: compare keys as double, 0: as int64
+  int32_t lk, li;       // lhs kind, column (CUR) / capture (CAP) index
+  int32_t rk, ri;
+  int64_t lc, rc;       // constant keys (CONST)
 };
 
 struct ChainQuery {
@@ -37,10 +59,11 @@ struct ChainQuery {
   int32_t n_cap;
   int64_t within;       // ms, -1 = no within
   int32_t chunkable;    // planner proof that warm-up chunking is exact
-  int32_t n_attr;       // attributes of the (first) stream
+  int32_t n_col;        // pre-keyed operand columns
+  int32_t col_attr[MAXCOL], col_conv[MAXCOL], col_stream[MAXCOL];
   int32_t state_stream[MAXS];
   int32_t atom_begin[MAXS + 1];
-  int32_t cap_slot[MAXCAP], cap_attr[MAXCAP];
+  int32_t cap_slot[MAXCAP], cap_col[MAXCAP];
   Atom atoms[MAXATOM];
 };
 

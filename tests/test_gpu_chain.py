@@ -114,3 +114,89 @@ def test_snapshot_restore_roundtrip():
     b.engine.restore(snap)
     b.engine.push_columns(0, ts2, cols2)
     assert b.engine.take_matches(lambda q: 2) == ref
+
+
+TYPED_STREAM = "define stream T (i int, l long, f float, d double, b bool, s string);"
+NUMERIC = ["i", "l", "f", "d"]
+OPS = ["==", "!=", ">", ">=", "<", "<="]
+
+
+def typed_events(n=400, seed=3):
+    """Adversarial values for Java's typed compares: int->float and long->float/double rounding
+    boundaries, signed zeros, NaN, infinities, extremes; some nulls."""
+    rng = np.random.default_rng(seed)
+    ints = [0, 1, -1, 16777216, 16777217, -16777217, 2**31 - 1, -2**31, 123456789, 7]
+    longs = [0, 1, -1, 16777217, 2**53, 2**53 + 1, 2**62 + 1, -2**63, 2**63 - 1, 9007199254740993, 7]
+    floats = [0.0, -0.0, 1.0, 16777216.0, 16777218.0, float("nan"), float("inf"), -float("inf"),
+              3.4028235e38, 1e-45, 7.0, 0.1]
+    doubles = [0.0, -0.0, 1.0, 16777217.0, 9007199254740992.0, 9007199254740994.0, float("nan"),
+               float("inf"), 0.1, 7.0, 1e300]
+    rows = []
+    for k in range(n):
+        row = [int(rng.choice(ints)), int(rng.choice(longs)), float(np.float32(rng.choice(floats))),
+               float(rng.choice(doubles)), bool(rng.integers(2)), str(rng.choice(["a", "b", "c"]))]
+        if rng.random() < 0.05:
+            row[int(rng.integers(6))] = None
+        rows.append(row)
+    return rows
+
+
+def test_typed_compare_semantics():
+    qs = [TYPED_STREAM]
+    n = 0
+    for a in NUMERIC:
+        for b in NUMERIC:
+            for op in OPS:
+                qs.append(f"@info(name='u{n}') from every e1=T[{a} {op} {b}] select e1.i as x insert into O;")
+                qs.append(f"@info(name='x{n}') from every e1=T -> e2=T[{a} {op} e1.{b}] "
+                          f"select e1.i as x insert into O;")
+                n += 1
+    for op in ("==", "!="):
+        qs.append(f"@info(name='bb{op}') from every e1=T -> e2=T[b {op} e1.b] select e1.i as x insert into O;")
+        qs.append(f"@info(name='ss{op}') from every e1=T -> e2=T[s {op} e1.s and s {op} 'b'] "
+                  f"select e1.i as x insert into O;")
+    qs.append("@info(name='flag') from every e1=T[b] select e1.i as x insert into O;")
+    qs.append("@info(name='consts') from every e1=T[f > 16777216 and l < 3.0f and d >= 7L] "
+              "select e1.i as x insert into O;")
+    src = " ".join(qs)
+    o = App(src)
+    g = hip_app(src, partials=512)
+    rows = typed_events()
+    for k, row in enumerate(rows):
+        o.send("T", [row], [1000 + k])
+        g.send("T", [row], [1000 + k])
+    assert len(o.matches) > 1000
+    assert g.matches == o.matches
+
+
+def test_multi_stream_chain_and_within():
+    src = ("define stream A (v int, p float); define stream B (v int, p float); "
+           "@info(name='q1') from every e1=A[p > 10] -> e2=B[p > e1.p] -> e3=A[v == e1.v] within 50 "
+           "milliseconds select e1.v as a insert into O; "
+           "@info(name='q2') from e1=A[p > 50] -> e2=B[p < e1.p] select e1.v as a insert into O;")
+    o = App(src)
+    g = hip_app(src)
+    rng = np.random.default_rng(11)
+    t = 0
+    for k in range(600):
+        t += int(rng.integers(0, 7))
+        s = "A" if rng.random() < 0.5 else "B"
+        row = [int(rng.integers(0, 5)), float(np.float32(rng.uniform(0, 100)))]
+        o.send(s, [row], [t])
+        g.send(s, [row], [t])
+    assert len(o.matches) > 50
+    assert g.matches == o.matches
+
+
+def test_unordered_timestamps_fall_back_exactly():
+    # out-of-order timestamps disable warm-up chunking; the result must still be exact
+    src = c2_app(6)
+    o = App(src)
+    g = hip_app(src, chunk_events=512, partials=256)
+    ts, cols = c2_columns(0, 20000)
+    ts = ts.copy()
+    ts[7000:7100] -= 5000
+    vals = np.stack([c.astype(np.int64) for c in cols], 1)
+    o.engine.send(0, ts, vals, None)
+    g.engine.push_columns(0, ts, cols)
+    assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2)
