@@ -907,25 +907,26 @@ void deliver_deferred(Engine* e) {
   e->deferred.clear();
 }
 
-void send_one(Engine* e, int stream, i64 seq, i64 ts) {
+// One junction subscriber (a top-level query, or a partition's PartitionStreamReceiver) receives
+// the whole chunk before the next subscriber does (StreamJunction.sendEvent:185-205 loops over
+// receivers in subscription order); single-stream receivers hand their matches to the selector at
+// the end of their chunk (SingleProcessStreamReceiver.processAndClear:57-80).
+void deliver_to(Engine* e, int qi, int stream, const std::vector<i64>& seqs) {
   const Program& P = e->prog;
-  // top-level queries and partitions in app order: queries carry their partition index
-  std::vector<char> part_done(P.parts.size(), 0);
-  for (size_t qi = 0; qi < P.queries.size(); ++qi) {
-    const QueryDef& q = P.queries[qi];
-    if (q.partition < 0) {
-      e->top[qi]->receive(stream, seq, ts);
-      continue;
-    }
-    int pi = q.partition;
-    if (part_done[pi]) continue;
-    part_done[pi] = 1;
-    const PartDef& pd = P.parts[pi];
+  const QueryDef& q = P.queries[qi];
+  if (q.partition < 0) {
+    for (i64 seq : seqs) e->top[qi]->receive(stream, seq, e->log[seq].ts);
+    deliver_deferred(e);
+    return;
+  }
+  const int pi = q.partition;
+  const PartDef& pd = P.parts[pi];
+  for (i64 seq : seqs) {
     for (const PartKey& k : pd.keys) {
       if (k.stream != stream) continue;
       EvalCtx cx{&e->log, &P.stream_types};
       std::vector<StreamEvent*> slots(1);
-      StreamEvent tmp{seq, ts};
+      StreamEvent tmp{seq, e->log[seq].ts};
       slots[0] = &tmp;
       Value kv = run_code(cx, k.code, slots);
       if (kv.null) continue;  // PartitionStreamReceiver.send: null key drops the event
@@ -942,8 +943,22 @@ void send_one(Engine* e, int stream, i64 seq, i64 ts) {
         it = inst.emplace(key, std::move(rts)).first;
         e->key_order[pi].push_back(key);
       }
-      for (auto& rt : it->second) rt->receive(stream, seq, ts);
+      for (auto& rt : it->second) rt->receive(stream, seq, e->log[seq].ts);
+      deliver_deferred(e);
     }
+  }
+}
+
+void send_chunk(Engine* e, int stream, const std::vector<i64>& seqs) {
+  const Program& P = e->prog;
+  std::vector<char> part_done(P.parts.size(), 0);
+  for (size_t qi = 0; qi < P.queries.size(); ++qi) {
+    const QueryDef& q = P.queries[qi];
+    if (q.partition >= 0) {
+      if (part_done[q.partition]) continue;
+      part_done[q.partition] = 1;
+    }
+    deliver_to(e, (int)qi, stream, seqs);
   }
 }
 
@@ -978,6 +993,7 @@ int oracle_send(OracleEngine* e, int32_t stream, int64_t n, const int64_t* ts, c
   try {
     if (stream < 0 || stream >= (int)e->prog.stream_types.size()) throw std::runtime_error("bad stream");
     size_t na = e->prog.stream_types[stream].size();
+    std::vector<i64> seqs;
     for (int64_t k = 0; k < n; ++k) {
       InEvent ev;
       ev.stream = stream;
@@ -985,13 +1001,16 @@ int oracle_send(OracleEngine* e, int32_t stream, int64_t n, const int64_t* ts, c
       ev.vals.assign(vals + k * na, vals + (k + 1) * na);
       if (nulls) ev.nulls.assign(nulls + k * na, nulls + (k + 1) * na);
       else ev.nulls.assign(na, 0);
-      i64 seq = (i64)e->log.size();
+      seqs.push_back((i64)e->log.size());
       e->log.push_back(std::move(ev));
-      send_one(e, stream, seq, ts[k]);
-      if (!as_chunk) deliver_deferred(e);
-      e->gc();
+      if (!as_chunk) {
+        send_chunk(e, stream, seqs);
+        seqs.clear();
+        e->gc();
+      }
     }
-    deliver_deferred(e);
+    if (!seqs.empty()) send_chunk(e, stream, seqs);
+    e->gc();
     return 0;
   } catch (const std::exception& ex) {
     e->err = ex.what();

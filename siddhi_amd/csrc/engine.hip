@@ -168,7 +168,7 @@ int conv_of(int t, int d) {
   switch (d) {
     case D_I32:
     case D_I64: return t == T_INT ? CV_I64_INT : CV_I64_LONG;
-    case D_F32: return t == T_INT ? CV_F32_INT : t == T_LONG ? CV_F32_LONG : CV_F32_FLOAT;
+    case D_F32: return t == T_INT ? CV_F32_INT : t == T_LONG ? CV_F32_LONG : CV_F64_FLOAT;  // float->double is exact
     case D_F64:
       return t == T_INT ? CV_F64_INT : t == T_LONG ? CV_F64_LONG : t == T_FLOAT ? CV_F64_FLOAT : CV_F64_DOUBLE;
     default: return CV_RAW;
@@ -250,6 +250,8 @@ Lowered lower_query(const IProgram& P, int qi) {
   int na = 0;
   for (int s = 0; s < n; ++s) {
     c.atom_begin[s] = na;
+    std::vector<Atom> const_atoms, x_atoms;
+    std::vector<int> x_cols;
     for (const auto& code : q.st[s].filters) {
       // postfix -> tree
       std::vector<Node> nodes;
@@ -279,8 +281,7 @@ Lowered lower_query(const IProgram& P, int qi) {
         else leaves.push_back(x);
       }
       for (int x : leaves) {
-        if (na >= MAXATOM) return fail("too many predicate atoms");
-        Atom& A = c.atoms[na];
+        Atom A{};
         const Node& nd = nodes[x];
         Insn li, ri;
         int op;
@@ -333,8 +334,26 @@ Lowered lower_query(const IProgram& P, int qi) {
         };
         if (!operand(li, A.lk, A.li, A.lc) || !operand(ri, A.rk, A.ri, A.rc))
           return fail("operand not addressable (too many columns / captures)");
-        ++na;
+        if (A.lk == OPK_CAP || A.rk == OPK_CAP) {
+          x_atoms.push_back(A);
+          x_cols.push_back(A.lk == OPK_CUR ? A.li : A.rk == OPK_CUR ? A.ri : -1);
+        } else {
+          const_atoms.push_back(A);
+        }
       }
+    }
+    // partial-independent atoms first (tile-vectorized), capture readers last (per partial)
+    if (na + (int)(const_atoms.size() + x_atoms.size()) > MAXATOM) return fail("too many predicate atoms");
+    if (c.n_xa + (int)x_atoms.size() > MAXXA) return fail("too many capture-reading predicate atoms");
+    for (const Atom& A : const_atoms) c.atoms[na++] = A;
+    c.xa_first[s] = c.n_xa;
+    c.xa_count[s] = (int)x_atoms.size();
+    for (size_t k = 0; k < x_atoms.size(); ++k) {
+      c.atoms[na] = x_atoms[k];
+      c.xa_atom[c.n_xa] = na;
+      c.xa_col[c.n_xa] = x_cols[k];
+      ++c.n_xa;
+      ++na;
     }
   }
   c.atom_begin[n] = na;
@@ -529,7 +548,7 @@ void launch(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2
   L.rec_words = e->rec_words;
   L.seg_count = e->d_seg_count.p;
   L.err = e->d_err.p;
-  const size_t lds = (size_t)4 * WAVE * (MAXCOL + 2) * 8;
+  const size_t lds = 0;
   HIPCHK(hipEventRecord(e->ev0, e->stream));
   for (int i0 = 0; i0 < n_items;) {
     const int S = e->lq[e->work[i0].q].cq.n_states;

@@ -101,39 +101,15 @@ __device__ __forceinline__ int64_t cap_get(const PSet P, int idx) {
   return v;
 }
 
-// LDS tile of one wave: [n_col][64] keys, [64] ts, [64] null bits (per column)
-struct Tile {
-  const int64_t* key;
-  const int64_t* ts;
-  const uint32_t* nul;
-};
-
-__device__ __forceinline__ int64_t operand(int kind, int idx, int64_t c, const Tile T, int k,
-                                           const PSet P, bool& nul) {
-  if (kind == OPK_CUR) {
-    nul = (T.nul[k] >> idx) & 1u;
-    return T.key[idx * WAVE + k];
-  }
-  if (kind == OPK_CAP) {
-    nul = (P.cn >> idx) & 1u;
-    return cap_get(P, idx);
-  }
-  nul = kind != OPK_CONST;
-  return c;
+__device__ __forceinline__ int64_t readlane64(int64_t v, int k) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, k);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), k);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-// conjunction of the atoms of state s (FilterProcessor chain, null -> false)
-__device__ __forceinline__ bool eval_state(const ChainQuery* __restrict__ Q, int a0, int a1,
-                                           const Tile T, int k, const PSet P) {
-  bool ok = true;
-  for (int a = a0; a < a1; ++a) {
-    const Atom& A = Q->atoms[a];
-    bool ln, rn;
-    const int64_t l = operand(A.lk, A.li, A.lc, T, k, P, ln);
-    const int64_t r = operand(A.rk, A.ri, A.rc, T, k, P, rn);
-    ok = ok && !ln && !rn && cmp_keys(A.mask, A.f64, l, r);
-  }
-  return ok;
+// one atom on per-lane operands (tile time: lane = event; step time: lane = partial)
+__device__ __forceinline__ bool atom_eval(const Atom& A, int64_t l, bool ln, int64_t r, bool rn) {
+  return !ln && !rn && cmp_keys(A.mask, A.f64, l, r);
 }
 
 // first index i in [0, c0) with ts[i] >= target (64-ary search, all lanes cooperate)
@@ -156,7 +132,6 @@ __device__ int64_t lower_bound_ts(const int64_t* ts, int64_t c0, int64_t target,
 
 template <int S, int K>
 __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
-  extern __shared__ __attribute__((aligned(16))) int64_t smem[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + wv;
@@ -173,11 +148,6 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
   for (int s = 0; s <= S; ++s) abeg[s] = Q->atom_begin[s];
   const int stream = L.b.stream;
   const int pcap = L.pcap;
-
-  int64_t* t_key = smem + (size_t)wv * WAVE * (MAXCOL + 2);
-  int64_t* t_ts = t_key + WAVE * MAXCOL;
-  uint32_t* t_nul = (uint32_t*)(t_ts + WAVE);
-  const Tile T{t_key, t_ts, t_nul};
 
   // ---- start state: persisted table (chunk 0 / window reaching the batch start) or replay ----
   int64_t w0 = 0;
@@ -217,41 +187,94 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
   bool unordered = false, overflow = false, seg_over = false;
   int64_t prev_tile_ts = (w0 == 0) ? L.b.prev_ts : L.b.ts[w0 - 1];
 
+  const int n_xa = Q->n_xa;
+  int xa_first[S], xa_count[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    xa_first[s] = Q->xa_first[s];
+    xa_count[s] = Q->xa_count[s];
+  }
+
   for (int64_t t = w0; t < W.c1; t += WAVE) {
-    // ---- stage 64 events: coalesced column loads, converted once into compare-domain keys ----
+    // ---- stage 64 events, one per lane: coalesced column loads converted once into
+    //      compare-domain keys; partial-independent atoms evaluated for the whole tile ----
     const int64_t e = t + lane;
     const bool live = e < W.c1;
     const int64_t ets = live ? L.b.ts[e] : INT64_MAX;
-    uint32_t enull = 0;
-    for (int c = 0; c < n_col; ++c) {
-      if (Q->col_stream[c] != stream) continue;  // columns of states fed by other streams
-      const int a = Q->col_attr[c];
-      uint64_t raw = 0;
-      if (live) {
-        const int wdt = L.b.width[a];
-        if (wdt == 8) raw = ((const uint64_t*)L.b.col[a])[e];
-        else if (wdt == 4) raw = ((const uint32_t*)L.b.col[a])[e];
-        else raw = ((const uint8_t*)L.b.col[a])[e];
-        if (L.b.nul[a] && ((const uint8_t*)L.b.nul[a])[e]) enull |= 1u << c;
+    int64_t ck[MAXCOL];
+    uint32_t cnul = 0;
+#pragma unroll
+    for (int c = 0; c < MAXCOL; ++c) {
+      ck[c] = 0;
+      if (c < n_col && Q->col_stream[c] == stream) {
+        const int a = Q->col_attr[c];
+        uint64_t raw = 0;
+        if (live) {
+          const int wdt = L.b.width[a];
+          if (wdt == 8) raw = ((const uint64_t*)L.b.col[a])[e];
+          else if (wdt == 4) raw = ((const uint32_t*)L.b.col[a])[e];
+          else raw = ((const uint8_t*)L.b.col[a])[e];
+          if (L.b.nul[a] && ((const uint8_t*)L.b.nul[a])[e]) cnul |= 1u << c;
+        }
+        ck[c] = to_key(raw, Q->col_conv[c]);
       }
-      t_key[c * WAVE + lane] = to_key(raw, Q->col_conv[c]);
     }
-    t_ts[lane] = ets;
-    t_nul[lane] = enull;
+    auto col_key = [&](int col) {
+      int64_t v = ck[0];
+#pragma unroll
+      for (int c = 1; c < MAXCOL; ++c) v = (col == c) ? ck[c] : v;
+      return v;
+    };
+    // per state: bit k set iff event k passes every atom of the state that reads no capture
+    uint64_t smask[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      bool ok = live && sstream[s] == stream;
+      if (sstream[s] == stream) {
+        const int a1 = abeg[s + 1] - xa_count[s];
+        for (int a = abeg[s]; a < a1; ++a) {
+          const Atom& A = Q->atoms[a];
+          const int64_t l = A.lk == OPK_CUR ? col_key(A.li) : A.lc;
+          const int64_t r = A.rk == OPK_CUR ? col_key(A.ri) : A.rc;
+          const bool ln = A.lk == OPK_NULL || (A.lk == OPK_CUR && ((cnul >> A.li) & 1u));
+          const bool rn = A.rk == OPK_NULL || (A.rk == OPK_CUR && ((cnul >> A.ri) & 1u));
+          ok = ok && atom_eval(A, l, ln, r, rn);
+        }
+      }
+      smask[s] = __ballot(ok);
+    }
+    // current-event operands of the x-atoms, and the captured columns, stay in VGPRs
+    int64_t xcur[MAXXA];
+    uint32_t xnul = 0;
+#pragma unroll
+    for (int j = 0; j < MAXXA; ++j) {
+      xcur[j] = 0;
+      if (j < n_xa && Q->xa_col[j] >= 0) {
+        xcur[j] = col_key(Q->xa_col[j]);
+        xnul |= ((cnul >> Q->xa_col[j]) & 1u) << j;
+      }
+    }
+    int64_t capv[MAXCAP];
+    uint32_t capn = 0;
+#pragma unroll
+    for (int c = 0; c < MAXCAP; ++c) {
+      capv[c] = 0;
+      if (c < n_cap) {
+        capv[c] = col_key(Q->cap_col[c]);
+        capn |= ((cnul >> Q->cap_col[c]) & 1u) << c;
+      }
+    }
     // timestamps must be non-decreasing for chunk warm-up to be exact
     int64_t pred = __shfl_up(ets, 1, WAVE);
     if (lane == 0) pred = prev_tile_ts;
     if (live && ets < pred) unordered = true;
     prev_tile_ts = __shfl(ets, WAVE - 1, WAVE);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     const int cnt = (int)((W.c1 - t) < WAVE ? (W.c1 - t) : WAVE);
     for (int k = 0; k < cnt; ++k) {
       const int64_t j = t + k;
       const bool emit_ok = j >= W.c0;
-      const int64_t cts = t_ts[k];
+      const int64_t cts = readlane64(ets, k);
       const int64_t cseq = L.b.seq_base + j;
 
       // ---- non-start states, last to first (reverse registration order) ----
@@ -259,12 +282,29 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
       for (int s = S - 1; s >= 1; --s) {
         if (sstream[s] != stream) continue;
         const bool last = (s == S - 1);
+        const bool cpass = (smask[s] >> k) & 1ull;
 #pragma unroll
         for (int kk = 0; kk < K; ++kk) {
           const bool in_s = P[kk].st == s;
           if (__ballot(in_s) == 0) continue;
           const bool exp = in_s && within >= 0 && expired(P[kk].ts0, cts, within);
-          const bool pass = in_s && !exp && eval_state(Q, abeg[s], abeg[s + 1], T, k, P[kk]);
+          bool pass = in_s && !exp && cpass;
+          if (cpass) {
+#pragma unroll
+            for (int x = 0; x < MAXXA; ++x) {
+              if (x < xa_first[s] || x >= xa_first[s] + xa_count[s]) continue;
+              const Atom& A = Q->atoms[Q->xa_atom[x]];
+              const int64_t cur = readlane64(xcur[x], k);
+              const bool curn = (__builtin_amdgcn_readlane(xnul, k) >> x) & 1u;
+              const int64_t l = A.lk == OPK_CUR ? cur : A.lk == OPK_CAP ? cap_get(P[kk], A.li) : A.lc;
+              const int64_t r = A.rk == OPK_CUR ? cur : A.rk == OPK_CAP ? cap_get(P[kk], A.ri) : A.rc;
+              const bool ln = A.lk == OPK_NULL || (A.lk == OPK_CUR && curn) ||
+                              (A.lk == OPK_CAP && ((P[kk].cn >> A.li) & 1u));
+              const bool rn = A.rk == OPK_NULL || (A.rk == OPK_CUR && curn) ||
+                              (A.rk == OPK_CAP && ((P[kk].cn >> A.ri) & 1u));
+              pass = pass && atom_eval(A, l, ln, r, rn);
+            }
+          }
           if (last) {
             const uint64_t m = __ballot(pass);
             if (m && emit_ok) {
@@ -289,14 +329,11 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
 #pragma unroll
               for (int q2 = 1; q2 < MAXS - 1; ++q2)
                 if (q2 == s) P[kk].sq[q2] = cseq;
-              for (int c = 0; c < n_cap; ++c) {
-                if (Q->cap_slot[c] != s) continue;
-                const int col = Q->cap_col[c];
-                const int64_t v = t_key[col * WAVE + k];
-                const uint32_t nb = (t_nul[k] >> col) & 1u;
 #pragma unroll
-                for (int c2 = 0; c2 < MAXCAP; ++c2)
-                  if (c2 == c) P[kk].cp[c2] = v;
+              for (int c = 0; c < MAXCAP; ++c) {
+                if (c >= n_cap || Q->cap_slot[c] != s) continue;
+                P[kk].cp[c] = readlane64(capv[c], k);
+                const uint32_t nb = (__builtin_amdgcn_readlane(capn, k) >> c) & 1u;
                 P[kk].cn = (P[kk].cn & ~(1u << c)) | (nb << c);
               }
             }
@@ -305,52 +342,49 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
       }
 
       // ---- start state: the seed (every re-arms it, otherwise one match consumes it) ----
-      if (seed_alive && sstream[0] == stream) {
-        const bool p0 = eval_state(Q, abeg[0], abeg[1], T, k, P[0]);
-        if (__ballot(p0) != 0) {  // uniform: the seed only reads the current event
-          if (S == 1) {
-            if (emit_ok) {
-              if (nmatch + 1 > W.seg_cap) {
-                seg_over = true;
-              } else if (lane == 0) {
-                int64_t* r = seg + nmatch * RW;
-                r[0] = qid;
-                r[1] = cts;
-                r[2] = cseq;
-              }
-              nmatch += 1;
+      if (seed_alive && ((smask[0] >> k) & 1ull)) {
+        if (S == 1) {
+          if (emit_ok) {
+            if (nmatch + 1 > W.seg_cap) {
+              seg_over = true;
+            } else if (lane == 0) {
+              int64_t* r = seg + nmatch * RW;
+              r[0] = qid;
+              r[1] = cts;
+              r[2] = cseq;
             }
-          } else {
-            bool placed = false;
-#pragma unroll
-            for (int kk = 0; kk < K; ++kk) {
-              if (placed) continue;
-              const uint64_t freem = ~__ballot(P[kk].st >= 0);
-              if (freem == 0) continue;
-              placed = true;
-              if (lane == __builtin_ctzll(freem)) {
-                P[kk].st = 1;
-                P[kk].ts0 = cts;
-                P[kk].sq[0] = cseq;
-                P[kk].cn = 0;
-                for (int c = 0; c < n_cap; ++c) {
-                  if (Q->cap_slot[c] != 0) continue;
-                  const int col = Q->cap_col[c];
-                  const int64_t v = t_key[col * WAVE + k];
-#pragma unroll
-                  for (int c2 = 0; c2 < MAXCAP; ++c2)
-                    if (c2 == c) P[kk].cp[c2] = v;
-                  P[kk].cn |= ((t_nul[k] >> col) & 1u) << c;
-                }
-              }
-            }
-            if (!placed) overflow = true;
+            nmatch += 1;
           }
-          if (!every) seed_alive = 0;
+        } else {
+          bool placed = false;
+#pragma unroll
+          for (int kk = 0; kk < K; ++kk) {
+            if (placed) continue;
+            const uint64_t freem = ~__ballot(P[kk].st >= 0);
+            if (freem == 0) continue;
+            placed = true;
+            if (lane == __builtin_ctzll(freem)) {
+              P[kk].st = 1;
+              P[kk].ts0 = cts;
+              P[kk].sq[0] = cseq;
+              P[kk].cn = 0;
+            }
+#pragma unroll
+            for (int c = 0; c < MAXCAP; ++c) {
+              if (c >= n_cap || Q->cap_slot[c] != 0) continue;
+              const int64_t v = readlane64(capv[c], k);
+              const uint32_t nb = (__builtin_amdgcn_readlane(capn, k) >> c) & 1u;
+              if (lane == __builtin_ctzll(freem)) {
+                P[kk].cp[c] = v;
+                P[kk].cn |= nb << c;
+              }
+            }
+          }
+          if (!placed) overflow = true;
         }
+        if (!every) seed_alive = 0;
       }
     }
-    __builtin_amdgcn_wave_barrier();
   }
 
   // ---- outputs ----

@@ -14,6 +14,7 @@ constexpr int MAXS = 4;      // states per chain query
 constexpr int MAXCAP = 4;    // captured operand keys per partial match
 constexpr int MAXATOM = 12;  // compare atoms per query (all states)
 constexpr int MAXCOL = 8;    // pre-keyed operand columns of the current event
+constexpr int MAXXA = 4;     // atoms reading captured values (evaluated per partial)
 constexpr int MAXATTR = 16;  // attributes per stream
 constexpr int WAVE = 64;
 
@@ -62,7 +63,15 @@ struct ChainQuery {
   int32_t n_col;        // pre-keyed operand columns
   int32_t col_attr[MAXCOL], col_conv[MAXCOL], col_stream[MAXCOL];
   int32_t state_stream[MAXS];
+  // atoms of state s are [atom_begin[s], atom_begin[s+1]); those that read captured values are
+  // listed as "x-atoms" xa_first[s] .. xa_first[s]+xa_count[s]-1 (xa_atom[j] = atom index) and
+  // evaluated per partial; all others read only the current event and constants and are
+  // evaluated for a whole 64-event tile at once (one lane per event).
   int32_t atom_begin[MAXS + 1];
+  int32_t xa_first[MAXS], xa_count[MAXS];
+  int32_t n_xa;
+  int32_t xa_atom[MAXXA];      // atom index of x-atom j
+  int32_t xa_col[MAXXA];       // column of its current-event operand (-1: none)
   int32_t cap_slot[MAXCAP], cap_col[MAXCAP];
   Atom atoms[MAXATOM];
 };
