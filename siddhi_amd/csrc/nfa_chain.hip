@@ -130,6 +130,20 @@ __device__ int64_t lower_bound_ts(const int64_t* ts, int64_t c0, int64_t target,
   return lo;
 }
 
+// Per-state predicate/capture descriptor, resolved once per wave into SGPRs so that the event
+// loop carries no data-dependent decisions about the query's shape.
+struct StateDesc {
+  int active;        // state fed by this launch's stream
+  int has_x;         // state has a capture-reading atom (at most one, planner-enforced)
+  int l_cap, r_cap;  // operand is a captured value (index in lcap/rcap)
+  int l_cur, r_cur;  // operand is the current event (key in xcur)
+  int lcap, rcap;
+  int64_t lc, rc;    // constant keys (used when neither CAP nor CUR)
+  int l_null, r_null;
+  int f64, mask;
+  uint32_t capmask;  // captures taken when a partial passes this state
+};
+
 template <int S, int K>
 __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -138,16 +152,31 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
   if (wid >= L.n_work) return;
   const WorkItem W = L.work[wid];
   const ChainQuery* __restrict__ Q = L.queries + W.q;
-  // wave-uniform program fields, kept in SGPRs for the whole chunk
-  const int64_t within = Q->within;
-  const int every = Q->every, n_cap = Q->n_cap, qid = Q->qid, n_col = Q->n_col;
-  int sstream[S], abeg[S + 1];
-#pragma unroll
-  for (int s = 0; s < S; ++s) sstream[s] = Q->state_stream[s];
-#pragma unroll
-  for (int s = 0; s <= S; ++s) abeg[s] = Q->atom_begin[s];
   const int stream = L.b.stream;
   const int pcap = L.pcap;
+  // ---- wave-uniform program, resolved into SGPRs for the whole chunk ----
+  const int64_t within = Q->within < 0 ? INT64_MAX : Q->within;
+  const int every = Q->every, n_cap = Q->n_cap, qid = Q->qid, n_col = Q->n_col;
+  StateDesc D[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    StateDesc d{};
+    d.active = Q->state_stream[s] == stream;
+    d.has_x = Q->xa_count[s] > 0;
+    if (d.has_x) {
+      const Atom& A = Q->atoms[Q->xa_atom[Q->xa_first[s]]];
+      d.l_cap = A.lk == OPK_CAP; d.r_cap = A.rk == OPK_CAP;
+      d.l_cur = A.lk == OPK_CUR; d.r_cur = A.rk == OPK_CUR;
+      d.lcap = d.l_cap ? A.li : 0; d.rcap = d.r_cap ? A.ri : 0;
+      d.lc = A.lc; d.rc = A.rc;
+      d.l_null = A.lk == OPK_NULL; d.r_null = A.rk == OPK_NULL;
+      d.f64 = A.f64; d.mask = A.mask;
+    }
+    uint32_t cm = 0;
+    for (int c = 0; c < n_cap; ++c) cm |= (Q->cap_slot[c] == s ? 1u : 0u) << c;
+    d.capmask = cm;
+    D[s] = d;
+  }
 
   // ---- start state: persisted table (chunk 0 / window reaching the batch start) or replay ----
   int64_t w0 = 0;
@@ -187,14 +216,6 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
   bool unordered = false, overflow = false, seg_over = false;
   int64_t prev_tile_ts = (w0 == 0) ? L.b.prev_ts : L.b.ts[w0 - 1];
 
-  const int n_xa = Q->n_xa;
-  int xa_first[S], xa_count[S];
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    xa_first[s] = Q->xa_first[s];
-    xa_count[s] = Q->xa_count[s];
-  }
-
   for (int64_t t = w0; t < W.c1; t += WAVE) {
     // ---- stage 64 events, one per lane: coalesced column loads converted once into
     //      compare-domain keys; partial-independent atoms evaluated for the whole tile ----
@@ -227,12 +248,15 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
     };
     // per state: bit k set iff event k passes every atom of the state that reads no capture
     uint64_t smask[S];
+    int64_t xcur[S];      // current-event operand of the state's capture-reading atom
+    uint32_t xnul = 0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      bool ok = live && sstream[s] == stream;
-      if (sstream[s] == stream) {
-        const int a1 = abeg[s + 1] - xa_count[s];
-        for (int a = abeg[s]; a < a1; ++a) {
+      bool ok = live && D[s].active;
+      xcur[s] = 0;
+      if (D[s].active) {
+        const int a1 = Q->atom_begin[s + 1] - Q->xa_count[s];
+        for (int a = Q->atom_begin[s]; a < a1; ++a) {
           const Atom& A = Q->atoms[a];
           const int64_t l = A.lk == OPK_CUR ? col_key(A.li) : A.lc;
           const int64_t r = A.rk == OPK_CUR ? col_key(A.ri) : A.rc;
@@ -240,19 +264,15 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
           const bool rn = A.rk == OPK_NULL || (A.rk == OPK_CUR && ((cnul >> A.ri) & 1u));
           ok = ok && atom_eval(A, l, ln, r, rn);
         }
+        if (D[s].has_x) {
+          const int col = Q->xa_col[Q->xa_first[s]];
+          if (col >= 0) {
+            xcur[s] = col_key(col);
+            xnul |= ((cnul >> col) & 1u) << s;
+          }
+        }
       }
       smask[s] = __ballot(ok);
-    }
-    // current-event operands of the x-atoms, and the captured columns, stay in VGPRs
-    int64_t xcur[MAXXA];
-    uint32_t xnul = 0;
-#pragma unroll
-    for (int j = 0; j < MAXXA; ++j) {
-      xcur[j] = 0;
-      if (j < n_xa && Q->xa_col[j] >= 0) {
-        xcur[j] = col_key(Q->xa_col[j]);
-        xnul |= ((cnul >> Q->xa_col[j]) & 1u) << j;
-      }
     }
     int64_t capv[MAXCAP];
     uint32_t capn = 0;
@@ -271,39 +291,37 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
     prev_tile_ts = __shfl(ets, WAVE - 1, WAVE);
 
     const int cnt = (int)((W.c1 - t) < WAVE ? (W.c1 - t) : WAVE);
+#pragma unroll 1
     for (int k = 0; k < cnt; ++k) {
       const int64_t j = t + k;
       const bool emit_ok = j >= W.c0;
       const int64_t cts = readlane64(ets, k);
       const int64_t cseq = L.b.seq_base + j;
+      const uint32_t capn_k = __builtin_amdgcn_readlane(capn, k);
+      const uint32_t xnul_k = __builtin_amdgcn_readlane(xnul, k);
 
       // ---- non-start states, last to first (reverse registration order) ----
 #pragma unroll
       for (int s = S - 1; s >= 1; --s) {
-        if (sstream[s] != stream) continue;
+        const StateDesc& d = D[s];
+        if (!d.active) continue;
         const bool last = (s == S - 1);
         const bool cpass = (smask[s] >> k) & 1ull;
+        const int64_t cur = readlane64(xcur[s], k);
+        const bool curn = (xnul_k >> s) & 1u;
 #pragma unroll
         for (int kk = 0; kk < K; ++kk) {
           const bool in_s = P[kk].st == s;
           if (__ballot(in_s) == 0) continue;
-          const bool exp = in_s && within >= 0 && expired(P[kk].ts0, cts, within);
+          const bool exp = in_s && expired(P[kk].ts0, cts, within);
           bool pass = in_s && !exp && cpass;
-          if (cpass) {
-#pragma unroll
-            for (int x = 0; x < MAXXA; ++x) {
-              if (x < xa_first[s] || x >= xa_first[s] + xa_count[s]) continue;
-              const Atom& A = Q->atoms[Q->xa_atom[x]];
-              const int64_t cur = readlane64(xcur[x], k);
-              const bool curn = (__builtin_amdgcn_readlane(xnul, k) >> x) & 1u;
-              const int64_t l = A.lk == OPK_CUR ? cur : A.lk == OPK_CAP ? cap_get(P[kk], A.li) : A.lc;
-              const int64_t r = A.rk == OPK_CUR ? cur : A.rk == OPK_CAP ? cap_get(P[kk], A.ri) : A.rc;
-              const bool ln = A.lk == OPK_NULL || (A.lk == OPK_CUR && curn) ||
-                              (A.lk == OPK_CAP && ((P[kk].cn >> A.li) & 1u));
-              const bool rn = A.rk == OPK_NULL || (A.rk == OPK_CUR && curn) ||
-                              (A.rk == OPK_CAP && ((P[kk].cn >> A.ri) & 1u));
-              pass = pass && atom_eval(A, l, ln, r, rn);
-            }
+          if (d.has_x) {
+            const int64_t lcap = cap_get(P[kk], d.lcap), rcap = cap_get(P[kk], d.rcap);
+            const int64_t l = d.l_cap ? lcap : d.l_cur ? cur : d.lc;
+            const int64_t r = d.r_cap ? rcap : d.r_cur ? cur : d.rc;
+            const bool ln = d.l_null || (d.l_cur && curn) || (d.l_cap && ((P[kk].cn >> d.lcap) & 1u));
+            const bool rn = d.r_null || (d.r_cur && curn) || (d.r_cap && ((P[kk].cn >> d.rcap) & 1u));
+            pass = pass && !ln && !rn && cmp_keys(d.mask, d.f64, l, r);
           }
           if (last) {
             const uint64_t m = __ballot(pass);
@@ -326,15 +344,14 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
             if (exp) P[kk].st = -1;
             if (pass) {
               P[kk].st = s + 1;
-#pragma unroll
-              for (int q2 = 1; q2 < MAXS - 1; ++q2)
-                if (q2 == s) P[kk].sq[q2] = cseq;
+              P[kk].sq[s] = cseq;
 #pragma unroll
               for (int c = 0; c < MAXCAP; ++c) {
-                if (c >= n_cap || Q->cap_slot[c] != s) continue;
-                P[kk].cp[c] = readlane64(capv[c], k);
-                const uint32_t nb = (__builtin_amdgcn_readlane(capn, k) >> c) & 1u;
-                P[kk].cn = (P[kk].cn & ~(1u << c)) | (nb << c);
+                const bool take = (d.capmask >> c) & 1u;
+                const int64_t v = readlane64(capv[c], k);
+                const uint32_t nb = (capn_k >> c) & 1u;
+                P[kk].cp[c] = take ? v : P[kk].cp[c];
+                P[kk].cn = take ? ((P[kk].cn & ~(1u << c)) | (nb << c)) : P[kk].cn;
               }
             }
           }
@@ -356,31 +373,33 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
             nmatch += 1;
           }
         } else {
-          bool placed = false;
+          int slot_set = -1, slot_lane = 0;
 #pragma unroll
           for (int kk = 0; kk < K; ++kk) {
-            if (placed) continue;
             const uint64_t freem = ~__ballot(P[kk].st >= 0);
-            if (freem == 0) continue;
-            placed = true;
-            if (lane == __builtin_ctzll(freem)) {
-              P[kk].st = 1;
-              P[kk].ts0 = cts;
-              P[kk].sq[0] = cseq;
-              P[kk].cn = 0;
-            }
-#pragma unroll
-            for (int c = 0; c < MAXCAP; ++c) {
-              if (c >= n_cap || Q->cap_slot[c] != 0) continue;
-              const int64_t v = readlane64(capv[c], k);
-              const uint32_t nb = (__builtin_amdgcn_readlane(capn, k) >> c) & 1u;
-              if (lane == __builtin_ctzll(freem)) {
-                P[kk].cp[c] = v;
-                P[kk].cn |= nb << c;
-              }
+            if (slot_set < 0 && freem != 0) {
+              slot_set = kk;
+              slot_lane = __builtin_ctzll(freem);
             }
           }
-          if (!placed) overflow = true;
+          if (slot_set < 0) overflow = true;
+          const uint32_t cm0 = D[0].capmask;
+#pragma unroll
+          for (int kk = 0; kk < K; ++kk) {
+            if (kk != slot_set) continue;
+            const bool mine = lane == slot_lane;
+            P[kk].st = mine ? 1 : P[kk].st;
+            P[kk].ts0 = mine ? cts : P[kk].ts0;
+            P[kk].sq[0] = mine ? cseq : P[kk].sq[0];
+            P[kk].cn = mine ? 0u : P[kk].cn;
+#pragma unroll
+            for (int c = 0; c < MAXCAP; ++c) {
+              const bool take = mine && ((cm0 >> c) & 1u);
+              const int64_t v = readlane64(capv[c], k);
+              P[kk].cp[c] = take ? v : P[kk].cp[c];
+              P[kk].cn = take ? (P[kk].cn | (((capn_k >> c) & 1u) << c)) : P[kk].cn;
+            }
+          }
         }
         if (!every) seed_alive = 0;
       }
