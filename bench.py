@@ -159,7 +159,7 @@ def main():
                    "matches": matches},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": None,
-                     "kernel": "nfa_chain_kernel", "kernel_ms": avg_ms},
+                     "kernel": "nfa_ratchet_kernel", "kernel_ms": avg_ms},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(None, args.cpu_seconds)

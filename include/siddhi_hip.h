@@ -58,6 +58,9 @@ typedef struct sdh_config {
  * to the host (they stay countable via sdh_engine_pending_matches until then). For consumers that
  * read matches on the device, and for throughput benchmarking of the NFA step. */
 #define SDH_FLAG_DEVICE_MATCHES 1
+/* Disable the K_ratchet plan (every query of that shape runs on the general chain kernel instead);
+ * for differential testing of the two plans. */
+#define SDH_FLAG_NO_RATCHET 2
 
 /* One columnar (SoA) batch of events of one stream, in arrival order.
  * cols[a] points to n elements of attribute a with the stream schema's native width:

@@ -21,6 +21,8 @@
 
 extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaunch* L, int n_blocks,
                                        size_t lds, hipStream_t s);
+extern "C" hipError_t sdh_launch_ratchet(int key_kind, int full, int M, const sdh::RatchetLaunch* L,
+                                         hipStream_t s);
 extern "C" hipError_t sdh_launch_compact(const int64_t* src, const int64_t* seg_off,
                                          const int64_t* seg_count, const int64_t* dst_off,
                                          int rec_words, int n_items, int64_t* dst, hipStream_t s);
@@ -370,6 +372,83 @@ int attr_width(int t) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// K_ratchet plan selection: 2-state `every e1=S[f0] -> e2=S[cur.a OP e1.a]`
+// ------------------------------------------------------------------------------------------
+struct RatchetPlan {
+  bool ok = false;
+  int stream = 0, key_attr = 0, key_conv = 0, key_kind = 0, xmask = 0;
+  std::vector<RatchetAtom> f0;
+  std::vector<int64_t> f0c;
+  int64_t within = -1;
+  // grouping signature: everything except the per-lane constants and `within`
+  std::vector<int64_t> sig() const {
+    std::vector<int64_t> v{stream, key_kind, key_attr, key_conv, xmask, within >= 0, (int64_t)f0.size()};
+    for (const auto& a : f0)
+      v.insert(v.end(), {a.attr, a.conv, a.cur_left, a.mask, a.f64, a.cur2, a.attr2, a.conv2});
+    return v;
+  }
+};
+
+RatchetPlan ratchet_plan(const ChainQuery& c) {
+  RatchetPlan r;
+  if (c.n_states != 2 || !c.every || c.state_stream[0] != c.state_stream[1]) return r;
+  if (c.n_cap != 1 || c.cap_slot[0] != 0) return r;
+  if (c.atom_begin[2] - c.atom_begin[1] != 1 || c.xa_count[1] != 1 || c.xa_count[0] != 0) return r;
+  const Atom& X = c.atoms[c.xa_atom[c.xa_first[1]]];
+  int mask = X.mask;
+  if (mask & CM_NOT) return r;
+  if (!(mask & (CM_LT | CM_GT)) || ((mask & CM_LT) && (mask & CM_GT))) return r;  // ordering only
+  int cur_col;
+  if (X.lk == OPK_CUR && X.rk == OPK_CAP) {
+    cur_col = X.li;
+  } else if (X.lk == OPK_CAP && X.rk == OPK_CUR) {
+    cur_col = X.ri;
+    const int lt = mask & CM_LT, gt = mask & CM_GT;
+    mask = (mask & CM_EQ) | (lt ? CM_GT : 0) | (gt ? CM_LT : 0);  // key OP cur == cur OP' key
+  } else {
+    return r;
+  }
+  if (c.cap_col[0] != cur_col) return r;  // key = e1 value of the same column and conversion
+  const int conv = c.col_conv[cur_col];
+  switch (conv) {
+    case CV_F32_INT: case CV_F32_LONG: case CV_F32_FLOAT: r.key_kind = KK_F32; break;
+    case CV_I64_INT: r.key_kind = X.f64 ? -1 : KK_I32; break;
+    case CV_I64_LONG: r.key_kind = KK_I64; break;
+    case CV_F64_INT: case CV_F64_LONG: case CV_F64_FLOAT: case CV_F64_DOUBLE: r.key_kind = KK_F64; break;
+    default: return r;
+  }
+  if (r.key_kind < 0) return r;
+  const int na0 = c.atom_begin[1] - c.atom_begin[0];
+  if (na0 > RMAXF0) return r;
+  for (int a = c.atom_begin[0]; a < c.atom_begin[1]; ++a) {
+    const Atom& A = c.atoms[a];
+    RatchetAtom ra{};
+    ra.mask = A.mask;
+    ra.f64 = A.f64;
+    int64_t cst = 0;
+    if (A.lk == OPK_CUR && A.rk == OPK_CONST) {
+      ra.attr = c.col_attr[A.li]; ra.conv = c.col_conv[A.li]; ra.cur_left = 1; cst = A.rc;
+    } else if (A.lk == OPK_CONST && A.rk == OPK_CUR) {
+      ra.attr = c.col_attr[A.ri]; ra.conv = c.col_conv[A.ri]; ra.cur_left = 0; cst = A.lc;
+    } else if (A.lk == OPK_CUR && A.rk == OPK_CUR) {
+      ra.attr = c.col_attr[A.li]; ra.conv = c.col_conv[A.li]; ra.cur_left = 1;
+      ra.cur2 = 1; ra.attr2 = c.col_attr[A.ri]; ra.conv2 = c.col_conv[A.ri];
+    } else {
+      return r;  // null operands / constant-only atoms: leave them to K_chain
+    }
+    r.f0.push_back(ra);
+    r.f0c.push_back(cst);
+  }
+  r.stream = c.state_stream[0];
+  r.key_attr = c.col_attr[cur_col];
+  r.key_conv = conv;
+  r.xmask = mask;
+  r.within = c.within;
+  r.ok = true;
+  return r;
+}
+
 template <class T>
 struct DevBuf {
   T* p = nullptr;
@@ -417,6 +496,24 @@ struct sdh_engine {
   int64_t device_matches = 0;
   bool device_unpolled = false;
   std::vector<int64_t> backlog;      // host-side match records (rec_words int64 each)
+  // ---- K_ratchet groups ----
+  std::vector<RatchetGroup> rg;
+  std::vector<int> rcur;             // per group: buffer holding its deques
+  DevBuf<RatchetGroup> d_rg;
+  DevBuf<RatchetState> d_rst[2];
+  DevBuf<int64_t> d_rts[2], d_rsq[2], d_rky[2];
+  DevBuf<RatchetItem> d_ritems;
+  std::vector<RatchetItem> ritems;
+  DevBuf<int64_t> d_rmatch;
+  DevBuf<int32_t> d_blk_count, d_blk_next;
+  int64_t r_blocks = 0;              // capacity in blocks
+  int r_blk_recs = 8192;
+  int r_blocks_used = 0;             // of the last launch
+  std::vector<int32_t> r_blk_count;
+  int rM = 32;                       // LDS deque capacity per lane (power of two <= RSMAX)
+  std::vector<char> r_full_expiry;   // per stream: timestamps were seen out of order
+  int64_t r_matches = 0;
+  double r_kernel_ms = 0, r_kernel_bytes = 0;
   // poll output
   std::vector<int64_t> o_query, o_key, o_ts, o_off, o_words;
   sdh_stats stats{};
@@ -446,13 +543,18 @@ void ensure_state(sdh_engine* e) {
   e->cur.assign(nq, 0);
 }
 
+void ratchet_collect(sdh_engine* e);
+
 void collect_device_matches(sdh_engine* e, bool discard = false) {
   if (!e->device_unpolled) return;
   e->device_unpolled = false;
   if (discard) {
     e->device_matches = 0;
+    e->r_matches = 0;
+    e->r_blocks_used = 0;
     return;
   }
+  ratchet_collect(e);
   const int n_items = (int)e->work.size();
   if (e->device_matches == 0 || n_items == 0) return;
   std::vector<int64_t> seg_off(n_items), dst_off(n_items);
@@ -593,6 +695,233 @@ void launch(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2
   e->device_matches = total_matches;
 }
 
+// ------------------------------------------------------------------------------------------
+// K_ratchet host side
+// ------------------------------------------------------------------------------------------
+void ratchet_build(sdh_engine* e, std::vector<std::pair<RatchetPlan, int>>& plans) {
+  std::stable_sort(plans.begin(), plans.end(), [](const auto& a, const auto& b) {
+    const auto sa = a.first.sig(), sb = b.first.sig();
+    if (sa != sb) return sa < sb;
+    return a.first.within < b.first.within;  // similar warm-up windows share a wave
+  });
+  for (size_t i = 0; i < plans.size();) {
+    size_t j = i;
+    const auto sg = plans[i].first.sig();
+    while (j < plans.size() && j - i < 64 && plans[j].first.sig() == sg) ++j;
+    RatchetGroup g{};
+    const RatchetPlan& P = plans[i].first;
+    g.n_lanes = (int)(j - i);
+    g.stream = P.stream;
+    g.key_attr = P.key_attr;
+    g.key_conv = P.key_conv;
+    g.key_kind = P.key_kind;
+    g.xmask = P.xmask;
+    g.n_f0 = (int)P.f0.size();
+    for (int a = 0; a < g.n_f0; ++a) g.f0[a] = P.f0[a];
+    g.wmax = -1;
+    for (int l = 0; l < 64; ++l) {
+      const size_t k = i + std::min<size_t>(l, j - i - 1);  // idle lanes mirror the last pattern
+      const RatchetPlan& Q = plans[k].first;
+      g.qid[l] = plans[k].second;
+      g.within[l] = Q.within < 0 ? INT64_MAX : Q.within;
+      if (l < g.n_lanes) g.wmax = std::max(g.wmax, Q.within);
+      for (int a = 0; a < g.n_f0; ++a) g.f0c[a][l] = Q.f0c[a];
+    }
+    e->rg.push_back(g);
+    i = j;
+  }
+  const size_t ng = e->rg.size();
+  e->rcur.assign(ng, 0);
+  e->r_full_expiry.assign(e->prog.stream_types.size(), 0);
+  if (!ng) return;
+  e->d_rg.ensure(ng);
+  HIPCHK(hipMemcpy(e->d_rg.p, e->rg.data(), ng * sizeof(RatchetGroup), hipMemcpyHostToDevice));
+  for (int b = 0; b < 2; ++b) {
+    e->d_rst[b].ensure(ng);
+    HIPCHK(hipMemset(e->d_rst[b].p, 0, ng * sizeof(RatchetState)));
+    e->d_rts[b].ensure(ng * RSMAX * WAVE);
+    e->d_rsq[b].ensure(ng * RSMAX * WAVE);
+    e->d_rky[b].ensure(ng * RSMAX * WAVE);
+  }
+  e->d_blk_next.ensure(4);
+}
+
+int64_t ratchet_count_matches(sdh_engine* e) {
+  int64_t n = 0;
+  for (int i = 0; i < e->r_blocks_used; ++i) n += e->r_blk_count[i];
+  return n;
+}
+
+// one NFA step of every ratchet group fed by `stream` over batch B (exact re-runs on overflow /
+// out-of-order timestamps: the groups' input deques are double-buffered and untouched until the
+// launch succeeds)
+void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2]) {
+  e->r_blocks_used = 0;
+  e->r_matches = 0;
+  e->r_kernel_ms = 0;
+  e->r_kernel_bytes = 0;
+  std::vector<int> gs;
+  for (int g = 0; g < (int)e->rg.size(); ++g)
+    if (e->rg[g].stream == stream) gs.push_back(g);
+  if (gs.empty()) return;
+  const int64_t n = B.n;
+  int64_t lanes = 0;
+  for (int g : gs) lanes += e->rg[g].n_lanes;
+  if (e->r_blocks == 0) {
+    const int64_t want = e->cfg.match_capacity > 0 ? e->cfg.match_capacity
+                                                   : std::max<int64_t>(1 << 20, n * lanes * 3 / 4);
+    e->r_blocks = (want + e->r_blk_recs - 1) / e->r_blk_recs;
+  }
+  double ev_per_ms = 1.0;
+  if (n > 1) ev_per_ms = (double)n / (double)std::max<int64_t>(1, t01[1] - t01[0]);
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    const bool full = e->r_full_expiry[stream] != 0;
+    // ---- chunk planning: waves of about equal length (warm-up + emitted events) ----
+    const double target_waves = 2048.0;
+    const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : 4096;
+    double max_warm = 0;
+    for (int g : gs)
+      if (e->rg[g].wmax >= 0) max_warm = std::max(max_warm, (double)e->rg[g].wmax * ev_per_ms + 64.0);
+    const double T = std::max({2.0 * max_warm, (double)n * gs.size() / target_waves, 2.0 * min_chunk});
+    e->ritems.clear();
+    for (int kk = 0; kk < 4; ++kk) {
+      for (int g : gs) {
+        const RatchetGroup& G = e->rg[g];
+        if (G.key_kind != kk) continue;
+        int64_t C = 1;
+        if (!full && G.wmax >= 0) {
+          const double warm = (double)G.wmax * ev_per_ms + 64.0;
+          C = std::max<int64_t>(1, (int64_t)std::ceil((double)n / std::max((double)min_chunk, T - warm)));
+        }
+        for (int64_t ch = 0; ch < C; ++ch) {
+          RatchetItem it{};
+          it.g = g;
+          it.chunk = (int)ch;
+          it.n_chunks = (int)C;
+          it.inb = e->rcur[g];
+          it.c0 = n * ch / C;
+          it.c1 = n * (ch + 1) / C;
+          e->ritems.push_back(it);
+        }
+      }
+    }
+    const int n_items = (int)e->ritems.size();
+    e->d_ritems.ensure(n_items);
+    HIPCHK(hipMemcpyAsync(e->d_ritems.p, e->ritems.data(), n_items * sizeof(RatchetItem),
+                          hipMemcpyHostToDevice, e->stream));
+    e->d_rmatch.ensure((size_t)e->r_blocks * e->r_blk_recs * 4);
+    e->d_blk_count.ensure((size_t)e->r_blocks);
+    e->d_err.ensure(4);
+    HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
+    HIPCHK(hipMemsetAsync(e->d_blk_next.p, 0, 4, e->stream));
+    RatchetLaunch L{};
+    L.groups = e->d_rg.p;
+    L.full_expiry = full;
+    L.b = B;
+    for (int b = 0; b < 2; ++b) {
+      L.st[b] = e->d_rst[b].p;
+      L.ent_ts[b] = e->d_rts[b].p;
+      L.ent_seq[b] = e->d_rsq[b].p;
+      L.ent_key[b] = e->d_rky[b].p;
+    }
+    L.match = e->d_rmatch.p;
+    L.blk_count = e->d_blk_count.p;
+    L.blk_next = e->d_blk_next.p;
+    L.n_blocks = (int32_t)std::min<int64_t>(e->r_blocks, INT32_MAX);
+    L.blk_recs = e->r_blk_recs;
+    L.err = e->d_err.p;
+    HIPCHK(hipEventRecord(e->ev0, e->stream));
+    for (int i0 = 0; i0 < n_items;) {
+      const int kk = e->rg[e->ritems[i0].g].key_kind;
+      int i1 = i0;
+      while (i1 < n_items && e->rg[e->ritems[i1].g].key_kind == kk) ++i1;
+      RatchetLaunch Ls = L;
+      Ls.items = e->d_ritems.p + i0;
+      Ls.n_items = i1 - i0;
+      HIPCHK(sdh_launch_ratchet(kk, full, e->rM, &Ls, e->stream));
+      i0 = i1;
+    }
+    HIPCHK(hipEventRecord(e->ev1, e->stream));
+    int32_t errs[4], used = 0;
+    HIPCHK(hipMemcpyAsync(errs, e->d_err.p, 16, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&used, e->d_blk_next.p, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    if (errs[3]) throw Error(SDH_E_CAPACITY, "a pending partial is more than 2^31 events old");
+    if (errs[1] && !full) {  // timestamps out of order: exact re-run with the full expiry scan
+      e->r_full_expiry[stream] = 1;
+      continue;
+    }
+    if (errs[0]) {
+      if (e->rM >= RSMAX) throw Error(SDH_E_CAPACITY, "ratchet deque overflow (more than 128 pending partials)");
+      e->rM *= 2;
+      continue;
+    }
+    if (errs[2]) {
+      e->r_blocks *= 2;
+      continue;
+    }
+    e->r_blocks_used = std::min<int>(used, (int)e->r_blocks);
+    e->r_blk_count.resize(e->r_blocks_used);
+    if (e->r_blocks_used)
+      HIPCHK(hipMemcpy(e->r_blk_count.data(), e->d_blk_count.p, e->r_blocks_used * 4, hipMemcpyDeviceToHost));
+    for (int g : gs) e->rcur[g] ^= 1;
+    e->r_matches = ratchet_count_matches(e);
+    e->r_kernel_ms = ms;
+    // algorithmic bytes: every wave streams its events once (ts + operand columns)
+    double bytes = 0;
+    for (const RatchetItem& it : e->ritems) {
+      const RatchetGroup& G = e->rg[it.g];
+      int64_t ev_bytes = 8 + B.width[G.key_attr];
+      for (int a = 0; a < G.n_f0; ++a) {
+        if (G.f0[a].attr != G.key_attr) ev_bytes += B.width[G.f0[a].attr];
+        if (G.f0[a].cur2 && G.f0[a].attr2 != G.key_attr) ev_bytes += B.width[G.f0[a].attr2];
+      }
+      const double warm = (it.chunk > 0 && G.wmax >= 0) ? std::min<double>((double)it.c0, (double)G.wmax * ev_per_ms) : 0.0;
+      bytes += ((double)(it.c1 - it.c0) + warm) * ev_bytes;
+    }
+    bytes += (double)e->r_matches * 32.0;
+    e->r_kernel_bytes = bytes;
+    return;
+  }
+  throw Error(SDH_E_CAPACITY, "ratchet launch did not converge");
+}
+
+// append the last ratchet launch's matches (block-compacted) to the host backlog
+void ratchet_collect(sdh_engine* e) {
+  const int nb = e->r_blocks_used;
+  if (nb == 0 || e->r_matches == 0) return;
+  std::vector<int64_t> seg_off(nb), dst_off(nb), cnt(nb);
+  int64_t acc = 0;
+  for (int i = 0; i < nb; ++i) {
+    seg_off[i] = (int64_t)i * e->r_blk_recs;
+    dst_off[i] = acc;
+    cnt[i] = e->r_blk_count[i];
+    acc += cnt[i];
+  }
+  e->d_seg_off.ensure(nb);
+  e->d_dst_off.ensure(nb);
+  DevBuf<int64_t> d_cnt;
+  d_cnt.ensure(nb);
+  e->d_dense.ensure((size_t)acc * 4);
+  HIPCHK(hipMemcpyAsync(e->d_seg_off.p, seg_off.data(), nb * 8, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemcpyAsync(e->d_dst_off.p, dst_off.data(), nb * 8, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemcpyAsync(d_cnt.p, cnt.data(), nb * 8, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(sdh_launch_compact(e->d_rmatch.p, e->d_seg_off.p, d_cnt.p, e->d_dst_off.p, 4, nb, e->d_dense.p,
+                            e->stream));
+  std::vector<int64_t> rec((size_t)acc * 4);
+  HIPCHK(hipMemcpyAsync(rec.data(), e->d_dense.p, rec.size() * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const int RW = e->rec_words;
+  const size_t base = e->backlog.size();
+  e->backlog.resize(base + (size_t)acc * RW, 0);
+  for (int64_t i = 0; i < acc; ++i)
+    for (int w = 0; w < 4; ++w) e->backlog[base + i * RW + w] = rec[i * 4 + w];
+  e->r_matches = 0;
+  e->r_blocks_used = 0;
+}
+
 int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   if (!b || stream < 0 || stream >= (int)e->prog.stream_types.size())
     throw Error(SDH_E_INVALID, "bad stream or batch");
@@ -651,6 +980,10 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     t01[0] = b->ts[0];
     t01[1] = b->ts[b->n - 1];
   }
+  double ms = 0, bytes = 0;
+  int64_t consumers = 0;
+  e->work.clear();
+  e->device_matches = 0;
   if (!qs.empty()) {
     bool unordered = false;
     launch(e, stream, B, t01, qs, true, &unordered);
@@ -658,9 +991,21 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     for (auto& w : e->work) chunked |= w.n_chunks > 1;
     if (unordered && chunked) launch(e, stream, B, t01, qs, false, &unordered);  // exact fallback
     for (int li : qs) e->cur[li] ^= 1;
+    ms += e->stats.last_kernel_ms;
+    bytes += e->stats.last_kernel_bytes;
+    consumers += (int64_t)qs.size();
+  }
+  launch_ratchet(e, stream, B, t01);
+  for (const auto& g : e->rg)
+    if (g.stream == stream) consumers += g.n_lanes;
+  ms += e->r_kernel_ms;
+  bytes += e->r_kernel_bytes;
+  if (consumers) {
     e->device_unpolled = true;
-    e->stats.pattern_events += b->n * (int64_t)qs.size();
-    e->stats.matches += e->device_matches;
+    e->stats.pattern_events += b->n * consumers;
+    e->stats.matches += e->device_matches + e->r_matches;
+    e->stats.last_kernel_ms = ms;
+    e->stats.last_kernel_bytes = bytes;
   }
   e->prev_ts[stream] = t01[1];
   e->seq += b->n;
@@ -702,16 +1047,20 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     if (ndev <= 0) throw Error(SDH_E_DEVICE, "no HIP device (the engine has no CPU fallback)");
     HIPCHK(hipSetDevice(e->dev));
     e->prog = read_ir(ir, len);
+    std::vector<std::pair<RatchetPlan, int>> rplans;
+    const bool no_ratchet = (e->cfg.flags & SDH_FLAG_NO_RATCHET) != 0;
     for (int qi = 0; qi < (int)e->prog.q.size(); ++qi) {
       if (qi % e->cfg.shard_world != e->cfg.shard_rank) continue;
       Lowered L = lower_query(e->prog, qi);
       if (!L.ok) throw Error(SDH_E_UNSUPPORTED, L.why);
-      e->lq.push_back(L);
+      RatchetPlan rp = no_ratchet ? RatchetPlan() : ratchet_plan(L.cq);
+      if (rp.ok) rplans.push_back({rp, qi});
+      else e->lq.push_back(L);
     }
     int want = e->cfg.partials_per_inst > 0 ? e->cfg.partials_per_inst : 128;
     e->K = want <= 64 ? 1 : want <= 128 ? 2 : want <= 256 ? 4 : 8;
     e->pcap = 64 * e->K;
-    int maxS = 1;
+    int maxS = rplans.empty() ? 1 : 2;
     for (auto& L : e->lq) maxS = std::max(maxS, L.cq.n_states);
     e->rec_words = 2 + maxS;
     e->prev_ts.assign(e->prog.stream_types.size(), INT64_MIN);
@@ -724,6 +1073,7 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     if (!cqs.empty())
       HIPCHK(hipMemcpy(e->d_q.p, cqs.data(), cqs.size() * sizeof(ChainQuery), hipMemcpyHostToDevice));
     ensure_state(e);
+    ratchet_build(e, rplans);
     return SDH_OK;
   });
   if (rc != SDH_OK) {
@@ -750,7 +1100,7 @@ int sdh_engine_flush(sdh_engine* e) {
 
 int sdh_engine_pending_matches(sdh_engine* e, int64_t* n) {
   if (!e || !n) return SDH_E_INVALID;
-  *n = (int64_t)(e->backlog.size() / e->rec_words) + (e->device_unpolled ? e->device_matches : 0);
+  *n = (int64_t)(e->backlog.size() / e->rec_words) + (e->device_unpolled ? e->device_matches + e->r_matches : 0);
   return SDH_OK;
 }
 
@@ -813,6 +1163,14 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
       d2h_sync(e, h[b].data(), e->d_hdr[b].p, nq * sizeof(InstHeader));
     }
     for (size_t q = 0; q < nq; ++q) live += h[e->cur[q]][q].n_live;
+    const size_t ng = e->rg.size();
+    for (int b = 0; b < 2 && ng; ++b) {
+      std::vector<RatchetState> rs(ng);
+      d2h_sync(e, rs.data(), e->d_rst[b].p, ng * sizeof(RatchetState));
+      for (size_t g = 0; g < ng; ++g)
+        if (e->rcur[g] == b)
+          for (int l = 0; l < e->rg[g].n_lanes; ++l) live += rs[g].n[l];
+    }
     e->stats.live_partials = live;
     *out = e->stats;
     return SDH_OK;
@@ -836,6 +1194,27 @@ int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
       size_t o = w.size();
       w.resize(o + tbl);
       HIPCHK(hipMemcpy(&w[o], e->d_part[e->cur[q]].p + q * tbl, tbl * 8, hipMemcpyDeviceToHost));
+    }
+    // K_ratchet deques: per group, per lane: n then n x (ts0, seq, key)
+    const size_t ng = e->rg.size();
+    w.push_back((int64_t)ng);
+    for (size_t g = 0; g < ng; ++g) {
+      const int b = e->rcur[g];
+      RatchetState rs;
+      HIPCHK(hipMemcpy(&rs, e->d_rst[b].p + g, sizeof rs, hipMemcpyDeviceToHost));
+      std::vector<int64_t> t(RSMAX * WAVE), sq(RSMAX * WAVE), ky(RSMAX * WAVE);
+      const size_t o = g * RSMAX * WAVE;
+      HIPCHK(hipMemcpy(t.data(), e->d_rts[b].p + o, t.size() * 8, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(sq.data(), e->d_rsq[b].p + o, sq.size() * 8, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(ky.data(), e->d_rky[b].p + o, ky.size() * 8, hipMemcpyDeviceToHost));
+      for (int l = 0; l < WAVE; ++l) {
+        w.push_back(rs.n[l]);
+        for (int i = 0; i < rs.n[l]; ++i) {
+          w.push_back(t[i * WAVE + l]);
+          w.push_back(sq[i * WAVE + l]);
+          w.push_back(ky[i * WAVE + l]);
+        }
+      }
     }
     *len = w.size() * 8;
     *blob = malloc(*len);
@@ -868,9 +1247,33 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
       HIPCHK(hipMemcpy(e->d_part[e->cur[q]].p + q * tbl, &w[i], tbl * 8, hipMemcpyHostToDevice));
       i += tbl;
     }
+    const size_t ng = (size_t)nx();
+    if (ng != e->rg.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
+    for (size_t g = 0; g < ng; ++g) {
+      const int b = e->rcur[g];
+      RatchetState rs{};
+      std::vector<int64_t> t(RSMAX * WAVE, 0), sq(RSMAX * WAVE, 0), ky(RSMAX * WAVE, 0);
+      for (int l = 0; l < WAVE; ++l) {
+        const int64_t nl = nx();
+        if (nl < 0 || nl > RSMAX) throw Error(SDH_E_INVALID, "bad snapshot deque length");
+        rs.n[l] = (int32_t)nl;
+        for (int i = 0; i < nl; ++i) {
+          t[i * WAVE + l] = nx();
+          sq[i * WAVE + l] = nx();
+          ky[i * WAVE + l] = nx();
+        }
+      }
+      const size_t o = g * RSMAX * WAVE;
+      HIPCHK(hipMemcpy(e->d_rst[b].p + g, &rs, sizeof rs, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(e->d_rts[b].p + o, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(e->d_rsq[b].p + o, sq.data(), sq.size() * 8, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(e->d_rky[b].p + o, ky.data(), ky.size() * 8, hipMemcpyHostToDevice));
+    }
     e->backlog.clear();
     e->device_unpolled = false;
     e->device_matches = 0;
+    e->r_matches = 0;
+    e->r_blocks_used = 0;
     return SDH_OK;
   });
 }

@@ -125,4 +125,68 @@ struct ChainLaunch {
   int32_t* err;             // [0] overflow, [1] unordered, [2] segment overflow
 };
 
+// ------------------------------------------------------------------------------------------
+// K_ratchet: the 2-state threshold-ratchet family
+//     every e1=S[f0] -> e2=S[cur.a OP e1.a] within T        OP in {<, <=, >, >=}
+// One lane per pattern; 64 same-shape patterns per wave group. Per lane the pending partials of
+// state 1 form a deque ordered by insertion whose keys (e1.a in the x-atom's compare domain) are
+// monotone, so each event costs O(1) amortised: expire from the bottom, match from the top, push.
+// ------------------------------------------------------------------------------------------
+constexpr int RMAXF0 = 4;     // f0 atoms (event-only, per-lane constant operand)
+constexpr int RSMAX = 128;    // persisted deque capacity per lane (entries)
+
+enum KeyKind { KK_F32 = 0, KK_I32, KK_F64, KK_I64 };
+
+struct RatchetAtom {
+  int32_t attr, conv;    // current-event operand: attribute and key conversion
+  int32_t cur_left;      // 1: `cur OP const`, 0: `const OP cur`
+  int32_t mask;          // CmpMask
+  int32_t f64;           // compare keys as double
+  int32_t cur2;          // 1: the other operand is a current-event attribute too (no constant)
+  int32_t attr2, conv2;  //    (lhs = attr, rhs = attr2)
+};
+
+struct RatchetGroup {
+  int32_t n_lanes;
+  int32_t stream;
+  int32_t key_attr, key_conv, key_kind;   // x-atom operand column (same on both sides)
+  int32_t xmask;                          // normalized `cur OP key` CmpMask (never EQ/NE)
+  int32_t n_f0, pad0;
+  RatchetAtom f0[RMAXF0];
+  int64_t wmax;                           // max within over lanes (-1: none)
+  int32_t qid[64];
+  int64_t within[64];                     // per lane; INT64_MAX = none
+  int64_t f0c[RMAXF0][64];                // per lane constant key of each f0 atom
+};
+
+struct RatchetItem {
+  int32_t g;          // group
+  int32_t chunk, n_chunks;
+  int32_t inb;        // state buffer holding the group's current deques
+  int64_t c0, c1;     // events this item emits for
+};
+
+// persisted per-group deque state: n[64] + entries [RSMAX][64] x {ts0, seq, key}
+struct RatchetState {
+  int32_t n[64];
+  int32_t pad[64];
+};
+
+struct RatchetLaunch {
+  const RatchetGroup* groups;
+  const RatchetItem* items;
+  int32_t n_items;
+  int32_t full_expiry;          // timestamps seen out of order: scan the whole deque for expiry
+  StreamBatch b;
+  RatchetState* st[2];          // [g]
+  int64_t* ent_ts[2];           // [g][RSMAX][64] ts0
+  int64_t* ent_seq[2];          // [g][RSMAX][64] e1 sequence number
+  int64_t* ent_key[2];          // [g][RSMAX][64] key (32-bit kinds in the low word)
+  int64_t* match;               // blocks of blk_recs records x 4 int64 (qid, ts, seq1, seq2)
+  int32_t* blk_count;           // records written per block
+  int32_t* blk_next;            // [0] next free block
+  int32_t n_blocks, blk_recs;
+  int32_t* err;                 // [0] deque overflow, [1] unordered ts, [2] match overflow
+};
+
 }  // namespace sdh

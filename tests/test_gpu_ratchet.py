@@ -1,0 +1,153 @@
+"""GPU parity of the K_ratchet plan (2-state `every e1=S[f0] -> e2=S[a OP e1.a]`) against the CPU
+oracle and against the general chain kernel (SDH_FLAG_NO_RATCHET), bit-exact match tuples."""
+import numpy as np
+import pytest
+
+from harness import App
+from siddhi_amd.workloads import c2_app, stock_events
+
+pytestmark = pytest.mark.gpu
+
+SDH_FLAG_NO_RATCHET = 2
+
+
+def hip_app(src, **kw):
+    from siddhi_amd.engine import HipEngine
+    app = App(src, engine_factory=lambda blob: None)
+    app.engine = HipEngine(app.blob, stream_types=[s.attr_types for s in app.ir.streams], **kw)
+    return app
+
+
+def c2_columns(start, n):
+    ts, sym, price, vol = stock_events(start, n)
+    return ts, [sym, price.view(np.uint32), vol]
+
+
+def words(cols):
+    return np.stack([c.astype(np.int64) for c in cols], 1)
+
+
+@pytest.mark.parametrize("chunk", [0, 2048])
+def test_c2_ratchet_vs_oracle_and_chain(chunk):
+    src = c2_app(130)  # three wave groups, the last one partial
+    o = App(src)
+    r = hip_app(src, chunk_events=chunk)
+    c = hip_app(src, chunk_events=chunk, partials=256, flags=SDH_FLAG_NO_RATCHET)
+    start = 0
+    for n in (5000, 1, 40000, 777):
+        ts, cols = c2_columns(start, n)
+        start += n
+        o.engine.send(0, ts, words(cols), None)
+        om = o.engine.take_matches(lambda q: 2)
+        r.engine.push_columns(0, ts, cols)
+        rm = r.engine.take_matches(lambda q: 2)
+        c.engine.push_columns(0, ts, cols)
+        cm = c.engine.take_matches(lambda q: 2)
+        assert rm == om
+        assert cm == om
+    assert r.engine.stats().matches > 100000
+
+
+ORIENT = ["v > e1.v", "v >= e1.v", "v < e1.v", "v <= e1.v", "e1.v < v", "e1.v >= v"]
+
+
+@pytest.mark.parametrize("typ", ["int", "long", "float", "double"])
+def test_orientations_ties_nulls_nan(typ):
+    qs = [f"define stream S (v {typ}, w int);"]
+    for k, cond in enumerate(ORIENT):
+        qs.append(f"@info(name='a{k}') from every e1=S[w > 2] -> e2=S[{cond}] within 40 milliseconds "
+                  f"select e1.v as x insert into O;")
+        qs.append(f"@info(name='b{k}') from every e1=S -> e2=S[{cond}] within 25 milliseconds "
+                  f"select e1.v as x insert into O;")
+    src = " ".join(qs)
+    o = App(src)
+    g = hip_app(src)
+    rng = np.random.default_rng(5)
+    vals = [0, 1, 2, 3, 3, 5, -1]
+    if typ in ("float", "double"):
+        vals += [float("nan"), -0.0, float("inf")]
+    t = 0
+    for k in range(1500):
+        t += int(rng.integers(0, 4))
+        v = vals[int(rng.integers(len(vals)))]
+        if rng.random() < 0.04:
+            v = None
+        row = [v if v is None or typ in ("float", "double") else int(v), int(rng.integers(0, 6))]
+        o.send("S", [row], [t])
+        g.send("S", [row], [t])
+    assert len(o.matches) > 2000
+    assert g.matches == o.matches
+
+
+def test_two_column_start_filter_and_batches():
+    src = ("define stream S (a int, b float, c double); "
+           "@info(name='q0') from every e1=S[a > 3 and b < c and c >= 2.5] -> e2=S[b > e1.b] within 30 "
+           "milliseconds select e1.a as x insert into O; "
+           "@info(name='q1') from every e1=S[b < c] -> e2=S[e1.b > b] within 90 milliseconds "
+           "select e1.a as x insert into O;")
+    o = App(src)
+    g = hip_app(src, chunk_events=512)
+    rng = np.random.default_rng(9)
+    n = 20000
+    ts = np.cumsum(rng.integers(0, 3, n)).astype(np.int64)
+    a = rng.integers(0, 8, n).astype(np.int32)
+    b = rng.integers(0, 50, n).astype(np.float32)
+    c = rng.integers(0, 50, n).astype(np.float64)
+    cols = [a, b.view(np.uint32), c.view(np.int64)]
+    vals = np.stack([a.astype(np.int64), b.view(np.uint32).astype(np.int64), c.view(np.int64)], 1)
+    for lo, hi in ((0, 3000), (3000, 3001), (3001, n)):
+        o.engine.send(0, ts[lo:hi], vals[lo:hi], None)
+        g.engine.push_columns(0, ts[lo:hi], [x[lo:hi] for x in cols])
+        assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2)
+
+
+def test_deque_growth_and_overflow_is_loud():
+    from siddhi_amd.engine import EngineError
+    src = "define stream S (v int); @info(name='q') from every e1=S -> e2=S[v > e1.v] select e1.v as a insert into O;"
+    o = App(src)
+    g = hip_app(src)
+    # strictly decreasing values pile up 100 pending partials (deque grows 32 -> 64 -> 128) ...
+    ts = np.arange(101, dtype=np.int64)
+    v = np.concatenate([np.arange(100, 0, -1), [1000]]).astype(np.int32)
+    o.engine.send(0, ts, v.astype(np.int64)[:, None], None)
+    g.engine.push_columns(0, ts, [v])
+    got = g.engine.take_matches(lambda q: 2)
+    assert got == o.engine.take_matches(lambda q: 2) and len(got) == 100
+    # ... and more than 128 is a loud SDH_E_CAPACITY, never a wrong answer
+    ts2 = np.arange(101, 301, dtype=np.int64)
+    with pytest.raises(EngineError) as ei:
+        g.engine.push_columns(0, ts2, [np.arange(200, 0, -1).astype(np.int32)])
+    assert ei.value.code == -4
+
+
+def test_ratchet_unordered_timestamps_exact():
+    src = c2_app(70)
+    o = App(src)
+    g = hip_app(src, chunk_events=1024)
+    ts, cols = c2_columns(0, 30000)
+    ts = ts.copy()
+    ts[9000:9050] -= 20000
+    o.engine.send(0, ts, words(cols), None)
+    g.engine.push_columns(0, ts, cols)
+    assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2)
+    ts2, cols2 = c2_columns(30000, 5000)
+    o.engine.send(0, ts2, words(cols2), None)
+    g.engine.push_columns(0, ts2, cols2)
+    assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2)
+
+
+def test_ratchet_snapshot_restore():
+    src = c2_app(66)
+    a = hip_app(src)
+    ts, cols = c2_columns(0, 8000)
+    a.engine.push_columns(0, ts, cols)
+    a.engine.poll()
+    snap = a.engine.snapshot()
+    ts2, cols2 = c2_columns(8000, 6000)
+    a.engine.push_columns(0, ts2, cols2)
+    ref = a.engine.take_matches(lambda q: 2)
+    b = hip_app(src)
+    b.engine.restore(snap)
+    b.engine.push_columns(0, ts2, cols2)
+    assert b.engine.take_matches(lambda q: 2) == ref
+    assert len(ref) > 1000

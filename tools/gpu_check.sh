@@ -1,8 +1,12 @@
+#!/bin/bash
+# GPU check: pytest -m gpu (optionally a subset), smoke(), then bench.py. Usage: gpu_check.sh [pytest-args] [-- bench-args]
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
+TESTS=${1:-tests}
+BENCH=${2:-}
+timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
 tail -3 gpurun_out/gpu_tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
-cat gpurun_out/smoke.log
-timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
-cat gpurun_out/bench.log
+tail -1 gpurun_out/smoke.log
+timeout -k 10 300 python bench.py $BENCH > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log
