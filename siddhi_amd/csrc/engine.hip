@@ -772,27 +772,22 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
                                                    : std::max<int64_t>(1 << 20, n * lanes * 3 / 4);
     e->r_blocks = (want + e->r_blk_recs - 1) / e->r_blk_recs;
   }
-  double ev_per_ms = 1.0;
-  if (n > 1) ev_per_ms = (double)n / (double)std::max<int64_t>(1, t01[1] - t01[0]);
+  (void)t01;
   for (int attempt = 0; attempt < 8; ++attempt) {
     const bool full = e->r_full_expiry[stream] != 0;
-    // ---- chunk planning: waves of about equal length (warm-up + emitted events) ----
-    const double target_waves = 2048.0;
-    const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : 4096;
-    double max_warm = 0;
-    for (int g : gs)
-      if (e->rg[g].wmax >= 0) max_warm = std::max(max_warm, (double)e->rg[g].wmax * ev_per_ms + 64.0);
-    const double T = std::max({2.0 * max_warm, (double)n * gs.size() / target_waves, 2.0 * min_chunk});
+    // ---- chunk planning: chunk c > 0 rebuilds its starting deques by a reverse scan of the
+    // `within` window (a few instructions per 64 events), so chunks can be short: aim for
+    // ~4096 waves (16 per CU) of at least min_chunk emitted events each ----
+    const double target_waves = 4096.0;
+    const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : 2048;
+    const double len = std::max((double)min_chunk, (double)n * gs.size() / target_waves);
     e->ritems.clear();
     for (int kk = 0; kk < 4; ++kk) {
       for (int g : gs) {
         const RatchetGroup& G = e->rg[g];
         if (G.key_kind != kk) continue;
         int64_t C = 1;
-        if (!full && G.wmax >= 0) {
-          const double warm = (double)G.wmax * ev_per_ms + 64.0;
-          C = std::max<int64_t>(1, (int64_t)std::ceil((double)n / std::max((double)min_chunk, T - warm)));
-        }
+        if (!full && G.wmax >= 0) C = std::max<int64_t>(1, (int64_t)std::ceil((double)n / len));
         for (int64_t ch = 0; ch < C; ++ch) {
           RatchetItem it{};
           it.g = g;
@@ -869,17 +864,18 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     for (int g : gs) e->rcur[g] ^= 1;
     e->r_matches = ratchet_count_matches(e);
     e->r_kernel_ms = ms;
-    // algorithmic bytes: every wave streams its events once (ts + operand columns)
+    // algorithmic bytes: every group streams the batch's operand columns once
+    // (ts + x-atom column + f0 columns; the warm-up re-reads are overhead, not counted), writes
+    // 32 B per match and reads + writes its persisted deques (24 B per pending partial)
     double bytes = 0;
-    for (const RatchetItem& it : e->ritems) {
-      const RatchetGroup& G = e->rg[it.g];
+    for (int g : gs) {
+      const RatchetGroup& G = e->rg[g];
       int64_t ev_bytes = 8 + B.width[G.key_attr];
       for (int a = 0; a < G.n_f0; ++a) {
         if (G.f0[a].attr != G.key_attr) ev_bytes += B.width[G.f0[a].attr];
         if (G.f0[a].cur2 && G.f0[a].attr2 != G.key_attr) ev_bytes += B.width[G.f0[a].attr2];
       }
-      const double warm = (it.chunk > 0 && G.wmax >= 0) ? std::min<double>((double)it.c0, (double)G.wmax * ev_per_ms) : 0.0;
-      bytes += ((double)(it.c1 - it.c0) + warm) * ev_bytes;
+      bytes += (double)n * ev_bytes;
     }
     bytes += (double)e->r_matches * 32.0;
     e->r_kernel_bytes = bytes;

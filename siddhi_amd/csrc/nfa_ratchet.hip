@@ -31,6 +31,8 @@
 // per-wave output blocks (one atomic per 8K records). No MFMA: compare/branch work.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "nfa_types.h"
 
 namespace sdh {
@@ -166,16 +168,78 @@ __device__ __forceinline__ uint64_t load_raw(const void* p, int width, int64_t e
 
 }  // namespace
 
-// LDS ring per lane, entry (slot e, lane l) at index e*64 + l:
-//   A: uint4 {ts0.lo, ts0.hi, key.lo, key.hi}       B: uint32 seq (low 32 bits of e1's sequence)
+// ---- key traits: 32-bit keys (binary32 / int32) or 64-bit keys (binary64 / int64) ----
+template <int KK>
+struct KT {
+  static constexpr bool W64 = (KK == KK_F64 || KK == KK_I64);
+  using U = typename std::conditional<W64, uint64_t, uint32_t>::type;
+};
+
+template <class U>
+__device__ __forceinline__ U rlane(U v, int k) {
+  if constexpr (sizeof(U) == 8) return (U)readlane64((int64_t)v, k);
+  else return (U)__builtin_amdgcn_readlane((uint32_t)v, k);
+}
+
+template <class U>
+__device__ __forceinline__ U shdown(U v, int d) {
+  if constexpr (sizeof(U) == 8) {
+    const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, d, WAVE);
+    const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), d, WAVE);
+    return ((uint64_t)hi << 32) | lo;
+  } else {
+    return (U)__shfl_down((int)v, d, WAVE);
+  }
+}
+
+// `a` dominates `b` for the reduction of the x-atom's current-event values: max for `>`/`>=`,
+// min for `<`/`<=` (keys are valid: no NaN)
+template <int KK>
+__device__ __forceinline__ bool dominates(bool is_max, uint64_t a, uint64_t b) {
+  return xcmp<KK>(is_max ? CM_GT : CM_LT, a, b);
+}
+
+// LDS ring per lane; entry (slot e, lane l) at index e*64 + l.
+//   32-bit keys: A = uint4 {ts0.lo, ts0.hi, key, seq}
+//   64-bit keys: A = uint4 {ts0.lo, ts0.hi, key.lo, key.hi}, B = uint32 seq
+// (seq = low 32 bits of e1's global sequence number; a live partial is < 2^31 events old)
+template <int KK>
+struct Ring {
+  using U = typename KT<KK>::U;
+  uint4* A;
+  uint32_t* B;
+  int lane;
+  __device__ __forceinline__ void put(int slot, int64_t ts, U key, uint32_t seq) const {
+    const int i = slot * WAVE + lane;
+    if constexpr (KT<KK>::W64) {
+      A[i] = make_uint4((uint32_t)ts, (uint32_t)((uint64_t)ts >> 32), (uint32_t)key, (uint32_t)(key >> 32));
+      B[i] = seq;
+    } else {
+      A[i] = make_uint4((uint32_t)ts, (uint32_t)((uint64_t)ts >> 32), key, seq);
+    }
+  }
+  __device__ __forceinline__ void get(int slot, int64_t& ts, U& key, uint32_t& seq) const {
+    const int i = slot * WAVE + lane;
+    const uint4 a = A[i];
+    ts = (int64_t)((uint64_t)a.x | ((uint64_t)a.y << 32));
+    if constexpr (KT<KK>::W64) {
+      key = (uint64_t)a.z | ((uint64_t)a.w << 32);
+      seq = B[i];
+    } else {
+      key = a.z;
+      seq = a.w;
+    }
+  }
+};
+
 template <int KK, bool FULL>
 __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M) {
+  using U = typename KT<KK>::U;
   extern __shared__ uint4 lds[];
-  uint4* __restrict__ A = lds;
-  uint32_t* __restrict__ B = reinterpret_cast<uint32_t*>(lds + (size_t)M * WAVE);
   const int lane = threadIdx.x;
   const int wid = blockIdx.x;
   if (wid >= L.n_items) return;
+  const Ring<KK> R{lds, reinterpret_cast<uint32_t*>(lds + (size_t)M * WAVE), lane};
   const RatchetItem W = L.items[wid];
   const RatchetGroup* __restrict__ G = L.groups + W.g;
   const int mask = M - 1;
@@ -186,6 +250,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
   const bool has_within = wmax >= 0;
   const int n_f0 = G->n_f0;
   const int xmask = G->xmask, kconv = G->key_conv, kattr = G->key_attr;
+  const bool is_max = (xmask & CM_GT) != 0;
   // f0 atoms: per-lane constants; operand columns resolved once (wave-uniform)
   int64_t f0c[RMAXF0];
   int f_left[RMAXF0], f_mask[RMAXF0], f_f64[RMAXF0], f_cur2[RMAXF0], f_conv[RMAXF0], f_conv2[RMAXF0];
@@ -206,60 +271,18 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
   const void* k_ptr = pick(L.b.col, kattr);
   const uint8_t* k_nul = pick(L.b.nul, kattr);
   const int k_w = pick(L.b.width, kattr);
-
-  // ---- initial deque: persisted (window reaches the batch start) or empty (warm-up replay) ----
-  int64_t w0 = 0;
-  if (W.chunk > 0 && !FULL) w0 = lower_bound_ts(L.b.ts, W.c0, L.b.ts[W.c0 - 1] - wmax, lane);
-  int n = 0, bot = 0;
-  if (w0 == 0) {
-    const size_t gb = (size_t)W.g * RSMAX * WAVE;
-    n = pick(L.st, W.inb)[W.g].n[lane];
-    const int64_t* __restrict__ i_ts = pick(L.ent_ts, W.inb);
-    const int64_t* __restrict__ i_sq = pick(L.ent_seq, W.inb);
-    const int64_t* __restrict__ i_ky = pick(L.ent_key, W.inb);
-    for (int i = 0; i < n; ++i) {
-      const size_t o = gb + (size_t)i * WAVE + lane;
-      const int64_t t0 = i_ts[o];
-      const int64_t sq = i_sq[o];
-      const int64_t ky = i_ky[o];
-      A[i * WAVE + lane] = make_uint4((uint32_t)t0, (uint32_t)((uint64_t)t0 >> 32), (uint32_t)ky,
-                                      (uint32_t)((uint64_t)ky >> 32));
-      B[i * WAVE + lane] = (uint32_t)sq;
-    }
-  }
-  // VGPR caches of the deque ends
-  uint64_t tkey = 0;
-  uint32_t tseq = 0, bseq = 0;
-  int64_t bts = 0;
-  if (n > 0) {
-    const uint4 t = A[((n - 1) & mask) * WAVE + lane];
-    tkey = (uint64_t)t.z | ((uint64_t)t.w << 32);
-    tseq = B[((n - 1) & mask) * WAVE + lane];
-    const uint4 b = A[lane];
-    bts = (int64_t)((uint64_t)b.x | ((uint64_t)b.y << 32));
-    bseq = B[lane];
-  }
-
-  int blk = -1, fill = 0;
-  bool overflow = false, unordered = false, mover = false, aged = false;
-  int64_t prev_tile_ts = (w0 == 0) ? L.b.prev_ts : L.b.ts[w0 - 1];
   const int64_t seq_base = L.b.seq_base;
-  const int RW = 4;
 
-  for (int64_t t = w0; t < W.c1; t += WAVE) {
-    // ---- stage 64 events (lane = event): ts, x-atom key, f0 column keys, validity bits ----
-    const int64_t e = t + lane;
-    const bool live = e < W.c1;
-    const int64_t ets = live ? L.b.ts[e] : INT64_MAX;
-    uint64_t xk = 0;
+  // stage one event per lane: ts, x-atom key, f0 operand keys, validity bits
+  int64_t fk[RMAXF0], fk2[RMAXF0];
+  auto stage = [&](int64_t e, bool live, int64_t& ets, U& xk, uint32_t& vbits) {
+    ets = live ? L.b.ts[e] : INT64_MAX;
     bool xok = false;
+    xk = 0;
     if (live) {
-      const uint64_t raw = load_raw(k_ptr, k_w, e);
       const bool nl = k_nul && k_nul[e];
-      xk = stage_key<KK>(raw, kconv, nl, xok);
+      xk = (U)stage_key<KK>(load_raw(k_ptr, k_w, e), kconv, nl, xok);
     }
-    // f0 operand keys, one per atom (lane = event)
-    int64_t fk[RMAXF0], fk2[RMAXF0];
     uint32_t fnul = 0;
 #pragma unroll
     for (int a = 0; a < RMAXF0; ++a) {
@@ -275,7 +298,183 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
         if (nl) fnul |= 1u << a;
       }
     }
-    const uint32_t vbits = (xok ? 1u : 0u) | (fnul << 1);
+    vbits = (xok ? 1u : 0u) | (fnul << 1);
+  };
+  // f0 of this lane's pattern on staged event k (x-atom key validity checked by the caller)
+  auto f0_pass = [&](int k, uint32_t vb) {
+    bool ok = active;
+#pragma unroll
+    for (int a = 0; a < RMAXF0; ++a) {
+      if (a < n_f0) {
+        const int64_t cv = readlane64(fk[a], k);
+        const bool cn = (vb >> (1 + a)) & 1u;
+        bool r;
+        if (f_cur2[a]) {
+          r = !cn && cmp_keys(f_mask[a], f_f64[a], cv, readlane64(fk2[a], k));
+        } else {
+          r = !cn && (f_left[a] ? cmp_keys(f_mask[a], f_f64[a], cv, f0c[a])
+                                : cmp_keys(f_mask[a], f_f64[a], f0c[a], cv));
+        }
+        ok = ok && r;
+      }
+    }
+    return ok;
+  };
+
+  int n = 0, bot = 0;
+  bool overflow = false, unordered = false, mover = false, aged = false;
+  // persisted deques of the group (pending partials at the start of the batch), oldest first
+  const size_t gb = (size_t)W.g * RSMAX * WAVE;
+  const int n_in = pick(L.st, W.inb)[W.g].n[lane];
+  const int64_t* __restrict__ i_ts = pick(L.ent_ts, W.inb);
+  const int64_t* __restrict__ i_sq = pick(L.ent_seq, W.inb);
+  const int64_t* __restrict__ i_ky = pick(L.ent_key, W.inb);
+
+  if (W.c0 == 0) {
+    // ---- first chunk: start from the persisted deques ----
+    for (int i = 0; i < n_in; ++i) {
+      const size_t o = gb + (size_t)i * WAVE + lane;
+      if (i < M) R.put(i, i_ts[o], (U)i_ky[o], (uint32_t)i_sq[o]);
+    }
+    n = n_in;
+    if (n > M) { overflow = true; n = M; }
+  } else {
+    // ---- later chunk: rebuild the pending partials at c0 by a REVERSE scan (exact, O(1) per
+    // event, no LDS traffic): partial i (f0 passed, valid key k_i) is still pending before event
+    // c0 iff it is not expired at c0-1 and no valid x_j, i < j < c0, satisfies `x_j OP k_i`,
+    // i.e. iff the max (for >, >=) / min (for <, <=) of those x_j does not. Partials older than
+    // w0 = lower_bound(ts, ts[c0-1] - wmax) are expired by c0-1 (timestamps non-decreasing,
+    // verified on every event read).
+    const int64_t t_last = L.b.ts[W.c0 - 1];
+    const int64_t w0 = has_within ? lower_bound_ts(L.b.ts, W.c0, t_last - wmax, lane) : 0;
+    bool r_has = false;  // reduction of the valid x over (current tile end, c0)
+    U r_val = 0;
+    int64_t next_first_ts = t_last;  // ts of the first event of the tile after the current one
+    for (int64_t hi = W.c0; hi > w0; hi -= WAVE) {
+      const int64_t lo = hi - WAVE;
+      const int64_t e = lo + lane;
+      const bool live = e >= w0;
+      int64_t ets;
+      U xk;
+      uint32_t vb;
+      stage(e, live, ets, xk, vb);
+      // monotone timestamps inside the tile and across the tile boundary
+      const int64_t nxt = __shfl_down(ets, 1, WAVE);
+      if (live && ets > (lane == WAVE - 1 ? next_first_ts : nxt)) unordered = true;
+      if (live && e == 0 && L.b.prev_ts > ets) unordered = true;
+      const int fl = (int)(lo < w0 ? w0 - lo : 0);
+      next_first_ts = readlane64(ets, fl);
+      // inclusive suffix reduction over lanes (events) of this tile
+      bool vh = (vb & 1u) != 0;
+      U vv = xk;
+#pragma unroll
+      for (int d = 1; d < WAVE; d <<= 1) {
+        const U ov = shdown(vv, d);
+        const bool oh = __shfl_down((int)vh, d, WAVE) != 0 && lane + d < WAVE;
+        const bool take = oh && (!vh || dominates<KK>(is_max, ov, vv));
+        vv = take ? ov : vv;
+        vh = vh || oh;
+      }
+      // exclusive: events after this one in the tile, then the later tiles
+      U sv = shdown(vv, 1);
+      bool sh = __shfl_down((int)vh, 1, WAVE) != 0 && lane + 1 < WAVE;
+      if (r_has && (!sh || dominates<KK>(is_max, r_val, sv))) sv = r_val;
+      sh = sh || r_has;
+      const bool cand = live && (vb & 1u) && !(sh && xcmp<KK>(xmask, sv, xk));
+      uint64_t cm = __ballot(cand);
+      while (cm) {  // newest candidate first: push at the front (bottom) of the deque
+        const int k = 63 - __builtin_clzll(cm);
+        cm &= ~(1ull << k);
+        const uint32_t vbk = __builtin_amdgcn_readlane(vb, k);
+        const int64_t tk = readlane64(ets, k);
+        const U xkk = rlane(xk, k);
+        const bool ok = f0_pass(k, vbk) && !expired(tk, t_last, within);
+        if (ok) {
+          if (n == M) {
+            overflow = true;
+          } else {
+            bot = (bot - 1) & mask;
+            R.put(bot, tk, xkk, (uint32_t)(seq_base + lo + k));
+            ++n;
+          }
+        }
+      }
+      // fold this tile into the running reduction
+      const U tv = rlane(vv, fl);
+      const bool th = __builtin_amdgcn_readlane((uint32_t)vh, fl) != 0;
+      if (th && (!r_has || dominates<KK>(is_max, tv, r_val))) r_val = tv;
+      r_has = r_has || th;
+    }
+    if (w0 == 0) {
+      // the window reaches the batch start: carried partials survive unless expired or matched
+      if (L.b.prev_ts > L.b.ts[0]) unordered = true;
+      for (int i = n_in - 1; i >= 0; --i) {
+        const size_t o = gb + (size_t)i * WAVE + lane;
+        const int64_t t0 = i_ts[o];
+        const U ky = (U)i_ky[o];
+        if (!expired(t0, t_last, within) && !(r_has && xcmp<KK>(xmask, r_val, ky))) {
+          if (n == M) {
+            overflow = true;
+          } else {
+            bot = (bot - 1) & mask;
+            R.put(bot, t0, ky, (uint32_t)i_sq[o]);
+            ++n;
+          }
+        }
+      }
+    }
+  }
+
+  // VGPR caches of the deque ends
+  U tkey = 0;
+  uint32_t tseq = 0, bseq = 0;
+  int64_t bts = 0;
+  if (n > 0) {
+    int64_t t0;
+    R.get((bot + n - 1) & mask, t0, tkey, tseq);
+    U k0;
+    R.get(bot, bts, k0, bseq);
+  }
+
+  int blk = -1, fill = 0;
+  int64_t prev_tile_ts = (W.c0 == 0) ? L.b.prev_ts : L.b.ts[W.c0 - 1];
+  const int RW = 4;
+
+  // emit one record per lane with `mt` (ballot m); per-wave output blocks, ranks by mbcnt
+  auto emit = [&](bool mt, uint64_t m, int64_t tt, int64_t s1, int64_t s) {
+    if (mover) return;
+    const int c = __popcll(m);
+    if (fill + c > L.blk_recs) {
+      if (blk >= 0 && lane == 0) L.blk_count[blk] = fill;
+      blk = -1;
+    }
+    if (blk < 0) {
+      int nb = 0;
+      if (lane == 0) nb = atomicAdd(L.blk_next, 1);
+      nb = __builtin_amdgcn_readfirstlane(nb);
+      if (nb >= L.n_blocks) {
+        mover = true;
+        return;
+      }
+      blk = nb;
+      fill = 0;
+    }
+    if (mt) {
+      int64_t* r = L.match + ((size_t)blk * L.blk_recs + fill + wave_mbcnt(m)) * RW;
+      reinterpret_cast<longlong2*>(r)[0] = make_longlong2(qid, tt);
+      reinterpret_cast<longlong2*>(r)[1] = make_longlong2(s1, s);
+    }
+    fill += c;
+  };
+
+  // ---- forward NFA step over the events this item emits for ----
+  for (int64_t t = W.c0; t < W.c1; t += WAVE) {
+    const int64_t e = t + lane;
+    const bool live = e < W.c1;
+    int64_t ets;
+    U xk;
+    uint32_t vbits;
+    stage(e, live, ets, xk, vbits);
     int64_t pred = __shfl_up(ets, 1, WAVE);
     if (lane == 0) pred = prev_tile_ts;
     if (live && ets < pred) unordered = true;
@@ -284,14 +483,11 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
     const int cnt = (int)((W.c1 - t) < WAVE ? (W.c1 - t) : WAVE);
 #pragma unroll 1
     for (int k = 0; k < cnt; ++k) {
-      const int64_t j = t + k;
-      const bool emit_ok = j >= W.c0;
       const int64_t tt = readlane64(ets, k);
-      const int64_t s = seq_base + j;
+      const int64_t s = seq_base + t + k;
       const uint32_t slo = (uint32_t)s;
       const uint32_t vb = __builtin_amdgcn_readlane(vbits, k);
-      const uint64_t x = (KK == KK_F32 || KK == KK_I32) ? (uint64_t)__builtin_amdgcn_readlane((uint32_t)xk, k)
-                                                         : (uint64_t)readlane64((int64_t)xk, k);
+      const U x = rlane(xk, k);
       const bool x_ok = vb & 1u;
 
       // ---- 1. lazy `within` expiry (oldest first) ----
@@ -304,9 +500,8 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
               bot = (bot + 1) & mask;
               --n;
               if (n > 0) {
-                const uint4 b = A[bot * WAVE + lane];
-                bts = (int64_t)((uint64_t)b.x | ((uint64_t)b.y << 32));
-                bseq = B[bot * WAVE + lane];
+                U k0;
+                R.get(bot, bts, k0, bseq);
               }
             }
           }
@@ -315,100 +510,78 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
           int w = 0;
           for (int i = 0; i < n; ++i) {
             const int si = (bot + i) & mask;
-            const uint4 a = A[si * WAVE + lane];
-            const int64_t t0 = (int64_t)((uint64_t)a.x | ((uint64_t)a.y << 32));
+            int64_t t0;
+            U ky;
+            uint32_t sq;
+            R.get(si, t0, ky, sq);
             if (!expired(t0, tt, within)) {
-              const int di = (bot + w) & mask;
-              if (di != si) {
-                A[di * WAVE + lane] = a;
-                B[di * WAVE + lane] = B[si * WAVE + lane];
-              }
+              if (w != i) R.put((bot + w) & mask, t0, ky, sq);
               ++w;
             }
           }
-          n = w;
-          if (n > 0) {
-            const uint4 b = A[bot * WAVE + lane];
-            bts = (int64_t)((uint64_t)b.x | ((uint64_t)b.y << 32));
-            bseq = B[bot * WAVE + lane];
-            const int ti = (bot + n - 1) & mask;
-            const uint4 tp = A[ti * WAVE + lane];
-            tkey = (uint64_t)tp.z | ((uint64_t)tp.w << 32);
-            tseq = B[ti * WAVE + lane];
+          if (w != n) {
+            n = w;
+            if (n > 0) {
+              int64_t t0;
+              R.get((bot + n - 1) & mask, t0, tkey, tseq);
+              U k0;
+              R.get(bot, bts, k0, bseq);
+            }
           }
         }
       }
       // sequence numbers are kept as their low 32 bits: a live partial must be < 2^31 events old
       if (n > 0 && (slo - bseq) >= 0x80000000u) aged = true;
 
-      // ---- 2. matches: the newest partials whose key satisfies `cur OP key` ----
+      // ---- 2. matches: the newest partials whose key satisfies `cur OP key`; up to four pops
+      //         per LDS round trip (the three entries under the top are fetched together) ----
       while (true) {
         const bool mt = x_ok && n > 0 && xcmp<KK>(xmask, x, tkey);
-        const uint64_t m = __ballot(mt);
-        if (m == 0) break;
-        if (emit_ok && !mover) {
-          const int c = __popcll(m);
-          if (fill + c > L.blk_recs) {
-            if (blk >= 0 && lane == 0) L.blk_count[blk] = fill;
-            blk = -1;
-          }
-          if (blk < 0) {
-            int nb = 0;
-            if (lane == 0) nb = atomicAdd(L.blk_next, 1);
-            nb = __builtin_amdgcn_readfirstlane(nb);
-            if (nb >= L.n_blocks) {
-              mover = true;
-            } else {
-              blk = nb;
-              fill = 0;
+        if (__ballot(mt) == 0) break;
+        U k1 = 0, k2 = 0, k3 = 0;
+        uint32_t q1 = 0, q2 = 0, q3 = 0;
+        int64_t tdummy;
+        const int top = bot + n - 1;
+        if (mt && n > 1) R.get((top - 1) & mask, tdummy, k1, q1);
+        if (mt && n > 2) R.get((top - 2) & mask, tdummy, k2, q2);
+        if (mt && n > 3) R.get((top - 3) & mask, tdummy, k3, q3);
+        int p = 0;
+        if (mt) {
+          p = 1;
+          if (n > 1 && xcmp<KK>(xmask, x, k1)) {
+            p = 2;
+            if (n > 2 && xcmp<KK>(xmask, x, k2)) {
+              p = 3;
+              if (n > 3 && xcmp<KK>(xmask, x, k3)) p = 4;
             }
-          }
-          if (!mover) {
-            if (mt) {
-              const int64_t s1 = s - (int64_t)(uint32_t)(slo - tseq);
-              int64_t* r = L.match + ((size_t)blk * L.blk_recs + fill + wave_mbcnt(m)) * RW;
-              reinterpret_cast<longlong2*>(r)[0] = make_longlong2(qid, tt);
-              reinterpret_cast<longlong2*>(r)[1] = make_longlong2(s1, s);
-            }
-            fill += c;
           }
         }
+        const uint32_t qs[4] = {tseq, q1, q2, q3};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool mj = p > j;
+          const uint64_t m = __ballot(mj);
+          if (m == 0) break;
+          const int64_t s1 = s - (int64_t)(uint32_t)(slo - qs[j]);
+          emit(mj, m, tt, s1, s);
+        }
         if (mt) {
-          --n;
+          n -= p;
           if (n > 0) {
-            const int ti = (bot + n - 1) & mask;
-            const uint4 tp = A[ti * WAVE + lane];
-            tkey = (uint64_t)tp.z | ((uint64_t)tp.w << 32);
-            tseq = B[ti * WAVE + lane];
+            if (p == 1) { tkey = k1; tseq = q1; }
+            else if (p == 2) { tkey = k2; tseq = q2; }
+            else if (p == 3) { tkey = k3; tseq = q3; }
+            else R.get((top - 4) & mask, tdummy, tkey, tseq);
           }
         }
       }
 
       // ---- 3. start state: every event passing f0 opens a partial (pending from j+1) ----
-      bool f0ok = active && x_ok;
-#pragma unroll
-      for (int a = 0; a < RMAXF0; ++a) {
-        if (a < n_f0) {
-          const int64_t cv = readlane64(fk[a], k);
-          const bool cn = (vb >> (1 + a)) & 1u;
-          bool ok;
-          if (f_cur2[a]) {
-            ok = !cn && cmp_keys(f_mask[a], f_f64[a], cv, readlane64(fk2[a], k));
-          } else {
-            ok = !cn && (f_left[a] ? cmp_keys(f_mask[a], f_f64[a], cv, f0c[a])
-                                   : cmp_keys(f_mask[a], f_f64[a], f0c[a], cv));
-          }
-          f0ok = f0ok && ok;
-        }
-      }
-      if (f0ok) {
+      if (x_ok && f0_pass(k, vb)) {
         if (n == M) {
           overflow = true;
         } else {
-          const int ti = (bot + n) & mask;
-          A[ti * WAVE + lane] = make_uint4((uint32_t)tt, (uint32_t)((uint64_t)tt >> 32), (uint32_t)x,
-                                           (uint32_t)(x >> 32));
-          B[ti * WAVE + lane] = slo;
+          R.put((bot + n) & mask, tt, x, slo);
           if (n == 0) {
             bts = tt;
             bseq = slo;
@@ -432,19 +605,20 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
   }
   if (W.chunk == W.n_chunks - 1) {  // the last chunk owns the group's final deques
     const int ob = 1 - W.inb;
-    const size_t gb = (size_t)W.g * RSMAX * WAVE;
     const int64_t slast = seq_base + W.c1 - 1;
     const uint32_t llo = (uint32_t)slast;
     int64_t* __restrict__ o_ts = pick(L.ent_ts, ob);
     int64_t* __restrict__ o_sq = pick(L.ent_seq, ob);
     int64_t* __restrict__ o_ky = pick(L.ent_key, ob);
     for (int i = 0; i < n; ++i) {
-      const int si = (bot + i) & mask;
-      const uint4 a = A[si * WAVE + lane];
+      int64_t t0;
+      U ky;
+      uint32_t sq;
+      R.get((bot + i) & mask, t0, ky, sq);
       const size_t o = gb + (size_t)i * WAVE + lane;
-      o_ts[o] = (int64_t)((uint64_t)a.x | ((uint64_t)a.y << 32));
-      o_ky[o] = (int64_t)((uint64_t)a.z | ((uint64_t)a.w << 32));
-      o_sq[o] = slast - (int64_t)(uint32_t)(llo - B[si * WAVE + lane]);
+      o_ts[o] = t0;
+      o_ky[o] = (int64_t)(uint64_t)ky;
+      o_sq[o] = slast - (int64_t)(uint32_t)(llo - sq);
     }
     pick(L.st, ob)[W.g].n[lane] = n;
   }
@@ -454,7 +628,8 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
 
 template <int KK>
 static hipError_t launch_kk(bool full, const sdh::RatchetLaunch* L, int M, hipStream_t s) {
-  const size_t lds = (size_t)M * 64 * (sizeof(uint4) + sizeof(uint32_t));
+  const bool w64 = (KK == sdh::KK_F64 || KK == sdh::KK_I64);
+  const size_t lds = (size_t)M * 64 * (sizeof(uint4) + (w64 ? sizeof(uint32_t) : 0));
   if (full)
     hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, true>), dim3(L->n_items), dim3(64), lds, s, *L, M);
   else
