@@ -21,8 +21,8 @@
 
 extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaunch* L, int n_blocks,
                                        size_t lds, hipStream_t s);
-extern "C" hipError_t sdh_launch_ratchet(int key_kind, int full, int M, const sdh::RatchetLaunch* L,
-                                         hipStream_t s);
+extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int ML, int SC,
+                                         const sdh::RatchetLaunch* L, hipStream_t s);
 extern "C" hipError_t sdh_launch_compact(const int64_t* src, const int64_t* seg_off,
                                          const int64_t* seg_count, const int64_t* dst_off,
                                          int rec_words, int n_items, int64_t* dst, hipStream_t s);
@@ -411,11 +411,13 @@ RatchetPlan ratchet_plan(const ChainQuery& c) {
   }
   if (c.cap_col[0] != cur_col) return r;  // key = e1 value of the same column and conversion
   const int conv = c.col_conv[cur_col];
+  // both operands are the same column with the same conversion: a float column compared in
+  // binary64 orders exactly as in binary32, an int column as int32 (32-bit ring entries)
   switch (conv) {
-    case CV_F32_INT: case CV_F32_LONG: case CV_F32_FLOAT: r.key_kind = KK_F32; break;
-    case CV_I64_INT: r.key_kind = X.f64 ? -1 : KK_I32; break;
+    case CV_F32_INT: case CV_F32_LONG: case CV_F32_FLOAT: case CV_F64_FLOAT: r.key_kind = KK_F32; break;
+    case CV_I64_INT: case CV_F64_INT: r.key_kind = KK_I32; break;
     case CV_I64_LONG: r.key_kind = KK_I64; break;
-    case CV_F64_INT: case CV_F64_LONG: case CV_F64_FLOAT: case CV_F64_DOUBLE: r.key_kind = KK_F64; break;
+    case CV_F64_LONG: case CV_F64_DOUBLE: r.key_kind = KK_F64; break;
     default: return r;
   }
   if (r.key_kind < 0) return r;
@@ -510,7 +512,10 @@ struct sdh_engine {
   int r_blk_recs = 8192;
   int r_blocks_used = 0;             // of the last launch
   std::vector<int32_t> r_blk_count;
-  int rM = 32;                       // LDS deque capacity per lane (power of two <= RSMAX)
+  int rML = 16;                      // LDS ring entries per lane (power of two)
+  int rSC = 256;                     // global spill ring entries per lane (power of two)
+  DevBuf<uint4> d_rspillA;
+  DevBuf<uint32_t> d_rspillB;
   std::vector<char> r_full_expiry;   // per stream: timestamps were seen out of order
   int64_t r_matches = 0;
   double r_kernel_ms = 0, r_kernel_bytes = 0;
@@ -774,7 +779,11 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
   }
   (void)t01;
   for (int attempt = 0; attempt < 8; ++attempt) {
-    const bool full = e->r_full_expiry[stream] != 0;
+    // out-of-order timestamps seen on this stream, or timestamps so extreme that `ts0 + within`
+    // could wrap: exact per-entry expiry scan, no chunking
+    const int64_t lim = (int64_t)1 << 61;
+    const bool full = e->r_full_expiry[stream] != 0 || t01[0] < -lim || t01[0] > lim || t01[1] < -lim ||
+                      t01[1] > lim || (B.prev_ts != INT64_MIN && (B.prev_ts < -lim || B.prev_ts > lim));
     // ---- chunk planning: chunk c > 0 rebuilds its starting deques by a reverse scan of the
     // `within` window (a few instructions per 64 events), so chunks can be short: aim for
     // ~4096 waves (16 per CU) of at least min_chunk emitted events each ----
@@ -782,22 +791,23 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : 2048;
     const double len = std::max((double)min_chunk, (double)n * gs.size() / target_waves);
     e->ritems.clear();
-    for (int kk = 0; kk < 4; ++kk) {
-      for (int g : gs) {
-        const RatchetGroup& G = e->rg[g];
-        if (G.key_kind != kk) continue;
-        int64_t C = 1;
-        if (!full && G.wmax >= 0) C = std::max<int64_t>(1, (int64_t)std::ceil((double)n / len));
-        for (int64_t ch = 0; ch < C; ++ch) {
-          RatchetItem it{};
-          it.g = g;
-          it.chunk = (int)ch;
-          it.n_chunks = (int)C;
-          it.inb = e->rcur[g];
-          it.c0 = n * ch / C;
-          it.c1 = n * (ch + 1) / C;
-          e->ritems.push_back(it);
-        }
+    std::vector<int> order(gs);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+      return std::make_pair(e->rg[a].key_kind, e->rg[a].xmask) < std::make_pair(e->rg[b].key_kind, e->rg[b].xmask);
+    });
+    for (int g : order) {
+      const RatchetGroup& G = e->rg[g];
+      int64_t C = 1;
+      if (!full && G.wmax >= 0) C = std::max<int64_t>(1, (int64_t)std::ceil((double)n / len));
+      for (int64_t ch = 0; ch < C; ++ch) {
+        RatchetItem it{};
+        it.g = g;
+        it.chunk = (int)ch;
+        it.n_chunks = (int)C;
+        it.inb = e->rcur[g];
+        it.c0 = n * ch / C;
+        it.c1 = n * (ch + 1) / C;
+        e->ritems.push_back(it);
       }
     }
     const int n_items = (int)e->ritems.size();
@@ -805,6 +815,10 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     HIPCHK(hipMemcpyAsync(e->d_ritems.p, e->ritems.data(), n_items * sizeof(RatchetItem),
                           hipMemcpyHostToDevice, e->stream));
     e->d_rmatch.ensure((size_t)e->r_blocks * e->r_blk_recs * 4);
+    e->d_rspillA.ensure((size_t)n_items * e->rSC * WAVE);
+    bool any64 = false;
+    for (int g : gs) any64 |= e->rg[g].key_kind == KK_F64 || e->rg[g].key_kind == KK_I64;
+    if (any64) e->d_rspillB.ensure((size_t)n_items * e->rSC * WAVE);
     e->d_blk_count.ensure((size_t)e->r_blocks);
     e->d_err.ensure(4);
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
@@ -819,6 +833,8 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       L.ent_seq[b] = e->d_rsq[b].p;
       L.ent_key[b] = e->d_rky[b].p;
     }
+    L.spillA = e->d_rspillA.p;
+    L.spillB = e->d_rspillB.p;
     L.match = e->d_rmatch.p;
     L.blk_count = e->d_blk_count.p;
     L.blk_next = e->d_blk_next.p;
@@ -827,13 +843,16 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.err = e->d_err.p;
     HIPCHK(hipEventRecord(e->ev0, e->stream));
     for (int i0 = 0; i0 < n_items;) {
-      const int kk = e->rg[e->ritems[i0].g].key_kind;
+      const int kk = e->rg[e->ritems[i0].g].key_kind, xm = e->rg[e->ritems[i0].g].xmask;
       int i1 = i0;
-      while (i1 < n_items && e->rg[e->ritems[i1].g].key_kind == kk) ++i1;
+      while (i1 < n_items && e->rg[e->ritems[i1].g].key_kind == kk && e->rg[e->ritems[i1].g].xmask == xm) ++i1;
       RatchetLaunch Ls = L;
       Ls.items = e->d_ritems.p + i0;
       Ls.n_items = i1 - i0;
-      HIPCHK(sdh_launch_ratchet(kk, full, e->rM, &Ls, e->stream));
+      // spill regions are indexed by the item's position in its launch
+      Ls.spillA = e->d_rspillA.p + (size_t)i0 * e->rSC * WAVE;
+      Ls.spillB = any64 ? e->d_rspillB.p + (size_t)i0 * e->rSC * WAVE : nullptr;
+      HIPCHK(sdh_launch_ratchet(kk, xm, full, e->rML, e->rSC, &Ls, e->stream));
       i0 = i1;
     }
     HIPCHK(hipEventRecord(e->ev1, e->stream));
@@ -849,8 +868,9 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       continue;
     }
     if (errs[0]) {
-      if (e->rM >= RSMAX) throw Error(SDH_E_CAPACITY, "ratchet deque overflow (more than 128 pending partials)");
-      e->rM *= 2;
+      if (e->rML + 2 * e->rSC > RSMAX)
+        throw Error(SDH_E_CAPACITY, fmt("more than %d pending partials in one pattern", e->rML + e->rSC));
+      e->rSC *= 2;  // exact re-run with a larger spill ring
       continue;
     }
     if (errs[2]) {

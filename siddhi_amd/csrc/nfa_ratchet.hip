@@ -192,57 +192,216 @@ __device__ __forceinline__ U shdown(U v, int d) {
   }
 }
 
-// `a` dominates `b` for the reduction of the x-atom's current-event values: max for `>`/`>=`,
-// min for `<`/`<=` (keys are valid: no NaN)
-template <int KK>
-__device__ __forceinline__ bool dominates(bool is_max, uint64_t a, uint64_t b) {
-  return xcmp<KK>(is_max ? CM_GT : CM_LT, a, b);
+// x-atom compare `cur OP key` with the normalized operator known at compile time (XM >= 0) or at
+// run time (XM < 0: FULL-expiry kernels). Keys are valid (no NaN).
+template <int KK, int XM>
+__device__ __forceinline__ bool xop(int xmask, uint64_t cur, uint64_t key) {
+  if constexpr (XM < 0) {
+    return xcmp<KK>(xmask, cur, key);
+  } else {
+    constexpr int m = XM == 0 ? CM_GT : XM == 1 ? (CM_GT | CM_EQ) : XM == 2 ? CM_LT : (CM_LT | CM_EQ);
+    if constexpr (KK == KK_F32) {
+      const float a = __uint_as_float((uint32_t)cur), b = __uint_as_float((uint32_t)key);
+      return m == CM_GT ? a > b : m == (CM_GT | CM_EQ) ? a >= b : m == CM_LT ? a < b : a <= b;
+    } else if constexpr (KK == KK_I32) {
+      const int32_t a = (int32_t)(uint32_t)cur, b = (int32_t)(uint32_t)key;
+      return m == CM_GT ? a > b : m == (CM_GT | CM_EQ) ? a >= b : m == CM_LT ? a < b : a <= b;
+    } else if constexpr (KK == KK_F64) {
+      const double a = __longlong_as_double((int64_t)cur), b = __longlong_as_double((int64_t)key);
+      return m == CM_GT ? a > b : m == (CM_GT | CM_EQ) ? a >= b : m == CM_LT ? a < b : a <= b;
+    } else {
+      const int64_t a = (int64_t)cur, b = (int64_t)key;
+      return m == CM_GT ? a > b : m == (CM_GT | CM_EQ) ? a >= b : m == CM_LT ? a < b : a <= b;
+    }
+  }
 }
 
-// LDS ring per lane; entry (slot e, lane l) at index e*64 + l.
+// order-preserving int64 image of a binary64 key: -0.0 and +0.0 map together, NaN to INT64_MIN
+__device__ __forceinline__ int64_t sortable_f64(int64_t b) {
+  const double d = __longlong_as_double(b);
+  if (d != d) return INT64_MIN;
+  if (d == 0.0) return 0;
+  return b >= 0 ? b : (b ^ INT64_MAX);
+}
+
+// f0 atom `cur OP c` (mask over the current-event operand; CM_NOT allowed with EQ only) as an
+// interval [lo, hi] of sortable keys, optionally complemented: pass = (lo <= v <= hi) ^ neg.
+// NaN operands (INT64_MIN) fall outside every non-complemented interval.
+__device__ __forceinline__ void f0_interval(int mask, bool f64, int64_t c, int64_t& lo, int64_t& hi, bool& neg) {
+  neg = (mask & CM_NOT) != 0;
+  const int m = mask & (CM_LT | CM_GT | CM_EQ);
+  const int64_t vmin = f64 ? INT64_MIN + 1 : INT64_MIN;
+  if (f64) {
+    const double d = __longlong_as_double(c);
+    if (d != d) {  // compares with NaN are false (!= true)
+      lo = 1;
+      hi = 0;
+      return;
+    }
+    c = sortable_f64(c);
+  }
+  lo = vmin;
+  hi = INT64_MAX;
+  const bool empty_lo = (m & CM_GT) && !(m & CM_EQ) && c == INT64_MAX;
+  const bool empty_hi = (m & CM_LT) && !(m & CM_EQ) && c == vmin;
+  if (m == CM_EQ) { lo = c; hi = c; }
+  else if (m == CM_GT) { lo = c + (c == INT64_MAX ? 0 : 1); }
+  else if (m == (CM_GT | CM_EQ)) { lo = c; }
+  else if (m == CM_LT) { hi = c - (c == vmin ? 0 : 1); }
+  else if (m == (CM_LT | CM_EQ)) { hi = c; }
+  if (empty_lo || empty_hi) { lo = 1; hi = 0; }
+}
+
+extern __shared__ uint4 ratchet_lds[];
+
+// One deque entry in LDS ([slot][lane]) or in the lane's global spill ring.
 //   32-bit keys: A = uint4 {ts0.lo, ts0.hi, key, seq}
 //   64-bit keys: A = uint4 {ts0.lo, ts0.hi, key.lo, key.hi}, B = uint32 seq
 // (seq = low 32 bits of e1's global sequence number; a live partial is < 2^31 events old)
 template <int KK>
-struct Ring {
-  using U = typename KT<KK>::U;
-  uint4* A;
-  uint32_t* B;
-  int lane;
-  __device__ __forceinline__ void put(int slot, int64_t ts, U key, uint32_t seq) const {
-    const int i = slot * WAVE + lane;
-    if constexpr (KT<KK>::W64) {
-      A[i] = make_uint4((uint32_t)ts, (uint32_t)((uint64_t)ts >> 32), (uint32_t)key, (uint32_t)(key >> 32));
-      B[i] = seq;
-    } else {
-      A[i] = make_uint4((uint32_t)ts, (uint32_t)((uint64_t)ts >> 32), key, seq);
-    }
+__device__ __forceinline__ uint4 pack_entry(int64_t ts, typename KT<KK>::U key, uint32_t seq) {
+  if constexpr (KT<KK>::W64)
+    return make_uint4((uint32_t)ts, (uint32_t)((uint64_t)ts >> 32), (uint32_t)key, (uint32_t)(key >> 32));
+  else
+    return make_uint4((uint32_t)ts, (uint32_t)((uint64_t)ts >> 32), key, seq);
+}
+
+template <int KK>
+__device__ __forceinline__ void unpack_entry(uint4 a, uint32_t b, int64_t& ts, typename KT<KK>::U& key, uint32_t& seq) {
+  ts = (int64_t)((uint64_t)a.x | ((uint64_t)a.y << 32));
+  if constexpr (KT<KK>::W64) {
+    key = (uint64_t)a.z | ((uint64_t)a.w << 32);
+    seq = b;
+  } else {
+    key = a.z;
+    seq = a.w;
   }
-  __device__ __forceinline__ void get(int slot, int64_t& ts, U& key, uint32_t& seq) const {
-    const int i = slot * WAVE + lane;
-    const uint4 a = A[i];
-    ts = (int64_t)((uint64_t)a.x | ((uint64_t)a.y << 32));
-    if constexpr (KT<KK>::W64) {
-      key = (uint64_t)a.z | ((uint64_t)a.w << 32);
-      seq = B[i];
-    } else {
-      key = a.z;
-      seq = a.w;
+}
+
+// Two-level per-lane deque: the newest ML entries in an LDS ring (ratchet_lds, [slot][lane]),
+// older ones in a global spill ring of SC entries (oldest first: spill, then LDS). Pops happen at
+// the newest end (LDS), expiry at the oldest end; the spill is touched only while a lane holds
+// more than ML pending partials.
+template <int KK>
+struct Deque {
+  using U = typename KT<KK>::U;
+  uint4* SA;
+  uint32_t* SB;
+  int lane, lmask, smask, ML, SC;
+  size_t sbase;  // (item * SC) * 64
+  int lbot = 0, ln = 0, sbot = 0, sn = 0;
+  __device__ __forceinline__ int li(int slot) const { return (slot & lmask) * WAVE + lane; }
+  __device__ __forceinline__ size_t si(int slot) const { return sbase + (size_t)(slot & smask) * WAVE + lane; }
+  __device__ __forceinline__ void lput(int i, int64_t ts, U key, uint32_t seq) const {
+    ratchet_lds[i] = pack_entry<KK>(ts, key, seq);
+    if constexpr (KT<KK>::W64) reinterpret_cast<uint32_t*>(&ratchet_lds[ML * WAVE])[i] = seq;
+  }
+  __device__ __forceinline__ void lget(int i, int64_t& ts, U& key, uint32_t& seq) const {
+    uint32_t b = 0;
+    if constexpr (KT<KK>::W64) b = reinterpret_cast<const uint32_t*>(&ratchet_lds[ML * WAVE])[i];
+    unpack_entry<KK>(ratchet_lds[i], b, ts, key, seq);
+  }
+  __device__ __forceinline__ void sput(size_t i, int64_t ts, U key, uint32_t seq) const {
+    SA[i] = pack_entry<KK>(ts, key, seq);
+    if constexpr (KT<KK>::W64) SB[i] = seq;
+  }
+  __device__ __forceinline__ void sget(size_t i, int64_t& ts, U& key, uint32_t& seq) const {
+    uint32_t b = 0;
+    if constexpr (KT<KK>::W64) b = SB[i];
+    unpack_entry<KK>(SA[i], b, ts, key, seq);
+  }
+  __device__ __forceinline__ int n() const { return ln + sn; }
+  // i-th entry counted from the oldest
+  __device__ __forceinline__ void at(int i, int64_t& ts, U& key, uint32_t& seq) const {
+    if (i < sn) sget(si(sbot + i), ts, key, seq);
+    else lget(li(lbot + i - sn), ts, key, seq);
+  }
+  __device__ __forceinline__ void top(int64_t& ts, U& key, uint32_t& seq) const { at(n() - 1, ts, key, seq); }
+  __device__ __forceinline__ void bottom(int64_t& ts, U& key, uint32_t& seq) const { at(0, ts, key, seq); }
+  // append the newest entry; returns false on overflow
+  __device__ __forceinline__ bool push_back(int64_t ts, U key, uint32_t seq) {
+    if (ln == ML) {
+      if (sn == SC) return false;
+      int64_t t0; U k0; uint32_t q0;
+      lget(li(lbot), t0, k0, q0);
+      sput(si(sbot + sn), t0, k0, q0);
+      ++sn;
+      lbot = (lbot + 1) & lmask;
+      --ln;
     }
+    lput(li(lbot + ln), ts, key, seq);
+    ++ln;
+    return true;
+  }
+  // prepend an entry older than all held ones (reverse-scan warm-up); false on overflow
+  __device__ __forceinline__ bool push_front(int64_t ts, U key, uint32_t seq) {
+    if (sn == 0 && ln < ML) {
+      lbot = (lbot - 1) & lmask;
+      lput(li(lbot), ts, key, seq);
+      ++ln;
+      return true;
+    }
+    if (sn == SC) return false;
+    sbot = (sbot - 1) & smask;
+    sput(si(sbot), ts, key, seq);
+    ++sn;
+    return true;
+  }
+  __device__ __forceinline__ void pop_back(int p) {  // p <= ln, or p == 1
+    if (ln > 0) ln -= p;
+    else sn -= p;
+  }
+  __device__ __forceinline__ void pop_front() {
+    if (sn > 0) { sbot = (sbot + 1) & smask; --sn; }
+    else { lbot = (lbot + 1) & lmask; --ln; }
+  }
+  // timestamps out of order: drop every expired entry, keeping the order of the rest
+  __device__ void compact_expired(int64_t tt, int64_t within) {
+    int w = 0;
+    for (int i = 0; i < sn; ++i) {
+      int64_t t0; U k; uint32_t q;
+      sget(si(sbot + i), t0, k, q);
+      if (!expired(t0, tt, within)) {
+        if (w != i) sput(si(sbot + w), t0, k, q);
+        ++w;
+      }
+    }
+    sn = w;
+    w = 0;
+    for (int i = 0; i < ln; ++i) {
+      int64_t t0; U k; uint32_t q;
+      lget(li(lbot + i), t0, k, q);
+      if (!expired(t0, tt, within)) {
+        if (w != i) lput(li(lbot + w), t0, k, q);
+        ++w;
+      }
+    }
+    ln = w;
   }
 };
 
-template <int KK, bool FULL>
-__global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M) {
+__device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {  // b >= 0
+  return a > INT64_MAX - b ? INT64_MAX : a + b;
+}
+
+template <int KK, int XM, bool FULL>
+__global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
   using U = typename KT<KK>::U;
-  extern __shared__ uint4 lds[];
+  constexpr bool W64 = KT<KK>::W64;
   const int lane = threadIdx.x;
   const int wid = blockIdx.x;
   if (wid >= L.n_items) return;
-  const Ring<KK> R{lds, reinterpret_cast<uint32_t*>(lds + (size_t)M * WAVE), lane};
   const RatchetItem W = L.items[wid];
   const RatchetGroup* __restrict__ G = L.groups + W.g;
-  const int mask = M - 1;
+  Deque<KK> D;
+  D.SA = L.spillA;
+  D.SB = L.spillB;
+  D.lane = lane;
+  D.ML = ML;
+  D.SC = SC;
+  D.lmask = ML - 1;
+  D.smask = SC - 1;
+  D.sbase = ((size_t)wid * SC) * WAVE;
   const bool active = lane < G->n_lanes;
   const int64_t qid = G->qid[lane & 63];
   const int64_t within = G->within[lane & 63];
@@ -251,9 +410,11 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
   const int n_f0 = G->n_f0;
   const int xmask = G->xmask, kconv = G->key_conv, kattr = G->key_attr;
   const bool is_max = (xmask & CM_GT) != 0;
-  // f0 atoms: per-lane constants; operand columns resolved once (wave-uniform)
-  int64_t f0c[RMAXF0];
-  int f_left[RMAXF0], f_mask[RMAXF0], f_f64[RMAXF0], f_cur2[RMAXF0], f_conv[RMAXF0], f_conv2[RMAXF0];
+  // f0 atoms: constant atoms become per-lane intervals of sortable keys; two-column atoms stay
+  // generic compares. Operand columns are resolved once (wave-uniform).
+  int64_t f_lo[RMAXF0], f_hi[RMAXF0];
+  bool f_neg[RMAXF0];
+  int f_mask[RMAXF0], f_f64[RMAXF0], f_cur2[RMAXF0], f_conv[RMAXF0], f_conv2[RMAXF0];
   int f_w[RMAXF0], f_w2[RMAXF0];
   const void* f_ptr[RMAXF0];
   const void* f_ptr2[RMAXF0];
@@ -261,10 +422,19 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
   const uint8_t* f_nul2[RMAXF0];
 #pragma unroll
   for (int a = 0; a < RMAXF0; ++a) {
-    f0c[a] = a < n_f0 ? G->f0c[a][lane & 63] : 0;
     const RatchetAtom A0 = G->f0[a];
-    f_left[a] = A0.cur_left; f_mask[a] = A0.mask; f_f64[a] = A0.f64; f_cur2[a] = A0.cur2;
-    f_conv[a] = A0.conv; f_conv2[a] = A0.conv2;
+    const int64_t c = a < n_f0 ? G->f0c[a][lane & 63] : 0;
+    int m = A0.mask;
+    if (!A0.cur_left && !A0.cur2) {  // `c OP cur` -> `cur OP' c`
+      const int lt = m & CM_LT, gt = m & CM_GT;
+      m = (m & (CM_EQ | CM_NOT)) | (lt ? CM_GT : 0) | (gt ? CM_LT : 0);
+    }
+    f_mask[a] = m;
+    f_f64[a] = A0.f64;
+    f_cur2[a] = A0.cur2;
+    f_conv[a] = A0.conv;
+    f_conv2[a] = A0.conv2;
+    f0_interval(m, A0.f64 != 0, c, f_lo[a], f_hi[a], f_neg[a]);
     f_ptr[a] = pick(L.b.col, A0.attr); f_w[a] = pick(L.b.width, A0.attr); f_nul[a] = pick(L.b.nul, A0.attr);
     f_ptr2[a] = pick(L.b.col, A0.attr2); f_w2[a] = pick(L.b.width, A0.attr2); f_nul2[a] = pick(L.b.nul, A0.attr2);
   }
@@ -273,7 +443,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
   const int k_w = pick(L.b.width, kattr);
   const int64_t seq_base = L.b.seq_base;
 
-  // stage one event per lane: ts, x-atom key, f0 operand keys, validity bits
+  // stage one event per lane: ts, x-atom key, f0 operand keys (sortable), validity bits
   int64_t fk[RMAXF0], fk2[RMAXF0];
   auto stage = [&](int64_t e, bool live, int64_t& ets, U& xk, uint32_t& vbits) {
     ets = live ? L.b.ts[e] : INT64_MAX;
@@ -289,39 +459,37 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
       fk[a] = 0;
       fk2[a] = 0;
       if (a < n_f0 && live) {
-        fk[a] = to_key(load_raw(f_ptr[a], f_w[a], e), f_conv[a]);
+        const int64_t k1 = to_key(load_raw(f_ptr[a], f_w[a], e), f_conv[a]);
         bool nl = f_nul[a] && f_nul[a][e];
         if (f_cur2[a]) {
+          fk[a] = k1;
           fk2[a] = to_key(load_raw(f_ptr2[a], f_w2[a], e), f_conv2[a]);
           nl = nl || (f_nul2[a] && f_nul2[a][e]);
+        } else {
+          fk[a] = f_f64[a] ? sortable_f64(k1) : k1;
         }
         if (nl) fnul |= 1u << a;
       }
     }
     vbits = (xok ? 1u : 0u) | (fnul << 1);
   };
-  // f0 of this lane's pattern on staged event k (x-atom key validity checked by the caller)
+  // f0 of this lane's pattern on staged event k
   auto f0_pass = [&](int k, uint32_t vb) {
-    bool ok = active;
+    bool ok = active && (vb & 1u);
 #pragma unroll
     for (int a = 0; a < RMAXF0; ++a) {
       if (a < n_f0) {
-        const int64_t cv = readlane64(fk[a], k);
+        const int64_t v = readlane64(fk[a], k);
         const bool cn = (vb >> (1 + a)) & 1u;
         bool r;
-        if (f_cur2[a]) {
-          r = !cn && cmp_keys(f_mask[a], f_f64[a], cv, readlane64(fk2[a], k));
-        } else {
-          r = !cn && (f_left[a] ? cmp_keys(f_mask[a], f_f64[a], cv, f0c[a])
-                                : cmp_keys(f_mask[a], f_f64[a], f0c[a], cv));
-        }
-        ok = ok && r;
+        if (f_cur2[a]) r = cmp_keys(f_mask[a], f_f64[a], v, readlane64(fk2[a], k));
+        else r = ((v >= f_lo[a]) && (v <= f_hi[a])) != f_neg[a];
+        ok = ok && !cn && r;
       }
     }
     return ok;
   };
 
-  int n = 0, bot = 0;
   bool overflow = false, unordered = false, mover = false, aged = false;
   // persisted deques of the group (pending partials at the start of the batch), oldest first
   const size_t gb = (size_t)W.g * RSMAX * WAVE;
@@ -334,22 +502,20 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
     // ---- first chunk: start from the persisted deques ----
     for (int i = 0; i < n_in; ++i) {
       const size_t o = gb + (size_t)i * WAVE + lane;
-      if (i < M) R.put(i, i_ts[o], (U)i_ky[o], (uint32_t)i_sq[o]);
+      if (!D.push_back(i_ts[o], (U)i_ky[o], (uint32_t)i_sq[o])) overflow = true;
     }
-    n = n_in;
-    if (n > M) { overflow = true; n = M; }
   } else {
     // ---- later chunk: rebuild the pending partials at c0 by a REVERSE scan (exact, O(1) per
-    // event, no LDS traffic): partial i (f0 passed, valid key k_i) is still pending before event
-    // c0 iff it is not expired at c0-1 and no valid x_j, i < j < c0, satisfies `x_j OP k_i`,
-    // i.e. iff the max (for >, >=) / min (for <, <=) of those x_j does not. Partials older than
-    // w0 = lower_bound(ts, ts[c0-1] - wmax) are expired by c0-1 (timestamps non-decreasing,
-    // verified on every event read).
+    // event): partial i (f0 passed, valid key k_i) is still pending before event c0 iff it is
+    // not expired at c0-1 and no valid x_j, i < j < c0, satisfies `x_j OP k_i` -- i.e. iff the
+    // max (for >, >=) / min (for <, <=) of those x_j does not. Partials older than
+    // w0 = lower_bound(ts, ts[c0-1] - wmax) are expired by c0-1 (timestamps non-decreasing:
+    // verified on every event the item reads; the host re-runs exactly otherwise).
     const int64_t t_last = L.b.ts[W.c0 - 1];
     const int64_t w0 = has_within ? lower_bound_ts(L.b.ts, W.c0, t_last - wmax, lane) : 0;
     bool r_has = false;  // reduction of the valid x over (current tile end, c0)
     U r_val = 0;
-    int64_t next_first_ts = t_last;  // ts of the first event of the tile after the current one
+    int64_t next_first_ts = t_last;
     for (int64_t hi = W.c0; hi > w0; hi -= WAVE) {
       const int64_t lo = hi - WAVE;
       const int64_t e = lo + lane;
@@ -358,51 +524,39 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
       U xk;
       uint32_t vb;
       stage(e, live, ets, xk, vb);
-      // monotone timestamps inside the tile and across the tile boundary
       const int64_t nxt = __shfl_down(ets, 1, WAVE);
       if (live && ets > (lane == WAVE - 1 ? next_first_ts : nxt)) unordered = true;
-      if (live && e == 0 && L.b.prev_ts > ets) unordered = true;
       const int fl = (int)(lo < w0 ? w0 - lo : 0);
       next_first_ts = readlane64(ets, fl);
-      // inclusive suffix reduction over lanes (events) of this tile
+      // inclusive suffix reduction over the tile's lanes (events)
       bool vh = (vb & 1u) != 0;
       U vv = xk;
 #pragma unroll
       for (int d = 1; d < WAVE; d <<= 1) {
         const U ov = shdown(vv, d);
         const bool oh = __shfl_down((int)vh, d, WAVE) != 0 && lane + d < WAVE;
-        const bool take = oh && (!vh || dominates<KK>(is_max, ov, vv));
+        const bool take = oh && (!vh || xcmp<KK>(is_max ? CM_GT : CM_LT, ov, vv));
         vv = take ? ov : vv;
         vh = vh || oh;
       }
-      // exclusive: events after this one in the tile, then the later tiles
       U sv = shdown(vv, 1);
       bool sh = __shfl_down((int)vh, 1, WAVE) != 0 && lane + 1 < WAVE;
-      if (r_has && (!sh || dominates<KK>(is_max, r_val, sv))) sv = r_val;
+      if (r_has && (!sh || xcmp<KK>(is_max ? CM_GT : CM_LT, r_val, sv))) sv = r_val;
       sh = sh || r_has;
-      const bool cand = live && (vb & 1u) && !(sh && xcmp<KK>(xmask, sv, xk));
+      const bool cand = live && (vb & 1u) && !(sh && xop<KK, XM>(xmask, sv, xk));
       uint64_t cm = __ballot(cand);
-      while (cm) {  // newest candidate first: push at the front (bottom) of the deque
+      while (cm) {  // newest candidate first: prepend
         const int k = 63 - __builtin_clzll(cm);
         cm &= ~(1ull << k);
         const uint32_t vbk = __builtin_amdgcn_readlane(vb, k);
         const int64_t tk = readlane64(ets, k);
         const U xkk = rlane(xk, k);
-        const bool ok = f0_pass(k, vbk) && !expired(tk, t_last, within);
-        if (ok) {
-          if (n == M) {
-            overflow = true;
-          } else {
-            bot = (bot - 1) & mask;
-            R.put(bot, tk, xkk, (uint32_t)(seq_base + lo + k));
-            ++n;
-          }
-        }
+        if (f0_pass(k, vbk) && !expired(tk, t_last, within))
+          if (!D.push_front(tk, xkk, (uint32_t)(seq_base + lo + k))) overflow = true;
       }
-      // fold this tile into the running reduction
       const U tv = rlane(vv, fl);
       const bool th = __builtin_amdgcn_readlane((uint32_t)vh, fl) != 0;
-      if (th && (!r_has || dominates<KK>(is_max, tv, r_val))) r_val = tv;
+      if (th && (!r_has || xcmp<KK>(is_max ? CM_GT : CM_LT, tv, r_val))) r_val = tv;
       r_has = r_has || th;
     }
     if (w0 == 0) {
@@ -412,35 +566,34 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
         const size_t o = gb + (size_t)i * WAVE + lane;
         const int64_t t0 = i_ts[o];
         const U ky = (U)i_ky[o];
-        if (!expired(t0, t_last, within) && !(r_has && xcmp<KK>(xmask, r_val, ky))) {
-          if (n == M) {
-            overflow = true;
-          } else {
-            bot = (bot - 1) & mask;
-            R.put(bot, t0, ky, (uint32_t)i_sq[o]);
-            ++n;
-          }
-        }
+        if (!expired(t0, t_last, within) && !(r_has && xop<KK, XM>(xmask, r_val, ky)))
+          if (!D.push_front(t0, ky, (uint32_t)i_sq[o])) overflow = true;
       }
     }
   }
 
-  // VGPR caches of the deque ends
+  // VGPR caches of the deque ends: top key/seq, bottom deadline/seq
   U tkey = 0;
   uint32_t tseq = 0, bseq = 0;
-  int64_t bts = 0;
-  if (n > 0) {
-    int64_t t0;
-    R.get((bot + n - 1) & mask, t0, tkey, tseq);
-    U k0;
-    R.get(bot, bts, k0, bseq);
-  }
+  int64_t bdead = INT64_MAX, bts = 0;
+  auto refresh_top = [&]() {
+    if (D.n() > 0) { int64_t t0; D.top(t0, tkey, tseq); }
+  };
+  auto refresh_bottom = [&]() {
+    if (D.n() > 0) {
+      U k0;
+      D.bottom(bts, k0, bseq);
+      bdead = sat_add(bts, within);
+    }
+  };
+  refresh_top();
+  refresh_bottom();
 
   int blk = -1, fill = 0;
   int64_t prev_tile_ts = (W.c0 == 0) ? L.b.prev_ts : L.b.ts[W.c0 - 1];
   const int RW = 4;
 
-  // emit one record per lane with `mt` (ballot m); per-wave output blocks, ranks by mbcnt
+  // emit one record per lane with `mt` (ballot m): per-wave output blocks, ranks by mbcnt
   auto emit = [&](bool mt, uint64_t m, int64_t tt, int64_t s1, int64_t s) {
     if (mover) return;
     const int c = __popcll(m);
@@ -492,67 +645,51 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
 
       // ---- 1. lazy `within` expiry (oldest first) ----
       if (has_within) {
-        if (!FULL) {
+        if constexpr (!FULL) {
+          // timestamps non-decreasing: expired(bts, tt) <=> tt > bts + within
           while (true) {
-            const bool ex = n > 0 && expired(bts, tt, within);
+            const bool ex = D.n() > 0 && tt > bdead;
             if (__ballot(ex) == 0) break;
             if (ex) {
-              bot = (bot + 1) & mask;
-              --n;
-              if (n > 0) {
-                U k0;
-                R.get(bot, bts, k0, bseq);
-              }
+              D.pop_front();
+              bdead = INT64_MAX;
+              refresh_bottom();
+              if (D.n() == 0) refresh_top();
             }
           }
         } else {
-          // timestamps out of order: the expired partials are no longer a prefix
-          int w = 0;
-          for (int i = 0; i < n; ++i) {
-            const int si = (bot + i) & mask;
-            int64_t t0;
-            U ky;
-            uint32_t sq;
-            R.get(si, t0, ky, sq);
-            if (!expired(t0, tt, within)) {
-              if (w != i) R.put((bot + w) & mask, t0, ky, sq);
-              ++w;
-            }
-          }
-          if (w != n) {
-            n = w;
-            if (n > 0) {
-              int64_t t0;
-              R.get((bot + n - 1) & mask, t0, tkey, tseq);
-              U k0;
-              R.get(bot, bts, k0, bseq);
-            }
+          const int n0 = D.n();
+          D.compact_expired(tt, within);
+          if (D.n() != n0) {
+            refresh_top();
+            refresh_bottom();
           }
         }
       }
       // sequence numbers are kept as their low 32 bits: a live partial must be < 2^31 events old
-      if (n > 0 && (slo - bseq) >= 0x80000000u) aged = true;
+      if (D.n() > 0 && (slo - bseq) >= 0x80000000u) aged = true;
 
       // ---- 2. matches: the newest partials whose key satisfies `cur OP key`; up to four pops
-      //         per LDS round trip (the three entries under the top are fetched together) ----
+      //         per LDS round trip (the three LDS entries under the top are fetched together) ----
       while (true) {
-        const bool mt = x_ok && n > 0 && xcmp<KK>(xmask, x, tkey);
+        const bool mt = x_ok && D.n() > 0 && xop<KK, XM>(xmask, x, tkey);
         if (__ballot(mt) == 0) break;
         U k1 = 0, k2 = 0, k3 = 0;
         uint32_t q1 = 0, q2 = 0, q3 = 0;
-        int64_t tdummy;
-        const int top = bot + n - 1;
-        if (mt && n > 1) R.get((top - 1) & mask, tdummy, k1, q1);
-        if (mt && n > 2) R.get((top - 2) & mask, tdummy, k2, q2);
-        if (mt && n > 3) R.get((top - 3) & mask, tdummy, k3, q3);
+        int64_t td;
+        const int ln = D.ln;
+        const int topl = D.lbot + ln - 1;
+        if (mt && ln > 1) D.lget(D.li(topl - 1), td, k1, q1);
+        if (mt && ln > 2) D.lget(D.li(topl - 2), td, k2, q2);
+        if (mt && ln > 3) D.lget(D.li(topl - 3), td, k3, q3);
         int p = 0;
         if (mt) {
           p = 1;
-          if (n > 1 && xcmp<KK>(xmask, x, k1)) {
+          if (ln > 1 && xop<KK, XM>(xmask, x, k1)) {
             p = 2;
-            if (n > 2 && xcmp<KK>(xmask, x, k2)) {
+            if (ln > 2 && xop<KK, XM>(xmask, x, k2)) {
               p = 3;
-              if (n > 3 && xcmp<KK>(xmask, x, k3)) p = 4;
+              if (ln > 3 && xop<KK, XM>(xmask, x, k3)) p = 4;
             }
           }
         }
@@ -562,33 +699,38 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
           const bool mj = p > j;
           const uint64_t m = __ballot(mj);
           if (m == 0) break;
-          const int64_t s1 = s - (int64_t)(uint32_t)(slo - qs[j]);
-          emit(mj, m, tt, s1, s);
+          emit(mj, m, tt, s - (int64_t)(uint32_t)(slo - qs[j]), s);
         }
         if (mt) {
-          n -= p;
-          if (n > 0) {
-            if (p == 1) { tkey = k1; tseq = q1; }
-            else if (p == 2) { tkey = k2; tseq = q2; }
-            else if (p == 3) { tkey = k3; tseq = q3; }
-            else R.get((top - 4) & mask, tdummy, tkey, tseq);
+          D.pop_back(p);
+          if (D.n() > 0) {
+            if (p < ln) {  // new top is an LDS entry; fetched above unless p == 4
+              if (p == 1) { tkey = k1; tseq = q1; }
+              else if (p == 2) { tkey = k2; tseq = q2; }
+              else if (p == 3) { tkey = k3; tseq = q3; }
+              else refresh_top();
+            } else {
+              refresh_top();
+            }
+          } else {
+            bdead = INT64_MAX;
           }
         }
       }
 
       // ---- 3. start state: every event passing f0 opens a partial (pending from j+1) ----
-      if (x_ok && f0_pass(k, vb)) {
-        if (n == M) {
+      if (f0_pass(k, vb)) {
+        const bool was_empty = D.n() == 0;
+        if (!D.push_back(tt, x, slo)) {
           overflow = true;
         } else {
-          R.put((bot + n) & mask, tt, x, slo);
-          if (n == 0) {
-            bts = tt;
-            bseq = slo;
-          }
-          ++n;
           tkey = x;
           tseq = slo;
+          if (was_empty) {
+            bts = tt;
+            bseq = slo;
+            bdead = sat_add(tt, within);
+          }
         }
       }
     }
@@ -610,11 +752,12 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
     int64_t* __restrict__ o_ts = pick(L.ent_ts, ob);
     int64_t* __restrict__ o_sq = pick(L.ent_seq, ob);
     int64_t* __restrict__ o_ky = pick(L.ent_key, ob);
+    const int n = D.n();
     for (int i = 0; i < n; ++i) {
       int64_t t0;
       U ky;
       uint32_t sq;
-      R.get((bot + i) & mask, t0, ky, sq);
+      D.at(i, t0, ky, sq);
       const size_t o = gb + (size_t)i * WAVE + lane;
       o_ts[o] = t0;
       o_ky[o] = (int64_t)(uint64_t)ky;
@@ -622,30 +765,44 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int M)
     }
     pick(L.st, ob)[W.g].n[lane] = n;
   }
+  (void)W64;
 }
 
 }  // namespace sdh
 
-template <int KK>
-static hipError_t launch_kk(bool full, const sdh::RatchetLaunch* L, int M, hipStream_t s) {
+template <int KK, int XM, bool FULL>
+static void launch_one(const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {
   const bool w64 = (KK == sdh::KK_F64 || KK == sdh::KK_I64);
-  const size_t lds = (size_t)M * 64 * (sizeof(uint4) + (w64 ? sizeof(uint32_t) : 0));
-  if (full)
-    hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, true>), dim3(L->n_items), dim3(64), lds, s, *L, M);
-  else
-    hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, false>), dim3(L->n_items), dim3(64), lds, s, *L, M);
+  const size_t lds = (size_t)ML * 64 * (sizeof(uint4) + (w64 ? sizeof(uint32_t) : 0));
+  hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL>), dim3(L->n_items), dim3(64), lds, s, *L, ML, SC);
+}
+
+template <int KK>
+static hipError_t launch_kk(int xm, bool full, const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {
+  if (full) {
+    launch_one<KK, -1, true>(L, ML, SC, s);
+  } else {
+    switch (xm) {
+      case 0: launch_one<KK, 0, false>(L, ML, SC, s); break;
+      case 1: launch_one<KK, 1, false>(L, ML, SC, s); break;
+      case 2: launch_one<KK, 2, false>(L, ML, SC, s); break;
+      default: launch_one<KK, 3, false>(L, ML, SC, s); break;
+    }
+  }
   return hipGetLastError();
 }
 
-extern "C" hipError_t sdh_launch_ratchet(int key_kind, int full, int M, const sdh::RatchetLaunch* L,
-                                         hipStream_t s) {
+// xmask: normalized `cur OP key` CmpMask of the launched groups (all equal); ML, SC powers of two
+extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int ML, int SC,
+                                         const sdh::RatchetLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
-  if (M < 1 || (M & (M - 1)) || M > sdh::RSMAX) return hipErrorInvalidValue;
+  if (ML < 4 || (ML & (ML - 1)) || SC < 1 || (SC & (SC - 1))) return hipErrorInvalidValue;
+  const int xm = xmask == sdh::CM_GT ? 0 : xmask == (sdh::CM_GT | sdh::CM_EQ) ? 1 : xmask == sdh::CM_LT ? 2 : 3;
   switch (key_kind) {
-    case sdh::KK_F32: return launch_kk<sdh::KK_F32>(full, L, M, s);
-    case sdh::KK_I32: return launch_kk<sdh::KK_I32>(full, L, M, s);
-    case sdh::KK_F64: return launch_kk<sdh::KK_F64>(full, L, M, s);
-    case sdh::KK_I64: return launch_kk<sdh::KK_I64>(full, L, M, s);
+    case sdh::KK_F32: return launch_kk<sdh::KK_F32>(xm, full, L, ML, SC, s);
+    case sdh::KK_I32: return launch_kk<sdh::KK_I32>(xm, full, L, ML, SC, s);
+    case sdh::KK_F64: return launch_kk<sdh::KK_F64>(xm, full, L, ML, SC, s);
+    case sdh::KK_I64: return launch_kk<sdh::KK_I64>(xm, full, L, ML, SC, s);
     default: return hipErrorInvalidValue;
   }
 }

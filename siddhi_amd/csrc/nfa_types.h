@@ -133,7 +133,7 @@ struct ChainLaunch {
 // monotone, so each event costs O(1) amortised: expire from the bottom, match from the top, push.
 // ------------------------------------------------------------------------------------------
 constexpr int RMAXF0 = 4;     // f0 atoms (event-only, per-lane constant operand)
-constexpr int RSMAX = 128;    // persisted deque capacity per lane (entries)
+constexpr int RSMAX = 512;    // persisted deque capacity per lane (>= LDS ring + spill ring)
 
 enum KeyKind { KK_F32 = 0, KK_I32, KK_F64, KK_I64 };
 
@@ -182,6 +182,8 @@ struct RatchetLaunch {
   int64_t* ent_ts[2];           // [g][RSMAX][64] ts0
   int64_t* ent_seq[2];          // [g][RSMAX][64] e1 sequence number
   int64_t* ent_key[2];          // [g][RSMAX][64] key (32-bit kinds in the low word)
+  uint4* spillA;                // [item][SC][64] deque entries beyond the LDS ring
+  uint32_t* spillB;             //   (seq words of 64-bit-key entries)
   int64_t* match;               // blocks of blk_recs records x 4 int64 (qid, ts, seq1, seq2)
   int32_t* blk_count;           // records written per block
   int32_t* blk_next;            // [0] next free block

@@ -126,17 +126,17 @@ def test_deque_growth_and_overflow_is_loud():
     src = "define stream S (v int); @info(name='q') from every e1=S -> e2=S[v > e1.v] select e1.v as a insert into O;"
     o = App(src)
     g = hip_app(src)
-    # strictly decreasing values pile up 100 pending partials (deque grows 32 -> 64 -> 128) ...
+    # strictly decreasing values pile up 100 pending partials (LDS ring of 16 + global spill) ...
     ts = np.arange(101, dtype=np.int64)
     v = np.concatenate([np.arange(100, 0, -1), [1000]]).astype(np.int32)
     o.engine.send(0, ts, v.astype(np.int64)[:, None], None)
     g.engine.push_columns(0, ts, [v])
     got = g.engine.take_matches(lambda q: 2)
     assert got == o.engine.take_matches(lambda q: 2) and len(got) == 100
-    # ... and more than 128 is a loud SDH_E_CAPACITY, never a wrong answer
-    ts2 = np.arange(101, 301, dtype=np.int64)
+    # ... and more than the ring + spill capacity (272) is a loud SDH_E_CAPACITY, never a wrong answer
+    ts2 = np.arange(101, 401, dtype=np.int64)
     with pytest.raises(EngineError) as ei:
-        g.engine.push_columns(0, ts2, [np.arange(200, 0, -1).astype(np.int32)])
+        g.engine.push_columns(0, ts2, [np.arange(300, 0, -1).astype(np.int32)])
     assert ei.value.code == -4
 
 
