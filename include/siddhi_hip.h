@@ -52,6 +52,13 @@ typedef struct sdh_config {
   int64_t match_capacity;    /* max matches held between polls (0 = sized automatically)     */
   int32_t chunk_events;      /* target events per parallel chunk (0 = automatic)             */
   int32_t flags;             /* SDH_FLAG_*                                                   */
+  /* K_gen (general interpreter) pools per query instance (0 = defaults 64 / 128 / 48) and the
+   * partition key capacity (0 = 2^20 keys per partition)                                     */
+  int32_t gen_pool_states;   /* StateEvent objects (<= 64)                                   */
+  int32_t gen_pool_nodes;    /* chained event copies (<= 256)                                */
+  int32_t gen_list_cap;      /* entries per pending / newAndEvery list                       */
+  int32_t gen_pad;
+  int64_t gen_max_keys;      /* distinct partition keys per partition                        */
 } sdh_config;
 
 /* Matches of a push that are not polled before the next push are dropped instead of being copied
@@ -61,6 +68,9 @@ typedef struct sdh_config {
 /* Disable the K_ratchet plan (every query of that shape runs on the general chain kernel instead);
  * for differential testing of the two plans. */
 #define SDH_FLAG_NO_RATCHET 2
+/* Run every query on the general interpreter K_gen (no chain / ratchet plans); for differential
+ * testing. */
+#define SDH_FLAG_FORCE_GEN 4
 
 /* One columnar (SoA) batch of events of one stream, in arrival order.
  * cols[a] points to n elements of attribute a with the stream schema's native width:

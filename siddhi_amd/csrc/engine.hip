@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <memory>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -17,7 +18,17 @@
 #include <vector>
 
 #include "../../include/siddhi_hip.h"
+#include "gen_lower.h"
 #include "nfa_types.h"
+
+extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s);
+extern "C" hipError_t sdh_route_partition(const sdh::StreamBatch* B, int attr, int type, unsigned long long* tkey,
+                                          int32_t* tid, int64_t table_mask, int32_t* n_keys, int64_t* key_of_id,
+                                          int64_t key_cap, int64_t* key, uint32_t* kid, uint32_t* kid_sorted,
+                                          int32_t* idx, int32_t* idx_sorted, uint32_t* uniq, int32_t* cnt,
+                                          int32_t* off, int32_t* n_runs_dev, void* temp, size_t temp_bytes,
+                                          int32_t* err, hipStream_t s);
+extern "C" size_t sdh_route_temp_bytes(int64_t n);
 
 extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaunch* L, int n_blocks,
                                        size_t lds, hipStream_t s);
@@ -498,6 +509,39 @@ struct sdh_engine {
   int64_t device_matches = 0;
   bool device_unpolled = false;
   std::vector<int64_t> backlog;      // host-side match records (rec_words int64 each)
+  // ---- K_gen (general interpreter) ----
+  kg::LProgram lp;                   // full IR (receivers, runtime tree, partitions)
+  std::vector<int> out_rank;         // R18 rank per (query, stream)
+  std::vector<kg::GQuery> gq;
+  DevBuf<kg::GQuery> d_gq;
+  std::vector<int32_t> lane_q;       // [group][64]
+  DevBuf<int32_t> d_lane_q;
+  int gB32 = 1, gB64 = 1;
+  struct GenSet {
+    int partition = -1;              // -1: the unpartitioned K_gen queries
+    int group_base = 0, n_groups = 0;
+    int64_t key_cap = 0;             // instance blocks = key_cap * n_groups (partitioned)
+    DevBuf<int32_t> a32;
+    DevBuf<int64_t> a64;
+    // partition routing
+    DevBuf<unsigned long long> tkey;
+    DevBuf<int32_t> tid, n_keys;
+    DevBuf<int64_t> key_of_id;
+    int64_t tmask = 0, max_keys = 0;
+  };
+  std::vector<std::unique_ptr<GenSet>> gsets;
+  DevBuf<int64_t> r_key;
+  DevBuf<uint32_t> r_kid, r_kid_s, r_uniq;
+  DevBuf<int32_t> r_idx, r_idx_s, r_cnt, r_off, r_nruns;
+  DevBuf<uint8_t> r_temp;
+  DevBuf<int64_t> g_out;
+  int64_t g_chunks = 0;
+  int g_chunk_words = 512;
+  DevBuf<int32_t> g_chunk_next;
+  DevBuf<unsigned long long> g_nrec;
+  std::vector<int64_t> g_host;       // collected K_gen records (variable length)
+  int64_t g_host_n = 0;
+  int64_t g_dev_matches = 0;         // matches of the last push left on the device
   // ---- K_ratchet groups ----
   std::vector<RatchetGroup> rg;
   std::vector<int> rcur;             // per group: buffer holding its deques
@@ -557,6 +601,7 @@ void collect_device_matches(sdh_engine* e, bool discard = false) {
     e->device_matches = 0;
     e->r_matches = 0;
     e->r_blocks_used = 0;
+    e->g_dev_matches = 0;
     return;
   }
   ratchet_collect(e);
@@ -938,6 +983,241 @@ void ratchet_collect(sdh_engine* e) {
   e->r_blocks_used = 0;
 }
 
+// ------------------------------------------------------------------------------------------
+// K_gen host side: lowering, instance arenas, partition routing, launch, match collection
+// ------------------------------------------------------------------------------------------
+void gen_build(sdh_engine* e, const std::vector<int>& qis) {
+  kg::Sizing sz;
+  if (e->cfg.gen_pool_states > 0) sz.R = std::min(64, e->cfg.gen_pool_states);
+  if (e->cfg.gen_pool_nodes > 0) sz.N = std::min(256, e->cfg.gen_pool_nodes);
+  if (e->cfg.gen_list_cap > 0) sz.LC = e->cfg.gen_list_cap;
+  std::vector<int> gidx(e->lp.q.size(), -1);
+  for (int qi : qis) {
+    try {
+      kg::GQuery g = kg::lower_gen(e->lp, qi, sz);
+      g.rank = 0;
+      gidx[qi] = (int)e->gq.size();
+      e->gq.push_back(g);
+      e->gB32 = std::max(e->gB32, g.lay.n32);
+      e->gB64 = std::max(e->gB64, g.lay.n64);
+    } catch (const kg::LowerError& ex) {
+      throw Error(SDH_E_UNSUPPORTED, fmt("query %d: %s", qi, ex.what()));
+    }
+  }
+  if (e->gq.empty()) return;
+  // sets: the unpartitioned queries, then one per partition; 64 queries per group (wave)
+  auto add_set = [&](int partition, const std::vector<int>& members) {
+    if (members.empty()) return;
+    auto gs = std::make_unique<sdh_engine::GenSet>();
+    gs->partition = partition;
+    gs->group_base = (int)(e->lane_q.size() / 64);
+    gs->n_groups = (int)((members.size() + 63) / 64);
+    for (int g = 0; g < gs->n_groups; ++g)
+      for (int l = 0; l < 64; ++l) {
+        const size_t k = (size_t)g * 64 + l;
+        e->lane_q.push_back(k < members.size() ? gidx[members[k]] : -1);
+      }
+    const size_t per_block32 = (size_t)e->gB32 * 64, per_block64 = (size_t)e->gB64 * 64;
+    if (partition < 0) {
+      gs->a32.ensure(per_block32 * gs->n_groups);
+      gs->a64.ensure(per_block64 * gs->n_groups);
+      HIPCHK(hipMemset(gs->a32.p, 0, per_block32 * gs->n_groups * 4));
+      HIPCHK(hipMemset(gs->a64.p, 0, per_block64 * gs->n_groups * 8));
+    } else {
+      gs->max_keys = e->cfg.gen_max_keys > 0 ? e->cfg.gen_max_keys : (1 << 20);
+      int64_t slots = 1;
+      while (slots < 2 * gs->max_keys) slots <<= 1;
+      gs->tmask = slots - 1;
+      gs->tkey.ensure(slots + 1);
+      gs->tid.ensure(slots + 1);
+      std::vector<unsigned long long> init((size_t)slots + 1, 0x8000000000000000ull);
+      init[slots] = 0;
+      HIPCHK(hipMemcpy(gs->tkey.p, init.data(), init.size() * 8, hipMemcpyHostToDevice));
+      HIPCHK(hipMemset(gs->tid.p, 0xff, (slots + 1) * 4));
+      gs->n_keys.ensure(1);
+      HIPCHK(hipMemset(gs->n_keys.p, 0, 4));
+      gs->key_of_id.ensure(gs->max_keys);
+      gs->key_cap = 0;
+    }
+    e->gsets.push_back(std::move(gs));
+  };
+  std::vector<int> top;
+  for (int qi : qis)
+    if (e->lp.q[qi].partition < 0) top.push_back(qi);
+  add_set(-1, top);
+  for (int pi = 0; pi < (int)e->lp.parts.size(); ++pi) {
+    std::vector<int> m;
+    for (int qi : e->lp.parts[pi].queries)
+      if (gidx[qi] >= 0) m.push_back(qi);
+    add_set(pi, m);
+  }
+  e->d_gq.ensure(e->gq.size());
+  HIPCHK(hipMemcpy(e->d_gq.p, e->gq.data(), e->gq.size() * sizeof(kg::GQuery), hipMemcpyHostToDevice));
+  e->d_lane_q.ensure(e->lane_q.size());
+  HIPCHK(hipMemcpy(e->d_lane_q.p, e->lane_q.data(), e->lane_q.size() * 4, hipMemcpyHostToDevice));
+  e->g_chunk_next.ensure(1);
+  e->g_nrec.ensure(1);
+}
+
+// grow a partition set's instance arena to hold `keys` keys (blocks are key-major: a prefix copy)
+void gen_grow(sdh_engine* e, sdh_engine::GenSet& gs, int64_t keys) {
+  if (keys <= gs.key_cap) return;
+  int64_t cap = std::max<int64_t>(64, gs.key_cap);
+  while (cap < keys) cap *= 2;
+  const size_t b32 = (size_t)e->gB32 * 64 * gs.n_groups, b64 = (size_t)e->gB64 * 64 * gs.n_groups;
+  DevBuf<int32_t> n32;
+  DevBuf<int64_t> n64;
+  n32.ensure(b32 * cap);
+  n64.ensure(b64 * cap);
+  HIPCHK(hipMemsetAsync(n32.p, 0, b32 * cap * 4, e->stream));
+  HIPCHK(hipMemsetAsync(n64.p, 0, b64 * cap * 8, e->stream));
+  if (gs.key_cap > 0) {
+    HIPCHK(hipMemcpyAsync(n32.p, gs.a32.p, b32 * gs.key_cap * 4, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(n64.p, gs.a64.p, b64 * gs.key_cap * 8, hipMemcpyDeviceToDevice, e->stream));
+  }
+  HIPCHK(hipStreamSynchronize(e->stream));
+  std::swap(gs.a32.p, n32.p);
+  std::swap(gs.a32.n, n32.n);
+  std::swap(gs.a64.p, n64.p);
+  std::swap(gs.a64.n, n64.n);
+  gs.key_cap = cap;
+}
+
+int64_t gen_collect_device(sdh_engine* e);
+
+// one K_gen step for every set fed by `stream`
+void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out) {
+  *ms_out = 0;
+  if (e->gsets.empty()) return;
+  const int64_t n = B.n;
+  if (e->g_chunks == 0) {
+    const int64_t words = std::max<int64_t>(1 << 22, n * 64);
+    e->g_chunks = words / e->g_chunk_words;
+  }
+  e->g_out.ensure((size_t)e->g_chunks * e->g_chunk_words);
+  e->d_err.ensure(4);
+  HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
+  HIPCHK(hipMemsetAsync(e->g_chunk_next.p, 0, 4, e->stream));
+  HIPCHK(hipMemsetAsync(e->g_nrec.p, 0, 8, e->stream));
+  const bool write = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) == 0;
+  HIPCHK(hipEventRecord(e->ev0, e->stream));
+  bool any = false;
+  for (auto& up : e->gsets) {
+    auto& gs = *up;
+    sdh::GenLaunch L{};
+    L.queries = e->d_gq.p;
+    L.lane_q = e->d_lane_q.p;
+    L.b = B;
+    L.groups = gs.n_groups;
+    L.group_base = gs.group_base;
+    L.B32 = e->gB32;
+    L.B64 = e->gB64;
+    L.out = e->g_out.p;
+    L.n_chunks = e->g_chunks;
+    L.chunk_words = e->g_chunk_words;
+    L.chunk_next = e->g_chunk_next.p;
+    L.err = e->d_err.p;
+    L.rec_count = e->g_nrec.p;
+    L.write_records = write;
+    if (gs.partition < 0) {
+      bool reads = false;
+      for (int g = 0; g < gs.n_groups * 64; ++g) {
+        const int gi = e->lane_q[(size_t)gs.group_base * 64 + g];
+        reads |= gi >= 0 && e->gq[gi].recv_n[stream] > 0;
+      }
+      if (!reads) continue;
+      L.a32 = gs.a32.p;
+      L.a64 = gs.a64.p;
+      L.n_items = gs.n_groups;
+      HIPCHK(sdh_launch_gen(&L, e->stream));
+      any = true;
+      continue;
+    }
+    // partitioned: the partition's key attribute of this stream
+    const kg::LPart& pd = e->lp.parts[gs.partition];
+    int attr = -1;
+    for (const auto& k : pd.keys)
+      if (k.stream == stream) attr = (int)k.code[0].imm;
+    if (attr < 0) continue;
+    const int type = e->lp.stream_types[stream][attr];
+    e->r_key.ensure(n);
+    e->r_kid.ensure(n);
+    e->r_kid_s.ensure(n);
+    e->r_uniq.ensure(n);
+    e->r_idx.ensure(n);
+    e->r_idx_s.ensure(n);
+    e->r_cnt.ensure(n);
+    e->r_off.ensure(n);
+    e->r_nruns.ensure(1);
+    const size_t tb = sdh_route_temp_bytes(n);
+    e->r_temp.ensure(tb);
+    HIPCHK(sdh_route_partition(&B, attr, type, gs.tkey.p, gs.tid.p, gs.tmask, gs.n_keys.p, gs.key_of_id.p,
+                               gs.max_keys, e->r_key.p, e->r_kid.p, e->r_kid_s.p, e->r_idx.p, e->r_idx_s.p,
+                               e->r_uniq.p, e->r_cnt.p, e->r_off.p, e->r_nruns.p, e->r_temp.p, e->r_temp.n,
+                               e->d_err.p + 3, e->stream));
+    int32_t hv[2];
+    HIPCHK(hipMemcpyAsync(&hv[0], gs.n_keys.p, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&hv[1], e->r_nruns.p, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (hv[0] > gs.max_keys) throw Error(SDH_E_CAPACITY, "more partition keys than gen_max_keys");
+    gen_grow(e, gs, hv[0]);
+    L.a32 = gs.a32.p;
+    L.a64 = gs.a64.p;
+    L.seg_begin = e->r_off.p;
+    L.seg_len = e->r_cnt.p;
+    L.seg_kid = e->r_uniq.p;
+    L.key_of_id = gs.key_of_id.p;
+    L.ev_idx = e->r_idx_s.p;
+    L.n_items = hv[1] * gs.n_groups;
+    HIPCHK(sdh_launch_gen(&L, e->stream));
+    any = true;
+  }
+  HIPCHK(hipEventRecord(e->ev1, e->stream));
+  int32_t errs[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(errs, e->d_err.p, 16, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+  *ms_out = ms;
+  if (errs[3]) throw Error(SDH_E_CAPACITY, "partition key table full");
+  if (errs[1]) throw Error(SDH_E_REFERENCE, "the reference engine would throw on this stream "
+                                            "(ConcurrentModification / IllegalState / NullPointer)");
+  if (errs[0]) throw Error(SDH_E_CAPACITY, "K_gen instance pool or list capacity exceeded "
+                                           "(raise gen_pool_states / gen_pool_nodes / gen_list_cap)");
+  unsigned long long nrec = 0;
+  if (any) HIPCHK(hipMemcpy(&nrec, e->g_nrec.p, 8, hipMemcpyDeviceToHost));
+  if (write && any) gen_collect_device(e);
+  e->g_dev_matches = write ? 0 : (int64_t)nrec;
+  if (errs[2]) {
+    e->g_chunks *= 4;  // the next push gets a larger output buffer
+    throw Error(SDH_E_CAPACITY, "K_gen match output buffer overflow (matches of this push were lost)");
+  }
+  e->stats.matches += (int64_t)nrec;
+}
+
+// copy the used output chunks back and append their records to g_host
+int64_t gen_collect_device(sdh_engine* e) {
+  int32_t used = 0;
+  HIPCHK(hipMemcpy(&used, e->g_chunk_next.p, 4, hipMemcpyDeviceToHost));
+  used = (int32_t)std::min<int64_t>(used, e->g_chunks);
+  if (used <= 0) return 0;
+  std::vector<int64_t> buf((size_t)used * e->g_chunk_words);
+  HIPCHK(hipMemcpy(buf.data(), e->g_out.p, buf.size() * 8, hipMemcpyDeviceToHost));
+  int64_t n = 0;
+  for (int c = 0; c < used; ++c) {
+    const int64_t* ch = buf.data() + (size_t)c * e->g_chunk_words;
+    const int64_t fill = ch[0];
+    for (int64_t w = 0; w < fill;) {
+      const int64_t len = ch[1 + w];
+      e->g_host.insert(e->g_host.end(), ch + 1 + w, ch + 1 + w + len);
+      w += len;
+      ++n;
+      ++e->g_host_n;
+    }
+  }
+  return n;
+}
+
 int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   if (!b || stream < 0 || stream >= (int)e->prog.stream_types.size())
     throw Error(SDH_E_INVALID, "bad stream or batch");
@@ -1016,6 +1296,11 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     if (g.stream == stream) consumers += g.n_lanes;
   ms += e->r_kernel_ms;
   bytes += e->r_kernel_bytes;
+  double gms = 0;
+  launch_gen(e, stream, B, &gms);
+  ms += gms;
+  for (const auto& g : e->gq)
+    if (g.recv_n[stream] > 0) consumers += 1;
   if (consumers) {
     e->device_unpolled = true;
     e->stats.pattern_events += b->n * consumers;
@@ -1063,12 +1348,28 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     if (ndev <= 0) throw Error(SDH_E_DEVICE, "no HIP device (the engine has no CPU fallback)");
     HIPCHK(hipSetDevice(e->dev));
     e->prog = read_ir(ir, len);
+    try {
+      e->lp = kg::read_program(ir, len);
+    } catch (const kg::LowerError& ex) {
+      throw Error(SDH_E_INVALID, ex.what());
+    }
+    e->out_rank = kg::output_ranks(e->lp);
+    // plan selection per query: K_ratchet (2-state threshold ratchet) > K_chain (stream-state
+    // chains) > K_gen (everything else: count, logical, sequences, partitions, general predicates)
     std::vector<std::pair<RatchetPlan, int>> rplans;
+    std::vector<int> gen_qs;
     const bool no_ratchet = (e->cfg.flags & SDH_FLAG_NO_RATCHET) != 0;
+    const bool force_gen = (e->cfg.flags & SDH_FLAG_FORCE_GEN) != 0;
     for (int qi = 0; qi < (int)e->prog.q.size(); ++qi) {
-      if (qi % e->cfg.shard_world != e->cfg.shard_rank) continue;
-      Lowered L = lower_query(e->prog, qi);
-      if (!L.ok) throw Error(SDH_E_UNSUPPORTED, L.why);
+      // pattern-set sharding; a partition's queries stay together on one shard
+      const int pi = e->lp.q[qi].partition;
+      const int shard_key = pi < 0 ? qi : e->lp.parts[pi].queries[0];
+      if (shard_key % e->cfg.shard_world != e->cfg.shard_rank) continue;
+      Lowered L = force_gen ? Lowered() : lower_query(e->prog, qi);
+      if (!L.ok) {
+        gen_qs.push_back(qi);
+        continue;
+      }
       RatchetPlan rp = no_ratchet ? RatchetPlan() : ratchet_plan(L.cq);
       if (rp.ok) rplans.push_back({rp, qi});
       else e->lq.push_back(L);
@@ -1090,6 +1391,7 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
       HIPCHK(hipMemcpy(e->d_q.p, cqs.data(), cqs.size() * sizeof(ChainQuery), hipMemcpyHostToDevice));
     ensure_state(e);
     ratchet_build(e, rplans);
+    gen_build(e, gen_qs);
     return SDH_OK;
   });
   if (rc != SDH_OK) {
@@ -1116,7 +1418,8 @@ int sdh_engine_flush(sdh_engine* e) {
 
 int sdh_engine_pending_matches(sdh_engine* e, int64_t* n) {
   if (!e || !n) return SDH_E_INVALID;
-  *n = (int64_t)(e->backlog.size() / e->rec_words) + (e->device_unpolled ? e->device_matches + e->r_matches : 0);
+  *n = (int64_t)(e->backlog.size() / e->rec_words) + e->g_host_n +
+       (e->device_unpolled ? e->device_matches + e->r_matches + e->g_dev_matches : 0);
   return SDH_OK;
 }
 
@@ -1125,19 +1428,42 @@ int sdh_engine_poll(sdh_engine* e, sdh_matches* out) {
   return guard(e, [&]() {
     collect_device_matches(e);
     const int RW = e->rec_words;
+    const int NS = (int)e->lp.stream_types.size();
     const int64_t* v = e->backlog.data();
-    const size_t n = e->backlog.size() / RW;
+    const size_t nb = e->backlog.size() / RW;
+    // K_gen records: [len, qid, key, ts, seq, idx, S | stream << 16, (count, seqs...) x S]
+    std::vector<size_t> goff;
+    for (size_t w = 0; w < e->g_host.size(); w += (size_t)e->g_host[w]) goff.push_back(w);
+    const int64_t* gv = e->g_host.data();
+    const size_t n = nb + goff.size();
     auto S_of = [&](size_t i) { return (int)e->prog.q[v[i * RW]].st.size(); };
-    auto last = [&](size_t i) { return v[i * RW + 2 + S_of(i) - 1]; };
-    // reference delivery order (R18): per event, per query, per pending partial in insertion
-    // order -- for chain queries a state's pending list is ordered by the earlier slots' events
-    std::vector<size_t> idx(n);
-    for (size_t i = 0; i < n; ++i) idx[i] = i;
-    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
-      if (last(a) != last(b)) return last(a) < last(b);
-      if (v[a * RW] != v[b * RW]) return v[a * RW] < v[b * RW];
-      for (int k = S_of(a) - 2; k >= 0; --k)
-        if (v[a * RW + 2 + k] != v[b * RW + 2 + k]) return v[a * RW + 2 + k] < v[b * RW + 2 + k];
+    // reference delivery order (R18): per triggering event; per junction subscriber / partition
+    // delivery (out_rank); per pending partial in insertion order -- for chain-family plans the
+    // earlier slots' events order a state's pending list, K_gen records carry their emission index
+    struct Key {
+      int64_t seq, rank;
+      size_t i;
+      bool gen;
+    };
+    std::vector<Key> keys(n);
+    for (size_t i = 0; i < nb; ++i) {
+      const int q = (int)v[i * RW];
+      const int S = S_of(i);
+      const int st = e->prog.q[q].st[S - 1].stream;
+      keys[i] = Key{v[i * RW + 2 + S - 1], e->out_rank[(size_t)q * NS + st], i, false};
+    }
+    for (size_t j = 0; j < goff.size(); ++j) {
+      const int64_t* r = gv + goff[j];
+      const int q = (int)r[1], st = (int)(r[6] >> 16);
+      keys[nb + j] = Key{r[4], e->out_rank[(size_t)q * NS + st], j, true};
+    }
+    std::stable_sort(keys.begin(), keys.end(), [&](const Key& a, const Key& b) {
+      if (a.seq != b.seq) return a.seq < b.seq;
+      if (a.rank != b.rank) return a.rank < b.rank;
+      if (a.gen != b.gen) return !a.gen;
+      if (a.gen) return gv[goff[a.i] + 5] < gv[goff[b.i] + 5];
+      for (int k = S_of(a.i) - 2; k >= 0; --k)
+        if (v[a.i * RW + 2 + k] != v[b.i * RW + 2 + k]) return v[a.i * RW + 2 + k] < v[b.i * RW + 2 + k];
       return false;
     });
     e->o_query.resize(n);
@@ -1146,18 +1472,29 @@ int sdh_engine_poll(sdh_engine* e, sdh_matches* out) {
     e->o_off.resize(n + 1);
     e->o_words.clear();
     for (size_t j = 0; j < n; ++j) {
-      const size_t i = idx[j];
-      e->o_query[j] = v[i * RW];
-      e->o_key[j] = -1;
-      e->o_ts[j] = v[i * RW + 1];
+      const Key& k = keys[j];
       e->o_off[j] = (int64_t)e->o_words.size();
-      for (int k = 0; k < S_of(i); ++k) {
-        e->o_words.push_back(1);
-        e->o_words.push_back(v[i * RW + 2 + k]);
+      if (!k.gen) {
+        const size_t i = k.i;
+        e->o_query[j] = v[i * RW];
+        e->o_key[j] = -1;
+        e->o_ts[j] = v[i * RW + 1];
+        for (int s2 = 0; s2 < S_of(i); ++s2) {
+          e->o_words.push_back(1);
+          e->o_words.push_back(v[i * RW + 2 + s2]);
+        }
+      } else {
+        const int64_t* r = gv + goff[k.i];
+        e->o_query[j] = r[1];
+        e->o_key[j] = r[2];
+        e->o_ts[j] = r[3];
+        e->o_words.insert(e->o_words.end(), r + 7, r + r[0]);
       }
     }
     e->o_off[n] = (int64_t)e->o_words.size();
     e->backlog.clear();
+    e->g_host.clear();
+    e->g_host_n = 0;
     out->n = (int64_t)n;
     out->query = e->o_query.data();
     out->key = e->o_key.data();
@@ -1197,6 +1534,8 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
 int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
   if (!e || !blob || !len) return SDH_E_INVALID;
   return guard(e, [&]() {
+    if (!e->gsets.empty())
+      throw Error(SDH_E_UNSUPPORTED, "snapshot of K_gen instance arenas is not implemented yet");
     HIPCHK(hipStreamSynchronize(e->stream));
     const size_t nq = e->lq.size();
     const size_t tbl = (size_t)NF * e->pcap;

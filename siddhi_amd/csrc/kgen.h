@@ -1,0 +1,786 @@
+// kgen.h -- K_gen: the general NFA interpreter, one lane per query instance (query, partition key).
+//
+// Restates the reference's object model for ONE state-stream runtime, so every query shape the IR
+// expresses runs on the device: stream / count `<n:m>` / logical and-or states, PATTERN and
+// SEQUENCE semantics, every scopes, `within` and within-every re-arming, count callbacks
+// (startStateReset), partitions (one instance per key). Paths relative to siddhi-core
+// .../query/input/stream/state/ (= state/):
+//
+//   objects     StateEvent (slots of StreamEvent chains; event/state/StateEvent.java:42-258),
+//               shallow every-clones (event/state/StateEventCloner.java:46-58), StreamEvent
+//               copies with their own `next` link; a per-instance pool of each, reclaimed by
+//               mark/sweep from the pending / newAndEvery lists (the JVM's job in the reference)
+//   lists       pending + newAndEvery per pre-processor, two-phase promotion
+//               (StreamPreStateProcessor.java:203-227,281-289)
+//   processors  StreamPre.processAndReturn:292-337, CountPre:53-156, LogicalPre:57-183,
+//               StreamPost:53-72, CountPost:45-95, LogicalPost:59-87
+//   runtime     init / reset / update orders of the inner-state-runtime tree (state/runtime/*),
+//               flattened on the host; receivers (PatternMultiProcessStreamReceiver.java:38-44)
+//
+// The code is written once for host and device (KG_FN): the device kernel (nfa_gen.hip) runs it
+// per lane over lane-interleaved arenas in HBM; tests/native builds the same header for the host
+// to cross-check the restatement against the oracle (test infrastructure only).
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#define KG_FN __host__ __device__ inline
+#else
+#define KG_FN inline
+#endif
+
+namespace sdh {
+namespace kg {
+
+constexpr int GMAXS = 8;         // states per query
+constexpr int GMAXF = 4;         // filters per state
+constexpr int GMAXCODE = 192;    // bytecode instructions per query
+constexpr int GMAXNA = 8;        // captured attributes per node (per stream)
+constexpr int GMAXSTREAM = 8;    // streams a query may read
+constexpr int GSTACK = 12;       // bytecode evaluation stack
+constexpr int GMAXRET = 64;      // matches one processAndReturn may return
+
+enum { T_INT = 0, T_LONG, T_FLOAT, T_DOUBLE, T_BOOL, T_STRING };
+enum { OP_CONST = 1, OP_ATTR, OP_IS_NULL, OP_STREAM_IS_NULL, OP_CMP, OP_AND, OP_OR, OP_NOT, OP_ARITH };
+enum { CMP_EQ = 0, CMP_NE, CMP_GT, CMP_GE, CMP_LT, CMP_LE };
+enum { AR_ADD = 0, AR_SUB, AR_MUL, AR_DIV, AR_MOD };
+enum { K_STREAM = 0, K_COUNT, K_LOGICAL };
+enum { L_AND = 0, L_OR };
+enum { Q_PATTERN = 0, Q_SEQUENCE };
+enum { R_SINGLE = 0, R_MULTI };
+
+// error codes (per lane, first one wins)
+enum { GE_OK = 0, GE_CAPACITY = 1, GE_REFERENCE = 2 };
+
+struct GInsn {
+  int8_t op, lt, rt, res;
+  int32_t a;     // slot (state id) for ATTR / STREAM_IS_NULL
+  int64_t b;     // chain index (CURRENT=-1, LAST=-2, ...)
+  int64_t imm;   // constant bits / node attribute word / cmp or arith op
+};
+
+struct GState {
+  int32_t kind, stream, is_start, min, max, ltype, partner, next_pre, next_every, within_every, callback,
+      this_last, has_selector;
+  int32_t n_filt;
+  int32_t fb[GMAXF], fe[GMAXF];   // filter code ranges
+};
+
+// arena layout (word offsets; 32-bit and 64-bit arenas, lane-interleaved on the device)
+struct GLayout {
+  int32_t S, R, N, LC, NA, NU;     // states, StateEvents, nodes, list capacity, node attrs, node-mask words
+  int32_t o_flags, o_pn, o_nn, o_plist, o_nlist, o_seslot, o_ndnext, o_ndnull, o_init, n32;
+  int32_t o_seused, o_ndused, o_sets, o_ndseq, o_ndts, o_ndval, n64;
+};
+
+struct GQuery {
+  int32_t qid, type, n_states, partition, rank;
+  int32_t pad0;
+  int64_t within;                                  // ms, -1 = none
+  int32_t n_start, start_ids[GMAXS];
+  int32_t recv_kind[GMAXSTREAM], recv_n[GMAXSTREAM], recv_procs[GMAXSTREAM][GMAXS];
+  int32_t n_init, init_order[GMAXS];               // node_init(0): init_pre order
+  int32_t n_reset, reset_order[2 * GMAXS];         // node_reset(0): resetState order
+  int32_t n_update, update_order[2 * GMAXS];       // node_update(0): updateState order
+  int32_t n_cap[GMAXSTREAM], cap_attr[GMAXSTREAM][GMAXNA];  // node attribute words per stream
+  int32_t cap_type[GMAXSTREAM][GMAXNA];
+  GLayout lay;
+  GState st[GMAXS];
+  int32_t n_code;
+  int32_t pad1;
+  GInsn code[GMAXCODE];
+};
+
+// ---- Java value semantics (executor/condition/compare/**, executor/math/**) ----
+struct Val {
+  int32_t type;
+  int32_t null;
+  int64_t bits;   // int/long/bool/string id (sign-extended), float bits (low 32), double bits
+};
+
+KG_FN float f_of(int64_t b) { union { uint32_t u; float f; } x; x.u = (uint32_t)b; return x.f; }
+KG_FN double d_of(int64_t b) { union { int64_t i; double d; } x; x.i = b; return x.d; }
+KG_FN int64_t bits_f(float f) { union { uint32_t u; float f; } x; x.f = f; return (int64_t)x.u; }
+KG_FN int64_t bits_d(double d) { union { int64_t i; double d; } x; x.d = d; return x.i; }
+
+KG_FN float as_f(const Val& v) {
+  switch (v.type) {
+    case T_INT: return (float)(int32_t)v.bits;
+    case T_LONG: return (float)v.bits;
+    case T_FLOAT: return f_of(v.bits);
+    default: return (float)d_of(v.bits);
+  }
+}
+KG_FN double as_d(const Val& v) {
+  switch (v.type) {
+    case T_INT: return (double)(int32_t)v.bits;
+    case T_LONG: return (double)v.bits;
+    case T_FLOAT: return (double)f_of(v.bits);
+    default: return d_of(v.bits);
+  }
+}
+
+template <class T>
+KG_FN bool cmp_op(int op, T a, T b) {
+  switch (op) {
+    case CMP_EQ: return a == b;
+    case CMP_NE: return a != b;
+    case CMP_GT: return a > b;
+    case CMP_GE: return a >= b;
+    case CMP_LT: return a < b;
+    default: return a <= b;
+  }
+}
+
+// the typed compare table (compare/*/...Executor*.java execute() at :33-38)
+KG_FN bool typed_compare(int op, const Val& l, const Val& r) {
+  const int lt = l.type, rt = r.type;
+  if (lt == T_STRING || lt == T_BOOL) {
+    const bool eq = l.bits == r.bits;
+    return op == CMP_EQ ? eq : !eq;
+  }
+  const bool is_eq = (op == CMP_EQ || op == CMP_NE);
+  if (lt == T_DOUBLE || rt == T_DOUBLE) return cmp_op(op, as_d(l), as_d(r));
+  if (lt == T_FLOAT || rt == T_FLOAT) {
+    if (is_eq && (lt == T_LONG || rt == T_LONG)) return cmp_op(op, as_d(l), as_d(r));  // ...LongFloat.java:36
+    return cmp_op(op, as_f(l), as_f(r));
+  }
+  if (lt == T_LONG || rt == T_LONG) return cmp_op(op, l.bits, r.bits);
+  return cmp_op(op, (int32_t)l.bits, (int32_t)r.bits);
+}
+
+// executor/math/{add,subtract,multiply,divide,mod}: null in -> null; /0 and %0 -> null for every
+// type (0.0f / -0.0 included, DivideExpressionExecutorFloat.java:46); integer ops wrap
+KG_FN Val arith(int op, int res, const Val& l, const Val& r) {
+  Val v{res, 1, 0};
+  if (l.null || r.null) return v;
+  v.null = 0;
+  if (res == T_INT) {
+    const int32_t a = (int32_t)l.bits, b = (int32_t)r.bits;
+    const uint32_t ua = (uint32_t)a, ub = (uint32_t)b;
+    switch (op) {
+      case AR_ADD: v.bits = (int32_t)(ua + ub); break;
+      case AR_SUB: v.bits = (int32_t)(ua - ub); break;
+      case AR_MUL: v.bits = (int32_t)(ua * ub); break;
+      case AR_DIV:
+        if (b == 0) { v.null = 1; return v; }
+        v.bits = (a == INT32_MIN && b == -1) ? INT32_MIN : a / b;
+        break;
+      default:
+        if (b == 0) { v.null = 1; return v; }
+        v.bits = (b == -1) ? 0 : a % b;
+    }
+  } else if (res == T_LONG) {
+    const int64_t a = l.bits, b = r.bits;
+    const uint64_t ua = (uint64_t)a, ub = (uint64_t)b;
+    switch (op) {
+      case AR_ADD: v.bits = (int64_t)(ua + ub); break;
+      case AR_SUB: v.bits = (int64_t)(ua - ub); break;
+      case AR_MUL: v.bits = (int64_t)(ua * ub); break;
+      case AR_DIV:
+        if (b == 0) { v.null = 1; return v; }
+        v.bits = (a == INT64_MIN && b == -1) ? INT64_MIN : a / b;
+        break;
+      default:
+        if (b == 0) { v.null = 1; return v; }
+        v.bits = (b == -1) ? 0 : a % b;
+    }
+  } else if (res == T_FLOAT) {
+    const float a = as_f(l), b = as_f(r);
+    float o;
+    switch (op) {
+      case AR_ADD: o = a + b; break;
+      case AR_SUB: o = a - b; break;
+      case AR_MUL: o = a * b; break;
+      case AR_DIV: if (b == 0.0f) { v.null = 1; return v; } o = a / b; break;
+      default: if (b == 0.0f) { v.null = 1; return v; } o = fmodf(a, b);
+    }
+    v.bits = bits_f(o);
+  } else {
+    const double a = as_d(l), b = as_d(r);
+    double o;
+    switch (op) {
+      case AR_ADD: o = a + b; break;
+      case AR_SUB: o = a - b; break;
+      case AR_MUL: o = a * b; break;
+      case AR_DIV: if (b == 0.0) { v.null = 1; return v; } o = a / b; break;
+      default: if (b == 0.0) { v.null = 1; return v; } o = fmod(a, b);
+    }
+    v.bits = bits_d(o);
+  }
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// per-lane runtime over the instance arena
+// ------------------------------------------------------------------------------------------
+enum { FL_CHANGED = 1, FL_INIT = 2, FL_SUCCESS = 4, FL_SSRESET = 8, FL_RETURNED = 16, FL_ITER = 32 };
+
+struct Emitter;  // defined by the caller: void emit(const Ctx&, int se)
+
+struct Ctx {
+  const GQuery* q;
+  int32_t* w32;
+  int64_t* w64;
+  int64_t stride;
+  // current event (the instance's view of it)
+  int64_t seq, ts;
+  int32_t stream;
+  int64_t ev_val[GMAXNA];
+  uint32_t ev_null;
+  int32_t err;
+  // GC roots outside the lists: partials unlinked or not yet linked while they are worked on
+  int32_t pins[4];
+  int32_t npin;
+  int32_t ret[GMAXRET];
+  int32_t n_ret;
+
+  KG_FN int32_t& i32(int i) const { return w32[(int64_t)i * stride]; }
+  KG_FN int64_t& i64(int i) const { return w64[(int64_t)i * stride]; }
+  KG_FN const GState& S(int i) const { return q->st[i]; }
+  KG_FN int nS() const { return q->lay.S; }
+
+  // ---- arena fields ----
+  KG_FN int32_t& flags(int i) const { return i32(q->lay.o_flags + i); }
+  KG_FN int32_t& pn(int i) const { return i32(q->lay.o_pn + i); }
+  KG_FN int32_t& nn(int i) const { return i32(q->lay.o_nn + i); }
+  KG_FN int32_t& pl(int i, int k) const { return i32(q->lay.o_plist + i * q->lay.LC + k); }
+  KG_FN int32_t& nl(int i, int k) const { return i32(q->lay.o_nlist + i * q->lay.LC + k); }
+  KG_FN int32_t& slot(int se, int i) const { return i32(q->lay.o_seslot + se * q->lay.S + i); }
+  KG_FN int64_t& se_ts(int se) const { return i64(q->lay.o_sets + se); }
+  KG_FN int32_t& nd_next(int n) const { return i32(q->lay.o_ndnext + n); }
+  KG_FN int32_t& nd_null(int n) const { return i32(q->lay.o_ndnull + n); }
+  KG_FN int64_t& nd_seq(int n) const { return i64(q->lay.o_ndseq + n); }
+  KG_FN int64_t& nd_ts(int n) const { return i64(q->lay.o_ndts + n); }
+  KG_FN int64_t& nd_val(int n, int j) const { return i64(q->lay.o_ndval + n * q->lay.NA + j); }
+  KG_FN int64_t& se_used() const { return i64(q->lay.o_seused); }
+  KG_FN int64_t& nd_used(int w) const { return i64(q->lay.o_ndused + w); }
+
+  KG_FN void fail(int e) {
+    if (err == GE_OK) err = e;
+  }
+
+  // ---- allocation with mark/sweep reclamation ----
+  KG_FN void mark_chain(int n, uint64_t* nm) const {
+    while (n >= 0 && !((nm[n >> 6] >> (n & 63)) & 1ull)) {
+      nm[n >> 6] |= 1ull << (n & 63);
+      n = nd_next(n);
+    }
+  }
+  KG_FN void mark_se(int se, uint64_t& sm, uint64_t* nm) const {
+    if (se < 0 || ((sm >> se) & 1ull)) return;
+    sm |= 1ull << se;
+    for (int i = 0; i < nS(); ++i) mark_chain(slot(se, i), nm);
+  }
+  KG_FN void gc() {
+    uint64_t sm = 0, nm[4] = {0, 0, 0, 0};
+    for (int i = 0; i < nS(); ++i) {
+      for (int k = 0; k < pn(i); ++k) mark_se(pl(i, k), sm, nm);
+      for (int k = 0; k < nn(i); ++k) mark_se(nl(i, k), sm, nm);
+    }
+    for (int k = 0; k < npin; ++k) mark_se(pins[k], sm, nm);
+    for (int k = 0; k < n_ret; ++k) mark_se(ret[k], sm, nm);
+    se_used() = (int64_t)sm;
+    for (int w = 0; w < q->lay.NU; ++w) nd_used(w) = (int64_t)nm[w];
+  }
+  KG_FN int find_free_se() const {
+    const uint64_t u = (uint64_t)se_used();
+    const uint64_t fr = ~u & (q->lay.R >= 64 ? ~0ull : ((1ull << q->lay.R) - 1));
+    if (!fr) return -1;
+    return __builtin_ctzll(fr);
+  }
+  KG_FN int find_free_nd() const {
+    for (int w = 0; w < q->lay.NU; ++w) {
+      const int lim = q->lay.N - w * 64;
+      const uint64_t u = (uint64_t)nd_used(w);
+      const uint64_t fr = ~u & (lim >= 64 ? ~0ull : ((1ull << lim) - 1));
+      if (fr) return w * 64 + __builtin_ctzll(fr);
+    }
+    return -1;
+  }
+  KG_FN int new_state() {
+    int s = find_free_se();
+    if (s < 0) {
+      gc();
+      s = find_free_se();
+      if (s < 0) { fail(GE_CAPACITY); return -1; }
+    }
+    se_used() = (int64_t)((uint64_t)se_used() | (1ull << s));
+    for (int i = 0; i < nS(); ++i) slot(s, i) = -1;
+    se_ts(s) = -1;
+    return s;
+  }
+  KG_FN void pin(int se) {
+    if (npin < 4) pins[npin] = se;
+    ++npin;
+  }
+  KG_FN void unpin() { --npin; }
+  KG_FN int clone(int se) {  // StateEventCloner.copyStateEvent:46-58 (shallow)
+    pin(se);
+    const int c = new_state();
+    unpin();
+    if (c < 0) return -1;
+    for (int i = 0; i < nS(); ++i) slot(c, i) = slot(se, i);
+    se_ts(c) = se_ts(se);
+    return c;
+  }
+  // copy of the current event (StreamEvent copy with its own `next` link)
+  KG_FN int copy_event(int pinned) {
+    int n = find_free_nd();
+    if (n < 0) {
+      pin(pinned);
+      gc();
+      unpin();
+      n = find_free_nd();
+      if (n < 0) { fail(GE_CAPACITY); return -1; }
+    }
+    nd_used(n >> 6) = (int64_t)((uint64_t)nd_used(n >> 6) | (1ull << (n & 63)));
+    nd_seq(n) = seq;
+    nd_ts(n) = ts;
+    nd_next(n) = -1;
+    nd_null(n) = (int32_t)ev_null;
+    const int na = q->n_cap[stream];
+    for (int j = 0; j < na; ++j) nd_val(n, j) = ev_val[j];
+    return n;
+  }
+
+  // ---- lists ----
+  KG_FN void nae_push(int i, int se) {
+    if (nn(i) >= q->lay.LC) { fail(GE_CAPACITY); return; }
+    nl(i, nn(i)) = se;
+    nn(i) += 1;
+  }
+  KG_FN void promote(int i) {  // pending.addAll(newAndEvery); newAndEvery.clear()
+    if ((flags(i) & FL_ITER) && nn(i) > 0) { fail(GE_REFERENCE); return; }  // Java CME
+    const int n = nn(i);
+    if (pn(i) + n > q->lay.LC) { fail(GE_CAPACITY); return; }
+    for (int k = 0; k < n; ++k) pl(i, pn(i) + k) = nl(i, k);
+    pn(i) += n;
+    nn(i) = 0;
+  }
+
+  // ---- pre processors ----
+  KG_FN void init_pre(int i) {  // StreamPreStateProcessor.init:157-166
+    const GState& s = S(i);
+    if (s.is_start && (!(flags(i) & FL_INIT) || s.next_every >= 0)) {
+      const int se = new_state();
+      if (se < 0) return;
+      add_state(i, se);
+      flags(i) |= FL_INIT;
+    }
+  }
+  // addState (StreamPre:203-216 / CountPre:109-132 / LogicalPre:57-76) including the count min-0
+  // forwarding chain (CountPost.processMinCountReached:73-85), recursion unrolled: every-targets
+  // of the chain are applied deepest first, as the nested calls do
+  KG_FN void add_state(int i, int se) {
+    int every_t[GMAXS];
+    int ne = 0;
+    pin(se);
+    while (i >= 0) {
+      const GState& s = S(i);
+      if (s.kind == K_LOGICAL) {
+        const int p = s.partner;
+        if (s.is_start || q->type == Q_SEQUENCE) {
+          if (nn(i) == 0) nae_push(i, se);
+          if (nn(p) == 0) nae_push(p, se);
+        } else {
+          nae_push(i, se);
+          nae_push(p, se);
+        }
+        break;
+      }
+      if (q->type == Q_SEQUENCE) {
+        if (nn(i) == 0) nae_push(i, se);
+      } else {
+        nae_push(i, se);
+      }
+      if (!(s.kind == K_COUNT && s.min == 0 && slot(se, i) < 0)) break;
+      // processMinCountReached(i, se)
+      if (s.has_selector) {
+        flags(i) |= FL_CHANGED;
+        flags(i) |= FL_RETURNED;
+      }
+      if (s.next_every >= 0 && ne < GMAXS) every_t[ne++] = s.next_every;
+      i = s.next_pre;
+    }
+    for (int k = ne - 1; k >= 0; --k) add_every_state(every_t[k], se);
+    unpin();
+  }
+  // addEveryState: StreamPre:218-227 (slot NOT cleared) / LogicalPre:78-92 (both slots cleared)
+  KG_FN void add_every_state(int i, int se) {
+    const GState& s = S(i);
+    const int c = clone(se);
+    if (c < 0) return;
+    if (s.kind == K_LOGICAL) {
+      slot(c, i) = -1;
+      nae_push(i, c);
+      slot(c, s.partner) = -1;
+      nae_push(s.partner, c);
+      return;
+    }
+    nae_push(i, c);
+  }
+  // updateState: StreamPre:281-289, CountPre:149-156, LogicalPre:118-130
+  KG_FN void update_state(int i) {
+    const GState& s = S(i);
+    if (s.kind == K_COUNT && (flags(i) & FL_SSRESET)) {
+      flags(i) &= ~FL_SSRESET;
+      init_pre(i);
+    }
+    promote(i);
+    if (s.kind == K_LOGICAL) promote(s.partner);
+  }
+  KG_FN bool next_pending_nonempty(int i) {
+    const int n = S(i).next_pre;
+    if (n < 0) { fail(GE_REFERENCE); return false; }  // NullPointerException in the reference
+    return pn(n) > 0;
+  }
+  // resetState: StreamPre:262-278, LogicalPre:94-116
+  KG_FN void reset_state(int i) {
+    const GState& s = S(i);
+    if (s.kind == K_LOGICAL) {
+      const int p = s.partner;
+      if (s.ltype == L_OR || pn(i) == pn(p)) {
+        pn(i) = 0;
+        pn(p) = 0;
+        if (s.is_start && nn(i) == 0) {
+          if (q->type == Q_SEQUENCE && s.next_every < 0 && next_pending_nonempty(i)) return;
+          init_pre(i);
+        }
+      }
+      return;
+    }
+    pn(i) = 0;
+    if (s.is_start && nn(i) == 0) {
+      if (q->type == Q_SEQUENCE && s.next_every < 0 && next_pending_nonempty(i)) return;
+      init_pre(i);
+    }
+  }
+  KG_FN void start_state_reset(int i) {  // CountPreStateProcessor.startStateReset:142-147
+    if (S(i).kind != K_COUNT) { fail(GE_REFERENCE); return; }
+    flags(i) |= FL_SSRESET;
+    if (S(i).callback >= 0) fail(GE_REFERENCE);  // StackOverflowError in the reference
+  }
+  KG_FN bool is_expired(int i, int se) const {  // StreamPreStateProcessor.isExpired:102-113
+    const GState& s = S(i);
+    if (s.is_start || q->within < 0) return false;
+    for (int k = 0; k < q->n_start; ++k) {
+      const int n = slot(se, q->start_ids[k]);
+      if (n >= 0) {
+        const int64_t d = (int64_t)((uint64_t)nd_ts(n) - (uint64_t)ts);
+        const int64_t a = d < 0 ? (int64_t)(0ull - (uint64_t)d) : d;
+        if (a > q->within) return true;
+      }
+    }
+    return false;
+  }
+
+  // ---- predicates ----
+  KG_FN int chain_at(int head, int64_t idx) const {  // StateEvent.getStreamEvent:138-182
+    if (head < 0) return -1;
+    if (idx >= 0) {
+      int e = head;
+      for (int64_t k = 1; k <= idx; ++k) {
+        e = nd_next(e);
+        if (e < 0) return -1;
+      }
+      return e;
+    }
+    if (idx == -1) {
+      int e = head;
+      while (nd_next(e) >= 0) e = nd_next(e);
+      return e;
+    }
+    if (idx == -2) {
+      if (nd_next(head) < 0) return -1;
+      int e = head;
+      while (nd_next(nd_next(e)) >= 0) e = nd_next(e);
+      return e;
+    }
+    int64_t len = 0;
+    for (int e = head; e >= 0; e = nd_next(e)) ++len;
+    int64_t k = len + idx;
+    if (k < 0) return -1;
+    int e = head;
+    for (int64_t j = 0; j < k; ++j) e = nd_next(e);
+    return e;
+  }
+  KG_FN Val run_code(int b, int e, int se) const {
+    Val st[GSTACK];
+    int sp = 0;
+    for (int pc = b; pc < e; ++pc) {
+      const GInsn& in = q->code[pc];
+      switch (in.op) {
+        case OP_CONST: {
+          Val v{in.res, 0, 0};
+          if (in.res == T_FLOAT) v.bits = (int64_t)(uint32_t)in.imm;
+          else if (in.res == T_INT) v.bits = (int32_t)in.imm;
+          else v.bits = in.imm;
+          st[sp++] = v;
+          break;
+        }
+        case OP_ATTR: {
+          const int n = chain_at(slot(se, in.a), in.b);
+          Val v{in.res, 1, 0};
+          if (n >= 0 && !((nd_null(n) >> in.imm) & 1)) {
+            v.null = 0;
+            const int64_t raw = nd_val(n, (int)in.imm);
+            v.bits = in.res == T_INT ? (int64_t)(int32_t)raw : in.res == T_FLOAT ? (int64_t)(uint32_t)raw : raw;
+          }
+          st[sp++] = v;
+          break;
+        }
+        case OP_STREAM_IS_NULL: {
+          st[sp++] = Val{T_BOOL, 0, chain_at(slot(se, in.a), in.b) < 0 ? 1 : 0};
+          break;
+        }
+        case OP_IS_NULL: {
+          const Val x = st[--sp];
+          st[sp++] = Val{T_BOOL, 0, x.null ? 1 : 0};
+          break;
+        }
+        case OP_NOT: {  // NotConditionExpressionExecutor: only TRUE -> FALSE
+          const Val x = st[--sp];
+          st[sp++] = Val{T_BOOL, 0, (!x.null && x.bits) ? 0 : 1};
+          break;
+        }
+        case OP_AND:
+        case OP_OR: {
+          const Val r = st[--sp];
+          const Val l = st[--sp];
+          const bool lb = !l.null && l.bits, rb = !r.null && r.bits;
+          st[sp++] = Val{T_BOOL, 0, (in.op == OP_AND ? (lb && rb) : (lb || rb)) ? 1 : 0};
+          break;
+        }
+        case OP_CMP: {  // CompareConditionExpressionExecutor.java:39-43
+          const Val r = st[--sp];
+          const Val l = st[--sp];
+          st[sp++] = Val{T_BOOL, 0, (!l.null && !r.null && typed_compare((int)in.imm, l, r)) ? 1 : 0};
+          break;
+        }
+        case OP_ARITH: {
+          const Val r = st[--sp];
+          const Val l = st[--sp];
+          st[sp++] = arith((int)in.imm, in.res, l, r);
+          break;
+        }
+        default:
+          st[sp++] = Val{T_BOOL, 1, 0};
+      }
+      if (sp >= GSTACK) sp = GSTACK - 1;
+    }
+    return sp == 1 ? st[0] : Val{T_BOOL, 1, 0};
+  }
+  KG_FN bool filters_pass(int i, int se) const {  // FilterProcessor.process:55-66
+    const GState& s = S(i);
+    for (int f = 0; f < s.n_filt; ++f) {
+      const Val v = run_code(s.fb[f], s.fe[f], se);
+      if (v.null || !v.bits) return false;
+    }
+    return true;
+  }
+
+  // ---- post processors ----
+  KG_FN void stream_post(int i, int se) {  // StreamPostStateProcessor.process:53-72
+    const GState& s = S(i);
+    flags(i) |= FL_CHANGED;
+    se_ts(se) = nd_ts(slot(se, i));
+    if (s.has_selector) flags(i) |= FL_RETURNED;
+    if (s.next_pre >= 0) add_state(s.next_pre, se);
+    if (s.next_every >= 0) add_every_state(s.next_every, se);
+    if (s.callback >= 0) start_state_reset(s.callback);
+  }
+  KG_FN void min_count_reached(int i, int se) {  // CountPost.processMinCountReached:73-85
+    const GState& s = S(i);
+    if (s.has_selector) {
+      flags(i) |= FL_CHANGED;
+      flags(i) |= FL_RETURNED;
+    }
+    if (s.next_pre >= 0) add_state(s.next_pre, se);
+    if (s.next_every >= 0) add_every_state(s.next_every, se);
+  }
+  KG_FN void count_post(int i, int se) {  // CountPostStateProcessor.process:45-71
+    const GState& s = S(i);
+    int e = slot(se, i);
+    int64_t n = 1;
+    while (nd_next(e) >= 0) { ++n; e = nd_next(e); }
+    flags(i) |= FL_SUCCESS;
+    se_ts(se) = nd_ts(e);
+    if (n >= s.min) {
+      if (q->type == Q_SEQUENCE) {
+        if (s.next_pre >= 0) add_state(s.next_pre, se);
+        if (n != s.max) add_state(i, se);
+      } else if (n == s.min) {
+        min_count_reached(i, se);
+      }
+      if (n == s.max) flags(i) |= FL_CHANGED;
+    }
+  }
+  KG_FN void logical_post(int i, int se) {  // LogicalPostStateProcessor.process:59-87
+    const GState& s = S(i);
+    if (s.ltype == L_AND) {
+      if (slot(se, s.partner) >= 0) stream_post(i, se);
+      else flags(i) |= FL_CHANGED;
+    } else {
+      stream_post(i, se);
+      if (S(s.partner).has_selector && s.this_last == s.partner) flags(s.partner) |= FL_RETURNED;
+    }
+  }
+  KG_FN void process(int i, int se) {
+    flags(i) &= ~FL_CHANGED;
+    if (!filters_pass(i, se)) return;
+    switch (S(i).kind) {
+      case K_STREAM: stream_post(i, se); break;
+      case K_COUNT: count_post(i, se); break;
+      default: logical_post(i, se); break;
+    }
+  }
+  KG_FN bool take_returned(int i) {
+    const int tl = S(i).this_last;
+    if (tl < 0) return false;
+    if (flags(tl) & FL_RETURNED) {
+      flags(tl) &= ~FL_RETURNED;
+      return true;
+    }
+    return false;
+  }
+  KG_FN void push_ret(int se) {
+    if (n_ret >= GMAXRET) { fail(GE_CAPACITY); return; }
+    ret[n_ret++] = se;
+  }
+
+  // processAndReturn: StreamPre:292-337, CountPre:53-93, LogicalPre:133-178. Emitted partials
+  // are collected in `ret` (GC roots) and handed to the emitter after the loop, as the reference
+  // returns its ComplexEventChunk.
+  KG_FN void process_and_return(int i) {
+    const GState& s = S(i);
+    flags(i) |= FL_ITER;
+    int w = 0;
+    const int nS_ = nS();
+    const int n0 = pn(i);
+    int k = 0;
+    for (; k < n0 && err == GE_OK; ++k) {
+      const int se = pl(i, k);
+      pin(se);
+      bool keep = true;
+      if (s.kind == K_COUNT) {
+        if ((nS_ > i + 1 && slot(se, i + 1) >= 0) || (nS_ > i + 2 && slot(se, i + 2) >= 0)) {
+          keep = false;
+        } else {
+          const int ev = copy_event(se);
+          if (ev < 0) { unpin(); break; }
+          if (slot(se, i) < 0) slot(se, i) = ev;  // StateEvent.addEvent:212-222
+          else {
+            int t = slot(se, i);
+            while (nd_next(t) >= 0) t = nd_next(t);
+            nd_next(t) = ev;
+          }
+          flags(i) &= ~FL_SUCCESS;
+          process(i, se);
+          if (take_returned(i)) push_ret(se);
+          bool removed = false;
+          if (flags(i) & FL_CHANGED) { keep = false; removed = true; }
+          if (!(flags(i) & FL_SUCCESS)) {
+            // StateEvent.removeLastEvent:224-236
+            int a = slot(se, i);
+            if (a >= 0) {
+              bool done = false;
+              while (nd_next(a) >= 0) {
+                if (nd_next(nd_next(a)) < 0) { nd_next(a) = -1; done = true; break; }
+                a = nd_next(a);
+              }
+              if (!done) slot(se, i) = -1;
+            }
+            if (q->type == Q_SEQUENCE) {
+              if (removed) fail(GE_REFERENCE);  // IllegalStateException (second iterator.remove)
+              keep = false;
+            }
+          }
+        }
+      } else if (is_expired(i, se)) {
+        keep = false;
+        if (s.within_every >= 0) {
+          add_every_state(s.within_every, se);
+          update_state(s.within_every);
+        }
+      } else if (s.kind == K_LOGICAL && s.ltype == L_OR && slot(se, s.partner) >= 0) {
+        keep = false;
+      } else {
+        const int ev = copy_event(se);
+        if (ev < 0) { unpin(); break; }
+        slot(se, i) = ev;
+        process(i, se);
+        if (take_returned(i)) push_ret(se);
+        if (flags(i) & FL_CHANGED) {
+          keep = false;
+        } else {
+          slot(se, i) = -1;
+          if (q->type == Q_SEQUENCE) {
+            keep = false;
+            if (s.kind == K_STREAM && s.callback >= 0) start_state_reset(s.callback);
+          }
+        }
+      }
+      unpin();
+      if (keep) pl(i, w++) = se;
+    }
+    for (; k < n0; ++k) pl(i, w++) = pl(i, k);  // not visited (error): kept
+    pn(i) = w;
+    flags(i) &= ~FL_ITER;
+  }
+
+  // one event of this instance's streams (Runtime.receive: SingleProcessStreamReceiver.java:57-80,
+  // MultiProcessStreamReceiver.receive:268-279 + StateMultiProcessStreamReceiver:53-74; sequences
+  // reset and update the whole runtime first, StateStreamRuntime.java:89-92)
+  template <class Emit>
+  KG_FN void receive(Emit& em) {
+    const int sidx = stream;
+    const int np = q->recv_n[sidx];
+    if (np == 0) return;
+    if (q->type == Q_SEQUENCE) {
+      for (int k = 0; k < q->n_reset; ++k) reset_state(q->reset_order[k]);
+      for (int k = 0; k < q->n_update; ++k) update_state(q->update_order[k]);
+    } else {
+      for (int k = 0; k < np; ++k) update_state(q->recv_procs[sidx][k]);
+    }
+    for (int k = np - 1; k >= 0 && err == GE_OK; --k) {  // reverse registration order
+      n_ret = 0;
+      process_and_return(q->recv_procs[sidx][k]);
+      for (int r = 0; r < n_ret; ++r) em(*this, ret[r]);
+      n_ret = 0;
+    }
+  }
+  KG_FN void init_instance() {  // QueryRuntime.init -> node_init(0)
+    for (int k = 0; k < q->n_init; ++k) init_pre(q->init_order[k]);
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// host-side layout of one query's arenas
+// ------------------------------------------------------------------------------------------
+inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA) {
+  L.S = S; L.R = R; L.N = N; L.LC = LC; L.NA = NA; L.NU = (N + 63) / 64;
+  int o = 0;
+  L.o_flags = o; o += S;
+  L.o_pn = o; o += S;
+  L.o_nn = o; o += S;
+  L.o_plist = o; o += S * LC;
+  L.o_nlist = o; o += S * LC;
+  L.o_seslot = o; o += R * S;
+  L.o_ndnext = o; o += N;
+  L.o_ndnull = o; o += N;
+  L.o_init = o; o += 1;
+  L.n32 = o;
+  o = 0;
+  L.o_seused = o; o += 1;
+  L.o_ndused = o; o += L.NU;
+  L.o_sets = o; o += R;
+  L.o_ndseq = o; o += N;
+  L.o_ndts = o; o += N;
+  L.o_ndval = o; o += N * NA;
+  L.n64 = o;
+}
+
+}  // namespace kg
+}  // namespace sdh

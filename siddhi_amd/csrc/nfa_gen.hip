@@ -1,0 +1,280 @@
+// nfa_gen.hip -- K_gen: the general NFA step, one lane per query instance (query, partition key),
+// plus the device-side partition routing that feeds it.
+//
+// Mapping to CDNA4: a wave is 64 instances that see the SAME event sequence -- 64 queries of one
+// partition for one key (or 64 unpartitioned queries of one stream) -- so every event is read at
+// one uniform address by the whole wave. Each lane runs the reference's processor logic
+// (kgen.h: pending / newAndEvery lists, StateEvent + StreamEvent-chain pools, mark/sweep) over its
+// instance arena in HBM. Arenas are lane-interleaved ([block][word][lane]) so that lanes touching the
+// same logical field coalesce into one 256-B access. Matches go to lane-private output chunks
+// (one atomic per 4 KiB chunk) and are ordered by the host (R18 sort key).
+//
+// Partition routing (PartitionStreamReceiver.java:80-281, R19): key = the partition attribute's
+// value (String.valueOf identity on raw words, NaN canonical); null keys drop the event. Keys get
+// dense ids from a device hash table (open addressing, CAS on the key word); events are grouped by
+// key with a stable radix sort of (key id, event index), so each key's events keep their order.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "kgen.h"
+#include "nfa_types.h"
+
+namespace sdh {
+
+namespace {
+
+template <class T, int N>
+__device__ __forceinline__ T gpick(const T (&arr)[N], int idx) {
+  T v = arr[0];
+#pragma unroll
+  for (int c = 1; c < N; ++c) v = (idx == c) ? arr[c] : v;
+  return v;
+}
+
+__device__ __forceinline__ int64_t raw_word(const StreamBatch& b, int attr, int64_t e, bool& isnull) {
+  const void* p = gpick(b.col, attr);
+  const uint8_t* nl = gpick(b.nul, attr);
+  const int w = gpick(b.width, attr);
+  isnull = nl && nl[e];
+  if (w == 8) return ((const int64_t*)p)[e];
+  if (w == 4) return (int64_t)((const int32_t*)p)[e];  // int / string id sign-extended; float bits
+  return (int64_t)((const uint8_t*)p)[e];
+}
+
+// lane-private output: records [len, qid, key, ts, seq, idx, S, (count, seqs...)xS]
+struct LaneOut {
+  int64_t* out;
+  int64_t n_chunks;
+  int32_t cw;
+  int32_t* next;
+  int64_t chunk = -1;
+  int32_t fill = 0;
+  bool over = false;
+  __device__ void close() {
+    if (chunk >= 0) out[chunk * cw] = fill;
+    chunk = -1;
+  }
+  __device__ int64_t* reserve(int words) {
+    if (over) return nullptr;
+    if (words + 1 > cw) { over = true; return nullptr; }
+    if (chunk < 0 || fill + words > cw - 1) {
+      close();
+      const int64_t c = atomicAdd(next, 1);
+      if (c >= n_chunks) { over = true; return nullptr; }
+      chunk = c;
+      fill = 0;
+    }
+    int64_t* p = out + chunk * cw + 1 + fill;
+    fill += words;
+    return p;
+  }
+};
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void nfa_gen_kernel(GenLaunch L) {
+  const int lane = threadIdx.x;
+  const int item = blockIdx.x;
+  if (item >= L.n_items) return;
+  const int seg = item / L.groups, g = item % L.groups;
+  int64_t e0 = 0, e1 = L.b.n;
+  uint32_t kid = 0;
+  if (L.seg_begin) {
+    kid = L.seg_kid[seg];
+    if (kid == 0xFFFFFFFFu) return;  // events with a null partition key
+    e0 = L.seg_begin[seg];
+    e1 = e0 + L.seg_len[seg];
+  }
+  const int qi = L.lane_q[(int64_t)(L.group_base + g) * 64 + lane];
+  if (qi < 0) return;
+  const kg::GQuery* __restrict__ q = L.queries + qi;
+  if (q->recv_n[L.b.stream] == 0) return;  // this query does not read the stream
+  const int64_t block = L.block_base + (int64_t)kid * L.groups + g;
+  kg::Ctx c;
+  c.q = q;
+  c.w32 = L.a32 + block * L.B32 * 64 + lane;
+  c.w64 = L.a64 + block * L.B64 * 64 + lane;
+  c.stride = 64;
+  c.err = kg::GE_OK;
+  c.npin = 0;
+  c.n_ret = 0;
+  c.stream = L.b.stream;
+  const int64_t key = L.key_of_id ? L.key_of_id[kid] : -1;
+  if (c.i32(q->lay.o_init) == 0) {  // PartitionRuntime.cloneIfNotExist / QueryRuntime.init: seed
+    c.init_instance();
+    c.i32(q->lay.o_init) = 1;
+  }
+  LaneOut o{L.out, L.n_chunks, L.chunk_words, L.chunk_next};
+  const int S = q->n_states;
+  const int ncap = q->n_cap[c.stream];
+  unsigned long long nrec = 0;
+  for (int64_t k = e0; k < e1 && c.err == kg::GE_OK; ++k) {
+    const int64_t e = L.ev_idx ? L.ev_idx[k] : k;
+    c.seq = L.b.seq_base + e;
+    c.ts = L.b.ts[e];
+    c.ev_null = 0;
+    for (int j = 0; j < ncap; ++j) {
+      bool nl;
+      c.ev_val[j] = raw_word(L.b, q->cap_attr[c.stream][j], e, nl);
+      if (nl) c.ev_null |= 1u << j;
+    }
+    int64_t idx = 0;
+    auto emit = [&](const kg::Ctx& cx, int se) {
+      int words = 7;
+      for (int i = 0; i < S; ++i) {
+        words += 1;
+        for (int n = cx.slot(se, i); n >= 0; n = cx.nd_next(n)) ++words;
+      }
+      ++nrec;
+      if (!L.write_records) return;
+      int64_t* r = o.reserve(words);
+      if (!r) return;
+      r[0] = words;
+      r[1] = q->qid;
+      r[2] = key;
+      r[3] = cx.se_ts(se);
+      r[4] = cx.seq;
+      r[5] = idx++;
+      r[6] = S | (c.stream << 16);
+      int w = 7;
+      for (int i = 0; i < S; ++i) {
+        const int cw = w++;
+        int64_t cnt = 0;
+        for (int n = cx.slot(se, i); n >= 0; n = cx.nd_next(n)) {
+          r[w++] = cx.nd_seq(n);
+          ++cnt;
+        }
+        r[cw] = cnt;
+      }
+    };
+    c.receive(emit);
+  }
+  o.close();
+  if (nrec) atomicAdd(L.rec_count, nrec);
+  if (c.err == kg::GE_CAPACITY) atomicOr(&L.err[0], 1);
+  if (c.err == kg::GE_REFERENCE) atomicOr(&L.err[1], 1);
+  if (o.over) atomicOr(&L.err[2], 1);
+}
+
+// ---- partition routing ----
+__global__ void gen_keys_kernel(StreamBatch b, int attr, int type, int64_t* key, uint32_t* kid) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= b.n) return;
+  bool nl;
+  int64_t raw = raw_word(b, attr, e, nl);
+  if (type == kg::T_FLOAT) {
+    const float f = __uint_as_float((uint32_t)raw);
+    raw = (f != f) ? 0x7fc00000 : (int64_t)(uint32_t)raw;
+  } else if (type == kg::T_DOUBLE) {
+    const double d = __longlong_as_double(raw);
+    if (d != d) raw = 0x7ff8000000000000LL;
+  }
+  key[e] = raw;
+  kid[e] = nl ? 0xFFFFFFFFu : 0u;  // 0 = valid, resolved by the lookup
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+constexpr long long KEY_EMPTY = (long long)0x8000000000000000ull;  // INT64_MIN keys use slot `cap`
+
+__global__ void gen_insert_kernel(int64_t n, const int64_t* key, const uint32_t* kid, unsigned long long* tkey,
+                                  int64_t mask, int32_t* err) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n || kid[e] == 0xFFFFFFFFu) return;
+  const long long k = key[e];
+  if (k == KEY_EMPTY) {  // the INT64_MIN key lives in the extra slot mask+1 (1 = present)
+    tkey[mask + 1] = 1ull;
+    return;
+  }
+  int64_t h = (int64_t)(mix64((uint64_t)k) & (uint64_t)mask);
+  for (int64_t p = 0; p <= mask; ++p) {
+    const unsigned long long cur = atomicCAS(&tkey[h], (unsigned long long)KEY_EMPTY, (unsigned long long)k);
+    if (cur == (unsigned long long)KEY_EMPTY || cur == (unsigned long long)k) return;
+    h = (h + 1) & mask;
+  }
+  atomicOr(err, 1);
+}
+
+__global__ void gen_assign_kernel(const unsigned long long* tkey, int32_t* tid, int64_t slots, int32_t* n_keys,
+                                  int64_t* key_of_id, int64_t key_cap, int32_t* err) {
+  const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= slots) return;
+  const bool special = h == slots - 1;  // INT64_MIN key slot (initialized to 0, 1 = present)
+  const bool used = special ? tkey[h] == 1ull : tkey[h] != (unsigned long long)KEY_EMPTY;
+  if (!used || tid[h] >= 0) return;
+  const int32_t id = atomicAdd(n_keys, 1);
+  if (id >= key_cap) {
+    atomicOr(err, 1);
+    return;
+  }
+  tid[h] = id;
+  key_of_id[id] = special ? INT64_MIN : (int64_t)tkey[h];
+}
+
+__global__ void gen_lookup_kernel(int64_t n, const int64_t* key, uint32_t* kid, int32_t* idx,
+                                  const unsigned long long* tkey, const int32_t* tid, int64_t mask) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  idx[e] = (int32_t)e;
+  if (kid[e] == 0xFFFFFFFFu) return;
+  const long long k = key[e];
+  if (k == KEY_EMPTY) {
+    kid[e] = (uint32_t)tid[mask + 1];
+    return;
+  }
+  int64_t h = (int64_t)(mix64((uint64_t)k) & (uint64_t)mask);
+  while (tkey[h] != (unsigned long long)k) h = (h + 1) & mask;
+  kid[e] = (uint32_t)tid[h];
+}
+
+}  // namespace sdh
+
+extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s) {
+  if (L->n_items <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::nfa_gen_kernel, dim3(L->n_items), dim3(64), 0, s, *L);
+  return hipGetLastError();
+}
+
+// Route batch B of a partitioned stream: dense key ids (persistent hash table), then events grouped
+// by key id (stable). Outputs: sorted kids/idx, run-length segments; *n_seg on the host.
+// Scratch: key[n], kid[n], kid_sorted[n], idx[n], idx_sorted[n], uniq[n], cnt[n], off[n], temp.
+extern "C" hipError_t sdh_route_partition(const sdh::StreamBatch* B, int attr, int type, unsigned long long* tkey,
+                                          int32_t* tid, int64_t table_mask, int32_t* n_keys, int64_t* key_of_id,
+                                          int64_t key_cap, int64_t* key, uint32_t* kid, uint32_t* kid_sorted,
+                                          int32_t* idx, int32_t* idx_sorted, uint32_t* uniq, int32_t* cnt,
+                                          int32_t* off, int32_t* n_runs_dev, void* temp, size_t temp_bytes,
+                                          int32_t* err, hipStream_t s) {
+  const int64_t n = B->n;
+  const int T = 256;
+  const int nb = (int)((n + T - 1) / T);
+  hipLaunchKernelGGL(sdh::gen_keys_kernel, dim3(nb), dim3(T), 0, s, *B, attr, type, key, kid);
+  hipLaunchKernelGGL(sdh::gen_insert_kernel, dim3(nb), dim3(T), 0, s, n, key, kid, tkey, table_mask, err);
+  const int64_t slots = table_mask + 2;
+  hipLaunchKernelGGL(sdh::gen_assign_kernel, dim3((int)((slots + T - 1) / T)), dim3(T), 0, s, tkey, tid, slots,
+                     n_keys, key_of_id, key_cap, err);
+  hipLaunchKernelGGL(sdh::gen_lookup_kernel, dim3(nb), dim3(T), 0, s, n, key, kid, idx, tkey, tid, table_mask);
+  size_t tb = temp_bytes;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, tb, kid, kid_sorted, idx, idx_sorted, (int)n, 0, 32, s);
+  if (e != hipSuccess) return e;
+  tb = temp_bytes;
+  e = hipcub::DeviceRunLengthEncode::Encode(temp, tb, kid_sorted, uniq, cnt, n_runs_dev, (int)n, s);
+  if (e != hipSuccess) return e;
+  tb = temp_bytes;
+  e = hipcub::DeviceScan::ExclusiveSum(temp, tb, cnt, off, (int)n, s);
+  return e == hipSuccess ? hipGetLastError() : e;
+}
+
+// temp storage the routing needs for n events
+extern "C" size_t sdh_route_temp_bytes(int64_t n) {
+  size_t a = 0, b = 0, c = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs((void*)nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
+                                     (int32_t*)nullptr, (int)n, 0, 32);
+  (void)hipcub::DeviceRunLengthEncode::Encode((void*)nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
+                                        (int32_t*)nullptr, (int)n);
+  (void)hipcub::DeviceScan::ExclusiveSum((void*)nullptr, c, (int32_t*)nullptr, (int32_t*)nullptr, (int)n);
+  return std::max(a, std::max(b, c)) + 256;
+}

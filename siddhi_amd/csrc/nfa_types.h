@@ -191,4 +191,37 @@ struct RatchetLaunch {
   int32_t* err;                 // [0] deque overflow, [1] unordered ts, [2] match overflow
 };
 
+// ------------------------------------------------------------------------------------------
+// K_gen launch (nfa_gen.hip): item = (segment of one key's events, group of 64 queries)
+// ------------------------------------------------------------------------------------------
+namespace kg {
+struct GQuery;
+}
+
+struct GenLaunch {
+  const kg::GQuery* queries;
+  const int32_t* lane_q;      // [group][64] query index (-1 = idle lane)
+  StreamBatch b;
+  const int32_t* seg_begin;   // [n_seg] ranges into ev_idx (nullptr: one segment = whole batch)
+  const int32_t* seg_len;
+  const uint32_t* seg_kid;    // dense key id per segment (0xFFFFFFFF: dropped events)
+  const int64_t* key_of_id;   // raw key per dense id (nullptr: unpartitioned, key -1)
+  const int32_t* ev_idx;      // event indices grouped by key (nullptr: identity)
+  int32_t groups;             // groups per segment
+  int32_t group_base;         // first row of lane_q for this launch
+  int64_t block_base;         // arena block of (kid, g) = block_base + kid * groups + g
+  int32_t* a32;
+  int64_t* a64;
+  int32_t B32, B64;           // arena words per lane and block
+  int64_t* out;               // chunks of chunk_words int64: [used, records...]
+  int64_t n_chunks;
+  int32_t chunk_words;
+  int32_t n_items;
+  int32_t* chunk_next;
+  int32_t* err;               // [0] instance capacity, [1] reference would throw, [2] output overflow
+  unsigned long long* rec_count;  // matches emitted (records), counted even when not written
+  int32_t write_records;      // 0: count only (device-resident benchmarking mode)
+  int32_t pad;
+};
+
 }  // namespace sdh

@@ -17,6 +17,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsiddhi_h
 
 SDH_OK = 0
 SDH_FLAG_DEVICE_MATCHES = 1
+SDH_FLAG_NO_RATCHET = 2
+SDH_FLAG_FORCE_GEN = 4
 ERRORS = {-1: "SDH_E_INVALID", -2: "SDH_E_UNSUPPORTED", -3: "SDH_E_DEVICE", -4: "SDH_E_CAPACITY",
           -5: "SDH_E_REFERENCE"}
 
@@ -25,7 +27,10 @@ class SdhConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("shard_rank", ctypes.c_int32),
                 ("shard_world", ctypes.c_int32), ("partials_per_inst", ctypes.c_int32),
                 ("max_batch", ctypes.c_int64), ("match_capacity", ctypes.c_int64),
-                ("chunk_events", ctypes.c_int32), ("flags", ctypes.c_int32)]
+                ("chunk_events", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("gen_pool_states", ctypes.c_int32), ("gen_pool_nodes", ctypes.c_int32),
+                ("gen_list_cap", ctypes.c_int32), ("gen_pad", ctypes.c_int32),
+                ("gen_max_keys", ctypes.c_int64)]
 
 
 class SdhBatch(ctypes.Structure):
@@ -110,11 +115,15 @@ class HipEngine:
     """One engine instance on one GPU."""
 
     def __init__(self, blob: bytes, device: int = 0, partials: int = 128, shard_rank: int = 0,
-                 shard_world: int = 1, chunk_events: int = 0, stream_types=None, flags: int = 0):
+                 shard_world: int = 1, chunk_events: int = 0, stream_types=None, flags: int = 0,
+                 gen_pool_states: int = 0, gen_pool_nodes: int = 0, gen_list_cap: int = 0,
+                 gen_max_keys: int = 0):
         self.lib = load_library()
         cfg = SdhConfig(device=device, shard_rank=shard_rank, shard_world=shard_world,
                         partials_per_inst=partials, max_batch=0, match_capacity=0,
-                        chunk_events=chunk_events, flags=flags)
+                        chunk_events=chunk_events, flags=flags, gen_pool_states=gen_pool_states,
+                        gen_pool_nodes=gen_pool_nodes, gen_list_cap=gen_list_cap, gen_pad=0,
+                        gen_max_keys=gen_max_keys)
         self.h = ctypes.c_void_p()
         self._blob = ctypes.create_string_buffer(blob, len(blob))
         rc = self.lib.sdh_engine_create(self._blob, len(blob), ctypes.byref(cfg), ctypes.byref(self.h))

@@ -1,0 +1,195 @@
+// kgen_host.cpp -- TEST INFRASTRUCTURE ONLY: the K_gen interpreter (siddhi_amd/csrc/kgen.h, the
+// per-lane body of the device kernel) compiled for the host with one lane per instance, driven the
+// way nfa_gen.hip drives it (instances own the whole batch; matches re-ordered by the output
+// sort key), so the restatement can be cross-checked against the oracle and the reference KATs on
+// a machine without a GPU. Never part of the product path (libsiddhi_hip.so does not link it).
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../siddhi_amd/csrc/gen_lower.h"
+
+using namespace sdh::kg;
+
+namespace {
+
+struct Rec {
+  int64_t seq, rank, idx;
+  int64_t query, key, ts;
+  std::vector<std::vector<int64_t>> slots;
+};
+
+struct Inst {
+  int qi;
+  int64_t key;
+  std::vector<int32_t> w32;
+  std::vector<int64_t> w64;
+  bool init = false;
+};
+
+struct Host {
+  LProgram P;
+  std::vector<GQuery> gq;  // per query
+  std::vector<int> rank;
+  std::vector<std::unique_ptr<Inst>> top;                       // unpartitioned instances
+  std::vector<std::map<int64_t, std::vector<std::unique_ptr<Inst>>>> part;
+  std::vector<Rec> out;
+  std::string err;
+};
+
+Inst* make_inst(Host* h, int qi, int64_t key) {
+  auto* in = new Inst;
+  in->qi = qi;
+  in->key = key;
+  in->w32.assign(h->gq[qi].lay.n32, 0);
+  in->w64.assign(h->gq[qi].lay.n64, 0);
+  return in;
+}
+
+// run one event through one instance (what one lane does for one event)
+void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* vals, const uint8_t* nulls) {
+  const GQuery& q = h->gq[in->qi];
+  Ctx c{};
+  c.q = &q;
+  c.w32 = in->w32.data();
+  c.w64 = in->w64.data();
+  c.stride = 1;
+  c.npin = 0;
+  c.n_ret = 0;
+  c.err = GE_OK;
+  if (!in->init) {
+    c.seq = seq;
+    c.ts = ts;
+    c.stream = stream;
+    c.init_instance();
+    in->init = true;
+  }
+  c.seq = seq;
+  c.ts = ts;
+  c.stream = stream;
+  c.ev_null = 0;
+  for (int j = 0; j < q.n_cap[stream]; ++j) {
+    const int a = q.cap_attr[stream][j];
+    c.ev_val[j] = vals[a];
+    if (nulls && nulls[a]) c.ev_null |= 1u << j;
+  }
+  int64_t idx = 0;
+  auto emit = [&](const Ctx& cx, int se) {
+    Rec r;
+    r.seq = seq;
+    r.rank = h->rank[(size_t)in->qi * h->P.stream_types.size() + stream];
+    r.idx = idx++;
+    r.query = in->qi;
+    r.key = in->key;
+    r.ts = cx.se_ts(se);
+    for (int i = 0; i < cx.nS(); ++i) {
+      std::vector<int64_t> ch;
+      for (int n = cx.slot(se, i); n >= 0; n = cx.nd_next(n)) ch.push_back(cx.nd_seq(n));
+      r.slots.push_back(ch);
+    }
+    h->out.push_back(r);
+  };
+  c.receive(emit);
+  if (c.err == GE_CAPACITY) throw std::runtime_error("K_gen instance capacity exceeded");
+  if (c.err == GE_REFERENCE) throw std::runtime_error("reference engine would throw here");
+}
+
+}  // namespace
+
+extern "C" {
+
+void* kgh_create(const void* blob, size_t len, int R, int N, int LC) {
+  try {
+    auto* h = new Host;
+    h->P = read_program(blob, len);
+    Sizing sz;
+    if (R > 0) sz.R = R;
+    if (N > 0) sz.N = N;
+    if (LC > 0) sz.LC = LC;
+    for (int qi = 0; qi < (int)h->P.q.size(); ++qi) h->gq.push_back(lower_gen(h->P, qi, sz));
+    h->rank = output_ranks(h->P);
+    h->top.resize(h->P.q.size());
+    for (int qi = 0; qi < (int)h->P.q.size(); ++qi)
+      if (h->P.q[qi].partition < 0) h->top[qi].reset(make_inst(h, qi, -1));
+    h->part.resize(h->P.parts.size());
+    return h;
+  } catch (const std::exception&) {
+    return nullptr;
+  }
+}
+
+// events are delivered one at a time (per-event sends), like sdh_engine_push
+int kgh_send(void* hp, int stream, int64_t n, int64_t seq0, const int64_t* ts, const int64_t* vals,
+             const uint8_t* nulls) {
+  Host* h = (Host*)hp;
+  try {
+    const size_t na = h->P.stream_types[stream].size();
+    // every instance processes the whole batch (the device order), then matches are sorted
+    for (auto& in : h->top)
+      if (in)
+        for (int64_t k = 0; k < n; ++k)
+          run(h, in.get(), stream, seq0 + k, ts[k], vals + k * na, nulls ? nulls + k * na : nullptr);
+    for (size_t pi = 0; pi < h->P.parts.size(); ++pi) {
+      const LPart& pd = h->P.parts[pi];
+      for (const auto& key : pd.keys) {
+        if (key.stream != stream) continue;
+        const int attr = (int)key.code[0].imm;
+        const int type = h->P.stream_types[stream][attr];
+        for (int64_t k = 0; k < n; ++k) {
+          if (nulls && nulls[k * na + attr]) continue;  // null key drops the event
+          const int64_t kv = key_of_raw(type, vals[k * na + attr]);
+          auto it = h->part[pi].find(kv);
+          if (it == h->part[pi].end()) {
+            std::vector<std::unique_ptr<Inst>> v;
+            for (int pq : pd.queries) v.emplace_back(make_inst(h, pq, kv));
+            it = h->part[pi].emplace(kv, std::move(v)).first;
+          }
+          for (auto& in : it->second)
+            run(h, in.get(), stream, seq0 + k, ts[k], vals + k * na, nulls ? nulls + k * na : nullptr);
+        }
+      }
+    }
+    std::stable_sort(h->out.begin(), h->out.end(), [](const Rec& a, const Rec& b) {
+      if (a.seq != b.seq) return a.seq < b.seq;
+      if (a.rank != b.rank) return a.rank < b.rank;
+      return a.idx < b.idx;
+    });
+    return 0;
+  } catch (const std::exception& ex) {
+    h->err = ex.what();
+    return -1;
+  }
+}
+
+int64_t kgh_num_matches(void* hp) { return (int64_t)((Host*)hp)->out.size(); }
+int64_t kgh_match_words(void* hp) {
+  int64_t w = 0;
+  for (auto& r : ((Host*)hp)->out)
+    for (auto& s : r.slots) w += 1 + (int64_t)s.size();
+  return w;
+}
+int kgh_get_matches(void* hp, int64_t* query, int64_t* key, int64_t* ts, int64_t* off, int64_t* words) {
+  Host* h = (Host*)hp;
+  int64_t w = 0;
+  for (size_t i = 0; i < h->out.size(); ++i) {
+    const Rec& r = h->out[i];
+    query[i] = r.query;
+    key[i] = r.key;
+    ts[i] = r.ts;
+    off[i] = w;
+    for (auto& s : r.slots) {
+      words[w++] = (int64_t)s.size();
+      for (int64_t x : s) words[w++] = x;
+    }
+  }
+  off[h->out.size()] = w;
+  return 0;
+}
+void kgh_clear(void* hp) { ((Host*)hp)->out.clear(); }
+const char* kgh_error(void* hp) { return ((Host*)hp)->err.c_str(); }
+void kgh_destroy(void* hp) { delete (Host*)hp; }
+
+}  // extern "C"

@@ -14,58 +14,11 @@ pytestmark = pytest.mark.gpu
 KAT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kat.json")))
 
 
-def hip_factory(**kw):
-    from siddhi_amd.engine import HipEngine
-
-    def make(blob, _kw=kw):
-        return HipEngine(blob, **_kw)
-    return make
-
-
 def hip_app(src, **kw):
     app = App(src, engine_factory=lambda blob: None)
     from siddhi_amd.engine import HipEngine
     app.engine = HipEngine(app.blob, stream_types=[s.attr_types for s in app.ir.streams], **kw)
     return app
-
-
-def chain_fixtures():
-    from siddhi_amd.engine import EngineError  # noqa: F401
-    out = []
-    for fx in KAT["fixtures"]:
-        src = fx["app"]
-        if any(k in src for k in ("partition", "<", "*", "+", "?", " and ", " or ", ",")):
-            pass
-        out.append(fx)
-    return out
-
-
-def run_both(fx):
-    o = App(fx["app"])
-    try:
-        g = hip_app(fx["app"])
-    except Exception as ex:  # unsupported on the chain kernel: must be a loud SDH_E_UNSUPPORTED
-        from siddhi_amd.engine import EngineError
-        assert isinstance(ex, EngineError) and ex.code == -2, ex
-        return None, None
-    for ev in fx["events"]:
-        row = [[parse_literal(t) for t in ev["data"]]]
-        o.send(ev["stream"], row, [ev["ts"]])
-        g.send(ev["stream"], row, [ev["ts"]])
-    return o.matches, g.matches
-
-
-@pytest.mark.parametrize("fx", KAT["fixtures"], ids=[f["id"] for f in KAT["fixtures"]])
-def test_reference_kat_on_gpu(fx):
-    try:
-        o, g = run_both(fx)
-    except (SiddhiAppCreationException, Exception) as ex:
-        if "outside the accelerated path" in str(ex) or isinstance(ex, SiddhiAppCreationException):
-            pytest.skip("out of scope")
-        raise
-    if o is None:
-        pytest.skip("query shape not on the GPU path yet")
-    assert g == o
 
 
 def c2_columns(start, n):

@@ -1,0 +1,145 @@
+"""GPU parity of K_gen (the general per-instance interpreter) and of the plan selection as a whole,
+against the CPU oracle: every in-scope reference KAT, seeded random apps (count, logical, sequences,
+partitions, arithmetic, nulls), batched pushes through the device partition routing."""
+import numpy as np
+import pytest
+
+from fuzz_apps import random_app, random_events
+from harness import App, OracleError
+from siddhi_amd.ql import SiddhiAppCreationException, SiddhiParserException
+from test_oracle_reference_kat import KAT, OUT_OF_SCOPE, check_rows, run_fixture
+
+pytestmark = pytest.mark.gpu
+
+SDH_FLAG_FORCE_GEN = 4
+FIXTURES = [f for f in KAT["fixtures"] if f["id"] not in OUT_OF_SCOPE]
+
+
+def hip_factory(**kw):
+    def make(blob):
+        from siddhi_amd.engine import HipEngine
+        return HipEngine(blob, **kw)
+    return make
+
+
+def hip_app(src, **kw):
+    app = App(src, engine_factory=lambda blob: None)
+    from siddhi_amd.engine import HipEngine
+    app.engine = HipEngine(app.blob, stream_types=[s.attr_types for s in app.ir.streams], **kw)
+    return app
+
+
+def _types_factory(flags):
+    def make_app(fx):
+        a = App(fx["app"], engine_factory=lambda blob: None)
+        from siddhi_amd.engine import HipEngine
+        return HipEngine(a.blob, stream_types=[s.attr_types for s in a.ir.streams], flags=flags)
+    return make_app
+
+
+@pytest.mark.parametrize("flags", [0, SDH_FLAG_FORCE_GEN], ids=["planned", "force_gen"])
+@pytest.mark.parametrize("fx", FIXTURES, ids=[f["id"] for f in FIXTURES])
+def test_reference_kat_on_gpu(fx, flags):
+    try:
+        o, _ = run_fixture(fx)
+    except OracleError:
+        pytest.skip("the reference engine throws on this stream")
+    probe = App(fx["app"], engine_factory=lambda blob: None)
+    types = [s.attr_types for s in probe.ir.streams]
+    g, grows = run_fixture(fx, engine_factory=hip_factory(stream_types=types, flags=flags))
+    assert g.matches == o.matches
+    check_rows(fx, grows)
+
+
+def _fuzz(seed, flags, batch):
+    src = random_app(seed, partition=seed % 3 == 0)
+    try:
+        o = App(src)
+    except (SiddhiAppCreationException, SiddhiParserException):
+        return None
+    g = hip_app(src, flags=flags)
+    ev = random_events(seed)
+    by = {}
+    try:
+        if batch:
+            # runs of same-stream events pushed as one batch (device routing + sort)
+            i = 0
+            while i < len(ev):
+                j = i
+                while j < len(ev) and ev[j][0] == ev[i][0] and j - i < 40:
+                    j += 1
+                rows = [r for _, r, _ in ev[i:j]]
+                ts = [t for _, _, t in ev[i:j]]
+                o.send(ev[i][0], rows, ts)
+                g.send(ev[i][0], rows, ts)
+                i = j
+        else:
+            for stream, row, t in ev:
+                o.send(stream, [row], [t])
+                g.send(stream, [row], [t])
+    except OracleError:
+        return None
+    except Exception as ex:  # loud capacity errors are allowed, wrong answers are not
+        from siddhi_amd.engine import EngineError
+        if isinstance(ex, EngineError) and ex.code == -4:
+            return "capacity"
+        raise
+    return o, g
+
+
+@pytest.mark.parametrize("batch", [False, True], ids=["per_event", "batched"])
+@pytest.mark.parametrize("seed", range(40))
+def test_fuzz_apps_on_gpu(seed, batch):
+    r = _fuzz(seed, 0, batch)
+    if r is None:
+        pytest.skip("app rejected by the planner or the reference would throw")
+    if r == "capacity":
+        pytest.skip("instance pools exceeded (loud SDH_E_CAPACITY)")
+    o, g = r
+    assert g.matches == o.matches
+
+
+def test_partitioned_many_keys_batched():
+    """count <2:4> and logical and/or over 700 partition keys, batches of 2000 events."""
+    src = ("define stream S (sym int, price float, vol int); "
+           "partition with (sym of S) begin "
+           "@info(name='c') from every e1=S[price > 60] <2:4> -> e2=S[price > e1[last].price] within 40 "
+           "milliseconds select e1[0].price as a, e2.price as b insert into O; "
+           "@info(name='a') from every e1=S[price > 50] -> e2=S[vol > 500] and e3=S[price < 20] within 60 "
+           "milliseconds select e1.price as a insert into O; "
+           "@info(name='o') from every e1=S[vol < 100] -> e2=S[price > 90] or e3=S[vol > 990] within 30 "
+           "milliseconds select e1.vol as a insert into O; "
+           "@info(name='s') from every e1=S[price > 80], e2=S[price > e1.price] select e1.price as a insert into O; "
+           "end;")
+    o = App(src)
+    g = hip_app(src, gen_pool_states=32, gen_pool_nodes=64, gen_list_cap=32)
+    rng = np.random.default_rng(4)
+    n = 20000
+    ts = np.arange(n, dtype=np.int64) // 4
+    sym = rng.integers(0, 700, n).astype(np.int32)
+    price = (rng.integers(0, 10000, n) / 100.0).astype(np.float32)
+    vol = rng.integers(0, 1000, n).astype(np.int32)
+    vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64), vol.astype(np.int64)], 1)
+    for lo in range(0, n, 2000):
+        o.engine.send(0, ts[lo:lo + 2000], vals[lo:lo + 2000], None)
+        g.engine.push_columns(0, ts[lo:lo + 2000], [sym[lo:lo + 2000], price[lo:lo + 2000].view(np.uint32),
+                                                    vol[lo:lo + 2000]])
+        om = o.engine.take_matches(lambda q: len(o.ir.queries[q].states))
+        gm = g.engine.take_matches(lambda q: len(o.ir.queries[q].states))
+        assert gm == om
+    assert g.engine.stats().matches > 1000
+
+
+def test_force_gen_matches_chain_plans_on_c2():
+    from siddhi_amd.workloads import c2_app, stock_events
+    src = c2_app(40)
+    r = hip_app(src)
+    k = hip_app(src, flags=SDH_FLAG_FORCE_GEN)
+    ts, sym, price, vol = stock_events(0, 6000)
+    cols = [sym, price.view(np.uint32), vol]
+    r.engine.push_columns(0, ts, cols)
+    k.engine.push_columns(0, ts, cols)
+    a, b = r.engine.poll(), k.engine.poll()
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert len(a[0]) > 10000
