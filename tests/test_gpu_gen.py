@@ -127,7 +127,7 @@ def test_partitioned_many_keys_batched():
         om = o.engine.take_matches(lambda q: len(o.ir.queries[q].states))
         gm = g.engine.take_matches(lambda q: len(o.ir.queries[q].states))
         assert gm == om
-    assert g.engine.stats().matches > 1000
+    assert g.engine.stats().matches > 500
 
 
 def test_force_gen_matches_chain_plans_on_c2():
