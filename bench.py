@@ -29,6 +29,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=["c2", "c3"], default="c2",
+                    help="c2: BASELINE configs[1] (headline); c3: configs[2] (count/logical, partitioned)")
+    ap.add_argument("--keys", type=int, default=10000, help="C3 partition keys (symbols)")
     ap.add_argument("--patterns", type=int, default=1000)
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--partials", type=int, default=128)
@@ -48,29 +51,46 @@ def c2_app_for_rank(rank, P):
     return " ".join(qs)
 
 
-def cpu_baseline(app_src, budget_s):
+def cpu_baseline(workload, n_symbols, budget_s):
     """Reference-semantics CPU engine (the oracle, single thread) on a bounded sample of the
-    same workload: the first 32 patterns over consecutive batches of the same stream until the
-    time budget is spent."""
+    same workload: the first 32 patterns of the family over consecutive batches of the same
+    stream until the time budget is spent."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from harness import App
-    from siddhi_amd.workloads import c2_app, stock_events
+    from siddhi_amd.workloads import c2_app, c3_app, stock_events
     P = 32
-    app = App(c2_app(P))
+    app = App(c2_app(P) if workload == "c2" else c3_app(P))
+    nslots = [len(q.states) for q in app.ir.queries]
     done, t0, start = 0, time.perf_counter(), 0
     n = 20000
     while time.perf_counter() - t0 < budget_s:
-        ts, sym, price, vol = stock_events(start, n)
+        ts, sym, price, vol = stock_events(start, n, n_symbols=n_symbols)
         vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64),
                          vol.astype(np.int64)], 1)
         app.engine.send(0, ts, vals, None)
-        app.engine.take_matches(lambda q: 2)
+        app.engine.take_matches(lambda q: nslots[q])
         start += n
         done += n
     dt = time.perf_counter() - t0
     return {"value": done * P / dt, "unit": "pattern-events/s", "cores": 1, "kind": "port",
-            "sample": f"{P} C2 patterns x {done} events (oracle/liboracle.so, 1 thread, "
+            "sample": f"{P} {workload.upper()} patterns x {done} events (oracle/liboracle.so, 1 thread, "
                       f"{dt:.1f} s)"}
+
+
+def profiled_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC run of this same command
+    (profiles/*/counters.json; FETCH_SIZE x2 gfx950 streaming-read correction + WRITE_SIZE, KiB)."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "counters.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:  # noqa: BLE001
+            continue
+        for k, c in d.items():
+            if kernel in k and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                best = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0, os.path.relpath(f, ROOT)
+    return best
 
 
 def main():
@@ -92,15 +112,22 @@ def main():
     from siddhi_amd.workloads import stock_events
 
     P = args.patterns
-    ir = plan(ql.parse(c2_app_for_rank(rank, P)))
-    eng = HipEngine(ir.serialize(), device=local, partials=args.partials, flags=SDH_FLAG_DEVICE_MATCHES)
+    K = args.keys if args.workload == "c3" else 100
+    if args.workload == "c2":
+        ir = plan(ql.parse(c2_app_for_rank(rank, P)))
+        eng = HipEngine(ir.serialize(), device=local, partials=args.partials, flags=SDH_FLAG_DEVICE_MATCHES)
+    else:
+        from siddhi_amd.workloads import c3_app
+        ir = plan(ql.parse(c3_app(P, first=rank * P)))
+        eng = HipEngine(ir.serialize(), device=local, flags=SDH_FLAG_DEVICE_MATCHES, gen_pool_states=32,
+                        gen_pool_nodes=128, gen_list_cap=32, gen_max_keys=max(1024, 2 * K))
 
     B = args.batch
     n_batches = args.warmup + args.steps
     # synthetic batches resident in HBM before the timed region
     batches = []
     for s in range(n_batches):
-        ts, sym, price, vol = stock_events(s * B, B)
+        ts, sym, price, vol = stock_events(s * B, B, n_symbols=K)
         batches.append((torch.from_numpy(ts).to(dev), torch.from_numpy(sym).to(dev),
                         torch.from_numpy(price.view(np.int32)).to(dev), torch.from_numpy(vol).to(dev)))
     torch.cuda.synchronize()
@@ -140,6 +167,15 @@ def main():
     avg_bytes = float(np.mean(kern_bytes))
     achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
     peak = 8000.0
+    if args.workload == "c2":
+        wl = ("C2: 1K concurrent 2-state filter+reference patterns "
+              "(every e1[price>T_p] -> e2[price>e1.price] within W_p)")
+        kernel = "nfa_ratchet_kernel"
+    else:
+        wl = (f"C3: count <2:5> + logical and/or patterns, partition with (symbol) over {K} keys, "
+              "within 10 sec")
+        kernel = "nfa_gen_kernel"
+    traffic = profiled_traffic(kernel)
     result = {
         "metric": "events/sec x active patterns (whole node); achieved HBM GB/s",
         "value": value,
@@ -153,16 +189,15 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded splitmix64 StockStream, SURVEY §8(d))",
-        "config": {"workload": "C2: 1K concurrent 2-state filter+reference patterns "
-                               "(every e1[price>T_p] -> e2[price>e1.price] within W_p)",
-                   "patterns_per_gpu": P, "events_per_step": B, "parallelism": f"pattern-set x{world}",
-                   "matches": matches},
+        "config": {"workload": wl, "patterns_per_gpu": P, "events_per_step": B, "keys": K,
+                   "parallelism": f"pattern-set x{world}", "matches": matches},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                     "frac": achieved / peak, "traffic": None,
-                     "kernel": "nfa_ratchet_kernel", "kernel_ms": avg_ms},
+                     "frac": achieved / peak, "traffic": traffic[0] if traffic else None,
+                     "traffic_source": traffic[1] if traffic else None,
+                     "kernel": kernel, "kernel_ms": avg_ms},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(None, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(args.workload, K, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

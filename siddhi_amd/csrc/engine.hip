@@ -1086,8 +1086,12 @@ void gen_grow(sdh_engine* e, sdh_engine::GenSet& gs, int64_t keys) {
 int64_t gen_collect_device(sdh_engine* e);
 
 // one K_gen step for every set fed by `stream`
-void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out) {
+void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out, double* bytes_out) {
   *ms_out = 0;
+  *bytes_out = 0;
+  double bytes = 0;
+  int64_t ev_bytes = 8;
+  for (int a = 0; a < B.n_attr; ++a) ev_bytes += B.width[a];
   if (e->gsets.empty()) return;
   const int64_t n = B.n;
   if (e->g_chunks == 0) {
@@ -1131,6 +1135,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out)
       L.n_items = gs.n_groups;
       HIPCHK(sdh_launch_gen(&L, e->stream));
       any = true;
+      bytes += (double)n * ev_bytes * gs.n_groups;  // every group streams the batch once
       continue;
     }
     // partitioned: the partition's key attribute of this stream
@@ -1171,6 +1176,8 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out)
     L.n_items = hv[1] * gs.n_groups;
     HIPCHK(sdh_launch_gen(&L, e->stream));
     any = true;
+    // routing (key column read, key/kid/idx written and sorted) + every group streaming its keys' events
+    bytes += (double)n * (8 + 8 + 4 + 4 + 2 * (4 + 4) + 3 * 4) + (double)n * ev_bytes * gs.n_groups;
   }
   HIPCHK(hipEventRecord(e->ev1, e->stream));
   int32_t errs[4] = {0, 0, 0, 0};
@@ -1179,6 +1186,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out)
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
   *ms_out = ms;
+  *bytes_out = bytes;
   if (errs[3]) throw Error(SDH_E_CAPACITY, "partition key table full");
   if (errs[1]) throw Error(SDH_E_REFERENCE, "the reference engine would throw on this stream "
                                             "(ConcurrentModification / IllegalState / NullPointer)");
@@ -1296,9 +1304,10 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     if (g.stream == stream) consumers += g.n_lanes;
   ms += e->r_kernel_ms;
   bytes += e->r_kernel_bytes;
-  double gms = 0;
-  launch_gen(e, stream, B, &gms);
+  double gms = 0, gbytes = 0;
+  launch_gen(e, stream, B, &gms, &gbytes);
   ms += gms;
+  bytes += gbytes;
   for (const auto& g : e->gq)
     if (g.recv_n[stream] > 0) consumers += 1;
   if (consumers) {

@@ -79,3 +79,33 @@ def c2_app(n_patterns: int, within=None) -> str:
                   f"e2=StockStream[price > e1.price] within {w} sec "
                   f"select e1.price as p1, e2.price as p2 insert into OutStream;")
     return " ".join(qs)
+
+
+def c3_query(p: int, seed: int = PATTERN_SEED) -> str:
+    """Pattern p of the C3 family: count <2:5>, logical and, logical or, within 10 sec,
+    all inside `partition with (symbol of StockStream)`."""
+    t = c2_threshold_text(p)
+    v = 100 + (splitmix64(seed ^ (p + 1000)) % 800)
+    kind = p % 3
+    if kind == 0:
+        # count <2:5> in the middle of the chain (chained events, shared with the next state while it
+        # keeps counting). `every e1=S[..]<2:5>` at the START is avoided: there the reference's
+        # shallow every-clones share one event chain, two appends per event can skip over `max`, and
+        # such partials then stay pending for ever (unbounded state in the reference itself).
+        body = (f"every e1=StockStream[price > {t}] -> e2=StockStream[volume > {v // 4}] <2:5> -> "
+                f"e3=StockStream[price > e2[last].price] within 10 sec "
+                f"select e1.price as a, e2[0].volume as b, e3.price as c")
+    elif kind == 1:
+        body = (f"every e1=StockStream[price > {t}] -> e2=StockStream[volume > {v}] and "
+                f"e3=StockStream[price < {t}] within 10 sec select e1.price as a, e2.volume as b")
+    else:
+        body = (f"every e1=StockStream[volume < {v}] -> e2=StockStream[price > {t}] or "
+                f"e3=StockStream[volume > {1000 - v // 4}] within 10 sec select e1.volume as a, e2.price as b")
+    return f"@info(name='c3p{p}') from {body} insert into OutStream;"
+
+
+def c3_app(n_patterns: int, first: int = 0) -> str:
+    """C3 (BASELINE.json configs[2]): count/kleene <2:5> plus logical and/or patterns,
+    `partition with (symbol)` (keys = the stream's symbols)."""
+    qs = " ".join(c3_query(p) for p in range(first, first + n_patterns))
+    return f"{STOCK_STREAM} partition with (symbol of StockStream) begin {qs} end;"
