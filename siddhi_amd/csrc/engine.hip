@@ -1196,6 +1196,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   if (any) HIPCHK(hipMemcpy(&nrec, e->g_nrec.p, 8, hipMemcpyDeviceToHost));
   if (write && any) gen_collect_device(e);
   e->g_dev_matches = write ? 0 : (int64_t)nrec;
+  *bytes_out += (double)nrec * 32.0;  // one (query, ts, seqs) record per match, as for K_ratchet
   if (errs[2]) {
     e->g_chunks *= 4;  // the next push gets a larger output buffer
     throw Error(SDH_E_CAPACITY, "K_gen match output buffer overflow (matches of this push were lost)");

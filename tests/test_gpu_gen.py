@@ -143,3 +143,21 @@ def test_force_gen_matches_chain_plans_on_c2():
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
     assert len(a[0]) > 10000
+
+
+def test_engine_shards_merge_to_single_engine():
+    """sdh_config.shard_rank/shard_world on the device: the union of two shards, merged by
+    siddhi_amd.dist.merge_matches, equals one engine running every query (and the oracle)."""
+    from siddhi_amd import dist as sdist
+    from test_dist import events, full_src
+    o = App(full_src())
+    shards = [hip_app(full_src(), shard_rank=r, shard_world=2) for r in range(2)]
+    for stream, row, t in events():
+        o.send(stream, [row], [t])
+        for s in shards:
+            s.send(stream, [row], [t])
+    for r, s in enumerate(shards):
+        assert {m[0] for m in s.matches} <= {q for q in range(len(o.ir.queries))
+                                            if sdist.shard_of(o.ir, q, 2) == r}
+    merged = sdist.merge_matches(o.ir, lambda q: o.log.stream[q], [s.matches for s in shards])
+    assert merged == o.matches and len(merged) > 50
