@@ -1544,8 +1544,6 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
 int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
   if (!e || !blob || !len) return SDH_E_INVALID;
   return guard(e, [&]() {
-    if (!e->gsets.empty())
-      throw Error(SDH_E_UNSUPPORTED, "snapshot of K_gen instance arenas is not implemented yet");
     HIPCHK(hipStreamSynchronize(e->stream));
     const size_t nq = e->lq.size();
     const size_t tbl = (size_t)NF * e->pcap;
@@ -1579,6 +1577,31 @@ int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
           w.push_back(sq[i * WAVE + l]);
           w.push_back(ky[i * WAVE + l]);
         }
+      }
+    }
+    // K_gen sets: instance arenas (Snapshotable state of every pre-processor of every instance)
+    // and, for partitions, the key table (PartitionRuntime's key -> instance map)
+    w.push_back((int64_t)e->gsets.size());
+    auto put_dev = [&](const void* dptr, size_t bytes) {
+      const size_t o = w.size();
+      w.resize(o + (bytes + 7) / 8);
+      if (bytes) HIPCHK(hipMemcpy(&w[o], dptr, bytes, hipMemcpyDeviceToHost));
+    };
+    for (auto& up : e->gsets) {
+      auto& gs = *up;
+      const int64_t blocks = gs.partition < 0 ? gs.n_groups : gs.key_cap * gs.n_groups;
+      w.push_back(gs.partition);
+      w.push_back(gs.key_cap);
+      w.push_back(blocks);
+      put_dev(gs.a32.p, (size_t)blocks * e->gB32 * 64 * 4);
+      put_dev(gs.a64.p, (size_t)blocks * e->gB64 * 64 * 8);
+      if (gs.partition >= 0) {
+        const size_t slots = (size_t)gs.tmask + 2;
+        w.push_back((int64_t)slots);
+        put_dev(gs.tkey.p, slots * 8);
+        put_dev(gs.tid.p, slots * 4);
+        put_dev(gs.n_keys.p, 4);
+        put_dev(gs.key_of_id.p, (size_t)gs.max_keys * 8);
       }
     }
     *len = w.size() * 8;
@@ -1634,7 +1657,36 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
       HIPCHK(hipMemcpy(e->d_rsq[b].p + o, sq.data(), sq.size() * 8, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(e->d_rky[b].p + o, ky.data(), ky.size() * 8, hipMemcpyHostToDevice));
     }
+    if ((size_t)nx() != e->gsets.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
+    auto get_dev = [&](void* dptr, size_t bytes) {
+      const size_t nw8 = (bytes + 7) / 8;
+      if (i + nw8 > nw) throw Error(SDH_E_INVALID, "snapshot truncated");
+      if (bytes) HIPCHK(hipMemcpy(dptr, &w[i], bytes, hipMemcpyHostToDevice));
+      i += nw8;
+    };
+    for (auto& up : e->gsets) {
+      auto& gs = *up;
+      if (nx() != gs.partition) throw Error(SDH_E_INVALID, "snapshot of a different program");
+      const int64_t key_cap = nx(), blocks = nx();
+      if (gs.partition >= 0) {
+        gen_grow(e, gs, key_cap);
+        if (gs.key_cap != key_cap) throw Error(SDH_E_INVALID, "snapshot key capacity mismatch");
+      }
+      get_dev(gs.a32.p, (size_t)blocks * e->gB32 * 64 * 4);
+      get_dev(gs.a64.p, (size_t)blocks * e->gB64 * 64 * 8);
+      if (gs.partition >= 0) {
+        const size_t slots = (size_t)nx();
+        if (slots != (size_t)gs.tmask + 2) throw Error(SDH_E_INVALID, "snapshot key table mismatch");
+        get_dev(gs.tkey.p, slots * 8);
+        get_dev(gs.tid.p, slots * 4);
+        get_dev(gs.n_keys.p, 4);
+        get_dev(gs.key_of_id.p, (size_t)gs.max_keys * 8);
+      }
+    }
     e->backlog.clear();
+    e->g_host.clear();
+    e->g_host_n = 0;
+    e->g_dev_matches = 0;
     e->device_unpolled = false;
     e->device_matches = 0;
     e->r_matches = 0;

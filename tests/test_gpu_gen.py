@@ -161,3 +161,34 @@ def test_engine_shards_merge_to_single_engine():
                                             if sdist.shard_of(o.ir, q, 2) == r}
     merged = sdist.merge_matches(o.ir, lambda q: o.log.stream[q], [s.matches for s in shards])
     assert merged == o.matches and len(merged) > 50
+
+
+def test_gen_snapshot_restore_count_and_partition():
+    """Snapshot/restore of K_gen arenas and the partition key table (the reference's persist() ->
+    new runtime -> restoreLastRevision(), PersistenceTestCase.java:150-235): the restored engine
+    continues exactly like the original."""
+    src = ("define stream S (k int, v int, p float); "
+           "@info(name='c') from every e1=S[v > 3] <2:4> -> e2=S[p > e1[last].p] select e1[0].v as a insert into O; "
+           "partition with (k of S) begin "
+           "@info(name='s') from every e1=S[v > 5], e2=S[v < e1.v]+ within 30 milliseconds select e1.v as a insert into O; "
+           "@info(name='l') from every e1=S[p > 5] -> e2=S[v > 8] or e3=S[p < 1] select e1.v as a insert into O; "
+           "end;")
+    ev = random_events(17, n=600, keys=40)
+    ev = [(s if s == "A" else "A", r[:3], t) for s, r, t in ev]
+    a = hip_app(src.replace("S", "A"))
+    o = App(src.replace("S", "A"))
+    for stream, row, t in ev[:300]:
+        a.send(stream, [row], [t])
+        o.send(stream, [row], [t])
+    a.engine.poll()
+    snap = a.engine.snapshot()
+    b = hip_app(src.replace("S", "A"))
+    b.engine.restore(snap)
+    o.matches.clear()
+    a.matches.clear()
+    for stream, row, t in ev[300:]:
+        a.send(stream, [row], [t])
+        b.send(stream, [row], [t])
+        o.send(stream, [row], [t])
+    assert a.matches == o.matches
+    assert b.matches == o.matches and len(b.matches) > 20
