@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <memory>
 #include <cstdarg>
@@ -34,6 +35,9 @@ extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaun
                                        size_t lds, hipStream_t s);
 extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int ML, int SC,
                                          const sdh::RatchetLaunch* L, hipStream_t s);
+extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::StreamBatch* B, int attr, int conv,
+                                                 int64_t n_tiles, uint64_t* tmax, uint64_t* tmin, uint8_t* thas,
+                                                 hipStream_t s);
 extern "C" hipError_t sdh_launch_compact(const int64_t* src, const int64_t* seg_off,
                                          const int64_t* seg_count, const int64_t* dst_off,
                                          int rec_words, int n_items, int64_t* dst, hipStream_t s);
@@ -557,6 +561,9 @@ struct sdh_engine {
   int r_blocks_used = 0;             // of the last launch
   std::vector<int32_t> r_blk_count;
   int rML = 16;                      // LDS ring entries per lane (power of two)
+  std::vector<std::array<int, 4>> r_sum_specs;  // tile-summary rows: (stream, attr, conv, key kind)
+  DevBuf<uint64_t> d_tsmax, d_tsmin;
+  DevBuf<uint8_t> d_tshas;
   int rSC = 256;                     // global spill ring entries per lane (power of two)
   DevBuf<uint4> d_rspillA;
   DevBuf<uint32_t> d_rspillB;
@@ -780,6 +787,19 @@ void ratchet_build(sdh_engine* e, std::vector<std::pair<RatchetPlan, int>>& plan
     e->rg.push_back(g);
     i = j;
   }
+  // per-tile x summaries: one row per distinct (stream, key column, conversion, key kind)
+  e->r_sum_specs.clear();
+  for (auto& g : e->rg) {
+    const std::array<int, 4> spec{g.stream, g.key_attr, g.key_conv, g.key_kind};
+    int slot = -1;
+    for (size_t k = 0; k < e->r_sum_specs.size(); ++k)
+      if (e->r_sum_specs[k] == spec) slot = (int)k;
+    if (slot < 0) {
+      slot = (int)e->r_sum_specs.size();
+      e->r_sum_specs.push_back(spec);
+    }
+    g.sum_slot = slot;
+  }
   const size_t ng = e->rg.size();
   e->rcur.assign(ng, 0);
   e->r_full_expiry.assign(e->prog.stream_types.size(), 0);
@@ -868,9 +888,26 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     e->d_err.ensure(4);
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
     HIPCHK(hipMemsetAsync(e->d_blk_next.p, 0, 4, e->stream));
+    // per-tile x summaries for the warm-up scans (rows of this stream's key specs)
+    const int64_t n_tiles = (n + 63) / 64;
+    const size_t n_rows = e->r_sum_specs.size();
+    e->d_tsmax.ensure(n_rows * n_tiles);
+    e->d_tsmin.ensure(n_rows * n_tiles);
+    e->d_tshas.ensure(n_rows * n_tiles);
+    if (!full)
+      for (size_t r = 0; r < n_rows; ++r) {
+        const auto& sp = e->r_sum_specs[r];
+        if (sp[0] != stream) continue;
+        HIPCHK(sdh_launch_ratchet_summary(sp[3], &B, sp[1], sp[2], n_tiles, e->d_tsmax.p + r * n_tiles,
+                                          e->d_tsmin.p + r * n_tiles, e->d_tshas.p + r * n_tiles, e->stream));
+      }
     RatchetLaunch L{};
     L.groups = e->d_rg.p;
     L.full_expiry = full;
+    L.tsum_max = e->d_tsmax.p;
+    L.tsum_min = e->d_tsmin.p;
+    L.tsum_has = e->d_tshas.p;
+    L.n_tiles = n_tiles;
     L.b = B;
     for (int b = 0; b < 2; ++b) {
       L.st[b] = e->d_rst[b].p;

@@ -443,35 +443,62 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   const int k_w = pick(L.b.width, kattr);
   const int64_t seq_base = L.b.seq_base;
 
-  // stage one event per lane: ts, x-atom key, f0 operand keys (sortable), validity bits
+  // stage one event per lane in two halves so that the next tile's loads are in flight while
+  // the current tile is processed: load() issues the global loads, convert() builds ts, the
+  // x-atom key, the f0 operand keys (sortable) and the validity bits
+  struct Raw {
+    int64_t ts;
+    uint64_t k;
+    uint64_t f[RMAXF0], f2[RMAXF0];
+    uint32_t nul;  // bit 0: key null, 1+a: f0 atom a null
+    bool live;
+  };
   int64_t fk[RMAXF0], fk2[RMAXF0];
-  auto stage = [&](int64_t e, bool live, int64_t& ets, U& xk, uint32_t& vbits) {
-    ets = live ? L.b.ts[e] : INT64_MAX;
-    bool xok = false;
-    xk = 0;
-    if (live) {
-      const bool nl = k_nul && k_nul[e];
-      xk = (U)stage_key<KK>(load_raw(k_ptr, k_w, e), kconv, nl, xok);
+  auto load = [&](int64_t e, bool live, Raw& r) {
+    r.live = live;
+    r.ts = live ? L.b.ts[e] : INT64_MAX;
+    r.k = live ? load_raw(k_ptr, k_w, e) : 0;
+    uint32_t nl = (live && k_nul && k_nul[e]) ? 1u : 0u;
+#pragma unroll
+    for (int a = 0; a < RMAXF0; ++a) {
+      r.f[a] = 0;
+      r.f2[a] = 0;
+      if (a < n_f0 && live) {
+        r.f[a] = load_raw(f_ptr[a], f_w[a], e);
+        bool n1 = f_nul[a] && f_nul[a][e];
+        if (f_cur2[a]) {
+          r.f2[a] = load_raw(f_ptr2[a], f_w2[a], e);
+          n1 = n1 || (f_nul2[a] && f_nul2[a][e]);
+        }
+        if (n1) nl |= 2u << a;
+      }
     }
-    uint32_t fnul = 0;
+    r.nul = nl;
+  };
+  auto convert = [&](const Raw& r, int64_t& ets, U& xk, uint32_t& vbits) {
+    ets = r.ts;
+    bool xok = false;
+    xk = r.live ? (U)stage_key<KK>(r.k, kconv, (r.nul & 1u) != 0, xok) : (U)0;
 #pragma unroll
     for (int a = 0; a < RMAXF0; ++a) {
       fk[a] = 0;
       fk2[a] = 0;
-      if (a < n_f0 && live) {
-        const int64_t k1 = to_key(load_raw(f_ptr[a], f_w[a], e), f_conv[a]);
-        bool nl = f_nul[a] && f_nul[a][e];
+      if (a < n_f0 && r.live) {
+        const int64_t k1 = to_key(r.f[a], f_conv[a]);
         if (f_cur2[a]) {
           fk[a] = k1;
-          fk2[a] = to_key(load_raw(f_ptr2[a], f_w2[a], e), f_conv2[a]);
-          nl = nl || (f_nul2[a] && f_nul2[a][e]);
+          fk2[a] = to_key(r.f2[a], f_conv2[a]);
         } else {
           fk[a] = f_f64[a] ? sortable_f64(k1) : k1;
         }
-        if (nl) fnul |= 1u << a;
       }
     }
-    vbits = (xok ? 1u : 0u) | (fnul << 1);
+    vbits = (xok ? 1u : 0u) | (r.nul & ~1u);
+  };
+  auto stage = [&](int64_t e, bool live, int64_t& ets, U& xk, uint32_t& vbits) {
+    Raw r;
+    load(e, live, r);
+    convert(r, ets, xk, vbits);
   };
   // f0 of this lane's pattern on staged event k
   auto f0_pass = [&](int k, uint32_t vb) {
@@ -513,21 +540,17 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
     // verified on every event the item reads; the host re-runs exactly otherwise).
     const int64_t t_last = L.b.ts[W.c0 - 1];
     const int64_t w0 = has_within ? lower_bound_ts(L.b.ts, W.c0, t_last - wmax, lane) : 0;
-    bool r_has = false;  // reduction of the valid x over (current tile end, c0)
+    bool r_has = false;  // reduction (max for >,>= / min for <,<=) of the valid x after the scan point
     U r_val = 0;
-    int64_t next_first_ts = t_last;
-    for (int64_t hi = W.c0; hi > w0; hi -= WAVE) {
-      const int64_t lo = hi - WAVE;
+    auto better = [&](U a, U b) { return xcmp<KK>(is_max ? CM_GT : CM_LT, a, b); };
+    // events [lo, hi) of one tile in detail (events < w0 masked off)
+    auto detail_tile = [&](int64_t lo, int64_t hi) {
       const int64_t e = lo + lane;
-      const bool live = e >= w0;
+      const bool live = e >= w0 && e < hi;
       int64_t ets;
       U xk;
       uint32_t vb;
       stage(e, live, ets, xk, vb);
-      const int64_t nxt = __shfl_down(ets, 1, WAVE);
-      if (live && ets > (lane == WAVE - 1 ? next_first_ts : nxt)) unordered = true;
-      const int fl = (int)(lo < w0 ? w0 - lo : 0);
-      next_first_ts = readlane64(ets, fl);
       // inclusive suffix reduction over the tile's lanes (events)
       bool vh = (vb & 1u) != 0;
       U vv = xk;
@@ -535,13 +558,13 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
       for (int d = 1; d < WAVE; d <<= 1) {
         const U ov = shdown(vv, d);
         const bool oh = __shfl_down((int)vh, d, WAVE) != 0 && lane + d < WAVE;
-        const bool take = oh && (!vh || xcmp<KK>(is_max ? CM_GT : CM_LT, ov, vv));
+        const bool take = oh && (!vh || better(ov, vv));
         vv = take ? ov : vv;
         vh = vh || oh;
       }
       U sv = shdown(vv, 1);
       bool sh = __shfl_down((int)vh, 1, WAVE) != 0 && lane + 1 < WAVE;
-      if (r_has && (!sh || xcmp<KK>(is_max ? CM_GT : CM_LT, r_val, sv))) sv = r_val;
+      if (r_has && (!sh || better(r_val, sv))) sv = r_val;
       sh = sh || r_has;
       const bool cand = live && (vb & 1u) && !(sh && xop<KK, XM>(xmask, sv, xk));
       uint64_t cm = __ballot(cand);
@@ -554,10 +577,57 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
         if (f0_pass(k, vbk) && !expired(tk, t_last, within))
           if (!D.push_front(tk, xkk, (uint32_t)(seq_base + lo + k))) overflow = true;
       }
-      const U tv = rlane(vv, fl);
-      const bool th = __builtin_amdgcn_readlane((uint32_t)vh, fl) != 0;
-      if (th && (!r_has || xcmp<KK>(is_max ? CM_GT : CM_LT, tv, r_val))) r_val = tv;
+      const U tv = rlane(vv, 0);
+      const bool th = __builtin_amdgcn_readlane((uint32_t)vh, 0) != 0;
+      if (th && (!r_has || better(tv, r_val))) r_val = tv;
       r_has = r_has || th;
+    };
+    // the partial tile up to c0, then aligned tiles 64 at a time: a tile can hold a survivor only
+    // if its best x is not dominated by the reduction of everything after it (x_i must satisfy
+    // !(R OP x_i)); dominated tiles leave the reduction unchanged and are skipped on their summary
+    int64_t hi = W.c0;
+    const int64_t al = W.c0 & ~(int64_t)63;
+    if (al < hi) {
+      detail_tile(al, hi);
+      hi = al;
+    }
+    const int slot = G->sum_slot;
+    while (hi > w0) {
+      const int64_t jhi = hi >> 6;
+      const int64_t j = jhi - WAVE + lane;
+      const bool tl = j >= 0 && (j + 1) * 64 > w0;
+      U smx = 0;
+      bool shs = false;
+      if (tl) {
+        const size_t o = (size_t)slot * L.n_tiles + j;
+        shs = L.tsum_has[o] != 0;
+        smx = (U)(is_max ? L.tsum_max[o] : L.tsum_min[o]);
+      }
+      // reduction after each tile: the later tiles of this group, then everything scanned before
+      bool vh = shs;
+      U vv = smx;
+#pragma unroll
+      for (int d = 1; d < WAVE; d <<= 1) {
+        const U ov = shdown(vv, d);
+        const bool oh = __shfl_down((int)vh, d, WAVE) != 0 && lane + d < WAVE;
+        const bool take = oh && (!vh || better(ov, vv));
+        vv = take ? ov : vv;
+        vh = vh || oh;
+      }
+      U rv = shdown(vv, 1);
+      bool rh = __shfl_down((int)vh, 1, WAVE) != 0 && lane + 1 < WAVE;
+      if (r_has && (!rh || better(r_val, rv))) rv = r_val;
+      rh = rh || r_has;
+      const bool need = tl && shs && !(rh && xop<KK, XM>(xmask, rv, smx));
+      uint64_t nm = __ballot(need);
+      while (nm) {  // newest tile first
+        const int b = 63 - __builtin_clzll(nm);
+        nm &= ~(1ull << b);
+        const int64_t jt = jhi - WAVE + b;
+        detail_tile(jt * 64, jt * 64 + 64);
+      }
+      // skipped tiles are dominated, so the reduction only moved on the detailed ones
+      hi = (jhi - WAVE) * 64;
     }
     if (w0 == 0) {
       // the window reaches the batch start: carried partials survive unless expired or matched
@@ -572,16 +642,33 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
     }
   }
 
+  // Keep the top of every non-empty deque in LDS (ln >= 1): move the newest spilled entry up.
+  auto refill = [&]() {
+    if (D.ln == 0 && D.sn > 0) {
+      int64_t t0; U k0; uint32_t q0;
+      D.sget(D.si(D.sbot + D.sn - 1), t0, k0, q0);
+      --D.sn;
+      D.lput(D.li(D.lbot), t0, k0, q0);
+      D.ln = 1;
+    }
+  };
+  refill();
+
   // VGPR caches of the deque ends: top key/seq, bottom deadline/seq
   U tkey = 0;
   uint32_t tseq = 0, bseq = 0;
-  int64_t bdead = INT64_MAX, bts = 0;
+  int64_t bdead = INT64_MAX;
   auto refresh_top = [&]() {
-    if (D.n() > 0) { int64_t t0; D.top(t0, tkey, tseq); }
+    if (D.ln > 0) {
+      int64_t t0;
+      D.lget(D.li(D.lbot + D.ln - 1), t0, tkey, tseq);
+    }
   };
   auto refresh_bottom = [&]() {
+    bdead = INT64_MAX;
     if (D.n() > 0) {
       U k0;
+      int64_t bts;
       D.bottom(bts, k0, bseq);
       bdead = sat_add(bts, within);
     }
@@ -590,50 +677,58 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   refresh_bottom();
 
   int blk = -1, fill = 0;
+  int64_t* wp = nullptr;  // next record of the wave's current output block
   int64_t prev_tile_ts = (W.c0 == 0) ? L.b.prev_ts : L.b.ts[W.c0 - 1];
-  const int RW = 4;
 
-  // emit one record per lane with `mt` (ballot m): per-wave output blocks, ranks by mbcnt
+  // one record per lane with `mt` (ballot m): per-wave output blocks (one atomic per block), ranks by mbcnt
   auto emit = [&](bool mt, uint64_t m, int64_t tt, int64_t s1, int64_t s) {
     if (mover) return;
     const int c = __popcll(m);
-    if (fill + c > L.blk_recs) {
+    if (blk < 0 || fill + c > L.blk_recs) {
       if (blk >= 0 && lane == 0) L.blk_count[blk] = fill;
-      blk = -1;
-    }
-    if (blk < 0) {
       int nb = 0;
       if (lane == 0) nb = atomicAdd(L.blk_next, 1);
       nb = __builtin_amdgcn_readfirstlane(nb);
       if (nb >= L.n_blocks) {
+        blk = -1;
         mover = true;
         return;
       }
       blk = nb;
       fill = 0;
+      wp = L.match + (size_t)blk * L.blk_recs * 4;
     }
     if (mt) {
-      int64_t* r = L.match + ((size_t)blk * L.blk_recs + fill + wave_mbcnt(m)) * RW;
-      reinterpret_cast<longlong2*>(r)[0] = make_longlong2(qid, tt);
-      reinterpret_cast<longlong2*>(r)[1] = make_longlong2(s1, s);
+      longlong2* r = reinterpret_cast<longlong2*>(wp + (size_t)wave_mbcnt(m) * 4);
+      r[0] = make_longlong2(qid, tt);
+      r[1] = make_longlong2(s1, s);
     }
+    wp += (size_t)c * 4;
     fill += c;
   };
 
-  // ---- forward NFA step over the events this item emits for ----
+  // ---- forward NFA step over the events this item emits for. Fast path: straight-line per
+  // event (expiry check, up to four pops from one LDS round trip, push); rare cases (expiry,
+  // spill refill / eviction, a fifth pop) branch to slow paths on a wave-uniform ballot ----
+  Raw nxt;
+  load(W.c0 + lane, W.c0 + lane < W.c1, nxt);
   for (int64_t t = W.c0; t < W.c1; t += WAVE) {
-    const int64_t e = t + lane;
-    const bool live = e < W.c1;
+    const Raw cur = nxt;
+    if (t + WAVE < W.c1) load(t + WAVE + lane, t + WAVE + lane < W.c1, nxt);  // prefetch
     int64_t ets;
     U xk;
     uint32_t vbits;
-    stage(e, live, ets, xk, vbits);
+    convert(cur, ets, xk, vbits);
+    const bool live = cur.live;
     int64_t pred = __shfl_up(ets, 1, WAVE);
     if (lane == 0) pred = prev_tile_ts;
     if (live && ets < pred) unordered = true;
     prev_tile_ts = __shfl(ets, WAVE - 1, WAVE);
-
     const int cnt = (int)((W.c1 - t) < WAVE ? (W.c1 - t) : WAVE);
+    // sequence numbers are kept as their low 32 bits: a live partial must stay < 2^31 events old
+    // (checked once per tile against the tile's last event; the bottom only gets younger)
+    if (D.n() > 0 && (uint32_t)((uint32_t)(seq_base + t + cnt - 1) - bseq) >= 0x80000000u) aged = true;
+
 #pragma unroll 1
     for (int k = 0; k < cnt; ++k) {
       const int64_t tt = readlane64(ets, k);
@@ -647,92 +742,99 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
       if (has_within) {
         if constexpr (!FULL) {
           // timestamps non-decreasing: expired(bts, tt) <=> tt > bts + within
-          while (true) {
-            const bool ex = D.n() > 0 && tt > bdead;
-            if (__ballot(ex) == 0) break;
-            if (ex) {
-              D.pop_front();
-              bdead = INT64_MAX;
-              refresh_bottom();
-              if (D.n() == 0) refresh_top();
+          if (__ballot(tt > bdead) != 0) {
+            while (true) {
+              const bool ex = D.n() > 0 && tt > bdead;
+              if (__ballot(ex) == 0) break;
+              if (ex) {
+                D.pop_front();
+                refill();
+                refresh_bottom();
+                if (D.n() == 0) bdead = INT64_MAX;
+              }
             }
           }
         } else {
           const int n0 = D.n();
           D.compact_expired(tt, within);
-          if (D.n() != n0) {
+          if (__ballot(D.n() != n0) != 0) {
+            refill();
             refresh_top();
             refresh_bottom();
           }
         }
       }
-      // sequence numbers are kept as their low 32 bits: a live partial must be < 2^31 events old
-      if (D.n() > 0 && (slo - bseq) >= 0x80000000u) aged = true;
 
-      // ---- 2. matches: the newest partials whose key satisfies `cur OP key`; up to four pops
-      //         per LDS round trip (the three LDS entries under the top are fetched together) ----
-      while (true) {
-        const bool mt = x_ok && D.n() > 0 && xop<KK, XM>(xmask, x, tkey);
-        if (__ballot(mt) == 0) break;
-        U k1 = 0, k2 = 0, k3 = 0;
-        uint32_t q1 = 0, q2 = 0, q3 = 0;
+      // ---- 2. matches: the newest partials whose key satisfies `cur OP key` ----
+      bool mt = x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey);
+      uint64_t m = __ballot(mt);
+      while (m) {
+        // the three LDS entries under the top, read unconditionally (in-bounds ring slots)
+        const int topl = D.lbot + D.ln - 1;
         int64_t td;
-        const int ln = D.ln;
-        const int topl = D.lbot + ln - 1;
-        if (mt && ln > 1) D.lget(D.li(topl - 1), td, k1, q1);
-        if (mt && ln > 2) D.lget(D.li(topl - 2), td, k2, q2);
-        if (mt && ln > 3) D.lget(D.li(topl - 3), td, k3, q3);
-        int p = 0;
-        if (mt) {
-          p = 1;
-          if (ln > 1 && xop<KK, XM>(xmask, x, k1)) {
-            p = 2;
-            if (ln > 2 && xop<KK, XM>(xmask, x, k2)) {
-              p = 3;
-              if (ln > 3 && xop<KK, XM>(xmask, x, k3)) p = 4;
-            }
+        U k1, k2, k3;
+        uint32_t q1, q2, q3;
+        D.lget(D.li(topl - 1), td, k1, q1);
+        D.lget(D.li(topl - 2), td, k2, q2);
+        D.lget(D.li(topl - 3), td, k3, q3);
+        const bool c1 = mt && D.ln > 1 && xop<KK, XM>(xmask, x, k1);
+        const bool c2 = c1 && D.ln > 2 && xop<KK, XM>(xmask, x, k2);
+        const bool c3 = c2 && D.ln > 3 && xop<KK, XM>(xmask, x, k3);
+        emit(mt, m, tt, s - (int64_t)(uint32_t)(slo - tseq), s);
+        const uint64_t m1 = __ballot(c1);
+        if (m1) {
+          emit(c1, m1, tt, s - (int64_t)(uint32_t)(slo - q1), s);
+          const uint64_t m2 = __ballot(c2);
+          if (m2) {
+            emit(c2, m2, tt, s - (int64_t)(uint32_t)(slo - q2), s);
+            const uint64_t m3 = __ballot(c3);
+            if (m3) emit(c3, m3, tt, s - (int64_t)(uint32_t)(slo - q3), s);
           }
         }
-        const uint32_t qs[4] = {tseq, q1, q2, q3};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool mj = p > j;
-          const uint64_t m = __ballot(mj);
-          if (m == 0) break;
-          emit(mj, m, tt, s - (int64_t)(uint32_t)(slo - qs[j]), s);
-        }
-        if (mt) {
-          D.pop_back(p);
-          if (D.n() > 0) {
-            if (p < ln) {  // new top is an LDS entry; fetched above unless p == 4
-              if (p == 1) { tkey = k1; tseq = q1; }
-              else if (p == 2) { tkey = k2; tseq = q2; }
-              else if (p == 3) { tkey = k3; tseq = q3; }
-              else refresh_top();
-            } else {
-              refresh_top();
-            }
-          } else {
-            bdead = INT64_MAX;
+        const int p = (int)mt + (int)c1 + (int)c2 + (int)c3;
+        D.ln -= p;
+        // new top: prefetched unless four popped (then read it) or the LDS part ran dry
+        tkey = p == 1 ? k1 : p == 2 ? k2 : p == 3 ? k3 : tkey;
+        tseq = p == 1 ? q1 : p == 2 ? q2 : p == 3 ? q3 : tseq;
+        const bool fix = (p == 4 && D.ln > 0) || (p > 0 && D.ln == 0);
+        if (__ballot(fix) != 0) {
+          if (fix) {
+            refill();
+            refresh_top();
           }
         }
+        if (p > 0 && D.n() == 0) bdead = INT64_MAX;
+        // more matches are possible only where four were popped or the top was refilled
+        mt = fix && x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey);
+        m = __ballot(mt);
       }
 
       // ---- 3. start state: every event passing f0 opens a partial (pending from j+1) ----
-      if (f0_pass(k, vb)) {
-        const bool was_empty = D.n() == 0;
-        if (!D.push_back(tt, x, slo)) {
-          overflow = true;
-        } else {
-          tkey = x;
-          tseq = slo;
-          if (was_empty) {
-            bts = tt;
-            bseq = slo;
-            bdead = sat_add(tt, within);
+      const bool f = f0_pass(k, vb);
+      if (__ballot(f && D.ln == ML) != 0) {
+        // LDS ring full: move its oldest entry to the spill ring (rare)
+        if (f && D.ln == ML) {
+          if (D.sn == SC) {
+            overflow = true;
+          } else {
+            int64_t t0; U k0; uint32_t q0;
+            D.lget(D.li(D.lbot), t0, k0, q0);
+            D.sput(D.si(D.sbot + D.sn), t0, k0, q0);
+            ++D.sn;
+            D.lbot = (D.lbot + 1) & D.lmask;
+            --D.ln;
           }
         }
       }
+      const bool push = f && D.ln < ML;
+      if (push) D.lput(D.li(D.lbot + D.ln), tt, x, slo);
+      if (push && D.n() == 0) {
+        bseq = slo;
+        bdead = sat_add(tt, within);
+      }
+      D.ln += push ? 1 : 0;
+      tkey = push ? x : tkey;
+      tseq = push ? slo : tseq;
     }
   }
 
@@ -768,7 +870,62 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   (void)W64;
 }
 
+// per aligned 64-event tile: max and min x-atom key over the valid events (one wave per tile)
+template <int KK>
+__global__ __launch_bounds__(256) void ratchet_tile_summary(StreamBatch b, int attr, int conv, int64_t n_tiles,
+                                                            uint64_t* tmax, uint64_t* tmin, uint8_t* thas) {
+  using U = typename KT<KK>::U;
+  const int lane = threadIdx.x & 63;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile >= n_tiles) return;
+  const int64_t e = tile * 64 + lane;
+  bool ok = false;
+  U k = 0;
+  if (e < b.n) {
+    const uint8_t* nl = pick(b.nul, attr);
+    k = (U)stage_key<KK>(load_raw(pick(b.col, attr), pick(b.width, attr), e), conv, nl && nl[e], ok);
+  }
+  U mx = k, mn = k;
+  bool h = ok;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    U omx, omn;
+    if constexpr (sizeof(U) == 8) {
+      omx = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mx >> 32), d, WAVE) << 32) |
+            (uint32_t)__shfl_xor((int)(uint32_t)mx, d, WAVE);
+      omn = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mn >> 32), d, WAVE) << 32) |
+            (uint32_t)__shfl_xor((int)(uint32_t)mn, d, WAVE);
+    } else {
+      omx = (U)__shfl_xor((int)mx, d, WAVE);
+      omn = (U)__shfl_xor((int)mn, d, WAVE);
+    }
+    const bool oh = __shfl_xor((int)h, d, WAVE) != 0;
+    if (oh && (!h || xcmp<KK>(CM_GT, omx, mx))) mx = omx;
+    if (oh && (!h || xcmp<KK>(CM_LT, omn, mn))) mn = omn;
+    h = h || oh;
+  }
+  if (lane == 0) {
+    tmax[tile] = (uint64_t)mx;
+    tmin[tile] = (uint64_t)mn;
+    thas[tile] = h ? 1 : 0;
+  }
+}
+
 }  // namespace sdh
+
+extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::StreamBatch* B, int attr, int conv,
+                                                 int64_t n_tiles, uint64_t* tmax, uint64_t* tmin, uint8_t* thas,
+                                                 hipStream_t s) {
+  if (n_tiles <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((n_tiles + 3) / 4)), block(256);
+  switch (key_kind) {
+    case sdh::KK_F32: hipLaunchKernelGGL(sdh::ratchet_tile_summary<sdh::KK_F32>, grid, block, 0, s, *B, attr, conv, n_tiles, tmax, tmin, thas); break;
+    case sdh::KK_I32: hipLaunchKernelGGL(sdh::ratchet_tile_summary<sdh::KK_I32>, grid, block, 0, s, *B, attr, conv, n_tiles, tmax, tmin, thas); break;
+    case sdh::KK_F64: hipLaunchKernelGGL(sdh::ratchet_tile_summary<sdh::KK_F64>, grid, block, 0, s, *B, attr, conv, n_tiles, tmax, tmin, thas); break;
+    default: hipLaunchKernelGGL(sdh::ratchet_tile_summary<sdh::KK_I64>, grid, block, 0, s, *B, attr, conv, n_tiles, tmax, tmin, thas); break;
+  }
+  return hipGetLastError();
+}
 
 template <int KK, int XM, bool FULL>
 static void launch_one(const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {

@@ -151,7 +151,8 @@ struct RatchetGroup {
   int32_t stream;
   int32_t key_attr, key_conv, key_kind;   // x-atom operand column (same on both sides)
   int32_t xmask;                          // normalized `cur OP key` CmpMask (never EQ/NE)
-  int32_t n_f0, pad0;
+  int32_t n_f0;
+  int32_t sum_slot;                       // row of the launch's per-tile x-summaries (host-set)
   RatchetAtom f0[RMAXF0];
   int64_t wmax;                           // max within over lanes (-1: none)
   int32_t qid[64];
@@ -182,6 +183,10 @@ struct RatchetLaunch {
   int64_t* ent_ts[2];           // [g][RSMAX][64] ts0
   int64_t* ent_seq[2];          // [g][RSMAX][64] e1 sequence number
   int64_t* ent_key[2];          // [g][RSMAX][64] key (32-bit kinds in the low word)
+  const uint64_t* tsum_max;     // [slot][n_tiles] max / min key of the valid x of each aligned
+  const uint64_t* tsum_min;     //   64-event tile (warm-up skips tiles that cannot hold a survivor)
+  const uint8_t* tsum_has;      //   tile has a valid x
+  int64_t n_tiles;
   uint4* spillA;                // [item][SC][64] deque entries beyond the LDS ring
   uint32_t* spillB;             //   (seq words of 64-bit-key entries)
   int64_t* match;               // blocks of blk_recs records x 4 int64 (qid, ts, seq1, seq2)
