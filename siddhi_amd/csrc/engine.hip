@@ -566,6 +566,7 @@ struct sdh_engine {
   DevBuf<uint8_t> d_tshas;
   int rSC = 256;                     // global spill ring entries per lane (power of two)
   DevBuf<uint4> d_rspillA;
+  DevBuf<int64_t> d_rlts;
   DevBuf<uint32_t> d_rspillB;
   std::vector<char> r_full_expiry;   // per stream: timestamps were seen out of order
   int64_t r_matches = 0;
@@ -881,6 +882,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
                           hipMemcpyHostToDevice, e->stream));
     e->d_rmatch.ensure((size_t)e->r_blocks * e->r_blk_recs * 4);
     e->d_rspillA.ensure((size_t)n_items * e->rSC * WAVE);
+    e->d_rlts.ensure((size_t)n_items * e->rML * WAVE);
     bool any64 = false;
     for (int g : gs) any64 |= e->rg[g].key_kind == KK_F64 || e->rg[g].key_kind == KK_I64;
     if (any64) e->d_rspillB.ensure((size_t)n_items * e->rSC * WAVE);
@@ -933,6 +935,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       Ls.n_items = i1 - i0;
       // spill regions are indexed by the item's position in its launch
       Ls.spillA = e->d_rspillA.p + (size_t)i0 * e->rSC * WAVE;
+      Ls.lds_ts = e->d_rlts.p + (size_t)i0 * e->rML * WAVE;
       Ls.spillB = any64 ? e->d_rspillB.p + (size_t)i0 * e->rSC * WAVE : nullptr;
       HIPCHK(sdh_launch_ratchet(kk, xm, full, e->rML, e->rSC, &Ls, e->stream));
       i0 = i1;

@@ -254,9 +254,8 @@ __device__ __forceinline__ void f0_interval(int mask, bool f64, int64_t c, int64
 
 extern __shared__ uint4 ratchet_lds[];
 
-// One deque entry in LDS ([slot][lane]) or in the lane's global spill ring.
-//   32-bit keys: A = uint4 {ts0.lo, ts0.hi, key, seq}
-//   64-bit keys: A = uint4 {ts0.lo, ts0.hi, key.lo, key.hi}, B = uint32 seq
+// Spill / persisted entries: 32-bit keys A = uint4 {ts0.lo, ts0.hi, key, seq};
+// 64-bit keys A = uint4 {ts0.lo, ts0.hi, key.lo, key.hi}, B = uint32 seq.
 // (seq = low 32 bits of e1's global sequence number; a live partial is < 2^31 events old)
 template <int KK>
 __device__ __forceinline__ uint4 pack_entry(int64_t ts, typename KT<KK>::U key, uint32_t seq) {
@@ -281,25 +280,41 @@ __device__ __forceinline__ void unpack_entry(uint4 a, uint32_t b, int64_t& ts, t
 // Two-level per-lane deque: the newest ML entries in an LDS ring (ratchet_lds, [slot][lane]),
 // older ones in a global spill ring of SC entries (oldest first: spill, then LDS). Pops happen at
 // the newest end (LDS), expiry at the oldest end; the spill is touched only while a lane holds
-// more than ML pending partials.
+// more than ML pending partials. LDS ring entries hold only what the pops read -- {key, seq},
+// 8 B for 32-bit keys -- and their ts0 lives in a per-lane HBM side ring (LT) that is read only
+// when an entry becomes the oldest (expiry deadline) or leaves LDS; half-size entries double the
+// waves an LDS-limited CU holds.
 template <int KK>
 struct Deque {
   using U = typename KT<KK>::U;
   uint4* SA;
   uint32_t* SB;
+  int64_t* LT;
   int lane, lmask, smask, ML, SC;
-  size_t sbase;  // (item * SC) * 64
+  size_t sbase;   // (item * SC) * 64
+  size_t ltbase;  // (item * ML) * 64
   int lbot = 0, ln = 0, sbot = 0, sn = 0;
   __device__ __forceinline__ int li(int slot) const { return (slot & lmask) * WAVE + lane; }
   __device__ __forceinline__ size_t si(int slot) const { return sbase + (size_t)(slot & smask) * WAVE + lane; }
   __device__ __forceinline__ void lput(int i, int64_t ts, U key, uint32_t seq) const {
-    ratchet_lds[i] = pack_entry<KK>(ts, key, seq);
-    if constexpr (KT<KK>::W64) reinterpret_cast<uint32_t*>(&ratchet_lds[ML * WAVE])[i] = seq;
+    if constexpr (KT<KK>::W64) ratchet_lds[i] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), seq, 0u);
+    else reinterpret_cast<uint2*>(ratchet_lds)[i] = make_uint2(key, seq);
+    LT[ltbase + i] = ts;
+  }
+  __device__ __forceinline__ void lget_ks(int i, U& key, uint32_t& seq) const {
+    if constexpr (KT<KK>::W64) {
+      const uint4 a = ratchet_lds[i];
+      key = (uint64_t)a.x | ((uint64_t)a.y << 32);
+      seq = a.z;
+    } else {
+      const uint2 a = reinterpret_cast<const uint2*>(ratchet_lds)[i];
+      key = a.x;
+      seq = a.y;
+    }
   }
   __device__ __forceinline__ void lget(int i, int64_t& ts, U& key, uint32_t& seq) const {
-    uint32_t b = 0;
-    if constexpr (KT<KK>::W64) b = reinterpret_cast<const uint32_t*>(&ratchet_lds[ML * WAVE])[i];
-    unpack_entry<KK>(ratchet_lds[i], b, ts, key, seq);
+    lget_ks(i, key, seq);
+    ts = LT[ltbase + i];
   }
   __device__ __forceinline__ void sput(size_t i, int64_t ts, U key, uint32_t seq) const {
     SA[i] = pack_entry<KK>(ts, key, seq);
@@ -396,6 +411,8 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   Deque<KK> D;
   D.SA = L.spillA;
   D.SB = L.spillB;
+  D.LT = L.lds_ts;
+  D.ltbase = ((size_t)wid * ML) * WAVE;
   D.lane = lane;
   D.ML = ML;
   D.SC = SC;
@@ -659,10 +676,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   uint32_t tseq = 0, bseq = 0;
   int64_t bdead = INT64_MAX;
   auto refresh_top = [&]() {
-    if (D.ln > 0) {
-      int64_t t0;
-      D.lget(D.li(D.lbot + D.ln - 1), t0, tkey, tseq);
-    }
+    if (D.ln > 0) D.lget_ks(D.li(D.lbot + D.ln - 1), tkey, tseq);
   };
   auto refresh_bottom = [&]() {
     bdead = INT64_MAX;
@@ -771,12 +785,11 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
       while (m) {
         // the three LDS entries under the top, read unconditionally (in-bounds ring slots)
         const int topl = D.lbot + D.ln - 1;
-        int64_t td;
         U k1, k2, k3;
         uint32_t q1, q2, q3;
-        D.lget(D.li(topl - 1), td, k1, q1);
-        D.lget(D.li(topl - 2), td, k2, q2);
-        D.lget(D.li(topl - 3), td, k3, q3);
+        D.lget_ks(D.li(topl - 1), k1, q1);
+        D.lget_ks(D.li(topl - 2), k2, q2);
+        D.lget_ks(D.li(topl - 3), k3, q3);
         const bool c1 = mt && D.ln > 1 && xop<KK, XM>(xmask, x, k1);
         const bool c2 = c1 && D.ln > 2 && xop<KK, XM>(xmask, x, k2);
         const bool c3 = c2 && D.ln > 3 && xop<KK, XM>(xmask, x, k3);
@@ -930,7 +943,7 @@ extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::Stream
 template <int KK, int XM, bool FULL>
 static void launch_one(const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {
   const bool w64 = (KK == sdh::KK_F64 || KK == sdh::KK_I64);
-  const size_t lds = (size_t)ML * 64 * (sizeof(uint4) + (w64 ? sizeof(uint32_t) : 0));
+  const size_t lds = (size_t)ML * 64 * (w64 ? 16 : 8);
   hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL>), dim3(L->n_items), dim3(64), lds, s, *L, ML, SC);
 }
 

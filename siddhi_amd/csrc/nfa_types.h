@@ -187,6 +187,7 @@ struct RatchetLaunch {
   const uint64_t* tsum_min;     //   64-event tile (warm-up skips tiles that cannot hold a survivor)
   const uint8_t* tsum_has;      //   tile has a valid x
   int64_t n_tiles;
+  int64_t* lds_ts;              // [item][ML][64] ts0 of the LDS ring entries
   uint4* spillA;                // [item][SC][64] deque entries beyond the LDS ring
   uint32_t* spillB;             //   (seq words of 64-bit-key entries)
   int64_t* match;               // blocks of blk_recs records x 4 int64 (qid, ts, seq1, seq2)
