@@ -33,7 +33,7 @@ extern "C" size_t sdh_route_temp_bytes(int64_t n);
 
 extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaunch* L, int n_blocks,
                                        size_t lds, hipStream_t s);
-extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int ML, int SC,
+extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int nf, int ML, int SC,
                                          const sdh::RatchetLaunch* L, hipStream_t s);
 extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::StreamBatch* B, int attr, int conv,
                                                  int64_t n_tiles, uint64_t* tmax, uint64_t* tmin, uint8_t* thas,
@@ -933,11 +933,13 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       RatchetLaunch Ls = L;
       Ls.items = e->d_ritems.p + i0;
       Ls.n_items = i1 - i0;
+      int nf = 0;
+      for (int i = i0; i < i1; ++i) nf = std::max(nf, e->rg[e->ritems[i].g].n_f0);
       // spill regions are indexed by the item's position in its launch
       Ls.spillA = e->d_rspillA.p + (size_t)i0 * e->rSC * WAVE;
       Ls.lds_ts = e->d_rlts.p + (size_t)i0 * e->rML * WAVE;
       Ls.spillB = any64 ? e->d_rspillB.p + (size_t)i0 * e->rSC * WAVE : nullptr;
-      HIPCHK(sdh_launch_ratchet(kk, xm, full, e->rML, e->rSC, &Ls, e->stream));
+      HIPCHK(sdh_launch_ratchet(kk, xm, full, nf, e->rML, e->rSC, &Ls, e->stream));
       i0 = i1;
     }
     HIPCHK(hipEventRecord(e->ev1, e->stream));

@@ -399,7 +399,7 @@ __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {  // b >= 0
   return a > INT64_MAX - b ? INT64_MAX : a + b;
 }
 
-template <int KK, int XM, bool FULL>
+template <int KK, int XM, bool FULL, int NF>
 __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
   using U = typename KT<KK>::U;
   constexpr bool W64 = KT<KK>::W64;
@@ -429,16 +429,16 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   const bool is_max = (xmask & CM_GT) != 0;
   // f0 atoms: constant atoms become per-lane intervals of sortable keys; two-column atoms stay
   // generic compares. Operand columns are resolved once (wave-uniform).
-  int64_t f_lo[RMAXF0], f_hi[RMAXF0];
-  bool f_neg[RMAXF0];
-  int f_mask[RMAXF0], f_f64[RMAXF0], f_cur2[RMAXF0], f_conv[RMAXF0], f_conv2[RMAXF0];
-  int f_w[RMAXF0], f_w2[RMAXF0];
-  const void* f_ptr[RMAXF0];
-  const void* f_ptr2[RMAXF0];
-  const uint8_t* f_nul[RMAXF0];
-  const uint8_t* f_nul2[RMAXF0];
+  int64_t f_lo[NF], f_hi[NF];
+  bool f_neg[NF];
+  int f_mask[NF], f_f64[NF], f_cur2[NF], f_conv[NF], f_conv2[NF];
+  int f_w[NF], f_w2[NF];
+  const void* f_ptr[NF];
+  const void* f_ptr2[NF];
+  const uint8_t* f_nul[NF];
+  const uint8_t* f_nul2[NF];
 #pragma unroll
-  for (int a = 0; a < RMAXF0; ++a) {
+  for (int a = 0; a < NF; ++a) {
     const RatchetAtom A0 = G->f0[a];
     const int64_t c = a < n_f0 ? G->f0c[a][lane & 63] : 0;
     int m = A0.mask;
@@ -466,18 +466,18 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   struct Raw {
     int64_t ts;
     uint64_t k;
-    uint64_t f[RMAXF0], f2[RMAXF0];
+    uint64_t f[NF], f2[NF];
     uint32_t nul;  // bit 0: key null, 1+a: f0 atom a null
     bool live;
   };
-  int64_t fk[RMAXF0], fk2[RMAXF0];
+  int64_t fk[NF], fk2[NF];
   auto load = [&](int64_t e, bool live, Raw& r) {
     r.live = live;
     r.ts = live ? L.b.ts[e] : INT64_MAX;
     r.k = live ? load_raw(k_ptr, k_w, e) : 0;
     uint32_t nl = (live && k_nul && k_nul[e]) ? 1u : 0u;
 #pragma unroll
-    for (int a = 0; a < RMAXF0; ++a) {
+    for (int a = 0; a < NF; ++a) {
       r.f[a] = 0;
       r.f2[a] = 0;
       if (a < n_f0 && live) {
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
     bool xok = false;
     xk = r.live ? (U)stage_key<KK>(r.k, kconv, (r.nul & 1u) != 0, xok) : (U)0;
 #pragma unroll
-    for (int a = 0; a < RMAXF0; ++a) {
+    for (int a = 0; a < NF; ++a) {
       fk[a] = 0;
       fk2[a] = 0;
       if (a < n_f0 && r.live) {
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   auto f0_pass = [&](int k, uint32_t vb) {
     bool ok = active && (vb & 1u);
 #pragma unroll
-    for (int a = 0; a < RMAXF0; ++a) {
+    for (int a = 0; a < NF; ++a) {
       if (a < n_f0) {
         const int64_t v = readlane64(fk[a], k);
         const bool cn = (vb >> (1 + a)) & 1u;
@@ -940,39 +940,48 @@ extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::Stream
   return hipGetLastError();
 }
 
-template <int KK, int XM, bool FULL>
+template <int KK, int XM, bool FULL, int NF>
 static void launch_one(const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {
   const bool w64 = (KK == sdh::KK_F64 || KK == sdh::KK_I64);
   const size_t lds = (size_t)ML * 64 * (w64 ? 16 : 8);
-  hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL>), dim3(L->n_items), dim3(64), lds, s, *L, ML, SC);
+  hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF>), dim3(L->n_items), dim3(64), lds, s, *L, ML, SC);
 }
 
+// nf: max f0 atoms over the launched groups (one-atom start filters get a leaner register set)
 template <int KK>
-static hipError_t launch_kk(int xm, bool full, const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {
+static hipError_t launch_kk(int xm, bool full, int nf, const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {
   if (full) {
-    launch_one<KK, -1, true>(L, ML, SC, s);
+    launch_one<KK, -1, true, sdh::RMAXF0>(L, ML, SC, s);
+  } else if (nf <= 1) {
+    switch (xm) {
+      case 0: launch_one<KK, 0, false, 1>(L, ML, SC, s); break;
+      case 1: launch_one<KK, 1, false, 1>(L, ML, SC, s); break;
+      case 2: launch_one<KK, 2, false, 1>(L, ML, SC, s); break;
+      default: launch_one<KK, 3, false, 1>(L, ML, SC, s); break;
+    }
   } else {
     switch (xm) {
-      case 0: launch_one<KK, 0, false>(L, ML, SC, s); break;
-      case 1: launch_one<KK, 1, false>(L, ML, SC, s); break;
-      case 2: launch_one<KK, 2, false>(L, ML, SC, s); break;
-      default: launch_one<KK, 3, false>(L, ML, SC, s); break;
+      case 0: launch_one<KK, 0, false, sdh::RMAXF0>(L, ML, SC, s); break;
+      case 1: launch_one<KK, 1, false, sdh::RMAXF0>(L, ML, SC, s); break;
+      case 2: launch_one<KK, 2, false, sdh::RMAXF0>(L, ML, SC, s); break;
+      default: launch_one<KK, 3, false, sdh::RMAXF0>(L, ML, SC, s); break;
     }
   }
   return hipGetLastError();
 }
 
-// xmask: normalized `cur OP key` CmpMask of the launched groups (all equal); ML, SC powers of two
-extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int ML, int SC,
+// xmask: normalized `cur OP key` CmpMask of the launched groups (all equal); nf: max f0 atoms;
+// ML, SC powers of two
+extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int nf, int ML, int SC,
                                          const sdh::RatchetLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
-  if (ML < 4 || (ML & (ML - 1)) || SC < 1 || (SC & (SC - 1))) return hipErrorInvalidValue;
+  if (ML < 4 || (ML & (ML - 1)) || SC < 1 || (SC & (SC - 1)) || nf > sdh::RMAXF0) return hipErrorInvalidValue;
   const int xm = xmask == sdh::CM_GT ? 0 : xmask == (sdh::CM_GT | sdh::CM_EQ) ? 1 : xmask == sdh::CM_LT ? 2 : 3;
   switch (key_kind) {
-    case sdh::KK_F32: return launch_kk<sdh::KK_F32>(xm, full, L, ML, SC, s);
-    case sdh::KK_I32: return launch_kk<sdh::KK_I32>(xm, full, L, ML, SC, s);
-    case sdh::KK_F64: return launch_kk<sdh::KK_F64>(xm, full, L, ML, SC, s);
-    case sdh::KK_I64: return launch_kk<sdh::KK_I64>(xm, full, L, ML, SC, s);
+    case sdh::KK_F32: return launch_kk<sdh::KK_F32>(xm, full, nf, L, ML, SC, s);
+    case sdh::KK_I32: return launch_kk<sdh::KK_I32>(xm, full, nf, L, ML, SC, s);
+    case sdh::KK_F64: return launch_kk<sdh::KK_F64>(xm, full, nf, L, ML, SC, s);
+    case sdh::KK_I64: return launch_kk<sdh::KK_I64>(xm, full, nf, L, ML, SC, s);
     default: return hipErrorInvalidValue;
   }
 }
