@@ -296,10 +296,21 @@ struct Deque {
   int lbot = 0, ln = 0, sbot = 0, sn = 0;
   __device__ __forceinline__ int li(int slot) const { return (slot & lmask) * WAVE + lane; }
   __device__ __forceinline__ size_t si(int slot) const { return sbase + (size_t)(slot & smask) * WAVE + lane; }
-  __device__ __forceinline__ void lput(int i, int64_t ts, U key, uint32_t seq) const {
+  // ts0 of an LDS entry: events of the current batch read it back from the batch's ts column,
+  // older (carried) partials from the side ring LT, written when they enter the LDS ring
+  const int64_t* bts;  // batch timestamps
+  int64_t seq_base;    // global seq of batch event 0
+  int64_t sref;        // a seq >= every held entry's, within 2^31 (the item's last event)
+  __device__ __forceinline__ int64_t full_seq(uint32_t seq_lo) const {
+    return sref - (int64_t)(uint32_t)((uint32_t)sref - seq_lo);
+  }
+  __device__ __forceinline__ void lput_ks(int i, U key, uint32_t seq) const {
     if constexpr (KT<KK>::W64) ratchet_lds[i] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), seq, 0u);
     else reinterpret_cast<uint2*>(ratchet_lds)[i] = make_uint2(key, seq);
-    LT[ltbase + i] = ts;
+  }
+  __device__ __forceinline__ void lput(int i, int64_t ts, U key, uint32_t seq) const {
+    lput_ks(i, key, seq);
+    if (full_seq(seq) < seq_base) LT[ltbase + i] = ts;
   }
   __device__ __forceinline__ void lget_ks(int i, U& key, uint32_t& seq) const {
     if constexpr (KT<KK>::W64) {
@@ -314,7 +325,8 @@ struct Deque {
   }
   __device__ __forceinline__ void lget(int i, int64_t& ts, U& key, uint32_t& seq) const {
     lget_ks(i, key, seq);
-    ts = LT[ltbase + i];
+    const int64_t k = full_seq(seq) - seq_base;
+    ts = k >= 0 ? bts[k] : LT[ltbase + i];
   }
   __device__ __forceinline__ void sput(size_t i, int64_t ts, U key, uint32_t seq) const {
     SA[i] = pack_entry<KK>(ts, key, seq);
@@ -413,6 +425,9 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   D.SB = L.spillB;
   D.LT = L.lds_ts;
   D.ltbase = ((size_t)wid * ML) * WAVE;
+  D.bts = L.b.ts;
+  D.seq_base = L.b.seq_base;
+  D.sref = L.b.seq_base + W.c1 - 1;
   D.lane = lane;
   D.ML = ML;
   D.SC = SC;
@@ -840,7 +855,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
         }
       }
       const bool push = f && D.ln < ML;
-      if (push) D.lput(D.li(D.lbot + D.ln), tt, x, slo);
+      if (push) D.lput_ks(D.li(D.lbot + D.ln), x, slo);  // ts0 = ts of this batch event
       if (push && D.n() == 0) {
         bseq = slo;
         bdead = sat_add(tt, within);
