@@ -38,6 +38,11 @@ extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int 
 extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::StreamBatch* B, int attr, int conv,
                                                  int64_t n_tiles, uint64_t* tmax, uint64_t* tmin, uint8_t* thas,
                                                  hipStream_t s);
+extern "C" hipError_t sdh_launch_ratchet_decode(const int64_t* match, int blk_recs, int wide,
+                                                const int32_t* blk_count, const int32_t* blk_group,
+                                                const int64_t* dst_off, const sdh::RatchetGroup* groups,
+                                                const int64_t* ts, int64_t seq_base, int n_blocks, int64_t* out,
+                                                hipStream_t s);
 extern "C" hipError_t sdh_launch_compact(const int64_t* src, const int64_t* seg_off,
                                          const int64_t* seg_count, const int64_t* dst_off,
                                          int rec_words, int n_items, int64_t* dst, hipStream_t s);
@@ -555,7 +560,11 @@ struct sdh_engine {
   DevBuf<RatchetItem> d_ritems;
   std::vector<RatchetItem> ritems;
   DevBuf<int64_t> d_rmatch;
-  DevBuf<int32_t> d_blk_count, d_blk_next;
+  DevBuf<int32_t> d_blk_count, d_blk_next, d_blk_group;
+  DevBuf<int64_t> d_rbts;            // ts column of the batch the unpolled records refer to
+  const int64_t* r_ts = nullptr;
+  int64_t r_seq_base = 0;
+  int r_wide = 0;
   int64_t r_blocks = 0;              // capacity in blocks
   int r_blk_recs = 8192;
   int r_blocks_used = 0;             // of the last launch
@@ -880,13 +889,17 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     e->d_ritems.ensure(n_items);
     HIPCHK(hipMemcpyAsync(e->d_ritems.p, e->ritems.data(), n_items * sizeof(RatchetItem),
                           hipMemcpyHostToDevice, e->stream));
-    e->d_rmatch.ensure((size_t)e->r_blocks * e->r_blk_recs * 4);
+    // 8-B records address e2 by a 26-bit batch offset; larger batches use 16-B records
+    const int wide = n > ((int64_t)1 << 26) ? 1 : 0;
+    if (n > ((int64_t)1 << 32)) throw Error(SDH_E_INVALID, "batch larger than 2^32 events");
+    e->d_rmatch.ensure((size_t)e->r_blocks * e->r_blk_recs * (wide ? 2 : 1));
     e->d_rspillA.ensure((size_t)n_items * e->rSC * WAVE);
     e->d_rlts.ensure((size_t)n_items * e->rML * WAVE);
     bool any64 = false;
     for (int g : gs) any64 |= e->rg[g].key_kind == KK_F64 || e->rg[g].key_kind == KK_I64;
     if (any64) e->d_rspillB.ensure((size_t)n_items * e->rSC * WAVE);
     e->d_blk_count.ensure((size_t)e->r_blocks);
+    e->d_blk_group.ensure((size_t)e->r_blocks);
     e->d_err.ensure(4);
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
     HIPCHK(hipMemsetAsync(e->d_blk_next.p, 0, 4, e->stream));
@@ -921,6 +934,8 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.spillB = e->d_rspillB.p;
     L.match = e->d_rmatch.p;
     L.blk_count = e->d_blk_count.p;
+    L.blk_group = e->d_blk_group.p;
+    L.wide = wide;
     L.blk_next = e->d_blk_next.p;
     L.n_blocks = (int32_t)std::min<int64_t>(e->r_blocks, INT32_MAX);
     L.blk_recs = e->r_blk_recs;
@@ -971,9 +986,18 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     for (int g : gs) e->rcur[g] ^= 1;
     e->r_matches = ratchet_count_matches(e);
     e->r_kernel_ms = ms;
+    e->r_wide = wide;
+    e->r_seq_base = B.seq_base;
+    e->r_ts = B.ts;
+    if (e->r_matches > 0 && B.ts != e->d_ts.p) {  // records outlive a caller-owned device batch
+      e->d_rbts.ensure(n);
+      HIPCHK(hipMemcpyAsync(e->d_rbts.p, B.ts, n * 8, hipMemcpyDeviceToDevice, e->stream));
+      e->r_ts = e->d_rbts.p;
+    }
     // algorithmic bytes: every group streams the batch's operand columns once
     // (ts + x-atom column + f0 columns; the warm-up re-reads are overhead, not counted), writes
-    // 32 B per match and reads + writes its persisted deques (24 B per pending partial)
+    // 32 B per match (SURVEY §8(d)'s unit; the device record is 8 B, expanded at poll) and reads +
+    // writes its persisted deques (24 B per pending partial)
     double bytes = 0;
     for (int g : gs) {
       const RatchetGroup& G = e->rg[g];
@@ -991,36 +1015,37 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
   throw Error(SDH_E_CAPACITY, "ratchet launch did not converge");
 }
 
-// append the last ratchet launch's matches (block-compacted) to the host backlog
+// append the last ratchet launch's matches to the host backlog (decoded to (qid, ts, seq1, seq2))
 void ratchet_collect(sdh_engine* e) {
   const int nb = e->r_blocks_used;
   if (nb == 0 || e->r_matches == 0) return;
-  std::vector<int64_t> seg_off(nb), dst_off(nb), cnt(nb);
+  std::vector<int64_t> dst_off(nb);
   int64_t acc = 0;
   for (int i = 0; i < nb; ++i) {
-    seg_off[i] = (int64_t)i * e->r_blk_recs;
     dst_off[i] = acc;
-    cnt[i] = e->r_blk_count[i];
-    acc += cnt[i];
+    acc += e->r_blk_count[i];
   }
-  e->d_seg_off.ensure(nb);
   e->d_dst_off.ensure(nb);
-  DevBuf<int64_t> d_cnt;
-  d_cnt.ensure(nb);
   e->d_dense.ensure((size_t)acc * 4);
-  HIPCHK(hipMemcpyAsync(e->d_seg_off.p, seg_off.data(), nb * 8, hipMemcpyHostToDevice, e->stream));
   HIPCHK(hipMemcpyAsync(e->d_dst_off.p, dst_off.data(), nb * 8, hipMemcpyHostToDevice, e->stream));
-  HIPCHK(hipMemcpyAsync(d_cnt.p, cnt.data(), nb * 8, hipMemcpyHostToDevice, e->stream));
-  HIPCHK(sdh_launch_compact(e->d_rmatch.p, e->d_seg_off.p, d_cnt.p, e->d_dst_off.p, 4, nb, e->d_dense.p,
-                            e->stream));
-  std::vector<int64_t> rec((size_t)acc * 4);
-  HIPCHK(hipMemcpyAsync(rec.data(), e->d_dense.p, rec.size() * 8, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(sdh_launch_ratchet_decode(e->d_rmatch.p, e->r_blk_recs, e->r_wide, e->d_blk_count.p, e->d_blk_group.p,
+                                   e->d_dst_off.p, e->d_rg.p, e->r_ts, e->r_seq_base, nb, e->d_dense.p,
+                                   e->stream));
   const int RW = e->rec_words;
   const size_t base = e->backlog.size();
-  e->backlog.resize(base + (size_t)acc * RW, 0);
-  for (int64_t i = 0; i < acc; ++i)
-    for (int w = 0; w < 4; ++w) e->backlog[base + i * RW + w] = rec[i * 4 + w];
+  if (RW == 4) {
+    e->backlog.resize(base + (size_t)acc * 4);
+    HIPCHK(hipMemcpyAsync(e->backlog.data() + base, e->d_dense.p, (size_t)acc * 32, hipMemcpyDeviceToHost,
+                          e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  } else {
+    std::vector<int64_t> rec((size_t)acc * 4);
+    HIPCHK(hipMemcpyAsync(rec.data(), e->d_dense.p, rec.size() * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->backlog.resize(base + (size_t)acc * RW, 0);
+    for (int64_t i = 0; i < acc; ++i)
+      for (int w = 0; w < 4; ++w) e->backlog[base + i * RW + w] = rec[i * 4 + w];
+  }
   e->r_matches = 0;
   e->r_blocks_used = 0;
 }

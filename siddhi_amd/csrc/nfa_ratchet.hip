@@ -435,7 +435,6 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   D.smask = SC - 1;
   D.sbase = ((size_t)wid * SC) * WAVE;
   const bool active = lane < G->n_lanes;
-  const int64_t qid = G->qid[lane & 63];
   const int64_t within = G->within[lane & 63];
   const int64_t wmax = G->wmax;
   const bool has_within = wmax >= 0;
@@ -706,11 +705,13 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   refresh_bottom();
 
   int blk = -1, fill = 0;
-  int64_t* wp = nullptr;  // next record of the wave's current output block
+  uint2* wp = nullptr;  // next record of the wave's current output block
+  const int rsh = L.wide ? 1 : 0;  // record size: 8 B << rsh
   int64_t prev_tile_ts = (W.c0 == 0) ? L.b.prev_ts : L.b.ts[W.c0 - 1];
 
-  // one record per lane with `mt` (ballot m): per-wave output blocks (one atomic per block), ranks by mbcnt
-  auto emit = [&](bool mt, uint64_t m, int64_t tt, int64_t s1, int64_t s) {
+  // one record per lane with `mt` (ballot m): per-wave output blocks (one atomic per block), ranks
+  // by mbcnt. e2 = batch event `off`; e1 = the partial with low seq bits q1
+  auto emit = [&](bool mt, uint64_t m, uint32_t off, uint32_t q1) {
     if (mover) return;
     const int c = __popcll(m);
     if (blk < 0 || fill + c > L.blk_recs) {
@@ -723,16 +724,17 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
         mover = true;
         return;
       }
+      if (lane == 0) L.blk_group[nb] = W.g;
       blk = nb;
       fill = 0;
-      wp = L.match + (size_t)blk * L.blk_recs * 4;
+      wp = reinterpret_cast<uint2*>(L.match) + ((size_t)blk * L.blk_recs << rsh);
     }
     if (mt) {
-      longlong2* r = reinterpret_cast<longlong2*>(wp + (size_t)wave_mbcnt(m) * 4);
-      r[0] = make_longlong2(qid, tt);
-      r[1] = make_longlong2(s1, s);
+      const int r = wave_mbcnt(m);
+      if (!L.wide) wp[r] = make_uint2(off | ((uint32_t)lane << 26), q1);
+      else reinterpret_cast<uint4*>(wp)[r] = make_uint4(off, (uint32_t)lane, q1, 0u);
     }
-    wp += (size_t)c * 4;
+    wp += (size_t)c << rsh;
     fill += c;
   };
 
@@ -808,15 +810,16 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
         const bool c1 = mt && D.ln > 1 && xop<KK, XM>(xmask, x, k1);
         const bool c2 = c1 && D.ln > 2 && xop<KK, XM>(xmask, x, k2);
         const bool c3 = c2 && D.ln > 3 && xop<KK, XM>(xmask, x, k3);
-        emit(mt, m, tt, s - (int64_t)(uint32_t)(slo - tseq), s);
+        const uint32_t off = (uint32_t)(t + k);
+        emit(mt, m, off, tseq);
         const uint64_t m1 = __ballot(c1);
         if (m1) {
-          emit(c1, m1, tt, s - (int64_t)(uint32_t)(slo - q1), s);
+          emit(c1, m1, off, q1);
           const uint64_t m2 = __ballot(c2);
           if (m2) {
-            emit(c2, m2, tt, s - (int64_t)(uint32_t)(slo - q2), s);
+            emit(c2, m2, off, q2);
             const uint64_t m3 = __ballot(c3);
-            if (m3) emit(c3, m3, tt, s - (int64_t)(uint32_t)(slo - q3), s);
+            if (m3) emit(c3, m3, off, q3);
           }
         }
         const int p = (int)mt + (int)c1 + (int)c2 + (int)c3;
@@ -898,6 +901,39 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   (void)W64;
 }
 
+// expand the match blocks of one launch to dense (qid, ts, seq1, seq2) rows: one workgroup per block
+__global__ __launch_bounds__(256) void ratchet_decode(const int64_t* __restrict__ match, int blk_recs, int wide,
+                                                      const int32_t* __restrict__ blk_count,
+                                                      const int32_t* __restrict__ blk_group,
+                                                      const int64_t* __restrict__ dst_off,
+                                                      const RatchetGroup* __restrict__ groups,
+                                                      const int64_t* __restrict__ ts, int64_t seq_base,
+                                                      int64_t* __restrict__ out) {
+  const int b = blockIdx.x;
+  const int n = blk_count[b];
+  const RatchetGroup* G = groups + blk_group[b];
+  const uint2* R = reinterpret_cast<const uint2*>(match) + ((size_t)b * blk_recs << (wide ? 1 : 0));
+  longlong2* O = reinterpret_cast<longlong2*>(out) + (size_t)dst_off[b] * 2;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t off, ln, q1;
+    if (!wide) {
+      const uint2 r = R[i];
+      off = r.x & ((1u << 26) - 1);
+      ln = r.x >> 26;
+      q1 = r.y;
+    } else {
+      const uint4 r = reinterpret_cast<const uint4*>(R)[i];
+      off = r.x;
+      ln = r.y & 63;
+      q1 = r.z;
+    }
+    const int64_t s = seq_base + (int64_t)off;
+    const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
+    O[2 * (size_t)i] = make_longlong2(G->qid[ln], ts[off]);
+    O[2 * (size_t)i + 1] = make_longlong2(s1, s);
+  }
+}
+
 // per aligned 64-event tile: max and min x-atom key over the valid events (one wave per tile)
 template <int KK>
 __global__ __launch_bounds__(256) void ratchet_tile_summary(StreamBatch b, int attr, int conv, int64_t n_tiles,
@@ -952,6 +988,17 @@ extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::Stream
     case sdh::KK_F64: hipLaunchKernelGGL(sdh::ratchet_tile_summary<sdh::KK_F64>, grid, block, 0, s, *B, attr, conv, n_tiles, tmax, tmin, thas); break;
     default: hipLaunchKernelGGL(sdh::ratchet_tile_summary<sdh::KK_I64>, grid, block, 0, s, *B, attr, conv, n_tiles, tmax, tmin, thas); break;
   }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sdh_launch_ratchet_decode(const int64_t* match, int blk_recs, int wide,
+                                                const int32_t* blk_count, const int32_t* blk_group,
+                                                const int64_t* dst_off, const sdh::RatchetGroup* groups,
+                                                const int64_t* ts, int64_t seq_base, int n_blocks, int64_t* out,
+                                                hipStream_t s) {
+  if (n_blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::ratchet_decode, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, wide, blk_count,
+                     blk_group, dst_off, groups, ts, seq_base, out);
   return hipGetLastError();
 }
 

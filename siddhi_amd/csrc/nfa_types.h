@@ -190,10 +190,16 @@ struct RatchetLaunch {
   int64_t* lds_ts;              // [item][ML][64] ts0 of the LDS ring entries
   uint4* spillA;                // [item][SC][64] deque entries beyond the LDS ring
   uint32_t* spillB;             //   (seq words of 64-bit-key entries)
-  int64_t* match;               // blocks of blk_recs records x 4 int64 (qid, ts, seq1, seq2)
+  // match records, in per-wave blocks of blk_recs records. Narrow (wide == 0, batches of at most
+  // 2^26 events): 8 B {e2 batch offset | lane << 26, low 32 bits of e1's seq}; wide: 16 B
+  // {e2 batch offset, lane, low 32 bits of e1's seq, 0}. The block's group is blk_group[block];
+  // sdh_launch_ratchet_decode expands records to (qid, ts, seq1, seq2)
+  int64_t* match;
   int32_t* blk_count;           // records written per block
+  int32_t* blk_group;           // group of the wave that owns the block
   int32_t* blk_next;            // [0] next free block
   int32_t n_blocks, blk_recs;
+  int32_t wide;
   int32_t* err;                 // [0] deque overflow, [1] unordered ts, [2] match overflow
 };
 

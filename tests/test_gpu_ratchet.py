@@ -171,3 +171,74 @@ def test_ratchet_snapshot_restore():
     b.engine.push_columns(0, ts2, cols2)
     assert b.engine.take_matches(lambda q: 2) == ref
     assert len(ref) > 1000
+
+
+class _Hip:
+    """Device buffers through the HIP runtime the engine library links (libamdhip64)."""
+
+    def __init__(self):
+        import ctypes
+        self.c = ctypes
+        self.rt = ctypes.CDLL("libamdhip64.so.7")
+        self.bufs = []
+
+    def put(self, arr):
+        c = self.c
+        arr = np.ascontiguousarray(arr)
+        p = c.c_void_p()
+        assert self.rt.hipMalloc(c.byref(p), c.c_size_t(max(1, arr.nbytes))) == 0
+        assert self.rt.hipMemcpy(p, c.c_void_p(arr.ctypes.data), c.c_size_t(arr.nbytes), 1) == 0
+        self.bufs.append(p)
+        return p.value
+
+    def fill(self, ptr, nbytes, byte):
+        assert self.rt.hipMemset(self.c.c_void_p(ptr), byte, self.c.c_size_t(nbytes)) == 0
+        assert self.rt.hipDeviceSynchronize() == 0
+
+    def free(self):
+        for p in self.bufs:
+            self.rt.hipFree(p)
+
+
+def test_device_batch_records_outlive_caller_buffer():
+    """Records of a device-resident batch are decoded at poll time, after the caller has reused its
+    buffers: the engine keeps its own copy of the batch's timestamps."""
+    src = c2_app(40)
+    a, b = hip_app(src), hip_app(src)
+    ts, cols = c2_columns(0, 20000)
+    h = _Hip()
+    try:
+        dts = h.put(ts)
+        a.engine.push_device(0, len(ts), dts, [h.put(c) for c in cols])
+        h.fill(dts, ts.nbytes, 0xFF)
+        b.engine.push_columns(0, ts, cols)
+        x, y = a.engine.poll(), b.engine.poll()
+    finally:
+        h.free()
+    assert len(x[0]) > 10000
+    for u, v in zip(x, y):
+        assert np.array_equal(u, v)
+
+
+def test_wide_records_for_batches_beyond_2_26_events():
+    """A push of more than 2^26 events uses 16-B device records; the same events pushed as two
+    smaller batches (8-B records) must give identical matches."""
+    n = (1 << 26) + 4_000_000
+    qs = ["define stream StockStream (symbol string, price float, volume int);"]
+    for p in range(4):
+        qs.append(f"@info(name='w{p}') from every e1=StockStream[price > {99.2 + p / 10}] -> "
+                  f"e2=StockStream[price > e1.price] within {1 + p} sec select e1.price as p1 insert into O;")
+    src = " ".join(qs)
+    a, b = hip_app(src), hip_app(src)
+    ts, cols = c2_columns(0, n)
+    a.engine.push_columns(0, ts, cols)
+    x = a.engine.poll()
+    h = n // 2 + 12345
+    b.engine.push_columns(0, ts[:h], [c[:h] for c in cols])
+    y0 = b.engine.poll()
+    b.engine.push_columns(0, ts[h:], [c[h:] for c in cols])
+    y1 = b.engine.poll()
+    assert len(x[0]) > 500_000
+    for i in (0, 1, 2, 4):  # query, key, ts, slot words
+        assert np.array_equal(x[i], np.concatenate([y0[i], y1[i]]))
+    assert np.array_equal(x[3], np.concatenate([y0[3], y1[3][1:] + y0[3][-1]]))
