@@ -35,6 +35,7 @@ extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaun
                                        size_t lds, hipStream_t s);
 extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int nf, int ML, int SC,
                                          const sdh::RatchetLaunch* L, hipStream_t s);
+extern "C" int sdh_ratchet_occupancy(int key_kind, int full, int nf, int ML);
 extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::StreamBatch* B, int attr, int conv,
                                                  int64_t n_tiles, uint64_t* tmax, uint64_t* tmin, uint8_t* thas,
                                                  hipStream_t s);
@@ -569,7 +570,9 @@ struct sdh_engine {
   int r_blk_recs = 8192;
   int r_blocks_used = 0;             // of the last launch
   std::vector<int32_t> r_blk_count;
-  int rML = 16;                      // LDS ring entries per lane (power of two)
+  int rML = 8;                       // LDS ring entries per lane (power of two)
+  double r_waves = 0;                // resident-wave target per launch (0: CUs x occupancy)
+  int n_cu = 256;
   std::vector<std::array<int, 4>> r_sum_specs;  // tile-summary rows: (stream, attr, conv, key kind)
   DevBuf<uint64_t> d_tsmax, d_tsmin;
   DevBuf<uint8_t> d_tshas;
@@ -860,30 +863,44 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     const bool full = e->r_full_expiry[stream] != 0 || t01[0] < -lim || t01[0] > lim || t01[1] < -lim ||
                       t01[1] > lim || (B.prev_ts != INT64_MIN && (B.prev_ts < -lim || B.prev_ts > lim));
     // ---- chunk planning: chunk c > 0 rebuilds its starting deques by a reverse scan of the
-    // `within` window (a few instructions per 64 events), so chunks can be short: aim for
-    // ~4096 waves (16 per CU) of at least min_chunk emitted events each ----
-    const double target_waves = 4096.0;
+    // `within` window (a few instructions per 64 events), so chunks can be short. Each launch
+    // (one key kind x orientation) gets one resident wave per slot of the chip -- CUs x the
+    // kernel's occupancy -- of at least min_chunk emitted events each ----
     const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : 2048;
-    const double len = std::max((double)min_chunk, (double)n * gs.size() / target_waves);
     e->ritems.clear();
     std::vector<int> order(gs);
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
       return std::make_pair(e->rg[a].key_kind, e->rg[a].xmask) < std::make_pair(e->rg[b].key_kind, e->rg[b].xmask);
     });
-    for (int g : order) {
-      const RatchetGroup& G = e->rg[g];
-      int64_t C = 1;
-      if (!full && G.wmax >= 0) C = std::max<int64_t>(1, (int64_t)std::ceil((double)n / len));
-      for (int64_t ch = 0; ch < C; ++ch) {
-        RatchetItem it{};
-        it.g = g;
-        it.chunk = (int)ch;
-        it.n_chunks = (int)C;
-        it.inb = e->rcur[g];
-        it.c0 = n * ch / C;
-        it.c1 = n * (ch + 1) / C;
-        e->ritems.push_back(it);
+    for (size_t i0 = 0; i0 < order.size();) {
+      const RatchetGroup& G0 = e->rg[order[i0]];
+      size_t i1 = i0;
+      int nf = 0;
+      while (i1 < order.size() && e->rg[order[i1]].key_kind == G0.key_kind && e->rg[order[i1]].xmask == G0.xmask)
+        nf = std::max(nf, e->rg[order[i1++]].n_f0);
+      double slots = e->r_waves;
+      if (slots <= 0) {
+        const int occ = sdh_ratchet_occupancy(G0.key_kind, full, nf, e->rML);
+        slots = (double)e->n_cu * std::max(1, occ);
       }
+      const double len = std::max((double)min_chunk, (double)n * (double)(i1 - i0) / slots);
+      for (size_t i = i0; i < i1; ++i) {
+        const int g = order[i];
+        const RatchetGroup& G = e->rg[g];
+        int64_t C = 1;
+        if (!full && G.wmax >= 0) C = std::max<int64_t>(1, (int64_t)std::ceil((double)n / len));
+        for (int64_t ch = 0; ch < C; ++ch) {
+          RatchetItem it{};
+          it.g = g;
+          it.chunk = (int)ch;
+          it.n_chunks = (int)C;
+          it.inb = e->rcur[g];
+          it.c0 = n * ch / C;
+          it.c1 = n * (ch + 1) / C;
+          e->ritems.push_back(it);
+        }
+      }
+      i0 = i1;
     }
     const int n_items = (int)e->ritems.size();
     e->d_ritems.ensure(n_items);
@@ -1424,6 +1441,10 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     HIPCHK(hipGetDeviceCount(&ndev));
     if (ndev <= 0) throw Error(SDH_E_DEVICE, "no HIP device (the engine has no CPU fallback)");
     HIPCHK(hipSetDevice(e->dev));
+    HIPCHK(hipDeviceGetAttribute(&e->n_cu, hipDeviceAttributeMultiprocessorCount, e->dev));
+    // tuning overrides for kernel experiments: K_ratchet LDS ring depth and waves per launch
+    if (const char* v = getenv("SDH_RATCHET_ML")) e->rML = std::max(4, atoi(v));
+    if (const char* v = getenv("SDH_RATCHET_WAVES")) e->r_waves = atof(v);
     e->prog = read_ir(ir, len);
     try {
       e->lp = kg::read_program(ir, len);

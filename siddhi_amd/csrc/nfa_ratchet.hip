@@ -1009,6 +1009,23 @@ static void launch_one(const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t 
   hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF>), dim3(L->n_items), dim3(64), lds, s, *L, ML, SC);
 }
 
+template <int KK, int XM, bool FULL, int NF>
+static int occupancy_one(int ML) {
+  const bool w64 = (KK == sdh::KK_F64 || KK == sdh::KK_I64);
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sdh::nfa_ratchet_kernel<KK, XM, FULL, NF>, 64,
+                                                   (size_t)ML * 64 * (w64 ? 16 : 8)) != hipSuccess)
+    return 0;
+  return nb;
+}
+
+template <int KK>
+static int occupancy_kk(bool full, int nf, int ML) {
+  // the four orientations share one register allocation; XM = 0 stands for all
+  if (full) return occupancy_one<KK, -1, true, sdh::RMAXF0>(ML);
+  return nf <= 1 ? occupancy_one<KK, 0, false, 1>(ML) : occupancy_one<KK, 0, false, sdh::RMAXF0>(ML);
+}
+
 // nf: max f0 atoms over the launched groups (one-atom start filters get a leaner register set)
 template <int KK>
 static hipError_t launch_kk(int xm, bool full, int nf, const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {
@@ -1030,6 +1047,16 @@ static hipError_t launch_kk(int xm, bool full, int nf, const sdh::RatchetLaunch*
     }
   }
   return hipGetLastError();
+}
+
+// resident waves per CU of the K_ratchet instantiation (chunk planning fills the chip in one round)
+extern "C" int sdh_ratchet_occupancy(int key_kind, int full, int nf, int ML) {
+  switch (key_kind) {
+    case sdh::KK_F32: return occupancy_kk<sdh::KK_F32>(full, nf, ML);
+    case sdh::KK_I32: return occupancy_kk<sdh::KK_I32>(full, nf, ML);
+    case sdh::KK_F64: return occupancy_kk<sdh::KK_F64>(full, nf, ML);
+    default: return occupancy_kk<sdh::KK_I64>(full, nf, ML);
+  }
 }
 
 // xmask: normalized `cur OP key` CmpMask of the launched groups (all equal); nf: max f0 atoms;

@@ -63,6 +63,7 @@ def load_library(path: str = LIB_PATH):
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("SIDDHI_HIP_LIB", path)  # alternative builds (kernel tuning experiments)
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
                            "(the HIP engine has no CPU fallback)")
