@@ -194,7 +194,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic[0] if traffic else None,
                      "traffic_source": traffic[1] if traffic else None,
-                     "kernel": kernel, "kernel_ms": avg_ms},
+                     "kernel": kernel, "kernel_ms": avg_ms,
+                     # measured HBM rate (PMC traffic / live kernel time); below `achieved` when the
+                     # device record is narrower than §8(d)'s 32-B match unit
+                     "traffic_gbps": (traffic[0] / (avg_ms * 1e-3) / 1e9) if traffic else None},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.workload, K, args.cpu_seconds)
