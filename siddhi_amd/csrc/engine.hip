@@ -526,6 +526,8 @@ struct sdh_engine {
   DevBuf<kg::GQuery> d_gq;
   std::vector<int32_t> lane_q;       // [group][64]
   DevBuf<int32_t> d_lane_q;
+  std::vector<int32_t> group_tmpl;   // [group] shape template (a member query)
+  DevBuf<int32_t> d_group_tmpl;
   int gB32 = 1, gB64 = 1;
   struct GenSet {
     int partition = -1;              // -1: the unpartitioned K_gen queries
@@ -1095,12 +1097,29 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
     auto gs = std::make_unique<sdh_engine::GenSet>();
     gs->partition = partition;
     gs->group_base = (int)(e->lane_q.size() / 64);
-    gs->n_groups = (int)((members.size() + 63) / 64);
-    for (int g = 0; g < gs->n_groups; ++g)
-      for (int l = 0; l < 64; ++l) {
-        const size_t k = (size_t)g * 64 + l;
-        e->lane_q.push_back(k < members.size() ? gidx[members[k]] : -1);
+    // one shape per group: members are bucketed by kg::shape_of (first-appearance order) and each
+    // bucket is padded to whole groups, so a wave's control flow is its template's. Lane order is
+    // free: matches are ordered on the host by (seq, out_rank, emission index).
+    std::vector<std::pair<std::string, std::vector<int>>> shapes;
+    for (int qi : members) {
+      const kg::GQuery sh = kg::shape_of(e->gq[gidx[qi]]);
+      std::string sig((const char*)&sh, sizeof sh);
+      auto it = std::find_if(shapes.begin(), shapes.end(), [&](const auto& b) { return b.first == sig; });
+      if (it == shapes.end()) shapes.emplace_back(std::move(sig), std::vector<int>{gidx[qi]});
+      else it->second.push_back(gidx[qi]);
+    }
+    gs->n_groups = 0;
+    for (const auto& b : shapes) {
+      const int ng = (int)((b.second.size() + 63) / 64);
+      for (int g = 0; g < ng; ++g) {
+        e->group_tmpl.push_back(b.second[0]);
+        for (int l = 0; l < 64; ++l) {
+          const size_t k = (size_t)g * 64 + l;
+          e->lane_q.push_back(k < b.second.size() ? b.second[k] : -1);
+        }
       }
+      gs->n_groups += ng;
+    }
     const size_t per_block32 = (size_t)e->gB32 * 64, per_block64 = (size_t)e->gB64 * 64;
     if (partition < 0) {
       gs->a32.ensure(per_block32 * gs->n_groups);
@@ -1139,6 +1158,8 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   HIPCHK(hipMemcpy(e->d_gq.p, e->gq.data(), e->gq.size() * sizeof(kg::GQuery), hipMemcpyHostToDevice));
   e->d_lane_q.ensure(e->lane_q.size());
   HIPCHK(hipMemcpy(e->d_lane_q.p, e->lane_q.data(), e->lane_q.size() * 4, hipMemcpyHostToDevice));
+  e->d_group_tmpl.ensure(e->group_tmpl.size());
+  HIPCHK(hipMemcpy(e->d_group_tmpl.p, e->group_tmpl.data(), e->group_tmpl.size() * 4, hipMemcpyHostToDevice));
   e->g_chunk_next.ensure(1);
   e->g_nrec.ensure(1);
 }
@@ -1195,6 +1216,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     sdh::GenLaunch L{};
     L.queries = e->d_gq.p;
     L.lane_q = e->d_lane_q.p;
+    L.group_tmpl = e->d_group_tmpl.p;
     L.b = B;
     L.groups = gs.n_groups;
     L.group_base = gs.group_base;

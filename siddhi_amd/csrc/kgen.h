@@ -220,7 +220,14 @@ enum { FL_CHANGED = 1, FL_INIT = 2, FL_SUCCESS = 4, FL_SSRESET = 8, FL_RETURNED 
 struct Emitter;  // defined by the caller: void emit(const Ctx&, int se)
 
 struct Ctx {
+  // q: the query's structure. On the device it is the wave's template -- every lane of a group has
+  // the same structure (the host groups queries by shape), so q is wave-uniform and its fields are
+  // scalar loads. ql: the lane's own query, read only for what differs within a shape (bytecode
+  // constants, `within`, qid). lay/within are cached in registers for the whole item.
   const GQuery* q;
+  const GQuery* ql;
+  GLayout lay;
+  int64_t within;
   int32_t* w32;
   int64_t* w64;
   int64_t stride;
@@ -239,23 +246,29 @@ struct Ctx {
   KG_FN int32_t& i32(int i) const { return w32[(int64_t)i * stride]; }
   KG_FN int64_t& i64(int i) const { return w64[(int64_t)i * stride]; }
   KG_FN const GState& S(int i) const { return q->st[i]; }
-  KG_FN int nS() const { return q->lay.S; }
+  KG_FN int nS() const { return lay.S; }
+  KG_FN void bind(const GQuery* tmpl, const GQuery* own) {
+    q = tmpl;
+    ql = own;
+    lay = tmpl->lay;
+    within = own->within;
+  }
 
   // ---- arena fields ----
-  KG_FN int32_t& flags(int i) const { return i32(q->lay.o_flags + i); }
-  KG_FN int32_t& pn(int i) const { return i32(q->lay.o_pn + i); }
-  KG_FN int32_t& nn(int i) const { return i32(q->lay.o_nn + i); }
-  KG_FN int32_t& pl(int i, int k) const { return i32(q->lay.o_plist + i * q->lay.LC + k); }
-  KG_FN int32_t& nl(int i, int k) const { return i32(q->lay.o_nlist + i * q->lay.LC + k); }
-  KG_FN int32_t& slot(int se, int i) const { return i32(q->lay.o_seslot + se * q->lay.S + i); }
-  KG_FN int64_t& se_ts(int se) const { return i64(q->lay.o_sets + se); }
-  KG_FN int32_t& nd_next(int n) const { return i32(q->lay.o_ndnext + n); }
-  KG_FN int32_t& nd_null(int n) const { return i32(q->lay.o_ndnull + n); }
-  KG_FN int64_t& nd_seq(int n) const { return i64(q->lay.o_ndseq + n); }
-  KG_FN int64_t& nd_ts(int n) const { return i64(q->lay.o_ndts + n); }
-  KG_FN int64_t& nd_val(int n, int j) const { return i64(q->lay.o_ndval + n * q->lay.NA + j); }
-  KG_FN int64_t& se_used() const { return i64(q->lay.o_seused); }
-  KG_FN int64_t& nd_used(int w) const { return i64(q->lay.o_ndused + w); }
+  KG_FN int32_t& flags(int i) const { return i32(lay.o_flags + i); }
+  KG_FN int32_t& pn(int i) const { return i32(lay.o_pn + i); }
+  KG_FN int32_t& nn(int i) const { return i32(lay.o_nn + i); }
+  KG_FN int32_t& pl(int i, int k) const { return i32(lay.o_plist + i * lay.LC + k); }
+  KG_FN int32_t& nl(int i, int k) const { return i32(lay.o_nlist + i * lay.LC + k); }
+  KG_FN int32_t& slot(int se, int i) const { return i32(lay.o_seslot + se * lay.S + i); }
+  KG_FN int64_t& se_ts(int se) const { return i64(lay.o_sets + se); }
+  KG_FN int32_t& nd_next(int n) const { return i32(lay.o_ndnext + n); }
+  KG_FN int32_t& nd_null(int n) const { return i32(lay.o_ndnull + n); }
+  KG_FN int64_t& nd_seq(int n) const { return i64(lay.o_ndseq + n); }
+  KG_FN int64_t& nd_ts(int n) const { return i64(lay.o_ndts + n); }
+  KG_FN int64_t& nd_val(int n, int j) const { return i64(lay.o_ndval + n * lay.NA + j); }
+  KG_FN int64_t& se_used() const { return i64(lay.o_seused); }
+  KG_FN int64_t& nd_used(int w) const { return i64(lay.o_ndused + w); }
 
   KG_FN void fail(int e) {
     if (err == GE_OK) err = e;
@@ -282,17 +295,17 @@ struct Ctx {
     for (int k = 0; k < npin; ++k) mark_se(pins[k], sm, nm);
     for (int k = 0; k < n_ret; ++k) mark_se(ret[k], sm, nm);
     se_used() = (int64_t)sm;
-    for (int w = 0; w < q->lay.NU; ++w) nd_used(w) = (int64_t)nm[w];
+    for (int w = 0; w < lay.NU; ++w) nd_used(w) = (int64_t)nm[w];
   }
   KG_FN int find_free_se() const {
     const uint64_t u = (uint64_t)se_used();
-    const uint64_t fr = ~u & (q->lay.R >= 64 ? ~0ull : ((1ull << q->lay.R) - 1));
+    const uint64_t fr = ~u & (lay.R >= 64 ? ~0ull : ((1ull << lay.R) - 1));
     if (!fr) return -1;
     return __builtin_ctzll(fr);
   }
   KG_FN int find_free_nd() const {
-    for (int w = 0; w < q->lay.NU; ++w) {
-      const int lim = q->lay.N - w * 64;
+    for (int w = 0; w < lay.NU; ++w) {
+      const int lim = lay.N - w * 64;
       const uint64_t u = (uint64_t)nd_used(w);
       const uint64_t fr = ~u & (lim >= 64 ? ~0ull : ((1ull << lim) - 1));
       if (fr) return w * 64 + __builtin_ctzll(fr);
@@ -347,14 +360,14 @@ struct Ctx {
 
   // ---- lists ----
   KG_FN void nae_push(int i, int se) {
-    if (nn(i) >= q->lay.LC) { fail(GE_CAPACITY); return; }
+    if (nn(i) >= lay.LC) { fail(GE_CAPACITY); return; }
     nl(i, nn(i)) = se;
     nn(i) += 1;
   }
   KG_FN void promote(int i) {  // pending.addAll(newAndEvery); newAndEvery.clear()
     if ((flags(i) & FL_ITER) && nn(i) > 0) { fail(GE_REFERENCE); return; }  // Java CME
     const int n = nn(i);
-    if (pn(i) + n > q->lay.LC) { fail(GE_CAPACITY); return; }
+    if (pn(i) + n > lay.LC) { fail(GE_CAPACITY); return; }
     for (int k = 0; k < n; ++k) pl(i, pn(i) + k) = nl(i, k);
     pn(i) += n;
     nn(i) = 0;
@@ -464,13 +477,13 @@ struct Ctx {
   }
   KG_FN bool is_expired(int i, int se) const {  // StreamPreStateProcessor.isExpired:102-113
     const GState& s = S(i);
-    if (s.is_start || q->within < 0) return false;
+    if (s.is_start || within < 0) return false;
     for (int k = 0; k < q->n_start; ++k) {
       const int n = slot(se, q->start_ids[k]);
       if (n >= 0) {
         const int64_t d = (int64_t)((uint64_t)nd_ts(n) - (uint64_t)ts);
         const int64_t a = d < 0 ? (int64_t)(0ull - (uint64_t)d) : d;
-        if (a > q->within) return true;
+        if (a > within) return true;
       }
     }
     return false;
@@ -512,11 +525,12 @@ struct Ctx {
     for (int pc = b; pc < e; ++pc) {
       const GInsn& in = q->code[pc];
       switch (in.op) {
-        case OP_CONST: {
+        case OP_CONST: {  // constants differ within a shape: the lane's own query
+          const int64_t imm = ql->code[pc].imm;
           Val v{in.res, 0, 0};
-          if (in.res == T_FLOAT) v.bits = (int64_t)(uint32_t)in.imm;
-          else if (in.res == T_INT) v.bits = (int32_t)in.imm;
-          else v.bits = in.imm;
+          if (in.res == T_FLOAT) v.bits = (int64_t)(uint32_t)imm;
+          else if (in.res == T_INT) v.bits = (int32_t)imm;
+          else v.bits = imm;
           st[sp++] = v;
           break;
         }
@@ -780,6 +794,19 @@ inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA) {
   L.o_ndts = o; o += N;
   L.o_ndval = o; o += N * NA;
   L.n64 = o;
+}
+
+// Shape of a query: the lowered program with what may differ between lanes of one wave cleared
+// (qid, rank, the `within` value -- its presence stays -- and bytecode constants). Queries with
+// equal shapes share one wave-uniform template on the device.
+inline GQuery shape_of(const GQuery& g) {
+  GQuery s = g;
+  s.qid = 0;
+  s.rank = 0;
+  s.within = g.within < 0 ? -1 : 0;
+  for (int pc = 0; pc < s.n_code; ++pc)
+    if (s.code[pc].op == OP_CONST) s.code[pc].imm = 0;
+  return s;
 }
 
 }  // namespace kg

@@ -87,11 +87,13 @@ __global__ __launch_bounds__(64) void nfa_gen_kernel(GenLaunch L) {
   }
   const int qi = L.lane_q[(int64_t)(L.group_base + g) * 64 + lane];
   if (qi < 0) return;
-  const kg::GQuery* __restrict__ q = L.queries + qi;
+  // wave-uniform shape template (scalar loads) + the lane's own query (constants)
+  const kg::GQuery* __restrict__ q = L.queries + L.group_tmpl[L.group_base + g];
+  const kg::GQuery* __restrict__ ql = L.queries + qi;
   if (q->recv_n[L.b.stream] == 0) return;  // this query does not read the stream
   const int64_t block = L.block_base + (int64_t)kid * L.groups + g;
   kg::Ctx c;
-  c.q = q;
+  c.bind(q, ql);
   c.w32 = L.a32 + block * L.B32 * 64 + lane;
   c.w64 = L.a64 + block * L.B64 * 64 + lane;
   c.stride = 64;
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(64) void nfa_gen_kernel(GenLaunch L) {
       int64_t* r = o.reserve(words);
       if (!r) return;
       r[0] = words;
-      r[1] = q->qid;
+      r[1] = ql->qid;
       r[2] = key;
       r[3] = cx.se_ts(se);
       r[4] = cx.seq;

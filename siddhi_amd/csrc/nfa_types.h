@@ -213,6 +213,7 @@ struct GQuery;
 struct GenLaunch {
   const kg::GQuery* queries;
   const int32_t* lane_q;      // [group][64] query index (-1 = idle lane)
+  const int32_t* group_tmpl;  // [group] query whose structure every lane of the group shares
   StreamBatch b;
   const int32_t* seg_begin;   // [n_seg] ranges into ev_idx (nullptr: one segment = whole batch)
   const int32_t* seg_len;

@@ -53,7 +53,7 @@ Inst* make_inst(Host* h, int qi, int64_t key) {
 void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* vals, const uint8_t* nulls) {
   const GQuery& q = h->gq[in->qi];
   Ctx c{};
-  c.q = &q;
+  c.bind(&q, &q);
   c.w32 = in->w32.data();
   c.w64 = in->w64.data();
   c.stride = 1;
