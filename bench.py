@@ -29,10 +29,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["c2", "c3"], default="c2",
-                    help="c2: BASELINE configs[1] (headline); c3: configs[2] (count/logical, partitioned)")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2",
+                    help="c2: BASELINE configs[1] (headline); c3: configs[2] (count/logical, partitioned); "
+                         "c4: configs[3] (fraud-rule sequences, one GPU's pattern-set shard)")
     ap.add_argument("--keys", type=int, default=10000, help="C3 partition keys (symbols)")
-    ap.add_argument("--patterns", type=int, default=1000)
+    ap.add_argument("--patterns", type=int, default=0,
+                    help="patterns per GPU (default: 1000; c4: 1250 = 10K sequences / 8 GPUs)")
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--partials", type=int, default=128)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget")
@@ -57,14 +59,15 @@ def cpu_baseline(workload, n_symbols, budget_s):
     stream until the time budget is spent."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from harness import App
-    from siddhi_amd.workloads import c2_app, c3_app, stock_events
+    from siddhi_amd.workloads import c2_app, c3_app, c4_app, stock_events, txn_events
     P = 32
-    app = App(c2_app(P) if workload == "c2" else c3_app(P))
+    app = App({"c2": c2_app, "c3": c3_app, "c4": c4_app}[workload](P))
     nslots = [len(q.states) for q in app.ir.queries]
     done, t0, start = 0, time.perf_counter(), 0
     n = 20000
     while time.perf_counter() - t0 < budget_s:
-        ts, sym, price, vol = stock_events(start, n, n_symbols=n_symbols)
+        gen = txn_events if workload == "c4" else stock_events
+        ts, sym, price, vol = gen(start, n, n_symbols)
         vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64),
                          vol.astype(np.int64)], 1)
         app.engine.send(0, ts, vals, None)
@@ -111,9 +114,15 @@ def main():
     from siddhi_amd.planner import plan
     from siddhi_amd.workloads import stock_events
 
-    P = args.patterns
-    K = args.keys if args.workload == "c3" else 100
-    if args.workload == "c2":
+    P = args.patterns or (1250 if args.workload == "c4" else 1000)
+    K = {"c2": 100, "c3": args.keys, "c4": 100_000}[args.workload]
+    if args.workload == "c4":
+        from siddhi_amd.workloads import c4_app
+        ir = plan(ql.parse(c4_app(P, first=rank * P)))
+        # a sequence instance holds at most one partial per state (R8): small pools, loud if exceeded
+        eng = HipEngine(ir.serialize(), device=local, flags=SDH_FLAG_DEVICE_MATCHES, gen_pool_states=8,
+                        gen_pool_nodes=32, gen_list_cap=8)
+    elif args.workload == "c2":
         ir = plan(ql.parse(c2_app_for_rank(rank, P)))
         eng = HipEngine(ir.serialize(), device=local, partials=args.partials, flags=SDH_FLAG_DEVICE_MATCHES)
     else:
@@ -126,8 +135,10 @@ def main():
     n_batches = args.warmup + args.steps
     # synthetic batches resident in HBM before the timed region
     batches = []
+    from siddhi_amd.workloads import txn_events
+    gen = txn_events if args.workload == "c4" else stock_events
     for s in range(n_batches):
-        ts, sym, price, vol = stock_events(s * B, B, n_symbols=K)
+        ts, sym, price, vol = gen(s * B, B, K)
         batches.append((torch.from_numpy(ts).to(dev), torch.from_numpy(sym).to(dev),
                         torch.from_numpy(price.view(np.int32)).to(dev), torch.from_numpy(vol).to(dev)))
     torch.cuda.synchronize()
@@ -171,9 +182,13 @@ def main():
         wl = ("C2: 1K concurrent 2-state filter+reference patterns "
               "(every e1[price>T_p] -> e2[price>e1.price] within W_p)")
         kernel = "nfa_ratchet_kernel"
-    else:
+    elif args.workload == "c3":
         wl = (f"C3: count <2:5> + logical and/or patterns, partition with (symbol) over {K} keys, "
               "within 10 sec")
+        kernel = "nfa_gen_kernel"
+    else:
+        wl = ("C4: fraud-rule sequences every e1=Txn[..], e2=Txn[..e1.amount*M], e3=Txn[..] within 1 min "
+              f"(strict contiguity), {K} accounts, pattern-set shard {rank * P}..{rank * P + P - 1}")
         kernel = "nfa_gen_kernel"
     traffic = profiled_traffic(kernel)
     result = {

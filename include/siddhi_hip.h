@@ -111,6 +111,8 @@ typedef struct sdh_stats {
   int64_t live_partials;     /* live partial matches after the last push                     */
   double last_kernel_ms;     /* device time of the last NFA-step launch (HIP events)         */
   double last_kernel_bytes;  /* algorithmic bytes of that launch (DESIGN.md roofline model)   */
+  int64_t last_gen_items;    /* K_gen work items (waves) of the last push: groups x key       */
+                             /* segments, or groups x event chunks           */
 } sdh_stats;
 
 int sdh_engine_create(const void* ir_blob, size_t len, const sdh_config* cfg, sdh_engine** out);

@@ -535,6 +535,8 @@ struct sdh_engine {
     int64_t key_cap = 0;             // instance blocks = key_cap * n_groups (partitioned)
     DevBuf<int32_t> a32;
     DevBuf<int64_t> a64;
+    DevBuf<int32_t> s32;             // scratch arenas of event chunks 1.. (unpartitioned sets)
+    DevBuf<int64_t> s64;
     // partition routing
     DevBuf<unsigned long long> tkey;
     DevBuf<int32_t> tid, n_keys;
@@ -547,9 +549,8 @@ struct sdh_engine {
   DevBuf<int32_t> r_idx, r_idx_s, r_cnt, r_off, r_nruns;
   DevBuf<uint8_t> r_temp;
   DevBuf<int64_t> g_out;
-  int64_t g_chunks = 0;
-  int g_chunk_words = 512;
-  DevBuf<int32_t> g_chunk_next;
+  int64_t g_out_cap = 0;             // K_gen match record words per push
+  DevBuf<unsigned long long> g_out_next;
   DevBuf<unsigned long long> g_nrec;
   std::vector<int64_t> g_host;       // collected K_gen records (variable length)
   int64_t g_host_n = 0;
@@ -1160,7 +1161,7 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   HIPCHK(hipMemcpy(e->d_lane_q.p, e->lane_q.data(), e->lane_q.size() * 4, hipMemcpyHostToDevice));
   e->d_group_tmpl.ensure(e->group_tmpl.size());
   HIPCHK(hipMemcpy(e->d_group_tmpl.p, e->group_tmpl.data(), e->group_tmpl.size() * 4, hipMemcpyHostToDevice));
-  e->g_chunk_next.ensure(1);
+  e->g_out_next.ensure(1);
   e->g_nrec.ensure(1);
 }
 
@@ -1199,14 +1200,11 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   for (int a = 0; a < B.n_attr; ++a) ev_bytes += B.width[a];
   if (e->gsets.empty()) return;
   const int64_t n = B.n;
-  if (e->g_chunks == 0) {
-    const int64_t words = std::max<int64_t>(1 << 22, n * 64);
-    e->g_chunks = words / e->g_chunk_words;
-  }
-  e->g_out.ensure((size_t)e->g_chunks * e->g_chunk_words);
+  e->g_out_cap = std::max<int64_t>(e->g_out_cap, std::max<int64_t>(1 << 22, n * 64));
+  e->g_out.ensure((size_t)e->g_out_cap);
   e->d_err.ensure(4);
   HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
-  HIPCHK(hipMemsetAsync(e->g_chunk_next.p, 0, 4, e->stream));
+  HIPCHK(hipMemsetAsync(e->g_out_next.p, 0, 8, e->stream));
   HIPCHK(hipMemsetAsync(e->g_nrec.p, 0, 8, e->stream));
   const bool write = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) == 0;
   HIPCHK(hipEventRecord(e->ev0, e->stream));
@@ -1223,9 +1221,8 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     L.B32 = e->gB32;
     L.B64 = e->gB64;
     L.out = e->g_out.p;
-    L.n_chunks = e->g_chunks;
-    L.chunk_words = e->g_chunk_words;
-    L.chunk_next = e->g_chunk_next.p;
+    L.out_cap = e->g_out_cap;
+    L.out_next = e->g_out_next.p;
     L.err = e->d_err.p;
     L.rec_count = e->g_nrec.p;
     L.write_records = write;
@@ -1238,8 +1235,46 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
       if (!reads) continue;
       L.a32 = gs.a32.p;
       L.a64 = gs.a64.p;
-      L.n_items = gs.n_groups;
+      // event chunks when every group's shape has a bounded look-back (kg::seq_lookback): chunk
+      // c > 0 rebuilds its instances from a few replayed events, so one set fills the chip
+      int look = 0;
+      for (int g = 0; g < gs.n_groups && look >= 0; ++g) {
+        const kg::GQuery& t = e->gq[e->group_tmpl[gs.group_base + g]];
+        if (t.recv_n[stream] == 0) continue;
+        const int lb = kg::seq_lookback(t);
+        look = lb < 0 ? -1 : std::max(look, lb);
+      }
+      int64_t C = 1, clen = n;
+      if (look >= 0 && n > 0) {
+        int64_t minlen = std::max<int64_t>(256, 8 * look);
+        if (const char* v = getenv("SDH_GEN_CHUNK_LEN")) minlen = std::max<int64_t>(std::max(1, look), atoll(v));
+        const int64_t target = std::max<int64_t>(1, 8192 / gs.n_groups);
+        C = std::max<int64_t>(1, std::min<int64_t>((n + minlen - 1) / minlen, target));
+        clen = (n + C - 1) / C;
+        C = (n + clen - 1) / clen;
+      }
+      L.n_items = (int32_t)(C * gs.n_groups);
+      L.ev_chunks = (int32_t)C;
+      L.chunk_len = clen;
+      const size_t blk32 = (size_t)e->gB32 * 64, blk64 = (size_t)e->gB64 * 64;
+      if (C > 1) {
+        gs.s32.ensure(blk32 * gs.n_groups * (C - 1));
+        gs.s64.ensure(blk64 * gs.n_groups * (C - 1));
+        L.s32 = gs.s32.p;
+        L.s64 = gs.s64.p;
+      }
       HIPCHK(sdh_launch_gen(&L, e->stream));
+      e->stats.last_gen_items += L.n_items;
+      if (C > 1) {  // the last chunk's instances are the set's state after this batch
+        for (int g = 0; g < gs.n_groups; ++g) {
+          if (e->gq[e->group_tmpl[gs.group_base + g]].recv_n[stream] == 0) continue;
+          const size_t sb = (size_t)(C - 2) * gs.n_groups + g;
+          HIPCHK(hipMemcpyAsync(gs.a32.p + g * blk32, gs.s32.p + sb * blk32, blk32 * 4, hipMemcpyDeviceToDevice,
+                                e->stream));
+          HIPCHK(hipMemcpyAsync(gs.a64.p + g * blk64, gs.s64.p + sb * blk64, blk64 * 8, hipMemcpyDeviceToDevice,
+                                e->stream));
+        }
+      }
       any = true;
       bytes += (double)n * ev_bytes * gs.n_groups;  // every group streams the batch once
       continue;
@@ -1281,6 +1316,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     L.ev_idx = e->r_idx_s.p;
     L.n_items = hv[1] * gs.n_groups;
     HIPCHK(sdh_launch_gen(&L, e->stream));
+    e->stats.last_gen_items += L.n_items;
     any = true;
     // routing (key column read, key/kid/idx written and sorted) + every group streaming its keys' events
     bytes += (double)n * (8 + 8 + 4 + 4 + 2 * (4 + 4) + 3 * 4) + (double)n * ev_bytes * gs.n_groups;
@@ -1300,35 +1336,32 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
                                            "(raise gen_pool_states / gen_pool_nodes / gen_list_cap)");
   unsigned long long nrec = 0;
   if (any) HIPCHK(hipMemcpy(&nrec, e->g_nrec.p, 8, hipMemcpyDeviceToHost));
+  if (errs[2]) {
+    e->g_out_cap *= 4;  // the next push gets a larger output buffer
+    throw Error(SDH_E_CAPACITY, "K_gen match output buffer overflow (matches of this push were lost)");
+  }
   if (write && any) gen_collect_device(e);
   e->g_dev_matches = write ? 0 : (int64_t)nrec;
   *bytes_out += (double)nrec * 32.0;  // one (query, ts, seqs) record per match, as for K_ratchet
-  if (errs[2]) {
-    e->g_chunks *= 4;  // the next push gets a larger output buffer
-    throw Error(SDH_E_CAPACITY, "K_gen match output buffer overflow (matches of this push were lost)");
-  }
   e->stats.matches += (int64_t)nrec;
 }
 
 // copy the used output chunks back and append their records to g_host
 int64_t gen_collect_device(sdh_engine* e) {
-  int32_t used = 0;
-  HIPCHK(hipMemcpy(&used, e->g_chunk_next.p, 4, hipMemcpyDeviceToHost));
-  used = (int32_t)std::min<int64_t>(used, e->g_chunks);
-  if (used <= 0) return 0;
-  std::vector<int64_t> buf((size_t)used * e->g_chunk_words);
+  unsigned long long used = 0;
+  HIPCHK(hipMemcpy(&used, e->g_out_next.p, 8, hipMemcpyDeviceToHost));
+  used = std::min<unsigned long long>(used, (unsigned long long)e->g_out_cap);
+  if (used == 0) return 0;
+  std::vector<int64_t> buf((size_t)used);
   HIPCHK(hipMemcpy(buf.data(), e->g_out.p, buf.size() * 8, hipMemcpyDeviceToHost));
   int64_t n = 0;
-  for (int c = 0; c < used; ++c) {
-    const int64_t* ch = buf.data() + (size_t)c * e->g_chunk_words;
-    const int64_t fill = ch[0];
-    for (int64_t w = 0; w < fill;) {
-      const int64_t len = ch[1 + w];
-      e->g_host.insert(e->g_host.end(), ch + 1 + w, ch + 1 + w + len);
-      w += len;
-      ++n;
-      ++e->g_host_n;
-    }
+  for (size_t w = 0; w < buf.size();) {
+    const int64_t len = buf[w];
+    if (len < 7 || w + len > buf.size()) throw Error(SDH_E_DEVICE, "corrupt K_gen match record");
+    e->g_host.insert(e->g_host.end(), buf.data() + w, buf.data() + w + len);
+    w += len;
+    ++n;
+    ++e->g_host_n;
   }
   return n;
 }
@@ -1412,6 +1445,7 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   ms += e->r_kernel_ms;
   bytes += e->r_kernel_bytes;
   double gms = 0, gbytes = 0;
+  e->stats.last_gen_items = 0;
   launch_gen(e, stream, B, &gms, &gbytes);
   ms += gms;
   bytes += gbytes;

@@ -796,6 +796,26 @@ inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA) {
   L.n64 = o;
 }
 
+// Events of look-back that rebuild this query's state exactly at any point of a batch, or -1.
+// A SEQUENCE of stream states whose start re-arms itself (`every e1, e2, ...`) resets every pending
+// list before each event (R14, StateStreamRuntime.java:89-92) and drops a partial at its first
+// non-matching event (R6e), so a partial alive before event k was opened at most S-1 events
+// earlier, and the start state always holds one partial whose slots are overwritten before they
+// are read (a fresh seed is equivalent). The state before event k is therefore a function of
+// events k-S+1 .. k-1 alone: an event chunk can start from a fresh instance and replay S-1 events.
+inline int seq_lookback(const GQuery& g) {
+  if (g.type != Q_SEQUENCE) return -1;
+  int st0 = -1, n0 = 0;  // (start_ids lists the start states only for `within` checks)
+  for (int i = 0; i < g.n_states; ++i)
+    if (g.st[i].is_start) st0 = i, ++n0;
+  if (n0 != 1 || g.st[st0].next_every != st0) return -1;
+  for (int i = 0; i < g.n_states; ++i) {  // (a start state never expires: its within-every is inert)
+    const GState& s = g.st[i];
+    if (s.kind != K_STREAM || (s.within_every >= 0 && !s.is_start) || s.callback >= 0) return -1;
+  }
+  return g.n_states - 1;
+}
+
 // Shape of a query: the lowered program with what may differ between lanes of one wave cleared
 // (qid, rank, the `within` value -- its presence stays -- and bytecode constants). Queries with
 // equal shapes share one wave-uniform template on the device.

@@ -41,38 +41,28 @@ __device__ __forceinline__ int64_t raw_word(const StreamBatch& b, int attr, int6
   return (int64_t)((const uint8_t*)p)[e];
 }
 
-// lane-private output: records [len, qid, key, ts, seq, idx, S, (count, seqs...)xS]
+// match output: one flat word buffer; each record is reserved with an atomic add of its length
+// (the backend's atomic optimizer folds a wave's same-address adds into one atomic + a scan)
 struct LaneOut {
   int64_t* out;
-  int64_t n_chunks;
-  int32_t cw;
-  int32_t* next;
-  int64_t chunk = -1;
-  int32_t fill = 0;
+  int64_t cap;
+  unsigned long long* next;
   bool over = false;
-  __device__ void close() {
-    if (chunk >= 0) out[chunk * cw] = fill;
-    chunk = -1;
-  }
+  __device__ void close() {}
   __device__ int64_t* reserve(int words) {
-    if (over) return nullptr;
-    if (words + 1 > cw) { over = true; return nullptr; }
-    if (chunk < 0 || fill + words > cw - 1) {
-      close();
-      const int64_t c = atomicAdd(next, 1);
-      if (c >= n_chunks) { over = true; return nullptr; }
-      chunk = c;
-      fill = 0;
+    const unsigned long long o = atomicAdd(next, (unsigned long long)words);
+    if ((int64_t)(o + words) > cap) {
+      over = true;
+      return nullptr;
     }
-    int64_t* p = out + chunk * cw + 1 + fill;
-    fill += words;
-    return p;
+    return out + o;
   }
 };
 
 }  // namespace
 
-__global__ __launch_bounds__(64) void nfa_gen_kernel(GenLaunch L) {
+template <int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void nfa_gen_kernel(GenLaunch L) {
   const int lane = threadIdx.x;
   const int item = blockIdx.x;
   if (item >= L.n_items) return;
@@ -91,11 +81,27 @@ __global__ __launch_bounds__(64) void nfa_gen_kernel(GenLaunch L) {
   const kg::GQuery* __restrict__ q = L.queries + L.group_tmpl[L.group_base + g];
   const kg::GQuery* __restrict__ ql = L.queries + qi;
   if (q->recv_n[L.b.stream] == 0) return;  // this query does not read the stream
-  const int64_t block = L.block_base + (int64_t)kid * L.groups + g;
+  int64_t block = L.block_base + (int64_t)kid * L.groups + g;
+  int32_t* a32 = L.a32;
+  int64_t* a64 = L.a64;
+  int64_t w0 = e0;  // first event replayed (w0 < e0: look-back, nothing emitted)
+  if (L.ev_chunks > 1) {
+    e0 = (int64_t)seg * L.chunk_len;
+    e1 = e0 + L.chunk_len < L.b.n ? e0 + L.chunk_len : L.b.n;
+    w0 = e0;
+    if (seg > 0) {  // fresh instance in scratch, rebuilt from the look-back window
+      block = (int64_t)(seg - 1) * L.groups + g;
+      a32 = L.s32;
+      a64 = L.s64;
+      w0 = e0 - (q->n_states - 1);
+      for (int w = 0; w < q->lay.n32; ++w) a32[(block * L.B32 + w) * 64 + lane] = 0;
+      for (int w = 0; w < q->lay.n64; ++w) a64[(block * L.B64 + w) * 64 + lane] = 0;
+    }
+  }
   kg::Ctx c;
   c.bind(q, ql);
-  c.w32 = L.a32 + block * L.B32 * 64 + lane;
-  c.w64 = L.a64 + block * L.B64 * 64 + lane;
+  c.w32 = a32 + block * L.B32 * 64 + lane;
+  c.w64 = a64 + block * L.B64 * 64 + lane;
   c.stride = 64;
   c.err = kg::GE_OK;
   c.npin = 0;
@@ -106,11 +112,12 @@ __global__ __launch_bounds__(64) void nfa_gen_kernel(GenLaunch L) {
     c.init_instance();
     c.i32(q->lay.o_init) = 1;
   }
-  LaneOut o{L.out, L.n_chunks, L.chunk_words, L.chunk_next};
+  LaneOut o{L.out, L.out_cap, L.out_next};
   const int S = q->n_states;
   const int ncap = q->n_cap[c.stream];
   unsigned long long nrec = 0;
-  for (int64_t k = e0; k < e1 && c.err == kg::GE_OK; ++k) {
+  for (int64_t k = w0; k < e1 && c.err == kg::GE_OK; ++k) {
+    const bool live = k >= e0;
     const int64_t e = L.ev_idx ? L.ev_idx[k] : k;
     c.seq = L.b.seq_base + e;
     c.ts = L.b.ts[e];
@@ -122,6 +129,7 @@ __global__ __launch_bounds__(64) void nfa_gen_kernel(GenLaunch L) {
     }
     int64_t idx = 0;
     auto emit = [&](const kg::Ctx& cx, int se) {
+      if (!live) return;
       int words = 7;
       for (int i = 0; i < S; ++i) {
         words += 1;
@@ -237,7 +245,9 @@ __global__ void gen_lookup_kernel(int64_t n, const int64_t* key, uint32_t* kid, 
 
 extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
-  hipLaunchKernelGGL(sdh::nfa_gen_kernel, dim3(L->n_items), dim3(64), 0, s, *L);
+  // 4 waves/SIMD (128 VGPRs, a few spills) beat the unconstrained 152-VGPR build (3 waves) by 11 %
+  // on C3; 6 and 8 spill too much
+  hipLaunchKernelGGL(sdh::nfa_gen_kernel<4>, dim3(L->n_items), dim3(64), 0, s, *L);
   return hipGetLastError();
 }
 

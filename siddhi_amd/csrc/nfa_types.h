@@ -226,15 +226,20 @@ struct GenLaunch {
   int32_t* a32;
   int64_t* a64;
   int32_t B32, B64;           // arena words per lane and block
-  int64_t* out;               // chunks of chunk_words int64: [used, records...]
-  int64_t n_chunks;
-  int32_t chunk_words;
+  int64_t* out;               // flat record words: [len, qid, key, ts, seq, idx, S, (count, seqs...)xS]...
+  int64_t out_cap;            // words
+  unsigned long long* out_next;  // words used (atomic; may run past out_cap on overflow)
   int32_t n_items;
-  int32_t* chunk_next;
   int32_t* err;               // [0] instance capacity, [1] reference would throw, [2] output overflow
   unsigned long long* rec_count;  // matches emitted (records), counted even when not written
   int32_t write_records;      // 0: count only (device-resident benchmarking mode)
-  int32_t pad;
+  // event chunks of an unpartitioned set (kg::seq_lookback): item = chunk * groups + g; chunk 0
+  // continues the persistent arena, chunk c > 0 starts a fresh instance in scratch block
+  // (c-1) * groups + g and replays the template's look-back events before emitting
+  int32_t ev_chunks;          // 1: unchunked
+  int64_t chunk_len;
+  int32_t* s32;               // scratch arenas of chunks 1 .. ev_chunks-1
+  int64_t* s64;
 };
 
 }  // namespace sdh

@@ -11,6 +11,11 @@ C1: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 10 s
 C2: P patterns  every e1=StockStream[price > T_p] -> e2=StockStream[price > e1.price] within W_p
     T_p = 20 + (p % 750) / 10.0 (a DOUBLE literal -> Float x Double compare),
     W_p in {1, 10, 60} sec picked by splitmix64(7 ^ p) % 3.
+C4: fraud-rule sequences (strict contiguity, R14) over the Txn stream (same counter-based
+    generator: amount_i = (float)(h_1 % 100000) / 100.0f in [0, 1000), risk_i = h_2 % 100,
+    account_i = h_3 % K):
+    every e1=Txn[amount > A_p], e2=Txn[amount > e1.amount * M_p], e3=Txn[amount > e2.amount and
+    risk > R_p] within 1 min.
 """
 from __future__ import annotations
 
@@ -109,3 +114,38 @@ def c3_app(n_patterns: int, first: int = 0) -> str:
     `partition with (symbol)` (keys = the stream's symbols)."""
     qs = " ".join(c3_query(p) for p in range(first, first + n_patterns))
     return f"{STOCK_STREAM} partition with (symbol of StockStream) begin {qs} end;"
+
+
+TXN_STREAM = "define stream Txn (account string, amount float, risk int);"
+
+
+def txn_events(start: int, n: int, n_accounts: int = 100_000, seed: int = EVENT_SEED):
+    """Events [start, start+n) of the seeded Txn stream: (ts int64, account int32 dictionary id,
+    amount float32, risk int32)."""
+    i = np.arange(start, start + n, dtype=np.uint64)
+    s = np.uint64(seed)
+    h1 = splitmix64_np(s ^ (i * np.uint64(4) + np.uint64(1)))
+    h2 = splitmix64_np(s ^ (i * np.uint64(4) + np.uint64(2)))
+    h3 = splitmix64_np(s ^ (i * np.uint64(4) + np.uint64(3)))
+    ts = (np.int64(TS0) + i.astype(np.int64)).astype(np.int64)
+    amount = (h1 % np.uint64(100000)).astype(np.float32) / np.float32(100.0)
+    risk = (h2 % np.uint64(100)).astype(np.int32)
+    account = (h3 % np.uint64(n_accounts)).astype(np.int32)
+    return ts, account, amount.astype(np.float32), risk
+
+
+def c4_query(p: int, seed: int = PATTERN_SEED) -> str:
+    """Fraud rule p of the C4 family: a 3-event strict-contiguity sequence."""
+    h = splitmix64(seed ^ (p + 2000))
+    a = 100 + p % 800
+    m = ("1.05", "1.1", "1.2", "1.5")[h % 4]
+    r = (h >> 8) % 90
+    return (f"@info(name='f{p}') from every e1=Txn[amount > {a}], e2=Txn[amount > e1.amount * {m}], "
+            f"e3=Txn[amount > e2.amount and risk > {r}] within 1 min "
+            f"select e1.account as acct, e1.amount as a1, e3.amount as a3 insert into Alerts;")
+
+
+def c4_app(n_patterns: int, first: int = 0) -> str:
+    """C4 (BASELINE.json configs[3]): fraud-rule sequences; a shard holds patterns
+    first .. first+n_patterns-1 (pattern-set sharding across GPUs)."""
+    return " ".join([TXN_STREAM] + [c4_query(p) for p in range(first, first + n_patterns)])

@@ -90,3 +90,21 @@ def random_events(seed, n=300, keys=3):
             row[int(rng.integers(1, 4))] = None
         ev.append(("A" if rng.random() < 0.55 else "B", row, t))
     return ev
+
+
+def random_seq_app(seed):
+    """Unpartitioned every-start sequences of 2-4 stream states over A and B (cross-references,
+    arithmetic, strings, nulls; some with `within`)."""
+    rng = random.Random(seed)
+    qs = [STREAMS]
+    for qn in range(6):
+        n = rng.randint(2, 4)
+        parts, al = [], []
+        for i in range(n):
+            st = rng.choice("AB") if seed % 2 else "A"
+            parts.append(f"e{i}={st}[{_pred(rng, al, st)}]")
+            al.append(f"e{i}")
+        parts[0] = "every " + parts[0]
+        w = f" within {rng.choice([3, 10, 40])} milliseconds" if rng.random() < 0.5 else ""
+        qs.append(f"@info(name='s{qn}') from {', '.join(parts)}{w} select e0.v as a, e{n - 1}.v as b insert into O;")
+    return " ".join(qs)

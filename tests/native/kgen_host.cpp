@@ -38,6 +38,8 @@ struct Host {
   std::vector<std::map<int64_t, std::vector<std::unique_ptr<Inst>>>> part;
   std::vector<Rec> out;
   std::string err;
+  int64_t chunk_len = 0;  // >0: unpartitioned instances with a bounded look-back run event chunks
+                          // like the device (kg::seq_lookback; nfa_gen.hip)
 };
 
 Inst* make_inst(Host* h, int qi, int64_t key) {
@@ -50,7 +52,8 @@ Inst* make_inst(Host* h, int qi, int64_t key) {
 }
 
 // run one event through one instance (what one lane does for one event)
-void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* vals, const uint8_t* nulls) {
+void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* vals, const uint8_t* nulls,
+         bool live = true) {
   const GQuery& q = h->gq[in->qi];
   Ctx c{};
   c.bind(&q, &q);
@@ -78,6 +81,7 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
   }
   int64_t idx = 0;
   auto emit = [&](const Ctx& cx, int se) {
+    if (!live) return;  // look-back replay of an event chunk
     Rec r;
     r.seq = seq;
     r.rank = h->rank[(size_t)in->qi * h->P.stream_types.size() + stream];
@@ -128,10 +132,30 @@ int kgh_send(void* hp, int stream, int64_t n, int64_t seq0, const int64_t* ts, c
   try {
     const size_t na = h->P.stream_types[stream].size();
     // every instance processes the whole batch (the device order), then matches are sorted
-    for (auto& in : h->top)
-      if (in)
+    for (auto& in : h->top) {
+      if (!in) continue;
+      const int look = seq_lookback(h->gq[in->qi]);
+      const int64_t clen = h->chunk_len > 0 ? std::max<int64_t>(h->chunk_len, look) : n;
+      if (look < 0 || h->gq[in->qi].recv_n[stream] == 0 || clen >= n) {
         for (int64_t k = 0; k < n; ++k)
           run(h, in.get(), stream, seq0 + k, ts[k], vals + k * na, nulls ? nulls + k * na : nullptr);
+        continue;
+      }
+      // chunk 0 continues the instance; chunk c > 0 starts a fresh one and replays `look` events;
+      // the last chunk's instance carries on (the device copies its arena back)
+      for (int64_t e0 = 0; e0 < n; e0 += clen) {
+        std::unique_ptr<Inst> fresh;
+        Inst* cur = in.get();
+        if (e0 > 0) {
+          fresh.reset(make_inst(h, in->qi, in->key));
+          cur = fresh.get();
+        }
+        const int64_t e1 = std::min(n, e0 + clen);
+        for (int64_t k = e0 > 0 ? e0 - look : 0; k < e1; ++k)
+          run(h, cur, stream, seq0 + k, ts[k], vals + k * na, nulls ? nulls + k * na : nullptr, k >= e0);
+        if (e1 == n && fresh) in = std::move(fresh);
+      }
+    }
     for (size_t pi = 0; pi < h->P.parts.size(); ++pi) {
       const LPart& pd = h->P.parts[pi];
       for (const auto& key : pd.keys) {
@@ -189,6 +213,7 @@ int kgh_get_matches(void* hp, int64_t* query, int64_t* key, int64_t* ts, int64_t
   return 0;
 }
 void kgh_clear(void* hp) { ((Host*)hp)->out.clear(); }
+void kgh_set_chunk(void* hp, int64_t len) { ((Host*)hp)->chunk_len = len; }
 const char* kgh_error(void* hp) { return ((Host*)hp)->err.c_str(); }
 void kgh_destroy(void* hp) { delete (Host*)hp; }
 

@@ -4,7 +4,7 @@ partitions, arithmetic, nulls), batched pushes through the device partition rout
 import numpy as np
 import pytest
 
-from fuzz_apps import random_app, random_events
+from fuzz_apps import random_app, random_events, random_seq_app
 from harness import App, OracleError
 from siddhi_amd.ql import SiddhiAppCreationException, SiddhiParserException
 from test_oracle_reference_kat import KAT, OUT_OF_SCOPE, check_rows, run_fixture
@@ -192,3 +192,54 @@ def test_gen_snapshot_restore_count_and_partition():
         o.send(stream, [row], [t])
     assert a.matches == o.matches
     assert b.matches == o.matches and len(b.matches) > 20
+
+
+# ---- event-chunked K_gen (kg::seq_lookback): every-start stream-state sequences ----
+
+def _chunked_pair(src, chunk_len, monkeypatch):
+    monkeypatch.setenv("SDH_GEN_CHUNK_LEN", str(chunk_len))
+    return App(src), hip_app(src)
+
+
+@pytest.mark.parametrize("chunk_len", [1, 2, 3, 7])
+@pytest.mark.parametrize("seed", range(8))
+def test_chunked_random_sequences(seed, chunk_len, monkeypatch):
+    src = random_seq_app(seed)
+    o, g = _chunked_pair(src, chunk_len, monkeypatch)
+    # runs of up to 60 same-stream events (one push each): chunks inside, state across pushes
+    ev = [("AB"[(i // 60) % 2 if seed % 2 else 0], r, t) for i, (_, r, t) in enumerate(random_events(100 + seed, n=400))]
+    i, items = 0, 0
+    while i < len(ev):  # same-stream runs as one push: chunks inside, persisted state across pushes
+        j = i
+        while j < len(ev) and ev[j][0] == ev[i][0] and j - i < 90:
+            j += 1
+        rows = [r for _, r, _ in ev[i:j]]
+        ts = [t for _, _, t in ev[i:j]]
+        o.send(ev[i][0], rows, ts)
+        g.send(ev[i][0], rows, ts)
+        items = max(items, g.engine.stats().last_gen_items)
+        i = j
+    assert g.matches == o.matches
+    assert items > 6  # event chunks engaged (6 queries = at most 6 groups unchunked)
+
+
+@pytest.mark.parametrize("chunk_len", [2, 5, 256])
+def test_chunked_c4_family(chunk_len, monkeypatch):
+    """C4 fraud-rule sequences (float x double arithmetic compares) over 3 pushes of the Txn stream."""
+    from siddhi_amd.workloads import c4_app, txn_events
+    src = c4_app(96)
+    o, g = _chunked_pair(src, chunk_len, monkeypatch)
+    nq = len(o.ir.queries)
+    n = 0
+    for lo, hi in ((0, 3000), (3000, 3001), (3001, 9000)):
+        ts, acc, amt, risk = txn_events(lo, hi - lo, n_accounts=500)
+        vals = np.stack([acc.astype(np.int64), amt.view(np.uint32).astype(np.int64), risk.astype(np.int64)], 1)
+        o.engine.send(0, ts, vals, None)
+        g.engine.push_columns(0, ts, [acc, amt.view(np.uint32), risk])
+        if hi - lo > 2 * chunk_len:
+            assert g.engine.stats().last_gen_items > 2  # 96 same-shape queries = 2 groups, chunked
+        om = o.engine.take_matches(lambda q: 3)
+        gm = g.engine.take_matches(lambda q: 3)
+        assert gm == om
+        n += len(om)
+    assert nq == 96 and n > 5000

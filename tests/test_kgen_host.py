@@ -53,3 +53,41 @@ def test_kgen_host_fuzz(seed):
         pytest.skip("instance pools exceeded (loud SDH_E_CAPACITY on the device)")
     o, g = r
     assert g.matches == o.matches
+
+
+@pytest.mark.parametrize("chunk_len", [1, 2, 3, 7])
+@pytest.mark.parametrize("seed", range(12))
+def test_kgen_host_event_chunks(seed, chunk_len):
+    """The look-back rule behind K_gen's event chunks (kg::seq_lookback): every-start stream-state
+    sequences rebuilt from a fresh instance and S-1 replayed events give the oracle's matches."""
+    from fuzz_apps import random_events, random_seq_app
+    src = random_seq_app(seed)
+    o = App(src)
+    g = App(src, engine_factory=lambda blob: KGenHostEngine(blob, chunk_len=chunk_len))
+    # runs of up to 60 same-stream events (one push each): chunks inside, state across pushes
+    ev = [("AB"[(i // 60) % 2 if seed % 2 else 0], r, t) for i, (_, r, t) in enumerate(random_events(100 + seed, n=400))]
+    i = 0
+    while i < len(ev):
+        j = i
+        while j < len(ev) and ev[j][0] == ev[i][0] and j - i < 90:
+            j += 1
+        rows = [r for _, r, _ in ev[i:j]]
+        ts = [t for _, _, t in ev[i:j]]
+        o.send(ev[i][0], rows, ts)
+        g.send(ev[i][0], rows, ts)
+        i = j
+    assert g.matches == o.matches
+
+
+def test_kgen_host_event_chunks_c4():
+    import numpy as np
+    from siddhi_amd.workloads import c4_app, txn_events
+    src = c4_app(40)
+    o = App(src)
+    g = App(src, engine_factory=lambda blob: KGenHostEngine(blob, R=8, N=32, LC=8, chunk_len=3))
+    for lo, hi in ((0, 2000), (2000, 2001), (2001, 5000)):
+        ts, acc, amt, risk = txn_events(lo, hi - lo, n_accounts=500)
+        vals = np.stack([acc.astype(np.int64), amt.view(np.uint32).astype(np.int64), risk.astype(np.int64)], 1)
+        o.engine.send(0, ts, vals, None)
+        g.engine.send(0, ts, vals, None)
+        assert g.engine.take_matches(lambda q: 3) == o.engine.take_matches(lambda q: 3)
