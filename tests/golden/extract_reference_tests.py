@@ -28,6 +28,7 @@ FILES = [
     "sequence/SequenceTestCase.java",
     "partition/PatternPartitionTestCase.java",
     "partition/SequencePartitionTestCase.java",
+    "IsNullTestCase.java",
 ]
 TS0 = 1_500_000_000_000
 
