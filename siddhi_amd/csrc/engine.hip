@@ -23,6 +23,7 @@
 #include "nfa_types.h"
 
 extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s);
+extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, int32_t new_tail_len, int64_t* tail, hipStream_t s);
 extern "C" hipError_t sdh_route_partition(const sdh::StreamBatch* B, int attr, int type, unsigned long long* tkey,
                                           int32_t* tid, int64_t table_mask, int32_t* n_keys, int64_t* key_of_id,
                                           int64_t key_cap, int64_t* key, uint32_t* kid, uint32_t* kid_sorted,
@@ -528,6 +529,10 @@ struct sdh_engine {
   DevBuf<int32_t> d_lane_q;
   std::vector<int32_t> group_tmpl;   // [group] shape template (a member query)
   DevBuf<int32_t> d_group_tmpl;
+  std::vector<int32_t> group_seq;    // [group] window length S when the group runs on K_seq, else 0
+  std::vector<DevBuf<int32_t>> d_glists;  // [stream] unpartitioned groups: K_seq rows, then K_gen groups
+  std::vector<DevBuf<int64_t>> seq_tail;  // [stream] last SEQ_TMAX events (K_seq windows)
+  std::vector<int32_t> seq_tail_len;
   int gB32 = 1, gB64 = 1;
   struct GenSet {
     int partition = -1;              // -1: the unpartitioned K_gen queries
@@ -1112,7 +1117,9 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
     gs->n_groups = 0;
     for (const auto& b : shapes) {
       const int ng = (int)((b.second.size() + 63) / 64);
+      const int S = (partition < 0 && !(e->cfg.flags & SDH_FLAG_FORCE_GEN)) ? kg::seq_window(e->gq[b.second[0]]) : -1;
       for (int g = 0; g < ng; ++g) {
+        e->group_seq.push_back(S > 0 ? S : 0);
         e->group_tmpl.push_back(b.second[0]);
         for (int l = 0; l < 64; ++l) {
           const size_t k = (size_t)g * 64 + l;
@@ -1159,6 +1166,13 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   HIPCHK(hipMemcpy(e->d_gq.p, e->gq.data(), e->gq.size() * sizeof(kg::GQuery), hipMemcpyHostToDevice));
   e->d_lane_q.ensure(e->lane_q.size());
   HIPCHK(hipMemcpy(e->d_lane_q.p, e->lane_q.data(), e->lane_q.size() * 4, hipMemcpyHostToDevice));
+  e->seq_tail.resize(e->prog.stream_types.size());
+  e->seq_tail_len.assign(e->prog.stream_types.size(), 0);
+  for (auto& t : e->seq_tail) {
+    t.ensure(SEQ_TMAX * SEQ_TW);
+    HIPCHK(hipMemset(t.p, 0, SEQ_TMAX * SEQ_TW * 8));
+  }
+  e->d_glists.resize(e->prog.stream_types.size());
   e->d_group_tmpl.ensure(e->group_tmpl.size());
   HIPCHK(hipMemcpy(e->d_group_tmpl.p, e->group_tmpl.data(), e->group_tmpl.size() * 4, hipMemcpyHostToDevice));
   e->g_out_next.ensure(1);
@@ -1227,38 +1241,84 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     L.rec_count = e->g_nrec.p;
     L.write_records = write;
     if (gs.partition < 0) {
-      bool reads = false;
-      for (int g = 0; g < gs.n_groups * 64; ++g) {
-        const int gi = e->lane_q[(size_t)gs.group_base * 64 + g];
-        reads |= gi >= 0 && e->gq[gi].recv_n[stream] > 0;
+      // groups reading this stream: windowed sequences go to K_seq, the rest to K_gen
+      std::vector<int32_t> seq_rows, gen_groups;
+      int seqS = 1;
+      for (int g = 0; g < gs.n_groups; ++g) {
+        if (e->gq[e->group_tmpl[gs.group_base + g]].recv_n[stream] == 0) continue;
+        if (e->group_seq[gs.group_base + g] > 0) {
+          seq_rows.push_back(gs.group_base + g);
+          seqS = std::max(seqS, e->group_seq[gs.group_base + g]);
+        } else {
+          gen_groups.push_back(g);
+        }
       }
-      if (!reads) continue;
+      if (seq_rows.empty() && gen_groups.empty()) continue;
+      // the lists depend on the stream only: uploaded once, before any kernel reads them
+      auto& gl = e->d_glists[stream];
+      if (!gl.p) {
+        gl.ensure(std::max<size_t>(1, seq_rows.size() + gen_groups.size()));
+        std::vector<int32_t> both(seq_rows);
+        both.insert(both.end(), gen_groups.begin(), gen_groups.end());
+        if (!both.empty()) HIPCHK(hipMemcpy(gl.p, both.data(), both.size() * 4, hipMemcpyHostToDevice));
+      }
+      if (!seq_rows.empty()) {
+        sdh::SeqLaunch Q{};
+        Q.queries = e->d_gq.p;
+        Q.lane_q = e->d_lane_q.p;
+        Q.group_tmpl = e->d_group_tmpl.p;
+        Q.glist = gl.p;
+        Q.n_glist = (int32_t)seq_rows.size();
+        Q.b = B;
+        Q.tail = e->seq_tail[stream].p;
+        Q.tail_len = e->seq_tail_len[stream];
+        Q.write_records = write;
+        Q.out = e->g_out.p;
+        Q.out_cap = e->g_out_cap;
+        Q.out_next = e->g_out_next.p;
+        Q.rec_count = e->g_nrec.p;
+        Q.err = e->d_err.p;
+        const int64_t starts = n + Q.tail_len;
+        const int64_t target = std::max<int64_t>(1, 8192 / (int64_t)seq_rows.size());
+        int64_t clen = std::max<int64_t>(256, (starts + target - 1) / target);
+        clen = (clen + 63) / 64 * 64;  // whole LDS tiles
+        Q.chunk_len = clen;
+        Q.n_chunks = (int32_t)((starts + clen - 1) / clen);
+        const int32_t new_len = (int32_t)std::min<int64_t>(SEQ_TMAX, Q.tail_len + n);
+        HIPCHK(sdh_launch_seq(&Q, new_len, e->seq_tail[stream].p, e->stream));
+        e->seq_tail_len[stream] = new_len;
+        e->stats.last_seq_items += (int64_t)Q.n_glist * Q.n_chunks;
+        any = true;
+        bytes += (double)n * ev_bytes * seq_rows.size();  // every group stages the batch once
+      }
+      if (gen_groups.empty()) continue;
+      L.glist = gl.p + seq_rows.size();
+      L.n_glist = (int32_t)gen_groups.size();
       L.a32 = gs.a32.p;
       L.a64 = gs.a64.p;
       // event chunks when every group's shape has a bounded look-back (kg::seq_lookback): chunk
       // c > 0 rebuilds its instances from a few replayed events, so one set fills the chip
       int look = 0;
-      for (int g = 0; g < gs.n_groups && look >= 0; ++g) {
-        const kg::GQuery& t = e->gq[e->group_tmpl[gs.group_base + g]];
-        if (t.recv_n[stream] == 0) continue;
-        const int lb = kg::seq_lookback(t);
+      for (int g : gen_groups) {
+        const int lb = kg::seq_lookback(e->gq[e->group_tmpl[gs.group_base + g]]);
         look = lb < 0 ? -1 : std::max(look, lb);
+        if (look < 0) break;
       }
       int64_t C = 1, clen = n;
       if (look >= 0 && n > 0) {
         int64_t minlen = std::max<int64_t>(256, 8 * look);
         if (const char* v = getenv("SDH_GEN_CHUNK_LEN")) minlen = std::max<int64_t>(std::max(1, look), atoll(v));
-        const int64_t target = std::max<int64_t>(1, 8192 / gs.n_groups);
+        const int64_t target = std::max<int64_t>(1, 8192 / (int64_t)gen_groups.size());
         C = std::max<int64_t>(1, std::min<int64_t>((n + minlen - 1) / minlen, target));
         clen = (n + C - 1) / C;
         C = (n + clen - 1) / clen;
       }
-      L.n_items = (int32_t)(C * gs.n_groups);
+      L.n_items = (int32_t)(C * gen_groups.size());
       L.ev_chunks = (int32_t)C;
       L.chunk_len = clen;
       const size_t blk32 = (size_t)e->gB32 * 64, blk64 = (size_t)e->gB64 * 64;
       if (C > 1) {
-        gs.s32.ensure(blk32 * gs.n_groups * (C - 1));
+        gs.s32.ensure(blk32 * gs.n_groups * (C - 1));  // (indexed by set-relative group)
         gs.s64.ensure(blk64 * gs.n_groups * (C - 1));
         L.s32 = gs.s32.p;
         L.s64 = gs.s64.p;
@@ -1266,8 +1326,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
       HIPCHK(sdh_launch_gen(&L, e->stream));
       e->stats.last_gen_items += L.n_items;
       if (C > 1) {  // the last chunk's instances are the set's state after this batch
-        for (int g = 0; g < gs.n_groups; ++g) {
-          if (e->gq[e->group_tmpl[gs.group_base + g]].recv_n[stream] == 0) continue;
+        for (int g : gen_groups) {
           const size_t sb = (size_t)(C - 2) * gs.n_groups + g;
           HIPCHK(hipMemcpyAsync(gs.a32.p + g * blk32, gs.s32.p + sb * blk32, blk32 * 4, hipMemcpyDeviceToDevice,
                                 e->stream));
@@ -1276,7 +1335,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
         }
       }
       any = true;
-      bytes += (double)n * ev_bytes * gs.n_groups;  // every group streams the batch once
+      bytes += (double)n * ev_bytes * gen_groups.size();  // every group streams the batch once
       continue;
     }
     // partitioned: the partition's key attribute of this stream
@@ -1446,6 +1505,7 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   bytes += e->r_kernel_bytes;
   double gms = 0, gbytes = 0;
   e->stats.last_gen_items = 0;
+  e->stats.last_seq_items = 0;
   launch_gen(e, stream, B, &gms, &gbytes);
   ms += gms;
   bytes += gbytes;
@@ -1748,6 +1808,12 @@ int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
         put_dev(gs.key_of_id.p, (size_t)gs.max_keys * 8);
       }
     }
+    // K_seq: each stream's tail (the only state its windowed sequences carry between pushes)
+    w.push_back((int64_t)e->seq_tail.size());
+    for (size_t st = 0; st < e->seq_tail.size(); ++st) {
+      w.push_back(e->seq_tail_len[st]);
+      put_dev(e->seq_tail[st].p, SEQ_TMAX * SEQ_TW * 8);
+    }
     *len = w.size() * 8;
     *blob = malloc(*len);
     memcpy(*blob, w.data(), *len);
@@ -1826,6 +1892,13 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
         get_dev(gs.n_keys.p, 4);
         get_dev(gs.key_of_id.p, (size_t)gs.max_keys * 8);
       }
+    }
+    if ((size_t)nx() != e->seq_tail.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
+    for (size_t st = 0; st < e->seq_tail.size(); ++st) {
+      const int64_t tl = nx();
+      if (tl < 0 || tl > SEQ_TMAX) throw Error(SDH_E_INVALID, "bad snapshot tail length");
+      e->seq_tail_len[st] = (int32_t)tl;
+      get_dev(e->seq_tail[st].p, SEQ_TMAX * SEQ_TW * 8);
     }
     e->backlog.clear();
     e->g_host.clear();

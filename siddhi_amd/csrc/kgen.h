@@ -217,6 +217,71 @@ KG_FN Val arith(int op, int res, const Val& l, const Val& r) {
 // ------------------------------------------------------------------------------------------
 enum { FL_CHANGED = 1, FL_INIT = 2, FL_SUCCESS = 4, FL_SSRESET = 8, FL_RETURNED = 16, FL_ITER = 32 };
 
+// The predicate bytecode's stack machine (ExpressionExecutor trees: executor/condition/**,
+// executor/math/**, VariableExpressionExecutor.java:45-47). Structure comes from q (wave-uniform on
+// the device), constants from the lane's own query ql. attr(in) resolves OP_ATTR to a typed value,
+// stream_null(in) answers OP_STREAM_IS_NULL -- K_gen over its instance arena, K_seq over the
+// event window of a sequence.
+template <class Attr, class StreamNull>
+KG_FN Val eval_code(const GQuery* q, const GQuery* ql, int b, int e, Attr attr, StreamNull stream_null) {
+  Val st[GSTACK];
+  int sp = 0;
+  for (int pc = b; pc < e; ++pc) {
+    const GInsn& in = q->code[pc];
+    switch (in.op) {
+      case OP_CONST: {  // constants differ within a shape: the lane's own query
+        const int64_t imm = ql->code[pc].imm;
+        Val v{in.res, 0, 0};
+        if (in.res == T_FLOAT) v.bits = (int64_t)(uint32_t)imm;
+        else if (in.res == T_INT) v.bits = (int32_t)imm;
+        else v.bits = imm;
+        st[sp++] = v;
+        break;
+      }
+      case OP_ATTR:
+        st[sp++] = attr(in);
+        break;
+      case OP_STREAM_IS_NULL:
+        st[sp++] = Val{T_BOOL, 0, stream_null(in) ? 1 : 0};
+        break;
+      case OP_IS_NULL: {
+        const Val x = st[--sp];
+        st[sp++] = Val{T_BOOL, 0, x.null ? 1 : 0};
+        break;
+      }
+      case OP_NOT: {  // NotConditionExpressionExecutor: only TRUE -> FALSE
+        const Val x = st[--sp];
+        st[sp++] = Val{T_BOOL, 0, (!x.null && x.bits) ? 0 : 1};
+        break;
+      }
+      case OP_AND:
+      case OP_OR: {
+        const Val r = st[--sp];
+        const Val l = st[--sp];
+        const bool lb = !l.null && l.bits, rb = !r.null && r.bits;
+        st[sp++] = Val{T_BOOL, 0, (in.op == OP_AND ? (lb && rb) : (lb || rb)) ? 1 : 0};
+        break;
+      }
+      case OP_CMP: {  // CompareConditionExpressionExecutor.java:39-43
+        const Val r = st[--sp];
+        const Val l = st[--sp];
+        st[sp++] = Val{T_BOOL, 0, (!l.null && !r.null && typed_compare((int)in.imm, l, r)) ? 1 : 0};
+        break;
+      }
+      case OP_ARITH: {
+        const Val r = st[--sp];
+        const Val l = st[--sp];
+        st[sp++] = arith((int)in.imm, in.res, l, r);
+        break;
+      }
+      default:
+        st[sp++] = Val{T_BOOL, 1, 0};
+    }
+    if (sp >= GSTACK) sp = GSTACK - 1;
+  }
+  return sp == 1 ? st[0] : Val{T_BOOL, 1, 0};
+}
+
 struct Emitter;  // defined by the caller: void emit(const Ctx&, int se)
 
 struct Ctx {
@@ -520,21 +585,9 @@ struct Ctx {
     return e;
   }
   KG_FN Val run_code(int b, int e, int se) const {
-    Val st[GSTACK];
-    int sp = 0;
-    for (int pc = b; pc < e; ++pc) {
-      const GInsn& in = q->code[pc];
-      switch (in.op) {
-        case OP_CONST: {  // constants differ within a shape: the lane's own query
-          const int64_t imm = ql->code[pc].imm;
-          Val v{in.res, 0, 0};
-          if (in.res == T_FLOAT) v.bits = (int64_t)(uint32_t)imm;
-          else if (in.res == T_INT) v.bits = (int32_t)imm;
-          else v.bits = imm;
-          st[sp++] = v;
-          break;
-        }
-        case OP_ATTR: {
+    return eval_code(
+        q, ql, b, e,
+        [&](const GInsn& in) {  // OP_ATTR: the slot's chain element (CURRENT=-1, LAST=-2, ...)
           const int n = chain_at(slot(se, in.a), in.b);
           Val v{in.res, 1, 0};
           if (n >= 0 && !((nd_null(n) >> in.imm) & 1)) {
@@ -542,49 +595,9 @@ struct Ctx {
             const int64_t raw = nd_val(n, (int)in.imm);
             v.bits = in.res == T_INT ? (int64_t)(int32_t)raw : in.res == T_FLOAT ? (int64_t)(uint32_t)raw : raw;
           }
-          st[sp++] = v;
-          break;
-        }
-        case OP_STREAM_IS_NULL: {
-          st[sp++] = Val{T_BOOL, 0, chain_at(slot(se, in.a), in.b) < 0 ? 1 : 0};
-          break;
-        }
-        case OP_IS_NULL: {
-          const Val x = st[--sp];
-          st[sp++] = Val{T_BOOL, 0, x.null ? 1 : 0};
-          break;
-        }
-        case OP_NOT: {  // NotConditionExpressionExecutor: only TRUE -> FALSE
-          const Val x = st[--sp];
-          st[sp++] = Val{T_BOOL, 0, (!x.null && x.bits) ? 0 : 1};
-          break;
-        }
-        case OP_AND:
-        case OP_OR: {
-          const Val r = st[--sp];
-          const Val l = st[--sp];
-          const bool lb = !l.null && l.bits, rb = !r.null && r.bits;
-          st[sp++] = Val{T_BOOL, 0, (in.op == OP_AND ? (lb && rb) : (lb || rb)) ? 1 : 0};
-          break;
-        }
-        case OP_CMP: {  // CompareConditionExpressionExecutor.java:39-43
-          const Val r = st[--sp];
-          const Val l = st[--sp];
-          st[sp++] = Val{T_BOOL, 0, (!l.null && !r.null && typed_compare((int)in.imm, l, r)) ? 1 : 0};
-          break;
-        }
-        case OP_ARITH: {
-          const Val r = st[--sp];
-          const Val l = st[--sp];
-          st[sp++] = arith((int)in.imm, in.res, l, r);
-          break;
-        }
-        default:
-          st[sp++] = Val{T_BOOL, 1, 0};
-      }
-      if (sp >= GSTACK) sp = GSTACK - 1;
-    }
-    return sp == 1 ? st[0] : Val{T_BOOL, 1, 0};
+          return v;
+        },
+        [&](const GInsn& in) { return chain_at(slot(se, in.a), in.b) < 0; });
   }
   KG_FN bool filters_pass(int i, int se) const {  // FilterProcessor.process:55-66
     const GState& s = S(i);
@@ -814,6 +827,55 @@ inline int seq_lookback(const GQuery& g) {
     if (s.kind != K_STREAM || (s.within_every >= 0 && !s.is_start) || s.callback >= 0) return -1;
   }
   return g.n_states - 1;
+}
+
+// K_seq: a look-back sequence whose states all read one stream, chained 0 -> 1 -> ... -> S-1.
+// Then a partial alive at state j before event k was opened at event k-j and its slots are events
+// k-j .. k-1, so a match is a property of a window of S consecutive events alone: starting at s,
+// every state i passes its filters over events s .. s+i, and no step i >= 1 is expired
+// (|ts[s] - ts[s+i]| > within). Returns S, or -1.
+inline int seq_window(const GQuery& g) {
+  if (seq_lookback(g) < 0) return -1;
+  const int st = g.st[0].stream;
+  if (!g.st[0].is_start) return -1;
+  for (int i = 0; i < g.n_states; ++i)
+    if (g.st[i].stream != st || g.st[i].next_pre != (i + 1 < g.n_states ? i + 1 : -1)) return -1;
+  for (int k = 0; k < GMAXSTREAM; ++k)
+    if (k != st && g.recv_n[k] != 0) return -1;
+  return g.n_states;
+}
+
+// One window of a K_seq query: does the sequence started at window event 0 match events 0 .. S-1?
+// Win provides ts(p) and, for event p and captured attribute word j, raw(p, j) / null(p, j). Slots
+// hold one event each, so eK / eK[0] / eK[last] name it and every other index is null
+// (StateEvent.getStreamEvent:138-182 on a one-event chain); state i's filter sees slots 0 .. i.
+template <class Win>
+KG_FN bool seq_match(const GQuery* q, const GQuery* ql, int64_t within, const Win& w) {
+  const int S = q->n_states;
+  for (int i = 0; i < S; ++i) {
+    if (i >= 1 && within >= 0) {  // StreamPreStateProcessor.isExpired:102-113 before the filter
+      const int64_t d = (int64_t)((uint64_t)w.ts(0) - (uint64_t)w.ts(i));
+      const int64_t a = d < 0 ? (int64_t)(0ull - (uint64_t)d) : d;
+      if (a > within) return false;
+    }
+    const GState& st = q->st[i];
+    for (int f = 0; f < st.n_filt; ++f) {
+      const Val v = eval_code(
+          q, ql, st.fb[f], st.fe[f],
+          [&](const GInsn& in) {
+            Val x{in.res, 1, 0};
+            if (in.a <= i && (in.b == 0 || in.b == -1) && !w.null(in.a, (int)in.imm)) {
+              x.null = 0;
+              const int64_t raw = w.raw(in.a, (int)in.imm);
+              x.bits = in.res == T_INT ? (int64_t)(int32_t)raw : in.res == T_FLOAT ? (int64_t)(uint32_t)raw : raw;
+            }
+            return x;
+          },
+          [&](const GInsn& in) { return !(in.a <= i && (in.b == 0 || in.b == -1)); });
+      if (v.null || !v.bits) return false;
+    }
+  }
+  return true;
 }
 
 // Shape of a query: the lowered program with what may differ between lanes of one wave cleared

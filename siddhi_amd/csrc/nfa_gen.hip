@@ -66,7 +66,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   const int lane = threadIdx.x;
   const int item = blockIdx.x;
   if (item >= L.n_items) return;
-  const int seg = item / L.groups, g = item % L.groups;
+  int seg = item / L.groups, g = item % L.groups;
+  if (L.glist) {  // unpartitioned: a subset of the set's groups (K_seq runs the others)
+    seg = item / L.n_glist;
+    g = L.glist[item % L.n_glist];
+  }
   int64_t e0 = 0, e1 = L.b.n;
   uint32_t kid = 0;
   if (L.seg_begin) {
@@ -166,6 +170,125 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   if (o.over) atomicOr(&L.err[2], 1);
 }
 
+
+// ---- K_seq: sequences as windows of consecutive events (kg::seq_window / kg::seq_match) ----
+// A lane is a query; the wave's 64 queries share one shape (template q, scalar loads). Window
+// starts are tiled by 64: the tile's events (64 + S - 1, tail rows first) are staged once in LDS,
+// then every lane tests every start of the tile against its own constants -- all lanes read the
+// same LDS word at a time (a broadcast). No per-query state exists beyond the stream's tail.
+namespace {
+constexpr int SEQ_TILE = 64;
+constexpr int SEQ_ROW = 3 + kg::GMAXNA;  // ts, seq, null bits, raw words
+
+struct LdsWin {
+  const int64_t* base;  // row of window event 0
+  __device__ int64_t ts(int p) const { return base[p * SEQ_ROW]; }
+  __device__ int64_t raw(int p, int j) const { return base[p * SEQ_ROW + 3 + j]; }
+  __device__ bool null(int p, int j) const { return (base[p * SEQ_ROW + 2] >> j) & 1; }
+};
+}  // namespace
+
+__global__ __launch_bounds__(64) void nfa_seq_kernel(SeqLaunch L) {
+  __shared__ int64_t win[(SEQ_TILE + kg::GMAXS) * SEQ_ROW];
+  const int lane = threadIdx.x;
+  const int gi = L.glist[blockIdx.x % L.n_glist];
+  const int chunk = blockIdx.x / L.n_glist;
+  const int qi = L.lane_q[(int64_t)gi * 64 + lane];
+  const kg::GQuery* __restrict__ q = L.queries + L.group_tmpl[gi];
+  const kg::GQuery* __restrict__ ql = L.queries + (qi >= 0 ? qi : L.group_tmpl[gi]);
+  const int S = q->n_states;
+  const int stream = L.b.stream;
+  const int na = q->n_cap[stream];
+  const int64_t within = ql->within;
+  // window index w: tail rows 0 .. tail_len-1, then batch event w - tail_len. Start s is evaluated
+  // by the batch holding its last event s + S - 1.
+  const int64_t W = L.tail_len + L.b.n;
+  const int64_t s_begin = L.tail_len - (S - 1) > 0 ? L.tail_len - (S - 1) : 0;
+  const int64_t s_end = W - S + 1;
+  int64_t lo = s_begin + (int64_t)chunk * L.chunk_len;
+  int64_t hi = lo + L.chunk_len < s_end ? lo + L.chunk_len : s_end;
+  LaneOut o{L.out, L.out_cap, L.out_next};
+  unsigned long long nrec = 0;
+  for (int64_t t0 = lo; t0 < hi; t0 += SEQ_TILE) {
+    const int cnt = hi - t0 < SEQ_TILE ? (int)(hi - t0) : SEQ_TILE;
+    for (int p = lane; p < cnt + S - 1; p += 64) {  // stage window events t0 .. t0+cnt+S-2
+      const int64_t w = t0 + p;
+      int64_t* row = win + p * SEQ_ROW;
+      int64_t nb = 0;
+      if (w < L.tail_len) {
+        const int64_t* tr = L.tail + w * SEQ_TW;
+        row[0] = tr[0];
+        row[1] = tr[1];
+        for (int j = 0; j < na; ++j) {
+          const int a = q->cap_attr[stream][j];
+          row[3 + j] = tr[2 + a];
+          nb |= (tr[2 + MAXATTR + a] != 0 ? 1ll : 0ll) << j;
+        }
+      } else {
+        const int64_t e = w - L.tail_len;
+        row[0] = L.b.ts[e];
+        row[1] = L.b.seq_base + e;
+        for (int j = 0; j < na; ++j) {
+          bool nl;
+          row[3 + j] = raw_word(L.b, q->cap_attr[stream][j], e, nl);
+          nb |= (nl ? 1ll : 0ll) << j;
+        }
+      }
+      row[2] = nb;
+    }
+    __syncthreads();
+    if (qi >= 0) {
+      for (int s = 0; s < cnt; ++s) {
+        const LdsWin wv{win + s * SEQ_ROW};
+        if (!kg::seq_match(q, ql, within, wv)) continue;
+        ++nrec;
+        if (!L.write_records) continue;
+        const int words = 7 + 2 * S;
+        int64_t* r = o.reserve(words);
+        if (!r) continue;
+        r[0] = words;
+        r[1] = ql->qid;
+        r[2] = -1;
+        r[3] = wv.base[(S - 1) * SEQ_ROW];      // ts of the last event
+        r[4] = wv.base[(S - 1) * SEQ_ROW + 1];  // the triggering event's seq
+        r[5] = 0;                               // one match per event per query
+        r[6] = S | (stream << 16);
+        for (int i = 0; i < S; ++i) {
+          r[7 + 2 * i] = 1;
+          r[8 + 2 * i] = wv.base[i * SEQ_ROW + 1];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (nrec) atomicAdd(L.rec_count, nrec);
+  if (o.over) atomicOr(&L.err[2], 1);
+}
+
+// the stream's tail after this batch: the last min(SEQ_TMAX, tail_len + n) events of tail ++ batch
+// (rows move towards 0 only, so increasing order is safe in place)
+__global__ void seq_tail_kernel(StreamBatch b, int64_t* tail, int32_t tail_len, int32_t new_len) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int64_t W = tail_len + b.n;
+  for (int r = 0; r < new_len; ++r) {
+    const int64_t w = W - new_len + r;
+    int64_t* dst = tail + (int64_t)r * SEQ_TW;
+    if (w < tail_len) {
+      const int64_t* src = tail + w * SEQ_TW;
+      for (int k = 0; k < SEQ_TW; ++k) dst[k] = src[k];
+    } else {
+      const int64_t e = w - tail_len;
+      dst[0] = b.ts[e];
+      dst[1] = b.seq_base + e;
+      for (int a = 0; a < MAXATTR; ++a) {
+        bool nl = false;
+        dst[2 + a] = a < b.n_attr ? raw_word(b, a, e, nl) : 0;
+        dst[2 + MAXATTR + a] = nl ? 1 : 0;
+      }
+    }
+  }
+}
+
 // ---- partition routing ----
 __global__ void gen_keys_kernel(StreamBatch b, int attr, int type, int64_t* key, uint32_t* kid) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -248,6 +371,14 @@ extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s) {
   // 4 waves/SIMD (128 VGPRs, a few spills) beat the unconstrained 152-VGPR build (3 waves) by 11 %
   // on C3; 6 and 8 spill too much
   hipLaunchKernelGGL(sdh::nfa_gen_kernel<4>, dim3(L->n_items), dim3(64), 0, s, *L);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, int32_t new_tail_len, int64_t* tail,
+                                     hipStream_t s) {
+  if (L->n_glist > 0 && L->n_chunks > 0)
+    hipLaunchKernelGGL(sdh::nfa_seq_kernel, dim3(L->n_glist * L->n_chunks), dim3(64), 0, s, *L);
+  hipLaunchKernelGGL(sdh::seq_tail_kernel, dim3(1), dim3(64), 0, s, L->b, tail, L->tail_len, new_tail_len);
   return hipGetLastError();
 }
 

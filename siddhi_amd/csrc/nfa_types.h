@@ -236,10 +236,39 @@ struct GenLaunch {
   // event chunks of an unpartitioned set (kg::seq_lookback): item = chunk * groups + g; chunk 0
   // continues the persistent arena, chunk c > 0 starts a fresh instance in scratch block
   // (c-1) * groups + g and replays the template's look-back events before emitting
+  const int32_t* glist;       // unpartitioned: the set-relative groups this launch runs (item % n_glist)
+  int32_t n_glist;
   int32_t ev_chunks;          // 1: unchunked
   int64_t chunk_len;
   int32_t* s32;               // scratch arenas of chunks 1 .. ev_chunks-1
   int64_t* s64;
+};
+
+// ------------------------------------------------------------------------------------------
+// K_seq launch (nfa_gen.hip): every-start single-stream sequences of stream states evaluated as
+// windows of S consecutive events (kg::seq_window); item = (start chunk, group of 64 queries)
+// ------------------------------------------------------------------------------------------
+constexpr int SEQ_TMAX = 7;                   // events a stream's tail carries (GMAXS - 1)
+constexpr int SEQ_TW = 2 + 2 * MAXATTR;       // tail row: ts, seq, raw words, null flags
+
+struct SeqLaunch {
+  const kg::GQuery* queries;
+  const int32_t* lane_q;      // [group][64] query index (-1 = idle lane)
+  const int32_t* group_tmpl;  // [group] shape template
+  const int32_t* glist;       // [n_glist] groups (rows of lane_q) this launch runs
+  int32_t n_glist;
+  int32_t n_chunks;           // start chunks per group
+  int64_t chunk_len;          // window starts per chunk
+  StreamBatch b;
+  const int64_t* tail;        // [SEQ_TMAX][SEQ_TW]: the stream's last events before this batch
+  int32_t tail_len;
+  int32_t write_records;
+  int64_t* out;               // flat K_gen-format records (nfa_gen.hip)
+  int64_t out_cap;
+  unsigned long long* out_next;
+  unsigned long long* rec_count;
+  int32_t* err;               // [2] output overflow
+  int32_t pad;
 };
 
 }  // namespace sdh

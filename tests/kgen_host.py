@@ -29,6 +29,7 @@ def lib():
         L.kgh_get_matches.argtypes = [P, VP, VP, VP, VP, VP]
         L.kgh_clear.argtypes = [P]
         L.kgh_set_chunk.argtypes = [P, I64]
+        L.kgh_set_window.argtypes = [P, ctypes.c_int]
         L.kgh_error.argtypes = [P]
         L.kgh_error.restype = ctypes.c_char_p
         L.kgh_destroy.argtypes = [P]
@@ -37,13 +38,14 @@ def lib():
 
 
 class KGenHostEngine:
-    def __init__(self, blob, R=0, N=0, LC=0, chunk_len=0):
+    def __init__(self, blob, R=0, N=0, LC=0, chunk_len=0, window=False):
         self.lib = lib()
         self._blob = ctypes.create_string_buffer(blob, len(blob))
         self.h = self.lib.kgh_create(self._blob, len(blob), R, N, LC)
         if not self.h:
             raise RuntimeError("K_gen lowering failed")
         self.lib.kgh_set_chunk(self.h, chunk_len)
+        self.lib.kgh_set_window(self.h, int(window))
         self.seq = 0
 
     def send(self, stream, ts, vals, nulls, as_chunk=False):

@@ -40,6 +40,23 @@ struct Host {
   std::string err;
   int64_t chunk_len = 0;  // >0: unpartitioned instances with a bounded look-back run event chunks
                           // like the device (kg::seq_lookback; nfa_gen.hip)
+  bool window = false;    // unpartitioned K_seq-class instances evaluate event windows (kg::seq_match)
+  // last events of each stream (window mode): ts, seq, raw attribute words, null flags
+  struct Ev {
+    int64_t ts, seq;
+    std::vector<int64_t> v;
+    std::vector<uint8_t> nl;
+  };
+  std::map<int, std::vector<Ev>> tail;
+};
+
+struct HostWin {  // kg::seq_match's window over Host::Ev records
+  const std::vector<Host::Ev>* ev;
+  size_t s;
+  const int32_t* cap;
+  int64_t ts(int p) const { return (*ev)[s + p].ts; }
+  int64_t raw(int p, int j) const { return (*ev)[s + p].v[cap[j]]; }
+  bool null(int p, int j) const { return (*ev)[s + p].nl[cap[j]] != 0; }
 };
 
 Inst* make_inst(Host* h, int qi, int64_t key) {
@@ -132,8 +149,41 @@ int kgh_send(void* hp, int stream, int64_t n, int64_t seq0, const int64_t* ts, c
   try {
     const size_t na = h->P.stream_types[stream].size();
     // every instance processes the whole batch (the device order), then matches are sorted
+    std::vector<Host::Ev> win;  // this stream's tail ++ batch (window mode)
+    if (h->window) {
+      win = h->tail[stream];
+      for (int64_t k = 0; k < n; ++k) {
+        Host::Ev e{ts[k], seq0 + k, std::vector<int64_t>(vals + k * na, vals + (k + 1) * na),
+                   std::vector<uint8_t>(na, 0)};
+        if (nulls)
+          for (size_t a = 0; a < na; ++a) e.nl[a] = nulls[k * na + a];
+        win.push_back(e);
+      }
+    }
+    const int64_t t0 = (int64_t)win.size() - n;  // window index of batch event 0
     for (auto& in : h->top) {
       if (!in) continue;
+      const int S = h->window ? seq_window(h->gq[in->qi]) : -1;
+      if (S > 0) {
+        const GQuery& q = h->gq[in->qi];
+        if (q.recv_n[stream] == 0) continue;
+        for (int64_t k = 0; k < n; ++k) {  // the window ending at batch event k
+          const int64_t s = t0 + k - (S - 1);
+          if (s < 0) continue;  // fewer than S events seen so far
+          HostWin w{&win, (size_t)s, q.cap_attr[stream]};
+          if (!seq_match(&q, &q, q.within, w)) continue;
+          Rec r;
+          r.seq = seq0 + k;
+          r.rank = h->rank[(size_t)in->qi * h->P.stream_types.size() + stream];
+          r.idx = 0;
+          r.query = in->qi;
+          r.key = in->key;
+          r.ts = ts[k];
+          for (int i = 0; i < q.n_states; ++i) r.slots.push_back({win[s + i].seq});
+          h->out.push_back(r);
+        }
+        continue;
+      }
       const int look = seq_lookback(h->gq[in->qi]);
       const int64_t clen = h->chunk_len > 0 ? std::max<int64_t>(h->chunk_len, look) : n;
       if (look < 0 || h->gq[in->qi].recv_n[stream] == 0 || clen >= n) {
@@ -176,6 +226,10 @@ int kgh_send(void* hp, int stream, int64_t n, int64_t seq0, const int64_t* ts, c
         }
       }
     }
+    if (h->window) {
+      const size_t keep = std::min<size_t>(win.size(), GMAXS - 1);
+      h->tail[stream].assign(win.end() - keep, win.end());
+    }
     std::stable_sort(h->out.begin(), h->out.end(), [](const Rec& a, const Rec& b) {
       if (a.seq != b.seq) return a.seq < b.seq;
       if (a.rank != b.rank) return a.rank < b.rank;
@@ -214,6 +268,7 @@ int kgh_get_matches(void* hp, int64_t* query, int64_t* key, int64_t* ts, int64_t
 }
 void kgh_clear(void* hp) { ((Host*)hp)->out.clear(); }
 void kgh_set_chunk(void* hp, int64_t len) { ((Host*)hp)->chunk_len = len; }
+void kgh_set_window(void* hp, int on) { ((Host*)hp)->window = on != 0; }
 const char* kgh_error(void* hp) { return ((Host*)hp)->err.c_str(); }
 void kgh_destroy(void* hp) { delete (Host*)hp; }
 

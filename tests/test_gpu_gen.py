@@ -197,8 +197,9 @@ def test_gen_snapshot_restore_count_and_partition():
 # ---- event-chunked K_gen (kg::seq_lookback): every-start stream-state sequences ----
 
 def _chunked_pair(src, chunk_len, monkeypatch):
+    """Oracle + a K_gen-only engine (SDH_FLAG_FORCE_GEN keeps windowed sequences off K_seq)."""
     monkeypatch.setenv("SDH_GEN_CHUNK_LEN", str(chunk_len))
-    return App(src), hip_app(src)
+    return App(src), hip_app(src, flags=SDH_FLAG_FORCE_GEN)
 
 
 @pytest.mark.parametrize("chunk_len", [1, 2, 3, 7])
@@ -243,3 +244,75 @@ def test_chunked_c4_family(chunk_len, monkeypatch):
         assert gm == om
         n += len(om)
     assert nq == 96 and n > 5000
+
+
+# ---- K_seq (kg::seq_window): single-stream every-start sequences as windows of S events ----
+
+def _push_runs(o, g, ev, max_run):
+    i, items = 0, 0
+    while i < len(ev):
+        j = i
+        while j < len(ev) and ev[j][0] == ev[i][0] and j - i < max_run(i):
+            j += 1
+        rows = [r for _, r, _ in ev[i:j]]
+        ts = [t for _, _, t in ev[i:j]]
+        o.send(ev[i][0], rows, ts)
+        g.send(ev[i][0], rows, ts)
+        items = max(items, g.engine.stats().last_seq_items)
+        i = j
+    return items
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_seq_windows_random(seed):
+    """Planned path: even seeds are single-stream every-start sequences (K_seq); odd seeds read
+    two streams and stay on K_gen. Pushes of 1-7 events exercise the carried tail."""
+    src = random_seq_app(seed)
+    o, g = App(src), hip_app(src)
+    ev = [("AB"[(i // 60) % 2 if seed % 2 else 0], r, t) for i, (_, r, t) in
+          enumerate(random_events(200 + seed, n=500))]
+    items = _push_runs(o, g, ev, lambda i: 1 + (i % 7) if i < 250 else 200)
+    assert g.matches == o.matches
+    if seed % 2 == 0:
+        assert items > 0
+
+
+def test_seq_windows_c4_family():
+    from siddhi_amd.workloads import c4_app, txn_events
+    src = c4_app(200)
+    o, g = App(src), hip_app(src)
+    n = 0
+    for lo, hi in ((0, 3000), (3000, 3001), (3001, 3003), (3003, 20000)):
+        ts, acc, amt, risk = txn_events(lo, hi - lo, n_accounts=500)
+        vals = np.stack([acc.astype(np.int64), amt.view(np.uint32).astype(np.int64), risk.astype(np.int64)], 1)
+        o.engine.send(0, ts, vals, None)
+        g.engine.push_columns(0, ts, [acc, amt.view(np.uint32), risk])
+        assert g.engine.stats().last_seq_items > 0 and g.engine.stats().last_gen_items == 0
+        om = o.engine.take_matches(lambda q: 3)
+        assert g.engine.take_matches(lambda q: 3) == om
+        n += len(om)
+    assert n > 50000
+
+
+def test_seq_windows_snapshot_restore():
+    from siddhi_amd.workloads import c4_app, txn_events
+    src = c4_app(64)
+    o, a = App(src), hip_app(src)
+
+    def batch(lo, hi):
+        ts, acc, amt, risk = txn_events(lo, hi - lo, n_accounts=50)
+        vals = np.stack([acc.astype(np.int64), amt.view(np.uint32).astype(np.int64), risk.astype(np.int64)], 1)
+        return ts, vals, [acc, amt.view(np.uint32), risk]
+    ts, vals, cols = batch(0, 1001)
+    o.engine.send(0, ts, vals, None)
+    a.engine.push_columns(0, ts, cols)
+    o.engine.take_matches(lambda q: 3)
+    a.engine.poll()
+    snap = a.engine.snapshot()
+    b = hip_app(src)
+    b.engine.restore(snap)
+    ts, vals, cols = batch(1001, 3000)
+    o.engine.send(0, ts, vals, None)
+    b.engine.push_columns(0, ts, cols)
+    om = o.engine.take_matches(lambda q: 3)
+    assert b.engine.take_matches(lambda q: 3) == om and len(om) > 100

@@ -91,3 +91,44 @@ def test_kgen_host_event_chunks_c4():
         o.engine.send(0, ts, vals, None)
         g.engine.send(0, ts, vals, None)
         assert g.engine.take_matches(lambda q: 3) == o.engine.take_matches(lambda q: 3)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_kgen_host_seq_windows(seed):
+    """The window rule behind K_seq (kg::seq_window / seq_match): a single-stream every-start
+    stream-state sequence matches exactly the windows of S consecutive events whose states all
+    pass in order, tails carried across pushes."""
+    from fuzz_apps import random_events, random_seq_app
+    src = random_seq_app(seed)
+    o = App(src)
+    g = App(src, engine_factory=lambda blob: KGenHostEngine(blob, window=True))
+    ev = [("AB"[(i // 60) % 2 if seed % 2 else 0], r, t) for i, (_, r, t) in enumerate(random_events(200 + seed, n=400))]
+    i = 0
+    while i < len(ev):
+        j = i
+        while j < len(ev) and ev[j][0] == ev[i][0] and j - i < (1 + (i % 7)):
+            j += 1
+        rows = [r for _, r, _ in ev[i:j]]
+        ts = [t for _, _, t in ev[i:j]]
+        o.send(ev[i][0], rows, ts)
+        g.send(ev[i][0], rows, ts)
+        i = j
+    assert g.matches == o.matches
+
+
+def test_kgen_host_seq_windows_c4():
+    import numpy as np
+    from siddhi_amd.workloads import c4_app, txn_events
+    src = c4_app(40)
+    o = App(src)
+    g = App(src, engine_factory=lambda blob: KGenHostEngine(blob, window=True))
+    total = 0
+    for lo, hi in ((0, 2000), (2000, 2001), (2001, 2003), (2003, 5000)):
+        ts, acc, amt, risk = txn_events(lo, hi - lo, n_accounts=500)
+        vals = np.stack([acc.astype(np.int64), amt.view(np.uint32).astype(np.int64), risk.astype(np.int64)], 1)
+        o.engine.send(0, ts, vals, None)
+        g.engine.send(0, ts, vals, None)
+        om = o.engine.take_matches(lambda q: 3)
+        assert g.engine.take_matches(lambda q: 3) == om
+        total += len(om)
+    assert total > 1000
