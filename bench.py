@@ -189,7 +189,7 @@ def main():
     else:
         wl = ("C4: fraud-rule sequences every e1=Txn[..], e2=Txn[..e1.amount*M], e3=Txn[..] within 1 min "
               f"(strict contiguity), {K} accounts, pattern-set shard {rank * P}..{rank * P + P - 1}")
-        kernel = "nfa_gen_kernel"
+        kernel = "nfa_seq_kernel"
     traffic = profiled_traffic(kernel)
     result = {
         "metric": "events/sec x active patterns (whole node); achieved HBM GB/s",

@@ -26,8 +26,10 @@
 
 #ifdef __HIPCC__
 #define KG_FN __host__ __device__ inline
+#define KG_UNROLL _Pragma("unroll")
 #else
 #define KG_FN inline
+#define KG_UNROLL _Pragma("GCC unroll 8")
 #endif
 
 namespace sdh {
@@ -222,10 +224,42 @@ enum { FL_CHANGED = 1, FL_INIT = 2, FL_SUCCESS = 4, FL_SSRESET = 8, FL_RETURNED 
 // the device), constants from the lane's own query ql. attr(in) resolves OP_ATTR to a typed value,
 // stream_null(in) answers OP_STREAM_IS_NULL -- K_gen over its instance arena, K_seq over the
 // event window of a sequence.
-template <class Attr, class StreamNull>
-KG_FN Val eval_code(const GQuery* q, const GQuery* ql, int b, int e, Attr attr, StreamNull stream_null) {
+// Evaluation stacks. ArrStack: an indexed array (K_gen; private memory on the device). RegStack:
+// a shift register of RSTACK entries, every access at a constant index, so it lives in VGPRs
+// (K_seq, whose shapes are checked to need at most RSTACK entries, kg::code_depth).
+struct ArrStack {
   Val st[GSTACK];
   int sp = 0;
+  KG_FN void push(const Val& v) {
+    st[sp++] = v;
+    if (sp >= GSTACK) sp = GSTACK - 1;
+  }
+  KG_FN Val pop() { return st[--sp]; }
+  KG_FN Val result() const { return sp == 1 ? st[0] : Val{T_BOOL, 1, 0}; }
+};
+constexpr int RSTACK = 6;
+struct RegStack {
+  Val s[RSTACK];
+  int sp = 0;
+  KG_FN void push(const Val& v) {
+KG_UNROLL
+    for (int k = RSTACK - 1; k > 0; --k) s[k] = s[k - 1];
+    s[0] = v;
+    ++sp;
+  }
+  KG_FN Val pop() {
+    const Val v = s[0];
+KG_UNROLL
+    for (int k = 0; k < RSTACK - 1; ++k) s[k] = s[k + 1];
+    --sp;
+    return v;
+  }
+  KG_FN Val result() const { return sp == 1 ? s[0] : Val{T_BOOL, 1, 0}; }
+};
+
+template <class Stack = ArrStack, class Attr, class StreamNull>
+KG_FN Val eval_code(const GQuery* q, const GQuery* ql, int b, int e, Attr attr, StreamNull stream_null) {
+  Stack stk;
   for (int pc = b; pc < e; ++pc) {
     const GInsn& in = q->code[pc];
     switch (in.op) {
@@ -235,51 +269,50 @@ KG_FN Val eval_code(const GQuery* q, const GQuery* ql, int b, int e, Attr attr, 
         if (in.res == T_FLOAT) v.bits = (int64_t)(uint32_t)imm;
         else if (in.res == T_INT) v.bits = (int32_t)imm;
         else v.bits = imm;
-        st[sp++] = v;
+        stk.push(v);
         break;
       }
       case OP_ATTR:
-        st[sp++] = attr(in);
+        stk.push(attr(in));
         break;
       case OP_STREAM_IS_NULL:
-        st[sp++] = Val{T_BOOL, 0, stream_null(in) ? 1 : 0};
+        stk.push(Val{T_BOOL, 0, stream_null(in) ? 1 : 0});
         break;
       case OP_IS_NULL: {
-        const Val x = st[--sp];
-        st[sp++] = Val{T_BOOL, 0, x.null ? 1 : 0};
+        const Val x = stk.pop();
+        stk.push(Val{T_BOOL, 0, x.null ? 1 : 0});
         break;
       }
       case OP_NOT: {  // NotConditionExpressionExecutor: only TRUE -> FALSE
-        const Val x = st[--sp];
-        st[sp++] = Val{T_BOOL, 0, (!x.null && x.bits) ? 0 : 1};
+        const Val x = stk.pop();
+        stk.push(Val{T_BOOL, 0, (!x.null && x.bits) ? 0 : 1});
         break;
       }
       case OP_AND:
       case OP_OR: {
-        const Val r = st[--sp];
-        const Val l = st[--sp];
+        const Val r = stk.pop();
+        const Val l = stk.pop();
         const bool lb = !l.null && l.bits, rb = !r.null && r.bits;
-        st[sp++] = Val{T_BOOL, 0, (in.op == OP_AND ? (lb && rb) : (lb || rb)) ? 1 : 0};
+        stk.push(Val{T_BOOL, 0, (in.op == OP_AND ? (lb && rb) : (lb || rb)) ? 1 : 0});
         break;
       }
       case OP_CMP: {  // CompareConditionExpressionExecutor.java:39-43
-        const Val r = st[--sp];
-        const Val l = st[--sp];
-        st[sp++] = Val{T_BOOL, 0, (!l.null && !r.null && typed_compare((int)in.imm, l, r)) ? 1 : 0};
+        const Val r = stk.pop();
+        const Val l = stk.pop();
+        stk.push(Val{T_BOOL, 0, (!l.null && !r.null && typed_compare((int)in.imm, l, r)) ? 1 : 0});
         break;
       }
       case OP_ARITH: {
-        const Val r = st[--sp];
-        const Val l = st[--sp];
-        st[sp++] = arith((int)in.imm, in.res, l, r);
+        const Val r = stk.pop();
+        const Val l = stk.pop();
+        stk.push(arith((int)in.imm, in.res, l, r));
         break;
       }
       default:
-        st[sp++] = Val{T_BOOL, 1, 0};
+        stk.push(Val{T_BOOL, 1, 0});
     }
-    if (sp >= GSTACK) sp = GSTACK - 1;
   }
-  return sp == 1 ? st[0] : Val{T_BOOL, 1, 0};
+  return stk.result();
 }
 
 struct Emitter;  // defined by the caller: void emit(const Ctx&, int se)
@@ -834,8 +867,23 @@ inline int seq_lookback(const GQuery& g) {
 // k-j .. k-1, so a match is a property of a window of S consecutive events alone: starting at s,
 // every state i passes its filters over events s .. s+i, and no step i >= 1 is expired
 // (|ts[s] - ts[s+i]| > within). Returns S, or -1.
+inline int code_depth(const GQuery& g, int b, int e) {  // max evaluation-stack entries of a range
+  int sp = 0, mx = 0;
+  for (int pc = b; pc < e; ++pc) {
+    const int op = g.code[pc].op;
+    if (op == OP_CONST || op == OP_ATTR || op == OP_STREAM_IS_NULL) ++sp;
+    else if (op == OP_AND || op == OP_OR || op == OP_CMP || op == OP_ARITH) --sp;
+    else if (op != OP_IS_NULL && op != OP_NOT) ++sp;
+    mx = sp > mx ? sp : mx;
+  }
+  return mx;
+}
+
 inline int seq_window(const GQuery& g) {
   if (seq_lookback(g) < 0) return -1;
+  for (int i = 0; i < g.n_states; ++i)
+    for (int f = 0; f < g.st[i].n_filt; ++f)
+      if (code_depth(g, g.st[i].fb[f], g.st[i].fe[f]) > RSTACK) return -1;
   const int st = g.st[0].stream;
   if (!g.st[0].is_start) return -1;
   for (int i = 0; i < g.n_states; ++i)
@@ -860,7 +908,7 @@ KG_FN bool seq_match(const GQuery* q, const GQuery* ql, int64_t within, const Wi
     }
     const GState& st = q->st[i];
     for (int f = 0; f < st.n_filt; ++f) {
-      const Val v = eval_code(
+      const Val v = eval_code<RegStack>(
           q, ql, st.fb[f], st.fe[f],
           [&](const GInsn& in) {
             Val x{in.res, 1, 0};
