@@ -80,15 +80,20 @@ def cpu_baseline(workload, n_symbols, budget_s):
                       f"{dt:.1f} s)"}
 
 
-def profiled_traffic(kernel):
+def profiled_traffic(kernel, patterns, batch):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC run of this same command
-    (profiles/*/counters.json; FETCH_SIZE x2 gfx950 streaming-read correction + WRITE_SIZE, KiB)."""
+    (profiles/*/counters.json next to a bench_line.json of the same patterns and batch;
+    FETCH_SIZE x2 gfx950 streaming-read correction + WRITE_SIZE, KiB)."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "counters.json"))):
         try:
             d = json.load(open(f))
+            line = json.loads(open(os.path.join(os.path.dirname(f), "bench_line.json")).read().strip().splitlines()[-1])
         except Exception:  # noqa: BLE001
+            continue
+        cfg = line.get("config", {})
+        if cfg.get("patterns_per_gpu") != patterns or cfg.get("events_per_step") != batch:
             continue
         for k, c in d.items():
             if kernel in k and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
@@ -128,8 +133,9 @@ def main():
     else:
         from siddhi_amd.workloads import c3_app
         ir = plan(ql.parse(c3_app(P, first=rank * P)))
-        eng = HipEngine(ir.serialize(), device=local, flags=SDH_FLAG_DEVICE_MATCHES, gen_pool_states=32,
-                        gen_pool_nodes=128, gen_list_cap=32, gen_max_keys=max(1024, 2 * K))
+        pools = [int(x) for x in os.environ.get("SDH_C3_POOLS", "32,128,32").split(",")]
+        eng = HipEngine(ir.serialize(), device=local, flags=SDH_FLAG_DEVICE_MATCHES, gen_pool_states=pools[0],
+                        gen_pool_nodes=pools[1], gen_list_cap=pools[2], gen_max_keys=max(1024, 2 * K))
 
     B = args.batch
     n_batches = args.warmup + args.steps
@@ -179,7 +185,7 @@ def main():
     achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
     peak = 8000.0
     if args.workload == "c2":
-        wl = ("C2: 1K concurrent 2-state filter+reference patterns "
+        wl = (f"C2: {P} concurrent 2-state filter+reference patterns "
               "(every e1[price>T_p] -> e2[price>e1.price] within W_p)")
         kernel = "nfa_ratchet_kernel"
     elif args.workload == "c3":
@@ -190,7 +196,7 @@ def main():
         wl = ("C4: fraud-rule sequences every e1=Txn[..], e2=Txn[..e1.amount*M], e3=Txn[..] within 1 min "
               f"(strict contiguity), {K} accounts, pattern-set shard {rank * P}..{rank * P + P - 1}")
         kernel = "nfa_seq_kernel"
-    traffic = profiled_traffic(kernel)
+    traffic = profiled_traffic(kernel, P, B)
     result = {
         "metric": "events/sec x active patterns (whole node); achieved HBM GB/s",
         "value": value,

@@ -297,14 +297,20 @@ KG_FN Val eval_code(const GQuery* q, const GQuery* ql, int b, int e, Attr attr, 
         break;
       }
       case OP_CMP: {  // CompareConditionExpressionExecutor.java:39-43
-        const Val r = stk.pop();
-        const Val l = stk.pop();
+        // operand types are static (the planner's ltype/rtype): taking them from the instruction
+        // keeps the typed dispatch wave-uniform
+        Val r = stk.pop();
+        Val l = stk.pop();
+        l.type = in.lt;
+        r.type = in.rt;
         stk.push(Val{T_BOOL, 0, (!l.null && !r.null && typed_compare((int)in.imm, l, r)) ? 1 : 0});
         break;
       }
       case OP_ARITH: {
-        const Val r = stk.pop();
-        const Val l = stk.pop();
+        Val r = stk.pop();
+        Val l = stk.pop();
+        l.type = in.lt;
+        r.type = in.rt;
         stk.push(arith((int)in.imm, in.res, l, r));
         break;
       }
