@@ -137,9 +137,18 @@ def main():
     import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    # rehearsal knobs for a 1-GPU box (not used by the driver): every rank on one device, gloo
+    backend = os.environ.get("SDH_BENCH_BACKEND", "nccl")
+    if "SDH_BENCH_DEVICE" in os.environ:
+        local = int(os.environ["SDH_BENCH_DEVICE"])
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # where the timing reductions run
 
     from siddhi_amd import ql
     from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES, HipEngine
@@ -198,10 +207,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        mt = torch.tensor([matches], device=dev, dtype=torch.float64)
+        mt = torch.tensor([matches], device=cdev, dtype=torch.float64)
         dist.all_reduce(mt)
         matches = int(mt.item())
 
