@@ -269,6 +269,10 @@ inline GQuery lower_gen(const LProgram& P, int qi, const Sizing& sz) {
     }
   }
   g.n_code = pc;
+  g.max_depth = 0;
+  for (int i = 0; i < g.n_states; ++i)
+    for (int f = 0; f < g.st[i].n_filt; ++f)
+      g.max_depth = std::max(g.max_depth, code_depth(g, g.st[i].fb[f], g.st[i].fe[f]));
   make_layout(g.lay, S, sz.R, sz.N, sz.LC, NA);
   return g;
 }

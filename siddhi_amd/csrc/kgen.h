@@ -90,7 +90,7 @@ struct GQuery {
   GLayout lay;
   GState st[GMAXS];
   int32_t n_code;
-  int32_t pad1;
+  int32_t max_depth;  // deepest evaluation stack of any filter (kg::code_depth)
   GInsn code[GMAXCODE];
 };
 
@@ -624,7 +624,13 @@ struct Ctx {
     return e;
   }
   KG_FN Val run_code(int b, int e, int se) const {
-    return eval_code(
+    // shallow programs (a wave-uniform property of the shape) keep the stack in registers
+    if (q->max_depth <= RSTACK) return run_code_t<RegStack>(b, e, se);
+    return run_code_t<ArrStack>(b, e, se);
+  }
+  template <class Stack>
+  KG_FN Val run_code_t(int b, int e, int se) const {
+    return eval_code<Stack>(
         q, ql, b, e,
         [&](const GInsn& in) {  // OP_ATTR: the slot's chain element (CURRENT=-1, LAST=-2, ...)
           const int n = chain_at(slot(se, in.a), in.b);
