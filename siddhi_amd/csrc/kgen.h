@@ -42,6 +42,7 @@ constexpr int GMAXNA = 8;        // captured attributes per node (per stream)
 constexpr int GMAXSTREAM = 8;    // streams a query may read
 constexpr int GSTACK = 12;       // bytecode evaluation stack
 constexpr int GMAXRET = 64;      // matches one processAndReturn may return
+constexpr int GMAXNU = 4;        // node used-bitmask words (nodes per instance <= 256)
 
 enum { T_INT = 0, T_LONG, T_FLOAT, T_DOUBLE, T_BOOL, T_STRING };
 enum { OP_CONST = 1, OP_ATTR, OP_IS_NULL, OP_STREAM_IS_NULL, OP_CMP, OP_AND, OP_OR, OP_NOT, OP_ARITH };
@@ -322,6 +323,9 @@ KG_FN Val eval_code(const GQuery* q, const GQuery* ql, int b, int e, Attr attr, 
 }
 
 struct Emitter;  // defined by the caller: void emit(const Ctx&, int se)
+#ifdef KG_PROFILE
+void kg_prof_hit(const GLayout& L, int is64, int off);
+#endif
 
 struct Ctx {
   // q: the query's structure. On the device it is the wave's template -- every lane of a group has
@@ -335,20 +339,35 @@ struct Ctx {
   int32_t* w32;
   int64_t* w64;
   int64_t stride;
+  // hot words, cached for the whole work item (LDS on the device, [word][lane]): per state flags /
+  // pending count / newAndEvery count ([3][GMAXS]), and the two pools' used-bitmasks ([1 + GMAXNU]).
+  // They are touched on every event by every processor (about half of all arena accesses on C3);
+  // load_hot/store_hot move them between the arena and the cache at the item's ends.
+  int32_t* h32;
+  int64_t* h64;
+  int64_t hstride;
   // current event (the instance's view of it)
   int64_t seq, ts;
   int32_t stream;
-  int64_t ev_val[GMAXNA];
+  const int64_t* ev_val;  // [GMAXNA] the event's captured words (wave-uniform: LDS on the device)
   uint32_t ev_null;
   int32_t err;
+  // The dynamically indexed arrays (event words, pins, return list) live outside Ctx, behind
+  // pointers: an array indexed by a run-time value inside the struct would keep the whole Ctx in
+  // scratch memory on the device (no SROA), turning every field read into a scratch load.
   // GC roots outside the lists: partials unlinked or not yet linked while they are worked on
-  int32_t pins[4];
+  int32_t* pins;  // [4]
   int32_t npin;
-  int32_t ret[GMAXRET];
+  int32_t* ret;   // [GMAXRET]
   int32_t n_ret;
 
+#ifdef KG_PROFILE  // host-only access census (tests/native, test infrastructure)
+  int32_t& i32(int i) const { kg_prof_hit(lay, 0, i); return w32[(int64_t)i * stride]; }
+  int64_t& i64(int i) const { kg_prof_hit(lay, 1, i); return w64[(int64_t)i * stride]; }
+#else
   KG_FN int32_t& i32(int i) const { return w32[(int64_t)i * stride]; }
   KG_FN int64_t& i64(int i) const { return w64[(int64_t)i * stride]; }
+#endif
   KG_FN const GState& S(int i) const { return q->st[i]; }
   KG_FN int nS() const { return lay.S; }
   KG_FN void bind(const GQuery* tmpl, const GQuery* own) {
@@ -359,9 +378,9 @@ struct Ctx {
   }
 
   // ---- arena fields ----
-  KG_FN int32_t& flags(int i) const { return i32(lay.o_flags + i); }
-  KG_FN int32_t& pn(int i) const { return i32(lay.o_pn + i); }
-  KG_FN int32_t& nn(int i) const { return i32(lay.o_nn + i); }
+  KG_FN int32_t& flags(int i) const { return h32[(int64_t)i * hstride]; }
+  KG_FN int32_t& pn(int i) const { return h32[(int64_t)(GMAXS + i) * hstride]; }
+  KG_FN int32_t& nn(int i) const { return h32[(int64_t)(2 * GMAXS + i) * hstride]; }
   KG_FN int32_t& pl(int i, int k) const { return i32(lay.o_plist + i * lay.LC + k); }
   KG_FN int32_t& nl(int i, int k) const { return i32(lay.o_nlist + i * lay.LC + k); }
   KG_FN int32_t& slot(int se, int i) const { return i32(lay.o_seslot + se * lay.S + i); }
@@ -371,8 +390,26 @@ struct Ctx {
   KG_FN int64_t& nd_seq(int n) const { return i64(lay.o_ndseq + n); }
   KG_FN int64_t& nd_ts(int n) const { return i64(lay.o_ndts + n); }
   KG_FN int64_t& nd_val(int n, int j) const { return i64(lay.o_ndval + n * lay.NA + j); }
-  KG_FN int64_t& se_used() const { return i64(lay.o_seused); }
-  KG_FN int64_t& nd_used(int w) const { return i64(lay.o_ndused + w); }
+  KG_FN int64_t& se_used() const { return h64[0]; }
+  KG_FN int64_t& nd_used(int w) const { return h64[(int64_t)(1 + w) * hstride]; }
+  KG_FN void load_hot() {
+    for (int i = 0; i < lay.S; ++i) {
+      flags(i) = i32(lay.o_flags + i);
+      pn(i) = i32(lay.o_pn + i);
+      nn(i) = i32(lay.o_nn + i);
+    }
+    se_used() = i64(lay.o_seused);
+    for (int w = 0; w < lay.NU; ++w) nd_used(w) = i64(lay.o_ndused + w);
+  }
+  KG_FN void store_hot() const {
+    for (int i = 0; i < lay.S; ++i) {
+      i32(lay.o_flags + i) = flags(i);
+      i32(lay.o_pn + i) = pn(i);
+      i32(lay.o_nn + i) = nn(i);
+    }
+    i64(lay.o_seused) = se_used();
+    for (int w = 0; w < lay.NU; ++w) i64(lay.o_ndused + w) = nd_used(w);
+  }
 
   KG_FN void fail(int e) {
     if (err == GE_OK) err = e;

@@ -107,6 +107,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   c.w32 = a32 + block * L.B32 * 64 + lane;
   c.w64 = a64 + block * L.B64 * 64 + lane;
   c.stride = 64;
+  // hot words in LDS for the item (kgen.h Ctx::h32/h64): one wave per block, [word][lane]
+  __shared__ int32_t hot32[3 * kg::GMAXS * 64];
+  __shared__ int64_t hot64[(1 + kg::GMAXNU) * 64];
+  c.h32 = hot32 + lane;
+  c.h64 = hot64 + lane;
+  c.hstride = 64;
+  c.load_hot();
+  __shared__ int64_t evv[kg::GMAXNA];  // the current event's captured words (wave-uniform)
+  int32_t pins[4];
+  int32_t ret[kg::GMAXRET];
+  c.ev_val = evv;
+  c.pins = pins;
+  c.ret = ret;
   c.err = kg::GE_OK;
   c.npin = 0;
   c.n_ret = 0;
@@ -126,9 +139,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     c.seq = L.b.seq_base + e;
     c.ts = L.b.ts[e];
     c.ev_null = 0;
-    for (int j = 0; j < ncap; ++j) {
+    for (int j = 0; j < ncap; ++j) {  // the event is the same for every lane: identical LDS stores
       bool nl;
-      c.ev_val[j] = raw_word(L.b, q->cap_attr[c.stream][j], e, nl);
+      evv[j] = raw_word(L.b, q->cap_attr[c.stream][j], e, nl);
       if (nl) c.ev_null |= 1u << j;
     }
     int64_t idx = 0;
@@ -164,6 +177,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     c.receive(emit);
   }
   o.close();
+  c.store_hot();
   if (nrec) atomicAdd(L.rec_count, nrec);
   if (c.err == kg::GE_CAPACITY) atomicOr(&L.err[0], 1);
   if (c.err == kg::GE_REFERENCE) atomicOr(&L.err[1], 1);

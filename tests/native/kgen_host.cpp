@@ -77,6 +77,18 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
   c.w32 = in->w32.data();
   c.w64 = in->w64.data();
   c.stride = 1;
+  int32_t hot32[3 * GMAXS];
+  int64_t hot64[1 + GMAXNU];
+  c.h32 = hot32;
+  c.h64 = hot64;
+  c.hstride = 1;
+  c.load_hot();
+  int64_t evv[GMAXNA];
+  int32_t pins[4];
+  int32_t ret[GMAXRET];
+  c.ev_val = evv;
+  c.pins = pins;
+  c.ret = ret;
   c.npin = 0;
   c.n_ret = 0;
   c.err = GE_OK;
@@ -93,7 +105,7 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
   c.ev_null = 0;
   for (int j = 0; j < q.n_cap[stream]; ++j) {
     const int a = q.cap_attr[stream][j];
-    c.ev_val[j] = vals[a];
+    evv[j] = vals[a];
     if (nulls && nulls[a]) c.ev_null |= 1u << j;
   }
   int64_t idx = 0;
@@ -114,6 +126,7 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
     h->out.push_back(r);
   };
   c.receive(emit);
+  c.store_hot();
   if (c.err == GE_CAPACITY) throw std::runtime_error("K_gen instance capacity exceeded");
   if (c.err == GE_REFERENCE) throw std::runtime_error("reference engine would throw here");
 }
@@ -273,3 +286,26 @@ const char* kgh_error(void* hp) { return ((Host*)hp)->err.c_str(); }
 void kgh_destroy(void* hp) { delete (Host*)hp; }
 
 }  // extern "C"
+
+#ifdef KG_PROFILE
+// access census by arena field (test infrastructure: sizes the device's arena traffic)
+namespace sdh { namespace kg {
+int64_t g_prof[16];
+void kg_prof_hit(const GLayout& L, int is64, int off) {
+  int r;
+  if (!is64) {
+    const int b[] = {L.o_flags, L.o_pn, L.o_nn, L.o_plist, L.o_nlist, L.o_seslot, L.o_ndnext, L.o_ndnull, L.o_init};
+    r = 0;
+    for (int k = 0; k < 9; ++k) if (off >= b[k]) r = k;
+  } else {
+    const int b[] = {L.o_seused, L.o_ndused, L.o_sets, L.o_ndseq, L.o_ndts, L.o_ndval};
+    r = 9;
+    for (int k = 0; k < 6; ++k) if (off >= b[k]) r = 9 + k;
+  }
+  ++g_prof[r];
+}
+}}
+extern "C" void kgh_prof(int64_t* out) {
+  for (int k = 0; k < 16; ++k) { out[k] = sdh::kg::g_prof[k]; sdh::kg::g_prof[k] = 0; }
+}
+#endif
