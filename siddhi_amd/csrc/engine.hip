@@ -534,6 +534,7 @@ struct sdh_engine {
   std::vector<DevBuf<int64_t>> seq_tail;  // [stream] last SEQ_TMAX events (K_seq windows)
   std::vector<int32_t> seq_tail_len;
   int gB32 = 1, gB64 = 1;
+  int gHotS = 1, gHotNU = 1;  // K_gen LDS hot-word cache extents (max states / node-mask words)
   struct GenSet {
     int partition = -1;              // -1: the unpartitioned K_gen queries
     int group_base = 0, n_groups = 0;
@@ -1092,6 +1093,8 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
       e->gq.push_back(g);
       e->gB32 = std::max(e->gB32, g.lay.n32);
       e->gB64 = std::max(e->gB64, g.lay.n64);
+      e->gHotS = std::max(e->gHotS, g.lay.S);
+      e->gHotNU = std::max(e->gHotNU, g.lay.NU);
     } catch (const kg::LowerError& ex) {
       throw Error(SDH_E_UNSUPPORTED, fmt("query %d: %s", qi, ex.what()));
     }
@@ -1234,6 +1237,8 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     L.group_base = gs.group_base;
     L.B32 = e->gB32;
     L.B64 = e->gB64;
+    L.hot_s = e->gHotS;
+    L.hot_nu = e->gHotNU;
     L.out = e->g_out.p;
     L.out_cap = e->g_out_cap;
     L.out_next = e->g_out_next.p;

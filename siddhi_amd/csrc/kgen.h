@@ -43,6 +43,10 @@ constexpr int GMAXSTREAM = 8;    // streams a query may read
 constexpr int GSTACK = 12;       // bytecode evaluation stack
 constexpr int GMAXRET = 64;      // matches one processAndReturn may return
 constexpr int GMAXNU = 4;        // node used-bitmask words (nodes per instance <= 256)
+// the current event, not yet copied into the node pool: a stream / logical state's slot holds it
+// while that state's filters run, and it is copied only when they pass (fewer pool writes and
+// sweeps; observable behaviour is unchanged, the copy is invisible until a post processor runs)
+constexpr int VNODE = 0x7fff;
 
 enum { T_INT = 0, T_LONG, T_FLOAT, T_DOUBLE, T_BOOL, T_STRING };
 enum { OP_CONST = 1, OP_ATTR, OP_IS_NULL, OP_STREAM_IS_NULL, OP_CMP, OP_AND, OP_OR, OP_NOT, OP_ARITH };
@@ -346,6 +350,7 @@ struct Ctx {
   int32_t* h32;
   int64_t* h64;
   int64_t hstride;
+  int32_t hs;  // states the h32 cache holds per field (the launch's max)
   // current event (the instance's view of it)
   int64_t seq, ts;
   int32_t stream;
@@ -379,8 +384,8 @@ struct Ctx {
 
   // ---- arena fields ----
   KG_FN int32_t& flags(int i) const { return h32[(int64_t)i * hstride]; }
-  KG_FN int32_t& pn(int i) const { return h32[(int64_t)(GMAXS + i) * hstride]; }
-  KG_FN int32_t& nn(int i) const { return h32[(int64_t)(2 * GMAXS + i) * hstride]; }
+  KG_FN int32_t& pn(int i) const { return h32[(int64_t)(hs + i) * hstride]; }
+  KG_FN int32_t& nn(int i) const { return h32[(int64_t)(2 * hs + i) * hstride]; }
   KG_FN int32_t& pl(int i, int k) const { return i32(lay.o_plist + i * lay.LC + k); }
   KG_FN int32_t& nl(int i, int k) const { return i32(lay.o_nlist + i * lay.LC + k); }
   KG_FN int32_t& slot(int se, int i) const { return i32(lay.o_seslot + se * lay.S + i); }
@@ -417,7 +422,7 @@ struct Ctx {
 
   // ---- allocation with mark/sweep reclamation ----
   KG_FN void mark_chain(int n, uint64_t* nm) const {
-    while (n >= 0 && !((nm[n >> 6] >> (n & 63)) & 1ull)) {
+    while (n >= 0 && n < lay.N && !((nm[n >> 6] >> (n & 63)) & 1ull)) {
       nm[n >> 6] |= 1ull << (n & 63);
       n = nd_next(n);
     }
@@ -633,6 +638,7 @@ struct Ctx {
   // ---- predicates ----
   KG_FN int chain_at(int head, int64_t idx) const {  // StateEvent.getStreamEvent:138-182
     if (head < 0) return -1;
+    if (head == VNODE) return (idx == 0 || idx == -1) ? VNODE : -1;  // one-event chain
     if (idx >= 0) {
       int e = head;
       for (int64_t k = 1; k <= idx; ++k) {
@@ -672,9 +678,10 @@ struct Ctx {
         [&](const GInsn& in) {  // OP_ATTR: the slot's chain element (CURRENT=-1, LAST=-2, ...)
           const int n = chain_at(slot(se, in.a), in.b);
           Val v{in.res, 1, 0};
-          if (n >= 0 && !((nd_null(n) >> in.imm) & 1)) {
+          const bool cur = n == VNODE;
+          if (n >= 0 && !(((cur ? (int32_t)ev_null : nd_null(n)) >> in.imm) & 1)) {
             v.null = 0;
-            const int64_t raw = nd_val(n, (int)in.imm);
+            const int64_t raw = cur ? ev_val[in.imm] : nd_val(n, (int)in.imm);
             v.bits = in.res == T_INT ? (int64_t)(int32_t)raw : in.res == T_FLOAT ? (int64_t)(uint32_t)raw : raw;
           }
           return v;
@@ -739,6 +746,12 @@ struct Ctx {
   KG_FN void process(int i, int se) {
     flags(i) &= ~FL_CHANGED;
     if (!filters_pass(i, se)) return;
+    if (slot(se, i) == VNODE) {  // the filters passed: copy the current event now
+      slot(se, i) = -1;
+      const int ev = copy_event(se);
+      if (ev < 0) return;  // capacity (err is set; the push fails)
+      slot(se, i) = ev;
+    }
     switch (S(i).kind) {
       case K_STREAM: stream_post(i, se); break;
       case K_COUNT: count_post(i, se); break;
@@ -816,9 +829,7 @@ struct Ctx {
       } else if (s.kind == K_LOGICAL && s.ltype == L_OR && slot(se, s.partner) >= 0) {
         keep = false;
       } else {
-        const int ev = copy_event(se);
-        if (ev < 0) { unpin(); break; }
-        slot(se, i) = ev;
+        slot(se, i) = VNODE;  // copied into the pool by process() once the filters pass
         process(i, se);
         if (take_returned(i)) push_ret(se);
         if (flags(i) & FL_CHANGED) {

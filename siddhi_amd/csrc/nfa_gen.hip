@@ -107,14 +107,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   c.w32 = a32 + block * L.B32 * 64 + lane;
   c.w64 = a64 + block * L.B64 * 64 + lane;
   c.stride = 64;
-  // hot words in LDS for the item (kgen.h Ctx::h32/h64): one wave per block, [word][lane]
-  __shared__ int32_t hot32[3 * kg::GMAXS * 64];
-  __shared__ int64_t hot64[(1 + kg::GMAXNU) * 64];
-  c.h32 = hot32 + lane;
-  c.h64 = hot64 + lane;
+  // dynamic LDS (gen_lds_bytes): the current event's captured words (wave-uniform), then the hot
+  // words of the item (kgen.h Ctx::h32/h64), [word][lane] -- sized to the launch's largest shape so
+  // LDS does not cap occupancy
+  extern __shared__ int64_t gen_lds[];
+  int64_t* evv = gen_lds;
+  c.h64 = gen_lds + kg::GMAXNA + lane;
+  c.h32 = (int32_t*)(gen_lds + kg::GMAXNA + (1 + L.hot_nu) * 64) + lane;
   c.hstride = 64;
+  c.hs = L.hot_s;
   c.load_hot();
-  __shared__ int64_t evv[kg::GMAXNA];  // the current event's captured words (wave-uniform)
   int32_t pins[4];
   int32_t ret[kg::GMAXRET];
   c.ev_val = evv;
@@ -382,9 +384,10 @@ __global__ void gen_lookup_kernel(int64_t n, const int64_t* key, uint32_t* kid, 
 
 extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
-  // 4 waves/SIMD (128 VGPRs, a few spills) beat the unconstrained 152-VGPR build (3 waves) by 11 %
-  // on C3; 6 and 8 spill too much
-  hipLaunchKernelGGL(sdh::nfa_gen_kernel<4>, dim3(L->n_items), dim3(64), 0, s, *L);
+  // 4 waves/SIMD (116 VGPRs, no spills): on C3, 5 (96 VGPRs + spills) is level and 6 / 8 are
+  // 10-30 % slower
+  const size_t lds = (size_t)(sdh::kg::GMAXNA + (1 + L->hot_nu) * 64) * 8 + (size_t)3 * L->hot_s * 64 * 4;
+  hipLaunchKernelGGL(sdh::nfa_gen_kernel<4>, dim3(L->n_items), dim3(64), lds, s, *L);
   return hipGetLastError();
 }
 

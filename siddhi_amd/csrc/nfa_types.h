@@ -226,6 +226,7 @@ struct GenLaunch {
   int32_t* a32;
   int64_t* a64;
   int32_t B32, B64;           // arena words per lane and block
+  int32_t hot_s, hot_nu;      // LDS hot-word cache extents: max states, max node-mask words
   int64_t* out;               // flat record words: [len, qid, key, ts, seq, idx, S, (count, seqs...)xS]...
   int64_t out_cap;            // words
   unsigned long long* out_next;  // words used (atomic; may run past out_cap on overflow)

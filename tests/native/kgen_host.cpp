@@ -82,6 +82,7 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
   c.h32 = hot32;
   c.h64 = hot64;
   c.hstride = 1;
+  c.hs = GMAXS;
   c.load_hot();
   int64_t evv[GMAXNA];
   int32_t pins[4];
