@@ -329,6 +329,10 @@ KG_FN Val eval_code(const GQuery* q, const GQuery* ql, int b, int e, Attr attr, 
 struct Emitter;  // defined by the caller: void emit(const Ctx&, int se)
 #ifdef KG_PROFILE
 void kg_prof_hit(const GLayout& L, int is64, int off);
+extern int g_prof_phase;  // census phase (0 = processing, 1 = mark/sweep)
+#define KG_PHASE(p) (g_prof_phase = (p))
+#else
+#define KG_PHASE(p) ((void)0)
 #endif
 
 struct Ctx {
@@ -433,6 +437,7 @@ struct Ctx {
     for (int i = 0; i < nS(); ++i) mark_chain(slot(se, i), nm);
   }
   KG_FN void gc() {
+    KG_PHASE(1);
     uint64_t sm = 0, nm[4] = {0, 0, 0, 0};
     for (int i = 0; i < nS(); ++i) {
       for (int k = 0; k < pn(i); ++k) mark_se(pl(i, k), sm, nm);
@@ -442,6 +447,7 @@ struct Ctx {
     for (int k = 0; k < n_ret; ++k) mark_se(ret[k], sm, nm);
     se_used() = (int64_t)sm;
     for (int w = 0; w < lay.NU; ++w) nd_used(w) = (int64_t)nm[w];
+    KG_PHASE(0);
   }
   KG_FN int find_free_se() const {
     const uint64_t u = (uint64_t)se_used();

@@ -292,7 +292,9 @@ void kgh_destroy(void* hp) { delete (Host*)hp; }
 // access census by arena field (test infrastructure: sizes the device's arena traffic)
 namespace sdh { namespace kg {
 int64_t g_prof[16];
+int g_prof_phase = 0;
 void kg_prof_hit(const GLayout& L, int is64, int off) {
+  if (g_prof_phase) { ++g_prof[15]; return; }
   int r;
   if (!is64) {
     const int b[] = {L.o_flags, L.o_pn, L.o_nn, L.o_plist, L.o_nlist, L.o_seslot, L.o_ndnext, L.o_ndnull, L.o_init};
