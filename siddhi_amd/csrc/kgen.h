@@ -369,6 +369,10 @@ struct Ctx {
   int32_t npin;
   int32_t* ret;   // [GMAXRET]
   int32_t n_ret;
+  // the count state's chain as process_and_return just extended it (its last node and length), so
+  // CountPost does not walk it again; -1 = unknown
+  int32_t cnt_tail = -1;
+  int64_t cnt_len = 0;
 
 #ifdef KG_PROFILE  // host-only access census (tests/native, test infrastructure)
   int32_t& i32(int i) const { kg_prof_hit(lay, 0, i); return w32[(int64_t)i * stride]; }
@@ -724,9 +728,13 @@ struct Ctx {
   }
   KG_FN void count_post(int i, int se) {  // CountPostStateProcessor.process:45-71
     const GState& s = S(i);
-    int e = slot(se, i);
-    int64_t n = 1;
-    while (nd_next(e) >= 0) { ++n; e = nd_next(e); }
+    int e = cnt_tail;
+    int64_t n = cnt_len;
+    if (e < 0) {
+      e = slot(se, i);
+      n = 1;
+      for (int nx = nd_next(e); nx >= 0; nx = nd_next(e)) { ++n; e = nx; }
+    }
     flags(i) |= FL_SUCCESS;
     se_ts(se) = nd_ts(e);
     if (n >= s.min) {
@@ -798,28 +806,29 @@ struct Ctx {
         } else {
           const int ev = copy_event(se);
           if (ev < 0) { unpin(); break; }
+          int prev = -1;  // the node before ev
+          int64_t len = 1;
           if (slot(se, i) < 0) slot(se, i) = ev;  // StateEvent.addEvent:212-222
           else {
             int t = slot(se, i);
-            while (nd_next(t) >= 0) t = nd_next(t);
+            len = 2;
+            for (int nx = nd_next(t); nx >= 0; nx = nd_next(t)) { t = nx; ++len; }
             nd_next(t) = ev;
+            prev = t;
           }
           flags(i) &= ~FL_SUCCESS;
+          cnt_tail = ev;
+          cnt_len = len;
           process(i, se);
+          cnt_tail = -1;
           if (take_returned(i)) push_ret(se);
           bool removed = false;
           if (flags(i) & FL_CHANGED) { keep = false; removed = true; }
           if (!(flags(i) & FL_SUCCESS)) {
-            // StateEvent.removeLastEvent:224-236
-            int a = slot(se, i);
-            if (a >= 0) {
-              bool done = false;
-              while (nd_next(a) >= 0) {
-                if (nd_next(nd_next(a)) < 0) { nd_next(a) = -1; done = true; break; }
-                a = nd_next(a);
-              }
-              if (!done) slot(se, i) = -1;
-            }
+            // StateEvent.removeLastEvent:224-236. The filters failed, so nothing ran between the
+            // append and here and ev is still the chain's last node: unlink it from prev
+            if (prev >= 0) nd_next(prev) = -1;
+            else slot(se, i) = -1;
             if (q->type == Q_SEQUENCE) {
               if (removed) fail(GE_REFERENCE);  // IllegalStateException (second iterator.remove)
               keep = false;
