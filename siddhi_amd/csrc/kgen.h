@@ -468,7 +468,7 @@ struct Ctx {
     }
     return -1;
   }
-  KG_FN int new_state() {
+  KG_FN int new_state(bool blank = true) {  // blank = false: the caller writes every slot and ts
     int s = find_free_se();
     if (s < 0) {
       gc();
@@ -476,8 +476,10 @@ struct Ctx {
       if (s < 0) { fail(GE_CAPACITY); return -1; }
     }
     se_used() = (int64_t)((uint64_t)se_used() | (1ull << s));
-    for (int i = 0; i < nS(); ++i) slot(s, i) = -1;
-    se_ts(s) = -1;
+    if (blank) {
+      for (int i = 0; i < nS(); ++i) slot(s, i) = -1;
+      se_ts(s) = -1;
+    }
     return s;
   }
   KG_FN void pin(int se) {
@@ -487,7 +489,7 @@ struct Ctx {
   KG_FN void unpin() { --npin; }
   KG_FN int clone(int se) {  // StateEventCloner.copyStateEvent:46-58 (shallow)
     pin(se);
-    const int c = new_state();
+    const int c = new_state(false);
     unpin();
     if (c < 0) return -1;
     for (int i = 0; i < nS(); ++i) slot(c, i) = slot(se, i);
@@ -757,10 +759,10 @@ struct Ctx {
       if (S(s.partner).has_selector && s.this_last == s.partner) flags(s.partner) |= FL_RETURNED;
     }
   }
-  KG_FN void process(int i, int se) {
+  KG_FN void process(int i, int se, bool deferred) {  // deferred: slot i holds VNODE
     flags(i) &= ~FL_CHANGED;
     if (!filters_pass(i, se)) return;
-    if (slot(se, i) == VNODE) {  // the filters passed: copy the current event now
+    if (deferred) {  // the filters passed: copy the current event now
       slot(se, i) = -1;
       const int ev = copy_event(se);
       if (ev < 0) return;  // capacity (err is set; the push fails)
@@ -819,7 +821,7 @@ struct Ctx {
           flags(i) &= ~FL_SUCCESS;
           cnt_tail = ev;
           cnt_len = len;
-          process(i, se);
+          process(i, se, false);
           cnt_tail = -1;
           if (take_returned(i)) push_ret(se);
           bool removed = false;
@@ -845,7 +847,7 @@ struct Ctx {
         keep = false;
       } else {
         slot(se, i) = VNODE;  // copied into the pool by process() once the filters pass
-        process(i, se);
+        process(i, se, true);
         if (take_returned(i)) push_ret(se);
         if (flags(i) & FL_CHANGED) {
           keep = false;
