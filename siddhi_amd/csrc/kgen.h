@@ -365,7 +365,7 @@ struct Ctx {
   // pointers: an array indexed by a run-time value inside the struct would keep the whole Ctx in
   // scratch memory on the device (no SROA), turning every field read into a scratch load.
   // GC roots outside the lists: partials unlinked or not yet linked while they are worked on
-  int32_t* pins;  // [4]
+  int32_t* pins;  // [4] (stride hstride: LDS on the device)
   int32_t npin;
   int32_t* ret;   // [GMAXRET]
   int32_t n_ret;
@@ -447,7 +447,7 @@ struct Ctx {
       for (int k = 0; k < pn(i); ++k) mark_se(pl(i, k), sm, nm);
       for (int k = 0; k < nn(i); ++k) mark_se(nl(i, k), sm, nm);
     }
-    for (int k = 0; k < npin; ++k) mark_se(pins[k], sm, nm);
+    for (int k = 0; k < npin && k < 4; ++k) mark_se(pins[(int64_t)k * hstride], sm, nm);
     for (int k = 0; k < n_ret; ++k) mark_se(ret[k], sm, nm);
     se_used() = (int64_t)sm;
     for (int w = 0; w < lay.NU; ++w) nd_used(w) = (int64_t)nm[w];
@@ -483,7 +483,8 @@ struct Ctx {
     return s;
   }
   KG_FN void pin(int se) {
-    if (npin < 4) pins[npin] = se;
+    if (npin < 4) pins[(int64_t)npin * hstride] = se;
+    else fail(GE_CAPACITY);  // an unrecorded root could be swept: refuse rather than risk it
     ++npin;
   }
   KG_FN void unpin() { --npin; }

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   c.w32 = a32 + block * L.B32 * 64 + lane;
   c.w64 = a64 + block * L.B64 * 64 + lane;
   c.stride = 64;
-  // dynamic LDS (gen_lds_bytes): the current event's captured words (wave-uniform), then the hot
+  // dynamic LDS (sized in sdh_launch_gen): the current event's captured words (wave-uniform), the hot
   // words of the item (kgen.h Ctx::h32/h64), [word][lane] -- sized to the launch's largest shape so
   // LDS does not cap occupancy
   extern __shared__ int64_t gen_lds[];
@@ -117,10 +117,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   c.hstride = 64;
   c.hs = L.hot_s;
   c.load_hot();
-  int32_t pins[4];
   int32_t ret[kg::GMAXRET];
   c.ev_val = evv;
-  c.pins = pins;
+  c.pins = c.h32 + (int64_t)3 * L.hot_s * 64;  // [4][lane] after the hot words
   c.ret = ret;
   c.err = kg::GE_OK;
   c.npin = 0;
@@ -386,7 +385,7 @@ extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
   // 4 waves/SIMD (116 VGPRs, no spills): on C3, 5 (96 VGPRs + spills) is level and 6 / 8 are
   // 10-30 % slower
-  const size_t lds = (size_t)(sdh::kg::GMAXNA + (1 + L->hot_nu) * 64) * 8 + (size_t)3 * L->hot_s * 64 * 4;
+  const size_t lds = (size_t)(sdh::kg::GMAXNA + (1 + L->hot_nu) * 64) * 8 + (size_t)(3 * L->hot_s + 4) * 64 * 4;
   hipLaunchKernelGGL(sdh::nfa_gen_kernel<4>, dim3(L->n_items), dim3(64), lds, s, *L);
   return hipGetLastError();
 }
