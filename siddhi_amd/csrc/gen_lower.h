@@ -273,7 +273,11 @@ inline GQuery lower_gen(const LProgram& P, int qi, const Sizing& sz) {
   for (int i = 0; i < g.n_states; ++i)
     for (int f = 0; f < g.st[i].n_filt; ++f)
       g.max_depth = std::max(g.max_depth, code_depth(g, g.st[i].fb[f], g.st[i].fe[f]));
-  make_layout(g.lay, S, sz.R, sz.N, sz.LC, NA);
+  bool v32 = true;  // every captured attribute is 4 bytes or narrower
+  for (int s = 0; s < (int)P.stream_types.size() && s < GMAXSTREAM; ++s)
+    for (int j = 0; j < g.n_cap[s]; ++j)
+      if (g.cap_type[s][j] == T_LONG || g.cap_type[s][j] == T_DOUBLE) v32 = false;
+  make_layout(g.lay, S, sz.R, sz.N, sz.LC, NA, v32);
   return g;
 }
 

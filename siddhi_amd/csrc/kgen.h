@@ -79,6 +79,7 @@ struct GLayout {
   int32_t S, R, N, LC, NA, NU;     // states, StateEvents, nodes, list capacity, node attrs, node-mask words
   int32_t o_flags, o_pn, o_nn, o_plist, o_nlist, o_seslot, o_ndnext, o_ndnull, o_init, n32;
   int32_t o_seused, o_ndused, o_sets, o_ndseq, o_ndts, o_ndval, n64;
+  int32_t v32;  // node attribute words in the 32-bit arena (every captured type is 4 bytes or less)
 };
 
 struct GQuery {
@@ -402,7 +403,17 @@ struct Ctx {
   KG_FN int32_t& nd_null(int n) const { return i32(lay.o_ndnull + n); }
   KG_FN int64_t& nd_seq(int n) const { return i64(lay.o_ndseq + n); }
   KG_FN int64_t& nd_ts(int n) const { return i64(lay.o_ndts + n); }
-  KG_FN int64_t& nd_val(int n, int j) const { return i64(lay.o_ndval + n * lay.NA + j); }
+  // node attribute words: raw words of 4-byte-or-narrower types are stored as their low 32 bits
+  // and sign-extended back, which reproduces raw_word's value for every such column
+  KG_FN int64_t nd_val(int n, int j) const {
+    const int o = lay.o_ndval + n * lay.NA + j;
+    return lay.v32 ? (int64_t)i32(o) : i64(o);
+  }
+  KG_FN void set_nd_val(int n, int j, int64_t v) const {
+    const int o = lay.o_ndval + n * lay.NA + j;
+    if (lay.v32) i32(o) = (int32_t)v;
+    else i64(o) = v;
+  }
   KG_FN int64_t& se_used() const { return h64[0]; }
   KG_FN int64_t& nd_used(int w) const { return h64[(int64_t)(1 + w) * hstride]; }
   KG_FN void load_hot() {
@@ -513,7 +524,7 @@ struct Ctx {
     nd_next(n) = -1;
     nd_null(n) = (int32_t)ev_null;
     const int na = q->n_cap[stream];
-    for (int j = 0; j < na; ++j) nd_val(n, j) = ev_val[j];
+    for (int j = 0; j < na; ++j) set_nd_val(n, j, ev_val[j]);
     return n;
   }
 
@@ -897,8 +908,9 @@ struct Ctx {
 // ------------------------------------------------------------------------------------------
 // host-side layout of one query's arenas
 // ------------------------------------------------------------------------------------------
-inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA) {
+inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA, bool v32 = false) {
   L.S = S; L.R = R; L.N = N; L.LC = LC; L.NA = NA; L.NU = (N + 63) / 64;
+  L.v32 = v32 ? 1 : 0;
   int o = 0;
   L.o_flags = o; o += S;
   L.o_pn = o; o += S;
@@ -909,6 +921,7 @@ inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA) {
   L.o_ndnext = o; o += N;
   L.o_ndnull = o; o += N;
   L.o_init = o; o += 1;
+  if (v32) { L.o_ndval = o; o += N * NA; }
   L.n32 = o;
   o = 0;
   L.o_seused = o; o += 1;
@@ -916,7 +929,7 @@ inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA) {
   L.o_sets = o; o += R;
   L.o_ndseq = o; o += N;
   L.o_ndts = o; o += N;
-  L.o_ndval = o; o += N * NA;
+  if (!v32) { L.o_ndval = o; o += N * NA; }
   L.n64 = o;
 }
 

@@ -300,6 +300,7 @@ void kg_prof_hit(const GLayout& L, int is64, int off) {
     const int b[] = {L.o_flags, L.o_pn, L.o_nn, L.o_plist, L.o_nlist, L.o_seslot, L.o_ndnext, L.o_ndnull, L.o_init};
     r = 0;
     for (int k = 0; k < 9; ++k) if (off >= b[k]) r = k;
+    if (L.v32 && off >= L.o_ndval) r = 14;
   } else {
     const int b[] = {L.o_seused, L.o_ndused, L.o_sets, L.o_ndseq, L.o_ndts, L.o_ndval};
     r = 9;
