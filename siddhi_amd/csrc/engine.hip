@@ -1244,7 +1244,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     L.out_next = e->g_out_next.p;
     L.err = e->d_err.p;
     L.rec_count = e->g_nrec.p;
-    L.write_records = write;
+    L.write_records = write ? 1 : 2;
     if (gs.partition < 0) {
       // groups reading this stream: windowed sequences go to K_seq, the rest to K_gen
       std::vector<int32_t> seq_rows, gen_groups;
@@ -1277,7 +1277,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
         Q.b = B;
         Q.tail = e->seq_tail[stream].p;
         Q.tail_len = e->seq_tail_len[stream];
-        Q.write_records = write;
+        Q.write_records = write ? 1 : 2;
         Q.out = e->g_out.p;
         Q.out_cap = e->g_out_cap;
         Q.out_next = e->g_out_next.p;

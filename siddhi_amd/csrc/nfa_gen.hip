@@ -43,14 +43,19 @@ __device__ __forceinline__ int64_t raw_word(const StreamBatch& b, int attr, int6
 
 // match output: one flat word buffer; each record is reserved with an atomic add of its length
 // (the backend's atomic optimizer folds a wave's same-address adds into one atomic + a scan)
+// ring (write_records == 2, SDH_FLAG_DEVICE_MATCHES): every record is still written, at its
+// offset modulo the buffer less a one-record margin, because nobody reads it back
+constexpr int64_t RING_MARGIN = 8192;  // words; > the longest record
 struct LaneOut {
   int64_t* out;
   int64_t cap;
   unsigned long long* next;
+  bool ring;
   bool over = false;
   __device__ void close() {}
   __device__ int64_t* reserve(int words) {
     const unsigned long long o = atomicAdd(next, (unsigned long long)words);
+    if (ring) return out + (int64_t)(o % (unsigned long long)(cap - RING_MARGIN));
     if ((int64_t)(o + words) > cap) {
       over = true;
       return nullptr;
@@ -130,7 +135,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     c.init_instance();
     c.i32(q->lay.o_init) = 1;
   }
-  LaneOut o{L.out, L.out_cap, L.out_next};
+  LaneOut o{L.out, L.out_cap, L.out_next, L.write_records == 2};
   const int S = q->n_states;
   const int ncap = q->n_cap[c.stream];
   unsigned long long nrec = 0;
@@ -222,7 +227,7 @@ __global__ __launch_bounds__(64) void nfa_seq_kernel(SeqLaunch L) {
   const int64_t s_end = W - S + 1;
   int64_t lo = s_begin + (int64_t)chunk * L.chunk_len;
   int64_t hi = lo + L.chunk_len < s_end ? lo + L.chunk_len : s_end;
-  LaneOut o{L.out, L.out_cap, L.out_next};
+  LaneOut o{L.out, L.out_cap, L.out_next, L.write_records == 2};
   unsigned long long nrec = 0;
   for (int64_t t0 = lo; t0 < hi; t0 += SEQ_TILE) {
     const int cnt = hi - t0 < SEQ_TILE ? (int)(hi - t0) : SEQ_TILE;

@@ -233,7 +233,7 @@ struct GenLaunch {
   int32_t n_items;
   int32_t* err;               // [0] instance capacity, [1] reference would throw, [2] output overflow
   unsigned long long* rec_count;  // matches emitted (records), counted even when not written
-  int32_t write_records;      // 0: count only (device-resident benchmarking mode)
+  int32_t write_records;      // 1: write; 2: write into a ring nobody reads (SDH_FLAG_DEVICE_MATCHES); 0: count only
   // event chunks of an unpartitioned set (kg::seq_lookback): item = chunk * groups + g; chunk 0
   // continues the persistent arena, chunk c > 0 starts a fresh instance in scratch block
   // (c-1) * groups + g and replays the template's look-back events before emitting
