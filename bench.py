@@ -1,18 +1,27 @@
 #!/usr/bin/env python3
-"""NFA-step throughput benchmark (BASELINE.json metric: events/s x active patterns).
+"""NFA-step throughput benchmark (BASELINE.json metric: events/s x active patterns, at 10K patterns).
 
-Workload (BASELINE.json configs[1]): P = 1,000 concurrent 2-state patterns
+Workload (default; BASELINE.json configs[1] at the metric's 10K patterns, SURVEY §8(d) C2 family):
+P = 10,000 concurrent 2-state patterns per GPU
     every e1=StockStream[price > T_p] -> e2=StockStream[price > e1.price] within W_p
-over the seeded synthetic StockStream (20 B/event SoA), one MI355X per rank. One step = one
-NFA-step pass (one sdh_engine_push) over a batch of B events already resident in HBM; the
-matches it produces stay in HBM (per-wave output segments, counted on the host).
+over the seeded synthetic StockStream (20 B/event SoA), generated on the device and resident in HBM
+before the timed region. One step = one NFA-step pass (one sdh_engine_push) over a batch of B = 8M
+events; every match record is written to HBM (SDH_FLAG_DEVICE_MATCHES: counted, not polled).
+`--workload c3 | c4` runs the count/logical partitioned family or one GPU's shard of the fraud
+sequences instead.
 
-Multi-GPU (torchrun, one process per GPU): weak scaling by pattern set -- every rank runs its
-own P patterns (rank r uses patterns r*P .. r*P+P-1 of the family) over the same event stream;
-there is no data-path collective. Timing: barrier + device sync on both sides of the K timed
-steps, max over ranks.
+Match expansion (`expansion` in the JSON line): a second engine in normal mode runs pushes of a
+smaller batch followed by sdh_engine_poll_device -- the device R18 sort and the gather of the ABI
+tuples (query, key, ts, off, words) in HBM -- and times both.
+
+Multi-GPU (torchrun, one process per GPU): weak scaling by pattern set -- rank r runs patterns
+r*P .. r*P+P-1 of the family. Rank 0 generates each batch and broadcasts it over RCCL (the event
+broadcast of SURVEY §8(e)) inside the timed region; match counts are all-reduced. Timing: barrier +
+device sync on both sides of the K timed steps, max over ranks.
 """
 import argparse
+import glob
+import hashlib
 import json
 import os
 import sys
@@ -23,34 +32,70 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
+DEFAULTS = {  # workload -> (patterns per GPU, events per step, keys)
+    "c2": (10000, 1 << 23, 100),
+    "c3": (1000, 1 << 20, 10000),
+    "c4": (1250, 1 << 20, 100_000),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2",
-                    help="c2: BASELINE configs[1] (headline); c3: configs[2] (count/logical, partitioned); "
-                         "c4: configs[3] (fraud-rule sequences, one GPU's pattern-set shard)")
-    ap.add_argument("--keys", type=int, default=10000, help="C3 partition keys (symbols)")
-    ap.add_argument("--patterns", type=int, default=0,
-                    help="patterns per GPU (default: 1000; c4: 1250 = 10K sequences / 8 GPUs)")
-    ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--workload", choices=list(DEFAULTS), default="c2",
+                    help="c2: BASELINE configs[1] at 10K patterns (headline); c3: configs[2] (count/logical, "
+                         "partitioned); c4: configs[3] (fraud-rule sequences, one GPU's pattern-set shard)")
+    ap.add_argument("--keys", type=int, default=0, help="partition keys / symbols (default per workload)")
+    ap.add_argument("--patterns", type=int, default=0, help="patterns per GPU (default per workload)")
+    ap.add_argument("--batch", type=int, default=0, help="events per step (default per workload)")
     ap.add_argument("--partials", type=int, default=128)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget")
+    ap.add_argument("--expansion-batch", type=int, default=1 << 16)
+    ap.add_argument("--no-expansion", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
 
-def c2_app_for_rank(rank, P):
-    from siddhi_amd.workloads import STOCK_STREAM, c2_threshold_text, c2_within_sec
-    qs = [STOCK_STREAM]
-    for k in range(P):
-        p = rank * P + k
-        qs.append(f"@info(name='p{p}') from every e1=StockStream[price > {c2_threshold_text(p)}] -> "
-                  f"e2=StockStream[price > e1.price] within {c2_within_sec(p)} sec "
-                  f"select e1.price as p1, e2.price as p2 insert into OutStream;")
-    return " ".join(qs)
+def app_source(workload, P, first):
+    from siddhi_amd.workloads import c2_app, c3_app, c4_app
+    return {"c2": c2_app, "c3": c3_app, "c4": c4_app}[workload](P, first=first)
+
+
+def make_engine(workload, P, first, K, device, flags, partials):
+    from siddhi_amd import ql
+    from siddhi_amd.engine import HipEngine
+    from siddhi_amd.planner import plan
+    blob = plan(ql.parse(app_source(workload, P, first))).serialize()
+    if workload == "c4":
+        # a sequence instance holds at most one partial per state (R8): small pools
+        return HipEngine(blob, device=device, flags=flags, gen_pool_states=8, gen_pool_nodes=32, gen_list_cap=8)
+    if workload == "c3":
+        pools = [int(x) for x in os.environ.get("SDH_C3_POOLS", "32,128,32").split(",")]
+        return HipEngine(blob, device=device, flags=flags, gen_pool_states=pools[0], gen_pool_nodes=pools[1],
+                         gen_list_cap=pools[2], gen_max_keys=max(1024, 2 * K))
+    return HipEngine(blob, device=device, partials=partials, flags=flags)
+
+
+def gen_batch(workload, start, n, K, dev):
+    from siddhi_amd.workloads import stock_events_torch, txn_events_torch
+    gen = txn_events_torch if workload == "c4" else stock_events_torch
+    ts, a, b, c = gen(start, n, K, dev)
+    return [ts, a, b.view(__import__("torch").int32), c]
+
+
+def cpu_cores():
+    """Cores this job may use: the affinity mask, capped by a cgroup CPU quota (the GPU box gives one
+    GPU's job a share of the host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def _oracle_shard(workload, shard, P, n_symbols, budget_s):
@@ -59,10 +104,8 @@ def _oracle_shard(workload, shard, P, n_symbols, budget_s):
     Python decoding), and ctypes releases the GIL, so shards run in parallel."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from harness import App
-    from siddhi_amd.workloads import c3_app, c4_app, stock_events, txn_events
-    src = {"c2": lambda: c2_app_for_rank(shard, P), "c3": lambda: c3_app(P, first=shard * P),
-           "c4": lambda: c4_app(P, first=shard * P)}[workload]()
-    app = App(src)
+    from siddhi_amd.workloads import stock_events, txn_events
+    app = App(app_source(workload, P, shard * P))
     lib, h = app.engine.lib, app.engine.h
     gen = txn_events if workload == "c4" else stock_events
     done, start, n, matches = 0, 0, 20000, 0
@@ -76,18 +119,18 @@ def _oracle_shard(workload, shard, P, n_symbols, budget_s):
         lib.oracle_clear_matches(h)
         start += n
         done += n
-    return done, time.perf_counter() - t0, matches
+    live = lib.oracle_live_partials(h)
+    return done, time.perf_counter() - t0, matches, live
 
 
 def cpu_baseline(workload, n_symbols, budget_s):
     """Reference-semantics C++ CPU engine (the oracle) on the host cores, on a
     bounded sample of the same workload: one thread, then N threads sharded by pattern set
-    (N = the cores this job may use, at most 16), 32 patterns per thread."""
+    (N = the cores this job may use), 32 patterns per thread."""
     from concurrent.futures import ThreadPoolExecutor
     P = 32
-    d1, t1, _ = _oracle_shard(workload, 0, P, n_symbols, budget_s / 2)
-    ncores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    N = max(1, min(16, ncores))
+    d1, t1, m1, _ = _oracle_shard(workload, 0, P, n_symbols, budget_s / 2)
+    N = cpu_cores()
     with ThreadPoolExecutor(N) as ex:
         res = list(ex.map(lambda r: _oracle_shard(workload, r, P, n_symbols, budget_s / 2), range(N)))
     tn = max(r[1] for r in res)
@@ -101,31 +144,41 @@ def cpu_baseline(workload, n_symbols, budget_s):
     except OSError:
         pass
     return {"value": total / tn, "unit": "pattern-events/s", "cores": N, "kind": "port",
-            "single_thread_value": d1 * P / t1, "cpu_model": model,
-            "sample": f"{N} threads x {P} {workload.upper()} patterns (pattern-set shards) over consecutive "
-                      f"20K-event batches for {budget_s / 2:.0f} s; 1 thread: {P} patterns x {d1} events "
-                      "(oracle/liboracle.so, matches counted in the library)"}
+            "single_thread_value": d1 * P / t1, "matches_per_s": sum(r[2] for r in res) / tn,
+            "live_partials": int(sum(r[3] for r in res)), "host_cpus": os.cpu_count(), "cpu_model": model,
+            "sample": f"{N} threads x {P} {workload.upper()} patterns (pattern-set shards, patterns 0..{N * P - 1}) "
+                      f"over consecutive 20K-event batches for {budget_s / 2:.0f} s; 1 thread: {P} patterns x "
+                      f"{d1} events (oracle/liboracle.so, matches counted in the library)"}
 
 
-def profiled_traffic(kernel, patterns, batch):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC run of this same command
-    (profiles/*/counters.json next to a bench_line.json of the same patterns and batch;
-    FETCH_SIZE x2 gfx950 streaming-read correction + WRITE_SIZE, KiB)."""
-    import glob
-    best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "counters.json"))):
+def source_hash():
+    """Hash of the sources the kernels are built from (profiles are attached only at equal hashes)."""
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(ROOT, "siddhi_amd", "csrc", "*.h")) +
+                    glob.glob(os.path.join(ROOT, "siddhi_amd", "csrc", "*.hip")) +
+                    glob.glob(os.path.join(ROOT, "include", "*.h"))):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def profiled(kernel, workload, patterns, batch):
+    """The committed rocprofv3 profile of this same command at these sources (profiles/*/meta.json):
+    HBM bytes per launch of `kernel` (FETCH_SIZE x2 gfx950 streaming-read correction + WRITE_SIZE,
+    KiB) and the counter-derived issue / LDS figures."""
+    src = source_hash()
+    for meta_f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "meta.json"))):
         try:
-            d = json.load(open(f))
-            line = json.loads(open(os.path.join(os.path.dirname(f), "bench_line.json")).read().strip().splitlines()[-1])
-        except Exception:  # noqa: BLE001
+            meta = json.load(open(meta_f))
+        except (OSError, ValueError):
             continue
-        cfg = line.get("config", {})
-        if cfg.get("patterns_per_gpu") != patterns or cfg.get("events_per_step") != batch:
+        if (meta.get("source_hash") != src or meta.get("workload") != workload or
+                meta.get("patterns") != patterns or meta.get("batch") != batch):
             continue
-        for k, c in d.items():
-            if kernel in k and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-                best = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0, os.path.relpath(f, ROOT)
-    return best
+        k = meta.get("kernels", {}).get(kernel)
+        if k:
+            return k, os.path.relpath(os.path.dirname(meta_f), ROOT)
+    return None, None
 
 
 def main():
@@ -148,46 +201,29 @@ def main():
             dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    cdev = dev if backend == "nccl" else torch.device("cpu")  # where the timing reductions run
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # where the collectives run
 
-    from siddhi_amd import ql
-    from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES, HipEngine
-    from siddhi_amd.planner import plan
-    from siddhi_amd.workloads import stock_events
+    from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES
 
-    P = args.patterns or (1250 if args.workload == "c4" else 1000)
-    K = {"c2": 100, "c3": args.keys, "c4": 100_000}[args.workload]
-    if args.workload == "c4":
-        from siddhi_amd.workloads import c4_app
-        ir = plan(ql.parse(c4_app(P, first=rank * P)))
-        # a sequence instance holds at most one partial per state (R8): small pools, loud if exceeded
-        eng = HipEngine(ir.serialize(), device=local, flags=SDH_FLAG_DEVICE_MATCHES, gen_pool_states=8,
-                        gen_pool_nodes=32, gen_list_cap=8)
-    elif args.workload == "c2":
-        ir = plan(ql.parse(c2_app_for_rank(rank, P)))
-        eng = HipEngine(ir.serialize(), device=local, partials=args.partials, flags=SDH_FLAG_DEVICE_MATCHES)
-    else:
-        from siddhi_amd.workloads import c3_app
-        ir = plan(ql.parse(c3_app(P, first=rank * P)))
-        pools = [int(x) for x in os.environ.get("SDH_C3_POOLS", "32,128,32").split(",")]
-        eng = HipEngine(ir.serialize(), device=local, flags=SDH_FLAG_DEVICE_MATCHES, gen_pool_states=pools[0],
-                        gen_pool_nodes=pools[1], gen_list_cap=pools[2], gen_max_keys=max(1024, 2 * K))
+    P0, B0, K0 = DEFAULTS[args.workload]
+    P = args.patterns or P0
+    B = args.batch or B0
+    K = args.keys or K0
+    eng = make_engine(args.workload, P, rank * P, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials)
 
-    B = args.batch
     n_batches = args.warmup + args.steps
-    # synthetic batches resident in HBM before the timed region
-    batches = []
-    from siddhi_amd.workloads import txn_events
-    gen = txn_events if args.workload == "c4" else stock_events
-    for s in range(n_batches):
-        ts, sym, price, vol = gen(s * B, B, K)
-        batches.append((torch.from_numpy(ts).to(dev), torch.from_numpy(sym).to(dev),
-                        torch.from_numpy(price.view(np.int32)).to(dev), torch.from_numpy(vol).to(dev)))
+    # synthetic batches generated on the device before the timed region (rank 0's copy is the
+    # broadcast source in multi-GPU runs; the other ranks receive into their own buffers)
+    batches = [gen_batch(args.workload, s * B, B, K, dev) for s in range(n_batches)]
     torch.cuda.synchronize()
+    bcast = world > 1
 
     def step(i):
-        t, sy, pr, vo = batches[i]
-        eng.push_device(0, B, t.data_ptr(), [sy.data_ptr(), pr.data_ptr(), vo.data_ptr()])
+        cols = batches[i]
+        if bcast:
+            for t in cols:
+                dist.broadcast(t if backend == "nccl" else t.cpu(), src=0)
+        eng.push_device(0, B, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
 
     for i in range(args.warmup):
         step(i)
@@ -206,13 +242,15 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    live = eng.stats().live_partials
     if world > 1:
         t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        mt = torch.tensor([matches], device=cdev, dtype=torch.float64)
+        mt = torch.tensor([matches, live], device=cdev, dtype=torch.float64)
         dist.all_reduce(mt)
-        matches = int(mt.item())
+        matches, live = int(mt[0].item()), int(mt[1].item())
+    del batches
 
     total_pe = float(B) * args.steps * P * world
     value = total_pe / elapsed
@@ -221,7 +259,7 @@ def main():
     achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
     peak = 8000.0
     if args.workload == "c2":
-        wl = (f"C2: {P} concurrent 2-state filter+reference patterns "
+        wl = (f"C2 at the metric's 10K patterns: {P} concurrent 2-state filter+reference patterns per GPU "
               "(every e1[price>T_p] -> e2[price>e1.price] within W_p)")
         kernel = "nfa_ratchet_kernel"
     elif args.workload == "c3":
@@ -232,9 +270,10 @@ def main():
         wl = ("C4: fraud-rule sequences every e1=Txn[..], e2=Txn[..e1.amount*M], e3=Txn[..] within 1 min "
               f"(strict contiguity), {K} accounts, pattern-set shard {rank * P}..{rank * P + P - 1}")
         kernel = "nfa_seq_kernel"
-    traffic = profiled_traffic(kernel, P, B)
+    prof, prof_dir = profiled(kernel, args.workload, P, B)
+    traffic = prof.get("traffic_bytes") if prof else None
     result = {
-        "metric": "events/sec x active patterns (whole node); achieved HBM GB/s",
+        "metric": "events/sec x active patterns (whole node) at 10K patterns; achieved HBM GB/s",
         "value": value,
         "unit": "pattern-events/s",
         "n_gpus": world,
@@ -245,23 +284,90 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded splitmix64 StockStream, SURVEY §8(d))",
-        "config": {"workload": wl, "patterns_per_gpu": P, "events_per_step": B, "keys": K,
-                   "parallelism": f"pattern-set x{world}", "matches": matches},
+        "data": "synthetic (seeded splitmix64 StockStream / Txn stream, SURVEY §8(d)), generated in HBM",
+        "config": {"workload": wl, "patterns_per_gpu": P, "events_per_step": B, "timed_events": B * args.steps,
+                   "keys": K, "parallelism": f"pattern-set x{world}" + (" (RCCL event broadcast)" if bcast else ""),
+                   "matches": matches, "matches_per_s": matches / elapsed, "live_partials": live,
+                   "source_hash": source_hash()},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                     "frac": achieved / peak, "traffic": traffic[0] if traffic else None,
-                     "traffic_source": traffic[1] if traffic else None,
+                     "frac": achieved / peak, "traffic": traffic, "traffic_source": prof_dir,
                      "kernel": kernel, "kernel_ms": avg_ms,
                      # measured HBM rate (PMC traffic / live kernel time); below `achieved` when the
                      # device record is narrower than §8(d)'s 32-B match unit
-                     "traffic_gbps": (traffic[0] / (avg_ms * 1e-3) / 1e9) if traffic else None},
+                     "traffic_gbps": (traffic / (avg_ms * 1e-3) / 1e9) if traffic else None},
     }
+    if prof:
+        result["roofline"]["counters"] = {k: v for k, v in prof.items() if k != "traffic_bytes"}
+    if not args.no_expansion:
+        result["expansion"] = expansion(args, P, rank, K, local, dev, world, cdev, dist)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.workload, K, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def expansion(args, P, rank, K, local, dev, world, cdev, dist):
+    """Pushes of a smaller batch in normal mode, each followed by sdh_engine_poll_device (device R18
+    sort + gather of the ABI tuples in HBM): the NFA step with every match expanded. With N GPUs the
+    R18-sorted tuples are then gathered to rank 0 over RCCL and merged there (siddhi_amd/dist.py)."""
+    import torch
+    from siddhi_amd import dist as sdist
+    E = args.expansion_batch
+    eng = make_engine(args.workload, P, rank * P, K, local, 0, args.partials)
+    steps, warm = 4, 1
+    bs = [gen_batch(args.workload, s * E, E, K, dev) for s in range(steps + warm)]
+    log = sdist.StreamLog()
+    table = torch.arange(P * world, dtype=torch.int64)  # one stream, queries in definition order
+    torch.cuda.synchronize()
+    push_ms, gather_ms, matches, merged = 0.0, 0.0, 0, 0
+    for i, cols in enumerate(bs):
+        if i == warm:
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        t1 = time.perf_counter()
+        eng.push_device(0, E, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
+        log.push(0, E)
+        t2 = time.perf_counter()
+        if world > 1 and args.workload == "c2":
+            mc = sdist.columns_from_device(eng, dev)
+            mc["q"] += rank * P  # this rank's sub-app numbers its queries from 0
+            if cdev.type != "cuda":  # gloo rehearsal: the collectives take host tensors
+                mc = {k: v.to(cdev) for k, v in mc.items()}
+            t3 = time.perf_counter()
+            per_rank = sdist.gather_columns(mc)
+            if rank == 0:
+                out = sdist.merge_columns(None, per_rank, log, table=table, n_streams=1)
+                merged += int(out["q"].numel())
+            torch.cuda.synchronize()
+            n_local = int(mc["q"].numel())
+            t4 = time.perf_counter()
+        else:
+            n_local = eng.poll_device().n
+            t3 = t4 = time.perf_counter()
+        if i >= warm:
+            push_ms += (t2 - t1) * 1e3
+            gather_ms += (t4 - t3) * 1e3
+            matches += n_local
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el, matches], device=cdev, dtype=torch.float64)
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        mt = t[1:].clone()
+        dist.all_reduce(mt)
+        el, matches = float(t[0].item()), int(mt.item())
+    eng.close()
+    r = {"events_per_step": E, "steps": steps, "ms_per_step": el * 1e3 / steps,
+         "push_ms_per_step": push_ms / steps, "matches_per_step": matches / steps,
+         "pattern_events_per_s": E * steps * P * world / el, "matches_per_s": matches / el}
+    if world > 1 and args.workload == "c2":
+        r["rccl_gather_merge_ms_per_step"] = gather_ms / steps
+        r["merged_matches_per_step_rank0"] = merged / steps
+    return r
 
 
 if __name__ == "__main__":

@@ -14,13 +14,17 @@
  *   sdh_engine_poll     <- query/input/SingleProcessStreamReceiver.java:75-79 and
  *                          query/input/StateMultiProcessStreamReceiver.java:65-72 (hand-off of each
  *                          completed StateEvent to QuerySelector.process)
+ *   sdh_engine_poll_device  the same matches left in HBM (device consumers of the matches)
  *   sdh_engine_flush    <- (no reference equivalent: the reference is synchronous)
  *   sdh_engine_snapshot / sdh_engine_restore
  *                       <- state/StreamPreStateProcessor.java:352-367 (currentState/restoreState)
  *   sdh_last_error      <- Java exceptions (SiddhiAppCreationException, OperationNotSupportedException)
  *
  * Conventions: plain C, no exceptions cross the ABI, every call returns 0 on success and a
- * negative SDH_E* code on failure; sdh_last_error() then describes it. One producer thread per
+ * negative SDH_E* code on failure; sdh_last_error() then describes it. A push that fails after its
+ * kernels ran leaves the engine unusable (later calls fail with SDH_E_CAPACITY until
+ * sdh_engine_restore), except a K_gen match-output overflow: that push is applied, only its K_gen
+ * matches are lost, and the engine stays usable. One producer thread per
  * engine (the reference serialises receivers on a monitor, SingleProcessStreamReceiver.java:59).
  * There is NO CPU fallback: an engine that cannot run a query on the GPU fails at create time.
  */
@@ -38,15 +42,18 @@ extern "C" {
 #define SDH_E_INVALID (-1)     /* bad argument / malformed IR                               */
 #define SDH_E_UNSUPPORTED (-2) /* query shape not executable on the GPU path                */
 #define SDH_E_DEVICE (-3)      /* HIP runtime error                                          */
-#define SDH_E_CAPACITY (-4)    /* a partial-match table or match buffer overflowed           */
+#define SDH_E_CAPACITY (-4)    /* a partial-match table or match buffer overflowed (see below) */
 #define SDH_E_REFERENCE (-5)   /* the reference engine would throw here (e.g. CME)           */
 
 typedef struct sdh_engine sdh_engine;
 
 typedef struct sdh_config {
   int32_t device;            /* HIP device ordinal (one process per GPU)                      */
-  int32_t shard_rank;        /* pattern-set sharding: query q runs here iff q % shard_world   */
-  int32_t shard_world;       /*   == shard_rank (1/0 = unsharded)                             */
+  int32_t shard_rank;        /* multi-GPU: an unpartitioned query q runs here iff             */
+  int32_t shard_world;       /*   q % shard_world == shard_rank (1/0 = unsharded); partitioned */
+                             /*   queries run on every rank for the keys this rank owns:       */
+                             /*   |String.valueOf(key).hashCode() % shard_world| == shard_rank */
+                             /*   (PartitionedDistributionStrategy.java:98-109)                */
   int32_t partials_per_inst; /* live partial-match capacity per query instance (mult. of 64) */
   int64_t max_batch;         /* max events per push                                          */
   int64_t match_capacity;    /* max matches held between polls (0 = sized automatically)     */
@@ -89,10 +96,13 @@ typedef struct sdh_batch {
 } sdh_batch;
 
 /* Matches, in the reference's delivery order (per input event; per query; per state processor
- * in reverse registration order; per pending partial in insertion order -- SURVEY R18).
+ * in reverse registration order; per pending partial in insertion order -- SURVEY R18). The
+ * order is established on the device (a stable radix sort of the matches since the last poll).
  * Match i: query[i], key[i] (partition key id, -1 if unpartitioned), ts[i] (the StateEvent
  * timestamp); words[off[i] .. off[i+1]) holds, per state slot, a count c followed by c global
  * event sequence numbers (the slot's event chain when the selector would have run).
+ * seq[i] is the sequence number of the event whose processing completed the match (the R18 order
+ * is by that event first; a multi-GPU gather merges per-rank outputs on it).
  * Sequence numbers count pushed events from 0 across all streams in push order.
  * Buffers are owned by the engine and valid until the next push/poll/destroy. */
 typedef struct sdh_matches {
@@ -102,6 +112,7 @@ typedef struct sdh_matches {
   const int64_t* ts;
   const int64_t* off;
   const int64_t* words;
+  const int64_t* seq;
 } sdh_matches;
 
 typedef struct sdh_stats {
@@ -120,6 +131,9 @@ int sdh_engine_create(const void* ir_blob, size_t len, const sdh_config* cfg, sd
 int sdh_engine_push(sdh_engine* e, int32_t stream, const sdh_batch* batch);
 int sdh_engine_flush(sdh_engine* e);
 int sdh_engine_poll(sdh_engine* e, sdh_matches* out);
+/* As sdh_engine_poll, but every sdh_matches pointer is a HIP device pointer into engine-owned HBM
+ * (valid until the next push/poll/destroy): no copy to the host. */
+int sdh_engine_poll_device(sdh_engine* e, sdh_matches* out);
 /* Device-resident match count of the last push (no host copy of the matches). */
 int sdh_engine_pending_matches(sdh_engine* e, int64_t* n);
 int sdh_engine_stats(sdh_engine* e, sdh_stats* out);

@@ -1048,6 +1048,19 @@ int oracle_get_matches(const OracleEngine* e, int64_t* query, int64_t* key, int6
 
 void oracle_clear_matches(OracleEngine* e) { e->matches.clear(); }
 
+int64_t oracle_live_partials(const OracleEngine* e) {  // entries of every pending list
+  int64_t n = 0;
+  auto count = [&](const Runtime& r) {
+    for (const auto& p : r.pres) n += (int64_t)p.pending.size();
+  };
+  for (const auto& r : e->top)
+    if (r) count(*r);
+  for (const auto& pm : e->part_inst)
+    for (const auto& kv : pm)
+      for (const auto& r : kv.second) count(*r);
+  return n;
+}
+
 const char* oracle_error(const OracleEngine* e) { return e->err.c_str(); }
 
 void oracle_destroy(OracleEngine* e) { delete e; }

@@ -37,6 +37,8 @@ int64_t oracle_match_words(const OracleEngine* e);
 int oracle_get_matches(const OracleEngine* e, int64_t* query, int64_t* key, int64_t* ts,
                        int64_t* off, int64_t* words);
 void oracle_clear_matches(OracleEngine* e);
+/* Partial matches held in the pending lists of every pre-processor (after the last send). */
+int64_t oracle_live_partials(const OracleEngine* e);
 const char* oracle_error(const OracleEngine* e);
 void oracle_destroy(OracleEngine* e);
 

@@ -23,13 +23,15 @@
 #include "nfa_types.h"
 
 extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s);
-extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, int32_t new_tail_len, int64_t* tail, hipStream_t s);
+extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, hipStream_t s);
+extern "C" hipError_t sdh_seq_tail(const sdh::StreamBatch* b, int64_t* tail, int32_t tail_len, int32_t new_tail_len,
+                                   hipStream_t s);
 extern "C" hipError_t sdh_route_partition(const sdh::StreamBatch* B, int attr, int type, unsigned long long* tkey,
                                           int32_t* tid, int64_t table_mask, int32_t* n_keys, int64_t* key_of_id,
                                           int64_t key_cap, int64_t* key, uint32_t* kid, uint32_t* kid_sorted,
                                           int32_t* idx, int32_t* idx_sorted, uint32_t* uniq, int32_t* cnt,
                                           int32_t* off, int32_t* n_runs_dev, void* temp, size_t temp_bytes,
-                                          int32_t* err, hipStream_t s);
+                                          int32_t* err, int shard_rank, int shard_world, hipStream_t s);
 extern "C" size_t sdh_route_temp_bytes(int64_t n);
 
 extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaunch* L, int n_blocks,
@@ -40,14 +42,25 @@ extern "C" int sdh_ratchet_occupancy(int key_kind, int full, int nf, int ML);
 extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::StreamBatch* B, int attr, int conv,
                                                  int64_t n_tiles, uint64_t* tmax, uint64_t* tmin, uint8_t* thas,
                                                  hipStream_t s);
-extern "C" hipError_t sdh_launch_ratchet_decode(const int64_t* match, int blk_recs, int wide,
-                                                const int32_t* blk_count, const int32_t* blk_group,
-                                                const int64_t* dst_off, const sdh::RatchetGroup* groups,
-                                                const int64_t* ts, int64_t seq_base, int n_blocks, int64_t* out,
-                                                hipStream_t s);
-extern "C" hipError_t sdh_launch_compact(const int64_t* src, const int64_t* seg_off,
-                                         const int64_t* seg_count, const int64_t* dst_off,
-                                         int rec_words, int n_items, int64_t* dst, hipStream_t s);
+extern "C" hipError_t sdh_append_ratchet(const int64_t* match, int blk_recs, int wide, const int32_t* blk_count,
+                                         const int32_t* blk_group, const int64_t* dst_off,
+                                         const sdh::RatchetGroup* groups, const int64_t* ts, int64_t seq_base,
+                                         int64_t seq_ref, const int32_t* out_rank, int n_streams, int n_blocks,
+                                         sdh::MatchTable T, int64_t row0, int64_t word0, hipStream_t s);
+extern "C" hipError_t sdh_append_chain(const int64_t* src, const int64_t* seg_off, const int64_t* seg_count,
+                                       const int64_t* dst_off, int rec_words, int n_items, const int32_t* qinfo,
+                                       int64_t seq_ref, const int32_t* out_rank, int n_streams, sdh::MatchTable T,
+                                       int64_t row0, int64_t word0, hipStream_t s);
+extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t seq_ref,
+                                     const int32_t* out_rank, int n_streams, sdh::MatchTable T, int64_t row0,
+                                     int64_t word0, hipStream_t s);
+extern "C" size_t sdh_poll_temp_bytes(int64_t n);
+extern "C" hipError_t sdh_poll_sort(sdh::MatchTable T, int64_t n, int n_lo, int lo_bits, int hi_bits, uint64_t* kbuf,
+                                    int32_t* pbuf, void* temp, size_t temp_bytes, int64_t* oq, int64_t* okey,
+                                    int64_t* ots, int64_t* oseq, int64_t* olen, int64_t* ooff, int32_t** perm_out,
+                                    int64_t* total_words, hipStream_t s);
+extern "C" hipError_t sdh_poll_words(sdh::MatchTable T, const int32_t* perm, int64_t n, const int64_t* ooff,
+                                     int64_t* owords, hipStream_t s);
 
 using namespace sdh;
 
@@ -486,9 +499,51 @@ struct DevBuf {
     HIPCHK(hipMalloc(&p, cap * sizeof(T)));
     n = cap;
   }
+  // grow to at least `want` elements keeping the first `keep` (stream-ordered copy)
+  void grow_keep(size_t want, size_t keep, hipStream_t s) {
+    if (want <= n) return;
+    size_t cap = std::max(want, n * 2);
+    T* q = nullptr;
+    if (hipMalloc(&q, cap * sizeof(T)) != hipSuccess)
+      throw Error(SDH_E_CAPACITY, fmt("device memory exhausted growing a %zu-byte buffer", cap * sizeof(T)));
+    if (p && keep) HIPCHK(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (p) HIPCHK(hipFree(p));
+    p = q;
+    n = cap;
+  }
   ~DevBuf() {
     if (p) (void)hipFree(p);
   }
+};
+
+// host output buffer of a poll: pinned when the runtime grants it (faster D2H), else pageable
+template <class T>
+struct HostBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  bool pinned = false;
+  void ensure(size_t want) {
+    if (want <= n) return;
+    release();
+    const size_t cap = std::max(want, n * 2);
+    if (hipHostMalloc((void**)&p, cap * sizeof(T), hipHostMallocDefault) == hipSuccess) {
+      pinned = true;
+    } else {
+      (void)hipGetLastError();
+      p = (T*)malloc(cap * sizeof(T));
+      if (!p) throw Error(SDH_E_CAPACITY, "host memory exhausted for the poll output");
+      pinned = false;
+    }
+    n = cap;
+  }
+  void release() {
+    if (!p) return;
+    if (pinned) (void)hipHostFree(p);
+    else free(p);
+    p = nullptr;
+  }
+  ~HostBuf() { release(); }
 };
 
 
@@ -513,13 +568,27 @@ struct sdh_engine {
   int64_t seq = 0;
   // last launch
   DevBuf<WorkItem> d_work;
-  DevBuf<int64_t> d_seg_count, d_seg_off, d_dst_off, d_match, d_dense;
+  DevBuf<int64_t> d_seg_count, d_seg_off, d_dst_off, d_match;
   DevBuf<int32_t> d_err;
   std::vector<WorkItem> work;
   std::vector<int64_t> seg_count;
-  int64_t device_matches = 0;
-  bool device_unpolled = false;
-  std::vector<int64_t> backlog;      // host-side match records (rec_words int64 each)
+  int64_t device_matches = 0;        // K_chain matches of the last push
+  // device match table (matches.hip): every match since the last poll with its R18 sort keys
+  struct Table {
+    DevBuf<uint64_t> hi, lo[MAXLO];
+    DevBuf<int64_t> seq, q, key, ts, woff, wlen, words;
+    int64_t n = 0, nw = 0;           // rows / words used
+    int n_lo = 0;                    // tiebreak passes the rows need
+  } mt;
+  int64_t seq_ref = 0;               // global seq at the last poll (<= every trigger seq in mt)
+  DevBuf<int32_t> d_out_rank;        // [query][stream] R18 receiver rank
+  DevBuf<int32_t> d_qinfo;           // [query] (states, stream of the last state)
+  // poll scratch and outputs (device), host copies of the outputs
+  DevBuf<uint64_t> p_keys;
+  DevBuf<int32_t> p_perm;
+  DevBuf<uint8_t> p_temp;
+  DevBuf<int64_t> po_q, po_key, po_ts, po_seq, po_len, po_off, po_words;
+  HostBuf<int64_t> ho_q, ho_key, ho_ts, ho_seq, ho_off, ho_words;
   // ---- K_gen (general interpreter) ----
   kg::LProgram lp;                   // full IR (receivers, runtime tree, partitions)
   std::vector<int> out_rank;         // R18 rank per (query, stream)
@@ -543,6 +612,9 @@ struct sdh_engine {
     DevBuf<int64_t> a64;
     DevBuf<int32_t> s32;             // scratch arenas of event chunks 1.. (unpartitioned sets)
     DevBuf<int64_t> s64;
+    DevBuf<int32_t> bk32;            // the arenas before the current push (exact re-runs)
+    DevBuf<int64_t> bk64;
+    size_t bk_n32 = 0, bk_n64 = 0;
     // partition routing
     DevBuf<unsigned long long> tkey;
     DevBuf<int32_t> tid, n_keys;
@@ -558,9 +630,11 @@ struct sdh_engine {
   int64_t g_out_cap = 0;             // K_gen match record words per push
   DevBuf<unsigned long long> g_out_next;
   DevBuf<unsigned long long> g_nrec;
-  std::vector<int64_t> g_host;       // collected K_gen records (variable length)
-  int64_t g_host_n = 0;
-  int64_t g_dev_matches = 0;         // matches of the last push left on the device
+  DevBuf<int64_t> g_rec_off;         // word offset of each K_gen / K_seq record of the last push
+  DevBuf<unsigned long long> g_rec_next;
+  int64_t g_dev_matches = 0;         // K_gen / K_seq matches of the last push
+  int64_t g_used = 0;                // words of the last push's records in g_out (normal mode)
+  bool g_out_lost = false;           // the last push's records overflowed g_out (matches lost)
   // ---- K_ratchet groups ----
   std::vector<RatchetGroup> rg;
   std::vector<int> rcur;             // per group: buffer holding its deques
@@ -571,9 +645,7 @@ struct sdh_engine {
   std::vector<RatchetItem> ritems;
   DevBuf<int64_t> d_rmatch;
   DevBuf<int32_t> d_blk_count, d_blk_next, d_blk_group;
-  DevBuf<int64_t> d_rbts;            // ts column of the batch the unpolled records refer to
-  const int64_t* r_ts = nullptr;
-  int64_t r_seq_base = 0;
+  DevBuf<unsigned long long> d_rtotal;  // records written in ring mode (SDH_FLAG_DEVICE_MATCHES)
   int r_wide = 0;
   int64_t r_blocks = 0;              // capacity in blocks
   int r_blk_recs = 8192;
@@ -592,10 +664,9 @@ struct sdh_engine {
   std::vector<char> r_full_expiry;   // per stream: timestamps were seen out of order
   int64_t r_matches = 0;
   double r_kernel_ms = 0, r_kernel_bytes = 0;
-  // poll output
-  std::vector<int64_t> o_query, o_key, o_ts, o_off, o_words;
   sdh_stats stats{};
   std::string err;
+  std::string broken;                // set when a failed push left the state undefined
 };
 
 namespace {
@@ -621,19 +692,39 @@ void ensure_state(sdh_engine* e) {
   e->cur.assign(nq, 0);
 }
 
-void ratchet_collect(sdh_engine* e);
+// ---- device match table (matches.hip) ----
+sdh::MatchTable table_view(sdh_engine* e) {
+  sdh::MatchTable T{};
+  auto& t = e->mt;
+  T.hi = t.hi.p;
+  for (int k = 0; k < MAXLO; ++k) T.lo[k] = t.lo[k].p;
+  T.seq = t.seq.p;
+  T.q = t.q.p;
+  T.key = t.key.p;
+  T.ts = t.ts.p;
+  T.woff = t.woff.p;
+  T.wlen = t.wlen.p;
+  T.words = t.words.p;
+  return T;
+}
 
-void collect_device_matches(sdh_engine* e, bool discard = false) {
-  if (!e->device_unpolled) return;
-  e->device_unpolled = false;
-  if (discard) {
-    e->device_matches = 0;
-    e->r_matches = 0;
-    e->r_blocks_used = 0;
-    e->g_dev_matches = 0;
-    return;
-  }
-  ratchet_collect(e);
+// room for `rows` more rows and `words` more words (contents kept)
+void table_reserve(sdh_engine* e, int64_t rows, int64_t words) {
+  auto& t = e->mt;
+  const size_t want = (size_t)(t.n + rows), keep = (size_t)t.n;
+  t.hi.grow_keep(want, keep, e->stream);
+  for (int k = 0; k < MAXLO; ++k) t.lo[k].grow_keep(want, keep, e->stream);
+  t.seq.grow_keep(want, keep, e->stream);
+  t.q.grow_keep(want, keep, e->stream);
+  t.key.grow_keep(want, keep, e->stream);
+  t.ts.grow_keep(want, keep, e->stream);
+  t.woff.grow_keep(want, keep, e->stream);
+  t.wlen.grow_keep(want, keep, e->stream);
+  t.words.grow_keep((size_t)(t.nw + words), (size_t)t.nw, e->stream);
+}
+
+// the last push's K_chain matches (per work item output segments) -> table
+void append_chain(sdh_engine* e) {
   const int n_items = (int)e->work.size();
   if (e->device_matches == 0 || n_items == 0) return;
   std::vector<int64_t> seg_off(n_items), dst_off(n_items);
@@ -643,19 +734,96 @@ void collect_device_matches(sdh_engine* e, bool discard = false) {
     dst_off[i] = acc;
     acc += e->seg_count[i];
   }
+  table_reserve(e, acc, acc * 2 * MAXS);
   e->d_seg_off.ensure(n_items);
   e->d_dst_off.ensure(n_items);
-  e->d_dense.ensure((size_t)acc * e->rec_words);
   HIPCHK(hipMemcpyAsync(e->d_seg_off.p, seg_off.data(), n_items * 8, hipMemcpyHostToDevice, e->stream));
   HIPCHK(hipMemcpyAsync(e->d_dst_off.p, dst_off.data(), n_items * 8, hipMemcpyHostToDevice, e->stream));
-  HIPCHK(sdh_launch_compact(e->d_match.p, e->d_seg_off.p, e->d_seg_count.p, e->d_dst_off.p,
-                            e->rec_words, n_items, e->d_dense.p, e->stream));
-  const size_t base = e->backlog.size();
-  e->backlog.resize(base + (size_t)acc * e->rec_words);
-  HIPCHK(hipMemcpyAsync(e->backlog.data() + base, e->d_dense.p, (size_t)acc * e->rec_words * 8,
-                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(sdh_append_chain(e->d_match.p, e->d_seg_off.p, e->d_seg_count.p, e->d_dst_off.p, e->rec_words, n_items,
+                          e->d_qinfo.p, e->seq_ref, e->d_out_rank.p, (int)e->prog.stream_types.size(),
+                          table_view(e), e->mt.n, e->mt.nw, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
-  e->device_matches = 0;
+  e->mt.n += acc;
+  e->mt.nw += acc * 2 * MAXS;
+  e->mt.n_lo = std::max(e->mt.n_lo, e->rec_words - 3);
+}
+
+// the last push's K_ratchet match blocks -> table (ts_col: the batch's ts column, still valid)
+void append_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base) {
+  const int nb = e->r_blocks_used;
+  if (nb == 0 || e->r_matches == 0) return;
+  std::vector<int64_t> dst_off(nb);
+  int64_t acc = 0;
+  for (int i = 0; i < nb; ++i) {
+    dst_off[i] = acc;
+    acc += e->r_blk_count[i];
+  }
+  table_reserve(e, acc, acc * 4);
+  e->d_dst_off.ensure(nb);
+  HIPCHK(hipMemcpyAsync(e->d_dst_off.p, dst_off.data(), nb * 8, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(sdh_append_ratchet(e->d_rmatch.p, e->r_blk_recs, e->r_wide, e->d_blk_count.p, e->d_blk_group.p,
+                            e->d_dst_off.p, e->d_rg.p, ts_col, seq_base, e->seq_ref, e->d_out_rank.p,
+                            (int)e->prog.stream_types.size(), nb, table_view(e), e->mt.n, e->mt.nw, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  e->mt.n += acc;
+  e->mt.nw += acc * 4;
+  e->mt.n_lo = std::max(e->mt.n_lo, 1);
+}
+
+// the last push's K_gen / K_seq records -> table (the record words are copied whole)
+void append_gen(sdh_engine* e) {
+  const int64_t n_rec = e->g_dev_matches, used = e->g_used;
+  if (n_rec == 0) return;
+  table_reserve(e, n_rec, used);
+  HIPCHK(hipMemcpyAsync(e->mt.words.p + e->mt.nw, e->g_out.p, (size_t)used * 8, hipMemcpyDeviceToDevice, e->stream));
+  HIPCHK(sdh_append_gen(e->g_out.p, e->g_rec_off.p, n_rec, e->seq_ref, e->d_out_rank.p,
+                        (int)e->prog.stream_types.size(), table_view(e), e->mt.n, e->mt.nw, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  e->mt.n += n_rec;
+  e->mt.nw += used;
+  e->mt.n_lo = std::max(e->mt.n_lo, 1);
+}
+
+void table_clear(sdh_engine* e) {
+  e->mt.n = 0;
+  e->mt.nw = 0;
+  e->mt.n_lo = 0;
+  e->seq_ref = e->seq;
+}
+
+int bits_of(uint64_t v) {
+  int b = 0;
+  while (b < 64 && (v >> b) != 0) ++b;
+  return b;
+}
+
+// R18 sort of the table and gather of the ABI arrays in HBM (po_*); returns the match count
+int64_t table_sort(sdh_engine* e, int64_t* total_words) {
+  const int64_t n = e->mt.n;
+  *total_words = 0;
+  if (n == 0) return 0;
+  if (n >= INT32_MAX) throw Error(SDH_E_CAPACITY, "more than 2^31 matches between two polls");
+  e->p_keys.ensure((size_t)n * 2);
+  e->p_perm.ensure((size_t)n * 2);
+  const size_t tb = sdh_poll_temp_bytes(n);
+  e->p_temp.ensure(tb);
+  e->po_q.ensure(n);
+  e->po_key.ensure(n);
+  e->po_ts.ensure(n);
+  e->po_seq.ensure(n);
+  e->po_len.ensure(n + 1);
+  e->po_off.ensure(n + 1);
+  const int lo_bits = std::max(1, bits_of((uint64_t)std::max<int64_t>(e->seq, 1 << 16)));
+  const int hi_bits = bits_of((uint64_t)(e->seq - e->seq_ref)) + RANK_BITS;
+  int32_t* perm = nullptr;
+  HIPCHK(sdh_poll_sort(table_view(e), n, e->mt.n_lo, lo_bits, hi_bits, e->p_keys.p, e->p_perm.p, e->p_temp.p,
+                       e->p_temp.n, e->po_q.p, e->po_key.p, e->po_ts.p, e->po_seq.p, e->po_len.p, e->po_off.p, &perm,
+                       total_words, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  e->po_words.ensure((size_t)std::max<int64_t>(*total_words, 1));
+  HIPCHK(sdh_poll_words(table_view(e), perm, n, e->po_off.p, e->po_words.p, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return n;
 }
 
 void d2h_sync(sdh_engine* e, void* dst, const void* src, size_t bytes) {
@@ -859,11 +1027,13 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
   const int64_t n = B.n;
   int64_t lanes = 0;
   for (int g : gs) lanes += e->rg[g].n_lanes;
+  const bool ring = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) != 0;
   if (e->r_blocks == 0) {
-    const int64_t want = e->cfg.match_capacity > 0 ? e->cfg.match_capacity
-                                                   : std::max<int64_t>(1 << 20, n * lanes * 3 / 4);
+    int64_t want = e->cfg.match_capacity > 0 ? e->cfg.match_capacity : std::max<int64_t>(1 << 20, n * lanes * 3 / 4);
+    if (ring) want = std::min<int64_t>(want, (int64_t)1 << 30);  // 8 GiB of 8-B records, rewritten in a ring
     e->r_blocks = (want + e->r_blk_recs - 1) / e->r_blk_recs;
   }
+  e->d_rtotal.ensure(1);
   (void)t01;
   for (int attempt = 0; attempt < 8; ++attempt) {
     // out-of-order timestamps seen on this stream, or timestamps so extreme that `ts0 + within`
@@ -929,6 +1099,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     e->d_err.ensure(4);
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
     HIPCHK(hipMemsetAsync(e->d_blk_next.p, 0, 4, e->stream));
+    HIPCHK(hipMemsetAsync(e->d_rtotal.p, 0, 8, e->stream));
     // per-tile x summaries for the warm-up scans (rows of this stream's key specs)
     const int64_t n_tiles = (n + 63) / 64;
     const size_t n_rows = e->r_sum_specs.size();
@@ -965,6 +1136,8 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.blk_next = e->d_blk_next.p;
     L.n_blocks = (int32_t)std::min<int64_t>(e->r_blocks, INT32_MAX);
     L.blk_recs = e->r_blk_recs;
+    L.ring = ring ? 1 : 0;
+    L.rec_total = e->d_rtotal.p;
     L.err = e->d_err.p;
     HIPCHK(hipEventRecord(e->ev0, e->stream));
     for (int i0 = 0; i0 < n_items;) {
@@ -1005,21 +1178,21 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       e->r_blocks *= 2;
       continue;
     }
-    e->r_blocks_used = std::min<int>(used, (int)e->r_blocks);
-    e->r_blk_count.resize(e->r_blocks_used);
-    if (e->r_blocks_used)
-      HIPCHK(hipMemcpy(e->r_blk_count.data(), e->d_blk_count.p, e->r_blocks_used * 4, hipMemcpyDeviceToHost));
     for (int g : gs) e->rcur[g] ^= 1;
-    e->r_matches = ratchet_count_matches(e);
+    if (ring) {  // counted, not collected
+      unsigned long long tot = 0;
+      HIPCHK(hipMemcpy(&tot, e->d_rtotal.p, 8, hipMemcpyDeviceToHost));
+      e->r_blocks_used = 0;
+      e->r_matches = (int64_t)tot;
+    } else {
+      e->r_blocks_used = std::min<int>(used, (int)e->r_blocks);
+      e->r_blk_count.resize(e->r_blocks_used);
+      if (e->r_blocks_used)
+        HIPCHK(hipMemcpy(e->r_blk_count.data(), e->d_blk_count.p, e->r_blocks_used * 4, hipMemcpyDeviceToHost));
+      e->r_matches = ratchet_count_matches(e);
+    }
     e->r_kernel_ms = ms;
     e->r_wide = wide;
-    e->r_seq_base = B.seq_base;
-    e->r_ts = B.ts;
-    if (e->r_matches > 0 && B.ts != e->d_ts.p) {  // records outlive a caller-owned device batch
-      e->d_rbts.ensure(n);
-      HIPCHK(hipMemcpyAsync(e->d_rbts.p, B.ts, n * 8, hipMemcpyDeviceToDevice, e->stream));
-      e->r_ts = e->d_rbts.p;
-    }
     // algorithmic bytes: every group streams the batch's operand columns once
     // (ts + x-atom column + f0 columns; the warm-up re-reads are overhead, not counted), writes
     // 32 B per match (SURVEY §8(d)'s unit; the device record is 8 B, expanded at poll) and reads +
@@ -1041,41 +1214,6 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
   throw Error(SDH_E_CAPACITY, "ratchet launch did not converge");
 }
 
-// append the last ratchet launch's matches to the host backlog (decoded to (qid, ts, seq1, seq2))
-void ratchet_collect(sdh_engine* e) {
-  const int nb = e->r_blocks_used;
-  if (nb == 0 || e->r_matches == 0) return;
-  std::vector<int64_t> dst_off(nb);
-  int64_t acc = 0;
-  for (int i = 0; i < nb; ++i) {
-    dst_off[i] = acc;
-    acc += e->r_blk_count[i];
-  }
-  e->d_dst_off.ensure(nb);
-  e->d_dense.ensure((size_t)acc * 4);
-  HIPCHK(hipMemcpyAsync(e->d_dst_off.p, dst_off.data(), nb * 8, hipMemcpyHostToDevice, e->stream));
-  HIPCHK(sdh_launch_ratchet_decode(e->d_rmatch.p, e->r_blk_recs, e->r_wide, e->d_blk_count.p, e->d_blk_group.p,
-                                   e->d_dst_off.p, e->d_rg.p, e->r_ts, e->r_seq_base, nb, e->d_dense.p,
-                                   e->stream));
-  const int RW = e->rec_words;
-  const size_t base = e->backlog.size();
-  if (RW == 4) {
-    e->backlog.resize(base + (size_t)acc * 4);
-    HIPCHK(hipMemcpyAsync(e->backlog.data() + base, e->d_dense.p, (size_t)acc * 32, hipMemcpyDeviceToHost,
-                          e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-  } else {
-    std::vector<int64_t> rec((size_t)acc * 4);
-    HIPCHK(hipMemcpyAsync(rec.data(), e->d_dense.p, rec.size() * 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    e->backlog.resize(base + (size_t)acc * RW, 0);
-    for (int64_t i = 0; i < acc; ++i)
-      for (int w = 0; w < 4; ++w) e->backlog[base + i * RW + w] = rec[i * 4 + w];
-  }
-  e->r_matches = 0;
-  e->r_blocks_used = 0;
-}
-
 // ------------------------------------------------------------------------------------------
 // K_gen host side: lowering, instance arenas, partition routing, launch, match collection
 // ------------------------------------------------------------------------------------------
@@ -1089,6 +1227,7 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
     try {
       kg::GQuery g = kg::lower_gen(e->lp, qi, sz);
       g.rank = 0;
+      if (7 + g.lay.S + g.lay.N > GEN_RING_MARGIN) throw kg::LowerError("match record longer than the ring margin");
       gidx[qi] = (int)e->gq.size();
       e->gq.push_back(g);
       e->gB32 = std::max(e->gB32, g.lay.n32);
@@ -1206,26 +1345,19 @@ void gen_grow(sdh_engine* e, sdh_engine::GenSet& gs, int64_t keys) {
   gs.key_cap = cap;
 }
 
-int64_t gen_collect_device(sdh_engine* e);
 
 // one K_gen step for every set fed by `stream`
-void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out, double* bytes_out) {
-  *ms_out = 0;
-  *bytes_out = 0;
-  double bytes = 0;
+// One pass of every K_gen / K_seq launch of a push over `stream` (partition routing, arena growth,
+// kernels, the event-chunk copy-backs). Returns whether anything ran; *tail_new_len (>= 0) is the
+// stream's K_seq tail length once the pass is accepted.
+bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, double* bytes_out, int32_t* tail_new_len) {
+  const int64_t n = B.n;
   int64_t ev_bytes = 8;
   for (int a = 0; a < B.n_attr; ++a) ev_bytes += B.width[a];
-  if (e->gsets.empty()) return;
-  const int64_t n = B.n;
-  e->g_out_cap = std::max<int64_t>(e->g_out_cap, std::max<int64_t>(1 << 22, n * 64));
-  e->g_out.ensure((size_t)e->g_out_cap);
-  e->d_err.ensure(4);
-  HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
-  HIPCHK(hipMemsetAsync(e->g_out_next.p, 0, 8, e->stream));
-  HIPCHK(hipMemsetAsync(e->g_nrec.p, 0, 8, e->stream));
-  const bool write = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) == 0;
-  HIPCHK(hipEventRecord(e->ev0, e->stream));
+  double bytes = 0;
   bool any = false;
+  e->stats.last_gen_items = 0;
+  e->stats.last_seq_items = 0;
   for (auto& up : e->gsets) {
     auto& gs = *up;
     sdh::GenLaunch L{};
@@ -1244,6 +1376,9 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     L.out_next = e->g_out_next.p;
     L.err = e->d_err.p;
     L.rec_count = e->g_nrec.p;
+    L.rec_off = e->g_rec_off.p;
+    L.rec_cap = e->g_out_cap / 7 + 1;
+    L.rec_next = e->g_rec_next.p;
     L.write_records = write ? 1 : 2;
     if (gs.partition < 0) {
       // groups reading this stream: windowed sequences go to K_seq, the rest to K_gen
@@ -1282,6 +1417,9 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
         Q.out_cap = e->g_out_cap;
         Q.out_next = e->g_out_next.p;
         Q.rec_count = e->g_nrec.p;
+        Q.rec_off = e->g_rec_off.p;
+        Q.rec_cap = e->g_out_cap / 7 + 1;
+        Q.rec_next = e->g_rec_next.p;
         Q.err = e->d_err.p;
         const int64_t starts = n + Q.tail_len;
         const int64_t target = std::max<int64_t>(1, 8192 / (int64_t)seq_rows.size());
@@ -1289,9 +1427,8 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
         clen = (clen + 63) / 64 * 64;  // whole LDS tiles
         Q.chunk_len = clen;
         Q.n_chunks = (int32_t)((starts + clen - 1) / clen);
-        const int32_t new_len = (int32_t)std::min<int64_t>(SEQ_TMAX, Q.tail_len + n);
-        HIPCHK(sdh_launch_seq(&Q, new_len, e->seq_tail[stream].p, e->stream));
-        e->seq_tail_len[stream] = new_len;
+        HIPCHK(sdh_launch_seq(&Q, e->stream));
+        *tail_new_len = (int32_t)std::min<int64_t>(SEQ_TMAX, Q.tail_len + n);
         e->stats.last_seq_items += (int64_t)Q.n_glist * Q.n_chunks;
         any = true;
         bytes += (double)n * ev_bytes * seq_rows.size();  // every group stages the batch once
@@ -1364,7 +1501,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     HIPCHK(sdh_route_partition(&B, attr, type, gs.tkey.p, gs.tid.p, gs.tmask, gs.n_keys.p, gs.key_of_id.p,
                                gs.max_keys, e->r_key.p, e->r_kid.p, e->r_kid_s.p, e->r_idx.p, e->r_idx_s.p,
                                e->r_uniq.p, e->r_cnt.p, e->r_off.p, e->r_nruns.p, e->r_temp.p, e->r_temp.n,
-                               e->d_err.p + 3, e->stream));
+                               e->d_err.p + 3, e->cfg.shard_rank, e->cfg.shard_world, e->stream));
     int32_t hv[2];
     HIPCHK(hipMemcpyAsync(&hv[0], gs.n_keys.p, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&hv[1], e->r_nruns.p, 4, hipMemcpyDeviceToHost, e->stream));
@@ -1385,12 +1522,92 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     // routing (key column read, key/kid/idx written and sorted) + every group streaming its keys' events
     bytes += (double)n * (8 + 8 + 4 + 4 + 2 * (4 + 4) + 3 * 4) + (double)n * ev_bytes * gs.n_groups;
   }
-  HIPCHK(hipEventRecord(e->ev1, e->stream));
+  *bytes_out = bytes;
+  return any;
+}
+
+// arena state of every set a push over `stream` may touch, copied before the push so that a pass
+// whose match output overflowed can be undone and re-run exactly (normal mode only: in
+// SDH_FLAG_DEVICE_MATCHES mode records wrap in a ring and cannot overflow)
+bool gen_backup(sdh_engine* e) {
+  size_t total = 0;
+  for (auto& up : e->gsets) total += up->a32.n * 4 + up->a64.n * 8;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess || total > fr / 3) {
+    (void)hipGetLastError();
+    return false;
+  }
+  for (auto& up : e->gsets) {
+    auto& gs = *up;
+    gs.bk32.ensure(std::max<size_t>(1, gs.a32.n));
+    gs.bk64.ensure(std::max<size_t>(1, gs.a64.n));
+    gs.bk_n32 = gs.a32.n;
+    gs.bk_n64 = gs.a64.n;
+    if (gs.a32.n) HIPCHK(hipMemcpyAsync(gs.bk32.p, gs.a32.p, gs.a32.n * 4, hipMemcpyDeviceToDevice, e->stream));
+    if (gs.a64.n) HIPCHK(hipMemcpyAsync(gs.bk64.p, gs.a64.p, gs.a64.n * 8, hipMemcpyDeviceToDevice, e->stream));
+  }
+  return true;
+}
+
+void gen_restore_backup(sdh_engine* e) {
+  for (auto& up : e->gsets) {
+    auto& gs = *up;
+    // blocks added by arena growth during the undone pass are fresh again (zero: not yet seeded)
+    if (gs.a32.n > gs.bk_n32) HIPCHK(hipMemsetAsync(gs.a32.p + gs.bk_n32, 0, (gs.a32.n - gs.bk_n32) * 4, e->stream));
+    if (gs.a64.n > gs.bk_n64) HIPCHK(hipMemsetAsync(gs.a64.p + gs.bk_n64, 0, (gs.a64.n - gs.bk_n64) * 8, e->stream));
+    if (gs.bk_n32) HIPCHK(hipMemcpyAsync(gs.a32.p, gs.bk32.p, gs.bk_n32 * 4, hipMemcpyDeviceToDevice, e->stream));
+    if (gs.bk_n64) HIPCHK(hipMemcpyAsync(gs.a64.p, gs.bk64.p, gs.bk_n64 * 8, hipMemcpyDeviceToDevice, e->stream));
+  }
+}
+
+// one K_gen step for every set fed by `stream`
+void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out, double* bytes_out) {
+  *ms_out = 0;
+  *bytes_out = 0;
+  e->stats.last_gen_items = 0;
+  e->stats.last_seq_items = 0;
+  if (e->gsets.empty()) return;
+  const int64_t n = B.n;
+  e->g_out_cap = std::max<int64_t>(e->g_out_cap, std::max<int64_t>(1 << 22, n * 64));
+  static_assert((1 << 22) > 2 * GEN_RING_MARGIN, "ring capacity");
+  e->d_err.ensure(4);
+  e->g_rec_next.ensure(1);
+  const bool write = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) == 0;
+  const bool backed = write && gen_backup(e);
+  double bytes = 0;
+  int32_t tail_len = -1;
+  bool any = false;
   int32_t errs[4] = {0, 0, 0, 0};
-  HIPCHK(hipMemcpyAsync(errs, e->d_err.p, 16, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
+  unsigned long long nrec = 0, used = 0;
   float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+  for (int attempt = 0;; ++attempt) {
+    e->g_out.ensure((size_t)e->g_out_cap);
+    e->g_rec_off.ensure((size_t)(e->g_out_cap / 7 + 1));  // a record has at least 7 words
+    HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
+    HIPCHK(hipMemsetAsync(e->g_out_next.p, 0, 8, e->stream));
+    HIPCHK(hipMemsetAsync(e->g_nrec.p, 0, 8, e->stream));
+    HIPCHK(hipMemsetAsync(e->g_rec_next.p, 0, 8, e->stream));
+    HIPCHK(hipEventRecord(e->ev0, e->stream));
+    any = gen_pass(e, stream, B, write, &bytes, &tail_len);
+    HIPCHK(hipEventRecord(e->ev1, e->stream));
+    HIPCHK(hipMemcpyAsync(errs, e->d_err.p, 16, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&nrec, e->g_nrec.p, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&used, e->g_out_next.p, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    if (errs[2] && backed && attempt == 0 && !errs[0] && !errs[1] && !errs[3]) {
+      // the match output overflowed: undo the pass and re-run it with room for every record
+      // (out_next counts the words every record asked for)
+      gen_restore_backup(e);
+      while (e->g_out_cap < (int64_t)used + (int64_t)used / 4 + GEN_RING_MARGIN) e->g_out_cap *= 2;
+      continue;
+    }
+    break;
+  }
+  if (tail_len >= 0 && !errs[0] && !errs[1] && !errs[3]) {
+    HIPCHK(sdh_seq_tail(&B, e->seq_tail[stream].p, e->seq_tail_len[stream], tail_len, e->stream));
+    e->seq_tail_len[stream] = tail_len;
+  }
   *ms_out = ms;
   *bytes_out = bytes;
   if (errs[3]) throw Error(SDH_E_CAPACITY, "partition key table full");
@@ -1398,36 +1615,21 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
                                             "(ConcurrentModification / IllegalState / NullPointer)");
   if (errs[0]) throw Error(SDH_E_CAPACITY, "K_gen instance pool or list capacity exceeded "
                                            "(raise gen_pool_states / gen_pool_nodes / gen_list_cap)");
-  unsigned long long nrec = 0;
-  if (any) HIPCHK(hipMemcpy(&nrec, e->g_nrec.p, 8, hipMemcpyDeviceToHost));
-  if (errs[2]) {
-    e->g_out_cap *= 4;  // the next push gets a larger output buffer
-    throw Error(SDH_E_CAPACITY, "K_gen match output buffer overflow (matches of this push were lost)");
-  }
-  if (write && any) gen_collect_device(e);
-  e->g_dev_matches = write ? 0 : (int64_t)nrec;
+  if (!any) nrec = used = 0;
   *bytes_out += (double)nrec * 32.0;  // one (query, ts, seqs) record per match, as for K_ratchet
   e->stats.matches += (int64_t)nrec;
-}
-
-// copy the used output chunks back and append their records to g_host
-int64_t gen_collect_device(sdh_engine* e) {
-  unsigned long long used = 0;
-  HIPCHK(hipMemcpy(&used, e->g_out_next.p, 8, hipMemcpyDeviceToHost));
-  used = std::min<unsigned long long>(used, (unsigned long long)e->g_out_cap);
-  if (used == 0) return 0;
-  std::vector<int64_t> buf((size_t)used);
-  HIPCHK(hipMemcpy(buf.data(), e->g_out.p, buf.size() * 8, hipMemcpyDeviceToHost));
-  int64_t n = 0;
-  for (size_t w = 0; w < buf.size();) {
-    const int64_t len = buf[w];
-    if (len < 7 || w + len > buf.size()) throw Error(SDH_E_DEVICE, "corrupt K_gen match record");
-    e->g_host.insert(e->g_host.end(), buf.data() + w, buf.data() + w + len);
-    w += len;
-    ++n;
-    ++e->g_host_n;
+  e->g_dev_matches = (int64_t)nrec;
+  e->g_used = 0;
+  if (errs[2]) {
+    // the instances have consumed the batch (their arenas advance in place), so the push is
+    // committed and only the records that did not fit are lost; do_push reports it after the
+    // commit, and the next push gets a buffer that holds this one's records
+    while (e->g_out_cap < (int64_t)used + (int64_t)used / 2) e->g_out_cap *= 2;
+    e->g_out_lost = true;
+    e->g_dev_matches = 0;
+    return;
   }
-  return n;
+  if (write) e->g_used = (int64_t)used;
 }
 
 int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
@@ -1440,9 +1642,6 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     throw Error(SDH_E_INVALID, "batch larger than max_batch");
   if (b->n == 0) return SDH_OK;
   HIPCHK(hipSetDevice(e->dev));
-  // matches of the previous push that were not polled move to the host backlog (or are dropped
-  // under SDH_FLAG_DEVICE_MATCHES)
-  collect_device_matches(e, (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) != 0);
   StreamBatch B{};
   B.n = b->n;
   B.n_attr = na;
@@ -1490,34 +1689,48 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   }
   double ms = 0, bytes = 0;
   int64_t consumers = 0;
+  // the previous push's device-only matches (SDH_FLAG_DEVICE_MATCHES) are dropped here
   e->work.clear();
   e->device_matches = 0;
-  if (!qs.empty()) {
-    bool unordered = false;
-    launch(e, stream, B, t01, qs, true, &unordered);
-    bool chunked = false;
-    for (auto& w : e->work) chunked |= w.n_chunks > 1;
-    if (unordered && chunked) launch(e, stream, B, t01, qs, false, &unordered);  // exact fallback
-    for (int li : qs) e->cur[li] ^= 1;
-    ms += e->stats.last_kernel_ms;
-    bytes += e->stats.last_kernel_bytes;
-    consumers += (int64_t)qs.size();
+  e->r_blocks_used = 0;
+  e->r_matches = 0;
+  e->g_dev_matches = 0;
+  e->g_used = 0;
+  e->g_out_lost = false;
+  try {
+    if (!qs.empty()) {
+      bool unordered = false;
+      launch(e, stream, B, t01, qs, true, &unordered);
+      bool chunked = false;
+      for (auto& w : e->work) chunked |= w.n_chunks > 1;
+      if (unordered && chunked) launch(e, stream, B, t01, qs, false, &unordered);  // exact fallback
+      for (int li : qs) e->cur[li] ^= 1;
+      ms += e->stats.last_kernel_ms;
+      bytes += e->stats.last_kernel_bytes;
+      consumers += (int64_t)qs.size();
+    }
+    launch_ratchet(e, stream, B, t01);
+    for (const auto& g : e->rg)
+      if (g.stream == stream) consumers += g.n_lanes;
+    ms += e->r_kernel_ms;
+    bytes += e->r_kernel_bytes;
+    double gms = 0, gbytes = 0;
+    e->stats.last_gen_items = 0;
+    e->stats.last_seq_items = 0;
+    launch_gen(e, stream, B, &gms, &gbytes);
+    ms += gms;
+    bytes += gbytes;
+  } catch (const std::exception& ex) {
+    // kernels may already have advanced part of the state: the engine no longer mirrors the
+    // reference, so every later call fails (restore a snapshot or recreate)
+    e->prev_ts[stream] = t01[1];
+    e->seq += b->n;
+    e->broken = ex.what();
+    throw;
   }
-  launch_ratchet(e, stream, B, t01);
-  for (const auto& g : e->rg)
-    if (g.stream == stream) consumers += g.n_lanes;
-  ms += e->r_kernel_ms;
-  bytes += e->r_kernel_bytes;
-  double gms = 0, gbytes = 0;
-  e->stats.last_gen_items = 0;
-  e->stats.last_seq_items = 0;
-  launch_gen(e, stream, B, &gms, &gbytes);
-  ms += gms;
-  bytes += gbytes;
   for (const auto& g : e->gq)
     if (g.recv_n[stream] > 0) consumers += 1;
   if (consumers) {
-    e->device_unpolled = true;
     e->stats.pattern_events += b->n * consumers;
     e->stats.matches += e->device_matches + e->r_matches;
     e->stats.last_kernel_ms = ms;
@@ -1526,6 +1739,15 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   e->prev_ts[stream] = t01[1];
   e->seq += b->n;
   e->stats.events += b->n;
+  // the push is committed; its matches join the device table (R18-sorted at poll)
+  if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES)) {
+    append_chain(e);
+    append_ratchet(e, B.ts, B.seq_base);
+    append_gen(e);
+  }
+  if (e->g_out_lost)
+    throw Error(SDH_E_CAPACITY, "K_gen match output overflow: the push was applied but its K_gen matches were "
+                                "lost (the output buffer has grown for the next push)");
   return SDH_OK;
 }
 
@@ -1542,13 +1764,65 @@ int guard(sdh_engine* e, F f) {
   }
 }
 
+void check_usable(sdh_engine* e) {
+  if (!e->broken.empty())
+    throw Error(SDH_E_CAPACITY, "engine state is undefined after a failed push (" + e->broken +
+                                    "); restore a snapshot or create a new engine");
+}
+
+// R18-sorted matches since the last poll; host == false leaves them in HBM (sdh_engine_poll_device)
+int do_poll(sdh_engine* e, sdh_matches* out, bool host) {
+  check_usable(e);
+  int64_t tw = 0;
+  const int64_t n = table_sort(e, &tw);
+  if (host) {
+    e->ho_q.ensure(std::max<int64_t>(n, 1));
+    e->ho_key.ensure(std::max<int64_t>(n, 1));
+    e->ho_ts.ensure(std::max<int64_t>(n, 1));
+    e->ho_seq.ensure(std::max<int64_t>(n, 1));
+    e->ho_off.ensure(n + 1);
+    e->ho_words.ensure(std::max<int64_t>(tw, 1));
+    e->ho_off.p[0] = 0;
+    if (n) {
+      HIPCHK(hipMemcpyAsync(e->ho_q.p, e->po_q.p, n * 8, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipMemcpyAsync(e->ho_key.p, e->po_key.p, n * 8, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipMemcpyAsync(e->ho_ts.p, e->po_ts.p, n * 8, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipMemcpyAsync(e->ho_seq.p, e->po_seq.p, n * 8, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipMemcpyAsync(e->ho_off.p, e->po_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, e->stream));
+      if (tw) HIPCHK(hipMemcpyAsync(e->ho_words.p, e->po_words.p, tw * 8, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipStreamSynchronize(e->stream));
+    }
+    out->query = e->ho_q.p;
+    out->key = e->ho_key.p;
+    out->ts = e->ho_ts.p;
+    out->seq = e->ho_seq.p;
+    out->off = e->ho_off.p;
+    out->words = e->ho_words.p;
+  } else {
+    if (n == 0) {
+      e->po_off.ensure(1);
+      HIPCHK(hipMemsetAsync(e->po_off.p, 0, 8, e->stream));
+      HIPCHK(hipStreamSynchronize(e->stream));
+    }
+    out->query = e->po_q.p;
+    out->key = e->po_key.p;
+    out->ts = e->po_ts.p;
+    out->seq = e->po_seq.p;
+    out->off = e->po_off.p;
+    out->words = e->po_words.p;
+  }
+  out->n = n;
+  table_clear(e);
+  return SDH_OK;
+}
+
 thread_local std::string g_create_error;
 
 }  // namespace
 
 extern "C" {
 
-const char* sdh_version(void) { return "libsiddhi_hip 0.1 (gfx950, chain NFA kernel)"; }
+const char* sdh_version(void) { return "libsiddhi_hip 0.2 (gfx950: K_ratchet, K_chain, K_gen, K_seq; device R18 poll)"; }
 
 int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_engine** out) {
   if (!out) return SDH_E_INVALID;
@@ -1558,20 +1832,25 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     if (cfg) e->cfg = *cfg;
     if (e->cfg.shard_world <= 0) e->cfg.shard_world = 1;
     e->dev = e->cfg.device;
-    int ndev = 0;
-    HIPCHK(hipGetDeviceCount(&ndev));
-    if (ndev <= 0) throw Error(SDH_E_DEVICE, "no HIP device (the engine has no CPU fallback)");
-    HIPCHK(hipSetDevice(e->dev));
-    HIPCHK(hipDeviceGetAttribute(&e->n_cu, hipDeviceAttributeMultiprocessorCount, e->dev));
-    // tuning overrides for kernel experiments: K_ratchet LDS ring depth and waves per launch
-    if (const char* v = getenv("SDH_RATCHET_ML")) e->rML = std::max(4, atoi(v));
-    if (const char* v = getenv("SDH_RATCHET_WAVES")) e->r_waves = atof(v);
+    // the program is validated before any device call (a malformed blob is SDH_E_INVALID with or
+    // without a GPU)
     e->prog = read_ir(ir, len);
     try {
       e->lp = kg::read_program(ir, len);
     } catch (const kg::LowerError& ex) {
       throw Error(SDH_E_INVALID, ex.what());
     }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+      (void)hipGetLastError();
+      throw Error(SDH_E_DEVICE, "no HIP device (the engine has no CPU fallback)");
+    }
+    if (e->dev < 0 || e->dev >= ndev) throw Error(SDH_E_INVALID, fmt("device %d of %d", e->dev, ndev));
+    HIPCHK(hipSetDevice(e->dev));
+    HIPCHK(hipDeviceGetAttribute(&e->n_cu, hipDeviceAttributeMultiprocessorCount, e->dev));
+    // tuning overrides for kernel experiments: K_ratchet LDS ring depth and waves per launch
+    if (const char* v = getenv("SDH_RATCHET_ML")) e->rML = std::max(4, atoi(v));
+    if (const char* v = getenv("SDH_RATCHET_WAVES")) e->r_waves = atof(v);
     e->out_rank = kg::output_ranks(e->lp);
     // plan selection per query: K_ratchet (2-state threshold ratchet) > K_chain (stream-state
     // chains) > K_gen (everything else: count, logical, sequences, partitions, general predicates)
@@ -1580,10 +1859,10 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     const bool no_ratchet = (e->cfg.flags & SDH_FLAG_NO_RATCHET) != 0;
     const bool force_gen = (e->cfg.flags & SDH_FLAG_FORCE_GEN) != 0;
     for (int qi = 0; qi < (int)e->prog.q.size(); ++qi) {
-      // pattern-set sharding; a partition's queries stay together on one shard
-      const int pi = e->lp.q[qi].partition;
-      const int shard_key = pi < 0 ? qi : e->lp.parts[pi].queries[0];
-      if (shard_key % e->cfg.shard_world != e->cfg.shard_rank) continue;
+      // multi-GPU: unpartitioned queries are sharded by pattern set (query q on rank
+      // q % world); a partition's queries run on every rank, each rank owning the keys that
+      // key_shard maps to it (nfa_gen.hip: foreign keys' events are dropped at routing)
+      if (e->lp.q[qi].partition < 0 && qi % e->cfg.shard_world != e->cfg.shard_rank) continue;
       Lowered L = force_gen ? Lowered() : lower_query(e->prog, qi);
       if (!L.ok) {
         gen_qs.push_back(qi);
@@ -1611,6 +1890,20 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     ensure_state(e);
     ratchet_build(e, rplans);
     gen_build(e, gen_qs);
+    // R18 tables of the device match table: receiver rank per (query, stream), and per query its
+    // state count and the stream of its last state (the trigger of a chain-plan match)
+    const size_t nq_all = e->prog.q.size();
+    if (nq_all >= ((size_t)1 << RANK_BITS)) throw Error(SDH_E_UNSUPPORTED, "more than 2^20 queries");
+    e->d_out_rank.ensure(std::max<size_t>(1, e->out_rank.size()));
+    if (!e->out_rank.empty())
+      HIPCHK(hipMemcpy(e->d_out_rank.p, e->out_rank.data(), e->out_rank.size() * 4, hipMemcpyHostToDevice));
+    std::vector<int32_t> qinfo(std::max<size_t>(1, 2 * nq_all), 0);
+    for (size_t q = 0; q < nq_all; ++q) {
+      qinfo[2 * q] = (int32_t)e->prog.q[q].st.size();
+      qinfo[2 * q + 1] = e->prog.q[q].st.empty() ? 0 : e->prog.q[q].st.back().stream;
+    }
+    e->d_qinfo.ensure(qinfo.size());
+    HIPCHK(hipMemcpy(e->d_qinfo.p, qinfo.data(), qinfo.size() * 4, hipMemcpyHostToDevice));
     return SDH_OK;
   });
   if (rc != SDH_OK) {
@@ -1624,7 +1917,10 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
 
 int sdh_engine_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   if (!e) return SDH_E_INVALID;
-  return guard(e, [&]() { return do_push(e, stream, b); });
+  return guard(e, [&]() {
+    check_usable(e);
+    return do_push(e, stream, b);
+  });
 }
 
 int sdh_engine_flush(sdh_engine* e) {
@@ -1637,91 +1933,18 @@ int sdh_engine_flush(sdh_engine* e) {
 
 int sdh_engine_pending_matches(sdh_engine* e, int64_t* n) {
   if (!e || !n) return SDH_E_INVALID;
-  *n = (int64_t)(e->backlog.size() / e->rec_words) + e->g_host_n +
-       (e->device_unpolled ? e->device_matches + e->r_matches + e->g_dev_matches : 0);
+  *n = e->mt.n + ((e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) ? e->device_matches + e->r_matches + e->g_dev_matches : 0);
   return SDH_OK;
 }
 
 int sdh_engine_poll(sdh_engine* e, sdh_matches* out) {
   if (!e || !out) return SDH_E_INVALID;
-  return guard(e, [&]() {
-    collect_device_matches(e);
-    const int RW = e->rec_words;
-    const int NS = (int)e->lp.stream_types.size();
-    const int64_t* v = e->backlog.data();
-    const size_t nb = e->backlog.size() / RW;
-    // K_gen records: [len, qid, key, ts, seq, idx, S | stream << 16, (count, seqs...) x S]
-    std::vector<size_t> goff;
-    for (size_t w = 0; w < e->g_host.size(); w += (size_t)e->g_host[w]) goff.push_back(w);
-    const int64_t* gv = e->g_host.data();
-    const size_t n = nb + goff.size();
-    auto S_of = [&](size_t i) { return (int)e->prog.q[v[i * RW]].st.size(); };
-    // reference delivery order (R18): per triggering event; per junction subscriber / partition
-    // delivery (out_rank); per pending partial in insertion order -- for chain-family plans the
-    // earlier slots' events order a state's pending list, K_gen records carry their emission index
-    struct Key {
-      int64_t seq, rank;
-      size_t i;
-      bool gen;
-    };
-    std::vector<Key> keys(n);
-    for (size_t i = 0; i < nb; ++i) {
-      const int q = (int)v[i * RW];
-      const int S = S_of(i);
-      const int st = e->prog.q[q].st[S - 1].stream;
-      keys[i] = Key{v[i * RW + 2 + S - 1], e->out_rank[(size_t)q * NS + st], i, false};
-    }
-    for (size_t j = 0; j < goff.size(); ++j) {
-      const int64_t* r = gv + goff[j];
-      const int q = (int)r[1], st = (int)(r[6] >> 16);
-      keys[nb + j] = Key{r[4], e->out_rank[(size_t)q * NS + st], j, true};
-    }
-    std::stable_sort(keys.begin(), keys.end(), [&](const Key& a, const Key& b) {
-      if (a.seq != b.seq) return a.seq < b.seq;
-      if (a.rank != b.rank) return a.rank < b.rank;
-      if (a.gen != b.gen) return !a.gen;
-      if (a.gen) return gv[goff[a.i] + 5] < gv[goff[b.i] + 5];
-      for (int k = S_of(a.i) - 2; k >= 0; --k)
-        if (v[a.i * RW + 2 + k] != v[b.i * RW + 2 + k]) return v[a.i * RW + 2 + k] < v[b.i * RW + 2 + k];
-      return false;
-    });
-    e->o_query.resize(n);
-    e->o_key.resize(n);
-    e->o_ts.resize(n);
-    e->o_off.resize(n + 1);
-    e->o_words.clear();
-    for (size_t j = 0; j < n; ++j) {
-      const Key& k = keys[j];
-      e->o_off[j] = (int64_t)e->o_words.size();
-      if (!k.gen) {
-        const size_t i = k.i;
-        e->o_query[j] = v[i * RW];
-        e->o_key[j] = -1;
-        e->o_ts[j] = v[i * RW + 1];
-        for (int s2 = 0; s2 < S_of(i); ++s2) {
-          e->o_words.push_back(1);
-          e->o_words.push_back(v[i * RW + 2 + s2]);
-        }
-      } else {
-        const int64_t* r = gv + goff[k.i];
-        e->o_query[j] = r[1];
-        e->o_key[j] = r[2];
-        e->o_ts[j] = r[3];
-        e->o_words.insert(e->o_words.end(), r + 7, r + r[0]);
-      }
-    }
-    e->o_off[n] = (int64_t)e->o_words.size();
-    e->backlog.clear();
-    e->g_host.clear();
-    e->g_host_n = 0;
-    out->n = (int64_t)n;
-    out->query = e->o_query.data();
-    out->key = e->o_key.data();
-    out->ts = e->o_ts.data();
-    out->off = e->o_off.data();
-    out->words = e->o_words.data();
-    return SDH_OK;
-  });
+  return guard(e, [&]() { return do_poll(e, out, true); });
+}
+
+int sdh_engine_poll_device(sdh_engine* e, sdh_matches* out) {
+  if (!e || !out) return SDH_E_INVALID;
+  return guard(e, [&]() { return do_poll(e, out, false); });
 }
 
 int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
@@ -1749,14 +1972,18 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
   });
 }
 
-// snapshot: [magic][n_q][pcap][seq][n_streams][prev_ts...] then per query header + table
+// snapshot: [magic][version][n_q][pcap][gB32][gB64][seq][n_streams][prev_ts...] then per query
+// header + table, ratchet deques, K_gen arenas + key tables, K_seq tails
+constexpr int64_t SNAP_MAGIC = 0x5344485350415254LL;
+constexpr int64_t SNAP_VERSION = 2;
 int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
   if (!e || !blob || !len) return SDH_E_INVALID;
   return guard(e, [&]() {
     HIPCHK(hipStreamSynchronize(e->stream));
     const size_t nq = e->lq.size();
     const size_t tbl = (size_t)NF * e->pcap;
-    std::vector<int64_t> w{0x5344485350415254LL, (int64_t)nq, e->pcap, e->seq, (int64_t)e->prev_ts.size()};
+    std::vector<int64_t> w{SNAP_MAGIC, SNAP_VERSION, (int64_t)nq, e->pcap, e->gB32, e->gB64, e->seq,
+                           (int64_t)e->prev_ts.size()};
     w.insert(w.end(), e->prev_ts.begin(), e->prev_ts.end());
     for (size_t q = 0; q < nq; ++q) {
       InstHeader h;
@@ -1835,9 +2062,13 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
       if (i >= nw) throw Error(SDH_E_INVALID, "snapshot truncated");
       return w[i++];
     };
-    if (nx() != 0x5344485350415254LL) throw Error(SDH_E_INVALID, "bad snapshot magic");
+    if (nx() != SNAP_MAGIC) throw Error(SDH_E_INVALID, "bad snapshot magic");
+    if (nx() != SNAP_VERSION) throw Error(SDH_E_INVALID, "snapshot of another format version");
     const size_t nq = (size_t)nx();
     if (nq != e->lq.size() || nx() != e->pcap) throw Error(SDH_E_INVALID, "snapshot of a different program");
+    const int64_t b32 = nx(), b64 = nx();
+    if (b32 != e->gB32 || b64 != e->gB64)
+      throw Error(SDH_E_INVALID, "snapshot of a different K_gen arena layout (another build or pool sizing)");
     e->seq = nx();
     const size_t ns = (size_t)nx();
     if (ns != e->prev_ts.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
@@ -1887,6 +2118,8 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
         gen_grow(e, gs, key_cap);
         if (gs.key_cap != key_cap) throw Error(SDH_E_INVALID, "snapshot key capacity mismatch");
       }
+      const int64_t want_blocks = gs.partition < 0 ? gs.n_groups : gs.key_cap * gs.n_groups;
+      if (blocks != want_blocks) throw Error(SDH_E_INVALID, "snapshot arena size mismatch");
       get_dev(gs.a32.p, (size_t)blocks * e->gB32 * 64 * 4);
       get_dev(gs.a64.p, (size_t)blocks * e->gB64 * 64 * 8);
       if (gs.partition >= 0) {
@@ -1905,14 +2138,12 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
       e->seq_tail_len[st] = (int32_t)tl;
       get_dev(e->seq_tail[st].p, SEQ_TMAX * SEQ_TW * 8);
     }
-    e->backlog.clear();
-    e->g_host.clear();
-    e->g_host_n = 0;
     e->g_dev_matches = 0;
-    e->device_unpolled = false;
     e->device_matches = 0;
     e->r_matches = 0;
     e->r_blocks_used = 0;
+    table_clear(e);
+    e->broken.clear();
     return SDH_OK;
   });
 }

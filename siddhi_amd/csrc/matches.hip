@@ -1,0 +1,256 @@
+// matches.hip -- the device match table and the R18-ordered poll.
+//
+// The reference delivers every completed StateEvent to QuerySelector.process one at a time, in the
+// order R18 fixes: per input event (StreamJunction.java:179-181), per receiver / query, per state
+// processor in reverse registration order, per pending partial in insertion order
+// (StateMultiProcessStreamReceiver.java:53-74, SingleProcessStreamReceiver.java:57-80). The kernels
+// emit out of that order (lanes, chunks and keys run in parallel), so each push appends its matches
+// to a device table together with their R18 sort keys (nfa_types.h MatchTable), and a poll sorts the
+// table on the device -- stable LSD radix passes over the tiebreak keys, then the (trigger seq,
+// out_rank) key -- and gathers the ABI tuples of include/siddhi_hip.h (query, key, ts, off, words)
+// in HBM. sdh_engine_poll copies them to the host; sdh_engine_poll_device hands them out in place.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "nfa_types.h"
+
+namespace sdh {
+
+namespace {
+
+__device__ __forceinline__ uint64_t hi_key(int64_t seq, int64_t seq_ref, int rank) {
+  return ((uint64_t)(seq - seq_ref) << RANK_BITS) | (uint64_t)rank;
+}
+
+// K_ratchet blocks (nfa_ratchet.hip record format) -> table rows; one workgroup per block
+__global__ __launch_bounds__(256) void append_ratchet_kernel(
+    const int64_t* __restrict__ match, int blk_recs, int wide, const int32_t* __restrict__ blk_count,
+    const int32_t* __restrict__ blk_group, const int64_t* __restrict__ dst_off, const RatchetGroup* __restrict__ groups,
+    const int64_t* __restrict__ ts, int64_t seq_base, int64_t seq_ref, const int32_t* __restrict__ out_rank,
+    int n_streams, MatchTable T, int64_t row0, int64_t word0) {
+  const int b = blockIdx.x;
+  const int n = blk_count[b];
+  const RatchetGroup* G = groups + blk_group[b];
+  const uint2* R = reinterpret_cast<const uint2*>(match) + ((size_t)b * blk_recs << (wide ? 1 : 0));
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t off, ln, q1;
+    if (!wide) {
+      const uint2 r = R[i];
+      off = r.x & ((1u << 26) - 1);
+      ln = r.x >> 26;
+      q1 = r.y;
+    } else {
+      const uint4 r = reinterpret_cast<const uint4*>(R)[i];
+      off = r.x;
+      ln = r.y & 63;
+      q1 = r.z;
+    }
+    const int64_t s = seq_base + (int64_t)off;
+    const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
+    const int q = G->qid[ln];
+    const int64_t row = row0 + dst_off[b] + i;
+    const int64_t w = word0 + (row - row0) * 4;
+    T.hi[row] = hi_key(s, seq_ref, out_rank[(int64_t)q * n_streams + G->stream]);
+    T.lo[0][row] = (uint64_t)s1;
+    T.seq[row] = s;
+    T.q[row] = q;
+    T.key[row] = -1;
+    T.ts[row] = ts[off];
+    T.woff[row] = w;
+    T.wlen[row] = 4;
+    reinterpret_cast<longlong2*>(T.words + w)[0] = make_longlong2(1, s1);
+    reinterpret_cast<longlong2*>(T.words + w)[1] = make_longlong2(1, s);
+  }
+}
+
+// K_chain segments (records {qid, ts, seq_0 .. seq_{S-1}} of rec_words) -> table rows
+__global__ __launch_bounds__(256) void append_chain_kernel(
+    const int64_t* __restrict__ src, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ seg_count,
+    const int64_t* __restrict__ dst_off, int rec_words, const int32_t* __restrict__ qinfo, int64_t seq_ref,
+    const int32_t* __restrict__ out_rank, int n_streams, MatchTable T, int64_t row0, int64_t word0) {
+  const int item = blockIdx.x;
+  const int64_t n = seg_count[item];
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const int64_t* v = src + (seg_off[item] + i) * rec_words;
+    const int q = (int)v[0];
+    const int S = qinfo[2 * q], last_stream = qinfo[2 * q + 1];
+    const int64_t row = row0 + dst_off[item] + i;
+    const int64_t w = word0 + (row - row0) * 2 * MAXS;
+    T.hi[row] = hi_key(v[2 + S - 1], seq_ref, out_rank[(int64_t)q * n_streams + last_stream]);
+    T.seq[row] = v[2 + S - 1];
+#pragma unroll
+    for (int k = 0; k < MAXLO; ++k) T.lo[k][row] = k < S - 1 ? (uint64_t)v[2 + k] : 0ull;
+    T.q[row] = q;
+    T.key[row] = -1;
+    T.ts[row] = v[1];
+    T.woff[row] = w;
+    T.wlen[row] = 2 * S;
+    for (int k = 0; k < S; ++k) {
+      T.words[w + 2 * k] = 1;
+      T.words[w + 2 * k + 1] = v[2 + k];
+    }
+  }
+}
+
+// K_gen / K_seq records [len, qid, key, ts, seq, idx, S | stream << 16, (count, seqs...) x S] ->
+// table rows; the record words themselves are copied whole into the table's word area (word0 + o)
+__global__ __launch_bounds__(256) void append_gen_kernel(const int64_t* __restrict__ out,
+                                                         const int64_t* __restrict__ rec_off, int64_t n_rec,
+                                                         int64_t seq_ref, const int32_t* __restrict__ out_rank,
+                                                         int n_streams, MatchTable T, int64_t row0, int64_t word0) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_rec) return;
+  const int64_t o = rec_off[i];
+  const int64_t* r = out + o;
+  const int q = (int)r[1], stream = (int)(r[6] >> 16);
+  const int64_t row = row0 + i;
+  T.hi[row] = hi_key(r[4], seq_ref, out_rank[(int64_t)q * n_streams + stream]);
+  T.lo[0][row] = (uint64_t)r[5];
+  T.seq[row] = r[4];
+#pragma unroll
+  for (int k = 1; k < MAXLO; ++k) T.lo[k][row] = 0ull;
+  T.q[row] = q;
+  T.key[row] = r[2];
+  T.ts[row] = r[3];
+  T.woff[row] = word0 + o + 7;
+  T.wlen[row] = r[0] - 7;
+}
+
+__global__ void iota_kernel(int32_t* p, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = (int32_t)i;
+}
+
+__global__ void gather_key_kernel(const uint64_t* __restrict__ key, const int32_t* __restrict__ perm, int64_t n,
+                                  uint64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = key[perm[i]];
+}
+
+// sorted row i <- table row perm[i]; len[n] = 0 so that an exclusive scan of n+1 gives off[n]
+__global__ void gather_rows_kernel(MatchTable T, const int32_t* __restrict__ perm, int64_t n, int64_t* __restrict__ oq,
+                                   int64_t* __restrict__ okey, int64_t* __restrict__ ots, int64_t* __restrict__ oseq,
+                                   int64_t* __restrict__ olen) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  if (i == n) {
+    olen[n] = 0;
+    return;
+  }
+  const int32_t p = perm[i];
+  oq[i] = T.q[p];
+  okey[i] = T.key[p];
+  ots[i] = T.ts[p];
+  oseq[i] = T.seq[p];
+  olen[i] = T.wlen[p];
+}
+
+__global__ void gather_words_kernel(MatchTable T, const int32_t* __restrict__ perm, int64_t n,
+                                    const int64_t* __restrict__ ooff, int64_t* __restrict__ owords) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t p = perm[i];
+  const int64_t* s = T.words + T.woff[p];
+  int64_t* d = owords + ooff[i];
+  const int64_t len = T.wlen[p];
+  for (int64_t k = 0; k < len; ++k) d[k] = s[k];
+}
+
+inline unsigned grid(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace
+
+}  // namespace sdh
+
+using sdh::MatchTable;
+
+extern "C" hipError_t sdh_append_ratchet(const int64_t* match, int blk_recs, int wide, const int32_t* blk_count,
+                                         const int32_t* blk_group, const int64_t* dst_off,
+                                         const sdh::RatchetGroup* groups, const int64_t* ts, int64_t seq_base,
+                                         int64_t seq_ref, const int32_t* out_rank, int n_streams, int n_blocks,
+                                         MatchTable T, int64_t row0, int64_t word0, hipStream_t s) {
+  if (n_blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::append_ratchet_kernel, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, wide, blk_count,
+                     blk_group, dst_off, groups, ts, seq_base, seq_ref, out_rank, n_streams, T, row0, word0);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sdh_append_chain(const int64_t* src, const int64_t* seg_off, const int64_t* seg_count,
+                                       const int64_t* dst_off, int rec_words, int n_items, const int32_t* qinfo,
+                                       int64_t seq_ref, const int32_t* out_rank, int n_streams, MatchTable T,
+                                       int64_t row0, int64_t word0, hipStream_t s) {
+  if (n_items <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::append_chain_kernel, dim3(n_items), dim3(256), 0, s, src, seg_off, seg_count, dst_off,
+                     rec_words, qinfo, seq_ref, out_rank, n_streams, T, row0, word0);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t seq_ref,
+                                     const int32_t* out_rank, int n_streams, MatchTable T, int64_t row0,
+                                     int64_t word0, hipStream_t s) {
+  if (n_rec <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::append_gen_kernel, dim3(sdh::grid(n_rec, 256)), dim3(256), 0, s, out, rec_off, n_rec,
+                     seq_ref, out_rank, n_streams, T, row0, word0);
+  return hipGetLastError();
+}
+
+// Scratch the poll needs for n rows (bytes): hipcub temp storage.
+extern "C" size_t sdh_poll_temp_bytes(int64_t n) {
+  size_t a = 0, b = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs((void*)nullptr, a, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                           (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 64);
+  (void)hipcub::DeviceScan::ExclusiveSum((void*)nullptr, b, (int64_t*)nullptr, (int64_t*)nullptr, (int)(n + 1));
+  return (a > b ? a : b) + 256;
+}
+
+// R18 sort of the table's n rows and the gather of the ABI arrays except the words (device
+// pointers; off has n+1 entries). n_lo tiebreak passes; lo_bits / hi_bits bound the key bits that
+// vary. kbuf: 2 x n keys, pbuf: 2 x n permutation entries, olen: n + 1. On return *perm_out is the
+// sorted permutation (inside pbuf) and *total_words (host) receives off[n] once the stream has run.
+extern "C" hipError_t sdh_poll_sort(MatchTable T, int64_t n, int n_lo, int lo_bits, int hi_bits, uint64_t* kbuf,
+                                    int32_t* pbuf, void* temp, size_t temp_bytes, int64_t* oq, int64_t* okey,
+                                    int64_t* ots, int64_t* oseq, int64_t* olen, int64_t* ooff, int32_t** perm_out,
+                                    int64_t* total_words, hipStream_t s) {
+  using namespace sdh;
+  *total_words = 0;
+  *perm_out = pbuf;
+  if (n <= 0) return hipSuccess;
+  int32_t* perm = pbuf;
+  int32_t* perm2 = pbuf + n;
+  uint64_t* k1 = kbuf;
+  uint64_t* k2 = kbuf + n;
+  hipLaunchKernelGGL(iota_kernel, dim3(grid(n, 256)), dim3(256), 0, s, perm, n);
+  auto pass = [&](const uint64_t* key, int bits) -> hipError_t {
+    if (bits <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_key_kernel, dim3(grid(n, 256)), dim3(256), 0, s, key, perm, n, k1);
+    size_t tb = temp_bytes;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, tb, k1, k2, perm, perm2, (int)n, 0, bits, s);
+    if (e != hipSuccess) return e;
+    int32_t* t = perm;
+    perm = perm2;
+    perm2 = t;
+    return hipGetLastError();
+  };
+  for (int k = 0; k < n_lo && k < MAXLO; ++k) {
+    hipError_t e = pass(T.lo[k], lo_bits);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e = pass(T.hi, hi_bits);
+  if (e != hipSuccess) return e;
+  *perm_out = perm;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid(n + 1, 256)), dim3(256), 0, s, T, perm, n, oq, okey, ots, oseq, olen);
+  size_t tb = temp_bytes;
+  e = hipcub::DeviceScan::ExclusiveSum(temp, tb, olen, ooff, (int)(n + 1), s);
+  if (e != hipSuccess) return e;
+  e = hipMemcpyAsync(total_words, ooff + n, 8, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+// the words of the sorted rows (owords holds off[n] entries)
+extern "C" hipError_t sdh_poll_words(MatchTable T, const int32_t* perm, int64_t n, const int64_t* ooff,
+                                     int64_t* owords, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::gather_words_kernel, dim3(sdh::grid(n, 256)), dim3(256), 0, s, T, perm, n, ooff, owords);
+  return hipGetLastError();
+}

@@ -440,19 +440,6 @@ __global__ __launch_bounds__(256) void nfa_chain_kernel(ChainLaunch L) {
   }
 }
 
-// dense copy of the per-item output segments (for polling)
-__global__ void compact_matches_kernel(const int64_t* __restrict__ src, const int64_t* __restrict__ seg_off,
-                                       const int64_t* __restrict__ seg_count,
-                                       const int64_t* __restrict__ dst_off, int rec_words, int n_items,
-                                       int64_t* __restrict__ dst) {
-  const int item = blockIdx.x;
-  if (item >= n_items) return;
-  const int64_t n = seg_count[item] * rec_words;
-  const int64_t* s = src + seg_off[item] * rec_words;
-  int64_t* d = dst + dst_off[item] * rec_words;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) d[i] = s[i];
-}
-
 }  // namespace sdh
 
 template <int S>
@@ -478,13 +465,4 @@ extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaun
     case 4: return launch_s<4>(k, L, n_blocks, lds, s);
     default: return hipErrorInvalidValue;
   }
-}
-
-extern "C" hipError_t sdh_launch_compact(const int64_t* src, const int64_t* seg_off, const int64_t* seg_count,
-                                         const int64_t* dst_off, int rec_words, int n_items, int64_t* dst,
-                                         hipStream_t s) {
-  if (n_items == 0) return hipSuccess;
-  hipLaunchKernelGGL(sdh::compact_matches_kernel, dim3(n_items), dim3(256), 0, s, src, seg_off, seg_count,
-                     dst_off, rec_words, n_items, dst);
-  return hipGetLastError();
 }

@@ -45,12 +45,17 @@ __device__ __forceinline__ int64_t raw_word(const StreamBatch& b, int attr, int6
 // (the backend's atomic optimizer folds a wave's same-address adds into one atomic + a scan)
 // ring (write_records == 2, SDH_FLAG_DEVICE_MATCHES): every record is still written, at its
 // offset modulo the buffer less a one-record margin, because nobody reads it back
-constexpr int64_t RING_MARGIN = 8192;  // words; > the longest record
+constexpr int64_t RING_MARGIN = GEN_RING_MARGIN;  // words; > the longest record (checked by the host)
+// In normal mode each record's offset is also listed in rec_off (the device match table finds
+// records by it, matches.hip); a record fits only if its words and its index entry both do.
 struct LaneOut {
   int64_t* out;
   int64_t cap;
   unsigned long long* next;
   bool ring;
+  int64_t* rec_off;
+  int64_t rec_cap;
+  unsigned long long* rec_next;
   bool over = false;
   __device__ void close() {}
   __device__ int64_t* reserve(int words) {
@@ -60,6 +65,12 @@ struct LaneOut {
       over = true;
       return nullptr;
     }
+    const unsigned long long r = atomicAdd(rec_next, 1ull);
+    if ((int64_t)r >= rec_cap) {
+      over = true;
+      return nullptr;
+    }
+    rec_off[r] = (int64_t)o;
     return out + o;
   }
 };
@@ -135,7 +146,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     c.init_instance();
     c.i32(q->lay.o_init) = 1;
   }
-  LaneOut o{L.out, L.out_cap, L.out_next, L.write_records == 2};
+  LaneOut o{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
   const int S = q->n_states;
   const int ncap = q->n_cap[c.stream];
   unsigned long long nrec = 0;
@@ -227,7 +238,7 @@ __global__ __launch_bounds__(64) void nfa_seq_kernel(SeqLaunch L) {
   const int64_t s_end = W - S + 1;
   int64_t lo = s_begin + (int64_t)chunk * L.chunk_len;
   int64_t hi = lo + L.chunk_len < s_end ? lo + L.chunk_len : s_end;
-  LaneOut o{L.out, L.out_cap, L.out_next, L.write_records == 2};
+  LaneOut o{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
   unsigned long long nrec = 0;
   for (int64_t t0 = lo; t0 < hi; t0 += SEQ_TILE) {
     const int cnt = hi - t0 < SEQ_TILE ? (int)(hi - t0) : SEQ_TILE;
@@ -310,7 +321,43 @@ __global__ void seq_tail_kernel(StreamBatch b, int64_t* tail, int32_t tail_len, 
 }
 
 // ---- partition routing ----
-__global__ void gen_keys_kernel(StreamBatch b, int attr, int type, int64_t* key, uint32_t* kid) {
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Key-sharding rule of a multi-GPU engine: rank = |h % world| (Java int remainder), the reference's
+// PartitionedDistributionStrategy destination (PartitionedDistributionStrategy.java:98-109) with h
+// = String.valueOf(key).hashCode() for int / long / bool keys (the partition key IS that string,
+// ValuePartitionExecutor.java:34-40); float / double keys (Java's shortest-repr formatting) and
+// string dictionary ids hash their raw word instead. siddhi_amd/dist.py key_shard mirrors this.
+__device__ int key_shard(int64_t raw, int type, int world) {
+  int32_t h = 0;
+  if (type == kg::T_INT || type == kg::T_LONG) {
+    const int64_t v = type == kg::T_INT ? (int64_t)(int32_t)raw : raw;
+    uint64_t mag = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v;
+    char dig[20];
+    int nd = 0;
+    do {
+      dig[nd++] = (char)('0' + mag % 10);
+      mag /= 10;
+    } while (mag);
+    uint32_t u = v < 0 ? 45u : 0u;  // '-'
+    for (int i = nd - 1; i >= 0; --i) u = u * 31u + (uint32_t)dig[i];
+    h = (int32_t)u;
+  } else if (type == kg::T_BOOL) {
+    h = raw ? 3569038 : 97196323;  // "true".hashCode(), "false".hashCode()
+  } else {
+    h = (int32_t)(mix64((uint64_t)raw) >> 33);
+  }
+  const int32_t r = h % world;
+  return r < 0 ? -r : r;
+}
+
+// shard_world > 1: events whose key another rank owns are dropped here, like null keys
+__global__ void gen_keys_kernel(StreamBatch b, int attr, int type, int64_t* key, uint32_t* kid, int shard_rank,
+                                int shard_world) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= b.n) return;
   bool nl;
@@ -323,13 +370,8 @@ __global__ void gen_keys_kernel(StreamBatch b, int attr, int type, int64_t* key,
     if (d != d) raw = 0x7ff8000000000000LL;
   }
   key[e] = raw;
-  kid[e] = nl ? 0xFFFFFFFFu : 0u;  // 0 = valid, resolved by the lookup
-}
-
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
+  const bool foreign = shard_world > 1 && !nl && key_shard(raw, type, shard_world) != shard_rank;
+  kid[e] = (nl || foreign) ? 0xFFFFFFFFu : 0u;  // 0 = valid, resolved by the lookup
 }
 
 constexpr long long KEY_EMPTY = (long long)0x8000000000000000ull;  // INT64_MIN keys use slot `cap`
@@ -395,11 +437,16 @@ extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s) {
   return hipGetLastError();
 }
 
-extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, int32_t new_tail_len, int64_t* tail,
-                                     hipStream_t s) {
+extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, hipStream_t s) {
   if (L->n_glist > 0 && L->n_chunks > 0)
     hipLaunchKernelGGL(sdh::nfa_seq_kernel, dim3(L->n_glist * L->n_chunks), dim3(64), 0, s, *L);
-  hipLaunchKernelGGL(sdh::seq_tail_kernel, dim3(1), dim3(64), 0, s, L->b, tail, L->tail_len, new_tail_len);
+  return hipGetLastError();
+}
+
+// roll a stream's K_seq tail over batch b (after the push's K_seq launches have succeeded)
+extern "C" hipError_t sdh_seq_tail(const sdh::StreamBatch* b, int64_t* tail, int32_t tail_len, int32_t new_tail_len,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(sdh::seq_tail_kernel, dim3(1), dim3(64), 0, s, *b, tail, tail_len, new_tail_len);
   return hipGetLastError();
 }
 
@@ -411,11 +458,11 @@ extern "C" hipError_t sdh_route_partition(const sdh::StreamBatch* B, int attr, i
                                           int64_t key_cap, int64_t* key, uint32_t* kid, uint32_t* kid_sorted,
                                           int32_t* idx, int32_t* idx_sorted, uint32_t* uniq, int32_t* cnt,
                                           int32_t* off, int32_t* n_runs_dev, void* temp, size_t temp_bytes,
-                                          int32_t* err, hipStream_t s) {
+                                          int32_t* err, int shard_rank, int shard_world, hipStream_t s) {
   const int64_t n = B->n;
   const int T = 256;
   const int nb = (int)((n + T - 1) / T);
-  hipLaunchKernelGGL(sdh::gen_keys_kernel, dim3(nb), dim3(T), 0, s, *B, attr, type, key, kid);
+  hipLaunchKernelGGL(sdh::gen_keys_kernel, dim3(nb), dim3(T), 0, s, *B, attr, type, key, kid, shard_rank, shard_world);
   hipLaunchKernelGGL(sdh::gen_insert_kernel, dim3(nb), dim3(T), 0, s, n, key, kid, tkey, table_mask, err);
   const int64_t slots = table_mask + 2;
   hipLaunchKernelGGL(sdh::gen_assign_kernel, dim3((int)((slots + T - 1) / T)), dim3(T), 0, s, tkey, tid, slots,

@@ -705,6 +705,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   refresh_bottom();
 
   int blk = -1, fill = 0;
+  unsigned long long n_emit = 0;  // records of this wave (ring mode: the blocks wrap)
   uint2* wp = nullptr;  // next record of the wave's current output block
   const int rsh = L.wide ? 1 : 0;  // record size: 8 B << rsh
   int64_t prev_tile_ts = (W.c0 == 0) ? L.b.prev_ts : L.b.ts[W.c0 - 1];
@@ -719,6 +720,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
       int nb = 0;
       if (lane == 0) nb = atomicAdd(L.blk_next, 1);
       nb = __builtin_amdgcn_readfirstlane(nb);
+      if (L.ring) nb = (int)((uint32_t)nb % (uint32_t)L.n_blocks);
       if (nb >= L.n_blocks) {
         blk = -1;
         mover = true;
@@ -736,6 +738,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
     }
     wp += (size_t)c << rsh;
     fill += c;
+    n_emit += (unsigned long long)c;
   };
 
   // ---- forward NFA step over the events this item emits for. Fast path: straight-line per
@@ -873,6 +876,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   if (blk >= 0 && lane == 0) L.blk_count[blk] = fill;
   const uint64_t any_over = __ballot(overflow), any_unord = __ballot(unordered), any_aged = __ballot(aged);
   if (lane == 0) {
+    if (L.ring && n_emit) atomicAdd(L.rec_total, n_emit);
     if (any_over) atomicOr(&L.err[0], 1);
     if (any_unord) atomicOr(&L.err[1], 1);
     if (mover) atomicOr(&L.err[2], 1);
@@ -899,39 +903,6 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
     pick(L.st, ob)[W.g].n[lane] = n;
   }
   (void)W64;
-}
-
-// expand the match blocks of one launch to dense (qid, ts, seq1, seq2) rows: one workgroup per block
-__global__ __launch_bounds__(256) void ratchet_decode(const int64_t* __restrict__ match, int blk_recs, int wide,
-                                                      const int32_t* __restrict__ blk_count,
-                                                      const int32_t* __restrict__ blk_group,
-                                                      const int64_t* __restrict__ dst_off,
-                                                      const RatchetGroup* __restrict__ groups,
-                                                      const int64_t* __restrict__ ts, int64_t seq_base,
-                                                      int64_t* __restrict__ out) {
-  const int b = blockIdx.x;
-  const int n = blk_count[b];
-  const RatchetGroup* G = groups + blk_group[b];
-  const uint2* R = reinterpret_cast<const uint2*>(match) + ((size_t)b * blk_recs << (wide ? 1 : 0));
-  longlong2* O = reinterpret_cast<longlong2*>(out) + (size_t)dst_off[b] * 2;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    uint32_t off, ln, q1;
-    if (!wide) {
-      const uint2 r = R[i];
-      off = r.x & ((1u << 26) - 1);
-      ln = r.x >> 26;
-      q1 = r.y;
-    } else {
-      const uint4 r = reinterpret_cast<const uint4*>(R)[i];
-      off = r.x;
-      ln = r.y & 63;
-      q1 = r.z;
-    }
-    const int64_t s = seq_base + (int64_t)off;
-    const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
-    O[2 * (size_t)i] = make_longlong2(G->qid[ln], ts[off]);
-    O[2 * (size_t)i + 1] = make_longlong2(s1, s);
-  }
 }
 
 // per aligned 64-event tile: max and min x-atom key over the valid events (one wave per tile)
@@ -988,17 +959,6 @@ extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::Stream
     case sdh::KK_F64: hipLaunchKernelGGL(sdh::ratchet_tile_summary<sdh::KK_F64>, grid, block, 0, s, *B, attr, conv, n_tiles, tmax, tmin, thas); break;
     default: hipLaunchKernelGGL(sdh::ratchet_tile_summary<sdh::KK_I64>, grid, block, 0, s, *B, attr, conv, n_tiles, tmax, tmin, thas); break;
   }
-  return hipGetLastError();
-}
-
-extern "C" hipError_t sdh_launch_ratchet_decode(const int64_t* match, int blk_recs, int wide,
-                                                const int32_t* blk_count, const int32_t* blk_group,
-                                                const int64_t* dst_off, const sdh::RatchetGroup* groups,
-                                                const int64_t* ts, int64_t seq_base, int n_blocks, int64_t* out,
-                                                hipStream_t s) {
-  if (n_blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(sdh::ratchet_decode, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, wide, blk_count,
-                     blk_group, dst_off, groups, ts, seq_base, out);
   return hipGetLastError();
 }
 

@@ -200,6 +200,9 @@ struct RatchetLaunch {
   int32_t* blk_next;            // [0] next free block
   int32_t n_blocks, blk_recs;
   int32_t wide;
+  int32_t ring;                 // SDH_FLAG_DEVICE_MATCHES: blocks wrap modulo n_blocks (every record is
+                                //   written, none is read back); rec_total counts them
+  unsigned long long* rec_total;
   int32_t* err;                 // [0] deque overflow, [1] unordered ts, [2] match overflow
 };
 
@@ -209,6 +212,10 @@ struct RatchetLaunch {
 namespace kg {
 struct GQuery;
 }
+
+// ring mode (SDH_FLAG_DEVICE_MATCHES) writes a record at its offset modulo (out_cap - margin): the
+// host keeps out_cap > margin and every record (7 + S + pool nodes words) shorter than it
+constexpr int64_t GEN_RING_MARGIN = 8192;
 
 struct GenLaunch {
   const kg::GQuery* queries;
@@ -233,6 +240,9 @@ struct GenLaunch {
   int32_t n_items;
   int32_t* err;               // [0] instance capacity, [1] reference would throw, [2] output overflow
   unsigned long long* rec_count;  // matches emitted (records), counted even when not written
+  int64_t* rec_off;           // write_records == 1: word offset of each record, in reservation order
+  int64_t rec_cap;
+  unsigned long long* rec_next;
   int32_t write_records;      // 1: write; 2: write into a ring nobody reads (SDH_FLAG_DEVICE_MATCHES); 0: count only
   // event chunks of an unpartitioned set (kg::seq_lookback): item = chunk * groups + g; chunk 0
   // continues the persistent arena, chunk c > 0 starts a fresh instance in scratch block
@@ -268,8 +278,36 @@ struct SeqLaunch {
   int64_t out_cap;
   unsigned long long* out_next;
   unsigned long long* rec_count;
+  int64_t* rec_off;           // as GenLaunch
+  int64_t rec_cap;
+  unsigned long long* rec_next;
   int32_t* err;               // [2] output overflow
   int32_t pad;
+};
+
+// ------------------------------------------------------------------------------------------
+// Device match table (matches.hip): every plan's matches since the last poll, one row each, with
+// the R18 delivery-order sort keys (the reference hands each completed StateEvent to
+// QuerySelector.process per input event, per receiver, per state processor, per pending partial):
+//   hi    = (trigger seq - seq_ref) << RANK_BITS | out_rank(query, stream)
+//   lo[k] = tiebreaks of one (trigger event, query), least significant first: K_ratchet the e1
+//           seq; K_chain slot k's seq (k = 0 .. S-2; slot S-2 is compared first); K_gen the
+//           emission index within its processAndReturn chunk
+// words[woff .. woff+wlen) = per state slot a count c then c event sequence numbers.
+// ------------------------------------------------------------------------------------------
+constexpr int MAXLO = MAXS - 1;
+constexpr int RANK_BITS = 20;
+
+struct MatchTable {
+  uint64_t* hi;
+  uint64_t* lo[MAXLO];
+  int64_t* seq;         // trigger event sequence number
+  int64_t* q;
+  int64_t* key;
+  int64_t* ts;
+  int64_t* woff;
+  int64_t* wlen;
+  int64_t* words;
 };
 
 }  // namespace sdh

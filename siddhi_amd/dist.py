@@ -1,29 +1,70 @@
-"""Multi-GPU sharding and match gather.
+"""Multi-GPU sharding, event broadcast and match gather.
 
 One process per GPU. State is private per (pattern, key), so the path shards with no data-path
-collective: every rank sees the whole event stream (broadcast, or per-rank H2D from pinned host
-memory), runs only its own query shard, and keeps its matches. The one exchange step is the match
-gather to rank 0, where the per-rank match lists -- each already in the reference's delivery order
-(R18) -- are merged into the single-engine order.
+collective but two exchange steps: every rank sees the whole event stream (an RCCL broadcast of each
+batch from the ingest rank, or per-rank H2D from pinned host memory), runs only its share, and the
+matches are gathered to rank 0, where the per-rank outputs -- each already in the reference's
+delivery order (R18) -- are merged into the single-engine order.
 
-Shard rule (mirrors sdh_engine_create): query q runs on rank `shard_key(q) % world`, where
-shard_key is q itself for an unpartitioned query and the partition's first query for a partitioned
-one (a partition's queries share their per-key instances' routing, so they stay together).
+Shard rule (mirrors sdh_engine_create and nfa_gen.hip key_shard):
+* an unpartitioned query q runs on rank q % world (pattern-set sharding);
+* a partition's queries run on every rank, and rank r owns the keys with
+  |String.valueOf(key).hashCode() % world| == r -- the reference's PartitionedDistributionStrategy
+  destination (stream/output/sink/distributed/PartitionedDistributionStrategy.java:98-109). Float /
+  double keys and string dictionary ids hash their raw 64-bit word instead (key_shard below).
+
+The gather moves device buffers: every rank's R18-sorted tuples stay in HBM
+(sdh_engine_poll_device), counts are all-gathered and the columns are sent to rank 0 point-to-point
+(RCCL over xGMI, or gloo on CPU tensors in the tests). The merge is a stable sort by
+(trigger sequence number, receiver rank): a query's matches for one event come from one rank (its
+pattern shard, or the owner of the event's key), so the sort keeps their pending-list order.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+import ctypes
+from typing import Dict, List, Optional, Sequence, Tuple
 
-from .ir import R_MULTI, ProgramIR
+from .ir import R_MULTI, T_BOOL, T_INT, T_LONG, ProgramIR
 
-
-def shard_key(ir: ProgramIR, q: int) -> int:
-    pi = ir.queries[q].partition_idx
-    return q if pi < 0 else ir.partitions[pi].query_idx[0]
+RANK_BITS = 20  # as nfa_types.h
 
 
 def shard_of(ir: ProgramIR, q: int, world: int) -> int:
-    return shard_key(ir, q) % max(1, world)
+    """Rank of an unpartitioned query, -1 for a partitioned one (it runs on every rank)."""
+    if ir.queries[q].partition_idx >= 0:
+        return -1
+    return q % max(1, world)
+
+
+def _mix64(z: int) -> int:
+    m = (1 << 64) - 1
+    z &= m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def java_string_hash(s: str) -> int:
+    h = 0
+    for c in s:
+        h = (31 * h + ord(c)) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= (1 << 31) else h
+
+
+def key_shard(raw: int, attr_type: int, world: int) -> int:
+    """Owner rank of a partition key (raw attribute word, as the engine sees it)."""
+    if attr_type in (T_INT, T_LONG):
+        v = raw
+        if attr_type == T_INT:
+            v = ((raw & 0xFFFFFFFF) ^ 0x80000000) - 0x80000000
+        h = java_string_hash(str(v))
+    elif attr_type == T_BOOL:
+        h = java_string_hash("true" if raw else "false")
+    else:
+        h = (_mix64(raw) >> 33) & 0xFFFFFFFF
+        h = h - (1 << 32) if h >= (1 << 31) else h
+    r = abs(h) % world  # |h % world| (Java remainder keeps the dividend's sign)
+    return r
 
 
 def output_ranks(ir: ProgramIR) -> Dict[Tuple[int, int], int]:
@@ -56,26 +97,155 @@ def output_ranks(ir: ProgramIR) -> Dict[Tuple[int, int], int]:
     return rank
 
 
-def merge_matches(ir: ProgramIR, stream_of_seq, per_rank: Sequence[List[tuple]]) -> List[tuple]:
-    """Merge per-rank match lists (each in R18 order) into the single-engine order.
+class StreamLog:
+    """Which stream each global sequence number belongs to (the host pushes the batches, so it
+    knows): a list of (seq_base, n, stream) pushes."""
 
-    A match is (query, key, ts, slots); its triggering event is the newest event in its slots (the
-    event being processed is copied into a slot before the selector runs)."""
-    ranks = output_ranks(ir)
-    keyed = []
-    for r, lst in enumerate(per_rank):
-        for i, m in enumerate(lst):
-            seq = max(x for slot in m[3] for x in slot)
-            keyed.append(((seq, ranks[(m[0], stream_of_seq(seq))], r, i), m))
-    keyed.sort(key=lambda t: t[0])
-    return [m for _, m in keyed]
+    def __init__(self):
+        self.bases: List[int] = []
+        self.streams: List[int] = []
+        self.next = 0
+
+    def push(self, stream: int, n: int):
+        if self.streams and self.streams[-1] == stream:
+            self.next += n
+            return
+        self.bases.append(self.next)
+        self.streams.append(stream)
+        self.next += n
+
+    def stream_of(self, seq):
+        """torch int64 tensor of seqs -> stream index tensor."""
+        import torch
+        b = torch.tensor(self.bases, dtype=torch.int64, device=seq.device)
+        s = torch.tensor(self.streams, dtype=torch.int64, device=seq.device)
+        return s[torch.searchsorted(b, seq, right=True) - 1]
 
 
-def gather_matches(local: List[tuple], group=None) -> List[List[tuple]] | None:
-    """Gather every rank's match list to rank 0 (torch.distributed; RCCL or gloo). Returns the
-    per-rank lists on rank 0, None elsewhere."""
+FIELDS = ("q", "key", "ts", "seq", "len", "words")
+
+
+def columns_from_device(eng, device) -> Dict[str, "object"]:
+    """This rank's R18-sorted matches since the last poll, left in HBM by sdh_engine_poll_device and
+    copied device-to-device into torch tensors on `device`."""
+    import torch
+    m = eng.poll_device()
+    n = m.n
+    hip = _hip()
+    out = {}
+    for name, ptr in (("q", m.query), ("key", m.key), ("ts", m.ts), ("seq", m.seq), ("off", m.off)):
+        t = torch.empty(n + 1 if name == "off" else n, dtype=torch.int64, device=device)
+        if t.numel():
+            _d2d(hip, t.data_ptr(), ptr, t.numel() * 8)
+        out[name] = t
+    nw = int(out["off"][-1].item()) if n else 0
+    w = torch.empty(nw, dtype=torch.int64, device=device)
+    if nw:
+        _d2d(hip, w.data_ptr(), m.words, nw * 8)
+    out["words"] = w
+    out["len"] = out.pop("off").diff() if n else torch.empty(0, dtype=torch.int64, device=device)
+    return out
+
+
+def columns_from_arrays(q, key, ts, off, words, seq, device="cpu"):
+    import torch
+    t = lambda a: torch.as_tensor(a, dtype=torch.int64).to(device)  # noqa: E731
+    return {"q": t(q), "key": t(key), "ts": t(ts), "seq": t(seq), "len": t(off).diff(), "words": t(words)}
+
+
+def gather_columns(cols, group=None) -> Optional[List[dict]]:
+    """Gather every rank's match columns to rank 0 (torch.distributed: RCCL for device tensors, gloo
+    for CPU ones): an all-gather of (matches, words), then point-to-point sends to rank 0. Returns
+    the per-rank column dicts on rank 0, None elsewhere."""
+    import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    out = [None] * world if dist.get_rank(group) == 0 else None
-    dist.gather_object(local, out, dst=0, group=group)
+    me = dist.get_rank(group)
+    dev = cols["q"].device
+    cnt = torch.tensor([cols["q"].numel(), cols["words"].numel()], dtype=torch.int64, device=dev)
+    allc = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(allc, cnt, group=group)
+    if me != 0:
+        for f in FIELDS:
+            if cols[f].numel():
+                dist.send(cols[f].contiguous(), dst=0, group=group)
+        return None
+    out = [cols]
+    for r in range(1, world):
+        n, nw = (int(x) for x in allc[r].tolist())
+        got = {}
+        for f in FIELDS:
+            t = torch.empty(nw if f == "words" else n, dtype=torch.int64, device=dev)
+            if t.numel():
+                dist.recv(t, src=r, group=group)
+            got[f] = t
+        out.append(got)
     return out
+
+
+def rank_table(ir: ProgramIR):
+    """output_ranks as a [query * n_streams + stream] int64 tensor."""
+    import torch
+    ns = len(ir.streams)
+    table = torch.zeros(len(ir.queries) * ns, dtype=torch.int64)
+    for (q, s), r in output_ranks(ir).items():
+        table[q * ns + s] = r
+    return table
+
+
+def merge_columns(ir: Optional[ProgramIR], per_rank: Sequence[dict], stream_log: StreamLog, table=None,
+                  n_streams: int = 0) -> dict:
+    """Per-rank R18-ordered columns -> the single-engine order (stable sort by trigger seq, receiver
+    rank; rank-major concatenation keeps a query's own order). `table` (rank_table) may be given
+    instead of the program."""
+    import torch
+    dev = per_rank[0]["q"].device
+    cat = {f: torch.cat([c[f] for c in per_rank]) for f in FIELDS}
+    n = cat["q"].numel()
+    if n == 0:
+        return cat
+    ns = n_streams or len(ir.streams)
+    table = (rank_table(ir) if table is None else table).to(dev)
+    st = stream_log.stream_of(cat["seq"])
+    key = (cat["seq"] << RANK_BITS) | table[cat["q"] * ns + st]
+    perm = torch.sort(key, stable=True).indices
+    out = {f: cat[f][perm] for f in ("q", "key", "ts", "seq", "len")}
+    starts = torch.cumsum(cat["len"], 0) - cat["len"]
+    lens = out["len"]
+    new_off = torch.cumsum(lens, 0) - lens
+    src = torch.repeat_interleave(starts[perm] - new_off, lens) + torch.arange(int(lens.sum()), device=dev)
+    out["words"] = cat["words"][src]
+    return out
+
+
+def columns_to_tuples(cols) -> List[tuple]:
+    """(query, key, ts, slots) tuples (the harness' match form) from columns (n_slots from the words)."""
+    q, k, ts, lens, words = (cols[f].cpu().tolist() for f in ("q", "key", "ts", "len", "words"))
+    out, o = [], 0
+    for i in range(len(q)):
+        w = words[o:o + lens[i]]
+        o += lens[i]
+        slots, j = [], 0
+        while j < len(w):
+            c = w[j]
+            slots.append(tuple(w[j + 1:j + 1 + c]))
+            j += 1 + c
+        out.append((q[i], k[i], ts[i], tuple(slots)))
+    return out
+
+
+_hip_lib = None
+
+
+def _hip():
+    global _hip_lib
+    if _hip_lib is None:
+        _hip_lib = ctypes.CDLL("libamdhip64.so")
+        _hip_lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    return _hip_lib
+
+
+def _d2d(hip, dst: int, src_ptr, nbytes: int):
+    src = ctypes.cast(src_ptr, ctypes.c_void_p).value
+    if hip.hipMemcpy(dst, src, nbytes, 3) != 0:  # hipMemcpyDeviceToDevice
+        raise RuntimeError("hipMemcpy device-to-device failed")

@@ -42,7 +42,8 @@ class SdhBatch(ctypes.Structure):
 class SdhMatches(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("query", ctypes.POINTER(ctypes.c_int64)),
                 ("key", ctypes.POINTER(ctypes.c_int64)), ("ts", ctypes.POINTER(ctypes.c_int64)),
-                ("off", ctypes.POINTER(ctypes.c_int64)), ("words", ctypes.POINTER(ctypes.c_int64))]
+                ("off", ctypes.POINTER(ctypes.c_int64)), ("words", ctypes.POINTER(ctypes.c_int64)),
+                ("seq", ctypes.POINTER(ctypes.c_int64))]
 
 
 class SdhStats(ctypes.Structure):
@@ -52,7 +53,7 @@ class SdhStats(ctypes.Structure):
                 ("last_gen_items", ctypes.c_int64), ("last_seq_items", ctypes.c_int64)]
 
 
-EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engine_poll",
+EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engine_poll", "sdh_engine_poll_device",
            "sdh_engine_pending_matches", "sdh_engine_stats", "sdh_engine_snapshot",
            "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version"]
 
@@ -74,6 +75,7 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_engine_push.argtypes = [P, ctypes.c_int32, ctypes.POINTER(SdhBatch)]
     lib.sdh_engine_flush.argtypes = [P]
     lib.sdh_engine_poll.argtypes = [P, ctypes.POINTER(SdhMatches)]
+    lib.sdh_engine_poll_device.argtypes = [P, ctypes.POINTER(SdhMatches)]
     lib.sdh_engine_pending_matches.argtypes = [P, ctypes.POINTER(ctypes.c_int64)]
     lib.sdh_engine_stats.argtypes = [P, ctypes.POINTER(SdhStats)]
     lib.sdh_engine_snapshot.argtypes = [P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
@@ -166,18 +168,29 @@ class HipEngine:
             nl = [np.ascontiguousarray(nulls[:, j]) for j in range(len(types))]
         self.push_columns(stream, np.asarray(ts, dtype=np.int64), cols, nl)
 
-    def poll(self):
+    def poll(self, with_seq: bool = False):
+        """R18-ordered matches since the last poll as arrays (query, key, ts, off, words[, seq])."""
         m = SdhMatches()
         self._check(self.lib.sdh_engine_poll(self.h, ctypes.byref(m)))
         n = m.n
         if n == 0:
-            return (np.zeros(0, np.int64),) * 4 + (np.zeros(0, np.int64),)
+            z = np.zeros(0, np.int64)
+            return (z, z, z, np.zeros(1, np.int64), z) + ((z,) if with_seq else ())
         q = np.ctypeslib.as_array(m.query, shape=(n,)).copy()
         k = np.ctypeslib.as_array(m.key, shape=(n,)).copy()
         ts = np.ctypeslib.as_array(m.ts, shape=(n,)).copy()
         off = np.ctypeslib.as_array(m.off, shape=(n + 1,)).copy()
         words = np.ctypeslib.as_array(m.words, shape=(int(off[-1]),)).copy() if off[-1] else np.zeros(0, np.int64)
+        if with_seq:
+            return q, k, ts, off, words, np.ctypeslib.as_array(m.seq, shape=(n,)).copy()
         return q, k, ts, off, words
+
+    def poll_device(self) -> SdhMatches:
+        """R18-sorted matches since the last poll, left in HBM: the SdhMatches fields are device
+        pointers (valid until the next push / poll)."""
+        m = SdhMatches()
+        self._check(self.lib.sdh_engine_poll_device(self.h, ctypes.byref(m)))
+        return m
 
     def take_matches(self, n_slots_of):
         q, k, ts, off, words = self.poll()

@@ -75,10 +75,11 @@ def c2_within_sec(p: int, seed: int = PATTERN_SEED) -> int:
     return (1, 10, 60)[splitmix64(seed ^ p) % 3]
 
 
-def c2_app(n_patterns: int, within=None) -> str:
-    """1K concurrent 2-state filter+reference patterns (BASELINE.json configs[1])."""
+def c2_app(n_patterns: int, within=None, first: int = 0) -> str:
+    """1K concurrent 2-state filter+reference patterns (BASELINE.json configs[1]); a shard holds
+    patterns first .. first+n_patterns-1."""
     qs = [STOCK_STREAM]
-    for p in range(n_patterns):
+    for p in range(first, first + n_patterns):
         w = c2_within_sec(p) if within is None else within
         qs.append(f"@info(name='p{p}') from every e1=StockStream[price > {c2_threshold_text(p)}] -> "
                   f"e2=StockStream[price > e1.price] within {w} sec "
@@ -149,3 +150,46 @@ def c4_app(n_patterns: int, first: int = 0) -> str:
     """C4 (BASELINE.json configs[3]): fraud-rule sequences; a shard holds patterns
     first .. first+n_patterns-1 (pattern-set sharding across GPUs)."""
     return " ".join([TXN_STREAM] + [c4_query(p) for p in range(first, first + n_patterns)])
+
+
+# ---- the same streams generated on a device with torch (int64 ops wrap like uint64; logical shifts
+# and unsigned remainders are spelled out), bit-identical to the numpy generators above ----
+def _c64(v: int) -> int:
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def _srl(z, k: int):
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def _splitmix64_t(x):
+    z = x + _c64(0x9E3779B97F4A7C15)
+    z = (z ^ _srl(z, 30)) * _c64(0xBF58476D1CE4E5B9)
+    z = (z ^ _srl(z, 27)) * _c64(0x94D049BB133111EB)
+    return z ^ _srl(z, 31)
+
+
+def _umod_t(u, m: int):
+    return ((_srl(u, 1) % m) * 2 + (u & 1)) % m
+
+
+def _hashes_t(start: int, n: int, seed: int, device):
+    import torch
+    i = torch.arange(start, start + n, dtype=torch.int64, device=device)
+    return i, [_splitmix64_t(seed ^ (i * 4 + j)) for j in (1, 2, 3)]
+
+
+def stock_events_torch(start: int, n: int, n_symbols: int, device, seed: int = EVENT_SEED):
+    """stock_events as torch tensors on `device`: (ts int64, sym int32, price float32, volume int32)."""
+    import torch
+    i, (h1, h2, h3) = _hashes_t(start, n, seed, device)
+    price = _umod_t(h1, 10000).to(torch.float32) / 100.0
+    return TS0 + i, _umod_t(h3, n_symbols).to(torch.int32), price, (1 + _umod_t(h2, 1000)).to(torch.int32)
+
+
+def txn_events_torch(start: int, n: int, n_accounts: int, device, seed: int = EVENT_SEED):
+    """txn_events as torch tensors on `device`: (ts int64, account int32, amount float32, risk int32)."""
+    import torch
+    i, (h1, h2, h3) = _hashes_t(start, n, seed, device)
+    amount = _umod_t(h1, 100000).to(torch.float32) / 100.0
+    return TS0 + i, _umod_t(h3, n_accounts).to(torch.int32), amount, _umod_t(h2, 100).to(torch.int32)

@@ -39,6 +39,8 @@ def oracle_lib():
         lib.oracle_match_words.restype = I64
         lib.oracle_get_matches.argtypes = [P, VP, VP, VP, VP, VP]
         lib.oracle_clear_matches.argtypes = [P]
+        lib.oracle_live_partials.argtypes = [P]
+        lib.oracle_live_partials.restype = I64
         lib.oracle_error.argtypes = [P]
         lib.oracle_error.restype = ctypes.c_char_p
         lib.oracle_destroy.argtypes = [P]

@@ -31,3 +31,54 @@ def test_library_exports_every_declared_symbol():
 def test_gfx950_code_object_present():
     data = open(os.path.join(ROOT, "siddhi_amd", "libsiddhi_hip.so"), "rb").read()
     assert b"gfx950" in data
+
+
+def _create(lib, blob, device=0):
+    from siddhi_amd.engine import SdhConfig
+    cfg = SdhConfig(device=device, shard_rank=0, shard_world=1)
+    h = ctypes.c_void_p()
+    buf = ctypes.create_string_buffer(blob, max(1, len(blob)))
+    rc = lib.sdh_engine_create(buf, len(blob), ctypes.byref(cfg), ctypes.byref(h))
+    return rc, h
+
+
+def test_malformed_program_is_invalid_without_a_device():
+    """sdh_engine_create validates the program before any device call: a malformed blob fails with
+    SDH_E_INVALID and sdh_last_error(NULL) says why (the reference's SiddhiAppCreationException)."""
+    from siddhi_amd.engine import load_library
+    lib = load_library()
+    for blob, why in ((b"", b"magic"), (b"NOT-AN-IR-BLOB-AT-ALL", b"magic"),
+                      (b"SDHIR001" + (7).to_bytes(8, "little"), b"version"),
+                      (b"SDHIR001" + (1).to_bytes(8, "little") + (3).to_bytes(8, "little"), b"truncated")):
+        rc, h = _create(lib, blob)
+        assert rc == -1 and not h.value, (blob, rc)
+        assert why in lib.sdh_last_error(None).lower(), lib.sdh_last_error(None)
+
+
+def test_null_arguments_are_invalid():
+    from siddhi_amd.engine import load_library
+    lib = load_library()
+    assert lib.sdh_engine_create(None, 0, None, None) == -1
+    assert lib.sdh_engine_push(None, 0, None) == -1
+    assert lib.sdh_engine_poll(None, None) == -1
+    assert lib.sdh_engine_poll_device(None, None) == -1
+    assert lib.sdh_engine_flush(None) == -1
+    assert lib.sdh_engine_restore(None, None, 0) == -1
+    lib.sdh_engine_destroy(None)  # no-op
+
+
+def test_valid_program_needs_a_device():
+    """A well-formed program on a host with no HIP device fails loudly (SDH_E_DEVICE): the engine has
+    no CPU fallback."""
+    import torch
+    if torch.cuda.is_available():
+        import pytest
+        pytest.skip("a device is present")
+    from siddhi_amd import ql
+    from siddhi_amd.engine import load_library
+    from siddhi_amd.planner import plan
+    from siddhi_amd.workloads import c1_app
+    lib = load_library()
+    rc, h = _create(lib, plan(ql.parse(c1_app())).serialize())
+    assert rc == -3 and not h.value
+    assert b"no hip device" in lib.sdh_last_error(None).lower()

@@ -32,11 +32,11 @@ def full_src():
 
 
 def shard_src(ir, rank, world):
-    names = {ir.queries[q].name for q in range(len(ir.queries)) if sdist.shard_of(ir, q, world) == rank}
+    """Rank `rank`'s sub-app: its pattern shard of the unpartitioned queries plus the whole partition
+    block (every rank runs the partition for the keys it owns)."""
+    names = {ir.queries[q].name for q in range(len(ir.queries)) if sdist.shard_of(ir, q, world) in (rank, -1)}
     parts = [STREAMS] + [q for q in TOP[:2] if q.split("'")[1] in names]
-    pq = [q for q in PART if q.split("'")[1] in names]
-    if pq:
-        parts += ["partition with (k of A, k of B) begin", *pq, "end;"]
+    parts += ["partition with (k of A, k of B) begin", *PART, "end;"]
     parts += [q for q in TOP[2:] if q.split("'")[1] in names]
     return " ".join(parts), names
 
@@ -57,27 +57,40 @@ def _worker(rank, world, port, results):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from harness import App
     from siddhi_amd import ql
+    from siddhi_amd.ir import T_INT
     from siddhi_amd.planner import plan
     ir = plan(ql.parse(full_src()))
     src, names = shard_src(ir, rank, world)
-    local = App(src) if names else None
-    matches = []
-    for stream, row, t in events():  # every rank sees the whole stream (broadcast)
-        if local is not None:
-            local.send(stream, [row], [t])
-    if local is not None:
-        for m in local.matches:  # local query index -> global
-            gq = ir.query_index(local.ir.queries[m[0]].name)
-            matches.append((gq,) + tuple(m[1:]))
-    per_rank = sdist.gather_matches(matches)
+    local = App(src)
+    log = sdist.StreamLog()
+    for stream, row, t in events():  # every rank sees the whole stream (the broadcast)
+        local.send(stream, [row], [t])
+        log.push(ir.stream_index(stream), 1)
+    rows = []
+    for m in local.matches:
+        gq = ir.query_index(local.ir.queries[m[0]].name)  # local query index -> global
+        if ir.queries[gq].partition_idx >= 0 and sdist.key_shard(m[1], T_INT, world) != rank:
+            continue  # another rank owns this key (the device drops its events at routing)
+        rows.append((gq,) + tuple(m[1:]))
+    q = [m[0] for m in rows]
+    words, off = [], [0]
+    for m in rows:
+        for sl in m[3]:
+            words += [len(sl), *sl]
+        off.append(len(words))
+    seq = [max(x for sl in m[3] for x in sl) for m in rows]  # the triggering (newest) event
+    cols = sdist.columns_from_arrays(q, [m[1] for m in rows], [m[2] for m in rows], off, words, seq)
+    per_rank = sdist.gather_columns(cols)
     if rank == 0:
         full = App(full_src())
         for stream, row, t in events():
             full.send(stream, [row], [t])
-        merged = sdist.merge_matches(ir, lambda s: full.log.stream[s], per_rank)
+        merged = sdist.columns_to_tuples(sdist.merge_columns(ir, per_rank, log))
         results["ok"] = merged == full.matches
         results["n"] = len(full.matches)
-        results["sizes"] = [len(x) for x in per_rank]
+        results["sizes"] = [int(c["q"].numel()) for c in per_rank]
+        results["part_split"] = [int(sum(1 for x in c["q"].tolist() if ir.queries[x].partition_idx >= 0))
+                                 for c in per_rank]
     dist.barrier()
     dist.destroy_process_group()
 
@@ -90,22 +103,43 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_sharded_gather_merge_equals_single_engine(world):
+    """Pattern-set + key sharding, the column gather (gloo) and the R18 merge reproduce one engine."""
     mgr = mp.Manager()
     results = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), results), nprocs=world, join=True)
     assert results["n"] > 50
     assert all(s > 0 for s in results["sizes"])
+    assert sum(1 for x in results["part_split"] if x > 0) >= 2  # partition keys really split
     assert results["ok"]
 
 
-def test_shard_rule_keeps_partitions_together():
+def test_shard_rule():
     from siddhi_amd import ql
     from siddhi_amd.planner import plan
     ir = plan(ql.parse(full_src()))
     for world in (1, 2, 3, 8):
         owners = [sdist.shard_of(ir, q, world) for q in range(len(ir.queries))]
         for p in ir.partitions:
-            assert len({owners[q] for q in p.query_idx}) == 1
-        assert all(0 <= o < world for o in owners)
+            assert all(owners[q] == -1 for q in p.query_idx)  # partitions run on every rank
+        assert all(-1 <= o < world for o in owners)
+
+
+def test_key_shard_is_the_reference_destination_rule():
+    """|String.valueOf(key).hashCode() % N| (PartitionedDistributionStrategy.java:98-109)."""
+    from siddhi_amd.ir import T_BOOL, T_INT, T_LONG
+    assert sdist.java_string_hash("123") == 48690
+    assert sdist.java_string_hash("-7") == 1450
+    assert sdist.java_string_hash("true") == 3569038
+    assert sdist.key_shard(123, T_INT, 8) == 48690 % 8
+    assert sdist.key_shard(-7, T_INT, 4) == 1450 % 4
+    assert sdist.key_shard((1 << 32) - 7, T_INT, 4) == 1450 % 4  # raw word of int -7
+    big = -9223372036854775808
+    h = sdist.java_string_hash(str(big))
+    assert sdist.key_shard(big, T_LONG, 5) == abs(h) % 5
+    assert sdist.key_shard(1, T_BOOL, 3) == 3569038 % 3
+    counts = [0] * 4
+    for k in range(1000):
+        counts[sdist.key_shard(k, T_INT, 4)] += 1
+    assert min(counts) > 150

@@ -145,21 +145,39 @@ def test_force_gen_matches_chain_plans_on_c2():
     assert len(a[0]) > 10000
 
 
-def test_engine_shards_merge_to_single_engine():
-    """sdh_config.shard_rank/shard_world on the device: the union of two shards, merged by
-    siddhi_amd.dist.merge_matches, equals one engine running every query (and the oracle)."""
+@pytest.mark.parametrize("world", [2, 3])
+def test_engine_shards_merge_to_single_engine(world):
+    """sdh_config.shard_rank/shard_world on the device: pattern-set sharding of the unpartitioned
+    queries and key sharding of the partition (foreign keys dropped at routing); the union of the
+    shards, merged by siddhi_amd.dist.merge_columns, equals one engine running every query (and the
+    oracle)."""
     from siddhi_amd import dist as sdist
+    from siddhi_amd.engine import HipEngine
+    from siddhi_amd.ir import T_INT
     from test_dist import events, full_src
     o = App(full_src())
-    shards = [hip_app(full_src(), shard_rank=r, shard_world=2) for r in range(2)]
+    types = [s.attr_types for s in o.ir.streams]
+    shards = [HipEngine(o.blob, stream_types=types, shard_rank=r, shard_world=world) for r in range(world)]
+    log = sdist.StreamLog()
+    from siddhi_amd.events import encode_rows
     for stream, row, t in events():
         o.send(stream, [row], [t])
-        for s in shards:
-            s.send(stream, [row], [t])
-    for r, s in enumerate(shards):
-        assert {m[0] for m in s.matches} <= {q for q in range(len(o.ir.queries))
-                                            if sdist.shard_of(o.ir, q, 2) == r}
-    merged = sdist.merge_matches(o.ir, lambda q: o.log.stream[q], [s.matches for s in shards])
+        si = o.ir.stream_index(stream)
+        log.push(si, 1)
+        vals, nulls = encode_rows([row], o.ir.streams[si].attr_types, o.dictionary)
+        for sh in shards:  # every rank sees the whole stream
+            sh.send(si, [t], vals, nulls)
+    per_rank = []
+    for r, sh in enumerate(shards):
+        q, k, ts, off, words, seq = sh.poll(with_seq=True)
+        cols = sdist.columns_from_arrays(q, k, ts, off, words, seq)
+        for qi, key in zip(q.tolist(), k.tolist()):
+            if o.ir.queries[qi].partition_idx >= 0:
+                assert sdist.key_shard(key, T_INT, world) == r
+            else:
+                assert qi % world == r
+        per_rank.append(cols)
+    merged = sdist.columns_to_tuples(sdist.merge_columns(o.ir, per_rank, log))
     assert merged == o.matches and len(merged) > 50
 
 
@@ -339,3 +357,20 @@ def test_device_matches_ring_counts_every_record():
     n = ring.stats().matches
     assert n > 1_000_000
     assert n == normal.stats().matches
+
+
+def test_gen_output_overflow_reruns_exactly():
+    """A push whose K_gen match records overflow the output buffer is undone (arena backup) and re-run
+    with room for every record: no match is lost and later pushes continue exactly."""
+    from siddhi_amd.workloads import c2_app, stock_events
+    src = c2_app(64)
+    o = App(src)
+    g = hip_app(src, flags=SDH_FLAG_FORCE_GEN)
+    for lo, hi in ((0, 30000), (30000, 40000)):  # the first push needs ~16M record words (4M buffer)
+        ts, sym, price, vol = stock_events(lo, hi - lo)
+        vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64), vol.astype(np.int64)], 1)
+        o.engine.send(0, ts, vals, None)
+        g.engine.push_columns(0, ts, [sym, price.view(np.uint32), vol])
+        om = o.engine.take_matches(lambda q: 2)
+        gm = g.engine.take_matches(lambda q: 2)
+        assert gm == om and len(om) > 100000

@@ -1,0 +1,95 @@
+"""GPU parity at each BASELINE config's full pattern count (SURVEY §8(c) large-stream golden vectors).
+
+The HIP engine runs the whole pattern set of C1-C4 over the seeded synthetic stream, pushed from
+HBM in large batches and polled through the C-ABI (sdh_engine_poll: the device R18 sort); the
+R18-ordered match stream must reproduce the oracle's digest (tests/large_golden.py) and the
+committed explicit samples exactly. The goldens were generated in the container by
+tests/golden/make_large_golden.py (the oracle sharded by pattern set); nothing here runs the oracle.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from harness import App
+from large_golden import CONFIGS, Digest, app_source, events, load
+
+pytestmark = pytest.mark.gpu
+
+# push sizes on the device (the digest does not depend on how the stream is cut)
+PUSH = {"c1": 1 << 18, "c2": 1 << 17, "c3": 1 << 16, "c4": 1 << 16}
+
+
+def _engine(name, blob, types):
+    from siddhi_amd.engine import HipEngine
+    cfg = CONFIGS[name]
+    if name == "c3":
+        return HipEngine(blob, stream_types=types, gen_pool_states=32, gen_pool_nodes=128, gen_list_cap=32,
+                         gen_max_keys=2 * cfg["keys"])
+    return HipEngine(blob, stream_types=types)
+
+
+def _run(name, n_events=None, check_every=None):
+    import torch
+    cfg = CONFIGS[name]
+    g = load(name)
+    app = App(app_source(name, cfg["patterns"]), engine_factory=lambda blob: None)
+    eng = _engine(name, app.blob, [s.attr_types for s in app.ir.streams])
+    dig = Digest(g["sample_stride"])
+    dev = torch.device("cuda:0")
+    n_events = n_events or cfg["events"]
+    B = PUSH[name]
+    for lo in range(0, n_events, B):
+        n = min(B, n_events - lo)
+        ts, cols, _ = events(name, lo, n)
+        t_ts = torch.from_numpy(ts).to(dev)
+        t_cols = [torch.from_numpy(np.ascontiguousarray(c).view(np.int32)).to(dev) for c in cols]
+        eng.push_device(0, n, t_ts.data_ptr(), [c.data_ptr() for c in t_cols])
+        dig.update(*eng.poll())
+    return g, dig, eng
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4"])
+def test_large_golden_full_config(name):
+    g, dig, eng = _run(name)
+    assert dig.n == g["n_matches"], f"{name}: {dig.n} matches, golden {g['n_matches']}"
+    assert dig.first == g["sample_first"]
+    assert dig.strided == g["sample_strided"]
+    assert dig.n_words == g["n_words"]
+    assert dig.hexdigest() == g["digest"]
+    assert eng.stats().events == g["events"]
+
+
+def _hip():
+    lib = ctypes.CDLL("libamdhip64.so")
+    lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    return lib
+
+
+def test_poll_device_equals_poll():
+    """sdh_engine_poll_device leaves the same R18-ordered tuples in HBM that sdh_engine_poll copies
+    to the host (two engines over the same C2 stream: ratchet + chain + K_gen plans)."""
+    from siddhi_amd.engine import HipEngine
+    from siddhi_amd.workloads import c2_app, stock_events
+    src = c2_app(70) + (" @info(name='x3') from every e1=StockStream[price > 90] -> e2=StockStream[price < 10] "
+                        "-> e3=StockStream[price > e1.price] within 1 sec select e1.price as a insert into O;"
+                        " @info(name='xl') from every e1=StockStream[price > 95] -> e2=StockStream[volume > 900] "
+                        "or e3=StockStream[price < 1] within 1 sec select e1.price as a insert into O;")
+    app = App(src, engine_factory=lambda blob: None)
+    types = [s.attr_types for s in app.ir.streams]
+    a, b = HipEngine(app.blob, stream_types=types), HipEngine(app.blob, stream_types=types)
+    ts, sym, price, vol = stock_events(0, 30000)
+    cols = [sym, price.view(np.uint32), vol]
+    a.push_columns(0, ts, cols)
+    b.push_columns(0, ts, cols)
+    q, k, t, off, words = a.poll()
+    m = b.poll_device()
+    assert m.n == len(q) > 100000
+    hip = _hip()
+    D2H = 2
+    for ptr, want in ((m.query, q), (m.key, k), (m.ts, t), (m.off, off), (m.words, words)):
+        got = np.zeros(len(want), np.int64)
+        addr = ctypes.cast(ptr, ctypes.c_void_p).value
+        assert hip.hipMemcpy(got.ctypes.data, addr, got.nbytes, D2H) == 0
+        assert np.array_equal(got, want)
+    assert set(np.unique(q).tolist()) >= {70, 71}  # the chain and K_gen queries matched too
