@@ -151,14 +151,24 @@ def cpu_baseline(workload, n_symbols, budget_s):
                       f"{d1} events (oracle/liboracle.so, matches counted in the library)"}
 
 
-def source_hash():
-    """Hash of the sources the kernels are built from (profiles are attached only at equal hashes)."""
+KERNEL_SOURCES = {  # what a kernel's code and launch configuration are built from
+    "nfa_ratchet_kernel": ["nfa_ratchet.hip", "nfa_types.h", "engine.hip"],
+    "nfa_gen_kernel": ["nfa_gen.hip", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
+    "nfa_seq_kernel": ["nfa_gen.hip", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
+    "nfa_part_kernel": ["nfa_part.hip", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
+}
+
+
+def source_hash(kernel=None):
+    """Hash of the sources `kernel` is built from (all kernel sources when None); a committed profile
+    is attached to the bench line only at an equal hash."""
+    names = KERNEL_SOURCES.get(kernel) or sorted({f for v in KERNEL_SOURCES.values() for f in v})
     h = hashlib.sha256()
-    for f in sorted(glob.glob(os.path.join(ROOT, "siddhi_amd", "csrc", "*.h")) +
-                    glob.glob(os.path.join(ROOT, "siddhi_amd", "csrc", "*.hip")) +
-                    glob.glob(os.path.join(ROOT, "include", "*.h"))):
-        h.update(os.path.basename(f).encode())
-        h.update(open(f, "rb").read())
+    for name in names:
+        f = os.path.join(ROOT, "siddhi_amd", "csrc", name)
+        if os.path.exists(f):
+            h.update(name.encode())
+            h.update(open(f, "rb").read())
     return h.hexdigest()[:16]
 
 
@@ -166,7 +176,7 @@ def profiled(kernel, workload, patterns, batch):
     """The committed rocprofv3 profile of this same command at these sources (profiles/*/meta.json):
     HBM bytes per launch of `kernel` (FETCH_SIZE x2 gfx950 streaming-read correction + WRITE_SIZE,
     KiB) and the counter-derived issue / LDS figures."""
-    src = source_hash()
+    src = source_hash(kernel)
     for meta_f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "meta.json"))):
         try:
             meta = json.load(open(meta_f))
@@ -288,7 +298,7 @@ def main():
         "config": {"workload": wl, "patterns_per_gpu": P, "events_per_step": B, "timed_events": B * args.steps,
                    "keys": K, "parallelism": f"pattern-set x{world}" + (" (RCCL event broadcast)" if bcast else ""),
                    "matches": matches, "matches_per_s": matches / elapsed, "live_partials": live,
-                   "source_hash": source_hash()},
+                   "source_hash": source_hash(kernel)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic, "traffic_source": prof_dir,
                      "kernel": kernel, "kernel_ms": avg_ms,

@@ -1,13 +1,14 @@
 #!/bin/bash
 # rocprofv3 collection for the NFA-step kernel (run on the GPU box from the repo root).
 # Kernel trace + stats, then one PMC pass per counter group (gfx950 slot limits: 8 SQ, 4 TCC), each
-# pass its own run. Usage: profiles/collect.sh <out-dir> "<bench.py args>"
+# pass its own run. Usage: profiles/collect.sh <out-dir> "<bench.py args>" <kernel name>
 set -u
 OUT=${1:-gpurun_out/prof}
 ARGS=${2:-"--steps 2 --warmup 1 --no-cpu-baseline --no-expansion"}
+KERNEL=${3:-nfa_ratchet_kernel}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
-python3 -c "import bench; print(bench.source_hash())" > "$OUT/source_hash"
+python3 -c "import bench; print(bench.source_hash('$KERNEL'))" > "$OUT/source_hash"
 echo "$ARGS" > "$OUT/args"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 bench.py $ARGS > "$OUT/trace.log" 2>&1 || { echo "trace run failed"; tail -5 "$OUT/trace.log"; exit 1; }
 i=0

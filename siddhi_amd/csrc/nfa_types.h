@@ -256,6 +256,52 @@ struct GenLaunch {
 };
 
 // ------------------------------------------------------------------------------------------
+// K_part launch (nfa_part.hip): shape-specialised partitioned patterns on compact partial tables
+//   PK_OR / PK_AND:  every e1=S[f1] -> e2=S[f2] or|and e3=S[f3] [within T]
+//   PK_COUNT:        every e1=S[f1] -> e2=S[f2] <min:max> -> e3=S[f3(e1, e2[0], e2[last], cur)] [within T]
+// item = (segment of one key's events, group of 64 same-shape queries); state block of (key, group)
+// = [header words][cap entries x entry words], every word lane-interleaved ([word][lane], int64),
+// double-buffered across pushes so a push can be re-run exactly with a larger `cap`.
+// ------------------------------------------------------------------------------------------
+enum PartKind { PK_OR = 0, PK_AND = 1, PK_COUNT = 2 };
+constexpr int PK_HDR = 2;      // header words: n entries; logical: filled prefix F | side << 32
+constexpr int PK_CMAX = 8;     // count <min:max> with max <= PK_CMAX on K_part
+// count-kind entry words: ts1, seq1, flags (len | inL3 << 8 | null bits << 16), chain[max], then
+// the captured words the e3 filter reads: e1's, the chain's first event's, its last event's
+
+struct PartLaunch {
+  const kg::GQuery* queries;
+  const int32_t* lane_q;      // [group][64]
+  const int32_t* group_tmpl;  // [group]
+  StreamBatch b;
+  const int32_t* seg_begin;   // partition routing (as GenLaunch)
+  const int32_t* seg_len;
+  const uint32_t* seg_kid;
+  const int64_t* key_of_id;
+  const int32_t* ev_idx;
+  int32_t groups;             // groups of this set; state block (kid, g) = kid * groups + g
+  int32_t group_base;         // first row of lane_q / group_tmpl of the set
+  int32_t kind;               // PartKind
+  int32_t cap;                // entries per lane
+  int32_t ew;                 // words per entry
+  int32_t sA, sB;             // logical: state ids of the side processed second (A) and first (B)
+  int32_t cmin, cmax;         // count
+  int32_t n_e1, n_first, n_last;  // count: captured words stored per entry (0 or the stream's n_cap)
+  int32_t n_items;
+  const int64_t* st_in;       // [block][PK_HDR + cap * ew][64]
+  int64_t* st_out;
+  int64_t* out;               // K_gen-format match records (nfa_gen.hip), as GenLaunch
+  int64_t out_cap;
+  unsigned long long* out_next;
+  unsigned long long* rec_count;
+  int64_t* rec_off;
+  int64_t rec_cap;
+  unsigned long long* rec_next;
+  int32_t write_records;
+  int32_t* err;               // [0] entry capacity, [2] output overflow
+};
+
+// ------------------------------------------------------------------------------------------
 // K_seq launch (nfa_gen.hip): every-start single-stream sequences of stream states evaluated as
 // windows of S consecutive events (kg::seq_window); item = (start chunk, group of 64 queries)
 // ------------------------------------------------------------------------------------------
