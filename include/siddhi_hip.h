@@ -125,6 +125,7 @@ typedef struct sdh_stats {
   int64_t last_gen_items;    /* K_gen work items (waves) of the last push: groups x key       */
                              /* segments, or groups x event chunks           */
   int64_t last_seq_items;    /* K_seq work items of the last push: groups x window chunks     */
+  int64_t last_part_items;   /* K_part work items of the last push: groups x key segments     */
 } sdh_stats;
 
 int sdh_engine_create(const void* ir_blob, size_t len, const sdh_config* cfg, sdh_engine** out);

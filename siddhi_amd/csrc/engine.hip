@@ -23,6 +23,7 @@
 #include "nfa_types.h"
 
 extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s);
+extern "C" hipError_t sdh_launch_part(const sdh::PartLaunch* L, hipStream_t s);
 extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, hipStream_t s);
 extern "C" hipError_t sdh_seq_tail(const sdh::StreamBatch* b, int64_t* tail, int32_t tail_len, int32_t new_tail_len,
                                    hipStream_t s);
@@ -615,13 +616,31 @@ struct sdh_engine {
     DevBuf<int32_t> bk32;            // the arenas before the current push (exact re-runs)
     DevBuf<int64_t> bk64;
     size_t bk_n32 = 0, bk_n64 = 0;
-    // partition routing
+  };
+  std::vector<std::unique_ptr<GenSet>> gsets;
+  // per partition: PartitionRuntime's key -> instance map (dense key ids), shared by the
+  // partition's K_gen set and K_part sets (PartitionRuntime.java:257-306)
+  struct Route {
     DevBuf<unsigned long long> tkey;
     DevBuf<int32_t> tid, n_keys;
     DevBuf<int64_t> key_of_id;
     int64_t tmask = 0, max_keys = 0;
   };
-  std::vector<std::unique_ptr<GenSet>> gsets;
+  std::vector<std::unique_ptr<Route>> routes;  // [partition] (null: no device set uses it)
+  // K_part (nfa_part.hip): one set per (partition, kind); state blocks (key, group) double-buffered
+  // per key: cur[kid] says which of st[0] / st[1] holds the key's current tables
+  struct PartSet {
+    int partition = -1, kind = 0;
+    int group_base = 0, n_groups = 0;
+    int cap = 8, ew = 3, sA = 1, sB = 2, cmax = 0, n_e1 = 0, n_first = 0, n_last = 0;
+    int64_t key_cap = 0;
+    bool ran = false;                // launched in the current pass
+    DevBuf<int64_t> st;              // [2][key_cap * n_groups][PK_HDR + cap * ew][64]
+    DevBuf<int32_t> cur, nxt;        // [key_cap]
+    int64_t bw() const { return PK_HDR + (int64_t)cap * ew; }
+  };
+  std::vector<std::unique_ptr<PartSet>> psets;
+  DevBuf<int32_t> d_perr;            // per K_part set: [0] entry capacity, [2] output overflow
   DevBuf<int64_t> r_key;
   DevBuf<uint32_t> r_kid, r_kid_s, r_uniq;
   DevBuf<int32_t> r_idx, r_idx_s, r_cnt, r_off, r_nruns;
@@ -1217,12 +1236,91 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
 // ------------------------------------------------------------------------------------------
 // K_gen host side: lowering, instance arenas, partition routing, launch, match collection
 // ------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------
+// K_part shape selection (nfa_part.hip): partitioned `every e1 -> (e2 and|or e3)` and
+// `every e1 -> e2<min:max> -> e3` patterns whose structure the compact partial tables reproduce
+// exactly (the argument is in nfa_part.hip's header)
+// ------------------------------------------------------------------------------------------
+struct KPart {
+  int kind = -1, sA = 1, sB = 2, cmax = 0, n_e1 = 0, n_first = 0, n_last = 0;
+};
+
+// every slot reference of state i's filters: (slot, chain index) pairs; false if an instruction
+// names a slot in another way than OP_ATTR / OP_STREAM_IS_NULL
+void filter_refs(const kg::LState& st, std::vector<std::pair<int64_t, int64_t>>& refs) {
+  for (const auto& f : st.filters)
+    for (const auto& in : f)
+      if (in.op == kg::OP_ATTR || in.op == kg::OP_STREAM_IS_NULL) refs.push_back({in.a, in.b});
+}
+
+KPart kpart_shape(const kg::LProgram& P, int qi, const kg::GQuery& g) {
+  KPart k;
+  const kg::LQuery& q = P.q[qi];
+  if (q.partition < 0 || q.type != kg::Q_PATTERN || q.st.size() != 3) return k;
+  if (q.start_ids.size() != 1 || q.start_ids[0] != 0 || g.max_depth > kg::RSTACK) return k;
+  const int s = q.st[0].stream;
+  for (const auto& x : q.st)
+    if (x.stream != s || x.within_every != -1 || x.callback != -1) return k;
+  if (q.recvs.size() != 1 || q.recvs[0].stream != s || q.recvs[0].procs.size() != 3 || q.recvs[0].procs[0] != 0)
+    return k;
+  const kg::LState& e1 = q.st[0];
+  if (e1.kind != kg::K_STREAM || !e1.is_start || e1.next_every != 0 || e1.has_selector) return k;
+  std::vector<std::pair<int64_t, int64_t>> r;
+  const auto& procs = q.recvs[0].procs;
+  if (q.st[1].kind == kg::K_LOGICAL) {
+    const kg::LState &a = q.st[1], &b = q.st[2];
+    if (b.kind != kg::K_LOGICAL || a.partner != 2 || b.partner != 1 || a.ltype != b.ltype) return k;
+    for (const auto* x : {&a, &b})
+      if (x->is_start || x->next_pre != -1 || x->next_every != -1 || !x->has_selector) return k;
+    if (e1.next_pre != 1 && e1.next_pre != 2) return k;
+    if (!((procs[1] == 1 && procs[2] == 2) || (procs[1] == 2 && procs[2] == 1))) return k;
+    for (int i = 1; i <= 2; ++i) {  // the sides' filters read only their own slot (event-only)
+      r.clear();
+      filter_refs(q.st[i], r);
+      for (const auto& x : r)
+        if (x.first != i) return k;
+    }
+    k.sA = procs[1];  // registration order: the side processed second
+    k.sB = procs[2];
+    k.kind = a.ltype == kg::L_AND ? PK_AND : PK_OR;
+    return k;
+  }
+  const kg::LState &c = q.st[1], &e3 = q.st[2];
+  if (c.kind != kg::K_COUNT || c.min < 1 || c.max > PK_CMAX || c.min > c.max) return k;
+  if (c.next_pre != 2 || c.next_every != -1 || c.has_selector || e1.next_pre != 1) return k;
+  if (e3.kind != kg::K_STREAM || e3.next_pre != -1 || e3.next_every != -1 || !e3.has_selector) return k;
+  if (procs[1] != 1 || procs[2] != 2) return k;
+  r.clear();
+  filter_refs(c, r);  // the count filter reads only the event it is appending (CURRENT)
+  for (const auto& x : r)
+    if (x.first != 1 || x.second != -1) return k;
+  r.clear();
+  filter_refs(e3, r);  // e3 reads e1, e2[0], e2[last] (= CURRENT of another state) and itself
+  const int ncap = g.n_cap[s];
+  for (const auto& x : r) {
+    if (x.first == 1) {
+      if (x.second == 0) k.n_first = ncap;
+      else if (x.second == -1) k.n_last = ncap;
+      else return k;
+    } else if (x.first == 0) {
+      k.n_e1 = ncap;
+    }
+  }
+  r.clear();
+  filter_refs(e1, r);
+  k.cmax = c.max;
+  k.kind = PK_COUNT;
+  return k;
+}
+
 void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   kg::Sizing sz;
   if (e->cfg.gen_pool_states > 0) sz.R = std::min(64, e->cfg.gen_pool_states);
   if (e->cfg.gen_pool_nodes > 0) sz.N = std::min(256, e->cfg.gen_pool_nodes);
   if (e->cfg.gen_list_cap > 0) sz.LC = e->cfg.gen_list_cap;
   std::vector<int> gidx(e->lp.q.size(), -1);
+  std::vector<KPart> kpart(e->lp.q.size());
+  const bool use_part = !(e->cfg.flags & SDH_FLAG_FORCE_GEN) && !getenv("SDH_NO_KPART");
   for (int qi : qis) {
     try {
       kg::GQuery g = kg::lower_gen(e->lp, qi, sz);
@@ -1230,6 +1328,8 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
       if (7 + g.lay.S + g.lay.N > GEN_RING_MARGIN) throw kg::LowerError("match record longer than the ring margin");
       gidx[qi] = (int)e->gq.size();
       e->gq.push_back(g);
+      if (use_part) kpart[qi] = kpart_shape(e->lp, qi, g);
+      if (kpart[qi].kind >= 0) continue;  // K_part: no K_gen arena
       e->gB32 = std::max(e->gB32, g.lay.n32);
       e->gB64 = std::max(e->gB64, g.lay.n64);
       e->gHotS = std::max(e->gHotS, g.lay.S);
@@ -1239,15 +1339,8 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
     }
   }
   if (e->gq.empty()) return;
-  // sets: the unpartitioned queries, then one per partition; 64 queries per group (wave)
-  auto add_set = [&](int partition, const std::vector<int>& members) {
-    if (members.empty()) return;
-    auto gs = std::make_unique<sdh_engine::GenSet>();
-    gs->partition = partition;
-    gs->group_base = (int)(e->lane_q.size() / 64);
-    // one shape per group: members are bucketed by kg::shape_of (first-appearance order) and each
-    // bucket is padded to whole groups, so a wave's control flow is its template's. Lane order is
-    // free: matches are ordered on the host by (seq, out_rank, emission index).
+  // lane_q / group_tmpl rows of one set's members, bucketed by shape (see add_set)
+  auto add_groups = [&](const std::vector<int>& members, bool seq_ok) {
     std::vector<std::pair<std::string, std::vector<int>>> shapes;
     for (int qi : members) {
       const kg::GQuery sh = kg::shape_of(e->gq[gidx[qi]]);
@@ -1256,10 +1349,10 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
       if (it == shapes.end()) shapes.emplace_back(std::move(sig), std::vector<int>{gidx[qi]});
       else it->second.push_back(gidx[qi]);
     }
-    gs->n_groups = 0;
+    int n_groups = 0;
     for (const auto& b : shapes) {
       const int ng = (int)((b.second.size() + 63) / 64);
-      const int S = (partition < 0 && !(e->cfg.flags & SDH_FLAG_FORCE_GEN)) ? kg::seq_window(e->gq[b.second[0]]) : -1;
+      const int S = (seq_ok && !(e->cfg.flags & SDH_FLAG_FORCE_GEN)) ? kg::seq_window(e->gq[b.second[0]]) : -1;
       for (int g = 0; g < ng; ++g) {
         e->group_seq.push_back(S > 0 ? S : 0);
         e->group_tmpl.push_back(b.second[0]);
@@ -1268,8 +1361,72 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
           e->lane_q.push_back(k < b.second.size() ? b.second[k] : -1);
         }
       }
-      gs->n_groups += ng;
+      n_groups += ng;
     }
+    return n_groups;
+  };
+  auto route_of = [&](int partition) {
+    if ((int)e->routes.size() <= partition) e->routes.resize(partition + 1);
+    if (e->routes[partition]) return;
+    auto r = std::make_unique<sdh_engine::Route>();
+    r->max_keys = e->cfg.gen_max_keys > 0 ? e->cfg.gen_max_keys : (1 << 20);
+    int64_t slots = 1;
+    while (slots < 2 * r->max_keys) slots <<= 1;
+    r->tmask = slots - 1;
+    r->tkey.ensure(slots + 1);
+    r->tid.ensure(slots + 1);
+    std::vector<unsigned long long> init((size_t)slots + 1, 0x8000000000000000ull);
+    init[slots] = 0;
+    HIPCHK(hipMemcpy(r->tkey.p, init.data(), init.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(r->tid.p, 0xff, (slots + 1) * 4));
+    r->n_keys.ensure(1);
+    HIPCHK(hipMemset(r->n_keys.p, 0, 4));
+    r->key_of_id.ensure(r->max_keys);
+    e->routes[partition] = std::move(r);
+  };
+  auto add_part_sets = [&](int partition, const std::vector<int>& members) {
+    for (int kind = PK_OR; kind <= PK_COUNT; ++kind) {
+      std::vector<int> m;
+      for (int qi : members)
+        if (kpart[qi].kind == kind) m.push_back(qi);
+      if (m.empty()) continue;
+      route_of(partition);
+      auto ps = std::make_unique<sdh_engine::PartSet>();
+      ps->partition = partition;
+      ps->kind = kind;
+      ps->group_base = (int)(e->lane_q.size() / 64);
+      ps->n_groups = add_groups(m, false);
+      const KPart& k0 = kpart[m[0]];
+      ps->sA = k0.sA;
+      ps->sB = k0.sB;
+      for (int qi : m) {
+        ps->cmax = std::max(ps->cmax, kpart[qi].cmax);
+        ps->n_e1 = std::max(ps->n_e1, kpart[qi].n_e1);
+        ps->n_first = std::max(ps->n_first, kpart[qi].n_first);
+        ps->n_last = std::max(ps->n_last, kpart[qi].n_last);
+        if (kpart[qi].sA != ps->sA || kpart[qi].sB != ps->sB) throw Error(SDH_E_UNSUPPORTED, "K_part side order");
+      }
+      ps->ew = kind == PK_COUNT ? 3 + ps->cmax + ps->n_e1 + ps->n_first + ps->n_last : 3;
+      ps->cap = kind == PK_COUNT ? 8 : 16;
+      if (const char* v = getenv("SDH_KPART_CAP")) ps->cap = std::max(1, atoi(v));
+      e->psets.push_back(std::move(ps));
+    }
+  };
+  // sets: the unpartitioned queries, then one per partition; 64 queries per group (wave)
+  auto add_set = [&](int partition, const std::vector<int>& members) {
+    if (members.empty()) return;
+    std::vector<int> gen_m;
+    for (int qi : members)
+      if (kpart[qi].kind < 0) gen_m.push_back(qi);
+    if (partition >= 0) add_part_sets(partition, members);
+    if (gen_m.empty()) return;
+    auto gs = std::make_unique<sdh_engine::GenSet>();
+    gs->partition = partition;
+    gs->group_base = (int)(e->lane_q.size() / 64);
+    // one shape per group: members are bucketed by kg::shape_of (first-appearance order) and each
+    // bucket is padded to whole groups, so a wave's control flow is its template's. Lane order is
+    // free: matches are ordered by (seq, out_rank, emission index) in the device match table.
+    gs->n_groups = add_groups(gen_m, partition < 0);
     const size_t per_block32 = (size_t)e->gB32 * 64, per_block64 = (size_t)e->gB64 * 64;
     if (partition < 0) {
       gs->a32.ensure(per_block32 * gs->n_groups);
@@ -1277,19 +1434,7 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
       HIPCHK(hipMemset(gs->a32.p, 0, per_block32 * gs->n_groups * 4));
       HIPCHK(hipMemset(gs->a64.p, 0, per_block64 * gs->n_groups * 8));
     } else {
-      gs->max_keys = e->cfg.gen_max_keys > 0 ? e->cfg.gen_max_keys : (1 << 20);
-      int64_t slots = 1;
-      while (slots < 2 * gs->max_keys) slots <<= 1;
-      gs->tmask = slots - 1;
-      gs->tkey.ensure(slots + 1);
-      gs->tid.ensure(slots + 1);
-      std::vector<unsigned long long> init((size_t)slots + 1, 0x8000000000000000ull);
-      init[slots] = 0;
-      HIPCHK(hipMemcpy(gs->tkey.p, init.data(), init.size() * 8, hipMemcpyHostToDevice));
-      HIPCHK(hipMemset(gs->tid.p, 0xff, (slots + 1) * 4));
-      gs->n_keys.ensure(1);
-      HIPCHK(hipMemset(gs->n_keys.p, 0, 4));
-      gs->key_of_id.ensure(gs->max_keys);
+      route_of(partition);
       gs->key_cap = 0;
     }
     e->gsets.push_back(std::move(gs));
@@ -1319,6 +1464,7 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   HIPCHK(hipMemcpy(e->d_group_tmpl.p, e->group_tmpl.data(), e->group_tmpl.size() * 4, hipMemcpyHostToDevice));
   e->g_out_next.ensure(1);
   e->g_nrec.ensure(1);
+  e->d_perr.ensure(std::max<size_t>(1, e->psets.size()) * 4);
 }
 
 // grow a partition set's instance arena to hold `keys` keys (blocks are key-major: a prefix copy)
@@ -1347,6 +1493,74 @@ void gen_grow(sdh_engine* e, sdh_engine::GenSet& gs, int64_t keys) {
 
 
 // one K_gen step for every set fed by `stream`
+sdh::GenLaunch gen_launch_base(sdh_engine* e, const sdh_engine::GenSet& gs, const StreamBatch& B, bool write) {
+  sdh::GenLaunch L{};
+  L.queries = e->d_gq.p;
+  L.lane_q = e->d_lane_q.p;
+  L.group_tmpl = e->d_group_tmpl.p;
+  L.b = B;
+  L.groups = gs.n_groups;
+  L.group_base = gs.group_base;
+  L.B32 = e->gB32;
+  L.B64 = e->gB64;
+  L.hot_s = e->gHotS;
+  L.hot_nu = e->gHotNU;
+  L.out = e->g_out.p;
+  L.out_cap = e->g_out_cap;
+  L.out_next = e->g_out_next.p;
+  L.err = e->d_err.p;
+  L.rec_count = e->g_nrec.p;
+  L.rec_off = e->g_rec_off.p;
+  L.rec_cap = e->g_out_cap / 7 + 1;
+  L.rec_next = e->g_rec_next.p;
+  L.write_records = write ? 1 : 2;
+  return L;
+}
+
+// K_part state: room for `keys` keys (new keys' blocks start empty: n = 0, buffer 0)
+void part_grow(sdh_engine* e, sdh_engine::PartSet& ps, int64_t keys) {
+  if (keys <= ps.key_cap) return;
+  int64_t cap = std::max<int64_t>(64, ps.key_cap);
+  while (cap < keys) cap *= 2;
+  const size_t per_key = (size_t)ps.n_groups * ps.bw() * 64;  // int64 words per key and buffer
+  DevBuf<int64_t> nst;
+  DevBuf<int32_t> ncur, nnxt;
+  nst.ensure(2 * per_key * cap);
+  ncur.ensure(cap);
+  nnxt.ensure(cap);
+  HIPCHK(hipMemsetAsync(nst.p, 0, 2 * per_key * cap * 8, e->stream));
+  HIPCHK(hipMemsetAsync(ncur.p, 0, cap * 4, e->stream));
+  if (ps.key_cap > 0)
+    for (int b = 0; b < 2; ++b)
+      HIPCHK(hipMemcpyAsync(nst.p + b * per_key * cap, ps.st.p + b * per_key * ps.key_cap, per_key * ps.key_cap * 8,
+                            hipMemcpyDeviceToDevice, e->stream));
+  if (ps.key_cap > 0) HIPCHK(hipMemcpyAsync(ncur.p, ps.cur.p, ps.key_cap * 4, hipMemcpyDeviceToDevice, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  std::swap(ps.st.p, nst.p);
+  std::swap(ps.st.n, nst.n);
+  std::swap(ps.cur.p, ncur.p);
+  std::swap(ps.cur.n, ncur.n);
+  std::swap(ps.nxt.p, nnxt.p);
+  std::swap(ps.nxt.n, nnxt.n);
+  ps.key_cap = cap;
+}
+
+// K_part entry capacity x2: every block keeps its header and entries at the same word offsets
+void part_grow_cap(sdh_engine* e, sdh_engine::PartSet& ps) {
+  const int64_t blocks = 2 * ps.key_cap * ps.n_groups, obw = ps.bw();
+  ps.cap *= 2;
+  if (ps.key_cap == 0) return;
+  const int64_t nbw = ps.bw();
+  DevBuf<int64_t> nst;
+  nst.ensure((size_t)(blocks * nbw * 64));
+  HIPCHK(hipMemsetAsync(nst.p, 0, (size_t)blocks * nbw * 64 * 8, e->stream));
+  HIPCHK(hipMemcpy2DAsync(nst.p, (size_t)nbw * 64 * 8, ps.st.p, (size_t)obw * 64 * 8, (size_t)obw * 64 * 8, (size_t)blocks,
+                          hipMemcpyDeviceToDevice, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  std::swap(ps.st.p, nst.p);
+  std::swap(ps.st.n, nst.n);
+}
+
 // One pass of every K_gen / K_seq launch of a push over `stream` (partition routing, arena growth,
 // kernels, the event-chunk copy-backs). Returns whether anything ran; *tail_new_len (>= 0) is the
 // stream's K_seq tail length once the pass is accepted.
@@ -1358,29 +1572,12 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
   bool any = false;
   e->stats.last_gen_items = 0;
   e->stats.last_seq_items = 0;
+  e->stats.last_part_items = 0;
   for (auto& up : e->gsets) {
     auto& gs = *up;
-    sdh::GenLaunch L{};
-    L.queries = e->d_gq.p;
-    L.lane_q = e->d_lane_q.p;
-    L.group_tmpl = e->d_group_tmpl.p;
-    L.b = B;
-    L.groups = gs.n_groups;
-    L.group_base = gs.group_base;
-    L.B32 = e->gB32;
-    L.B64 = e->gB64;
-    L.hot_s = e->gHotS;
-    L.hot_nu = e->gHotNU;
-    L.out = e->g_out.p;
-    L.out_cap = e->g_out_cap;
-    L.out_next = e->g_out_next.p;
-    L.err = e->d_err.p;
-    L.rec_count = e->g_nrec.p;
-    L.rec_off = e->g_rec_off.p;
-    L.rec_cap = e->g_out_cap / 7 + 1;
-    L.rec_next = e->g_rec_next.p;
-    L.write_records = write ? 1 : 2;
-    if (gs.partition < 0) {
+    if (gs.partition >= 0) continue;  // partitions below
+    sdh::GenLaunch L = gen_launch_base(e, gs, B, write);
+    {
       // groups reading this stream: windowed sequences go to K_seq, the rest to K_gen
       std::vector<int32_t> seq_rows, gen_groups;
       int seqS = 1;
@@ -1480,12 +1677,24 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       bytes += (double)n * ev_bytes * gen_groups.size();  // every group streams the batch once
       continue;
     }
-    // partitioned: the partition's key attribute of this stream
-    const kg::LPart& pd = e->lp.parts[gs.partition];
+  }
+  // partitions: route the batch once (dense key ids, events grouped by key), then run the
+  // partition's K_gen set and its K_part sets over the same segments
+  for (int pi = 0; pi < (int)e->routes.size(); ++pi) {
+    if (!e->routes[pi]) continue;
+    auto& rt = *e->routes[pi];
+    const kg::LPart& pd = e->lp.parts[pi];
     int attr = -1;
     for (const auto& k : pd.keys)
       if (k.stream == stream) attr = (int)k.code[0].imm;
     if (attr < 0) continue;
+    sdh_engine::GenSet* gsp = nullptr;
+    for (auto& up : e->gsets)
+      if (up->partition == pi) gsp = up.get();
+    bool reads = gsp && gsp->n_groups > 0;
+    for (auto& ps : e->psets)
+      if (ps->partition == pi) reads = true;
+    if (!reads) continue;
     const int type = e->lp.stream_types[stream][attr];
     e->r_key.ensure(n);
     e->r_kid.ensure(n);
@@ -1498,29 +1707,81 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
     e->r_nruns.ensure(1);
     const size_t tb = sdh_route_temp_bytes(n);
     e->r_temp.ensure(tb);
-    HIPCHK(sdh_route_partition(&B, attr, type, gs.tkey.p, gs.tid.p, gs.tmask, gs.n_keys.p, gs.key_of_id.p,
-                               gs.max_keys, e->r_key.p, e->r_kid.p, e->r_kid_s.p, e->r_idx.p, e->r_idx_s.p,
+    HIPCHK(sdh_route_partition(&B, attr, type, rt.tkey.p, rt.tid.p, rt.tmask, rt.n_keys.p, rt.key_of_id.p,
+                               rt.max_keys, e->r_key.p, e->r_kid.p, e->r_kid_s.p, e->r_idx.p, e->r_idx_s.p,
                                e->r_uniq.p, e->r_cnt.p, e->r_off.p, e->r_nruns.p, e->r_temp.p, e->r_temp.n,
                                e->d_err.p + 3, e->cfg.shard_rank, e->cfg.shard_world, e->stream));
     int32_t hv[2];
-    HIPCHK(hipMemcpyAsync(&hv[0], gs.n_keys.p, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&hv[0], rt.n_keys.p, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&hv[1], e->r_nruns.p, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    if (hv[0] > gs.max_keys) throw Error(SDH_E_CAPACITY, "more partition keys than gen_max_keys");
-    gen_grow(e, gs, hv[0]);
-    L.a32 = gs.a32.p;
-    L.a64 = gs.a64.p;
-    L.seg_begin = e->r_off.p;
-    L.seg_len = e->r_cnt.p;
-    L.seg_kid = e->r_uniq.p;
-    L.key_of_id = gs.key_of_id.p;
-    L.ev_idx = e->r_idx_s.p;
-    L.n_items = hv[1] * gs.n_groups;
-    HIPCHK(sdh_launch_gen(&L, e->stream));
-    e->stats.last_gen_items += L.n_items;
-    any = true;
-    // routing (key column read, key/kid/idx written and sorted) + every group streaming its keys' events
-    bytes += (double)n * (8 + 8 + 4 + 4 + 2 * (4 + 4) + 3 * 4) + (double)n * ev_bytes * gs.n_groups;
+    if (hv[0] > rt.max_keys) throw Error(SDH_E_CAPACITY, "more partition keys than gen_max_keys");
+    // routing (key column read, key/kid/idx written and sorted)
+    bytes += (double)n * (8 + 8 + 4 + 4 + 2 * (4 + 4) + 3 * 4);
+    if (gsp && gsp->n_groups > 0) {
+      auto& gs = *gsp;
+      gen_grow(e, gs, hv[0]);
+      sdh::GenLaunch L = gen_launch_base(e, gs, B, write);
+      L.a32 = gs.a32.p;
+      L.a64 = gs.a64.p;
+      L.seg_begin = e->r_off.p;
+      L.seg_len = e->r_cnt.p;
+      L.seg_kid = e->r_uniq.p;
+      L.key_of_id = rt.key_of_id.p;
+      L.ev_idx = e->r_idx_s.p;
+      L.n_items = hv[1] * gs.n_groups;
+      HIPCHK(sdh_launch_gen(&L, e->stream));
+      e->stats.last_gen_items += L.n_items;
+      any = true;
+      bytes += (double)n * ev_bytes * gs.n_groups;  // every group streams its keys' events
+    }
+    for (size_t si = 0; si < e->psets.size(); ++si) {
+      auto& ps = *e->psets[si];
+      if (ps.partition != pi) continue;
+      part_grow(e, ps, hv[0]);
+      sdh::PartLaunch P{};
+      P.queries = e->d_gq.p;
+      P.lane_q = e->d_lane_q.p;
+      P.group_tmpl = e->d_group_tmpl.p;
+      P.b = B;
+      P.seg_begin = e->r_off.p;
+      P.seg_len = e->r_cnt.p;
+      P.seg_kid = e->r_uniq.p;
+      P.key_of_id = rt.key_of_id.p;
+      P.ev_idx = e->r_idx_s.p;
+      P.groups = ps.n_groups;
+      P.group_base = ps.group_base;
+      P.kind = ps.kind;
+      P.cap = ps.cap;
+      P.ew = ps.ew;
+      P.sA = ps.sA;
+      P.sB = ps.sB;
+      P.cmax = ps.cmax;
+      P.n_e1 = ps.n_e1;
+      P.n_first = ps.n_first;
+      P.n_last = ps.n_last;
+      P.n_items = hv[1] * ps.n_groups;
+      P.st = ps.st.p;
+      P.blocks = ps.key_cap * ps.n_groups;
+      P.cur = ps.cur.p;
+      P.nxt = ps.nxt.p;
+      P.out = e->g_out.p;
+      P.out_cap = e->g_out_cap;
+      P.out_next = e->g_out_next.p;
+      P.rec_count = e->g_nrec.p;
+      P.rec_off = e->g_rec_off.p;
+      P.rec_cap = e->g_out_cap / 7 + 1;
+      P.rec_next = e->g_rec_next.p;
+      P.write_records = write ? 1 : 2;
+      P.err = e->d_perr.p + 4 * si;
+      // the per-key buffer selector of untouched keys carries over
+      HIPCHK(hipMemcpyAsync(ps.nxt.p, ps.cur.p, (size_t)ps.key_cap * 4, hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(sdh_launch_part(&P, e->stream));
+      ps.ran = true;
+      e->stats.last_part_items += P.n_items;
+      any = true;
+      bytes += (double)n * ev_bytes * ps.n_groups;
+    }
   }
   *bytes_out = bytes;
   return any;
@@ -1573,17 +1834,20 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   e->d_err.ensure(4);
   e->g_rec_next.ensure(1);
   const bool write = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) == 0;
-  const bool backed = write && gen_backup(e);
+  const bool backed = (write || !e->psets.empty()) && gen_backup(e);
   double bytes = 0;
   int32_t tail_len = -1;
   bool any = false;
   int32_t errs[4] = {0, 0, 0, 0};
   unsigned long long nrec = 0, used = 0;
   float ms = 0;
+  const size_t nps = e->psets.size();
+  std::vector<int32_t> perr(4 * std::max<size_t>(1, nps), 0);
   for (int attempt = 0;; ++attempt) {
     e->g_out.ensure((size_t)e->g_out_cap);
     e->g_rec_off.ensure((size_t)(e->g_out_cap / 7 + 1));  // a record has at least 7 words
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
+    HIPCHK(hipMemsetAsync(e->d_perr.p, 0, perr.size() * 4, e->stream));
     HIPCHK(hipMemsetAsync(e->g_out_next.p, 0, 8, e->stream));
     HIPCHK(hipMemsetAsync(e->g_nrec.p, 0, 8, e->stream));
     HIPCHK(hipMemsetAsync(e->g_rec_next.p, 0, 8, e->stream));
@@ -1591,19 +1855,42 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     any = gen_pass(e, stream, B, write, &bytes, &tail_len);
     HIPCHK(hipEventRecord(e->ev1, e->stream));
     HIPCHK(hipMemcpyAsync(errs, e->d_err.p, 16, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(perr.data(), e->d_perr.p, perr.size() * 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&nrec, e->g_nrec.p, 8, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&used, e->g_out_next.p, 8, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
-    if (errs[2] && backed && attempt == 0 && !errs[0] && !errs[1] && !errs[3]) {
-      // the match output overflowed: undo the pass and re-run it with room for every record
-      // (out_next counts the words every record asked for)
+    bool out_over = errs[2] != 0, part_over = false;
+    for (size_t i = 0; i < nps; ++i) {
+      out_over |= perr[4 * i + 2] != 0;
+      part_over |= perr[4 * i] != 0;
+    }
+    if ((out_over || part_over) && backed && attempt < 12 && !errs[0] && !errs[1] && !errs[3]) {
+      // undo the pass (K_gen arenas from the backup; K_part tables are double-buffered and their
+      // per-key selectors are swapped only after success) and re-run it with room for every match
+      // record (out_next counts the words every record asked for) and every K_part partial
       gen_restore_backup(e);
-      while (e->g_out_cap < (int64_t)used + (int64_t)used / 4 + GEN_RING_MARGIN) e->g_out_cap *= 2;
+      if (out_over)
+        while (e->g_out_cap < (int64_t)used + (int64_t)used / 4 + GEN_RING_MARGIN) e->g_out_cap *= 2;
+      for (size_t i = 0; i < nps; ++i)
+        if (perr[4 * i]) {
+          if (e->psets[i]->cap >= (1 << 16))
+            throw Error(SDH_E_CAPACITY, "more than 65536 pending partials in one K_part instance");
+          part_grow_cap(e, *e->psets[i]);
+        }
       continue;
     }
+    if (part_over)
+      throw Error(SDH_E_CAPACITY, "K_part partial table overflow (no room for an exact re-run)");
     break;
   }
+  // the push succeeded: the K_part tables it wrote become current
+  for (auto& pp : e->psets)
+    if (pp->ran) {
+      std::swap(pp->cur.p, pp->nxt.p);
+      std::swap(pp->cur.n, pp->nxt.n);
+      pp->ran = false;
+    }
   if (tail_len >= 0 && !errs[0] && !errs[1] && !errs[3]) {
     HIPCHK(sdh_seq_tail(&B, e->seq_tail[stream].p, e->seq_tail_len[stream], tail_len, e->stream));
     e->seq_tail_len[stream] = tail_len;
@@ -1975,7 +2262,7 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
 // snapshot: [magic][version][n_q][pcap][gB32][gB64][seq][n_streams][prev_ts...] then per query
 // header + table, ratchet deques, K_gen arenas + key tables, K_seq tails
 constexpr int64_t SNAP_MAGIC = 0x5344485350415254LL;
-constexpr int64_t SNAP_VERSION = 2;
+constexpr int64_t SNAP_VERSION = 3;
 int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
   if (!e || !blob || !len) return SDH_E_INVALID;
   return guard(e, [&]() {
@@ -2031,14 +2318,29 @@ int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
       w.push_back(blocks);
       put_dev(gs.a32.p, (size_t)blocks * e->gB32 * 64 * 4);
       put_dev(gs.a64.p, (size_t)blocks * e->gB64 * 64 * 8);
-      if (gs.partition >= 0) {
-        const size_t slots = (size_t)gs.tmask + 2;
-        w.push_back((int64_t)slots);
-        put_dev(gs.tkey.p, slots * 8);
-        put_dev(gs.tid.p, slots * 4);
-        put_dev(gs.n_keys.p, 4);
-        put_dev(gs.key_of_id.p, (size_t)gs.max_keys * 8);
-      }
+    }
+    // partition key tables (PartitionRuntime's key -> instance map)
+    w.push_back((int64_t)e->routes.size());
+    for (auto& rp : e->routes) {
+      w.push_back(rp ? 1 : 0);
+      if (!rp) continue;
+      const size_t slots = (size_t)rp->tmask + 2;
+      w.push_back((int64_t)slots);
+      put_dev(rp->tkey.p, slots * 8);
+      put_dev(rp->tid.p, slots * 4);
+      put_dev(rp->n_keys.p, 4);
+      put_dev(rp->key_of_id.p, (size_t)rp->max_keys * 8);
+    }
+    // K_part tables: both buffers and the per-key selector
+    w.push_back((int64_t)e->psets.size());
+    for (auto& pp : e->psets) {
+      auto& ps = *pp;
+      w.push_back(ps.partition);
+      w.push_back(ps.kind);
+      w.push_back(ps.cap);
+      w.push_back(ps.key_cap);
+      put_dev(ps.st.p, (size_t)2 * ps.key_cap * ps.n_groups * ps.bw() * 64 * 8);
+      put_dev(ps.cur.p, (size_t)ps.key_cap * 4);
     }
     // K_seq: each stream's tail (the only state its windowed sequences carry between pushes)
     w.push_back((int64_t)e->seq_tail.size());
@@ -2122,14 +2424,34 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
       if (blocks != want_blocks) throw Error(SDH_E_INVALID, "snapshot arena size mismatch");
       get_dev(gs.a32.p, (size_t)blocks * e->gB32 * 64 * 4);
       get_dev(gs.a64.p, (size_t)blocks * e->gB64 * 64 * 8);
-      if (gs.partition >= 0) {
-        const size_t slots = (size_t)nx();
-        if (slots != (size_t)gs.tmask + 2) throw Error(SDH_E_INVALID, "snapshot key table mismatch");
-        get_dev(gs.tkey.p, slots * 8);
-        get_dev(gs.tid.p, slots * 4);
-        get_dev(gs.n_keys.p, 4);
-        get_dev(gs.key_of_id.p, (size_t)gs.max_keys * 8);
-      }
+    }
+    if ((size_t)nx() != e->routes.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
+    for (auto& rp : e->routes) {
+      if (nx() != (rp ? 1 : 0)) throw Error(SDH_E_INVALID, "snapshot of a different program");
+      if (!rp) continue;
+      const size_t slots = (size_t)nx();
+      if (slots != (size_t)rp->tmask + 2) throw Error(SDH_E_INVALID, "snapshot key table mismatch");
+      get_dev(rp->tkey.p, slots * 8);
+      get_dev(rp->tid.p, slots * 4);
+      get_dev(rp->n_keys.p, 4);
+      get_dev(rp->key_of_id.p, (size_t)rp->max_keys * 8);
+    }
+    if ((size_t)nx() != e->psets.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
+    for (auto& pp : e->psets) {
+      auto& ps = *pp;
+      if (nx() != ps.partition || nx() != ps.kind) throw Error(SDH_E_INVALID, "snapshot of a different program");
+      const int64_t cap = nx(), key_cap = nx();
+      if (cap < 1 || cap > (1 << 20) || key_cap < 0 || key_cap > (int64_t)1 << 40)
+        throw Error(SDH_E_INVALID, "bad snapshot K_part table size");
+      ps.cap = (int)cap;
+      ps.key_cap = 0;
+      ps.st.n = 0;  // reallocated at the snapshot's capacity
+      if (ps.st.p) HIPCHK(hipFree(ps.st.p));
+      ps.st.p = nullptr;
+      part_grow(e, ps, key_cap);
+      if (ps.key_cap != key_cap) throw Error(SDH_E_INVALID, "snapshot key capacity mismatch");
+      get_dev(ps.st.p, (size_t)2 * ps.key_cap * ps.n_groups * ps.bw() * 64 * 8);
+      get_dev(ps.cur.p, (size_t)ps.key_cap * 4);
     }
     if ((size_t)nx() != e->seq_tail.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
     for (size_t st = 0; st < e->seq_tail.size(); ++st) {

@@ -285,11 +285,13 @@ struct PartLaunch {
   int32_t cap;                // entries per lane
   int32_t ew;                 // words per entry
   int32_t sA, sB;             // logical: state ids of the side processed second (A) and first (B)
-  int32_t cmin, cmax;         // count
+  int32_t cmax;               // count: chain words per entry (the set's largest max)
   int32_t n_e1, n_first, n_last;  // count: captured words stored per entry (0 or the stream's n_cap)
   int32_t n_items;
-  const int64_t* st_in;       // [block][PK_HDR + cap * ew][64]
-  int64_t* st_out;
+  int64_t* st;                // [buffer 0/1][block][PK_HDR + cap * ew][64], block = kid * groups + g
+  int64_t blocks;             // blocks per buffer
+  const int32_t* cur;         // [kid] buffer holding the key's tables before this push
+  int32_t* nxt;               // [kid] after it (the host swaps cur / nxt once the push succeeded)
   int64_t* out;               // K_gen-format match records (nfa_gen.hip), as GenLaunch
   int64_t out_cap;
   unsigned long long* out_next;
