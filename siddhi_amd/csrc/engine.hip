@@ -1257,7 +1257,9 @@ KPart kpart_shape(const kg::LProgram& P, int qi, const kg::GQuery& g) {
   KPart k;
   const kg::LQuery& q = P.q[qi];
   if (q.partition < 0 || q.type != kg::Q_PATTERN || q.st.size() != 3) return k;
-  if (q.start_ids.size() != 1 || q.start_ids[0] != 0 || g.max_depth > kg::RSTACK) return k;
+  // start ids exist only with `within` (StateInputStreamParser.java:126-138): then e1 alone
+  if (!(q.start_ids.empty() || (q.start_ids.size() == 1 && q.start_ids[0] == 0)) || g.max_depth > kg::RSTACK) return k;
+  if (q.start_ids.empty() && q.within >= 0) return k;
   const int s = q.st[0].stream;
   for (const auto& x : q.st)
     if (x.stream != s || x.within_every != -1 || x.callback != -1) return k;
@@ -1827,7 +1829,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   *bytes_out = 0;
   e->stats.last_gen_items = 0;
   e->stats.last_seq_items = 0;
-  if (e->gsets.empty()) return;
+  if (e->gsets.empty() && e->psets.empty()) return;
   const int64_t n = B.n;
   e->g_out_cap = std::max<int64_t>(e->g_out_cap, std::max<int64_t>(1 << 22, n * 64));
   static_assert((1 << 22) > 2 * GEN_RING_MARGIN, "ring capacity");

@@ -82,6 +82,28 @@ struct GLayout {
   int32_t v32;  // node attribute words in the 32-bit arena (every captured type is 4 bytes or less)
 };
 
+// K_seq compare atoms: a state's filters as a conjunction of typed compares whose operands are a
+// leaf (a slot's attribute word or a bytecode constant) or one arithmetic op over two leaves -- the
+// same Java semantics as eval_code, without the evaluation stack (kg::lower_atoms, seq_match)
+constexpr int GMAXATOM = 16;
+enum { LF_ATTR = 0, LF_CONST = 1, LF_NULL = 2 };
+struct GLeaf {
+  int8_t kind, slot, cap, type;
+  int16_t pc;  // LF_CONST: instruction whose imm is the (per-lane) constant
+  int16_t pad;
+};
+struct GOpnd {
+  GLeaf a, b;
+  int8_t arith;  // -1: leaf a alone; else AR_* over (a, b) with operand types a.type / b.type
+  int8_t res;
+  int8_t pad[6];
+};
+struct GAtom {
+  int8_t state, op, lt, rt;
+  int32_t pad;
+  GOpnd l, r;
+};
+
 struct GQuery {
   int32_t qid, type, n_states, partition, rank;
   int32_t pad0;
@@ -98,6 +120,9 @@ struct GQuery {
   int32_t n_code;
   int32_t max_depth;  // deepest evaluation stack of any filter (kg::code_depth)
   GInsn code[GMAXCODE];
+  int32_t n_atoms;    // > 0: every filter lowered to atoms (atom_begin[i] .. atom_begin[i+1] of state i)
+  int32_t atom_begin[GMAXS + 1];
+  GAtom atoms[GMAXATOM];
 };
 
 // ---- Java value semantics (executor/condition/compare/**, executor/math/**) ----
@@ -989,6 +1014,39 @@ inline int seq_window(const GQuery& g) {
 // hold one event each, so eK / eK[0] / eK[last] name it and every other index is null
 // (StateEvent.getStreamEvent:138-182 on a one-event chain); state i's filter sees slots 0 .. i.
 template <class Win>
+KG_FN Val atom_leaf(const GLeaf& f, const GQuery* ql, const Win& w) {
+  Val v{f.type, 1, 0};
+  if (f.kind == LF_CONST) {
+    const int64_t imm = ql->code[f.pc].imm;
+    v.null = 0;
+    v.bits = f.type == T_FLOAT ? (int64_t)(uint32_t)imm : f.type == T_INT ? (int64_t)(int32_t)imm : imm;
+  } else if (f.kind == LF_ATTR && !w.null(f.slot, f.cap)) {
+    const int64_t raw = w.raw(f.slot, f.cap);
+    v.null = 0;
+    v.bits = f.type == T_INT ? (int64_t)(int32_t)raw : f.type == T_FLOAT ? (int64_t)(uint32_t)raw : raw;
+  }
+  return v;
+}
+template <class Win>
+KG_FN Val atom_opnd(const GOpnd& o, const GQuery* ql, const Win& w) {
+  Val a = atom_leaf(o.a, ql, w);
+  if (o.arith < 0) return a;
+  return arith(o.arith, o.res, a, atom_leaf(o.b, ql, w));
+}
+// the atoms of state i over window w (FilterProcessor + the typed compare / arithmetic executors)
+template <class Win>
+KG_FN bool atoms_pass(const GQuery* q, const GQuery* ql, int i, const Win& w) {
+  for (int t = q->atom_begin[i]; t < q->atom_begin[i + 1]; ++t) {
+    const GAtom& A = q->atoms[t];
+    Val l = atom_opnd(A.l, ql, w), r = atom_opnd(A.r, ql, w);
+    l.type = A.lt;
+    r.type = A.rt;
+    if (l.null || r.null || !typed_compare(A.op, l, r)) return false;
+  }
+  return true;
+}
+
+template <class Win>
 KG_FN bool seq_match(const GQuery* q, const GQuery* ql, int64_t within, const Win& w) {
   const int S = q->n_states;
   for (int i = 0; i < S; ++i) {
@@ -996,6 +1054,10 @@ KG_FN bool seq_match(const GQuery* q, const GQuery* ql, int64_t within, const Wi
       const int64_t d = (int64_t)((uint64_t)w.ts(0) - (uint64_t)w.ts(i));
       const int64_t a = d < 0 ? (int64_t)(0ull - (uint64_t)d) : d;
       if (a > within) return false;
+    }
+    if (q->n_atoms != 0) {  // the shape's filters are atoms (wave-uniform choice)
+      if (!atoms_pass(q, ql, i, w)) return false;
+      continue;
     }
     const GState& st = q->st[i];
     for (int f = 0; f < st.n_filt; ++f) {
@@ -1015,6 +1077,90 @@ KG_FN bool seq_match(const GQuery* q, const GQuery* ql, int64_t within, const Wi
     }
   }
   return true;
+}
+
+// Lower every filter of g to compare atoms (K_seq windows, seq_match): a filter must be an AND tree
+// of compares whose operands are leaves or one arithmetic op over two leaves. A slot reference
+// names state a's one event when a <= the filter's state and the chain index is 0 / CURRENT (a
+// window slot holds one event, StateEvent.getStreamEvent:138-182), and reads null otherwise.
+// Leaves g.n_atoms = 0 when some filter has another form (or / not / is null / deeper arithmetic).
+inline void lower_atoms(GQuery& g) {
+  g.n_atoms = 0;
+  int na = 0;
+  for (int i = 0; i < g.n_states; ++i) {
+    g.atom_begin[i] = na;
+    const GState& st = g.st[i];
+    for (int f = 0; f < st.n_filt; ++f) {
+      // postfix -> tree: node = instruction index, children by stack simulation
+      int stk[GSTACK], sp = 0, left[GMAXCODE], right[GMAXCODE];
+      for (int pc = st.fb[f]; pc < st.fe[f]; ++pc) {
+        const GInsn& in = g.code[pc];
+        left[pc] = right[pc] = -1;
+        if (in.op == OP_CONST || in.op == OP_ATTR) {
+          if (sp >= GSTACK) return;
+          stk[sp++] = pc;
+        } else if (in.op == OP_CMP || in.op == OP_AND || in.op == OP_ARITH) {
+          if (sp < 2) return;
+          right[pc] = stk[--sp];
+          left[pc] = stk[--sp];
+          stk[sp++] = pc;
+        } else {
+          return;  // or / not / is null / stream is null: interpreter
+        }
+      }
+      if (sp != 1) return;
+      int todo[GMAXCODE], nt = 0;
+      todo[nt++] = stk[0];
+      while (nt) {
+        const int x = todo[--nt];
+        const GInsn& in = g.code[x];
+        if (in.op == OP_AND) {
+          todo[nt++] = right[x];  // left conjunct first (short-circuit order does not matter: pure)
+          todo[nt++] = left[x];
+          continue;
+        }
+        if (in.op != OP_CMP || na >= GMAXATOM) return;
+        GAtom& A = g.atoms[na++];
+        A = GAtom{};
+        A.state = (int8_t)i;
+        A.op = (int8_t)in.imm;
+        A.lt = in.lt;
+        A.rt = in.rt;
+        auto leaf = [&](int pc, GLeaf& L) -> bool {
+          const GInsn& li = g.code[pc];
+          L = GLeaf{};
+          L.type = li.res;
+          if (li.op == OP_CONST) {
+            L.kind = LF_CONST;
+            L.pc = (int16_t)pc;
+            return true;
+          }
+          if (li.op != OP_ATTR) return false;
+          const bool here = li.a <= i && (li.b == 0 || li.b == -1);
+          L.kind = here ? LF_ATTR : LF_NULL;
+          L.slot = (int8_t)li.a;
+          L.cap = (int8_t)li.imm;
+          return true;
+        };
+        auto opnd = [&](int pc, GOpnd& O) -> bool {
+          O = GOpnd{};
+          O.arith = -1;
+          const GInsn& oi = g.code[pc];
+          if (oi.op != OP_ARITH) return leaf(pc, O.a);
+          O.arith = (int8_t)oi.imm;
+          O.res = oi.res;
+          if (!leaf(left[pc], O.a) || !leaf(right[pc], O.b)) return false;
+          O.a.type = oi.lt;  // eval_code types arithmetic operands from the instruction
+          O.b.type = oi.rt;
+          return true;
+        };
+        if (!opnd(left[x], A.l) || !opnd(right[x], A.r)) return;
+      }
+    }
+  }
+  g.atom_begin[g.n_states] = na;
+  for (int i = g.n_states + 1; i <= GMAXS; ++i) g.atom_begin[i] = na;
+  g.n_atoms = na > 0 ? na : -1;  // -1: atoms lowered, none needed (filterless states)
 }
 
 // Shape of a query: the lowered program with what may differ between lanes of one wave cleared

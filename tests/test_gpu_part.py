@@ -117,15 +117,15 @@ def test_kpart_snapshot_restore():
 
 
 def test_c3_family_kpart_equals_kgen():
-    """The C3 bench family (count <2:5> mid-chain, logical and, logical or; 50 keys) on K_part equals
-    the general interpreter, match for match in R18 order."""
+    """The C3 bench family (count <2:5> mid-chain, logical and, logical or; 1000 keys) on K_part
+    equals the general interpreter, match for match in R18 order."""
     from siddhi_amd.workloads import c3_app, stock_events
     src = c3_app(96)
     a = _hip_app(src)
-    b = _hip_app(src, flags=SDH_FLAG_FORCE_GEN, gen_pool_states=32, gen_pool_nodes=128, gen_list_cap=32)
+    b = _hip_app(src, flags=SDH_FLAG_FORCE_GEN, gen_pool_states=64, gen_pool_nodes=256, gen_list_cap=64)
     for lo in (0, 20000, 20001):
         n = 20000 if lo != 20000 else 1
-        ts, sym, price, vol = stock_events(lo, n, 50)
+        ts, sym, price, vol = stock_events(lo, n, 1000)
         cols = [sym, price.view(np.uint32), vol]
         a.engine.push_columns(0, ts, cols)
         b.engine.push_columns(0, ts, cols)
