@@ -1756,6 +1756,11 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       P.kind = ps.kind;
       P.cap = ps.cap;
       P.ew = ps.ew;
+      {  // LDS-resident entries: up to the budget (default 32 KiB per wave: 5 waves per CU)
+        int64_t budget = 32 << 10;
+        if (const char* v = getenv("SDH_KPART_LDS")) budget = atoll(v);
+        P.cl = (int32_t)std::max<int64_t>(0, std::min<int64_t>(ps.cap, budget / (64 * 8 * ps.ew)));
+      }
       P.sA = ps.sA;
       P.sB = ps.sB;
       P.cmax = ps.cmax;

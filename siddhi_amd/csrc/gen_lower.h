@@ -278,7 +278,7 @@ inline GQuery lower_gen(const LProgram& P, int qi, const Sizing& sz) {
     for (int j = 0; j < g.n_cap[s]; ++j)
       if (g.cap_type[s][j] == T_LONG || g.cap_type[s][j] == T_DOUBLE) v32 = false;
   make_layout(g.lay, S, sz.R, sz.N, sz.LC, NA, v32);
-  lower_atoms(g);
+  lower_atoms_or_none(g);
   return g;
 }
 

@@ -87,10 +87,11 @@ struct GLayout {
 // same Java semantics as eval_code, without the evaluation stack (kg::lower_atoms, seq_match)
 constexpr int GMAXATOM = 16;
 enum { LF_ATTR = 0, LF_CONST = 1, LF_NULL = 2 };
+constexpr int GMAXCONST = 16;  // CONST leaves of one query's atoms
 struct GLeaf {
   int8_t kind, slot, cap, type;
-  int16_t pc;  // LF_CONST: instruction whose imm is the (per-lane) constant
-  int16_t pad;
+  int16_t pc;     // LF_CONST: instruction whose imm is the (per-lane) constant
+  int16_t cslot;  // LF_CONST: index into GQuery::const_pc (staged per lane on the device)
 };
 struct GOpnd {
   GLeaf a, b;
@@ -123,6 +124,8 @@ struct GQuery {
   int32_t n_atoms;    // > 0: every filter lowered to atoms (atom_begin[i] .. atom_begin[i+1] of state i)
   int32_t atom_begin[GMAXS + 1];
   GAtom atoms[GMAXATOM];
+  int32_t n_const;    // CONST leaves of the atoms: their instructions
+  int32_t const_pc[GMAXCONST];
 };
 
 // ---- Java value semantics (executor/condition/compare/**, executor/math/**) ----
@@ -1013,11 +1016,19 @@ inline int seq_window(const GQuery& g) {
 // Win provides ts(p) and, for event p and captured attribute word j, raw(p, j) / null(p, j). Slots
 // hold one event each, so eK / eK[0] / eK[last] name it and every other index is null
 // (StateEvent.getStreamEvent:138-182 on a one-event chain); state i's filter sees slots 0 .. i.
+// the lane's constant of a CONST leaf: its query's bytecode immediate, or (Win::lane_const) a copy
+// the device kernel staged in LDS once per work item
+template <class Win>
+KG_FN int64_t leaf_const(const GLeaf& f, const GQuery* ql, const Win& w) {
+  if constexpr (Win::kStagedConsts) return w.lane_const(f.cslot);
+  else return ql->code[f.pc].imm;
+}
+
 template <class Win>
 KG_FN Val atom_leaf(const GLeaf& f, const GQuery* ql, const Win& w) {
   Val v{f.type, 1, 0};
   if (f.kind == LF_CONST) {
-    const int64_t imm = ql->code[f.pc].imm;
+    const int64_t imm = leaf_const(f, ql, w);
     v.null = 0;
     v.bits = f.type == T_FLOAT ? (int64_t)(uint32_t)imm : f.type == T_INT ? (int64_t)(int32_t)imm : imm;
   } else if (f.kind == LF_ATTR && !w.null(f.slot, f.cap)) {
@@ -1086,6 +1097,7 @@ KG_FN bool seq_match(const GQuery* q, const GQuery* ql, int64_t within, const Wi
 // Leaves g.n_atoms = 0 when some filter has another form (or / not / is null / deeper arithmetic).
 inline void lower_atoms(GQuery& g) {
   g.n_atoms = 0;
+  g.n_const = 0;
   int na = 0;
   for (int i = 0; i < g.n_states; ++i) {
     g.atom_begin[i] = na;
@@ -1131,8 +1143,11 @@ inline void lower_atoms(GQuery& g) {
           L = GLeaf{};
           L.type = li.res;
           if (li.op == OP_CONST) {
+            if (g.n_const >= GMAXCONST) return false;
             L.kind = LF_CONST;
             L.pc = (int16_t)pc;
+            L.cslot = (int16_t)g.n_const;
+            g.const_pc[g.n_const++] = pc;
             return true;
           }
           if (li.op != OP_ATTR) return false;
@@ -1161,6 +1176,10 @@ inline void lower_atoms(GQuery& g) {
   g.atom_begin[g.n_states] = na;
   for (int i = g.n_states + 1; i <= GMAXS; ++i) g.atom_begin[i] = na;
   g.n_atoms = na > 0 ? na : -1;  // -1: atoms lowered, none needed (filterless states)
+}
+inline void lower_atoms_or_none(GQuery& g) {
+  lower_atoms(g);
+  if (g.n_atoms == 0) g.n_const = 0;
 }
 
 // Shape of a query: the lowered program with what may differ between lanes of one wave cleared

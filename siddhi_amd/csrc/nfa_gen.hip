@@ -212,7 +212,10 @@ constexpr int SEQ_TILE = 64;
 constexpr int SEQ_ROW = 3 + kg::GMAXNA;  // ts, seq, null bits, raw words
 
 struct LdsWin {
+  static constexpr bool kStagedConsts = true;
   const int64_t* base;  // row of window event 0
+  const int64_t* cst;   // this lane's atom constants, [cslot][lane] in LDS
+  __device__ int64_t lane_const(int c) const { return cst[c * 64]; }
   __device__ int64_t ts(int p) const { return base[p * SEQ_ROW]; }
   __device__ int64_t raw(int p, int j) const { return base[p * SEQ_ROW + 3 + j]; }
   __device__ bool null(int p, int j) const { return (base[p * SEQ_ROW + 2] >> j) & 1; }
@@ -221,12 +224,14 @@ struct LdsWin {
 
 __global__ __launch_bounds__(64) void nfa_seq_kernel(SeqLaunch L) {
   __shared__ int64_t win[(SEQ_TILE + kg::GMAXS) * SEQ_ROW];
+  __shared__ int64_t cst[kg::GMAXCONST * 64];
   const int lane = threadIdx.x;
   const int gi = L.glist[blockIdx.x % L.n_glist];
   const int chunk = blockIdx.x / L.n_glist;
   const int qi = L.lane_q[(int64_t)gi * 64 + lane];
   const kg::GQuery* __restrict__ q = L.queries + L.group_tmpl[gi];
   const kg::GQuery* __restrict__ ql = L.queries + (qi >= 0 ? qi : L.group_tmpl[gi]);
+  for (int c = 0; c < q->n_const; ++c) cst[c * 64 + lane] = ql->code[q->const_pc[c]].imm;  // once per item
   const int S = q->n_states;
   const int stream = L.b.stream;
   const int na = q->n_cap[stream];
@@ -270,7 +275,7 @@ __global__ __launch_bounds__(64) void nfa_seq_kernel(SeqLaunch L) {
     __syncthreads();
     if (qi >= 0) {
       for (int s = 0; s < cnt; ++s) {
-        const LdsWin wv{win + s * SEQ_ROW};
+        const LdsWin wv{win + s * SEQ_ROW, cst + lane};
         if (!kg::seq_match(q, ql, within, wv)) continue;
         ++nrec;
         if (!L.write_records) continue;

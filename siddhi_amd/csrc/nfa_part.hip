@@ -128,16 +128,25 @@ __global__ __launch_bounds__(64) void nfa_part_kernel(PartLaunch L) {
   int64_t* __restrict__ st = L.st + ((int64_t)(1 - cb) * L.blocks + block) * bw * 64 + lane;
   if (g == 0 && lane == 0) L.nxt[kid] = 1 - cb;
   const int ew = L.ew;
+  // the lane's table works in LDS for its first `cl` entries ([entry][word][lane]: conflict-free,
+  // one bank per lane) and in the output block beyond them
+  extern __shared__ int64_t part_lds[];
+  const int cl = L.cl;
   auto W = [&](int64_t i) -> int64_t& { return st[i * 64]; };
-  auto E = [&](int k, int w) -> int64_t& { return st[(PK_HDR + (int64_t)k * ew + w) * 64]; };
+  auto E = [&](int k, int w) -> int64_t& {
+    return k < cl ? part_lds[((int64_t)k * ew + w) * 64 + lane] : st[(PK_HDR + (int64_t)k * ew + w) * 64];
+  };
 
-  // the lane's table: input buffer -> output buffer, which is the working copy
+  // the lane's table: input buffer -> working copy (LDS, then the output block)
   int n = (int)in[0];
   int64_t hdr1 = in[64];
   for (int k = 0; k < n; ++k)
     for (int w = 0; w < ew; ++w) E(k, w) = in[(PK_HDR + (int64_t)k * ew + w) * 64];
 
-  __shared__ int64_t evv[kg::GMAXNA];
+  // the key's events, staged 64 at a time (one coalesced index load and one gather per lane), then
+  // read by broadcast: ts, seq, null bits and the captured words
+  __shared__ int64_t t_ts[64], t_seq[64], t_w[kg::GMAXNA][64];
+  __shared__ uint32_t t_nul[64];
   POut o{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
   unsigned long long nrec = 0;
   bool cap_over = false;
@@ -149,17 +158,26 @@ __global__ __launch_bounds__(64) void nfa_part_kernel(PartLaunch L) {
   const kg::GState& sb = q->st[KIND == PK_COUNT ? 2 : sB];
   int F = (int)(hdr1 & 0xffffffff), side = (int)(hdr1 >> 32);  // logical: filled prefix and its side
 
-  for (int64_t k = e0; k < e1; ++k) {
-    const int64_t e = L.ev_idx[k];
-    const int64_t seq = L.b.seq_base + e;
-    const int64_t ts = L.b.ts[e];
-    uint32_t ev_null = 0;
-    for (int j = 0; j < ncap; ++j) {  // the event is the same for every lane: identical LDS stores
+  for (int64_t t0 = e0; t0 < e1; t0 += 64) {
+  const int cnt = e1 - t0 < 64 ? (int)(e1 - t0) : 64;
+  if (lane < cnt) {
+    const int64_t e = L.ev_idx[t0 + lane];
+    t_ts[lane] = L.b.ts[e];
+    t_seq[lane] = L.b.seq_base + e;
+    uint32_t nb = 0;
+    for (int j = 0; j < ncap; ++j) {
       bool nl;
-      evv[j] = event_word(L.b, q->cap_attr[stream][j], e, nl);
-      if (nl) ev_null |= 1u << j;
+      t_w[j][lane] = event_word(L.b, q->cap_attr[stream][j], e, nl);
+      if (nl) nb |= 1u << j;
     }
-    if (!live) continue;
+    t_nul[lane] = nb;
+  }
+  __syncthreads();
+  for (int te = 0; te < cnt && live; ++te) {
+    const int64_t seq = t_seq[te];
+    const int64_t ts = t_ts[te];
+    const uint32_t ev_null = t_nul[te];
+    auto evw = [&](int j) -> int64_t { return t_w[j][te]; };
     // an event-only filter of state `st` (FilterProcessor.java:55-66 over the typed bytecode)
     auto ev_filter = [&](const kg::GState& gs, int sid) -> bool {
       for (int f = 0; f < gs.n_filt; ++f) {
@@ -167,7 +185,7 @@ __global__ __launch_bounds__(64) void nfa_part_kernel(PartLaunch L) {
             q, ql, gs.fb[f], gs.fe[f],
             [&](const kg::GInsn& in) {  // the state's own one-event slot: index 0 / CURRENT only
               const bool here = in.a == sid && (in.b == 0 || in.b == -1);
-              return typed(in, here ? evv[in.imm] : 0, !here || ((ev_null >> in.imm) & 1u));
+              return typed(in, here ? evw(in.imm) : 0, !here || ((ev_null >> in.imm) & 1u));
             },
             [&](const kg::GInsn& in) { return !(in.a == sid && (in.b == 0 || in.b == -1)); });
         if (v.null || !v.bits) return false;
@@ -283,7 +301,7 @@ __global__ __launch_bounds__(64) void nfa_part_kernel(PartLaunch L) {
                   [&](const kg::GInsn& in) {
                     if (in.a == 2) {  // the current event
                       const bool here = in.b == 0 || in.b == -1;
-                      return typed(in, here ? evv[in.imm] : 0, !here || ((ev_null >> in.imm) & 1u));
+                      return typed(in, here ? evw(in.imm) : 0, !here || ((ev_null >> in.imm) & 1u));
                     }
                     if (in.a == 0) {  // e1
                       const bool here = in.b == 0 || in.b == -1;
@@ -328,10 +346,10 @@ __global__ __launch_bounds__(64) void nfa_part_kernel(PartLaunch L) {
           E(kk, 3 + len) = seq;
           const int64_t nb = (int64_t)(ev_null & 0xff);
           if (len == 0) {
-            for (int j = 0; j < L.n_first; ++j) E(kk, o_first + j) = evv[j];
+            for (int j = 0; j < L.n_first; ++j) E(kk, o_first + j) = evw(j);
             fl = (fl & ~(0xffll << 24)) | (nb << 24);
           }
-          for (int j = 0; j < L.n_last; ++j) E(kk, o_last + j) = evv[j];
+          for (int j = 0; j < L.n_last; ++j) E(kk, o_last + j) = evw(j);
           fl = (fl & ~(0xffll << 32)) | (nb << 32);
           ++len;
           if (len == cmin) inL3 = true;  // CountPost: next.addState at n == min (visible next event)
@@ -349,7 +367,7 @@ __global__ __launch_bounds__(64) void nfa_part_kernel(PartLaunch L) {
           E(n, 0) = ts;
           E(n, 1) = seq;
           int64_t fl = (int64_t)(ev_null & 0xff) << 16;  // e1's null bits
-          for (int j = 0; j < L.n_e1; ++j) E(n, o_e1 + j) = evv[j];
+          for (int j = 0; j < L.n_e1; ++j) E(n, o_e1 + j) = evw(j);
           E(n, 2) = fl;
           ++n;
         } else {
@@ -358,6 +376,10 @@ __global__ __launch_bounds__(64) void nfa_part_kernel(PartLaunch L) {
       }
     }
   }
+  __syncthreads();  // the tile is rewritten next
+  }
+  for (int k = 0; k < n && k < cl; ++k)  // LDS-resident entries back to the output block
+    for (int w = 0; w < ew; ++w) st[(PK_HDR + (int64_t)k * ew + w) * 64] = part_lds[((int64_t)k * ew + w) * 64 + lane];
   W(0) = n;
   W(1) = (int64_t)(uint32_t)F | ((int64_t)side << 32);
   if (nrec) atomicAdd(L.rec_count, nrec);
@@ -369,10 +391,11 @@ __global__ __launch_bounds__(64) void nfa_part_kernel(PartLaunch L) {
 
 extern "C" hipError_t sdh_launch_part(const sdh::PartLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
+  const size_t lds = (size_t)L->cl * L->ew * 64 * 8;  // dynamic: the LDS-resident table entries
   switch (L->kind) {
-    case sdh::PK_OR: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_OR>, dim3(L->n_items), dim3(64), 0, s, *L); break;
-    case sdh::PK_AND: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_AND>, dim3(L->n_items), dim3(64), 0, s, *L); break;
-    default: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_COUNT>, dim3(L->n_items), dim3(64), 0, s, *L);
+    case sdh::PK_OR: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_OR>, dim3(L->n_items), dim3(64), lds, s, *L); break;
+    case sdh::PK_AND: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_AND>, dim3(L->n_items), dim3(64), lds, s, *L); break;
+    default: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_COUNT>, dim3(L->n_items), dim3(64), lds, s, *L);
   }
   return hipGetLastError();
 }

@@ -284,6 +284,8 @@ struct PartLaunch {
   int32_t kind;               // PartKind
   int32_t cap;                // entries per lane
   int32_t ew;                 // words per entry
+  int32_t cl;                 // entries per lane held in LDS while the item runs (<= cap)
+  int32_t pad;
   int32_t sA, sB;             // logical: state ids of the side processed second (A) and first (B)
   int32_t cmax;               // count: chain words per entry (the set's largest max)
   int32_t n_e1, n_first, n_last;  // count: captured words stored per entry (0 or the stream's n_cap)

@@ -51,6 +51,8 @@ struct Host {
 };
 
 struct HostWin {  // kg::seq_match's window over Host::Ev records
+  static constexpr bool kStagedConsts = false;
+  int64_t lane_const(int) const { return 0; }
   const std::vector<Host::Ev>* ev;
   size_t s;
   const int32_t* cap;
