@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--partials", type=int, default=128)
     ap.add_argument("--expansion-batch", type=int, default=1 << 16)
     ap.add_argument("--no-expansion", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -310,12 +311,41 @@ def main():
         result["roofline"]["counters"] = {k: v for k, v in prof.items() if k != "traffic_bytes"}
     if not args.no_expansion:
         result["expansion"] = expansion(args, P, rank, K, local, dev, world, cdev, dist)
+    if not args.no_ingest and world == 1:
+        result["host_ingest"] = host_ingest(args, eng, B, K, n_batches)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.workload, K, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_ingest(args, eng, B, K, first_step):
+    """The same pushes with the batch in pinned HOST memory (sdh_batch.on_device = 0): the side-stream
+    copy to HBM is inside the step (PCIe-inclusive rate), continuing the stream."""
+    import torch
+    steps = 2
+    rows = []
+    for s in range(steps):
+        cols = gen_batch(args.workload, (first_step + s) * B, B, K, torch.device("cuda"))
+        rows.append([c.cpu().pin_memory() for c in cols])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ing = 0.0
+    for cols in rows:
+        eng.push_columns(0, cols[0].numpy(), [c.numpy() for c in cols[1:]])
+        ing += eng.stats().last_ingest_ms
+    el = time.perf_counter() - t0
+    nbytes = sum(c.numel() * c.element_size() for c in rows[0])
+    return {"events_per_step": B, "steps": steps, "ms_per_step": el * 1e3 / steps, "h2d_ms_per_step": ing / steps,
+            "h2d_gbps": nbytes / (ing / steps * 1e-3) / 1e9 if ing else None,
+            "pattern_events_per_s": B * steps * eng_patterns(eng) / el}
+
+
+def eng_patterns(eng):
+    st = eng.stats()
+    return st.pattern_events / max(1, st.events)
 
 
 def expansion(args, P, rank, K, local, dev, world, cdev, dist):

@@ -126,6 +126,11 @@ typedef struct sdh_stats {
                              /* segments, or groups x event chunks           */
   int64_t last_seq_items;    /* K_seq work items of the last push: groups x window chunks     */
   int64_t last_part_items;   /* K_part work items of the last push: groups x key segments     */
+  double last_ingest_ms;     /* host-to-HBM copy time of the last host-resident batch (side   */
+                             /* stream; 0 for on_device batches)                              */
+  int64_t ingest_bytes;      /* bytes copied from host batches so far                         */
+  int64_t spec_kernels;      /* shape-compiled kernels this engine launches (hiprtc at create; */
+                             /* SDH_SPEC=0 off, 1 every shape, default shapes of >= 128 queries) */
 } sdh_stats;
 
 int sdh_engine_create(const void* ir_blob, size_t len, const sdh_config* cfg, sdh_engine** out);

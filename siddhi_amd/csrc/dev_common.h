@@ -1,0 +1,162 @@
+// dev_common.h -- device helpers shared by the NFA kernels (nfa_gen.hip, nfa_part.hip) and by the
+// shape-compiled kernels built at engine creation (spec.hip: seq_body.h / part_body.h compiled at
+// run time with hiprtc, so this header also builds without the host's system headers).
+#pragma once
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#endif
+
+#include "kgen.h"
+#include "nfa_types.h"
+
+namespace sdh {
+namespace dev {
+
+template <class T, int N>
+__device__ __forceinline__ T gpick(const T (&arr)[N], int idx) {
+  T v = arr[0];
+#pragma unroll
+  for (int c = 1; c < N; ++c) v = (idx == c) ? arr[c] : v;
+  return v;
+}
+
+// attribute word `attr` of batch event e: int / string id sign-extended, float bits, long / double
+// bits, bool byte; *isnull from the column's null bytes
+__device__ __forceinline__ int64_t raw_word(const StreamBatch& b, int attr, int64_t e, bool& isnull) {
+  const void* p = gpick(b.col, attr);
+  const uint8_t* nl = gpick(b.nul, attr);
+  const int w = gpick(b.width, attr);
+  isnull = nl && nl[e];
+  if (w == 8) return ((const int64_t*)p)[e];
+  if (w == 4) return (int64_t)((const int32_t*)p)[e];
+  return (int64_t)((const uint8_t*)p)[e];
+}
+
+// match output: one flat word buffer; each record is reserved with an atomic add of its length
+// (the backend's atomic optimizer folds a wave's same-address adds into one atomic + a scan).
+// Ring mode (write_records == 2, SDH_FLAG_DEVICE_MATCHES): every record is still written, at its
+// offset modulo the buffer less a one-record margin, because nobody reads it back. In normal mode
+// each record's offset is also listed in rec_off (the device match table finds records by it,
+// matches.hip); a record fits only if its words and its index entry both do.
+struct LaneOut {
+  int64_t* out;
+  int64_t cap;
+  unsigned long long* next;
+  bool ring;
+  int64_t* rec_off;
+  int64_t rec_cap;
+  unsigned long long* rec_next;
+  bool over = false;
+  __device__ void close() {}
+  __device__ int64_t* reserve(int words) {
+    const unsigned long long o = atomicAdd(next, (unsigned long long)words);
+    if (ring) return out + (int64_t)(o % (unsigned long long)(cap - GEN_RING_MARGIN));
+    if ((int64_t)(o + words) > cap) {
+      over = true;
+      return nullptr;
+    }
+    const unsigned long long r = atomicAdd(rec_next, 1ull);
+    if ((int64_t)r >= rec_cap) {
+      over = true;
+      return nullptr;
+    }
+    rec_off[r] = (int64_t)o;
+    return out + o;
+  }
+};
+
+// Wave-buffered match output: a work group is ONE wave; its records are assembled in an LDS buffer
+// and flushed to the global buffer with one word reservation and one record-index reservation per
+// flush (a per-record atomic on the two global counters serialises the whole chip once the match
+// rate is ~1e9/s). Collective over the lanes active at the call: every active lane calls reserve()
+// (its record's words) at the same point; offsets inside the buffer come from an LDS atomic, so the
+// records of one call land in any order -- the device match table orders rows by their keys (R18).
+// A record longer than the buffer (or a call whose records cannot fit an empty buffer) is reserved
+// globally per lane, as LaneOut does.
+struct WaveOut {
+  static constexpr int CAPW = 512;             // words in the LDS buffer (4 KiB: occupancy)
+  static constexpr int CAPR = CAPW / 7 + 1;    // records (>= 7 words each)
+  struct Shared {
+    int64_t buf[CAPW];
+    int32_t roff[CAPR];
+    int64_t base, rbase;
+    int32_t used, nrec, need;
+  };
+  LaneOut g;
+  Shared* sh;
+  __device__ static unsigned long long active() { return __ballot(1); }
+  __device__ static int rank(unsigned long long m) {
+    return __popcll(m & ((1ull << __lane_id()) - 1ull));
+  }
+  __device__ static void fence() { __threadfence_block(); }
+  __device__ void init() {
+    if (__lane_id() == 0) sh->used = sh->nrec = sh->need = 0;
+    fence();
+  }
+  // copy the buffer out (active lanes cooperate)
+  __device__ void flush() {
+    const unsigned long long m = active();
+    const int cnt = __popcll(m), me = rank(m), lead = __ffsll((long long)m) - 1;
+    const int n = sh->used, nr = sh->nrec;
+    fence();
+    if (n == 0) return;
+    if (__lane_id() == lead) {
+      const unsigned long long o = atomicAdd(g.next, (unsigned long long)n);
+      int64_t base = (int64_t)o, rbase = 0;
+      if (!g.ring) {
+        if ((int64_t)(o + n) > g.cap) base = -1;
+        const unsigned long long r = atomicAdd(g.rec_next, (unsigned long long)nr);
+        if ((int64_t)(r + nr) > g.rec_cap) base = -1;
+        rbase = (int64_t)r;
+      }
+      sh->base = base;
+      sh->rbase = rbase;
+    }
+    fence();
+    const int64_t base = sh->base, rbase = sh->rbase;
+    if (base < 0) {
+      g.over = true;
+    } else if (g.ring) {
+      const unsigned long long rc = (unsigned long long)(g.cap - GEN_RING_MARGIN);
+      for (int i = me; i < n; i += cnt) g.out[(unsigned long long)(base + i) % rc] = sh->buf[i];
+    } else {
+      for (int i = me; i < n; i += cnt) g.out[base + i] = sh->buf[i];
+      for (int i = me; i < nr; i += cnt) g.rec_off[rbase + i] = base + sh->roff[i];
+    }
+    fence();
+    if (__lane_id() == lead) sh->used = sh->nrec = 0;
+    fence();
+  }
+  // room for this lane's record of `words` words: a pointer into the LDS buffer (or, for an
+  // oversized call, into the global buffer); nullptr once the global buffer overflowed
+  __device__ int64_t* reserve(int words) {
+    const unsigned long long m = active();
+    const int lead = __ffsll((long long)m) - 1, cnt = __popcll(m);
+    if (__lane_id() == lead) sh->need = 0;
+    fence();
+    atomicAdd(&sh->need, words);
+    fence();
+    const int total = sh->need;
+    if (total > CAPW || cnt > CAPR) return g.reserve(words);  // (uniform) oversized call
+    if (sh->used + total > CAPW || sh->nrec + cnt > CAPR) flush();
+    const int off = atomicAdd(&sh->used, words);
+    const int ri = atomicAdd(&sh->nrec, 1);
+    sh->roff[ri] = off;
+    return sh->buf + off;
+  }
+  __device__ void close() {
+    flush();
+    over |= g.over;
+  }
+  bool over = false;
+};
+
+__device__ __forceinline__ bool expired(int64_t ts1, int64_t ts, int64_t within) {
+  if (within < 0) return false;
+  const int64_t d = (int64_t)((uint64_t)ts1 - (uint64_t)ts);
+  const int64_t a = d < 0 ? (int64_t)(0ull - (uint64_t)d) : d;
+  return a > within;
+}
+
+}  // namespace dev
+}  // namespace sdh

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <map>
 #include <memory>
 #include <cstdarg>
 #include <cstdio>
@@ -21,6 +22,7 @@
 #include "../../include/siddhi_hip.h"
 #include "gen_lower.h"
 #include "nfa_types.h"
+#include "spec.h"
 
 extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s);
 extern "C" hipError_t sdh_launch_part(const sdh::PartLaunch* L, hipStream_t s);
@@ -563,8 +565,11 @@ struct sdh_engine {
   DevBuf<int64_t> d_part[2];
   std::vector<int> cur;              // which buffer holds each local query's state
   // batch staging for host-resident input
-  DevBuf<int64_t> d_ts;
-  std::vector<DevBuf<uint8_t>> d_col, d_nul;
+  DevBuf<uint8_t> d_batch;           // a host batch's columns in HBM (stage_host_batch)
+  HostBuf<uint8_t> stage[2];         // pinned staging slots
+  hipEvent_t ev_stage[2] = {nullptr, nullptr}, ev_h0 = nullptr, ev_h1 = nullptr;
+  int stage_next = 0;
+  hipStream_t h2d = nullptr;         // side stream of host-to-device batch copies
   std::vector<int64_t> prev_ts;      // per stream
   int64_t seq = 0;
   // last launch
@@ -600,6 +605,7 @@ struct sdh_engine {
   std::vector<int32_t> group_tmpl;   // [group] shape template (a member query)
   DevBuf<int32_t> d_group_tmpl;
   std::vector<int32_t> group_seq;    // [group] window length S when the group runs on K_seq, else 0
+  std::map<int, hipFunction_t> seq_spec;  // K_seq shape template -> its shape-compiled kernel (spec.h)
   std::vector<DevBuf<int32_t>> d_glists;  // [stream] unpartitioned groups: K_seq rows, then K_gen groups
   std::vector<DevBuf<int64_t>> seq_tail;  // [stream] last SEQ_TMAX events (K_seq windows)
   std::vector<int32_t> seq_tail_len;
@@ -638,6 +644,7 @@ struct sdh_engine {
     DevBuf<int64_t> st;              // [2][key_cap * n_groups][PK_HDR + cap * ew][64]
     DevBuf<int32_t> cur, nxt;        // [key_cap]
     int64_t bw() const { return PK_HDR + (int64_t)cap * ew; }
+    std::map<int, hipFunction_t> spec;  // shape template -> shape-compiled kernel (spec.h)
   };
   std::vector<std::unique_ptr<PartSet>> psets;
   DevBuf<int32_t> d_perr;            // per K_part set: [0] entry capacity, [2] output overflow
@@ -1315,6 +1322,47 @@ KPart kpart_shape(const kg::LProgram& P, int qi, const kg::GQuery& g) {
   return k;
 }
 
+// Shape-compiled kernels (spec.h): SDH_SPEC=0 none, 1 every shape, "require" every shape and a
+// failed compile is an error; default: shapes that fill at least two waves (a compile costs about
+// a second once per process and shape, the interpreted kernel is exact too)
+int spec_mode() {
+  const char* v = getenv("SDH_SPEC");
+  if (!v || !*v) return 1;
+  if (!strcmp(v, "0")) return 0;
+  if (!strcmp(v, "require")) return 3;
+  return 2;
+}
+
+void spec_build(sdh_engine* e) {
+  const int mode = spec_mode();
+  if (mode == 0) return;
+  std::map<int, int> groups;  // K_seq template -> groups
+  for (size_t g = 0; g < e->group_seq.size(); ++g)
+    if (e->group_seq[g] > 0) ++groups[e->group_tmpl[g]];
+  for (const auto& [t, ng] : groups) {
+    if (mode == 1 && ng < 2) continue;
+    std::string err;
+    hipFunction_t f = sdh::spec::get_kernel(sdh::spec::seq_source(e->gq[t]), "sdh_seq_spec", &err);
+    if (!f && mode == 3) throw Error(SDH_E_DEVICE, "shape-compiled K_seq kernel: " + err);
+    if (f) e->seq_spec[t] = f;
+  }
+  int64_t n = (int64_t)e->seq_spec.size();
+  for (auto& up : e->psets) {
+    auto& ps = *up;
+    std::map<int, int> pg;  // template -> groups
+    for (int g = 0; g < ps.n_groups; ++g) ++pg[e->group_tmpl[ps.group_base + g]];
+    for (const auto& [t, ng] : pg) {
+      if (mode == 1 && ng < 2) continue;
+      const sdh::spec::PartLayout lay{ps.kind, ps.sA, ps.sB, ps.cmax, ps.n_e1, ps.n_first, ps.n_last};
+      std::string err;
+      hipFunction_t f = sdh::spec::get_kernel(sdh::spec::part_source(e->gq[t], lay), "sdh_part_spec", &err);
+      if (!f && mode == 3) throw Error(SDH_E_DEVICE, "shape-compiled K_part kernel: " + err);
+      if (f) ps.spec[t] = f, ++n;
+    }
+  }
+  e->stats.spec_kernels = n;
+}
+
 void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   kg::Sizing sz;
   if (e->cfg.gen_pool_states > 0) sz.R = std::min(64, e->cfg.gen_pool_states);
@@ -1462,6 +1510,7 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
     HIPCHK(hipMemset(t.p, 0, SEQ_TMAX * SEQ_TW * 8));
   }
   e->d_glists.resize(e->prog.stream_types.size());
+  spec_build(e);
   e->d_group_tmpl.ensure(e->group_tmpl.size());
   HIPCHK(hipMemcpy(e->d_group_tmpl.p, e->group_tmpl.data(), e->group_tmpl.size() * 4, hipMemcpyHostToDevice));
   e->g_out_next.ensure(1);
@@ -1601,13 +1650,17 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
         both.insert(both.end(), gen_groups.begin(), gen_groups.end());
         if (!both.empty()) HIPCHK(hipMemcpy(gl.p, both.data(), both.size() * 4, hipMemcpyHostToDevice));
       }
-      if (!seq_rows.empty()) {
+      // K_seq: one launch per shape (rows of one shape are contiguous), its compiled kernel if any
+      for (size_t r0 = 0, r1 = 0; r0 < seq_rows.size(); r0 = r1) {
+        const int tmpl = e->group_tmpl[seq_rows[r0]];
+        for (r1 = r0 + 1; r1 < seq_rows.size() && e->group_tmpl[seq_rows[r1]] == tmpl;) ++r1;
+        const int nrows = (int)(r1 - r0);
         sdh::SeqLaunch Q{};
         Q.queries = e->d_gq.p;
         Q.lane_q = e->d_lane_q.p;
         Q.group_tmpl = e->d_group_tmpl.p;
-        Q.glist = gl.p;
-        Q.n_glist = (int32_t)seq_rows.size();
+        Q.glist = gl.p + r0;
+        Q.n_glist = nrows;
         Q.b = B;
         Q.tail = e->seq_tail[stream].p;
         Q.tail_len = e->seq_tail_len[stream];
@@ -1621,16 +1674,23 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
         Q.rec_next = e->g_rec_next.p;
         Q.err = e->d_err.p;
         const int64_t starts = n + Q.tail_len;
-        const int64_t target = std::max<int64_t>(1, 8192 / (int64_t)seq_rows.size());
+        const int64_t target = std::max<int64_t>(1, 8192 / (int64_t)nrows);
         int64_t clen = std::max<int64_t>(256, (starts + target - 1) / target);
         clen = (clen + 63) / 64 * 64;  // whole LDS tiles
         Q.chunk_len = clen;
         Q.n_chunks = (int32_t)((starts + clen - 1) / clen);
-        HIPCHK(sdh_launch_seq(&Q, e->stream));
+        auto sp = e->seq_spec.find(tmpl);
+        if (sp != e->seq_spec.end()) {
+          void* args[] = {&Q};
+          HIPCHK(hipModuleLaunchKernel(sp->second, (unsigned)(Q.n_glist * Q.n_chunks), 1, 1, 64, 1, 1, 0, e->stream, args,
+                                       nullptr));
+        } else {
+          HIPCHK(sdh_launch_seq(&Q, e->stream));
+        }
         *tail_new_len = (int32_t)std::min<int64_t>(SEQ_TMAX, Q.tail_len + n);
         e->stats.last_seq_items += (int64_t)Q.n_glist * Q.n_chunks;
         any = true;
-        bytes += (double)n * ev_bytes * seq_rows.size();  // every group stages the batch once
+        bytes += (double)n * ev_bytes * nrows;  // every group stages the batch once
       }
       if (gen_groups.empty()) continue;
       L.glist = gl.p + seq_rows.size();
@@ -1756,18 +1816,12 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       P.kind = ps.kind;
       P.cap = ps.cap;
       P.ew = ps.ew;
-      {  // LDS-resident entries: up to the budget (default 32 KiB per wave: 5 waves per CU)
-        int64_t budget = 32 << 10;
-        if (const char* v = getenv("SDH_KPART_LDS")) budget = atoll(v);
-        P.cl = (int32_t)std::max<int64_t>(0, std::min<int64_t>(ps.cap, budget / (64 * 8 * ps.ew)));
-      }
       P.sA = ps.sA;
       P.sB = ps.sB;
       P.cmax = ps.cmax;
       P.n_e1 = ps.n_e1;
       P.n_first = ps.n_first;
       P.n_last = ps.n_last;
-      P.n_items = hv[1] * ps.n_groups;
       P.st = ps.st.p;
       P.blocks = ps.key_cap * ps.n_groups;
       P.cur = ps.cur.p;
@@ -1783,9 +1837,25 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       P.err = e->d_perr.p + 4 * si;
       // the per-key buffer selector of untouched keys carries over
       HIPCHK(hipMemcpyAsync(ps.nxt.p, ps.cur.p, (size_t)ps.key_cap * 4, hipMemcpyDeviceToDevice, e->stream));
-      HIPCHK(sdh_launch_part(&P, e->stream));
+      // one launch per shape (its groups are contiguous), the shape-compiled kernel if there is one
+      for (int g0 = 0, g1 = 0; g0 < ps.n_groups; g0 = g1) {
+        const int tmpl = e->group_tmpl[ps.group_base + g0];
+        for (g1 = g0 + 1; g1 < ps.n_groups && e->group_tmpl[ps.group_base + g1] == tmpl;) ++g1;
+        P.g0 = g0;
+        P.gn = g1 - g0;
+        P.n_items = hv[1] * P.gn;
+        auto sp = ps.spec.find(tmpl);
+        if (sp != ps.spec.end()) {
+          if (P.n_items > 0) {
+            void* args[] = {&P};
+            HIPCHK(hipModuleLaunchKernel(sp->second, (unsigned)P.n_items, 1, 1, 64, 1, 1, 0, e->stream, args, nullptr));
+          }
+        } else {
+          HIPCHK(sdh_launch_part(&P, e->stream));
+        }
+        e->stats.last_part_items += P.n_items;
+      }
       ps.ran = true;
-      e->stats.last_part_items += P.n_items;
       any = true;
       bytes += (double)n * ev_bytes * ps.n_groups;
     }
@@ -1926,6 +1996,67 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   if (write) e->g_used = (int64_t)used;
 }
 
+// Host-resident batch -> HBM (the StreamJunction -> receiver hand-off of north_star (2)): the
+// columns go to one device buffer over the side stream `h2d`; pinned caller memory is copied
+// directly, pageable memory through two pinned staging slots whose host copy of slice i+1 overlaps
+// the DMA of slice i. The compute stream waits on the transfer's event.
+void stage_host_batch(sdh_engine* e, const sdh_batch* b, StreamBatch& B) {
+  const int na = B.n_attr;
+  const int64_t n = b->n;
+  struct Part {
+    const void* src;
+    size_t bytes, off;
+  };
+  std::vector<Part> parts;
+  size_t total = 0;
+  auto add = [&](const void* src, size_t bytes) {
+    total = (total + 255) & ~(size_t)255;
+    parts.push_back({src, bytes, total});
+    total += bytes;
+  };
+  add(b->ts, (size_t)n * 8);
+  for (int a = 0; a < na; ++a) add(b->cols[a], (size_t)n * B.width[a]);
+  for (int a = 0; a < na; ++a)
+    if (b->nulls && b->nulls[a]) add(b->nulls[a], (size_t)n);
+  e->d_batch.ensure(total);
+  float ms = 0;
+  HIPCHK(hipEventRecord(e->ev_h0, e->h2d));
+  const size_t SLICE = (size_t)4 << 20;
+  for (const Part& p : parts) {
+    hipPointerAttribute_t at{};
+    const bool pinned = hipPointerGetAttributes(&at, p.src) == hipSuccess && at.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    uint8_t* dst = e->d_batch.p + p.off;
+    if (pinned) {
+      HIPCHK(hipMemcpyAsync(dst, p.src, p.bytes, hipMemcpyHostToDevice, e->h2d));
+      continue;
+    }
+    for (size_t o = 0; o < p.bytes; o += SLICE) {
+      const size_t len = std::min(SLICE, p.bytes - o);
+      const int slot = e->stage_next;
+      e->stage_next ^= 1;
+      e->stage[slot].ensure(SLICE);
+      HIPCHK(hipEventSynchronize(e->ev_stage[slot]));  // the slot's previous DMA has drained
+      memcpy(e->stage[slot].p, (const uint8_t*)p.src + o, len);
+      HIPCHK(hipMemcpyAsync(dst + o, e->stage[slot].p, len, hipMemcpyHostToDevice, e->h2d));
+      HIPCHK(hipEventRecord(e->ev_stage[slot], e->h2d));
+    }
+  }
+  HIPCHK(hipEventRecord(e->ev_h1, e->h2d));
+  HIPCHK(hipStreamWaitEvent(e->stream, e->ev_h1, 0));
+  HIPCHK(hipEventSynchronize(e->ev_h1));
+  HIPCHK(hipEventElapsedTime(&ms, e->ev_h0, e->ev_h1));
+  e->stats.last_ingest_ms = ms;
+  e->stats.ingest_bytes += (int64_t)total;
+  size_t k = 0;
+  B.ts = (const int64_t*)(e->d_batch.p + parts[k++].off);
+  for (int a = 0; a < na; ++a) B.col[a] = e->d_batch.p + parts[k++].off;
+  for (int a = 0; a < na; ++a) {
+    B.nul[a] = nullptr;
+    if (b->nulls && b->nulls[a]) B.nul[a] = e->d_batch.p + parts[k++].off;
+  }
+}
+
 int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   if (!b || stream < 0 || stream >= (int)e->prog.stream_types.size())
     throw Error(SDH_E_INVALID, "bad stream or batch");
@@ -1950,24 +2081,7 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
       B.nul[a] = b->nulls ? b->nulls[a] : nullptr;
     }
   } else {
-    e->d_ts.ensure(b->n);
-    HIPCHK(hipMemcpyAsync(e->d_ts.p, b->ts, b->n * 8, hipMemcpyHostToDevice, e->stream));
-    B.ts = e->d_ts.p;
-    if ((int)e->d_col.size() < na) {
-      e->d_col.resize(na);
-      e->d_nul.resize(na);
-    }
-    for (int a = 0; a < na; ++a) {
-      e->d_col[a].ensure((size_t)b->n * B.width[a]);
-      HIPCHK(hipMemcpyAsync(e->d_col[a].p, b->cols[a], (size_t)b->n * B.width[a], hipMemcpyHostToDevice, e->stream));
-      B.col[a] = e->d_col[a].p;
-      B.nul[a] = nullptr;
-      if (b->nulls && b->nulls[a]) {
-        e->d_nul[a].ensure(b->n);
-        HIPCHK(hipMemcpyAsync(e->d_nul[a].p, b->nulls[a], b->n, hipMemcpyHostToDevice, e->stream));
-        B.nul[a] = e->d_nul[a].p;
-      }
-    }
+    stage_host_batch(e, b, B);
   }
   std::vector<int> qs;
   for (int li = 0; li < (int)e->lq.size(); ++li)
@@ -2174,8 +2288,12 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     e->rec_words = 2 + maxS;
     e->prev_ts.assign(e->prog.stream_types.size(), INT64_MIN);
     HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&e->h2d, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&e->ev0));
     HIPCHK(hipEventCreate(&e->ev1));
+    HIPCHK(hipEventCreate(&e->ev_h0));
+    HIPCHK(hipEventCreate(&e->ev_h1));
+    for (auto& ev : e->ev_stage) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     e->d_q.ensure(std::max<size_t>(1, e->lq.size()));
     std::vector<ChainQuery> cqs;
     for (auto& L : e->lq) cqs.push_back(L.cq);
@@ -2484,6 +2602,10 @@ void sdh_engine_destroy(sdh_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->h2d) (void)hipStreamSynchronize(e->h2d);
+  for (hipEvent_t ev : {e->ev_h0, e->ev_h1, e->ev_stage[0], e->ev_stage[1]})
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->h2d) (void)hipStreamDestroy(e->h2d);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }

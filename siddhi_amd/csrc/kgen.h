@@ -21,8 +21,10 @@
 // per lane over lane-interleaved arenas in HBM; tests/native builds the same header for the host
 // to cross-check the restatement against the oracle (test infrastructure only).
 #pragma once
+#ifndef __HIPCC_RTC__  // (hiprtc: spec.hip supplies the fixed-width types)
 #include <math.h>
 #include <stdint.h>
+#endif
 
 #ifdef __HIPCC__
 #define KG_FN __host__ __device__ inline
@@ -86,7 +88,9 @@ struct GLayout {
 // leaf (a slot's attribute word or a bytecode constant) or one arithmetic op over two leaves -- the
 // same Java semantics as eval_code, without the evaluation stack (kg::lower_atoms, seq_match)
 constexpr int GMAXATOM = 16;
-enum { LF_ATTR = 0, LF_CONST = 1, LF_NULL = 2 };
+// LF_ATTR0: a slot reference with chain index 0 (the chain's first event; in a one-event window
+// slot the same event as LF_ATTR's CURRENT / 0)
+enum { LF_ATTR = 0, LF_CONST = 1, LF_NULL = 2, LF_ATTR0 = 3 };
 constexpr int GMAXCONST = 16;  // CONST leaves of one query's atoms
 struct GLeaf {
   int8_t kind, slot, cap, type;
@@ -247,6 +251,42 @@ KG_FN Val arith(int op, int res, const Val& l, const Val& r) {
   }
   return v;
 }
+
+// Shape-compiled filters (spec.hip generates straight-line code from a shape's bytecode): one
+// helper per instruction kind, the instruction's static fields as template arguments, so every
+// type / operator dispatch of eval_code folds away at compile time. Same semantics, instruction
+// by instruction, as eval_code above.
+template <int RES>
+KG_FN Val sp_const(int64_t imm) {
+  return Val{RES, 0, RES == T_FLOAT ? (int64_t)(uint32_t)imm : RES == T_INT ? (int64_t)(int32_t)imm : imm};
+}
+template <int RES>
+KG_FN Val sp_attr(int64_t raw, bool isnull) {
+  Val x{RES, 1, 0};
+  if (!isnull) {
+    x.null = 0;
+    x.bits = RES == T_INT ? (int64_t)(int32_t)raw : RES == T_FLOAT ? (int64_t)(uint32_t)raw : raw;
+  }
+  return x;
+}
+KG_FN Val sp_bool(bool b) { return Val{T_BOOL, 0, b ? 1 : 0}; }
+KG_FN Val sp_is_null(const Val& x) { return sp_bool(x.null != 0); }
+KG_FN Val sp_not(const Val& x) { return sp_bool(!(!x.null && x.bits)); }
+KG_FN Val sp_and(const Val& l, const Val& r) { return sp_bool((!l.null && l.bits) && (!r.null && r.bits)); }
+KG_FN Val sp_or(const Val& l, const Val& r) { return sp_bool((!l.null && l.bits) || (!r.null && r.bits)); }
+template <int OP, int LT, int RT>
+KG_FN Val sp_cmp(Val l, Val r) {
+  l.type = LT;
+  r.type = RT;
+  return sp_bool(!l.null && !r.null && typed_compare(OP, l, r));
+}
+template <int OP, int RES, int LT, int RT>
+KG_FN Val sp_arith(Val l, Val r) {
+  l.type = LT;
+  r.type = RT;
+  return arith(OP, RES, l, r);
+}
+KG_FN bool sp_true(const Val& v) { return !v.null && v.bits; }
 
 // ------------------------------------------------------------------------------------------
 // per-lane runtime over the instance arena
@@ -1031,8 +1071,8 @@ KG_FN Val atom_leaf(const GLeaf& f, const GQuery* ql, const Win& w) {
     const int64_t imm = leaf_const(f, ql, w);
     v.null = 0;
     v.bits = f.type == T_FLOAT ? (int64_t)(uint32_t)imm : f.type == T_INT ? (int64_t)(int32_t)imm : imm;
-  } else if (f.kind == LF_ATTR && !w.null(f.slot, f.cap)) {
-    const int64_t raw = w.raw(f.slot, f.cap);
+  } else if ((f.kind == LF_ATTR || f.kind == LF_ATTR0) && !w.null(f.slot, f.cap, f.kind == LF_ATTR0)) {
+    const int64_t raw = w.raw(f.slot, f.cap, f.kind == LF_ATTR0);
     v.null = 0;
     v.bits = f.type == T_INT ? (int64_t)(int32_t)raw : f.type == T_FLOAT ? (int64_t)(uint32_t)raw : raw;
   }
@@ -1152,7 +1192,7 @@ inline void lower_atoms(GQuery& g) {
           }
           if (li.op != OP_ATTR) return false;
           const bool here = li.a <= i && (li.b == 0 || li.b == -1);
-          L.kind = here ? LF_ATTR : LF_NULL;
+          L.kind = here ? (li.b == 0 ? LF_ATTR0 : LF_ATTR) : LF_NULL;
           L.slot = (int8_t)li.a;
           L.cap = (int8_t)li.imm;
           return true;

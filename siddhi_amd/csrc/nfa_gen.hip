@@ -16,66 +16,14 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
-#include "kgen.h"
-#include "nfa_types.h"
+#include "dev_common.h"
+#include "seq_body.h"
 
 namespace sdh {
 
-namespace {
-
-template <class T, int N>
-__device__ __forceinline__ T gpick(const T (&arr)[N], int idx) {
-  T v = arr[0];
-#pragma unroll
-  for (int c = 1; c < N; ++c) v = (idx == c) ? arr[c] : v;
-  return v;
-}
-
-__device__ __forceinline__ int64_t raw_word(const StreamBatch& b, int attr, int64_t e, bool& isnull) {
-  const void* p = gpick(b.col, attr);
-  const uint8_t* nl = gpick(b.nul, attr);
-  const int w = gpick(b.width, attr);
-  isnull = nl && nl[e];
-  if (w == 8) return ((const int64_t*)p)[e];
-  if (w == 4) return (int64_t)((const int32_t*)p)[e];  // int / string id sign-extended; float bits
-  return (int64_t)((const uint8_t*)p)[e];
-}
-
-// match output: one flat word buffer; each record is reserved with an atomic add of its length
-// (the backend's atomic optimizer folds a wave's same-address adds into one atomic + a scan)
-// ring (write_records == 2, SDH_FLAG_DEVICE_MATCHES): every record is still written, at its
-// offset modulo the buffer less a one-record margin, because nobody reads it back
-constexpr int64_t RING_MARGIN = GEN_RING_MARGIN;  // words; > the longest record (checked by the host)
-// In normal mode each record's offset is also listed in rec_off (the device match table finds
-// records by it, matches.hip); a record fits only if its words and its index entry both do.
-struct LaneOut {
-  int64_t* out;
-  int64_t cap;
-  unsigned long long* next;
-  bool ring;
-  int64_t* rec_off;
-  int64_t rec_cap;
-  unsigned long long* rec_next;
-  bool over = false;
-  __device__ void close() {}
-  __device__ int64_t* reserve(int words) {
-    const unsigned long long o = atomicAdd(next, (unsigned long long)words);
-    if (ring) return out + (int64_t)(o % (unsigned long long)(cap - RING_MARGIN));
-    if ((int64_t)(o + words) > cap) {
-      over = true;
-      return nullptr;
-    }
-    const unsigned long long r = atomicAdd(rec_next, 1ull);
-    if ((int64_t)r >= rec_cap) {
-      over = true;
-      return nullptr;
-    }
-    rec_off[r] = (int64_t)o;
-    return out + o;
-  }
-};
-
-}  // namespace
+using dev::gpick;
+using dev::LaneOut;
+using dev::raw_word;
 
 template <int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void nfa_gen_kernel(GenLaunch L) {
@@ -202,104 +150,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
 }
 
 
-// ---- K_seq: sequences as windows of consecutive events (kg::seq_window / kg::seq_match) ----
-// A lane is a query; the wave's 64 queries share one shape (template q, scalar loads). Window
-// starts are tiled by 64: the tile's events (64 + S - 1, tail rows first) are staged once in LDS,
-// then every lane tests every start of the tile against its own constants -- all lanes read the
-// same LDS word at a time (a broadcast). No per-query state exists beyond the stream's tail.
-namespace {
-constexpr int SEQ_TILE = 64;
-constexpr int SEQ_ROW = 3 + kg::GMAXNA;  // ts, seq, null bits, raw words
-
-struct LdsWin {
-  static constexpr bool kStagedConsts = true;
-  const int64_t* base;  // row of window event 0
-  const int64_t* cst;   // this lane's atom constants, [cslot][lane] in LDS
-  __device__ int64_t lane_const(int c) const { return cst[c * 64]; }
-  __device__ int64_t ts(int p) const { return base[p * SEQ_ROW]; }
-  __device__ int64_t raw(int p, int j) const { return base[p * SEQ_ROW + 3 + j]; }
-  __device__ bool null(int p, int j) const { return (base[p * SEQ_ROW + 2] >> j) & 1; }
-};
-}  // namespace
-
-__global__ __launch_bounds__(64) void nfa_seq_kernel(SeqLaunch L) {
-  __shared__ int64_t win[(SEQ_TILE + kg::GMAXS) * SEQ_ROW];
-  __shared__ int64_t cst[kg::GMAXCONST * 64];
-  const int lane = threadIdx.x;
-  const int gi = L.glist[blockIdx.x % L.n_glist];
-  const int chunk = blockIdx.x / L.n_glist;
-  const int qi = L.lane_q[(int64_t)gi * 64 + lane];
-  const kg::GQuery* __restrict__ q = L.queries + L.group_tmpl[gi];
-  const kg::GQuery* __restrict__ ql = L.queries + (qi >= 0 ? qi : L.group_tmpl[gi]);
-  for (int c = 0; c < q->n_const; ++c) cst[c * 64 + lane] = ql->code[q->const_pc[c]].imm;  // once per item
-  const int S = q->n_states;
-  const int stream = L.b.stream;
-  const int na = q->n_cap[stream];
-  const int64_t within = ql->within;
-  // window index w: tail rows 0 .. tail_len-1, then batch event w - tail_len. Start s is evaluated
-  // by the batch holding its last event s + S - 1.
-  const int64_t W = L.tail_len + L.b.n;
-  const int64_t s_begin = L.tail_len - (S - 1) > 0 ? L.tail_len - (S - 1) : 0;
-  const int64_t s_end = W - S + 1;
-  int64_t lo = s_begin + (int64_t)chunk * L.chunk_len;
-  int64_t hi = lo + L.chunk_len < s_end ? lo + L.chunk_len : s_end;
-  LaneOut o{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
-  unsigned long long nrec = 0;
-  for (int64_t t0 = lo; t0 < hi; t0 += SEQ_TILE) {
-    const int cnt = hi - t0 < SEQ_TILE ? (int)(hi - t0) : SEQ_TILE;
-    for (int p = lane; p < cnt + S - 1; p += 64) {  // stage window events t0 .. t0+cnt+S-2
-      const int64_t w = t0 + p;
-      int64_t* row = win + p * SEQ_ROW;
-      int64_t nb = 0;
-      if (w < L.tail_len) {
-        const int64_t* tr = L.tail + w * SEQ_TW;
-        row[0] = tr[0];
-        row[1] = tr[1];
-        for (int j = 0; j < na; ++j) {
-          const int a = q->cap_attr[stream][j];
-          row[3 + j] = tr[2 + a];
-          nb |= (tr[2 + MAXATTR + a] != 0 ? 1ll : 0ll) << j;
-        }
-      } else {
-        const int64_t e = w - L.tail_len;
-        row[0] = L.b.ts[e];
-        row[1] = L.b.seq_base + e;
-        for (int j = 0; j < na; ++j) {
-          bool nl;
-          row[3 + j] = raw_word(L.b, q->cap_attr[stream][j], e, nl);
-          nb |= (nl ? 1ll : 0ll) << j;
-        }
-      }
-      row[2] = nb;
-    }
-    __syncthreads();
-    if (qi >= 0) {
-      for (int s = 0; s < cnt; ++s) {
-        const LdsWin wv{win + s * SEQ_ROW, cst + lane};
-        if (!kg::seq_match(q, ql, within, wv)) continue;
-        ++nrec;
-        if (!L.write_records) continue;
-        const int words = 7 + 2 * S;
-        int64_t* r = o.reserve(words);
-        if (!r) continue;
-        r[0] = words;
-        r[1] = ql->qid;
-        r[2] = -1;
-        r[3] = wv.base[(S - 1) * SEQ_ROW];      // ts of the last event
-        r[4] = wv.base[(S - 1) * SEQ_ROW + 1];  // the triggering event's seq
-        r[5] = 0;                               // one match per event per query
-        r[6] = S | (stream << 16);
-        for (int i = 0; i < S; ++i) {
-          r[7 + 2 * i] = 1;
-          r[8 + 2 * i] = wv.base[i * SEQ_ROW + 1];
-        }
-      }
-    }
-    __syncthreads();
+// ---- K_seq (seq_body.h) with the interpreted window test: the shape's atoms, else its bytecode ----
+struct SeqInterp {
+  static constexpr bool kBranchFree = false;
+  struct K {};
+  __device__ static void load(K&, const kg::GQuery*) {}
+  template <class Win>
+  __device__ static bool match(const K&, const kg::GQuery* q, const kg::GQuery* ql, int64_t within, const Win& w) {
+    return kg::seq_match(q, ql, within, w);
   }
-  if (nrec) atomicAdd(L.rec_count, nrec);
-  if (o.over) atomicOr(&L.err[2], 1);
-}
+};
+
+__global__ __launch_bounds__(64) void nfa_seq_kernel(SeqLaunch L) { seq_body<SeqInterp>(L); }
 
 // the stream's tail after this batch: the last min(SEQ_TMAX, tail_len + n) events of tail ++ batch
 // (rows move towards 0 only, so increasing order is safe in place)

@@ -6,7 +6,9 @@
 // (e.g. e1.price for `price > e1.price`). Device kernels read these tables through the scalar
 // cache (all fields are wave-uniform).
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#endif
 
 namespace sdh {
 
@@ -284,12 +286,11 @@ struct PartLaunch {
   int32_t kind;               // PartKind
   int32_t cap;                // entries per lane
   int32_t ew;                 // words per entry
-  int32_t cl;                 // entries per lane held in LDS while the item runs (<= cap)
-  int32_t pad;
+  int32_t g0, gn;             // this launch runs groups g0 .. g0+gn-1 of the set (one shape)
   int32_t sA, sB;             // logical: state ids of the side processed second (A) and first (B)
   int32_t cmax;               // count: chain words per entry (the set's largest max)
   int32_t n_e1, n_first, n_last;  // count: captured words stored per entry (0 or the stream's n_cap)
-  int32_t n_items;
+  int32_t n_items;            // key segments x gn
   int64_t* st;                // [buffer 0/1][block][PK_HDR + cap * ew][64], block = kid * groups + g
   int64_t blocks;             // blocks per buffer
   const int32_t* cur;         // [kid] buffer holding the key's tables before this push

@@ -1,0 +1,152 @@
+// seq_body.h -- K_seq: sequences as windows of consecutive events (kg::seq_window / kg::seq_match).
+//
+// A lane is a query; the wave's 64 queries share one shape (template q, scalar loads). Window
+// starts are tiled by 64: the tile's events (64 + S - 1, tail rows first) are staged once in LDS,
+// then every lane tests every start of the tile against its own constants -- all lanes read the
+// same LDS word at a time (a broadcast). No per-query state exists beyond the stream's tail.
+//
+// The window test is the Spec's: SeqInterp (nfa_gen.hip) walks the shape's atoms / bytecode, a
+// shape-compiled Spec (spec.hip, generated and compiled with hiprtc when the engine is created) is
+// the same test as straight-line code with the lane's constants in registers.
+#pragma once
+#include "dev_common.h"
+
+namespace sdh {
+
+constexpr int SEQ_TILE = 64;
+constexpr int SEQ_ROW = 3 + kg::GMAXNA;  // ts, seq, null bits, raw words
+
+struct LdsWin {
+  static constexpr bool kStagedConsts = false;
+  const int64_t* base;  // row of window event 0
+  __device__ int64_t lane_const(int) const { return 0; }
+  __device__ int64_t ts(int p) const { return base[p * SEQ_ROW]; }
+  __device__ int64_t raw(int p, int j, bool = false) const { return base[p * SEQ_ROW + 3 + j]; }
+  __device__ bool null(int p, int j, bool = false) const { return (base[p * SEQ_ROW + 2] >> j) & 1; }
+};
+
+template <class Spec>
+__device__ __forceinline__ void seq_body(const SeqLaunch& L) {
+  __shared__ int64_t win[(SEQ_TILE + 8 + kg::GMAXS) * SEQ_ROW];  // (+8: masked starts of the last group)
+  const int lane = threadIdx.x;
+  const int gi = L.glist[blockIdx.x % L.n_glist];
+  const int chunk = blockIdx.x / L.n_glist;
+  const int qi = L.lane_q[(int64_t)gi * 64 + lane];
+  const kg::GQuery* __restrict__ q = L.queries + L.group_tmpl[gi];
+  const kg::GQuery* __restrict__ ql = L.queries + (qi >= 0 ? qi : L.group_tmpl[gi]);
+  typename Spec::K k;
+  Spec::load(k, ql);
+  const int S = q->n_states;
+  const int stream = L.b.stream;
+  const int na = q->n_cap[stream];
+  const int64_t within = ql->within;
+  // window index w: tail rows 0 .. tail_len-1, then batch event w - tail_len. Start s is evaluated
+  // by the batch holding its last event s + S - 1.
+  const int64_t W = L.tail_len + L.b.n;
+  const int64_t s_begin = L.tail_len - (S - 1) > 0 ? L.tail_len - (S - 1) : 0;
+  const int64_t s_end = W - S + 1;
+  int64_t lo = s_begin + (int64_t)chunk * L.chunk_len;
+  int64_t hi = lo + L.chunk_len < s_end ? lo + L.chunk_len : s_end;
+  __shared__ dev::WaveOut::Shared out_sh;
+  dev::WaveOut o;
+  o.g = dev::LaneOut{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
+  o.sh = &out_sh;
+  o.init();
+  unsigned long long nrec = 0;
+  // one window row (event w of tail ++ batch) into registers: the next tile's rows are loaded
+  // while the current tile is tested, and written to LDS after it
+  struct Row {
+    int64_t ts, seq, nb, v[kg::GMAXNA];
+  };
+  auto fetch = [&](int64_t w, Row& r) {
+    r.nb = 0;
+    if (w < L.tail_len) {
+      const int64_t* tr = L.tail + w * SEQ_TW;
+      r.ts = tr[0];
+      r.seq = tr[1];
+      for (int j = 0; j < na; ++j) {
+        const int a = q->cap_attr[stream][j];
+        r.v[j] = tr[2 + a];
+        r.nb |= (tr[2 + MAXATTR + a] != 0 ? 1ll : 0ll) << j;
+      }
+    } else {
+      const int64_t e = w - L.tail_len;
+      r.ts = L.b.ts[e];
+      r.seq = L.b.seq_base + e;
+      for (int j = 0; j < na; ++j) {
+        bool nl;
+        r.v[j] = dev::raw_word(L.b, q->cap_attr[stream][j], e, nl);
+        r.nb |= (nl ? 1ll : 0ll) << j;
+      }
+    }
+  };
+  auto put = [&](int p, const Row& r) {
+    int64_t* row = win + p * SEQ_ROW;
+    row[0] = r.ts;
+    row[1] = r.seq;
+    row[2] = r.nb;
+    for (int j = 0; j < na; ++j) row[3 + j] = r.v[j];
+  };
+  // rows t0 + p for p = lane (and lane + 64 for the S - 1 rows past the tile) that exist
+  const int64_t rows_end = hi + S - 1;  // one past the last window row any start of the chunk reads
+  Row ra, rb;
+  if (lo + lane < rows_end) fetch(lo + lane, ra);
+  if (lane < S - 1 && lo + 64 + lane < rows_end) fetch(lo + 64 + lane, rb);
+  auto emit = [&](int s) {
+    const LdsWin wv{win + s * SEQ_ROW};
+    ++nrec;
+    if (!L.write_records) return;
+    const int words = 7 + 2 * S;
+    int64_t* r = o.reserve(words);
+    if (!r) return;
+    r[0] = words;
+    r[1] = ql->qid;
+    r[2] = -1;
+    r[3] = wv.base[(S - 1) * SEQ_ROW];      // ts of the last event
+    r[4] = wv.base[(S - 1) * SEQ_ROW + 1];  // the triggering event's seq
+    r[5] = 0;                               // one match per event per query
+    r[6] = S | (stream << 16);
+    for (int i = 0; i < S; ++i) {
+      r[7 + 2 * i] = 1;
+      r[8 + 2 * i] = wv.base[i * SEQ_ROW + 1];
+    }
+  };
+  for (int64_t t0 = lo; t0 < hi; t0 += SEQ_TILE) {
+    const int cnt = hi - t0 < SEQ_TILE ? (int)(hi - t0) : SEQ_TILE;
+    if (t0 + lane < rows_end) put(lane, ra);
+    if (lane < S - 1 && t0 + 64 + lane < rows_end) put(64 + lane, rb);
+    __syncthreads();
+    const int64_t t1 = t0 + SEQ_TILE;  // prefetch the next tile's rows
+    if (t1 < hi) {
+      if (t1 + lane < rows_end) fetch(t1 + lane, ra);
+      if (lane < S - 1 && t1 + 64 + lane < rows_end) fetch(t1 + 64 + lane, rb);
+    }
+    if (qi >= 0) {
+      if constexpr (Spec::kBranchFree) {
+        // 8 starts at a time, every state of each evaluated: their LDS reads overlap; starts past
+        // cnt read rows of the LDS window that are stale or unset, and are masked off
+        for (int s0 = 0; s0 < cnt; s0 += 8) {
+          uint32_t m = 0;
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            m |= (Spec::match(k, q, ql, within, LdsWin{win + (s0 + u) * SEQ_ROW}) ? 1u : 0u) << u;
+          if (cnt - s0 < 8) m &= (1u << (cnt - s0)) - 1u;
+          while (m) {
+            const int u = __builtin_ctz(m);
+            m &= m - 1;
+            emit(s0 + u);
+          }
+        }
+      } else {
+        for (int s = 0; s < cnt; ++s)
+          if (Spec::match(k, q, ql, within, LdsWin{win + s * SEQ_ROW})) emit(s);
+      }
+    }
+    __syncthreads();
+  }
+  if (nrec) atomicAdd(L.rec_count, nrec);
+  o.close();
+  if (o.over) atomicOr(&L.err[2], 1);
+}
+
+}  // namespace sdh

@@ -51,7 +51,8 @@ class SdhStats(ctypes.Structure):
                 ("matches", ctypes.c_int64), ("live_partials", ctypes.c_int64),
                 ("last_kernel_ms", ctypes.c_double), ("last_kernel_bytes", ctypes.c_double),
                 ("last_gen_items", ctypes.c_int64), ("last_seq_items", ctypes.c_int64),
-                ("last_part_items", ctypes.c_int64)]
+                ("last_part_items", ctypes.c_int64), ("last_ingest_ms", ctypes.c_double),
+                ("ingest_bytes", ctypes.c_int64), ("spec_kernels", ctypes.c_int64)]
 
 
 EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engine_poll", "sdh_engine_poll_device",

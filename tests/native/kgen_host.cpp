@@ -57,8 +57,8 @@ struct HostWin {  // kg::seq_match's window over Host::Ev records
   size_t s;
   const int32_t* cap;
   int64_t ts(int p) const { return (*ev)[s + p].ts; }
-  int64_t raw(int p, int j) const { return (*ev)[s + p].v[cap[j]]; }
-  bool null(int p, int j) const { return (*ev)[s + p].nl[cap[j]] != 0; }
+  int64_t raw(int p, int j, bool = false) const { return (*ev)[s + p].v[cap[j]]; }
+  bool null(int p, int j, bool = false) const { return (*ev)[s + p].nl[cap[j]] != 0; }
 };
 
 Inst* make_inst(Host* h, int qi, int64_t key) {
