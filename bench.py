@@ -155,8 +155,13 @@ def cpu_baseline(workload, n_symbols, budget_s):
 KERNEL_SOURCES = {  # what a kernel's code and launch configuration are built from
     "nfa_ratchet_kernel": ["nfa_ratchet.hip", "nfa_types.h", "engine.hip"],
     "nfa_gen_kernel": ["nfa_gen.hip", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
-    "nfa_seq_kernel": ["nfa_gen.hip", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
-    "nfa_part_kernel": ["nfa_part.hip", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
+    "nfa_seq_kernel": ["nfa_gen.hip", "seq_body.h", "dev_common.h", "kgen.h", "gen_lower.h", "nfa_types.h",
+                       "engine.hip"],
+    "nfa_part_kernel": ["nfa_part.hip", "part_body.h", "dev_common.h", "kgen.h", "gen_lower.h", "nfa_types.h",
+                        "engine.hip"],
+    # shape-compiled kernels (spec.hip generates and compiles them with hiprtc at engine creation)
+    "sdh_part_spec": ["spec.hip", "part_body.h", "dev_common.h", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
+    "sdh_seq_spec": ["spec.hip", "seq_body.h", "dev_common.h", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
 }
 
 
@@ -276,11 +281,11 @@ def main():
     elif args.workload == "c3":
         wl = (f"C3: count <2:5> + logical and/or patterns, partition with (symbol) over {K} keys, "
               "within 10 sec")
-        kernel = "nfa_gen_kernel"
+        kernel = "sdh_part_spec"
     else:
         wl = ("C4: fraud-rule sequences every e1=Txn[..], e2=Txn[..e1.amount*M], e3=Txn[..] within 1 min "
               f"(strict contiguity), {K} accounts, pattern-set shard {rank * P}..{rank * P + P - 1}")
-        kernel = "nfa_seq_kernel"
+        kernel = "sdh_seq_spec"
     prof, prof_dir = profiled(kernel, args.workload, P, B)
     traffic = prof.get("traffic_bytes") if prof else None
     result = {

@@ -148,6 +148,9 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len);
 void sdh_free(void* p);
 void sdh_engine_destroy(sdh_engine* e);
 const char* sdh_last_error(sdh_engine* e);
+/* Diagnostic, no device needed: generate and compile (hiprtc, gfx950) the shape-compiled kernels of
+ * representative K_seq / K_part shapes. Returns the number compiled, or -1 with the compiler log. */
+int sdh_spec_selftest(char* log, size_t cap);
 /* Library version / build info string (static storage). */
 const char* sdh_version(void);
 

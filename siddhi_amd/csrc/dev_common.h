@@ -69,10 +69,11 @@ struct LaneOut {
 // and flushed to the global buffer with one word reservation and one record-index reservation per
 // flush (a per-record atomic on the two global counters serialises the whole chip once the match
 // rate is ~1e9/s). Collective over the lanes active at the call: every active lane calls reserve()
-// (its record's words) at the same point; offsets inside the buffer come from an LDS atomic, so the
-// records of one call land in any order -- the device match table orders rows by their keys (R18).
-// A record longer than the buffer (or a call whose records cannot fit an empty buffer) is reserved
-// globally per lane, as LaneOut does.
+// (its record's words) at the same point. A lane's offset is the sum of the active lanes below it,
+// computed from six ballots of the record lengths' bits (no LDS atomics: the backend lowers a
+// divergent atomic add into a loop over the active lanes). Records of one call land in lane order;
+// the device match table orders rows by their keys anyway (R18). A call whose records cannot fit an
+// empty buffer reserves globally per lane, as LaneOut does.
 struct WaveOut {
   static constexpr int CAPW = 512;             // words in the LDS buffer (4 KiB: occupancy)
   static constexpr int CAPR = CAPW / 7 + 1;    // records (>= 7 words each)
@@ -80,25 +81,32 @@ struct WaveOut {
     int64_t buf[CAPW];
     int32_t roff[CAPR];
     int64_t base, rbase;
-    int32_t used, nrec, need;
+    int32_t used, nrec;
   };
+  // the wave's shared counters: relaxed atomics, so no lane keeps a stale copy in a register (other
+  // lanes update them) and, unlike volatile, the accesses stay ds_ operations
+  template <class T>
+  __device__ static T ld(T& x) { return __hip_atomic_load(&x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+  template <class T>
+  __device__ static void st(T& x, T v) { __hip_atomic_store(&x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
   LaneOut g;
   Shared* sh;
+  bool over = false;
   __device__ static unsigned long long active() { return __ballot(1); }
-  __device__ static int rank(unsigned long long m) {
-    return __popcll(m & ((1ull << __lane_id()) - 1ull));
-  }
-  __device__ static void fence() { __threadfence_block(); }
+  __device__ static unsigned long long below() { return (1ull << __lane_id()) - 1ull; }
   __device__ void init() {
-    if (__lane_id() == 0) sh->used = sh->nrec = sh->need = 0;
-    fence();
+    if (__lane_id() == 0) {
+      st(sh->used, 0);
+      st(sh->nrec, 0);
+    }
+    __threadfence_block();
   }
   // copy the buffer out (active lanes cooperate)
   __device__ void flush() {
+    __threadfence_block();  // the records' LDS words are written
     const unsigned long long m = active();
-    const int cnt = __popcll(m), me = rank(m), lead = __ffsll((long long)m) - 1;
-    const int n = sh->used, nr = sh->nrec;
-    fence();
+    const int cnt = __popcll(m), me = __popcll(m & below()), lead = __ffsll((long long)m) - 1;
+    const int n = ld(sh->used), nr = ld(sh->nrec);
     if (n == 0) return;
     if (__lane_id() == lead) {
       const unsigned long long o = atomicAdd(g.next, (unsigned long long)n);
@@ -109,46 +117,79 @@ struct WaveOut {
         if ((int64_t)(r + nr) > g.rec_cap) base = -1;
         rbase = (int64_t)r;
       }
-      sh->base = base;
-      sh->rbase = rbase;
+      st(sh->base, base);
+      st(sh->rbase, rbase);
     }
-    fence();
-    const int64_t base = sh->base, rbase = sh->rbase;
+    __threadfence_block();
+    const int64_t base = ld(sh->base), rbase = ld(sh->rbase);
     if (base < 0) {
       g.over = true;
     } else if (g.ring) {
-      const unsigned long long rc = (unsigned long long)(g.cap - GEN_RING_MARGIN);
-      for (int i = me; i < n; i += cnt) g.out[(unsigned long long)(base + i) % rc] = sh->buf[i];
+      const int64_t rc = g.cap - GEN_RING_MARGIN, b0 = (int64_t)((unsigned long long)base % (unsigned long long)rc);
+      for (int i = me; i < n; i += cnt) g.out[b0 + i < rc ? b0 + i : b0 + i - rc] = sh->buf[i];
     } else {
       for (int i = me; i < n; i += cnt) g.out[base + i] = sh->buf[i];
       for (int i = me; i < nr; i += cnt) g.rec_off[rbase + i] = base + sh->roff[i];
     }
-    fence();
-    if (__lane_id() == lead) sh->used = sh->nrec = 0;
-    fence();
+    __threadfence_block();
+    st(sh->used, 0);  // (every active lane writes the same values)
+    st(sh->nrec, 0);
+    __threadfence_block();
+  }
+  // this lane's record of `words` words, written by fill(int64_t* r): into the LDS buffer, or for
+  // an oversized call straight into the global buffer (two instantiations, so the LDS stores are
+  // ds_ writes, not flat ones); skipped once the global buffer overflowed
+  template <class F>
+  __device__ void emit(int words, F&& fill) {
+    const unsigned long long m = active(), lt = below();
+    const int cnt = __popcll(m), rank = __popcll(m & lt);
+    int prefix = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const unsigned long long mb = __ballot((words >> b) & 1);
+      prefix += __popcll(mb & lt) << b;
+      total += __popcll(mb) << b;
+    }
+    if (__ballot(words >= 64) || total > CAPW || cnt > CAPR) {  // (uniform)
+      int64_t* r = g.reserve(words);
+      if (r) fill(r);
+      return;
+    }
+    if (ld(sh->used) + total > CAPW || ld(sh->nrec) + cnt > CAPR) flush();
+    const int base = ld(sh->used), nr = ld(sh->nrec);
+    const int off = base + prefix;
+    sh->roff[nr + rank] = off;
+    __threadfence_block();
+    st(sh->used, base + total);  // (every active lane writes the same values)
+    st(sh->nrec, nr + cnt);
+    fill(sh->buf + off);
   }
   // room for this lane's record of `words` words: a pointer into the LDS buffer (or, for an
   // oversized call, into the global buffer); nullptr once the global buffer overflowed
   __device__ int64_t* reserve(int words) {
-    const unsigned long long m = active();
-    const int lead = __ffsll((long long)m) - 1, cnt = __popcll(m);
-    if (__lane_id() == lead) sh->need = 0;
-    fence();
-    atomicAdd(&sh->need, words);
-    fence();
-    const int total = sh->need;
-    if (total > CAPW || cnt > CAPR) return g.reserve(words);  // (uniform) oversized call
-    if (sh->used + total > CAPW || sh->nrec + cnt > CAPR) flush();
-    const int off = atomicAdd(&sh->used, words);
-    const int ri = atomicAdd(&sh->nrec, 1);
-    sh->roff[ri] = off;
+    const unsigned long long m = active(), lt = below();
+    const int cnt = __popcll(m), rank = __popcll(m & lt);
+    int prefix = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const unsigned long long mb = __ballot((words >> b) & 1);
+      prefix += __popcll(mb & lt) << b;
+      total += __popcll(mb) << b;
+    }
+    if (__ballot(words >= 64) || total > CAPW || cnt > CAPR) return g.reserve(words);  // (uniform)
+    if (ld(sh->used) + total > CAPW || ld(sh->nrec) + cnt > CAPR) flush();
+    const int base = ld(sh->used), nr = ld(sh->nrec);
+    const int off = base + prefix;
+    sh->roff[nr + rank] = off;
+    __threadfence_block();
+    st(sh->used, base + total);  // (every active lane writes the same values)
+    st(sh->nrec, nr + cnt);
     return sh->buf + off;
   }
   __device__ void close() {
     flush();
     over |= g.over;
   }
-  bool over = false;
 };
 
 __device__ __forceinline__ bool expired(int64_t ts1, int64_t ts, int64_t within) {

@@ -648,6 +648,7 @@ struct sdh_engine {
   };
   std::vector<std::unique_ptr<PartSet>> psets;
   DevBuf<int32_t> d_perr;            // per K_part set: [0] entry capacity, [2] output overflow
+  DevBuf<unsigned long long> d_pprof;  // SDH_PART_PROF measurement builds: phase clocks
   DevBuf<int64_t> r_key;
   DevBuf<uint32_t> r_kid, r_kid_s, r_uniq;
   DevBuf<int32_t> r_idx, r_idx_s, r_cnt, r_off, r_nruns;
@@ -1353,7 +1354,11 @@ void spec_build(sdh_engine* e) {
     for (int g = 0; g < ps.n_groups; ++g) ++pg[e->group_tmpl[ps.group_base + g]];
     for (const auto& [t, ng] : pg) {
       if (mode == 1 && ng < 2) continue;
-      const sdh::spec::PartLayout lay{ps.kind, ps.sA, ps.sB, ps.cmax, ps.n_e1, ps.n_first, ps.n_last};
+      // register-resident entries per lane: the first few partials of a (query, key) instance
+      // stay in VGPRs across the key's events (C3 instances hold a handful at a time)
+      int regs = ps.kind == PK_COUNT ? 3 : 8;
+      if (const char* v = getenv(ps.kind == PK_COUNT ? "SDH_KPART_REGS_COUNT" : "SDH_KPART_REGS")) regs = std::max(0, atoi(v));
+      const sdh::spec::PartLayout lay{ps.kind, ps.sA, ps.sB, ps.cmax, ps.n_e1, ps.n_first, ps.n_last, ps.ew, regs};
       std::string err;
       hipFunction_t f = sdh::spec::get_kernel(sdh::spec::part_source(e->gq[t], lay), "sdh_part_spec", &err);
       if (!f && mode == 3) throw Error(SDH_E_DEVICE, "shape-compiled K_part kernel: " + err);
@@ -1834,7 +1839,14 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       P.rec_cap = e->g_out_cap / 7 + 1;
       P.rec_next = e->g_rec_next.p;
       P.write_records = write ? 1 : 2;
+      if (!write && getenv("SDH_DEBUG_COUNT_ONLY")) P.write_records = 0;  // (measurement experiments)
       P.err = e->d_perr.p + 4 * si;
+      static const bool prof = getenv("SDH_PART_PROF") != nullptr;
+      if (prof) {
+        e->d_pprof.ensure(8);
+        HIPCHK(hipMemsetAsync(e->d_pprof.p, 0, 8 * 8, e->stream));
+        P.prof = e->d_pprof.p;
+      }
       // the per-key buffer selector of untouched keys carries over
       HIPCHK(hipMemcpyAsync(ps.nxt.p, ps.cur.p, (size_t)ps.key_cap * 4, hipMemcpyDeviceToDevice, e->stream));
       // one launch per shape (its groups are contiguous), the shape-compiled kernel if there is one
@@ -1854,6 +1866,14 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
           HIPCHK(sdh_launch_part(&P, e->stream));
         }
         e->stats.last_part_items += P.n_items;
+      }
+      if (prof) {  // per-phase clocks of this set's launches (measurement builds, part_body.h)
+        unsigned long long h[8];
+        HIPCHK(hipMemcpyAsync(h, e->d_pprof.p, 8 * 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        const double w = h[5] ? (double)h[5] : 1.0;
+        fprintf(stderr, "[part prof] kind %d waves %llu events/wave %.1f cycles/wave: setup %.0f stage %.0f loop %.0f end %.0f\n",
+                ps.kind, h[5], h[4] / w, h[0] / w, h[1] / w, h[2] / w, h[3] / w);
       }
       ps.ran = true;
       any = true;

@@ -39,8 +39,10 @@ __device__ __forceinline__ bool ev_filter(const kg::GQuery* q, const kg::GQuery*
 
 // K_part with the shape's filters interpreted (the bytecode walked per event)
 struct PartInterp {
+  static constexpr int kRegEntries = 0, kEW = 1;  // the whole table in the global state block
   struct K {};
   __device__ static void load(K&, const kg::GQuery*, const PartLaunch&) {}
+  __device__ static PartOffs offs(const PartLaunch& L) { return PartOffs{L.cmax, L.n_e1, L.n_first, L.n_last}; }
   __device__ static bool f1(const K&, const kg::GQuery* q, const kg::GQuery* ql, const PartLaunch&, const PartEv& ev) {
     return ev_filter(q, ql, 0, ev);
   }
@@ -55,8 +57,9 @@ struct PartInterp {
   }
   // e3 of the count chain over the partial as it is now: slot 2 the current event, slot 0 e1,
   // slot 1 the chain's first (index 0) or last (CURRENT) event -- all exist (len >= min >= 1)
+  template <class En>
   __device__ static bool f3(const K&, const kg::GQuery* q, const kg::GQuery* ql, const PartLaunch&, const PartEv& ev,
-                            const PartEnt& en) {
+                            const En& en) {
     const kg::GState& s3 = q->st[2];
     for (int f = 0; f < s3.n_filt; ++f) {
       const kg::Val v = kg::eval_code<kg::RegStack>(

@@ -304,6 +304,7 @@ struct PartLaunch {
   unsigned long long* rec_next;
   int32_t write_records;
   int32_t* err;               // [0] entry capacity, [2] output overflow
+  unsigned long long* prof;   // SDH_PART_PROF builds: per-phase clock sums (part_body.h), else null
 };
 
 // ------------------------------------------------------------------------------------------

@@ -48,23 +48,126 @@ struct PartEv {
   __device__ bool null(int j) const { return (nul >> j) & 1u; }
 };
 
-// a count partial as f3 sees it: e1's words, the chain's first and last event words (entry words
-// o_e1.., o_first.., o_last..) and their null bits in the flags word (16 / 24 / 32 + j)
+// entry word offsets of a count partial: chain words 3 .. 3+cmax-1, then e1's, the chain's first
+// and its last event's captured words (those f3 reads)
+struct PartOffs {
+  int cmax, n_e1, n_first, n_last;
+  __device__ int o_e1() const { return 3 + cmax; }
+  __device__ int o_first() const { return 3 + cmax + n_e1; }
+  __device__ int o_last() const { return 3 + cmax + n_e1 + n_first; }
+};
+
+// A partial's words wherever they live: GRef in the lane's global state block (stride 64 words),
+// RRef in registers (a row of the lane's register table; an index that is not a compile-time
+// constant selects among the row's words, so the row never leaves VGPRs)
+struct GRef {
+  int64_t* p;
+  __device__ int64_t get(int w) const { return p[(int64_t)w * 64]; }
+  __device__ void set(int w, int64_t v) const { p[(int64_t)w * 64] = v; }
+};
+template <int EW>
+struct RRef {
+  int64_t* p;
+  __device__ int64_t get(int w) const {
+    int64_t v = p[0];
+#pragma unroll
+    for (int x = 1; x < EW; ++x) v = (w == x) ? p[x] : v;
+    return v;
+  }
+  // (value selects and unconditional stores: conditional stores to different words get merged into
+  // one store through a selected pointer, which keeps the row out of registers)
+  __device__ void set(int w, int64_t v) const {
+#pragma unroll
+    for (int x = 0; x < EW; ++x) p[x] = (w == x) ? v : p[x];
+  }
+};
+
+// a count partial as f3 sees it: e1's words, the chain's first and last event words and their null
+// bits in the flags word (16 / 24 / 32 + j)
+template <class Ref>
 struct PartEnt {
-  const int64_t* p;  // entry word 0 of this lane (stride 64)
+  Ref e;
   int64_t fl;
-  int o_e1, o_first, o_last;
-  __device__ int64_t word(int x) const { return p[(int64_t)x * 64]; }
-  __device__ int64_t e1(int j) const { return word(o_e1 + j); }
-  __device__ int64_t first(int j) const { return word(o_first + j); }
-  __device__ int64_t last(int j) const { return word(o_last + j); }
+  PartOffs of;
+  __device__ int64_t e1(int j) const { return e.get(of.o_e1() + j); }
+  __device__ int64_t first(int j) const { return e.get(of.o_first() + j); }
+  __device__ int64_t last(int j) const { return e.get(of.o_last() + j); }
   __device__ bool e1_null(int j) const { return (fl >> (16 + j)) & 1; }
   __device__ bool first_null(int j) const { return (fl >> (24 + j)) & 1; }
   __device__ bool last_null(int j) const { return (fl >> (32 + j)) & 1; }
 };
 
+template <class Ref>
+__device__ __forceinline__ PartEnt<Ref> part_ent(const Ref& e, int64_t fl, const PartOffs& of) {
+  return PartEnt<Ref>{e, fl, of};
+}
+
+// The lane's partial table: entries 0 .. RC-1 in registers (RC = 0: none), the rest in its global
+// state block; every walk visits the entries in list (creation) order
+template <int RC, int EW>
+struct PartTable {
+  int64_t r[RC > 0 ? RC : 1][EW];
+  int64_t* g;  // entry kk word w at g[(kk * ew + w) * 64]
+  int ew;
+  __device__ GRef gref(int kk) const { return GRef{g + (int64_t)kk * ew * 64}; }
+  // body(kk, ref) for kk = 0 .. n-1
+  template <class F>
+  __device__ void each(int n, F&& body) {
+    if constexpr (RC > 0) {
+#pragma unroll
+      for (int kk = 0; kk < RC; ++kk)
+        if (kk < n) body(kk, RRef<EW>{r[kk]});
+    }
+    for (int kk = RC; kk < n; ++kk) body(kk, gref(kk));
+  }
+  // entry w <- the `words` words of src (w <= the index src was read from)
+  template <class Ref>
+  __device__ void put(int w, const Ref& src, int words) {
+    if constexpr (RC > 0) {
+      if (w < RC) {
+        int64_t v[EW];
+#pragma unroll
+        for (int x = 0; x < EW; ++x) v[x] = src.get(x);
+#pragma unroll
+        for (int t = 0; t < RC; ++t)
+#pragma unroll
+          for (int x = 0; x < EW; ++x) r[t][x] = (w == t && x < words) ? v[x] : r[t][x];
+        return;
+      }
+    }
+    const GRef d = gref(w);
+    for (int x = 0; x < words; ++x) d.set(x, src.get(x));
+  }
+  // one word of entry w
+  __device__ void set(int w, int x, int64_t v) {
+    if constexpr (RC > 0) {
+      if (w < RC) {
+#pragma unroll
+        for (int t = 0; t < RC; ++t)
+#pragma unroll
+          for (int y = 0; y < EW; ++y) r[t][y] = (w == t && x == y) ? v : r[t][y];
+        return;
+      }
+    }
+    gref(w).set(x, v);
+  }
+};
+
+#ifdef SDH_PART_PROF  // phase clocks (measurement builds only: SDH_PART_PROF=1 at engine creation)
+#define PPROF_T(v) const unsigned long long v = clock64()
+#define PPROF_ADD(i, d) (prof_acc[i] += (d))
+#else
+#define PPROF_T(v) ((void)0)
+#define PPROF_ADD(i, d) ((void)0)
+#endif
+
 template <int KIND, class Spec>
 __device__ __forceinline__ void part_body(const PartLaunch& L) {
+#ifdef SDH_PART_PROF
+  unsigned long long prof_acc[6] = {0, 0, 0, 0, 0, 0};
+#endif
+  PPROF_T(c_start);
+  constexpr int RC = Spec::kRegEntries, EW = Spec::kEW;
   const int lane = threadIdx.x;
   const int item = blockIdx.x;
   if (item >= L.n_items) return;
@@ -77,25 +180,34 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
   const kg::GQuery* __restrict__ ql = L.queries + (qi >= 0 ? qi : L.group_tmpl[L.group_base + g]);
   typename Spec::K k;
   Spec::load(k, ql, L);
+  const PartOffs of = Spec::offs(L);
   const int stream = L.b.stream;
   const int ncap = q->n_cap[stream];
   const int64_t within = ql->within;
   const int64_t key = L.key_of_id[kid];
-  const int64_t bw = PK_HDR + (int64_t)L.cap * L.ew;
+  const int ew = RC > 0 ? EW : L.ew;
+  const int64_t bw = PK_HDR + (int64_t)L.cap * ew;
   const int64_t block = (int64_t)kid * L.groups + g;
   const int cb = L.cur[kid];
   const int64_t* __restrict__ in = L.st + ((int64_t)cb * L.blocks + block) * bw * 64 + lane;
   int64_t* __restrict__ st = L.st + ((int64_t)(1 - cb) * L.blocks + block) * bw * 64 + lane;
   if (g == 0 && lane == 0) L.nxt[kid] = 1 - cb;
-  const int ew = L.ew;
-  auto W = [&](int64_t i) -> int64_t& { return st[i * 64]; };
-  auto E = [&](int kk, int w) -> int64_t& { return st[(PK_HDR + (int64_t)kk * ew + w) * 64]; };
 
-  // the lane's table: input buffer -> output block (the working copy)
+  // the lane's table: input buffer -> registers (first RC entries) and the output block (the rest)
+  PartTable<RC, EW> tab;
+  tab.g = st + PK_HDR * 64;
+  tab.ew = ew;
   int n = (int)in[0];
-  int64_t hdr1 = in[64];
-  for (int kk = 0; kk < n; ++kk)
-    for (int w = 0; w < ew; ++w) E(kk, w) = in[(PK_HDR + (int64_t)kk * ew + w) * 64];
+  const int64_t hdr1 = in[64];
+  {
+    const GRef src{const_cast<int64_t*>(in) + PK_HDR * 64};
+    for (int kk = 0; kk < n; ++kk) {
+      const GRef e{src.p + (int64_t)kk * ew * 64};
+      if (kk < RC) tab.put(kk, e, ew);
+      else
+        for (int w = 0; w < ew; ++w) tab.gref(kk).set(w, e.get(w));
+    }
+  }
 
   // the key's events, staged 64 at a time (one coalesced index load and one gather per lane), then
   // read by broadcast: ts, seq, null bits and the captured words
@@ -112,7 +224,10 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
   const int sA = L.sA;
   int F = (int)(hdr1 & 0xffffffff), side = (int)(hdr1 >> 32);  // logical: filled prefix and its side
 
+  PPROF_T(c_setup);
+  PPROF_ADD(0, c_setup - c_start);
   for (int64_t t0 = e0; t0 < e1; t0 += 64) {
+    PPROF_T(c_t0);
     const int cnt = e1 - t0 < 64 ? (int)(e1 - t0) : 64;
     if (lane < cnt) {
       const int64_t e = L.ev_idx[t0 + lane];
@@ -127,6 +242,8 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
       t_nul[lane] = nb;
     }
     __syncthreads();
+    PPROF_T(c_t1);
+    PPROF_ADD(1, c_t1 - c_t0);
     for (int te = 0; te < cnt && live; ++te) {
       const int64_t seq = t_seq[te];
       const int64_t ts = t_ts[te];
@@ -134,50 +251,50 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
       const bool f1 = Spec::f1(k, q, ql, L, ev);
       int64_t idx = 0;  // emission index of this (instance, event): the pending-list order
 
-      if (KIND == PK_OR || KIND == PK_AND) {
+      if constexpr (KIND == PK_OR || KIND == PK_AND) {
         const bool fb = Spec::fb(k, q, ql, L, ev), fa = Spec::fa(k, q, ql, L, ev);
         // expiry of every partial (both sides' isExpired see the same event timestamp)
         if (within >= 0) {
           int w = 0, Fw = 0;
-          for (int kk = 0; kk < n; ++kk) {
-            if (dev::expired(E(kk, 0), ts, within)) continue;
-            if (w != kk)
-              for (int x = 0; x < ew; ++x) E(w, x) = E(kk, x);
+          tab.each(n, [&](int kk, const auto& e) {
+            if (dev::expired(e.get(0), ts, within)) return;
+            if (w != kk) tab.put(w, e, 3);
             if (kk < F) ++Fw;
             ++w;
-          }
+          });
           n = w;
           F = Fw;
           if (F == 0) side = 0;
         }
-        auto emit = [&](int kk, int64_t a_seq, int64_t b_seq) {  // a_seq / b_seq: -1 = empty slot
+        auto emit = [&](int64_t e1seq, int64_t a_seq, int64_t b_seq) {  // a_seq / b_seq: -1 = empty slot
           ++nrec;
           if (!L.write_records) return;
           const int words = 7 + 2 + (a_seq >= 0 ? 2 : 1) + (b_seq >= 0 ? 2 : 1);
-          int64_t* r = o.reserve(words);
-          if (!r) return;
-          r[0] = words;
-          r[1] = ql->qid;
-          r[2] = key;
-          r[3] = ts;
-          r[4] = seq;
-          r[5] = idx++;
-          r[6] = 3 | (stream << 16);
-          int p = 7;
-          for (int s = 0; s < 3; ++s) {
-            const int64_t v = s == 0 ? E(kk, 1) : s == sA ? a_seq : b_seq;
-            if (v >= 0) {
-              r[p++] = 1;
-              r[p++] = v;
-            } else {
-              r[p++] = 0;
+          const int64_t my_idx = idx++;
+          o.emit(words, [&](int64_t* r) {
+            r[0] = words;
+            r[1] = ql->qid;
+            r[2] = key;
+            r[3] = ts;
+            r[4] = seq;
+            r[5] = my_idx;
+            r[6] = 3 | (stream << 16);
+            int p = 7;
+            for (int s = 0; s < 3; ++s) {
+              const int64_t v = s == 0 ? e1seq : s == sA ? a_seq : b_seq;
+              if (v >= 0) {
+                r[p++] = 1;
+                r[p++] = v;
+              } else {
+                r[p++] = 0;
+              }
             }
-          }
+          });
         };
-        if (KIND == PK_OR) {
+        if constexpr (KIND == PK_OR) {
           // side B first (its processor runs first), then side A; either empties the list
           if (fb || fa) {
-            for (int kk = 0; kk < n; ++kk) emit(kk, fb ? -1 : seq, fb ? seq : -1);
+            tab.each(n, [&](int, const auto& e) { emit(e.get(1), fb ? -1 : seq, fb ? seq : -1); });
             n = 0;
           }
         } else if (fb || fa) {
@@ -186,32 +303,31 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
           // in creation order and every completed partial precedes every surviving one, so one walk
           // in list order emits in the reference's order.
           int w = 0;
-          for (int kk = 0; kk < n; ++kk) {
+          tab.each(n, [&](int kk, const auto& e) {
             const bool filled = kk < F;
             int64_t aseq = -1, bseq = -1;
-            if (filled && side == 1) aseq = E(kk, 2);
-            if (filled && side == 2) bseq = E(kk, 2);
+            if (filled && side == 1) aseq = e.get(2);
+            if (filled && side == 2) bseq = e.get(2);
             if (fb && bseq < 0) bseq = seq;  // B pass: the partials whose B slot is empty
             if (fa && aseq < 0) aseq = seq;  // A pass: those whose A slot is empty (B-filled too)
             if (aseq >= 0 && bseq >= 0) {
-              emit(kk, aseq, bseq);
-              continue;
+              emit(e.get(1), aseq, bseq);
+              return;
             }
             // survivor: exactly one side filled
-            if (w != kk)
-              for (int x = 0; x < ew; ++x) E(w, x) = E(kk, x);
-            E(w, 2) = aseq >= 0 ? aseq : bseq;
+            e.set(2, aseq >= 0 ? aseq : bseq);
+            if (w != kk) tab.put(w, e, 3);
             ++w;
-          }
+          });
           n = w;
           F = w;
           side = n == 0 ? 0 : (fb ? 2 : 1);
         }
         if (f1) {  // e1 opens a partial; it joins both sides' lists at the next event
           if (n < L.cap) {
-            E(n, 0) = ts;
-            E(n, 1) = seq;
-            E(n, 2) = -1;
+            tab.set(n, 0, ts);
+            tab.set(n, 1, seq);
+            tab.set(n, 2, -1);
             ++n;
           } else {
             cap_over = true;
@@ -220,69 +336,66 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
       } else {  // PK_COUNT
         const bool f2 = Spec::f2(k, q, ql, L, ev);
         const int cmin = q->st[1].min, cmax = q->st[1].max;  // this shape's <min:max>
-        const int o_e1 = 3 + L.cmax, o_first = o_e1 + L.n_e1, o_last = o_first + L.n_first;
+        const int ewc = 3 + of.cmax + of.n_e1 + of.n_first + of.n_last;
         int w = 0;
-        for (int kk = 0; kk < n; ++kk) {
-          int64_t fl = E(kk, 2);
+        tab.each(n, [&](int kk, const auto& e) {
+          int64_t fl = e.get(2);
           int len = (int)(fl & 0xff);
           bool inL3 = (fl >> 8) & 1;
-          bool done = false;
           // e3 (processed first): expiry, then f3 over the partial as it is now
           if (inL3) {
-            if (dev::expired(E(kk, 0), ts, within)) {
+            if (dev::expired(e.get(0), ts, within)) {
               inL3 = false;
-            } else if (Spec::f3(k, q, ql, L, ev, PartEnt{&E(kk, 0), fl, o_e1, o_first, o_last})) {
-              done = true;  // completed: removed from e3's list now, from the count list at this event
+            } else if (Spec::f3(k, q, ql, L, ev, part_ent(e, fl, of))) {
+              // completed: removed from e3's list now, from the count list at this event
               ++nrec;
               if (L.write_records) {
                 const int words = 7 + 2 + 1 + len + 2;
-                int64_t* r = o.reserve(words);
-                if (r) {
+                const int64_t my_idx = idx++;
+                o.emit(words, [&](int64_t* r) {
                   r[0] = words;
                   r[1] = ql->qid;
                   r[2] = key;
                   r[3] = ts;
                   r[4] = seq;
-                  r[5] = idx++;
+                  r[5] = my_idx;
                   r[6] = 3 | (stream << 16);
                   r[7] = 1;
-                  r[8] = E(kk, 1);
+                  r[8] = e.get(1);
                   r[9] = len;
-                  for (int c = 0; c < len; ++c) r[10 + c] = E(kk, 3 + c);
+                  for (int c = 0; c < len; ++c) r[10 + c] = e.get(3 + c);
                   r[10 + len] = 1;
                   r[11 + len] = seq;
-                }
+                });
               }
+              return;
             }
           }
-          if (done) continue;
           // count state: a partial with len < max appends every f2-passing event
           if (len < cmax && f2) {
-            E(kk, 3 + len) = seq;
+            e.set(3 + len, seq);
             const int64_t nb = (int64_t)(ev.nul & 0xff);
             if (len == 0) {
-              for (int j = 0; j < L.n_first; ++j) E(kk, o_first + j) = ev.word(j);
+              for (int j = 0; j < of.n_first; ++j) e.set(of.o_first() + j, ev.word(j));
               fl = (fl & ~(0xffll << 24)) | (nb << 24);
             }
-            for (int j = 0; j < L.n_last; ++j) E(kk, o_last + j) = ev.word(j);
+            for (int j = 0; j < of.n_last; ++j) e.set(of.o_last() + j, ev.word(j));
             fl = (fl & ~(0xffll << 32)) | (nb << 32);
             ++len;
             if (len == cmin) inL3 = true;  // CountPost: next.addState at n == min (visible next event)
           }
-          if (!inL3 && len >= cmax) continue;  // in neither list any more
-          fl = (fl & ~0x1ffll) | (int64_t)len | ((int64_t)inL3 << 8);
-          if (w != kk)
-            for (int x = 0; x < ew; ++x) E(w, x) = E(kk, x);
-          E(w, 2) = fl;
+          if (!inL3 && len >= cmax) return;  // in neither list any more
+          e.set(2, (fl & ~0x1ffll) | (int64_t)len | ((int64_t)inL3 << 8));
+          if (w != kk) tab.put(w, e, ewc);
           ++w;
-        }
+        });
         n = w;
         if (f1) {
           if (n < L.cap) {
-            E(n, 0) = ts;
-            E(n, 1) = seq;
-            for (int j = 0; j < L.n_e1; ++j) E(n, o_e1 + j) = ev.word(j);
-            E(n, 2) = (int64_t)(ev.nul & 0xff) << 16;  // e1's null bits
+            tab.set(n, 0, ts);
+            tab.set(n, 1, seq);
+            for (int j = 0; j < of.n_e1; ++j) tab.set(n, of.o_e1() + j, ev.word(j));
+            tab.set(n, 2, (int64_t)(ev.nul & 0xff) << 16);  // e1's null bits
             ++n;
           } else {
             cap_over = true;
@@ -291,13 +404,31 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
       }
     }
     __syncthreads();  // the tile is rewritten next
+    PPROF_T(c_t2);
+    PPROF_ADD(2, c_t2 - c_t1);
+    PPROF_ADD(4, cnt);
   }
-  W(0) = n;
-  W(1) = (int64_t)(uint32_t)F | ((int64_t)side << 32);
+  PPROF_T(c_loop);
+  // register entries back to the output block
+  if constexpr (RC > 0) {
+#pragma unroll
+    for (int kk = 0; kk < RC; ++kk)
+      if (kk < n)
+        for (int w = 0; w < ew; ++w) tab.gref(kk).set(w, tab.r[kk][w]);
+  }
+  st[0] = n;
+  st[64] = (int64_t)(uint32_t)F | ((int64_t)side << 32);
+  o.close();
   if (nrec) atomicAdd(L.rec_count, nrec);
   if (cap_over) atomicOr(&L.err[0], 1);
-  o.close();
   if (o.over) atomicOr(&L.err[2], 1);
+#ifdef SDH_PART_PROF
+  PPROF_T(c_end);
+  PPROF_ADD(3, c_end - c_loop);
+  PPROF_ADD(5, 1);
+  if (lane == 0 && L.prof)
+    for (int i = 0; i < 6; ++i) atomicAdd(&L.prof[i], prof_acc[i]);
+#endif
 }
 
 }  // namespace sdh

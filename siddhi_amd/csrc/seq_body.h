@@ -64,7 +64,9 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
       const int64_t* tr = L.tail + w * SEQ_TW;
       r.ts = tr[0];
       r.seq = tr[1];
-      for (int j = 0; j < na; ++j) {
+#pragma unroll
+      for (int j = 0; j < kg::GMAXNA; ++j) {  // (constant indices: the row stays in registers)
+        if (j >= na) break;
         const int a = q->cap_attr[stream][j];
         r.v[j] = tr[2 + a];
         r.nb |= (tr[2 + MAXATTR + a] != 0 ? 1ll : 0ll) << j;
@@ -73,7 +75,9 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
       const int64_t e = w - L.tail_len;
       r.ts = L.b.ts[e];
       r.seq = L.b.seq_base + e;
-      for (int j = 0; j < na; ++j) {
+#pragma unroll
+      for (int j = 0; j < kg::GMAXNA; ++j) {
+        if (j >= na) break;
         bool nl;
         r.v[j] = dev::raw_word(L.b, q->cap_attr[stream][j], e, nl);
         r.nb |= (nl ? 1ll : 0ll) << j;
@@ -85,7 +89,9 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
     row[0] = r.ts;
     row[1] = r.seq;
     row[2] = r.nb;
-    for (int j = 0; j < na; ++j) row[3 + j] = r.v[j];
+#pragma unroll
+    for (int j = 0; j < kg::GMAXNA; ++j)
+      if (j < na) row[3 + j] = r.v[j];
   };
   // rows t0 + p for p = lane (and lane + 64 for the S - 1 rows past the tile) that exist
   const int64_t rows_end = hi + S - 1;  // one past the last window row any start of the chunk reads
@@ -97,19 +103,19 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
     ++nrec;
     if (!L.write_records) return;
     const int words = 7 + 2 * S;
-    int64_t* r = o.reserve(words);
-    if (!r) return;
-    r[0] = words;
-    r[1] = ql->qid;
-    r[2] = -1;
-    r[3] = wv.base[(S - 1) * SEQ_ROW];      // ts of the last event
-    r[4] = wv.base[(S - 1) * SEQ_ROW + 1];  // the triggering event's seq
-    r[5] = 0;                               // one match per event per query
-    r[6] = S | (stream << 16);
-    for (int i = 0; i < S; ++i) {
-      r[7 + 2 * i] = 1;
-      r[8 + 2 * i] = wv.base[i * SEQ_ROW + 1];
-    }
+    o.emit(words, [&](int64_t* r) {
+      r[0] = words;
+      r[1] = ql->qid;
+      r[2] = -1;
+      r[3] = wv.base[(S - 1) * SEQ_ROW];      // ts of the last event
+      r[4] = wv.base[(S - 1) * SEQ_ROW + 1];  // the triggering event's seq
+      r[5] = 0;                               // one match per event per query
+      r[6] = S | (stream << 16);
+      for (int i = 0; i < S; ++i) {
+        r[7 + 2 * i] = 1;
+        r[8 + 2 * i] = wv.base[i * SEQ_ROW + 1];
+      }
+    });
   };
   for (int64_t t0 = lo; t0 < hi; t0 += SEQ_TILE) {
     const int cnt = hi - t0 < SEQ_TILE ? (int)(hi - t0) : SEQ_TILE;

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <vector>
 
 #include "kgen.h"
 
@@ -25,8 +26,13 @@ std::string seq_source(const kg::GQuery& g);
 // kernel "sdh_part_spec"
 struct PartLayout {
   int kind, sA, sB, cmax, n_e1, n_first, n_last;
+  int ew;            // words per entry
+  int reg_entries;   // entries of a lane's table kept in registers
 };
 std::string part_source(const kg::GQuery& g, const PartLayout& lay);
+
+// hiprtc: src -> code object for `arch` (e.g. "gfx950"); empty and *err on failure
+std::vector<char> compile(const std::string& src, const std::string& arch, std::string* err);
 
 // Compile `src` for the current device and load it; returns kernel `name`. Cached per (device,
 // source) for the life of the process. nullptr and *err on failure.

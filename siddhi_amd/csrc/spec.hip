@@ -7,6 +7,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <functional>
 #include <map>
 #include <mutex>
@@ -190,8 +191,8 @@ std::string part_source(const kg::GQuery& g, const PartLayout& lay) {
   fns += ev_fn("fa", logical ? lay.sA : -1);
   fns += ev_fn("fb", logical ? lay.sB : -1);
   fns += ev_fn("f2", logical ? -1 : 1);
-  fns += "  __device__ static bool f3(const K& k, const sdh::kg::GQuery*, const sdh::kg::GQuery*, const sdh::PartLaunch&, "
-         "const sdh::PartEv& ev, const sdh::PartEnt& en) {\n    (void)k;\n    (void)ev;\n    (void)en;\n"
+  fns += "  template <class En>\n  __device__ static bool f3(const K& k, const sdh::kg::GQuery*, const sdh::kg::GQuery*, "
+         "const sdh::PartLaunch&, const sdh::PartEv& ev, const En& en) {\n    (void)k;\n    (void)ev;\n    (void)en;\n"
          "    bool ok = true;\n";
   if (!logical) {
     const kg::GState& st = g.st[2];
@@ -216,6 +217,9 @@ std::string part_source(const kg::GQuery& g, const PartLayout& lay) {
   }
   fns += "    return ok;\n  }\n";
   std::string s = header() + "#include \"part_body.h\"\n\nstruct SpecPart {\n";
+  s += fmt("  static constexpr int kRegEntries = %d, kEW = %d;\n", lay.reg_entries, lay.ew);
+  s += fmt("  __device__ static sdh::PartOffs offs(const sdh::PartLaunch&) { return sdh::PartOffs{%d, %d, %d, %d}; }\n",
+           lay.cmax, lay.n_e1, lay.n_first, lay.n_last);
   s += K.decl();
   s += "  __device__ static void load(K& k, const sdh::kg::GQuery* ql, const sdh::PartLaunch&) {\n";
   std::string ld = K.load();
@@ -226,6 +230,50 @@ std::string part_source(const kg::GQuery& g, const PartLayout& lay) {
            "  sdh::part_body<%d, SpecPart>(L);\n}\n",
            lay.kind);
   return s;
+}
+
+// hiprtc: src -> code object for `arch` (e.g. "gfx950"); empty and *err on failure
+std::vector<char> compile(const std::string& src_in, const std::string& arch, std::string* err) {
+  // measurement builds: SDH_PART_PROF=1 compiles part_body's phase clocks in (engine prints them)
+  const std::string src = getenv("SDH_PART_PROF") ? "#define SDH_PART_PROF 1\n" + src_in : src_in;
+  hiprtcProgram prog = nullptr;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "sdh_spec.hip", k_spec_n_headers, k_spec_headers,
+                          k_spec_header_names) != HIPRTC_SUCCESS) {
+    *err = "hiprtcCreateProgram failed";
+    return {};
+  }
+  // the static kernels' floating-point contract: no contraction, IEEE denormals (Java semantics)
+  const std::string a = "--offload-arch=" + arch;
+  const char* opts[] = {a.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                        "-fno-gpu-flush-denormals-to-zero"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+  if (rc != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    hiprtcDestroyProgram(&prog);
+    *err = "hiprtc: " + log.substr(0, 4000);
+    return {};
+  }
+  size_t n = 0;
+  hiprtcGetCodeSize(prog, &n);
+  std::vector<char> code(n);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  if (const char* dir = getenv("SDH_SPEC_DUMP")) {  // inspection: source + code object per kernel
+    const size_t h = std::hash<std::string>{}(src);
+    const std::string base = std::string(dir) + "/" + fmt("spec_%016zx", h);
+    if (FILE* f = fopen((base + ".hip").c_str(), "w")) {
+      fwrite(src.data(), 1, src.size(), f);
+      fclose(f);
+    }
+    if (FILE* f = fopen((base + ".co").c_str(), "wb")) {
+      fwrite(code.data(), 1, code.size(), f);
+      fclose(f);
+    }
+  }
+  return code;
 }
 
 hipFunction_t get_kernel(const std::string& src, const char* name, std::string* err) {
@@ -246,31 +294,8 @@ hipFunction_t get_kernel(const std::string& src, const char* name, std::string* 
     return nullptr;
   }
   std::string arch = prop.gcnArchName;
-  arch = "--offload-arch=" + arch.substr(0, arch.find(':'));
-  hiprtcProgram prog = nullptr;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "sdh_spec.hip", k_spec_n_headers, k_spec_headers,
-                          k_spec_header_names) != HIPRTC_SUCCESS) {
-    *err = "hiprtcCreateProgram failed";
-    return nullptr;
-  }
-  // the static kernels' floating-point contract: no contraction, IEEE denormals (Java semantics)
-  const char* opts[] = {arch.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                        "-fno-gpu-flush-denormals-to-zero"};
-  const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
-  if (rc != HIPRTC_SUCCESS) {
-    size_t n = 0;
-    hiprtcGetProgramLogSize(prog, &n);
-    std::string log(n, '\0');
-    if (n) hiprtcGetProgramLog(prog, &log[0]);
-    hiprtcDestroyProgram(&prog);
-    *err = "hiprtc: " + log.substr(0, 2000);
-    return nullptr;
-  }
-  size_t n = 0;
-  hiprtcGetCodeSize(prog, &n);
-  std::vector<char> code(n);
-  hiprtcGetCode(prog, code.data());
-  hiprtcDestroyProgram(&prog);
+  const std::vector<char> code = compile(src, arch.substr(0, arch.find(':')), err);
+  if (code.empty()) return nullptr;
   Loaded l;
   if (hipModuleLoadData(&l.mod, code.data()) != hipSuccess || hipModuleGetFunction(&l.fn, l.mod, name) != hipSuccess) {
     (void)hipGetLastError();
@@ -283,3 +308,29 @@ hipFunction_t get_kernel(const std::string& src, const char* name, std::string* 
 
 }  // namespace spec
 }  // namespace sdh
+
+// Build check without a device (tests/test_abi.py): the generated K_seq and K_part kernels of
+// representative shapes (filterless 3-state windows / partials; every K_part kind, register tables
+// on and off) compile for gfx950. Returns the number compiled, or -1 with the first log in `log`.
+extern "C" int sdh_spec_selftest(char* log, size_t cap) {
+  using namespace sdh;
+  kg::GQuery g{};
+  g.n_states = 3;
+  g.within = 0;
+  std::vector<std::string> srcs{spec::seq_source(g)};
+  for (int kind = PK_OR; kind <= PK_COUNT; ++kind)
+    for (int regs : {0, 4}) {
+      const int ew = kind == PK_COUNT ? 3 + 5 + 1 + 1 + 1 : 3;
+      srcs.push_back(spec::part_source(g, spec::PartLayout{kind, 1, 2, 5, 1, 1, 1, ew, regs}));
+    }
+  int ok = 0;
+  for (const auto& src : srcs) {
+    std::string err;
+    if (spec::compile(src, "gfx950", &err).empty()) {
+      if (log && cap) snprintf(log, cap, "%s", err.c_str());
+      return -1;
+    }
+    ++ok;
+  }
+  return ok;
+}

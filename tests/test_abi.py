@@ -82,3 +82,14 @@ def test_valid_program_needs_a_device():
     rc, h = _create(lib, plan(ql.parse(c1_app())).serialize())
     assert rc == -3 and not h.value
     assert b"no hip device" in lib.sdh_last_error(None).lower()
+
+
+def test_shape_compiled_kernels_build_without_a_device():
+    """spec.hip's generated K_seq / K_part sources (register tables on and off) compile for gfx950
+    through hiprtc on a host with no GPU."""
+    from siddhi_amd.engine import load_library
+    lib = load_library()
+    lib.sdh_spec_selftest.restype = ctypes.c_int
+    log = ctypes.create_string_buffer(8192)
+    n = lib.sdh_spec_selftest(log, len(log))
+    assert n == 7, log.value.decode(errors="replace")

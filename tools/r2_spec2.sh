@@ -10,7 +10,7 @@ tail -2 $OUT/gen.log
 timeout -k 10 300 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_gpu_golden.py > $OUT/golden.log 2>&1 || { tail -30 $OUT/golden.log; exit 1; }
 tail -2 $OUT/golden.log
 unset SDH_SPEC
-timeout -k 10 200 python -u tools/diag_pools.py > $OUT/pools.log 2>&1; tail -25 $OUT/pools.log
+PYTHONPATH=. timeout -k 10 200 python -u tools/diag_pools.py > $OUT/pools.log 2>&1; tail -25 $OUT/pools.log
 timeout -k 10 300 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_gpu_ingest.py > $OUT/ingest.log 2>&1 || { tail -30 $OUT/ingest.log; exit 1; }
 tail -2 $OUT/ingest.log
 B="timeout -k 10 200 python bench.py --no-cpu-baseline --no-expansion --no-ingest --steps 3 --warmup 1"
@@ -19,6 +19,8 @@ run "c4 spec" $B --workload c4
 run "c4 spec 10k" $B --workload c4 --patterns 10000
 run "c3 spec" $B --workload c3
 run "c3 interp" SDH_SPEC=0 $B --workload c3
+run "c3 regs0" SDH_KPART_REGS=0 $B --workload c3
+run "c3 regs2" SDH_KPART_REGS=2 $B --workload c3
 export TMPDIR=/tmp
 for w in c3 c4; do
 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d $OUT/pmc_$w -o run -- python3 bench.py --no-cpu-baseline --no-expansion --no-ingest --steps 1 --warmup 1 --workload $w > $OUT/pmc_$w.log 2>&1 || { echo "pmc $w failed"; tail -3 $OUT/pmc_$w.log; exit 1; }
