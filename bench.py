@@ -42,14 +42,14 @@ DEFAULTS = {  # workload -> (patterns per GPU, events per step, keys)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=list(DEFAULTS), default="c2",
                     help="c2: BASELINE configs[1] at 10K patterns (headline); c3: configs[2] (count/logical, "
                          "partitioned); c4: configs[3] (fraud-rule sequences, one GPU's pattern-set shard)")
     ap.add_argument("--keys", type=int, default=0, help="partition keys / symbols (default per workload)")
     ap.add_argument("--patterns", type=int, default=0, help="patterns per GPU (default per workload)")
-    ap.add_argument("--batch", type=int, default=0, help="events per step (default per workload)")
+    ap.add_argument("--batch", type=int, default=0, help="events per step (default per workload; C2: 12 steps x 8M = 1.0e8 timed events)")
     ap.add_argument("--partials", type=int, default=128)
     ap.add_argument("--expansion-batch", type=int, default=1 << 16)
     ap.add_argument("--no-expansion", action="store_true")

@@ -60,9 +60,11 @@ typedef struct sdh_config {
   int32_t chunk_events;      /* target events per parallel chunk (0 = automatic)             */
   int32_t flags;             /* SDH_FLAG_*                                                   */
   /* K_gen (general interpreter) pools per query instance (0 = defaults 64 / 128 / 48) and the
-   * partition key capacity (0 = 2^20 keys per partition)                                     */
-  int32_t gen_pool_states;   /* StateEvent objects (<= 64)                                   */
-  int32_t gen_pool_nodes;    /* chained event copies (<= 256)                                */
+   * partition key capacity (0 = 2^20 keys per partition). These are starting sizes: a push that
+   * overflows a pool or list is undone, the pools double (up to 4096 StateEvents / nodes) and the
+   * push is re-run exactly (sdh_stats.pool_regrows).                                         */
+  int32_t gen_pool_states;   /* StateEvent objects (<= 4096)                                 */
+  int32_t gen_pool_nodes;    /* chained event copies (<= 4096)                               */
   int32_t gen_list_cap;      /* entries per pending / newAndEvery list                       */
   int32_t gen_pad;
   int64_t gen_max_keys;      /* distinct partition keys per partition                        */
@@ -131,6 +133,8 @@ typedef struct sdh_stats {
   int64_t ingest_bytes;      /* bytes copied from host batches so far                         */
   int64_t spec_kernels;      /* shape-compiled kernels this engine launches (hiprtc at create; */
                              /* SDH_SPEC=0 off, 1 every shape, default shapes of >= 128 queries) */
+  int64_t pool_regrows;      /* K_gen pool / list growths (each re-lays the arenas and re-runs   */
+                             /* the push that overflowed; the reference's lists are unbounded)   */
 } sdh_stats;
 
 int sdh_engine_create(const void* ir_blob, size_t len, const sdh_config* cfg, sdh_engine** out);

@@ -36,6 +36,10 @@ extern "C" hipError_t sdh_route_partition(const sdh::StreamBatch* B, int attr, i
                                           int32_t* off, int32_t* n_runs_dev, void* temp, size_t temp_bytes,
                                           int32_t* err, int shard_rank, int shard_world, hipStream_t s);
 extern "C" size_t sdh_route_temp_bytes(int64_t n);
+extern "C" hipError_t sdh_gen_remap(const int32_t* lane_q, int group_base, int n_groups, int64_t blocks,
+                                    const sdh::kg::GLayout* oldL, const sdh::kg::GLayout* newL, const int32_t* o32,
+                                    const int64_t* o64, int64_t oB32, int64_t oB64, int32_t* n32, int64_t* n64,
+                                    int64_t nB32, int64_t nB64, hipStream_t s);
 
 extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaunch* L, int n_blocks,
                                        size_t lds, hipStream_t s);
@@ -611,6 +615,9 @@ struct sdh_engine {
   std::vector<int32_t> seq_tail_len;
   int gB32 = 1, gB64 = 1;
   int gHotS = 1, gHotNU = 1;  // K_gen LDS hot-word cache extents (max states / node-mask words)
+  kg::Sizing gsz;                    // K_gen pool sizing (grows on overflow: gen_relayout)
+  std::vector<char> gq_arena;        // [gq] the query runs on K_gen (has an instance arena)
+  int64_t gen_regrows = 0;           // pool growths so far (sdh_stats)
   struct GenSet {
     int partition = -1;              // -1: the unpartitioned K_gen queries
     int group_base = 0, n_groups = 0;
@@ -1370,9 +1377,10 @@ void spec_build(sdh_engine* e) {
 
 void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   kg::Sizing sz;
-  if (e->cfg.gen_pool_states > 0) sz.R = std::min(64, e->cfg.gen_pool_states);
-  if (e->cfg.gen_pool_nodes > 0) sz.N = std::min(256, e->cfg.gen_pool_nodes);
-  if (e->cfg.gen_list_cap > 0) sz.LC = e->cfg.gen_list_cap;
+  if (e->cfg.gen_pool_states > 0) sz.R = std::min(kg::GMAXPOOL, e->cfg.gen_pool_states);
+  if (e->cfg.gen_pool_nodes > 0) sz.N = std::min(kg::GMAXPOOL, e->cfg.gen_pool_nodes);
+  if (e->cfg.gen_list_cap > 0) sz.LC = std::min(1 << 16, e->cfg.gen_list_cap);
+  e->gsz = sz;
   std::vector<int> gidx(e->lp.q.size(), -1);
   std::vector<KPart> kpart(e->lp.q.size());
   const bool use_part = !(e->cfg.flags & SDH_FLAG_FORCE_GEN) && !getenv("SDH_NO_KPART");
@@ -1384,11 +1392,12 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
       gidx[qi] = (int)e->gq.size();
       e->gq.push_back(g);
       if (use_part) kpart[qi] = kpart_shape(e->lp, qi, g);
+      e->gq_arena.push_back(kpart[qi].kind < 0);
       if (kpart[qi].kind >= 0) continue;  // K_part: no K_gen arena
       e->gB32 = std::max(e->gB32, g.lay.n32);
       e->gB64 = std::max(e->gB64, g.lay.n64);
       e->gHotS = std::max(e->gHotS, g.lay.S);
-      e->gHotNU = std::max(e->gHotNU, g.lay.NU);
+      if (!g.lay.big) e->gHotNU = std::max(e->gHotNU, g.lay.NU);
     } catch (const kg::LowerError& ex) {
       throw Error(SDH_E_UNSUPPORTED, fmt("query %d: %s", qi, ex.what()));
     }
@@ -1545,6 +1554,66 @@ void gen_grow(sdh_engine* e, sdh_engine::GenSet& gs, int64_t keys) {
   std::swap(gs.a64.p, n64.p);
   std::swap(gs.a64.n, n64.n);
   gs.key_cap = cap;
+}
+
+
+// K_gen pools and lists at a new sizing: every query's layout is recomputed (make_layout) and each
+// set's arenas are re-laid on the device (gen_remap_kernel; remap = false: zeroed, the caller
+// overwrites them). Pools only grow between pushes, so the indices the arenas hold stay valid.
+void gen_relayout(sdh_engine* e, const kg::Sizing& sz, bool remap) {
+  if (7 + kg::GMAXS + sz.N > GEN_RING_MARGIN) throw Error(SDH_E_CAPACITY, "K_gen node pool beyond the match-record limit");
+  std::vector<kg::GLayout> oldL(e->gq.size()), newL(e->gq.size());
+  int b32 = 1, b64 = 1, hot_nu = 1;
+  for (size_t i = 0; i < e->gq.size(); ++i) {
+    kg::GQuery& g = e->gq[i];
+    oldL[i] = g.lay;
+    kg::make_layout(g.lay, g.lay.S, sz.R, sz.N, sz.LC, g.lay.NA, g.lay.v32 != 0);
+    newL[i] = g.lay;
+    if (!e->gq_arena[i]) continue;
+    b32 = std::max(b32, g.lay.n32);
+    b64 = std::max(b64, g.lay.n64);
+    if (!g.lay.big) hot_nu = std::max(hot_nu, g.lay.NU);
+  }
+  DevBuf<kg::GLayout> dOld, dNew;
+  dOld.ensure(oldL.size());
+  dNew.ensure(newL.size());
+  HIPCHK(hipMemcpy(dOld.p, oldL.data(), oldL.size() * sizeof(kg::GLayout), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dNew.p, newL.data(), newL.size() * sizeof(kg::GLayout), hipMemcpyHostToDevice));
+  for (auto& up : e->gsets) {
+    auto& gs = *up;
+    const int64_t blocks = gs.partition < 0 ? gs.n_groups : gs.key_cap * gs.n_groups;
+    DevBuf<int32_t> n32;
+    DevBuf<int64_t> n64;
+    n32.ensure(std::max<size_t>(1, (size_t)blocks * b32 * 64));
+    n64.ensure(std::max<size_t>(1, (size_t)blocks * b64 * 64));
+    HIPCHK(hipMemsetAsync(n32.p, 0, n32.n * 4, e->stream));
+    HIPCHK(hipMemsetAsync(n64.p, 0, n64.n * 8, e->stream));
+    if (remap)
+      HIPCHK(sdh_gen_remap(e->d_lane_q.p, gs.group_base, gs.n_groups, blocks, dOld.p, dNew.p, gs.a32.p, gs.a64.p,
+                           e->gB32, e->gB64, n32.p, n64.p, b32, b64, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    std::swap(gs.a32.p, n32.p);
+    std::swap(gs.a32.n, n32.n);
+    std::swap(gs.a64.p, n64.p);
+    std::swap(gs.a64.n, n64.n);
+  }
+  e->gB32 = b32;
+  e->gB64 = b64;
+  e->gHotNU = hot_nu;
+  e->gsz = sz;
+  HIPCHK(hipMemcpy(e->d_gq.p, e->gq.data(), e->gq.size() * sizeof(kg::GQuery), hipMemcpyHostToDevice));
+}
+
+// the sizing after a K_gen capacity failure of kinds `capk` (kg::CAP_*): each limit hit doubles
+bool gen_grown_sizing(const sdh_engine* e, int capk, kg::Sizing* out) {
+  kg::Sizing sz = e->gsz;
+  if (capk & kg::CAP_FIXED) return false;
+  if (capk & kg::CAP_STATES) sz.R = std::min(kg::GMAXPOOL, 2 * sz.R);
+  if (capk & kg::CAP_NODES) sz.N = std::min(kg::GMAXPOOL, 2 * sz.N);
+  if (capk & kg::CAP_LIST) sz.LC = std::min(1 << 16, 2 * sz.LC);
+  if (sz.R == e->gsz.R && sz.N == e->gsz.N && sz.LC == e->gsz.LC) return false;
+  *out = sz;
+  return true;
 }
 
 
@@ -1931,7 +2000,9 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   e->d_err.ensure(4);
   e->g_rec_next.ensure(1);
   const bool write = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) == 0;
-  const bool backed = (write || !e->psets.empty()) && gen_backup(e);
+  // arenas are backed up before the pass so that an overflow (match output, K_part tables, K_gen
+  // pools) can be undone and the push re-run exactly at the grown capacity
+  bool backed = gen_backup(e);
   double bytes = 0;
   int32_t tail_len = -1;
   bool any = false;
@@ -1962,11 +2033,20 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
       out_over |= perr[4 * i + 2] != 0;
       part_over |= perr[4 * i] != 0;
     }
-    if ((out_over || part_over) && backed && attempt < 12 && !errs[0] && !errs[1] && !errs[3]) {
+    kg::Sizing grown;
+    const bool pools_over = errs[0] != 0 && gen_grown_sizing(e, errs[0], &grown);
+    if ((out_over || part_over || pools_over) && backed && attempt < 24 && (!errs[0] || pools_over) && !errs[1] &&
+        !errs[3]) {
       // undo the pass (K_gen arenas from the backup; K_part tables are double-buffered and their
       // per-key selectors are swapped only after success) and re-run it with room for every match
-      // record (out_next counts the words every record asked for) and every K_part partial
+      // record (out_next counts the words every record asked for), every K_part partial and the
+      // K_gen pools / lists that overflowed
       gen_restore_backup(e);
+      if (pools_over) {
+        gen_relayout(e, grown, true);
+        ++e->gen_regrows;
+        backed = gen_backup(e);  // the pre-push state in the new layout
+      }
       if (out_over)
         while (e->g_out_cap < (int64_t)used + (int64_t)used / 4 + GEN_RING_MARGIN) e->g_out_cap *= 2;
       for (size_t i = 0; i < nps; ++i)
@@ -1997,8 +2077,10 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   if (errs[3]) throw Error(SDH_E_CAPACITY, "partition key table full");
   if (errs[1]) throw Error(SDH_E_REFERENCE, "the reference engine would throw on this stream "
                                             "(ConcurrentModification / IllegalState / NullPointer)");
-  if (errs[0]) throw Error(SDH_E_CAPACITY, "K_gen instance pool or list capacity exceeded "
-                                           "(raise gen_pool_states / gen_pool_nodes / gen_list_cap)");
+  if (errs[0]) throw Error(SDH_E_CAPACITY, (errs[0] & kg::CAP_FIXED)
+                                               ? "K_gen compiled-in limit exceeded (GC pins or matches per processAndReturn)"
+                                               : "K_gen instance pools could not grow further (4096 StateEvents / nodes per "
+                                                 "instance, or device memory)");
   if (!any) nrec = used = 0;
   *bytes_out += (double)nrec * 32.0;  // one (query, ts, seqs) record per match, as for K_ratchet
   e->stats.matches += (int64_t)nrec;
@@ -2399,23 +2481,24 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
           for (int l = 0; l < e->rg[g].n_lanes; ++l) live += rs[g].n[l];
     }
     e->stats.live_partials = live;
+    e->stats.pool_regrows = e->gen_regrows;
     *out = e->stats;
     return SDH_OK;
   });
 }
 
-// snapshot: [magic][version][n_q][pcap][gB32][gB64][seq][n_streams][prev_ts...] then per query
+// snapshot: [magic][version][n_q][pcap][gB32][gB64][R][N][LC][seq][n_streams][prev_ts...] then per query
 // header + table, ratchet deques, K_gen arenas + key tables, K_seq tails
 constexpr int64_t SNAP_MAGIC = 0x5344485350415254LL;
-constexpr int64_t SNAP_VERSION = 3;
+constexpr int64_t SNAP_VERSION = 4;
 int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
   if (!e || !blob || !len) return SDH_E_INVALID;
   return guard(e, [&]() {
     HIPCHK(hipStreamSynchronize(e->stream));
     const size_t nq = e->lq.size();
     const size_t tbl = (size_t)NF * e->pcap;
-    std::vector<int64_t> w{SNAP_MAGIC, SNAP_VERSION, (int64_t)nq, e->pcap, e->gB32, e->gB64, e->seq,
-                           (int64_t)e->prev_ts.size()};
+    std::vector<int64_t> w{SNAP_MAGIC, SNAP_VERSION, (int64_t)nq, e->pcap, e->gB32, e->gB64,
+                           e->gsz.R, e->gsz.N, e->gsz.LC, e->seq, (int64_t)e->prev_ts.size()};
     w.insert(w.end(), e->prev_ts.begin(), e->prev_ts.end());
     for (size_t q = 0; q < nq; ++q) {
       InstHeader h;
@@ -2514,6 +2597,14 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
     const size_t nq = (size_t)nx();
     if (nq != e->lq.size() || nx() != e->pcap) throw Error(SDH_E_INVALID, "snapshot of a different program");
     const int64_t b32 = nx(), b64 = nx();
+    kg::Sizing sz;
+    sz.R = (int)nx();
+    sz.N = (int)nx();
+    sz.LC = (int)nx();
+    if (sz.R < 1 || sz.R > kg::GMAXPOOL || sz.N < 1 || sz.N > kg::GMAXPOOL || sz.LC < 1 || sz.LC > (1 << 16))
+      throw Error(SDH_E_INVALID, "bad snapshot K_gen pool sizing");
+    // the snapshot's pools may have grown past this engine's: take its sizing (arenas are loaded below)
+    if (sz.R != e->gsz.R || sz.N != e->gsz.N || sz.LC != e->gsz.LC) gen_relayout(e, sz, false);
     if (b32 != e->gB32 || b64 != e->gB64)
       throw Error(SDH_E_INVALID, "snapshot of a different K_gen arena layout (another build or pool sizing)");
     e->seq = nx();

@@ -44,7 +44,8 @@ constexpr int GMAXNA = 8;        // captured attributes per node (per stream)
 constexpr int GMAXSTREAM = 8;    // streams a query may read
 constexpr int GSTACK = 12;       // bytecode evaluation stack
 constexpr int GMAXRET = 64;      // matches one processAndReturn may return
-constexpr int GMAXNU = 4;        // node used-bitmask words (nodes per instance <= 256)
+constexpr int GMAXNU = 4;        // node used-bitmask words the LDS hot cache holds (small pools)
+constexpr int GMAXPOOL = 4096;   // StateEvents / nodes per instance after growth (record <= ring margin)
 // the current event, not yet copied into the node pool: a stream / logical state's slot holds it
 // while that state's filters run, and it is copied only when they pass (fewer pool writes and
 // sweeps; observable behaviour is unchanged, the copy is invisible until a post processor runs)
@@ -61,6 +62,9 @@ enum { R_SINGLE = 0, R_MULTI };
 
 // error codes (per lane, first one wins)
 enum { GE_OK = 0, GE_CAPACITY = 1, GE_REFERENCE = 2 };
+// capacity kinds: the pools and lists grow (the engine re-lays the arenas and re-runs the push);
+// CAP_FIXED limits (GC pins, matches one processAndReturn returns) are compiled in
+enum { CAP_STATES = 1, CAP_NODES = 2, CAP_LIST = 4, CAP_FIXED = 8 };
 
 struct GInsn {
   int8_t op, lt, rt, res;
@@ -82,6 +86,9 @@ struct GLayout {
   int32_t o_flags, o_pn, o_nn, o_plist, o_nlist, o_seslot, o_ndnext, o_ndnull, o_init, n32;
   int32_t o_seused, o_ndused, o_sets, o_ndseq, o_ndts, o_ndval, n64;
   int32_t v32;  // node attribute words in the 32-bit arena (every captured type is 4 bytes or less)
+  // pools beyond the LDS hot cache (R > 64 StateEvents or N > 64 * GMAXNU nodes): the used-bitmasks
+  // stay in the arena (SU / NU words) and mark/sweep marks into o_mark (SU + NU words, 64-bit arena)
+  int32_t SU, big, o_mark, pad;
 };
 
 // K_seq compare atoms: a state's filters as a conjunction of typed compares whose operands are a
@@ -430,6 +437,7 @@ struct Ctx {
   const int64_t* ev_val;  // [GMAXNA] the event's captured words (wave-uniform: LDS on the device)
   uint32_t ev_null;
   int32_t err;
+  int32_t capk;  // GE_CAPACITY: CAP_* bits of the limits that were hit
   // The dynamically indexed arrays (event words, pins, return list) live outside Ctx, behind
   // pointers: an array indexed by a run-time value inside the struct would keep the whole Ctx in
   // scratch memory on the device (no SROA), turning every field read into a scratch load.
@@ -482,16 +490,19 @@ struct Ctx {
     if (lay.v32) i32(o) = (int32_t)v;
     else i64(o) = v;
   }
-  KG_FN int64_t& se_used() const { return h64[0]; }
-  KG_FN int64_t& nd_used(int w) const { return h64[(int64_t)(1 + w) * hstride]; }
+  // used-bitmask words: the LDS hot cache for small pools, the arena itself for big ones (lay.big is
+  // the template's, so the choice is wave-uniform)
+  KG_FN int64_t& se_used(int w) const { return lay.big ? i64(lay.o_seused + w) : h64[0]; }
+  KG_FN int64_t& nd_used(int w) const { return lay.big ? i64(lay.o_ndused + w) : h64[(int64_t)(1 + w) * hstride]; }
   KG_FN void load_hot() {
     for (int i = 0; i < lay.S; ++i) {
       flags(i) = i32(lay.o_flags + i);
       pn(i) = i32(lay.o_pn + i);
       nn(i) = i32(lay.o_nn + i);
     }
-    se_used() = i64(lay.o_seused);
-    for (int w = 0; w < lay.NU; ++w) nd_used(w) = i64(lay.o_ndused + w);
+    if (lay.big) return;
+    h64[0] = i64(lay.o_seused);
+    for (int w = 0; w < lay.NU; ++w) h64[(int64_t)(1 + w) * hstride] = i64(lay.o_ndused + w);
   }
   KG_FN void store_hot() const {
     for (int i = 0; i < lay.S; ++i) {
@@ -499,44 +510,85 @@ struct Ctx {
       i32(lay.o_pn + i) = pn(i);
       i32(lay.o_nn + i) = nn(i);
     }
-    i64(lay.o_seused) = se_used();
-    for (int w = 0; w < lay.NU; ++w) i64(lay.o_ndused + w) = nd_used(w);
+    if (lay.big) return;
+    i64(lay.o_seused) = h64[0];
+    for (int w = 0; w < lay.NU; ++w) i64(lay.o_ndused + w) = h64[(int64_t)(1 + w) * hstride];
   }
 
   KG_FN void fail(int e) {
     if (err == GE_OK) err = e;
   }
+  KG_FN void cap_fail(int kind) {  // GE_CAPACITY, and which limit: the host grows it and re-runs
+    capk |= kind;
+    fail(GE_CAPACITY);
+  }
 
   // ---- allocation with mark/sweep reclamation ----
-  KG_FN void mark_chain(int n, uint64_t* nm) const {
-    while (n >= 0 && n < lay.N && !((nm[n >> 6] >> (n & 63)) & 1ull)) {
-      nm[n >> 6] |= 1ull << (n & 63);
+  // mark bits: in registers for small pools, in the arena's o_mark words for big ones
+  struct RegMarks {
+    uint64_t s = 0, n[GMAXNU] = {0, 0, 0, 0};
+    KG_FN bool se(int i) const { return (s >> i) & 1ull; }
+    KG_FN void set_se(int i) { s |= 1ull << i; }
+    KG_FN bool nd(int i) const { return (n[i >> 6] >> (i & 63)) & 1ull; }
+    KG_FN void set_nd(int i) { n[i >> 6] |= 1ull << (i & 63); }
+  };
+  struct ArenaMarks {
+    const Ctx* c;
+    KG_FN int64_t& w(int k) const { return c->i64(c->lay.o_mark + k); }
+    KG_FN bool se(int i) const { return ((uint64_t)w(i >> 6) >> (i & 63)) & 1ull; }
+    KG_FN void set_se(int i) const { w(i >> 6) = (int64_t)((uint64_t)w(i >> 6) | (1ull << (i & 63))); }
+    KG_FN bool nd(int i) const { return ((uint64_t)w(c->lay.SU + (i >> 6)) >> (i & 63)) & 1ull; }
+    KG_FN void set_nd(int i) const {
+      int64_t& x = w(c->lay.SU + (i >> 6));
+      x = (int64_t)((uint64_t)x | (1ull << (i & 63)));
+    }
+  };
+  template <class M>
+  KG_FN void mark_chain(int n, M& m) const {
+    while (n >= 0 && n < lay.N && !m.nd(n)) {
+      m.set_nd(n);
       n = nd_next(n);
     }
   }
-  KG_FN void mark_se(int se, uint64_t& sm, uint64_t* nm) const {
-    if (se < 0 || ((sm >> se) & 1ull)) return;
-    sm |= 1ull << se;
-    for (int i = 0; i < nS(); ++i) mark_chain(slot(se, i), nm);
+  template <class M>
+  KG_FN void mark_se(int se, M& m) const {
+    if (se < 0 || m.se(se)) return;
+    m.set_se(se);
+    for (int i = 0; i < nS(); ++i) mark_chain(slot(se, i), m);
+  }
+  template <class M>
+  KG_FN void mark_roots(M& m) const {
+    for (int i = 0; i < nS(); ++i) {
+      for (int k = 0; k < pn(i); ++k) mark_se(pl(i, k), m);
+      for (int k = 0; k < nn(i); ++k) mark_se(nl(i, k), m);
+    }
+    for (int k = 0; k < npin && k < 4; ++k) mark_se(pins[(int64_t)k * hstride], m);
+    for (int k = 0; k < n_ret; ++k) mark_se(ret[k], m);
   }
   KG_FN void gc() {
     KG_PHASE(1);
-    uint64_t sm = 0, nm[4] = {0, 0, 0, 0};
-    for (int i = 0; i < nS(); ++i) {
-      for (int k = 0; k < pn(i); ++k) mark_se(pl(i, k), sm, nm);
-      for (int k = 0; k < nn(i); ++k) mark_se(nl(i, k), sm, nm);
+    if (lay.big) {
+      ArenaMarks m{this};
+      for (int k = 0; k < lay.SU + lay.NU; ++k) m.w(k) = 0;
+      mark_roots(m);
+      for (int k = 0; k < lay.SU; ++k) se_used(k) = m.w(k);
+      for (int k = 0; k < lay.NU; ++k) nd_used(k) = m.w(lay.SU + k);
+    } else {
+      RegMarks m;
+      mark_roots(m);
+      se_used(0) = (int64_t)m.s;
+      for (int w = 0; w < lay.NU; ++w) nd_used(w) = (int64_t)m.n[w];
     }
-    for (int k = 0; k < npin && k < 4; ++k) mark_se(pins[(int64_t)k * hstride], sm, nm);
-    for (int k = 0; k < n_ret; ++k) mark_se(ret[k], sm, nm);
-    se_used() = (int64_t)sm;
-    for (int w = 0; w < lay.NU; ++w) nd_used(w) = (int64_t)nm[w];
     KG_PHASE(0);
   }
   KG_FN int find_free_se() const {
-    const uint64_t u = (uint64_t)se_used();
-    const uint64_t fr = ~u & (lay.R >= 64 ? ~0ull : ((1ull << lay.R) - 1));
-    if (!fr) return -1;
-    return __builtin_ctzll(fr);
+    for (int w = 0; w < lay.SU; ++w) {
+      const int lim = lay.R - w * 64;
+      const uint64_t u = (uint64_t)se_used(w);
+      const uint64_t fr = ~u & (lim >= 64 ? ~0ull : ((1ull << lim) - 1));
+      if (fr) return w * 64 + __builtin_ctzll(fr);
+    }
+    return -1;
   }
   KG_FN int find_free_nd() const {
     for (int w = 0; w < lay.NU; ++w) {
@@ -552,9 +604,9 @@ struct Ctx {
     if (s < 0) {
       gc();
       s = find_free_se();
-      if (s < 0) { fail(GE_CAPACITY); return -1; }
+      if (s < 0) { cap_fail(CAP_STATES); return -1; }
     }
-    se_used() = (int64_t)((uint64_t)se_used() | (1ull << s));
+    se_used(s >> 6) = (int64_t)((uint64_t)se_used(s >> 6) | (1ull << (s & 63)));
     if (blank) {
       for (int i = 0; i < nS(); ++i) slot(s, i) = -1;
       se_ts(s) = -1;
@@ -563,7 +615,7 @@ struct Ctx {
   }
   KG_FN void pin(int se) {
     if (npin < 4) pins[(int64_t)npin * hstride] = se;
-    else fail(GE_CAPACITY);  // an unrecorded root could be swept: refuse rather than risk it
+    else cap_fail(CAP_FIXED);  // an unrecorded root could be swept: refuse rather than risk it
     ++npin;
   }
   KG_FN void unpin() { --npin; }
@@ -584,7 +636,7 @@ struct Ctx {
       gc();
       unpin();
       n = find_free_nd();
-      if (n < 0) { fail(GE_CAPACITY); return -1; }
+      if (n < 0) { cap_fail(CAP_NODES); return -1; }
     }
     nd_used(n >> 6) = (int64_t)((uint64_t)nd_used(n >> 6) | (1ull << (n & 63)));
     nd_seq(n) = seq;
@@ -598,14 +650,14 @@ struct Ctx {
 
   // ---- lists ----
   KG_FN void nae_push(int i, int se) {
-    if (nn(i) >= lay.LC) { fail(GE_CAPACITY); return; }
+    if (nn(i) >= lay.LC) { cap_fail(CAP_LIST); return; }
     nl(i, nn(i)) = se;
     nn(i) += 1;
   }
   KG_FN void promote(int i) {  // pending.addAll(newAndEvery); newAndEvery.clear()
     if ((flags(i) & FL_ITER) && nn(i) > 0) { fail(GE_REFERENCE); return; }  // Java CME
     const int n = nn(i);
-    if (pn(i) + n > lay.LC) { fail(GE_CAPACITY); return; }
+    if (pn(i) + n > lay.LC) { cap_fail(CAP_LIST); return; }
     for (int k = 0; k < n; ++k) pl(i, pn(i) + k) = nl(i, k);
     pn(i) += n;
     nn(i) = 0;
@@ -864,7 +916,7 @@ struct Ctx {
     return false;
   }
   KG_FN void push_ret(int se) {
-    if (n_ret >= GMAXRET) { fail(GE_CAPACITY); return; }
+    if (n_ret >= GMAXRET) { cap_fail(CAP_FIXED); return; }
     ret[n_ret++] = se;
   }
 
@@ -978,6 +1030,9 @@ struct Ctx {
 // ------------------------------------------------------------------------------------------
 inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA, bool v32 = false) {
   L.S = S; L.R = R; L.N = N; L.LC = LC; L.NA = NA; L.NU = (N + 63) / 64;
+  L.SU = (R + 63) / 64;
+  L.big = (L.SU > 1 || L.NU > GMAXNU) ? 1 : 0;
+  L.pad = 0;
   L.v32 = v32 ? 1 : 0;
   int o = 0;
   L.o_flags = o; o += S;
@@ -992,8 +1047,9 @@ inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA, bool v3
   if (v32) { L.o_ndval = o; o += N * NA; }
   L.n32 = o;
   o = 0;
-  L.o_seused = o; o += 1;
+  L.o_seused = o; o += L.SU;
   L.o_ndused = o; o += L.NU;
+  L.o_mark = o; o += L.big ? L.SU + L.NU : 0;
   L.o_sets = o; o += R;
   L.o_ndseq = o; o += N;
   L.o_ndts = o; o += N;

@@ -86,6 +86,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   c.pins = c.h32 + (int64_t)3 * L.hot_s * 64;  // [4][lane] after the hot words
   c.ret = ret;
   c.err = kg::GE_OK;
+  c.capk = 0;
   c.npin = 0;
   c.n_ret = 0;
   c.stream = L.b.stream;
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   o.close();
   c.store_hot();
   if (nrec) atomicAdd(L.rec_count, nrec);
-  if (c.err == kg::GE_CAPACITY) atomicOr(&L.err[0], 1);
+  if (c.err == kg::GE_CAPACITY) atomicOr(&L.err[0], c.capk);  // which limits (kg::CAP_*)
   if (c.err == kg::GE_REFERENCE) atomicOr(&L.err[1], 1);
   if (o.over) atomicOr(&L.err[2], 1);
 }
@@ -185,6 +186,54 @@ __global__ void seq_tail_kernel(StreamBatch b, int64_t* tail, int32_t tail_len, 
       }
     }
   }
+}
+
+// ---- pool growth: one instance arena re-laid from layout `a` to layout `b` (kgen.h make_layout) ----
+// Pools and lists only grow, so every index an arena holds (StateEvent, node, list entry) stays
+// valid: each field is copied entry by entry to its new offset and the new entries stay zero (free
+// pool bits, empty list slots). One thread per (block, lane); blocks are [key][group] (partitioned)
+// or [group].
+__global__ void gen_remap_kernel(const int32_t* __restrict__ lane_q, int group_base, int n_groups, int64_t blocks,
+                                 const kg::GLayout* __restrict__ oldL, const kg::GLayout* __restrict__ newL,
+                                 const int32_t* __restrict__ o32, const int64_t* __restrict__ o64, int64_t oB32,
+                                 int64_t oB64, int32_t* __restrict__ n32, int64_t* __restrict__ n64, int64_t nB32,
+                                 int64_t nB64) {
+  const int64_t block = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (block >= blocks) return;
+  const int g = (int)(block % n_groups);
+  const int qi = lane_q[(int64_t)(group_base + g) * 64 + lane];
+  if (qi < 0) return;
+  const kg::GLayout a = oldL[qi], b = newL[qi];
+  const int32_t* s32 = o32 + block * oB32 * 64 + lane;
+  const int64_t* s64 = o64 + block * oB64 * 64 + lane;
+  int32_t* d32 = n32 + block * nB32 * 64 + lane;
+  int64_t* d64 = n64 + block * nB64 * 64 + lane;
+  auto c32 = [&](int from, int to, int n) {
+    for (int k = 0; k < n; ++k) d32[(int64_t)(to + k) * 64] = s32[(int64_t)(from + k) * 64];
+  };
+  auto c64 = [&](int from, int to, int n) {
+    for (int k = 0; k < n; ++k) d64[(int64_t)(to + k) * 64] = s64[(int64_t)(from + k) * 64];
+  };
+  const int S = a.S;
+  c32(a.o_flags, b.o_flags, S);
+  c32(a.o_pn, b.o_pn, S);
+  c32(a.o_nn, b.o_nn, S);
+  for (int i = 0; i < S; ++i) {
+    c32(a.o_plist + i * a.LC, b.o_plist + i * b.LC, a.LC);
+    c32(a.o_nlist + i * a.LC, b.o_nlist + i * b.LC, a.LC);
+  }
+  c32(a.o_seslot, b.o_seslot, a.R * S);  // [StateEvent][state]: same stride S
+  c32(a.o_ndnext, b.o_ndnext, a.N);
+  c32(a.o_ndnull, b.o_ndnull, a.N);
+  c32(a.o_init, b.o_init, 1);
+  c64(a.o_seused, b.o_seused, a.SU);
+  c64(a.o_ndused, b.o_ndused, a.NU);
+  c64(a.o_sets, b.o_sets, a.R);
+  c64(a.o_ndseq, b.o_ndseq, a.N);
+  c64(a.o_ndts, b.o_ndts, a.N);
+  if (a.v32) c32(a.o_ndval, b.o_ndval, a.N * a.NA);  // [node][attr]: same stride NA
+  else c64(a.o_ndval, b.o_ndval, a.N * a.NA);
 }
 
 // ---- partition routing ----
@@ -314,6 +363,17 @@ extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, hipStream_t s) {
 extern "C" hipError_t sdh_seq_tail(const sdh::StreamBatch* b, int64_t* tail, int32_t tail_len, int32_t new_tail_len,
                                    hipStream_t s) {
   hipLaunchKernelGGL(sdh::seq_tail_kernel, dim3(1), dim3(64), 0, s, *b, tail, tail_len, new_tail_len);
+  return hipGetLastError();
+}
+
+// re-lay `blocks` instance blocks of one K_gen set from the old to the new pool sizing (zeroed `n32`/`n64`)
+extern "C" hipError_t sdh_gen_remap(const int32_t* lane_q, int group_base, int n_groups, int64_t blocks,
+                                    const sdh::kg::GLayout* oldL, const sdh::kg::GLayout* newL, const int32_t* o32,
+                                    const int64_t* o64, int64_t oB32, int64_t oB64, int32_t* n32, int64_t* n64,
+                                    int64_t nB32, int64_t nB64, hipStream_t s) {
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::gen_remap_kernel, dim3((unsigned)blocks), dim3(64), 0, s, lane_q, group_base, n_groups, blocks,
+                     oldL, newL, o32, o64, oB32, oB64, n32, n64, nB32, nB64);
   return hipGetLastError();
 }
 

@@ -52,7 +52,8 @@ class SdhStats(ctypes.Structure):
                 ("last_kernel_ms", ctypes.c_double), ("last_kernel_bytes", ctypes.c_double),
                 ("last_gen_items", ctypes.c_int64), ("last_seq_items", ctypes.c_int64),
                 ("last_part_items", ctypes.c_int64), ("last_ingest_ms", ctypes.c_double),
-                ("ingest_bytes", ctypes.c_int64), ("spec_kernels", ctypes.c_int64)]
+                ("ingest_bytes", ctypes.c_int64), ("spec_kernels", ctypes.c_int64),
+                ("pool_regrows", ctypes.c_int64)]
 
 
 EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engine_poll", "sdh_engine_poll_device",

@@ -130,7 +130,8 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
   };
   c.receive(emit);
   c.store_hot();
-  if (c.err == GE_CAPACITY) throw std::runtime_error("K_gen instance capacity exceeded");
+  if (c.err == GE_CAPACITY)
+    throw std::runtime_error("K_gen instance capacity exceeded (kinds " + std::to_string(c.capk) + ")");
   if (c.err == GE_REFERENCE) throw std::runtime_error("reference engine would throw here");
 }
 

@@ -93,10 +93,61 @@ def test_fuzz_apps_on_gpu(seed, batch):
     r = _fuzz(seed, 0, batch)
     if r is None:
         pytest.skip("app rejected by the planner or the reference would throw")
-    if r == "capacity":
-        pytest.skip("instance pools exceeded (loud SDH_E_CAPACITY)")
+    assert r != "capacity", "K_gen pools grow on overflow: no capacity error is expected"
     o, g = r
     assert g.matches == o.matches
+
+
+GROWTH_SEEDS = [7, 11, 12, 14, 30]  # streams that overflow the default pools (round-1 skips)
+
+
+@pytest.mark.parametrize("batch", [False, True], ids=["per_event", "batched"])
+@pytest.mark.parametrize("seed", GROWTH_SEEDS)
+def test_pool_growth_reruns_exactly(seed, batch):
+    """Pools that start tiny (2 StateEvents, 4 nodes, lists of 2) overflow on almost every push:
+    each overflow undoes the push, doubles the limit that was hit, re-lays every arena on the device
+    (gen_remap_kernel) and re-runs the push. The matches stay the oracle's."""
+    src = random_app(seed, partition=seed % 3 == 0)
+    o = App(src)
+    g = hip_app(src, flags=SDH_FLAG_FORCE_GEN, gen_pool_states=2, gen_pool_nodes=4, gen_list_cap=2)
+    ev = random_events(seed)
+    step = 40 if batch else 1
+    i = 0
+    while i < len(ev):
+        j = i + 1
+        while batch and j < len(ev) and ev[j][0] == ev[i][0] and j - i < step:
+            j += 1
+        rows = [r for _, r, _ in ev[i:j]]
+        ts = [t for _, _, t in ev[i:j]]
+        o.send(ev[i][0], rows, ts)
+        g.send(ev[i][0], rows, ts)
+        i = j
+    assert g.engine.stats().pool_regrows > 0
+    assert g.matches == o.matches
+
+
+def test_pool_growth_snapshot_restores_into_default_engine():
+    """A snapshot taken after the pools grew carries their sizing: a fresh engine with the default
+    pools restores it (re-laying its arenas to the snapshot's sizing) and continues exactly."""
+    seed = 11
+    src = random_app(seed, partition=seed % 3 == 0)
+    ev = random_events(seed)
+    half = len(ev) // 2
+    o = App(src)
+    a = hip_app(src, flags=SDH_FLAG_FORCE_GEN, gen_pool_states=2, gen_pool_nodes=4, gen_list_cap=2)
+    for stream, row, t in ev[:half]:
+        o.send(stream, [row], [t])
+        a.send(stream, [row], [t])
+    assert a.engine.stats().pool_regrows > 0
+    a.engine.poll()
+    snap = a.engine.snapshot()
+    b = hip_app(src, flags=SDH_FLAG_FORCE_GEN)
+    b.engine.restore(snap)
+    o.matches.clear()
+    for stream, row, t in ev[half:]:
+        o.send(stream, [row], [t])
+        b.send(stream, [row], [t])
+    assert b.matches == o.matches
 
 
 def test_partitioned_many_keys_batched():
