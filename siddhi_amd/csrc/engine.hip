@@ -692,6 +692,7 @@ struct sdh_engine {
   DevBuf<uint64_t> d_tsmax, d_tsmin;
   DevBuf<uint8_t> d_tshas;
   int rSC = 256;                     // global spill ring entries per lane (power of two)
+  int64_t rsmax = RSMAX;             // persisted deque entries per lane (grows with rSC)
   DevBuf<uint4> d_rspillA;
   DevBuf<int64_t> d_rlts;
   DevBuf<uint32_t> d_rspillB;
@@ -1033,11 +1034,29 @@ void ratchet_build(sdh_engine* e, std::vector<std::pair<RatchetPlan, int>>& plan
   for (int b = 0; b < 2; ++b) {
     e->d_rst[b].ensure(ng);
     HIPCHK(hipMemset(e->d_rst[b].p, 0, ng * sizeof(RatchetState)));
-    e->d_rts[b].ensure(ng * RSMAX * WAVE);
-    e->d_rsq[b].ensure(ng * RSMAX * WAVE);
-    e->d_rky[b].ensure(ng * RSMAX * WAVE);
+    e->d_rts[b].ensure(ng * e->rsmax * WAVE);
+    e->d_rsq[b].ensure(ng * e->rsmax * WAVE);
+    e->d_rky[b].ensure(ng * e->rsmax * WAVE);
   }
   e->d_blk_next.ensure(4);
+}
+
+// persisted deques with room for `want` entries per lane: [g][rsmax][64] re-strided (both buffers)
+void ratchet_grow_rsmax(sdh_engine* e, int64_t want) {
+  if (want <= e->rsmax) return;
+  int64_t cap = e->rsmax;
+  while (cap < want) cap *= 2;
+  const size_t ng = e->rg.size(), ob = (size_t)e->rsmax * WAVE * 8, nb = (size_t)cap * WAVE * 8;
+  for (int b = 0; b < 2; ++b)
+    for (DevBuf<int64_t>* buf : {&e->d_rts[b], &e->d_rsq[b], &e->d_rky[b]}) {
+      DevBuf<int64_t> nw;
+      nw.ensure(ng * cap * WAVE);
+      HIPCHK(hipMemcpy2DAsync(nw.p, nb, buf->p, ob, ob, ng, hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(hipStreamSynchronize(e->stream));
+      std::swap(buf->p, nw.p);
+      std::swap(buf->n, nw.n);
+    }
+  e->rsmax = cap;
 }
 
 int64_t ratchet_count_matches(sdh_engine* e) {
@@ -1069,7 +1088,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
   }
   e->d_rtotal.ensure(1);
   (void)t01;
-  for (int attempt = 0; attempt < 8; ++attempt) {
+  for (int attempt = 0; attempt < 40; ++attempt) {
     // out-of-order timestamps seen on this stream, or timestamps so extreme that `ts0 + within`
     // could wrap: exact per-entry expiry scan, no chunking
     const int64_t lim = (int64_t)1 << 61;
@@ -1155,6 +1174,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.tsum_has = e->d_tshas.p;
     L.n_tiles = n_tiles;
     L.b = B;
+    L.rsmax = e->rsmax;
     for (int b = 0; b < 2; ++b) {
       L.st[b] = e->d_rst[b].p;
       L.ent_ts[b] = e->d_rts[b].p;
@@ -1203,9 +1223,12 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       continue;
     }
     if (errs[0]) {
-      if (e->rML + 2 * e->rSC > RSMAX)
+      // exact re-run with a larger spill ring (and persisted deques to hold it): the reference's
+      // pending list is unbounded (StreamPreStateProcessor.java:298)
+      if (e->rSC >= (1 << 24))
         throw Error(SDH_E_CAPACITY, fmt("more than %d pending partials in one pattern", e->rML + e->rSC));
-      e->rSC *= 2;  // exact re-run with a larger spill ring
+      e->rSC *= 2;
+      ratchet_grow_rsmax(e, e->rML + e->rSC);
       continue;
     }
     if (errs[2]) {
@@ -2516,8 +2539,8 @@ int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
       const int b = e->rcur[g];
       RatchetState rs;
       HIPCHK(hipMemcpy(&rs, e->d_rst[b].p + g, sizeof rs, hipMemcpyDeviceToHost));
-      std::vector<int64_t> t(RSMAX * WAVE), sq(RSMAX * WAVE), ky(RSMAX * WAVE);
-      const size_t o = g * RSMAX * WAVE;
+      std::vector<int64_t> t(e->rsmax * WAVE), sq(e->rsmax * WAVE), ky(e->rsmax * WAVE);
+      const size_t o = g * e->rsmax * WAVE;
       HIPCHK(hipMemcpy(t.data(), e->d_rts[b].p + o, t.size() * 8, hipMemcpyDeviceToHost));
       HIPCHK(hipMemcpy(sq.data(), e->d_rsq[b].p + o, sq.size() * 8, hipMemcpyDeviceToHost));
       HIPCHK(hipMemcpy(ky.data(), e->d_rky[b].p + o, ky.size() * 8, hipMemcpyDeviceToHost));
@@ -2621,13 +2644,28 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
     }
     const size_t ng = (size_t)nx();
     if (ng != e->rg.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
+    // deques in snapshot order; the persisted capacity grows to the longest one first
+    std::vector<size_t> at(ng);
+    int64_t longest = 0;
     for (size_t g = 0; g < ng; ++g) {
-      const int b = e->rcur[g];
-      RatchetState rs{};
-      std::vector<int64_t> t(RSMAX * WAVE, 0), sq(RSMAX * WAVE, 0), ky(RSMAX * WAVE, 0);
+      at[g] = i;
       for (int l = 0; l < WAVE; ++l) {
         const int64_t nl = nx();
-        if (nl < 0 || nl > RSMAX) throw Error(SDH_E_INVALID, "bad snapshot deque length");
+        if (nl < 0 || nl > ((int64_t)1 << 26) || i + 3 * (size_t)nl > nw)
+          throw Error(SDH_E_INVALID, "bad snapshot deque length");
+        longest = std::max(longest, nl);
+        i += 3 * (size_t)nl;
+      }
+    }
+    ratchet_grow_rsmax(e, longest);
+    const size_t i_end = i;
+    for (size_t g = 0; g < ng; ++g) {
+      i = at[g];
+      const int b = e->rcur[g];
+      RatchetState rs{};
+      std::vector<int64_t> t(e->rsmax * WAVE, 0), sq(e->rsmax * WAVE, 0), ky(e->rsmax * WAVE, 0);
+      for (int l = 0; l < WAVE; ++l) {
+        const int64_t nl = nx();
         rs.n[l] = (int32_t)nl;
         for (int i = 0; i < nl; ++i) {
           t[i * WAVE + l] = nx();
@@ -2635,12 +2673,13 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
           ky[i * WAVE + l] = nx();
         }
       }
-      const size_t o = g * RSMAX * WAVE;
+      const size_t o = g * e->rsmax * WAVE;
       HIPCHK(hipMemcpy(e->d_rst[b].p + g, &rs, sizeof rs, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(e->d_rts[b].p + o, t.data(), t.size() * 8, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(e->d_rsq[b].p + o, sq.data(), sq.size() * 8, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(e->d_rky[b].p + o, ky.data(), ky.size() * 8, hipMemcpyHostToDevice));
     }
+    i = i_end;
     if ((size_t)nx() != e->gsets.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
     auto get_dev = [&](void* dptr, size_t bytes) {
       const size_t nw8 = (bytes + 7) / 8;

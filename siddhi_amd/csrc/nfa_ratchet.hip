@@ -550,7 +550,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
 
   bool overflow = false, unordered = false, mover = false, aged = false;
   // persisted deques of the group (pending partials at the start of the batch), oldest first
-  const size_t gb = (size_t)W.g * RSMAX * WAVE;
+  const size_t gb = (size_t)W.g * L.rsmax * WAVE;
   const int n_in = pick(L.st, W.inb)[W.g].n[lane];
   const int64_t* __restrict__ i_ts = pick(L.ent_ts, W.inb);
   const int64_t* __restrict__ i_sq = pick(L.ent_seq, W.inb);

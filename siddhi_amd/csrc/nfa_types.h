@@ -135,7 +135,8 @@ struct ChainLaunch {
 // monotone, so each event costs O(1) amortised: expire from the bottom, match from the top, push.
 // ------------------------------------------------------------------------------------------
 constexpr int RMAXF0 = 4;     // f0 atoms (event-only, per-lane constant operand)
-constexpr int RSMAX = 512;    // persisted deque capacity per lane (>= LDS ring + spill ring)
+constexpr int RSMAX = 512;    // initial persisted deque capacity per lane (>= LDS ring + spill ring;
+                              // the engine doubles it with the spill ring: RatchetLaunch::rsmax)
 
 enum KeyKind { KK_F32 = 0, KK_I32, KK_F64, KK_I64 };
 
@@ -169,7 +170,7 @@ struct RatchetItem {
   int64_t c0, c1;     // events this item emits for
 };
 
-// persisted per-group deque state: n[64] + entries [RSMAX][64] x {ts0, seq, key}
+// persisted per-group deque state: n[64] + entries [rsmax][64] x {ts0, seq, key}
 struct RatchetState {
   int32_t n[64];
   int32_t pad[64];
@@ -182,9 +183,10 @@ struct RatchetLaunch {
   int32_t full_expiry;          // timestamps seen out of order: scan the whole deque for expiry
   StreamBatch b;
   RatchetState* st[2];          // [g]
-  int64_t* ent_ts[2];           // [g][RSMAX][64] ts0
-  int64_t* ent_seq[2];          // [g][RSMAX][64] e1 sequence number
-  int64_t* ent_key[2];          // [g][RSMAX][64] key (32-bit kinds in the low word)
+  int64_t* ent_ts[2];           // [g][rsmax][64] ts0
+  int64_t* ent_seq[2];          // [g][rsmax][64] e1 sequence number
+  int64_t* ent_key[2];          // [g][rsmax][64] key (32-bit kinds in the low word)
+  int64_t rsmax;                // persisted entries per lane (>= ML + SC)
   const uint64_t* tsum_max;     // [slot][n_tiles] max / min key of the valid x of each aligned
   const uint64_t* tsum_min;     //   64-event tile (warm-up skips tiles that cannot hold a survivor)
   const uint8_t* tsum_has;      //   tile has a valid x

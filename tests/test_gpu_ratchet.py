@@ -121,23 +121,35 @@ def test_two_column_start_filter_and_batches():
         assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2)
 
 
-def test_deque_growth_and_overflow_is_loud():
-    from siddhi_amd.engine import EngineError
-    src = "define stream S (v int); @info(name='q') from every e1=S -> e2=S[v > e1.v] select e1.v as a insert into O;"
-    o = App(src)
-    g = hip_app(src)
-    # strictly decreasing values pile up 100 pending partials (LDS ring of 16 + global spill) ...
-    ts = np.arange(101, dtype=np.int64)
-    v = np.concatenate([np.arange(100, 0, -1), [1000]]).astype(np.int32)
-    o.engine.send(0, ts, v.astype(np.int64)[:, None], None)
-    g.engine.push_columns(0, ts, [v])
-    got = g.engine.take_matches(lambda q: 2)
-    assert got == o.engine.take_matches(lambda q: 2) and len(got) == 100
-    # ... and more than the ring + spill capacity (272) is a loud SDH_E_CAPACITY, never a wrong answer
-    ts2 = np.arange(101, 401, dtype=np.int64)
-    with pytest.raises(EngineError) as ei:
-        g.engine.push_columns(0, ts2, [np.arange(300, 0, -1).astype(np.int32)])
-    assert ei.value.code == -4
+def test_deque_growth_to_10k_partials():
+    """The reference's pending list is unbounded (StreamPreStateProcessor.java:298). A strictly
+    decreasing run piles up every partial (no event matches any earlier one); the spill ring and the
+    persisted deques double and the push re-runs exactly until 10K+ partials per pattern fit. The
+    closing high value then matches all of them. Also chunked (reverse-scan warm-up over the pile)
+    and through snapshot/restore into a fresh engine."""
+    src = ("define stream S (v int); @info(name='q') from every e1=S -> e2=S[v > e1.v] select e1.v as a insert into O; "
+           "@info(name='r') from every e1=S[v > 5000] -> e2=S[v > e1.v] select e1.v as a insert into O;")
+    n = 12000
+    ts = np.arange(n + 1, dtype=np.int64)
+    v = np.concatenate([np.arange(n, 0, -1), [10 * n]]).astype(np.int32)
+    for chunk in (0, 1024):
+        o = App(src)
+        g = hip_app(src, chunk_events=chunk)
+        o.engine.send(0, ts[:n], v[:n].astype(np.int64)[:, None], None)
+        g.engine.push_columns(0, ts[:n], [v[:n]])
+        assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2) == []
+        assert g.engine.stats().live_partials == n + (n - 5000)
+        g.engine.poll()
+        snap = g.engine.snapshot()
+        b = hip_app(src, chunk_events=chunk)
+        b.engine.restore(snap)
+        o.engine.send(0, ts[n:], v[n:].astype(np.int64)[:, None], None)
+        want = o.engine.take_matches(lambda q: 2)
+        g.engine.push_columns(0, ts[n:], [v[n:]])
+        b.engine.push_columns(0, ts[n:], [v[n:]])
+        assert len(want) == n + (n - 5000)
+        assert g.engine.take_matches(lambda q: 2) == want
+        assert b.engine.take_matches(lambda q: 2) == want
 
 
 def test_ratchet_unordered_timestamps_exact():
