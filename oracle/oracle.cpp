@@ -39,7 +39,7 @@ enum { T_INT, T_LONG, T_FLOAT, T_DOUBLE, T_BOOL, T_STRING };
 enum { OP_CONST = 1, OP_ATTR, OP_IS_NULL, OP_STREAM_IS_NULL, OP_CMP, OP_AND, OP_OR, OP_NOT, OP_ARITH };
 enum { CMP_EQ, CMP_NE, CMP_GT, CMP_GE, CMP_LT, CMP_LE };
 enum { AR_ADD, AR_SUB, AR_MUL, AR_DIV, AR_MOD };
-enum { K_STREAM, K_COUNT, K_LOGICAL };
+enum { K_STREAM, K_COUNT, K_LOGICAL, K_ABSENT };
 enum { L_AND, L_OR };
 enum { Q_PATTERN, Q_SEQUENCE };
 enum { R_SINGLE, R_MULTI };
@@ -54,6 +54,7 @@ using Code = std::vector<Insn>;
 struct StateDef {
   int kind, stream, is_start, min, max, ltype, partner, next_pre, next_every, within_every,
       callback, this_last, has_selector;
+  i64 waiting;  // K_ABSENT: the 'for' time (ms)
   std::vector<Code> filters;
 };
 struct RecvDef {
@@ -114,7 +115,7 @@ Program parse_ir(const void* blob, size_t len) {
   if (len < 16 || std::memcmp(blob, "SDHIR001", 8) != 0) throw std::runtime_error("bad IR magic");
   Reader r{reinterpret_cast<const i64*>(static_cast<const char*>(blob) + 8), (len - 8) / 8};
   Program p;
-  if (r.next() != 1) throw std::runtime_error("unsupported IR version");
+  if (r.next() != 2) throw std::runtime_error("unsupported IR version");
   p.stream_types.resize(r.next());
   for (auto& st : p.stream_types) {
     st.resize(r.next());
@@ -138,6 +139,7 @@ Program parse_ir(const void* blob, size_t len) {
       s.partner = (int)r.next(); s.next_pre = (int)r.next(); s.next_every = (int)r.next();
       s.within_every = (int)r.next(); s.callback = (int)r.next(); s.this_last = (int)r.next();
       s.has_selector = (int)r.next();
+      s.waiting = r.next();
       s.filters.resize(r.next());
       for (auto& f : s.filters) f = read_code(r);
     }
@@ -473,6 +475,11 @@ struct Pre {
   bool stateChanged = false, initialized = false;
   bool successCondition = false, startStateReset = false;  // CountPreStateProcessor
   bool iterating = false;
+  // AbsentStreamPreStateProcessor (state/AbsentStreamPreStateProcessor.java:38-54) and its
+  // Scheduler's toNotifyQueue (util/Scheduler.java:45: a FIFO of notification times)
+  i64 lastScheduledTime = 0;
+  bool active = true;
+  std::list<i64> timers;
 };
 struct Post {
   bool isEventReturned = false;
@@ -493,11 +500,12 @@ struct Runtime {
   const StateDef& S(int i) const { return q->states[i]; }
 
   // ---- pre processors -----------------------------------------------------------------------
-  // StreamPreStateProcessor.init():157-166
+  // StreamPreStateProcessor.init():157-166 (a SEQUENCE start whose next state is absent re-inits too)
   void init_pre(int i) {
     const StateDef& s = S(i);
     Pre& p = pres[i];
-    if (s.is_start && (!p.initialized || s.next_every >= 0)) {
+    const bool absent_next = q->type == Q_SEQUENCE && s.next_pre >= 0 && S(s.next_pre).kind == K_ABSENT;
+    if (s.is_start && (!p.initialized || s.next_every >= 0 || absent_next)) {
       StateEvent* se = new_state();
       addState(i, se);
       p.initialized = true;
@@ -518,6 +526,16 @@ struct Runtime {
       } else {
         p.newAndEvery.push_back(se);
         pp.newAndEvery.push_back(se);
+      }
+      return;
+    }
+    if (s.kind == K_ABSENT) {  // AbsentStreamPreStateProcessor.addState:78-101
+      if (!p.active) return;
+      if (q->type == Q_SEQUENCE) p.newAndEvery.clear();
+      p.newAndEvery.push_back(se);
+      if (!s.is_start) {
+        p.lastScheduledTime = se->ts + s.waiting;
+        p.timers.push_back(p.lastScheduledTime);
       }
       return;
     }
@@ -542,6 +560,10 @@ struct Runtime {
       return;
     }
     pres[i].newAndEvery.push_back(c);
+    if (s.kind == K_ABSENT) {  // AbsentStreamPreStateProcessor.addEveryState:103-115
+      pres[i].lastScheduledTime = se->ts + s.waiting;
+      pres[i].timers.push_back(pres[i].lastScheduledTime);
+    }
   }
 
   StateEvent* clone(StateEvent* se);  // StateEventCloner.copyStateEvent:46-58 (shallow)
@@ -581,7 +603,9 @@ struct Runtime {
       return;
     }
     p.pending.clear();
-    if (s.is_start && p.newAndEvery.empty()) {
+    // AbsentStreamPreStateProcessor.resetState:117-138 re-inits a start state whatever its
+    // newAndEvery list holds
+    if (s.is_start && (s.kind == K_ABSENT || p.newAndEvery.empty())) {
       if (q->type == Q_SEQUENCE && s.next_every < 0 && next_pending_nonempty(i)) return;
       init_pre(i);
     }
@@ -671,6 +695,24 @@ struct Runtime {
     }
   }
 
+  // AbsentStreamPostStateProcessor.process:31-52: the absent event arrived -- the partial is
+  // dropped (stateChanged) and the waiting restarts from this event
+  void absentPost(int i, StateEvent* se) {
+    const StateDef& s = S(i);
+    Pre& p = pres[i];
+    p.stateChanged = true;
+    StreamEvent* ev = se->slots[i];
+    se->ts = ev->ts;
+    posts[i].isEventReturned = true;
+    if (s.is_start && s.next_every == i) addEveryState(i, se);
+    p.lastScheduledTime = ev->ts + s.waiting;  // AbsentStreamPreStateProcessor.updateLastArrivalTime:69-75
+    p.timers.push_back(p.lastScheduledTime);
+  }
+  // AbsentStreamPreStateProcessor.sendEvent:212-228
+  void absentSend(int i, StateEvent* se);
+  // AbsentStreamPreStateProcessor.process:140-210: a timer event of this processor's scheduler
+  void absentTimer(int i, i64 currentTime);
+
   // ---- processAndReturn -----------------------------------------------------------------------
   std::vector<StateEvent*> processAndReturn(int i, i64 seq, i64 ts);
 
@@ -717,6 +759,59 @@ struct Engine {
   std::vector<std::pair<Runtime*, StateEvent*>> deferred;  // single-receiver chunk deferral
   std::string err;
   size_t gc_threshold = 1 << 20;
+  // time (the runtime's TimestampGenerator): the last event's timestamp or an explicit advance;
+  // absent processors' schedulers fire at their notification times as it passes them
+  bool started = false;
+  i64 now = 0;
+  bool has_absent = false;
+
+  // SiddhiAppRuntime.start -> AbsentStreamPreStateProcessor.start:276-286 (start states with a
+  // 'for' time schedule their first check)
+  void start(i64 t) {
+    started = true;
+    now = t;
+    for (auto& r : top) {
+      if (!r) continue;
+      for (size_t i = 0; i < r->pres.size(); ++i) {
+        const StateDef& s = r->q->states[i];
+        Pre& p = r->pres[i];
+        if (s.kind == K_ABSENT && s.is_start && s.waiting != -1 && p.active) {
+          p.lastScheduledTime = t + s.waiting;
+          p.timers.push_back(p.lastScheduledTime);
+        }
+      }
+    }
+  }
+  // Scheduler.sendTimerEvents:186-214 for every scheduler, in time order, up to time t: the
+  // scheduler whose queue head is earliest fires its head (ties: query, then state order); a timer
+  // may schedule more (they fire too if due)
+  void advance(i64 t) {
+    if (!started) start(t);
+    if (has_absent) {
+      for (;;) {
+        Runtime* best = nullptr;
+        int bi = -1;
+        i64 bt = 0;
+        for (auto& r : top) {
+          if (!r) continue;
+          for (size_t i = 0; i < r->pres.size(); ++i) {
+            const Pre& p = r->pres[i];
+            if (p.timers.empty() || p.timers.front() > t) continue;
+            if (!best || p.timers.front() < bt) {
+              best = r.get();
+              bi = (int)i;
+              bt = p.timers.front();
+            }
+          }
+        }
+        if (!best) break;
+        best->pres[bi].timers.pop_front();
+        now = bt;
+        best->absentTimer(bi, bt);
+      }
+    }
+    if (t > now) now = t;
+  }
 
   void emit(Runtime* rt, StateEvent* se) {
     Match m;
@@ -779,6 +874,7 @@ void Runtime::process(int i, StateEvent* se) {
   if (!filters_pass(i, se)) return;
   switch (S(i).kind) {
     case K_STREAM: streamPost(i, se); break;
+    case K_ABSENT: absentPost(i, se); break;
     case K_COUNT: countPost(i, se); break;
     default: logicalPost(i, se); break;
   }
@@ -788,6 +884,7 @@ std::vector<StateEvent*> Runtime::processAndReturn(int i, i64 seq, i64 ts) {
   std::vector<StateEvent*> ret;
   const StateDef& s = S(i);
   Pre& p = pres[i];
+  if (s.kind == K_ABSENT && !p.active) return ret;  // AbsentStreamPreStateProcessor.processAndReturn:231-244
   p.iterating = true;
   for (auto it = p.pending.begin(); it != p.pending.end();) {
     StateEvent* se = *it;
@@ -850,15 +947,69 @@ std::vector<StateEvent*> Runtime::processAndReturn(int i, i64 seq, i64 ts) {
     } else {
       se->slots[i] = nullptr;
       if (q->type == Q_SEQUENCE) {
-        it = p.pending.erase(it);
-        if (s.kind == K_STREAM && s.callback >= 0) startStateReset(s.callback);
+        // removeOnNoStateChange: true for StreamPre, false for AbsentStreamPre (:246-248)
+        if (s.kind == K_ABSENT) ++it;
+        else it = p.pending.erase(it);
+        if ((s.kind == K_STREAM || s.kind == K_ABSENT) && s.callback >= 0) startStateReset(s.callback);
       } else {
         ++it;
       }
     }
   }
   p.iterating = false;
+  if (s.kind == K_ABSENT) ret.clear();  // an absent processor always returns an empty chunk
   return ret;
+}
+
+void Runtime::absentSend(int i, StateEvent* se) {
+  const StateDef& s = S(i);
+  if (s.has_selector) eng->emit(this, se);   // thisStatePostProcessor.nextProcessor: the selector
+  if (s.next_pre >= 0) addState(s.next_pre, se);
+  if (s.next_every >= 0) addEveryState(s.next_every, se);
+  else if (s.is_start) pres[i].active = false;
+  if (s.callback >= 0) startStateReset(s.callback);
+}
+
+void Runtime::absentTimer(int i, i64 currentTime) {
+  const StateDef& s = S(i);
+  Pre& p = pres[i];
+  if (!p.active) return;
+  std::vector<StateEvent*> ret;
+  bool initialize = s.is_start && p.newAndEvery.empty() && p.pending.empty();
+  if (initialize && q->type == Q_SEQUENCE && s.next_every < 0 && p.lastScheduledTime > 0) initialize = false;
+  if (initialize) {
+    addState(i, new_state());
+  } else if (q->type == Q_SEQUENCE && !p.newAndEvery.empty()) {
+    resetState(i);
+  }
+  updateState(i);
+  for (auto it = p.pending.begin(); it != p.pending.end();) {
+    StateEvent* se = *it;
+    if (isExpired(i, se, currentTime)) {
+      it = p.pending.erase(it);
+      if (s.within_every >= 0 && s.next_every != i) {
+        if (s.next_every < 0) throw std::runtime_error("NullPointerException in absent expiry (reference)");
+        addEveryState(s.next_every, se);
+      }
+      continue;
+    }
+    if ((se->ts == -1 && currentTime >= p.lastScheduledTime) || (se->ts != -1 && currentTime >= se->ts + s.waiting)) {
+      it = p.pending.erase(it);
+      se->ts = currentTime;
+      ret.push_back(se);
+      continue;
+    }
+    ++it;
+  }
+  if (s.within_every >= 0) updateState(s.within_every);
+  const bool notProcessed = ret.empty();
+  for (StateEvent* se : ret) absentSend(i, se);
+  // (the timestamp generator's time equals the timer's here, so the actualCurrentTime branch at
+  // :202-205 never applies)
+  if (notProcessed && p.lastScheduledTime < currentTime) {
+    p.lastScheduledTime = currentTime + s.waiting;
+    p.timers.push_back(p.lastScheduledTime);
+  }
 }
 
 void Runtime::receive(int stream, i64 seq, i64 ts) {
@@ -980,6 +1131,8 @@ int oracle_create(const void* blob, size_t len, OracleEngine** out) {
     }
     e->part_inst.resize(e->prog.parts.size());
     e->key_order.resize(e->prog.parts.size());
+    for (const auto& q : e->prog.queries)
+      for (const auto& st : q.states) e->has_absent |= st.kind == K_ABSENT;
     *out = e;
     return 0;
   } catch (const std::exception& ex) {
@@ -1003,6 +1156,9 @@ int oracle_send(OracleEngine* e, int32_t stream, int64_t n, const int64_t* ts, c
       else ev.nulls.assign(na, 0);
       seqs.push_back((i64)e->log.size());
       e->log.push_back(std::move(ev));
+      // timers due up to this event fire before it (playback order: TimestampGenerator time
+      // change -> Scheduler.sendTimerEvents before the event reaches the junction)
+      if (!as_chunk || seqs.size() == 1) e->advance(ts[k]);
       if (!as_chunk) {
         send_chunk(e, stream, seqs);
         seqs.clear();
@@ -1047,6 +1203,30 @@ int oracle_get_matches(const OracleEngine* e, int64_t* query, int64_t* key, int6
 }
 
 void oracle_clear_matches(OracleEngine* e) { e->matches.clear(); }
+
+// the runtime starts at time t (SiddhiAppRuntime.start); without it the first event or advance starts it
+int oracle_start(OracleEngine* e, int64_t t) {
+  try {
+    if (e->started) throw std::runtime_error("already started");
+    e->start(t);
+    return 0;
+  } catch (const std::exception& ex) {
+    e->err = ex.what();
+    return -1;
+  }
+}
+
+// time passes to t with no event (the scheduler thread of a live runtime; a playback heartbeat)
+int oracle_advance_time(OracleEngine* e, int64_t t) {
+  try {
+    e->advance(t);
+    e->gc();
+    return 0;
+  } catch (const std::exception& ex) {
+    e->err = ex.what();
+    return -1;
+  }
+}
 
 int64_t oracle_live_partials(const OracleEngine* e) {  // entries of every pending list
   int64_t n = 0;

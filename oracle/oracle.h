@@ -37,6 +37,10 @@ int64_t oracle_match_words(const OracleEngine* e);
 int oracle_get_matches(const OracleEngine* e, int64_t* query, int64_t* key, int64_t* ts,
                        int64_t* off, int64_t* words);
 void oracle_clear_matches(OracleEngine* e);
+/* Absent patterns' time: the runtime starts at t (SiddhiAppRuntime.start; else at the first event
+ * or advance), and time passes to t with no event (the schedulers fire what falls due). */
+int oracle_start(OracleEngine* e, int64_t t);
+int oracle_advance_time(OracleEngine* e, int64_t t);
 /* Partial matches held in the pending lists of every pre-processor (after the last send). */
 int64_t oracle_live_partials(const OracleEngine* e);
 const char* oracle_error(const OracleEngine* e);

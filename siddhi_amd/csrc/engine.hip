@@ -107,6 +107,7 @@ struct Insn {
 struct IState {
   int kind, stream, is_start, min, max, ltype, partner, next_pre, next_every, within_every, callback,
       this_last, has_selector;
+  int64_t waiting;  // absent states: the 'for' time (ms), else -1
   std::vector<std::vector<Insn>> filters;
 };
 struct IQuery {
@@ -147,7 +148,7 @@ IProgram read_ir(const void* blob, size_t len) {
   if (!blob || len < 16 || memcmp(blob, "SDHIR001", 8) != 0) throw Error(SDH_E_INVALID, "bad IR magic");
   WordReader r{reinterpret_cast<const int64_t*>(static_cast<const char*>(blob) + 8), (len - 8) / 8};
   IProgram p;
-  if (r.next() != 1) throw Error(SDH_E_INVALID, "unsupported IR version");
+  if (r.next() != 2) throw Error(SDH_E_INVALID, "unsupported IR version");
   p.stream_types.resize((size_t)r.next());
   for (auto& s : p.stream_types) {
     s.resize((size_t)r.next());
@@ -171,6 +172,7 @@ IProgram read_ir(const void* blob, size_t len) {
       s.partner = (int)r.next(); s.next_pre = (int)r.next(); s.next_every = (int)r.next();
       s.within_every = (int)r.next(); s.callback = (int)r.next(); s.this_last = (int)r.next();
       s.has_selector = (int)r.next();
+      s.waiting = r.next();
       s.filters.resize((size_t)r.next());
       for (auto& f : s.filters) f = read_code(r);
     }

@@ -25,6 +25,7 @@ using LCode = std::vector<LInsn>;
 struct LState {
   int kind, stream, is_start, min, max, ltype, partner, next_pre, next_every, within_every, callback, this_last,
       has_selector;
+  int64_t waiting;  // K_ABSENT: the 'for' time (ms), else -1
   std::vector<LCode> filters;
 };
 struct LRecv {
@@ -84,7 +85,7 @@ inline LProgram read_program(const void* blob, size_t len) {
     return c;
   };
   LProgram p;
-  if (nx() != 1) throw LowerError("unsupported IR version");
+  if (nx() != 2) throw LowerError("unsupported IR version");
   p.stream_types.resize((size_t)nx());
   for (auto& s : p.stream_types) {
     s.resize((size_t)nx());
@@ -108,6 +109,7 @@ inline LProgram read_program(const void* blob, size_t len) {
       s.partner = (int)nx(); s.next_pre = (int)nx(); s.next_every = (int)nx();
       s.within_every = (int)nx(); s.callback = (int)nx(); s.this_last = (int)nx();
       s.has_selector = (int)nx();
+      s.waiting = nx();
       s.filters.resize((size_t)nx());
       for (auto& f : s.filters) f = code();
     }

@@ -22,7 +22,9 @@ the CPU oracle (``oracle/oracle.cpp``)::
              n_nodes node*     (runtime tree, node 0 is the root)
              n_outputs { n_insn insn* }
     state := kind stream_idx is_start min max logical_type partner next_pre next_every_pre
-             within_every_pre callback_pre this_last_post has_selector n_filters { n_insn insn* }
+             within_every_pre callback_pre this_last_post has_selector waiting_ms
+             n_filters { n_insn insn* }
+             (waiting_ms: the 'for' time of an absent state, -1 otherwise)
     node  := node_type a b pre
     insn  := w0 a b imm     w0 = op | ltype<<8 | rtype<<16 | restype<<24
 """
@@ -33,7 +35,7 @@ from dataclasses import dataclass, field
 from typing import List
 
 MAGIC = b"SDHIR001"
-VERSION = 1
+VERSION = 2
 
 # attribute / value types
 T_INT, T_LONG, T_FLOAT, T_DOUBLE, T_BOOL, T_STRING = range(6)
@@ -53,7 +55,7 @@ IDX_CURRENT = -1
 IDX_LAST = -2
 
 # state kinds / logical types / query types / receivers / runtime nodes
-K_STREAM, K_COUNT, K_LOGICAL = range(3)
+K_STREAM, K_COUNT, K_LOGICAL, K_ABSENT = range(4)  # K_ABSENT: AbsentStreamPre/PostStateProcessor
 L_AND, L_OR = range(2)
 Q_PATTERN, Q_SEQUENCE = range(2)
 R_SINGLE, R_MULTI = range(2)
@@ -92,6 +94,7 @@ class StateIR:
     callback_pre: int = -1
     this_last_post: int = -1
     has_selector: bool = False
+    waiting_ms: int = -1
     filters: List[List[Insn]] = field(default_factory=list)
     alias: str = ""
 
@@ -207,7 +210,7 @@ class ProgramIR:
             for s in q.states:
                 w.extend([s.kind, s.stream_idx, int(s.is_start), s.min, s.max, s.logical_type, s.partner,
                           s.next_pre, s.next_every_pre, s.within_every_pre, s.callback_pre,
-                          s.this_last_post, int(s.has_selector), len(s.filters)])
+                          s.this_last_post, int(s.has_selector), s.waiting_ms, len(s.filters)])
                 for f in s.filters:
                     code(f)
             w.append(len(q.start_ids))

@@ -32,7 +32,7 @@ import struct
 from typing import List, Optional
 
 from . import ql
-from .ir import (AR_CODE, CMP_CODE, INT_MAX, K_COUNT, K_LOGICAL, K_STREAM, L_AND, L_OR, N_COUNT,
+from .ir import (AR_CODE, CMP_CODE, INT_MAX, K_ABSENT, K_COUNT, K_LOGICAL, K_STREAM, L_AND, L_OR, N_COUNT,
                  N_EVERY, N_LOGICAL, N_NEXT, N_STREAM, OP_AND, OP_ARITH, OP_ATTR, OP_CMP, OP_CONST,
                  OP_IS_NULL, OP_NOT, OP_OR, OP_STREAM_IS_NULL, Q_PATTERN, Q_SEQUENCE, R_MULTI,
                  R_SINGLE, T_BOOL, T_DOUBLE, T_FLOAT, T_INT, T_LONG, T_STRING, TYPE_CODE, Insn,
@@ -263,6 +263,15 @@ class _QueryPlanner:
         """Returns (node, first_pre, last_post)."""
         if isinstance(e, ql.StreamSE):
             sid = self._parse_stream(e, is_start, K_STREAM, {})
+            pres.append(sid)
+            return self._new_node(NodeIR(N_STREAM, pre=sid)), sid, sid
+        if isinstance(e, ql.AbsentSE):
+            # AbsentStreamStateElement: a stream state with the absent pre/post pair and its own
+            # scheduler (StateInputStreamParser.java:174-200)
+            if self.partitioned:
+                raise SiddhiAppCreationException(
+                    "absent patterns inside a partition are not on the accelerated path")
+            sid = self._parse_stream(e.stream, is_start, K_ABSENT, {"waiting_ms": e.waiting_ms})
             pres.append(sid)
             return self._new_node(NodeIR(N_STREAM, pre=sid)), sid, sid
         if isinstance(e, ql.NextSE):

@@ -16,8 +16,12 @@ Covers the part of the SiddhiQL grammar that feeds the pattern/sequence (NFA) pa
 * literals: ``20`` INT, ``20L`` LONG, ``20.5``/``20.5d`` DOUBLE, ``20.5f`` FLOAT (``SiddhiQL.g4:715-732``)
 * ``partition with (attr of S, ...) begin <queries> end``
 
-Absent patterns (``not S for T``), windows, joins, functions, group-by and output rate limiting
-are outside the accelerated path and raise :class:`SiddhiParserException`.
+* absent states ``not S[..] for T`` (``SiddhiQL.g4:263-268``, ``basic_absent_pattern_source``) in
+  pattern and sequence chains, with or without ``every``
+
+Logical absent states (``e1=A and not B``, ``SiddhiQL.g4:251-260``), windows, joins, functions,
+group-by and output rate limiting are outside the accelerated path and raise
+:class:`SiddhiParserException`.
 """
 from __future__ import annotations
 
@@ -95,6 +99,13 @@ class StreamSE:
     alias: Optional[str]
     stream: str
     filters: List[object] = field(default_factory=list)
+
+
+@dataclass
+class AbsentSE:
+    """``not S[..] for T`` (AbsentStreamStateElement; the stream carries no alias)."""
+    stream: StreamSE
+    waiting_ms: int
 
 
 @dataclass
@@ -502,6 +513,8 @@ class Parser:
                 if "," in seps:
                     self.error("'every' over a parenthesised sequence chain is not valid SiddhiQL")
                 return EverySE(inner)
+            if self.at("not"):
+                return EverySE(self.absent())
             return EverySE(self.source())
         if self.at("("):
             self.i += 1
@@ -509,8 +522,23 @@ class Parser:
             self.expect(")")
             return inner
         if self.at("not"):
-            self.error("absent patterns ('not S for T') are outside the accelerated path")
+            return self.absent()
         return self.source()
+
+    def absent(self):
+        """basic_absent_pattern_source: NOT basic_source for_time (SiddhiQL.g4:267-268)."""
+        self.expect("not")
+        s = self.std_source()
+        if s.alias is not None:
+            self.error("an absent stream ('not S') cannot carry an alias")
+        if self.at("and") or self.at("or"):
+            self.error("logical absent patterns ('not A and B') are outside the accelerated path")
+        if not self.accept("for"):
+            self.error("an absent stream needs a 'for' waiting time")
+        w = self.time_value()
+        if self.at("and") or self.at("or"):
+            self.error("logical absent patterns ('not A for T and B') are outside the accelerated path")
+        return AbsentSE(s, w)
 
     def source(self):
         s1 = self.std_source()
@@ -518,7 +546,7 @@ class Parser:
             ty = self.peek().text
             self.i += 1
             if self.at("not"):
-                self.error("absent logical patterns are outside the accelerated path")
+                self.error("logical absent patterns ('A and not B') are outside the accelerated path")
             s2 = self.std_source()
             return LogicalSE(ty, s1, s2)
         # count / kleene

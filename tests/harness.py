@@ -44,6 +44,8 @@ def oracle_lib():
         lib.oracle_error.argtypes = [P]
         lib.oracle_error.restype = ctypes.c_char_p
         lib.oracle_destroy.argtypes = [P]
+        lib.oracle_start.argtypes = [P, I64]
+        lib.oracle_advance_time.argtypes = [P, I64]
         _lib = lib
     return _lib
 
@@ -84,6 +86,14 @@ class OracleEngine:
         rc = self.lib.oracle_send(self.h, stream, len(ts), ts.ctypes.data, vals.ctypes.data,
                                   None if nl is None else nl.ctypes.data, int(as_chunk))
         if rc != 0:
+            raise OracleError(self.lib.oracle_error(self.h).decode())
+
+    def start(self, t: int):
+        if self.lib.oracle_start(self.h, int(t)) != 0:
+            raise OracleError(self.lib.oracle_error(self.h).decode())
+
+    def advance_time(self, t: int):
+        if self.lib.oracle_advance_time(self.h, int(t)) != 0:
             raise OracleError(self.lib.oracle_error(self.h).decode())
 
     def take_matches(self, n_slots_of):
@@ -142,6 +152,15 @@ class App:
         vals, nulls = encode_rows(rows, self.ir.streams[si].attr_types, self.dictionary)
         self.log.append(si, ts, vals, nulls)
         self.engine.send(si, ts, vals, nulls, as_chunk)
+        self.matches.extend(self.engine.take_matches(lambda q: len(self.ir.queries[q].states)))
+
+    def start(self, t: int):
+        """SiddhiAppRuntime.start at time t (absent patterns schedule from it)."""
+        self.engine.start(t)
+
+    def advance_time(self, t: int):
+        """Time passes to t with no event: absent patterns' schedulers fire what falls due."""
+        self.engine.advance_time(t)
         self.matches.extend(self.engine.take_matches(lambda q: len(self.ir.queries[q].states)))
 
     def rows_for_query(self, qname: str):

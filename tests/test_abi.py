@@ -49,7 +49,7 @@ def test_malformed_program_is_invalid_without_a_device():
     lib = load_library()
     for blob, why in ((b"", b"magic"), (b"NOT-AN-IR-BLOB-AT-ALL", b"magic"),
                       (b"SDHIR001" + (7).to_bytes(8, "little"), b"version"),
-                      (b"SDHIR001" + (1).to_bytes(8, "little") + (3).to_bytes(8, "little"), b"truncated")):
+                      (b"SDHIR001" + (2).to_bytes(8, "little") + (3).to_bytes(8, "little"), b"truncated")):
         rc, h = _create(lib, blob)
         assert rc == -1 and not h.value, (blob, rc)
         assert why in lib.sdh_last_error(None).lower(), lib.sdh_last_error(None)
