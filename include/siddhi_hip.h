@@ -80,6 +80,9 @@ typedef struct sdh_config {
 /* Run every query on the general interpreter K_gen (no chain / ratchet plans); for differential
  * testing. */
 #define SDH_FLAG_FORCE_GEN 4
+/* @app:playback: while absent states' timers fire, the runtime's time is the event time that let
+ * them fire (TimestampGeneratorImpl.currentTime in playback), not the timer's own time. */
+#define SDH_FLAG_PLAYBACK 8
 
 /* One columnar (SoA) batch of events of one stream, in arrival order.
  * cols[a] points to n elements of attribute a with the stream schema's native width:
@@ -146,6 +149,13 @@ int sdh_engine_poll(sdh_engine* e, sdh_matches* out);
 int sdh_engine_poll_device(sdh_engine* e, sdh_matches* out);
 /* Device-resident match count of the last push (no host copy of the matches). */
 int sdh_engine_pending_matches(sdh_engine* e, int64_t* n);
+/* Absent patterns (`not S[..] for T`) and time. The runtime starts at t (SiddhiAppRuntime.start:
+ * start states with a 'for' time schedule their first check at t + T); without this call it starts
+ * with its first event or advance. sdh_engine_advance_time: time passes to t with no event, and
+ * every absent state's scheduler fires what falls due (Scheduler.java:186-287); pushes fire the
+ * timers due by each event before it. Replaces: the scheduler thread / playback heartbeat. */
+int sdh_engine_start(sdh_engine* e, int64_t t);
+int sdh_engine_advance_time(sdh_engine* e, int64_t t);
 int sdh_engine_stats(sdh_engine* e, sdh_stats* out);
 int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len);
 int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len);

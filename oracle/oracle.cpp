@@ -711,7 +711,7 @@ struct Runtime {
   // AbsentStreamPreStateProcessor.sendEvent:212-228
   void absentSend(int i, StateEvent* se);
   // AbsentStreamPreStateProcessor.process:140-210: a timer event of this processor's scheduler
-  void absentTimer(int i, i64 currentTime);
+  void absentTimer(int i, i64 currentTime, i64 actualCurrentTime);
 
   // ---- processAndReturn -----------------------------------------------------------------------
   std::vector<StateEvent*> processAndReturn(int i, i64 seq, i64 ts);
@@ -764,6 +764,7 @@ struct Engine {
   bool started = false;
   i64 now = 0;
   bool has_absent = false;
+  bool playback = false;  // @app:playback (TimestampGeneratorImpl.currentTime = the last event time)
 
   // SiddhiAppRuntime.start -> AbsentStreamPreStateProcessor.start:276-286 (start states with a
   // 'for' time schedule their first check)
@@ -807,7 +808,7 @@ struct Engine {
         if (!best) break;
         best->pres[bi].timers.pop_front();
         now = bt;
-        best->absentTimer(bi, bt);
+        best->absentTimer(bi, bt, playback ? t : bt);
       }
     }
     if (t > now) now = t;
@@ -970,7 +971,7 @@ void Runtime::absentSend(int i, StateEvent* se) {
   if (s.callback >= 0) startStateReset(s.callback);
 }
 
-void Runtime::absentTimer(int i, i64 currentTime) {
+void Runtime::absentTimer(int i, i64 currentTime, i64 actualCurrentTime) {
   const StateDef& s = S(i);
   Pre& p = pres[i];
   if (!p.active) return;
@@ -1004,8 +1005,9 @@ void Runtime::absentTimer(int i, i64 currentTime) {
   if (s.within_every >= 0) updateState(s.within_every);
   const bool notProcessed = ret.empty();
   for (StateEvent* se : ret) absentSend(i, se);
-  // (the timestamp generator's time equals the timer's here, so the actualCurrentTime branch at
-  // :202-205 never applies)
+  // actualCurrentTime: the timestamp generator's time -- the timer's own in a live runtime, the
+  // event time that let it fire in playback (:202-205)
+  if (actualCurrentTime > s.waiting + currentTime) p.lastScheduledTime = actualCurrentTime + s.waiting;
   if (notProcessed && p.lastScheduledTime < currentTime) {
     p.lastScheduledTime = currentTime + s.waiting;
     p.timers.push_back(p.lastScheduledTime);
@@ -1214,6 +1216,11 @@ int oracle_start(OracleEngine* e, int64_t t) {
     e->err = ex.what();
     return -1;
   }
+}
+
+int oracle_set_playback(OracleEngine* e, int on) {
+  e->playback = on != 0;
+  return 0;
 }
 
 // time passes to t with no event (the scheduler thread of a live runtime; a playback heartbeat)

@@ -41,6 +41,7 @@ void oracle_clear_matches(OracleEngine* e);
  * or advance), and time passes to t with no event (the schedulers fire what falls due). */
 int oracle_start(OracleEngine* e, int64_t t);
 int oracle_advance_time(OracleEngine* e, int64_t t);
+int oracle_set_playback(OracleEngine* e, int on);
 /* Partial matches held in the pending lists of every pre-processor (after the last send). */
 int64_t oracle_live_partials(const OracleEngine* e);
 const char* oracle_error(const OracleEngine* e);

@@ -618,6 +618,11 @@ struct sdh_engine {
   int gB32 = 1, gB64 = 1;
   int gHotS = 1, gHotNU = 1;  // K_gen LDS hot-word cache extents (max states / node-mask words)
   kg::Sizing gsz;                    // K_gen pool sizing (grows on overflow: gen_relayout)
+  // absent states (kgen.h fire_timers): the runtime's start time and whether any query has them
+  bool started = false;
+  int64_t start_ts = 0;
+  bool has_absent = false;
+  int64_t advance_to = INT64_MIN;    // set while a time advance runs (sdh_engine_advance_time)
   std::vector<char> gq_arena;        // [gq] the query runs on K_gen (has an instance arena)
   int64_t gen_regrows = 0;           // pool growths so far (sdh_stats)
   struct GenSet {
@@ -818,7 +823,7 @@ void append_gen(sdh_engine* e) {
   HIPCHK(hipStreamSynchronize(e->stream));
   e->mt.n += n_rec;
   e->mt.nw += used;
-  e->mt.n_lo = std::max(e->mt.n_lo, 1);
+  e->mt.n_lo = std::max(e->mt.n_lo, e->has_absent ? 2 : 1);  // timer records: (fire order, time)
 }
 
 void table_clear(sdh_engine* e) {
@@ -850,7 +855,8 @@ int64_t table_sort(sdh_engine* e, int64_t* total_words) {
   e->po_seq.ensure(n);
   e->po_len.ensure(n + 1);
   e->po_off.ensure(n + 1);
-  const int lo_bits = std::max(1, bits_of((uint64_t)std::max<int64_t>(e->seq, 1 << 16)));
+  // timer records' tiebreaks are a full timestamp and (query << 32 | fire ordinal)
+  const int lo_bits = e->has_absent ? 64 : std::max(1, bits_of((uint64_t)std::max<int64_t>(e->seq, 1 << 16)));
   const int hi_bits = bits_of((uint64_t)(e->seq - e->seq_ref)) + RANK_BITS;
   int32_t* perm = nullptr;
   HIPCHK(sdh_poll_sort(table_view(e), n, e->mt.n_lo, lo_bits, hi_bits, e->p_keys.p, e->p_perm.p, e->p_temp.p,
@@ -1418,6 +1424,7 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
       e->gq.push_back(g);
       if (use_part) kpart[qi] = kpart_shape(e->lp, qi, g);
       e->gq_arena.push_back(kpart[qi].kind < 0);
+      e->has_absent |= g.lay.TQ > 0;
       if (kpart[qi].kind >= 0) continue;  // K_part: no K_gen arena
       e->gB32 = std::max(e->gB32, g.lay.n32);
       e->gB64 = std::max(e->gB64, g.lay.n64);
@@ -1548,7 +1555,7 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
     t.ensure(SEQ_TMAX * SEQ_TW);
     HIPCHK(hipMemset(t.p, 0, SEQ_TMAX * SEQ_TW * 8));
   }
-  e->d_glists.resize(e->prog.stream_types.size());
+  e->d_glists.resize(e->prog.stream_types.size() + 1);
   spec_build(e);
   e->d_group_tmpl.ensure(e->group_tmpl.size());
   HIPCHK(hipMemcpy(e->d_group_tmpl.p, e->group_tmpl.data(), e->group_tmpl.size() * 4, hipMemcpyHostToDevice));
@@ -1592,7 +1599,7 @@ void gen_relayout(sdh_engine* e, const kg::Sizing& sz, bool remap) {
   for (size_t i = 0; i < e->gq.size(); ++i) {
     kg::GQuery& g = e->gq[i];
     oldL[i] = g.lay;
-    kg::make_layout(g.lay, g.lay.S, sz.R, sz.N, sz.LC, g.lay.NA, g.lay.v32 != 0);
+    kg::make_layout(g.lay, g.lay.S, sz.R, sz.N, sz.LC, g.lay.NA, g.lay.v32 != 0, g.lay.TQ > 0 ? sz.LC : 0);
     newL[i] = g.lay;
     if (!e->gq_arena[i]) continue;
     b32 = std::max(b32, g.lay.n32);
@@ -1664,6 +1671,10 @@ sdh::GenLaunch gen_launch_base(sdh_engine* e, const sdh_engine::GenSet& gs, cons
   L.rec_cap = e->g_out_cap / 7 + 1;
   L.rec_next = e->g_rec_next.p;
   L.write_records = write ? 1 : 2;
+  L.start_ts = e->start_ts;
+  L.advance_to = e->advance_to;
+  L.timer_seq = e->seq + B.n;
+  L.playback = (e->cfg.flags & SDH_FLAG_PLAYBACK) ? 1 : 0;
   return L;
 }
 
@@ -1732,7 +1743,9 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       std::vector<int32_t> seq_rows, gen_groups;
       int seqS = 1;
       for (int g = 0; g < gs.n_groups; ++g) {
-        if (e->gq[e->group_tmpl[gs.group_base + g]].recv_n[stream] == 0) continue;
+        const kg::GQuery& tq = e->gq[e->group_tmpl[gs.group_base + g]];
+        const bool timed = tq.lay.TQ > 0;  // absent states: time passes on every push and advance
+        if (n == 0 ? !timed : (tq.recv_n[stream] == 0 && !timed)) continue;
         if (e->group_seq[gs.group_base + g] > 0) {
           seq_rows.push_back(gs.group_base + g);
           seqS = std::max(seqS, e->group_seq[gs.group_base + g]);
@@ -1742,7 +1755,8 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       }
       if (seq_rows.empty() && gen_groups.empty()) continue;
       // the lists depend on the stream only: uploaded once, before any kernel reads them
-      auto& gl = e->d_glists[stream];
+      // (one cached list per stream, and one more for time advances: B.n == 0)
+      auto& gl = e->d_glists[n == 0 ? e->prog.stream_types.size() : (size_t)stream];
       if (!gl.p) {
         gl.ensure(std::max<size_t>(1, seq_rows.size() + gen_groups.size()));
         std::vector<int32_t> both(seq_rows);
@@ -1840,8 +1854,9 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
     }
   }
   // partitions: route the batch once (dense key ids, events grouped by key), then run the
-  // partition's K_gen set and its K_part sets over the same segments
-  for (int pi = 0; pi < (int)e->routes.size(); ++pi) {
+  // partition's K_gen set and its K_part sets over the same segments (a time advance has no
+  // events, and no partitioned query has absent states)
+  for (int pi = 0; pi < (int)e->routes.size() && n > 0; ++pi) {
     if (!e->routes[pi]) continue;
     auto& rt = *e->routes[pi];
     const kg::LPart& pd = e->lp.parts[pi];
@@ -2224,6 +2239,10 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   }
   double ms = 0, bytes = 0;
   int64_t consumers = 0;
+  if (!e->started) {  // the runtime starts with its first event unless sdh_engine_start said when
+    e->started = true;
+    e->start_ts = t01[0];
+  }
   // the previous push's device-only matches (SDH_FLAG_DEVICE_MATCHES) are dropped here
   e->work.clear();
   e->device_matches = 0;
@@ -2433,9 +2452,14 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     // state count and the stream of its last state (the trigger of a chain-plan match)
     const size_t nq_all = e->prog.q.size();
     if (nq_all >= ((size_t)1 << RANK_BITS)) throw Error(SDH_E_UNSUPPORTED, "more than 2^20 queries");
+    // device ranks are out_rank + 1: rank 0 orders the absent states' timer matches before the
+    // triggering event's own
     e->d_out_rank.ensure(std::max<size_t>(1, e->out_rank.size()));
-    if (!e->out_rank.empty())
-      HIPCHK(hipMemcpy(e->d_out_rank.p, e->out_rank.data(), e->out_rank.size() * 4, hipMemcpyHostToDevice));
+    if (!e->out_rank.empty()) {
+      std::vector<int32_t> r1(e->out_rank.size());
+      for (size_t k = 0; k < r1.size(); ++k) r1[k] = e->out_rank[k] + 1;
+      HIPCHK(hipMemcpy(e->d_out_rank.p, r1.data(), r1.size() * 4, hipMemcpyHostToDevice));
+    }
     std::vector<int32_t> qinfo(std::max<size_t>(1, 2 * nq_all), 0);
     for (size_t q = 0; q < nq_all; ++q) {
       qinfo[2 * q] = (int32_t)e->prog.q[q].st.size();
@@ -2466,6 +2490,60 @@ int sdh_engine_flush(sdh_engine* e) {
   if (!e) return SDH_E_INVALID;
   return guard(e, [&]() {
     HIPCHK(hipStreamSynchronize(e->stream));
+    return SDH_OK;
+  });
+}
+
+int sdh_engine_start(sdh_engine* e, int64_t t) {
+  if (!e) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    check_usable(e);
+    if (e->started) throw Error(SDH_E_INVALID, "the engine has already started");
+    e->started = true;
+    e->start_ts = t;
+    return SDH_OK;
+  });
+}
+
+// Time passes to t with no event: every absent state's scheduler fires what falls due (the timer
+// thread of a live runtime, Scheduler.java:258-287). Its matches join the device table like a
+// push's, ordered by (timer time, query, fire order) before the next event's.
+int sdh_engine_advance_time(sdh_engine* e, int64_t t) {
+  if (!e) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    check_usable(e);
+    if (!e->started) {
+      e->started = true;
+      e->start_ts = t;
+    }
+    if (!e->has_absent) return SDH_OK;
+    HIPCHK(hipSetDevice(e->dev));
+    StreamBatch B{};
+    B.n = 0;
+    B.stream = 0;
+    B.n_attr = (int)e->prog.stream_types[0].size();
+    B.seq_base = e->seq;
+    B.prev_ts = e->prev_ts[0];
+    e->work.clear();
+    e->device_matches = 0;
+    e->r_blocks_used = 0;
+    e->r_matches = 0;
+    e->g_dev_matches = 0;
+    e->g_used = 0;
+    e->g_out_lost = false;
+    double ms = 0, bytes = 0;
+    e->advance_to = t;
+    try {
+      launch_gen(e, 0, B, &ms, &bytes);
+    } catch (const std::exception& ex) {
+      e->advance_to = INT64_MIN;
+      e->broken = ex.what();
+      throw;
+    }
+    e->advance_to = INT64_MIN;
+    if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES)) append_gen(e);
+    if (e->g_out_lost)
+      throw Error(SDH_E_CAPACITY, "K_gen match output overflow: the advance was applied but its matches were lost");
     return SDH_OK;
   });
 }
@@ -2512,10 +2590,11 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
   });
 }
 
-// snapshot: [magic][version][n_q][pcap][gB32][gB64][R][N][LC][seq][n_streams][prev_ts...] then per query
+// snapshot: [magic][version][n_q][pcap][gB32][gB64][R][N][LC][started][start_ts][seq][n_streams][prev_ts...]
+// then per query
 // header + table, ratchet deques, K_gen arenas + key tables, K_seq tails
 constexpr int64_t SNAP_MAGIC = 0x5344485350415254LL;
-constexpr int64_t SNAP_VERSION = 4;
+constexpr int64_t SNAP_VERSION = 5;
 int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
   if (!e || !blob || !len) return SDH_E_INVALID;
   return guard(e, [&]() {
@@ -2523,7 +2602,8 @@ int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
     const size_t nq = e->lq.size();
     const size_t tbl = (size_t)NF * e->pcap;
     std::vector<int64_t> w{SNAP_MAGIC, SNAP_VERSION, (int64_t)nq, e->pcap, e->gB32, e->gB64,
-                           e->gsz.R, e->gsz.N, e->gsz.LC, e->seq, (int64_t)e->prev_ts.size()};
+                           e->gsz.R, e->gsz.N, e->gsz.LC, e->started ? 1 : 0, e->start_ts, e->seq,
+                           (int64_t)e->prev_ts.size()};
     w.insert(w.end(), e->prev_ts.begin(), e->prev_ts.end());
     for (size_t q = 0; q < nq; ++q) {
       InstHeader h;
@@ -2632,6 +2712,8 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
     if (sz.R != e->gsz.R || sz.N != e->gsz.N || sz.LC != e->gsz.LC) gen_relayout(e, sz, false);
     if (b32 != e->gB32 || b64 != e->gB64)
       throw Error(SDH_E_INVALID, "snapshot of a different K_gen arena layout (another build or pool sizing)");
+    e->started = nx() != 0;  // the runtime's start time (absent states' schedules)
+    e->start_ts = nx();
     e->seq = nx();
     const size_t ns = (size_t)nx();
     if (ns != e->prev_ts.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");

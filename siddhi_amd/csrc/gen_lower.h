@@ -243,6 +243,8 @@ inline GQuery lower_gen(const LProgram& P, int qi, const Sizing& sz) {
     d.ltype = s.ltype; d.partner = s.partner; d.next_pre = s.next_pre; d.next_every = s.next_every;
     d.within_every = s.within_every; d.callback = s.callback; d.this_last = s.this_last;
     d.has_selector = s.has_selector;
+    d.pad = 0;
+    d.waiting = s.waiting;
     if (s.filters.size() > (size_t)GMAXF) throw LowerError("too many filters");
     d.n_filt = (int)s.filters.size();
     for (size_t f = 0; f < s.filters.size(); ++f) {
@@ -279,7 +281,10 @@ inline GQuery lower_gen(const LProgram& P, int qi, const Sizing& sz) {
   for (int s = 0; s < (int)P.stream_types.size() && s < GMAXSTREAM; ++s)
     for (int j = 0; j < g.n_cap[s]; ++j)
       if (g.cap_type[s][j] == T_LONG || g.cap_type[s][j] == T_DOUBLE) v32 = false;
-  make_layout(g.lay, S, sz.R, sz.N, sz.LC, NA, v32);
+  bool absent = false;  // absent states' scheduler queues hold up to one list's worth of times
+  for (int i = 0; i < S; ++i) absent |= q.st[i].kind == K_ABSENT;
+  if (absent && q.partition >= 0) throw LowerError("absent states inside a partition");
+  make_layout(g.lay, S, sz.R, sz.N, sz.LC, NA, v32, absent ? sz.LC : 0);
   lower_atoms_or_none(g);
   return g;
 }

@@ -55,7 +55,7 @@ enum { T_INT = 0, T_LONG, T_FLOAT, T_DOUBLE, T_BOOL, T_STRING };
 enum { OP_CONST = 1, OP_ATTR, OP_IS_NULL, OP_STREAM_IS_NULL, OP_CMP, OP_AND, OP_OR, OP_NOT, OP_ARITH };
 enum { CMP_EQ = 0, CMP_NE, CMP_GT, CMP_GE, CMP_LT, CMP_LE };
 enum { AR_ADD = 0, AR_SUB, AR_MUL, AR_DIV, AR_MOD };
-enum { K_STREAM = 0, K_COUNT, K_LOGICAL };
+enum { K_STREAM = 0, K_COUNT, K_LOGICAL, K_ABSENT };  // K_ABSENT: AbsentStreamPre/PostStateProcessor
 enum { L_AND = 0, L_OR };
 enum { Q_PATTERN = 0, Q_SEQUENCE };
 enum { R_SINGLE = 0, R_MULTI };
@@ -78,6 +78,8 @@ struct GState {
       this_last, has_selector;
   int32_t n_filt;
   int32_t fb[GMAXF], fe[GMAXF];   // filter code ranges
+  int32_t pad;
+  int64_t waiting;                // K_ABSENT: the 'for' time (ms)
 };
 
 // arena layout (word offsets; 32-bit and 64-bit arenas, lane-interleaved on the device)
@@ -89,6 +91,10 @@ struct GLayout {
   // pools beyond the LDS hot cache (R > 64 StateEvents or N > 64 * GMAXNU nodes): the used-bitmasks
   // stay in the arena (SU / NU words) and mark/sweep marks into o_mark (SU + NU words, 64-bit arena)
   int32_t SU, big, o_mark, pad;
+  // absent states' schedulers (TQ > 0 only for queries with absent states): per state a FIFO ring of
+  // notification times o_tq [state][TQ] and lastScheduledTime o_lst (64-bit arena), ring head /
+  // length o_tqh [state][2] (32-bit arena)
+  int32_t TQ, o_tq, o_lst, o_tqh;
 };
 
 // K_seq compare atoms: a state's filters as a conjunction of typed compares whose operands are a
@@ -298,7 +304,8 @@ KG_FN bool sp_true(const Val& v) { return !v.null && v.bits; }
 // ------------------------------------------------------------------------------------------
 // per-lane runtime over the instance arena
 // ------------------------------------------------------------------------------------------
-enum { FL_CHANGED = 1, FL_INIT = 2, FL_SUCCESS = 4, FL_SSRESET = 8, FL_RETURNED = 16, FL_ITER = 32 };
+enum { FL_CHANGED = 1, FL_INIT = 2, FL_SUCCESS = 4, FL_SSRESET = 8, FL_RETURNED = 16, FL_ITER = 32,
+       FL_INACTIVE = 64 /* an absent start state without every that has fired (`active = false`) */ };
 
 // The predicate bytecode's stack machine (ExpressionExecutor trees: executor/condition/**,
 // executor/math/**, VariableExpressionExecutor.java:45-47). Structure comes from q (wave-uniform on
@@ -450,6 +457,11 @@ struct Ctx {
   // CountPost does not walk it again; -1 = unknown
   int32_t cnt_tail = -1;
   int64_t cnt_len = 0;
+  // absent states: a timer of state timer_state is being processed (its matches are timer records,
+  // ordered by (timer_ts, query, timer_idx) before the triggering event's own matches)
+  bool in_timer = false;
+  int64_t timer_ts = 0;
+  int32_t timer_idx = 0;
 
 #ifdef KG_PROFILE  // host-only access census (tests/native, test infrastructure)
   int32_t& i32(int i) const { kg_prof_hit(lay, 0, i); return w32[(int64_t)i * stride]; }
@@ -489,6 +501,17 @@ struct Ctx {
     const int o = lay.o_ndval + n * lay.NA + j;
     if (lay.v32) i32(o) = (int32_t)v;
     else i64(o) = v;
+  }
+  // absent states' schedulers: FIFO ring of notification times, its head / length, lastScheduledTime
+  KG_FN int64_t& tq(int i, int k) const { return i64(lay.o_tq + i * lay.TQ + k); }
+  KG_FN int32_t& tq_head(int i) const { return i32(lay.o_tqh + 2 * i); }
+  KG_FN int32_t& tq_len(int i) const { return i32(lay.o_tqh + 2 * i + 1); }
+  KG_FN int64_t& lst(int i) const { return i64(lay.o_lst + i); }
+  KG_FN void notify_at(int i, int64_t t) {  // Scheduler.notifyAt:118-126 (toNotifyQueue.put)
+    const int n = tq_len(i);
+    if (n >= lay.TQ) { cap_fail(CAP_LIST); return; }
+    tq(i, (tq_head(i) + n) % lay.TQ) = t;
+    tq_len(i) = n + 1;
   }
   // used-bitmask words: the LDS hot cache for small pools, the arena itself for big ones (lay.big is
   // the template's, so the choice is wave-uniform)
@@ -666,7 +689,8 @@ struct Ctx {
   // ---- pre processors ----
   KG_FN void init_pre(int i) {  // StreamPreStateProcessor.init:157-166
     const GState& s = S(i);
-    if (s.is_start && (!(flags(i) & FL_INIT) || s.next_every >= 0)) {
+    const bool absent_next = q->type == Q_SEQUENCE && s.next_pre >= 0 && S(s.next_pre).kind == K_ABSENT;
+    if (s.is_start && (!(flags(i) & FL_INIT) || s.next_every >= 0 || absent_next)) {
       const int se = new_state();
       if (se < 0) return;
       add_state(i, se);
@@ -690,6 +714,16 @@ struct Ctx {
         } else {
           nae_push(i, se);
           nae_push(p, se);
+        }
+        break;
+      }
+      if (s.kind == K_ABSENT) {  // AbsentStreamPreStateProcessor.addState:78-101
+        if (flags(i) & FL_INACTIVE) break;
+        if (q->type == Q_SEQUENCE) nn(i) = 0;
+        nae_push(i, se);
+        if (!s.is_start) {
+          lst(i) = se_ts(se) + s.waiting;
+          notify_at(i, lst(i));
         }
         break;
       }
@@ -723,6 +757,10 @@ struct Ctx {
       return;
     }
     nae_push(i, c);
+    if (s.kind == K_ABSENT) {  // AbsentStreamPreStateProcessor.addEveryState:103-115
+      lst(i) = se_ts(se) + s.waiting;
+      notify_at(i, lst(i));
+    }
   }
   // updateState: StreamPre:281-289, CountPre:149-156, LogicalPre:118-130
   KG_FN void update_state(int i) {
@@ -755,7 +793,9 @@ struct Ctx {
       return;
     }
     pn(i) = 0;
-    if (s.is_start && nn(i) == 0) {
+    // AbsentStreamPreStateProcessor.resetState:117-138 re-inits a start state whatever its
+    // newAndEvery list holds
+    if (s.is_start && (s.kind == K_ABSENT || nn(i) == 0)) {
       if (q->type == Q_SEQUENCE && s.next_every < 0 && next_pending_nonempty(i)) return;
       init_pre(i);
     }
@@ -891,6 +931,18 @@ struct Ctx {
       if (S(s.partner).has_selector && s.this_last == s.partner) flags(s.partner) |= FL_RETURNED;
     }
   }
+  // AbsentStreamPostStateProcessor.process:31-52: the absent event arrived -- the partial is dropped
+  // and the waiting restarts from this event (AbsentStreamPre.updateLastArrivalTime:69-75)
+  KG_FN void absent_post(int i, int se) {
+    const GState& s = S(i);
+    flags(i) |= FL_CHANGED;
+    const int64_t t = nd_ts(slot(se, i));
+    se_ts(se) = t;
+    flags(i) |= FL_RETURNED;
+    if (s.is_start && s.next_every == i) add_every_state(i, se);
+    lst(i) = t + s.waiting;
+    notify_at(i, lst(i));
+  }
   KG_FN void process(int i, int se, bool deferred) {  // deferred: slot i holds VNODE
     flags(i) &= ~FL_CHANGED;
     if (!filters_pass(i, se)) return;
@@ -902,6 +954,7 @@ struct Ctx {
     }
     switch (S(i).kind) {
       case K_STREAM: stream_post(i, se); break;
+      case K_ABSENT: absent_post(i, se); break;
       case K_COUNT: count_post(i, se); break;
       default: logical_post(i, se); break;
     }
@@ -925,6 +978,7 @@ struct Ctx {
   // returns its ComplexEventChunk.
   KG_FN void process_and_return(int i) {
     const GState& s = S(i);
+    if (s.kind == K_ABSENT && (flags(i) & FL_INACTIVE)) return;  // AbsentStreamPre.processAndReturn:231-244
     flags(i) |= FL_ITER;
     int w = 0;
     const int nS_ = nS();
@@ -980,14 +1034,16 @@ struct Ctx {
       } else {
         slot(se, i) = VNODE;  // copied into the pool by process() once the filters pass
         process(i, se, true);
-        if (take_returned(i)) push_ret(se);
+        // an absent processor always returns an empty chunk
+        if (take_returned(i) && s.kind != K_ABSENT) push_ret(se);
         if (flags(i) & FL_CHANGED) {
           keep = false;
         } else {
           slot(se, i) = -1;
           if (q->type == Q_SEQUENCE) {
-            keep = false;
-            if (s.kind == K_STREAM && s.callback >= 0) start_state_reset(s.callback);
+            // removeOnNoStateChange: true for StreamPre, false for AbsentStreamPre (:246-248)
+            if (s.kind != K_ABSENT) keep = false;
+            if ((s.kind == K_STREAM || s.kind == K_ABSENT) && s.callback >= 0) start_state_reset(s.callback);
           }
         }
       }
@@ -1023,12 +1079,115 @@ struct Ctx {
   KG_FN void init_instance() {  // QueryRuntime.init -> node_init(0)
     for (int k = 0; k < q->n_init; ++k) init_pre(q->init_order[k]);
   }
+  // SiddhiAppRuntime.start -> AbsentStreamPreStateProcessor.start:276-286: start states with a
+  // 'for' time schedule their first check at the runtime's start time
+  KG_FN void start_instance(int64_t start_ts) {
+    if (lay.TQ == 0) return;
+    for (int i = 0; i < lay.S; ++i) {
+      const GState& s = S(i);
+      if (s.kind == K_ABSENT && s.is_start && s.waiting != -1 && !(flags(i) & FL_INACTIVE)) {
+        lst(i) = start_ts + s.waiting;
+        notify_at(i, lst(i));
+      }
+    }
+  }
+
+  // AbsentStreamPreStateProcessor.sendEvent:212-228
+  template <class Emit>
+  KG_FN void absent_send(int i, int se, Emit& em) {
+    const GState& s = S(i);
+    if (s.has_selector) em(*this, se);  // thisStatePostProcessor.nextProcessor: the selector
+    if (s.next_pre >= 0) add_state(s.next_pre, se);
+    if (s.next_every >= 0) add_every_state(s.next_every, se);
+    else if (s.is_start) flags(i) |= FL_INACTIVE;
+    if (s.callback >= 0) start_state_reset(s.callback);
+  }
+  // AbsentStreamPreStateProcessor.process:140-210: a timer event of state i's scheduler at time t
+  // (`actual`: the timestamp generator's time -- t itself, or in playback the event time that let
+  // the timer fire)
+  template <class Emit>
+  KG_FN void absent_timer(int i, int64_t t, int64_t actual, Emit& em) {
+    const GState& s = S(i);
+    if (flags(i) & FL_INACTIVE) return;
+    bool initialize = s.is_start && nn(i) == 0 && pn(i) == 0;
+    if (initialize && q->type == Q_SEQUENCE && s.next_every < 0 && lst(i) > 0) initialize = false;
+    if (initialize) {
+      const int se = new_state();
+      if (se < 0) return;
+      add_state(i, se);
+    } else if (q->type == Q_SEQUENCE && nn(i) > 0) {
+      reset_state(i);
+    }
+    update_state(i);
+    n_ret = 0;
+    int w = 0;
+    const int n0 = pn(i);
+    int k = 0;
+    for (; k < n0 && err == GE_OK; ++k) {
+      const int se = pl(i, k);
+      if (is_expired(i, se)) {  // (ts == t here)
+        if (s.within_every >= 0 && s.next_every != i) {
+          if (s.next_every < 0) { fail(GE_REFERENCE); continue; }  // NullPointerException
+          add_every_state(s.next_every, se);
+        }
+        continue;
+      }
+      const int64_t st = se_ts(se);
+      if ((st == -1 && t >= lst(i)) || (st != -1 && t >= st + s.waiting)) {
+        se_ts(se) = t;
+        push_ret(se);
+        continue;
+      }
+      pl(i, w++) = se;
+    }
+    for (; k < n0; ++k) pl(i, w++) = pl(i, k);  // not visited (error): kept
+    pn(i) = w;
+    if (s.within_every >= 0) update_state(s.within_every);
+    const bool not_processed = n_ret == 0;
+    for (int r = 0; r < n_ret && err == GE_OK; ++r) absent_send(i, ret[r], em);
+    n_ret = 0;
+    if (actual > s.waiting + t) lst(i) = actual + s.waiting;
+    if (not_processed && lst(i) < t) {
+      lst(i) = t + s.waiting;
+      notify_at(i, lst(i));
+    }
+  }
+  // Scheduler.sendTimerEvents:186-214 of every absent state of the instance up to time `upto`: the
+  // earliest queue head fires first (ties: lower state id). `playback`: the generator's time is
+  // `upto` while the timers fire; else each timer's own time.
+  template <class Emit>
+  KG_FN void fire_timers(int64_t upto, bool playback, Emit& em) {
+    if (lay.TQ == 0) return;
+    const int64_t ev_ts = ts;
+    for (;;) {
+      int bi = -1;
+      int64_t bt = 0;
+      for (int i = 0; i < lay.S; ++i) {
+        if (S(i).kind != K_ABSENT || tq_len(i) == 0) continue;
+        const int64_t h = tq(i, tq_head(i));
+        if (h > upto) continue;
+        if (bi < 0 || h < bt) {
+          bi = i;
+          bt = h;
+        }
+      }
+      if (bi < 0 || err != GE_OK) break;
+      tq_head(bi) = (tq_head(bi) + 1) % lay.TQ;
+      tq_len(bi) -= 1;
+      in_timer = true;
+      timer_ts = bt;
+      ts = bt;
+      absent_timer(bi, bt, playback ? upto : bt, em);
+      in_timer = false;
+    }
+    ts = ev_ts;
+  }
 };
 
 // ------------------------------------------------------------------------------------------
 // host-side layout of one query's arenas
 // ------------------------------------------------------------------------------------------
-inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA, bool v32 = false) {
+inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA, bool v32 = false, int TQ = 0) {
   L.S = S; L.R = R; L.N = N; L.LC = LC; L.NA = NA; L.NU = (N + 63) / 64;
   L.SU = (R + 63) / 64;
   L.big = (L.SU > 1 || L.NU > GMAXNU) ? 1 : 0;
@@ -1045,6 +1204,8 @@ inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA, bool v3
   L.o_ndnull = o; o += N;
   L.o_init = o; o += 1;
   if (v32) { L.o_ndval = o; o += N * NA; }
+  L.TQ = TQ;
+  L.o_tqh = o; o += TQ > 0 ? 2 * S : 0;
   L.n32 = o;
   o = 0;
   L.o_seused = o; o += L.SU;
@@ -1054,6 +1215,8 @@ inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA, bool v3
   L.o_ndseq = o; o += N;
   L.o_ndts = o; o += N;
   if (!v32) { L.o_ndval = o; o += N * NA; }
+  L.o_tq = o; o += S * TQ;
+  L.o_lst = o; o += TQ > 0 ? S : 0;
   L.n64 = o;
 }
 

@@ -52,6 +52,8 @@ __global__ __launch_bounds__(256) void append_ratchet_kernel(
     const int64_t w = word0 + (row - row0) * 4;
     T.hi[row] = hi_key(s, seq_ref, out_rank[(int64_t)q * n_streams + G->stream]);
     T.lo[0][row] = (uint64_t)s1;
+#pragma unroll
+    for (int k = 1; k < MAXLO; ++k) T.lo[k][row] = 0ull;
     T.seq[row] = s;
     T.q[row] = q;
     T.key[row] = -1;
@@ -102,13 +104,22 @@ __global__ __launch_bounds__(256) void append_gen_kernel(const int64_t* __restri
   if (i >= n_rec) return;
   const int64_t o = rec_off[i];
   const int64_t* r = out + o;
-  const int q = (int)r[1], stream = (int)(r[6] >> 16);
+  const int q = (int)r[1], stream = (int)((r[6] >> 16) & 0xFFFF);
   const int64_t row = row0 + i;
-  T.hi[row] = hi_key(r[4], seq_ref, out_rank[(int64_t)q * n_streams + stream]);
-  T.lo[0][row] = (uint64_t)r[5];
   T.seq[row] = r[4];
 #pragma unroll
-  for (int k = 1; k < MAXLO; ++k) T.lo[k][row] = 0ull;
+  for (int k = 2; k < MAXLO; ++k) T.lo[k][row] = 0ull;
+  if (stream == 0xFFFF) {
+    // an absent state's timer match (nfa_gen.hip): rank 0, before the trigger event's own matches;
+    // then by (timer time, query, fire ordinal) -- lo[1] is the more significant tiebreak
+    T.hi[row] = hi_key(r[4], seq_ref, 0);
+    T.lo[1][row] = (uint64_t)r[5] ^ 0x8000000000000000ull;
+    T.lo[0][row] = ((uint64_t)(uint32_t)q << 32) | (uint64_t)(uint32_t)(r[6] >> 32);
+  } else {
+    T.hi[row] = hi_key(r[4], seq_ref, out_rank[(int64_t)q * n_streams + stream]);
+    T.lo[0][row] = (uint64_t)r[5];
+    T.lo[1][row] = 0ull;
+  }
   T.q[row] = q;
   T.key[row] = r[2];
   T.ts[row] = r[3];

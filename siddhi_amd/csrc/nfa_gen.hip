@@ -48,7 +48,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   // wave-uniform shape template (scalar loads) + the lane's own query (constants)
   const kg::GQuery* __restrict__ q = L.queries + L.group_tmpl[L.group_base + g];
   const kg::GQuery* __restrict__ ql = L.queries + qi;
-  if (q->recv_n[L.b.stream] == 0) return;  // this query does not read the stream
+  // a query that does not read the stream still sees time pass if it has absent states
+  const bool reads = q->recv_n[L.b.stream] != 0;
+  if (!reads && q->lay.TQ == 0) return;
   int64_t block = L.block_base + (int64_t)kid * L.groups + g;
   int32_t* a32 = L.a32;
   int64_t* a64 = L.a64;
@@ -93,54 +95,71 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   const int64_t key = L.key_of_id ? L.key_of_id[kid] : -1;
   if (c.i32(q->lay.o_init) == 0) {  // PartitionRuntime.cloneIfNotExist / QueryRuntime.init: seed
     c.init_instance();
+    c.start_instance(L.start_ts);
     c.i32(q->lay.o_init) = 1;
   }
   LaneOut o{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
   const int S = q->n_states;
   const int ncap = q->n_cap[c.stream];
   unsigned long long nrec = 0;
+  int64_t idx = 0;
+  bool live = true;
+  // a match record [len, qid, key, ts, trigger seq, idx, S | stream << 16, (count, seqs...) x S];
+  // a timer's record carries stream 0xFFFF, the timer time in idx and its fire ordinal in bits 32+
+  auto emit = [&](const kg::Ctx& cx, int se) {
+    if (!live) return;
+    int words = 7;
+    for (int i = 0; i < S; ++i) {
+      words += 1;
+      for (int n = cx.slot(se, i); n >= 0; n = cx.nd_next(n)) ++words;
+    }
+    ++nrec;
+    if (!L.write_records) return;
+    int64_t* r = o.reserve(words);
+    if (!r) return;
+    r[0] = words;
+    r[1] = ql->qid;
+    r[2] = key;
+    r[3] = cx.se_ts(se);
+    r[4] = cx.seq;
+    if (cx.in_timer) {
+      r[5] = cx.timer_ts;
+      r[6] = S | (0xFFFFll << 16) | ((int64_t)c.timer_idx++ << 32);
+    } else {
+      r[5] = idx++;
+      r[6] = S | (c.stream << 16);
+    }
+    int w = 7;
+    for (int i = 0; i < S; ++i) {
+      const int cw = w++;
+      int64_t cnt = 0;
+      for (int n = cx.slot(se, i); n >= 0; n = cx.nd_next(n)) {
+        r[w++] = cx.nd_seq(n);
+        ++cnt;
+      }
+      r[cw] = cnt;
+    }
+  };
   for (int64_t k = w0; k < e1 && c.err == kg::GE_OK; ++k) {
-    const bool live = k >= e0;
+    live = k >= e0;
     const int64_t e = L.ev_idx ? L.ev_idx[k] : k;
     c.seq = L.b.seq_base + e;
     c.ts = L.b.ts[e];
+    idx = 0;
+    c.fire_timers(c.ts, L.playback != 0, emit);  // timers due by this event fire before it
+    if (!reads) continue;
     c.ev_null = 0;
     for (int j = 0; j < ncap; ++j) {  // the event is the same for every lane: identical LDS stores
       bool nl;
       evv[j] = raw_word(L.b, q->cap_attr[c.stream][j], e, nl);
       if (nl) c.ev_null |= 1u << j;
     }
-    int64_t idx = 0;
-    auto emit = [&](const kg::Ctx& cx, int se) {
-      if (!live) return;
-      int words = 7;
-      for (int i = 0; i < S; ++i) {
-        words += 1;
-        for (int n = cx.slot(se, i); n >= 0; n = cx.nd_next(n)) ++words;
-      }
-      ++nrec;
-      if (!L.write_records) return;
-      int64_t* r = o.reserve(words);
-      if (!r) return;
-      r[0] = words;
-      r[1] = ql->qid;
-      r[2] = key;
-      r[3] = cx.se_ts(se);
-      r[4] = cx.seq;
-      r[5] = idx++;
-      r[6] = S | (c.stream << 16);
-      int w = 7;
-      for (int i = 0; i < S; ++i) {
-        const int cw = w++;
-        int64_t cnt = 0;
-        for (int n = cx.slot(se, i); n >= 0; n = cx.nd_next(n)) {
-          r[w++] = cx.nd_seq(n);
-          ++cnt;
-        }
-        r[cw] = cnt;
-      }
-    };
     c.receive(emit);
+  }
+  if (L.advance_to != INT64_MIN && c.err == kg::GE_OK) {  // time passes after the batch
+    live = true;
+    c.seq = L.timer_seq;
+    c.fire_timers(L.advance_to, L.playback != 0, emit);
   }
   o.close();
   c.store_hot();
@@ -234,6 +253,15 @@ __global__ void gen_remap_kernel(const int32_t* __restrict__ lane_q, int group_b
   c64(a.o_ndts, b.o_ndts, a.N);
   if (a.v32) c32(a.o_ndval, b.o_ndval, a.N * a.NA);  // [node][attr]: same stride NA
   else c64(a.o_ndval, b.o_ndval, a.N * a.NA);
+  if (a.TQ > 0) {  // absent schedulers: each FIFO ring is written out from its head (head 0)
+    c64(a.o_lst, b.o_lst, S);
+    for (int i = 0; i < S; ++i) {
+      const int h = s32[(int64_t)(a.o_tqh + 2 * i) * 64], n = s32[(int64_t)(a.o_tqh + 2 * i + 1) * 64];
+      for (int k = 0; k < n; ++k) d64[(int64_t)(b.o_tq + i * b.TQ + k) * 64] = s64[(int64_t)(a.o_tq + i * a.TQ + (h + k) % a.TQ) * 64];
+      d32[(int64_t)(b.o_tqh + 2 * i) * 64] = 0;
+      d32[(int64_t)(b.o_tqh + 2 * i + 1) * 64] = n;
+    }
+  }
 }
 
 // ---- partition routing ----

@@ -257,6 +257,14 @@ struct GenLaunch {
   int64_t chunk_len;
   int32_t* s32;               // scratch arenas of chunks 1 .. ev_chunks-1
   int64_t* s64;
+  // absent states (kgen.h fire_timers): the runtime's start time (instances seeded now schedule
+  // their start checks from it), timers due up to each event fire before it, and after the last
+  // event those due up to advance_to (INT64_MIN: none; a time advance with no events)
+  int64_t start_ts;
+  int64_t advance_to;
+  int64_t timer_seq;          // trigger seq of the timers fired after the last event
+  int32_t playback;           // @app:playback: the generator's time is the event time while timers fire
+  int32_t pad_t;
 };
 
 // ------------------------------------------------------------------------------------------

@@ -19,6 +19,7 @@ SDH_OK = 0
 SDH_FLAG_DEVICE_MATCHES = 1
 SDH_FLAG_NO_RATCHET = 2
 SDH_FLAG_FORCE_GEN = 4
+SDH_FLAG_PLAYBACK = 8  # @app:playback timer semantics (include/siddhi_hip.h)
 ERRORS = {-1: "SDH_E_INVALID", -2: "SDH_E_UNSUPPORTED", -3: "SDH_E_DEVICE", -4: "SDH_E_CAPACITY",
           -5: "SDH_E_REFERENCE"}
 
@@ -57,7 +58,8 @@ class SdhStats(ctypes.Structure):
 
 
 EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engine_poll", "sdh_engine_poll_device",
-           "sdh_engine_pending_matches", "sdh_engine_stats", "sdh_engine_snapshot",
+           "sdh_engine_pending_matches", "sdh_engine_start", "sdh_engine_advance_time", "sdh_engine_stats",
+           "sdh_engine_snapshot",
            "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version"]
 
 _lib = None
@@ -80,6 +82,8 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_engine_poll.argtypes = [P, ctypes.POINTER(SdhMatches)]
     lib.sdh_engine_poll_device.argtypes = [P, ctypes.POINTER(SdhMatches)]
     lib.sdh_engine_pending_matches.argtypes = [P, ctypes.POINTER(ctypes.c_int64)]
+    lib.sdh_engine_start.argtypes = [P, ctypes.c_int64]
+    lib.sdh_engine_advance_time.argtypes = [P, ctypes.c_int64]
     lib.sdh_engine_stats.argtypes = [P, ctypes.POINTER(SdhStats)]
     lib.sdh_engine_snapshot.argtypes = [P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
     lib.sdh_engine_restore.argtypes = [P, ctypes.c_void_p, ctypes.c_size_t]
@@ -207,6 +211,14 @@ class HipEngine:
                 j += 1 + c
             out.append((int(q[i]), int(k[i]), int(ts[i]), tuple(slots)))
         return out
+
+    def start(self, t: int):
+        """SiddhiAppRuntime.start at time t (absent states schedule their first checks from it)."""
+        self._check(self.lib.sdh_engine_start(self.h, int(t)))
+
+    def advance_time(self, t: int):
+        """Time passes to t with no event: absent states' schedulers fire what falls due."""
+        self._check(self.lib.sdh_engine_advance_time(self.h, int(t)))
 
     def pending_matches(self) -> int:
         n = ctypes.c_int64()

@@ -108,3 +108,48 @@ def random_seq_app(seed):
         w = f" within {rng.choice([3, 10, 40])} milliseconds" if rng.random() < 0.5 else ""
         qs.append(f"@info(name='s{qn}') from {', '.join(parts)}{w} select e0.v as a, e{n - 1}.v as b insert into O;")
     return " ".join(qs)
+
+
+def random_absent_app(seed, n_queries=4):
+    """Unpartitioned patterns / sequences of 2-4 states with absent states (`not S[..] for T`, maybe
+    under `every`) at any position, over A and B (cross-references into earlier states, within)."""
+    rng = random.Random(seed)
+    qs = [STREAMS]
+    for qn in range(n_queries):
+        seq = rng.random() < 0.35
+        n = rng.randint(2, 4)
+        parts, aliases = [], []
+        absent_at = rng.randrange(n)
+        for i in range(n):
+            st = rng.choice("AB")
+            pred = _pred(rng, aliases, st)
+            if i == absent_at or (i > 0 and rng.random() < 0.15):
+                ab = f"not {st}[{pred}] for {rng.randint(2, 12)} milliseconds"
+                if rng.random() < 0.3 and (not seq or i == 0):  # sequences: `every` only at the start
+                    ab = "every " + ab
+                parts.append(ab)
+                continue
+            al = f"e{i}"
+            parts.append(f"{al}={st}[{pred}]")
+            aliases.append(al)
+        if not aliases:  # the selector needs a stream state
+            parts.append(f"e{n}={rng.choice('AB')}[v >= 0]")
+            aliases.append(f"e{n}")
+        if not parts[0].startswith("every") and rng.random() < 0.5:
+            parts[0] = "every " + parts[0]
+        w = f" within {rng.choice([8, 20, 60])} milliseconds" if rng.random() < 0.5 else ""
+        sep = ", " if seq else " -> "
+        qs.append(f"@info(name='a{qn}') from {sep.join(parts)}{w} "
+                  f"select {aliases[0]}.v as a, {aliases[-1]}.v as b insert into Out;")
+    return " ".join(qs)
+
+
+def random_timeline(seed, n=200):
+    """Events of random_events interleaved with time advances (the gaps a live runtime idles)."""
+    rng = np.random.default_rng(seed + 1000)
+    out = []
+    for stream, row, t in random_events(seed, n=n):
+        if rng.random() < 0.15:
+            out.append(("advance", None, t - 1 if t > 0 else 0))
+        out.append((stream, row, t))
+    return out

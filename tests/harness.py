@@ -46,6 +46,7 @@ def oracle_lib():
         lib.oracle_destroy.argtypes = [P]
         lib.oracle_start.argtypes = [P, I64]
         lib.oracle_advance_time.argtypes = [P, I64]
+        lib.oracle_set_playback.argtypes = [P, ctypes.c_int]
         _lib = lib
     return _lib
 
@@ -87,6 +88,9 @@ class OracleEngine:
                                   None if nl is None else nl.ctypes.data, int(as_chunk))
         if rc != 0:
             raise OracleError(self.lib.oracle_error(self.h).decode())
+
+    def set_playback(self, on: bool):
+        self.lib.oracle_set_playback(self.h, int(on))
 
     def start(self, t: int):
         if self.lib.oracle_start(self.h, int(t)) != 0:
@@ -141,6 +145,9 @@ class App:
         self.string_ids = [self.dictionary.intern(s) for s in self.ir.strings]
         self.blob = self.ir.serialize(self.string_ids)
         self.engine = (engine_factory or OracleEngine)(self.blob)
+        self.playback = bool(self.ast.annotations.get("app:playback"))
+        if self.playback and hasattr(self.engine, "set_playback"):
+            self.engine.set_playback(True)   # (the HIP engine takes SDH_FLAG_PLAYBACK at create)
         self.log = EventLog()
         self.matches: List[tuple] = []
 

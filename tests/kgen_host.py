@@ -33,6 +33,9 @@ def lib():
         L.kgh_error.argtypes = [P]
         L.kgh_error.restype = ctypes.c_char_p
         L.kgh_destroy.argtypes = [P]
+        L.kgh_start.argtypes = [P, I64]
+        L.kgh_set_playback.argtypes = [P, ctypes.c_int]
+        L.kgh_advance.argtypes = [P, I64, I64]
         _lib = L
     return _lib
 
@@ -56,6 +59,16 @@ class KGenHostEngine:
                                None if nl is None else nl.ctypes.data)
         self.seq += len(ts)
         if rc != 0:
+            raise RuntimeError(self.lib.kgh_error(self.h).decode())
+
+    def set_playback(self, on: bool):
+        self.lib.kgh_set_playback(self.h, int(on))
+
+    def start(self, t: int):
+        self.lib.kgh_start(self.h, int(t))
+
+    def advance_time(self, t: int):
+        if self.lib.kgh_advance(self.h, int(t), self.seq) != 0:
             raise RuntimeError(self.lib.kgh_error(self.h).decode())
 
     def take_matches(self, n_slots_of):

@@ -18,6 +18,7 @@ namespace {
 
 struct Rec {
   int64_t seq, rank, idx;
+  int64_t tts = 0;  // timer records (rank -1): the timer's time, ordered before idx
   int64_t query, key, ts;
   std::vector<std::vector<int64_t>> slots;
 };
@@ -25,6 +26,7 @@ struct Rec {
 struct Inst {
   int qi;
   int64_t key;
+  int64_t timer_idx = 0;  // fire ordinal of this instance's timer matches
   std::vector<int32_t> w32;
   std::vector<int64_t> w64;
   bool init = false;
@@ -41,6 +43,9 @@ struct Host {
   int64_t chunk_len = 0;  // >0: unpartitioned instances with a bounded look-back run event chunks
                           // like the device (kg::seq_lookback; nfa_gen.hip)
   bool window = false;    // unpartitioned K_seq-class instances evaluate event windows (kg::seq_match)
+  bool started = false;   // absent states: the runtime's start time, playback mode
+  int64_t start_ts = 0;
+  bool playback = false;
   // last events of each stream (window mode): ts, seq, raw attribute words, null flags
   struct Ev {
     int64_t ts, seq;
@@ -70,9 +75,10 @@ Inst* make_inst(Host* h, int qi, int64_t key) {
   return in;
 }
 
-// run one event through one instance (what one lane does for one event)
+// run one event through one instance (what one lane does for one event): the absent states'
+// timers due by the event fire first (nfa_gen.hip); event == false: only time passes, to `upto`
 void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* vals, const uint8_t* nulls,
-         bool live = true) {
+         bool live = true, bool event = true, int64_t upto = 0) {
   const GQuery& q = h->gq[in->qi];
   Ctx c{};
   c.bind(&q, &q);
@@ -100,13 +106,14 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
     c.ts = ts;
     c.stream = stream;
     c.init_instance();
+    c.start_instance(h->start_ts);
     in->init = true;
   }
   c.seq = seq;
-  c.ts = ts;
+  c.ts = event ? ts : upto;
   c.stream = stream;
   c.ev_null = 0;
-  for (int j = 0; j < q.n_cap[stream]; ++j) {
+  for (int j = 0; event && j < q.n_cap[stream]; ++j) {
     const int a = q.cap_attr[stream][j];
     evv[j] = vals[a];
     if (nulls && nulls[a]) c.ev_null |= 1u << j;
@@ -116,8 +123,14 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
     if (!live) return;  // look-back replay of an event chunk
     Rec r;
     r.seq = seq;
-    r.rank = h->rank[(size_t)in->qi * h->P.stream_types.size() + stream];
-    r.idx = idx++;
+    if (cx.in_timer) {
+      r.rank = -1;
+      r.tts = cx.timer_ts;
+      r.idx = in->timer_idx++;
+    } else {
+      r.rank = h->rank[(size_t)in->qi * h->P.stream_types.size() + stream];
+      r.idx = idx++;
+    }
     r.query = in->qi;
     r.key = in->key;
     r.ts = cx.se_ts(se);
@@ -128,11 +141,22 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
     }
     h->out.push_back(r);
   };
-  c.receive(emit);
+  c.fire_timers(event ? ts : upto, h->playback, emit);
+  if (event && c.err == GE_OK) c.receive(emit);
   c.store_hot();
   if (c.err == GE_CAPACITY)
     throw std::runtime_error("K_gen instance capacity exceeded (kinds " + std::to_string(c.capk) + ")");
   if (c.err == GE_REFERENCE) throw std::runtime_error("reference engine would throw here");
+}
+
+void sort_out(Host* h) {
+  std::stable_sort(h->out.begin(), h->out.end(), [](const Rec& a, const Rec& b) {
+    if (a.seq != b.seq) return a.seq < b.seq;
+    if (a.rank != b.rank) return a.rank < b.rank;
+    if (a.rank == -1 && a.tts != b.tts) return a.tts < b.tts;
+    if (a.rank == -1 && a.query != b.query) return a.query < b.query;
+    return a.idx < b.idx;
+  });
 }
 
 }  // namespace
@@ -165,6 +189,10 @@ int kgh_send(void* hp, int stream, int64_t n, int64_t seq0, const int64_t* ts, c
   Host* h = (Host*)hp;
   try {
     const size_t na = h->P.stream_types[stream].size();
+    if (!h->started && n > 0) {
+      h->started = true;
+      h->start_ts = ts[0];
+    }
     // every instance processes the whole batch (the device order), then matches are sorted
     std::vector<Host::Ev> win;  // this stream's tail ++ batch (window mode)
     if (h->window) {
@@ -247,11 +275,7 @@ int kgh_send(void* hp, int stream, int64_t n, int64_t seq0, const int64_t* ts, c
       const size_t keep = std::min<size_t>(win.size(), GMAXS - 1);
       h->tail[stream].assign(win.end() - keep, win.end());
     }
-    std::stable_sort(h->out.begin(), h->out.end(), [](const Rec& a, const Rec& b) {
-      if (a.seq != b.seq) return a.seq < b.seq;
-      if (a.rank != b.rank) return a.rank < b.rank;
-      return a.idx < b.idx;
-    });
+    sort_out(h);
     return 0;
   } catch (const std::exception& ex) {
     h->err = ex.what();
@@ -284,6 +308,28 @@ int kgh_get_matches(void* hp, int64_t* query, int64_t* key, int64_t* ts, int64_t
   return 0;
 }
 void kgh_clear(void* hp) { ((Host*)hp)->out.clear(); }
+void kgh_start(void* hp, int64_t t) {
+  ((Host*)hp)->started = true;
+  ((Host*)hp)->start_ts = t;
+}
+void kgh_set_playback(void* hp, int on) { ((Host*)hp)->playback = on != 0; }
+// time passes to t with no event (sdh_engine_advance_time): timer records get trigger seq `seq`
+int kgh_advance(void* hp, int64_t t, int64_t seq) {
+  Host* h = (Host*)hp;
+  try {
+    if (!h->started) {
+      h->started = true;
+      h->start_ts = t;
+    }
+    for (auto& in : h->top)
+      if (in && h->gq[in->qi].lay.TQ > 0) run(h, in.get(), 0, seq, t, nullptr, nullptr, true, false, t);
+    sort_out(h);
+    return 0;
+  } catch (const std::exception& ex) {
+    h->err = ex.what();
+    return -1;
+  }
+}
 void kgh_set_chunk(void* hp, int64_t len) { ((Host*)hp)->chunk_len = len; }
 void kgh_set_window(void* hp, int on) { ((Host*)hp)->window = on != 0; }
 const char* kgh_error(void* hp) { return ((Host*)hp)->err.c_str(); }

@@ -146,3 +146,47 @@ def test_kgen_host_seq_windows_c4():
         assert g.engine.take_matches(lambda q: 3) == om
         total += len(om)
     assert total > 1000
+
+
+# ---- absent patterns (kgen.h fire_timers / absent_timer) against the oracle ----
+from test_absent_kat import FIXTURES as ABSENT_FIXTURES, check_absent_rows, out_of_scope, \
+    run_absent_fixture  # noqa: E402
+
+ABSENT_IN_SCOPE = [f for f in ABSENT_FIXTURES if not out_of_scope(f)]
+
+
+@pytest.mark.parametrize("fx", ABSENT_IN_SCOPE, ids=[f["id"] for f in ABSENT_IN_SCOPE])
+def test_kgen_host_absent_kat(fx):
+    """The host build of the device interpreter runs the reference's absent-pattern timelines: the
+    same match tuples as the oracle, in the same order, and the reference's asserted counts/rows."""
+    o, _, _ = run_absent_fixture(fx)
+    g, rows, checks = run_absent_fixture(fx, engine_factory=lambda blob: KGenHostEngine(blob))
+    assert g.matches == o.matches
+    check_absent_rows(fx, rows, checks)
+
+
+def run_timeline(src, seed, engine_factory=None):
+    from fuzz_apps import random_timeline
+    app = App(src, engine_factory)
+    app.start(0)
+    for stream, row, t in random_timeline(seed):
+        if stream == "advance":
+            app.advance_time(t)
+        else:
+            app.send(stream, [row], [t])
+    return app
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_kgen_host_absent_fuzz(seed):
+    """Random absent patterns / sequences (any position, every, within, cross-references) over a
+    random timeline of events and idle time: the host build of the device interpreter emits the
+    oracle's matches in the oracle's order."""
+    from fuzz_apps import random_absent_app
+    src = random_absent_app(seed)
+    try:
+        o = run_timeline(src, seed)
+    except OracleError:
+        pytest.skip("the reference engine throws on this stream")
+    g = run_timeline(src, seed, engine_factory=lambda blob: KGenHostEngine(blob, R=4096, N=4096, LC=4096))
+    assert g.matches == o.matches
