@@ -480,6 +480,7 @@ struct Pre {
   i64 lastScheduledTime = 0;
   bool active = true;
   std::list<i64> timers;
+  i64 lastArrivalTime = 0;  // AbsentLogicalPreStateProcessor.java:42
 };
 struct Post {
   bool isEventReturned = false;
@@ -498,13 +499,18 @@ struct Runtime {
 
   size_t nslots() const { return q->states.size(); }
   const StateDef& S(int i) const { return q->states[i]; }
+  // an absent side of a logical state (AbsentLogicalPre/PostStateProcessor); IR waiting_ms -2 is
+  // `and not B` without 'for' (the reference's waitingTime -1)
+  bool absentL(int i) const { return S(i).kind == K_LOGICAL && S(i).waiting != -1; }
+  i64 W(int i) const { return S(i).waiting == -2 ? -1 : S(i).waiting; }
+  bool absentAny(int i) const { return S(i).kind == K_ABSENT || absentL(i); }
 
   // ---- pre processors -----------------------------------------------------------------------
   // StreamPreStateProcessor.init():157-166 (a SEQUENCE start whose next state is absent re-inits too)
   void init_pre(int i) {
     const StateDef& s = S(i);
     Pre& p = pres[i];
-    const bool absent_next = q->type == Q_SEQUENCE && s.next_pre >= 0 && S(s.next_pre).kind == K_ABSENT;
+    const bool absent_next = q->type == Q_SEQUENCE && s.next_pre >= 0 && absentAny(s.next_pre);
     if (s.is_start && (!p.initialized || s.next_every >= 0 || absent_next)) {
       StateEvent* se = new_state();
       addState(i, se);
@@ -519,6 +525,7 @@ struct Runtime {
     const StateDef& s = S(i);
     Pre& p = pres[i];
     if (s.kind == K_LOGICAL) {
+      if (absentL(i) && !p.active) return;  // AbsentLogicalPreStateProcessor.addState:64-86
       Pre& pp = pres[s.partner];
       if (s.is_start || q->type == Q_SEQUENCE) {
         if (p.newAndEvery.empty()) p.newAndEvery.push_back(se);
@@ -526,6 +533,10 @@ struct Runtime {
       } else {
         p.newAndEvery.push_back(se);
         pp.newAndEvery.push_back(se);
+      }
+      if (absentL(i) && !s.is_start && W(i) != -1) {
+        p.timers.push_back(se->ts + W(i));
+        if (absentL(s.partner)) pp.timers.push_back(se->ts + W(s.partner));
       }
       return;
     }
@@ -553,6 +564,8 @@ struct Runtime {
     const StateDef& s = S(i);
     StateEvent* c = clone(se);
     if (s.kind == K_LOGICAL) {
+      // AbsentLogicalPreStateProcessor.addEveryState:89-100 keeps the time of its own last event
+      if (absentL(i) && c->slots[i]) c->ts = c->slots[i]->ts;
       c->slots[i] = nullptr;
       pres[i].newAndEvery.push_back(c);
       c->slots[s.partner] = nullptr;
@@ -685,8 +698,15 @@ struct Runtime {
   // LogicalPostStateProcessor.process:59-87
   void logicalPost(int i, StateEvent* se) {
     const StateDef& s = S(i);
+    if (absentL(i)) {  // AbsentLogicalPostStateProcessor.process:37-49
+      pres[i].stateChanged = true;
+      posts[i].isEventReturned = true;
+      pres[i].lastArrivalTime = se->slots[i]->ts;  // updateLastArrivalTime
+      return;
+    }
     if (s.ltype == L_AND) {
-      if (se->slots[s.partner] != nullptr) streamPost(i, se);
+      const bool go = absentL(s.partner) ? partnerCanProceed(s.partner, se) : se->slots[s.partner] != nullptr;
+      if (go) streamPost(i, se);
       else pres[i].stateChanged = true;
     } else {
       streamPost(i, se);
@@ -712,6 +732,28 @@ struct Runtime {
   void absentSend(int i, StateEvent* se);
   // AbsentStreamPreStateProcessor.process:140-210: a timer event of this processor's scheduler
   void absentTimer(int i, i64 currentTime, i64 actualCurrentTime);
+
+  // AbsentLogicalPreStateProcessor.partnerCanProceed:342-372 (asked by the partner's AND post)
+  bool partnerCanProceed(int j, StateEvent* se) {
+    const StateDef& a = S(j);
+    Pre& pa = pres[j];
+    if (q->type == Q_SEQUENCE && a.next_every < 0 && pa.lastArrivalTime > 0) return false;
+    if (W(j) == -1) {
+      if (a.next_every < 0) return se->slots[j] == nullptr;
+      if (pa.lastArrivalTime > 0) {
+        pa.lastArrivalTime = 0;
+        init_pre(j);
+        return false;
+      }
+      return true;
+    }
+    return se->slots[j] != nullptr;
+  }
+  // StateEvent.addEvent:212-222 with StreamEventPool.borrowEvent()'s empty event (no data, ts -1)
+  void addDummyEvent(StateEvent* se, int i);
+  void absentLogicalSend(int i, StateEvent* se);                        // :225-244
+  void absentLogicalTimer(int i, i64 currentTime, i64 actualCurrentTime);  // :107-181
+  std::vector<StateEvent*> absentLogicalProcessAndReturn(int i, i64 seq, i64 ts);  // :246-300
 
   // ---- processAndReturn -----------------------------------------------------------------------
   std::vector<StateEvent*> processAndReturn(int i, i64 seq, i64 ts);
@@ -780,6 +822,8 @@ struct Engine {
           p.lastScheduledTime = t + s.waiting;
           p.timers.push_back(p.lastScheduledTime);
         }
+        // AbsentLogicalPreStateProcessor.start:320-330
+        if (r->absentL((int)i) && s.is_start && r->W((int)i) != -1 && p.active) p.timers.push_back(t + r->W((int)i));
       }
     }
   }
@@ -808,7 +852,8 @@ struct Engine {
         if (!best) break;
         best->pres[bi].timers.pop_front();
         now = bt;
-        best->absentTimer(bi, bt, playback ? t : bt);
+        if (best->absentL(bi)) best->absentLogicalTimer(bi, bt, playback ? t : bt);
+        else best->absentTimer(bi, bt, playback ? t : bt);
       }
     }
     if (t > now) now = t;
@@ -854,6 +899,12 @@ struct Engine {
 
 StateEvent* Runtime::new_state() { return eng->heap.state(nslots()); }
 
+void Runtime::addDummyEvent(StateEvent* se, int i) {
+  StreamEvent* ev = eng->heap.copy(-1, -1);
+  if (!se->slots[i]) se->slots[i] = ev;
+  else { StreamEvent* t = se->slots[i]; while (t->next) t = t->next; t->next = ev; }
+}
+
 StateEvent* Runtime::clone(StateEvent* se) {
   StateEvent* c = eng->heap.state(nslots());
   c->slots = se->slots;
@@ -886,6 +937,7 @@ std::vector<StateEvent*> Runtime::processAndReturn(int i, i64 seq, i64 ts) {
   const StateDef& s = S(i);
   Pre& p = pres[i];
   if (s.kind == K_ABSENT && !p.active) return ret;  // AbsentStreamPreStateProcessor.processAndReturn:231-244
+  if (absentL(i)) return absentLogicalProcessAndReturn(i, seq, ts);
   p.iterating = true;
   for (auto it = p.pending.begin(); it != p.pending.end();) {
     StateEvent* se = *it;
@@ -969,6 +1021,115 @@ void Runtime::absentSend(int i, StateEvent* se) {
   if (s.next_every >= 0) addEveryState(s.next_every, se);
   else if (s.is_start) pres[i].active = false;
   if (s.callback >= 0) startStateReset(s.callback);
+}
+
+void Runtime::absentLogicalSend(int i, StateEvent* se) {
+  const StateDef& s = S(i);
+  if (s.has_selector) eng->emit(this, se);
+  if (s.next_pre >= 0) addState(s.next_pre, se);
+  if (s.next_every >= 0) {
+    addEveryState(s.next_every, se);
+  } else if (s.is_start) {
+    pres[i].active = false;
+    if (s.ltype == L_OR && absentL(s.partner)) pres[s.partner].active = false;
+  }
+  if (s.callback >= 0) startStateReset(s.callback);
+}
+
+void Runtime::absentLogicalTimer(int i, i64 currentTime, i64 actualCurrentTime) {
+  const StateDef& s = S(i);
+  Pre& p = pres[i];
+  const i64 w = W(i);
+  if (!p.active) return;
+  bool notProcessed = true;
+  if (currentTime >= p.lastArrivalTime + w) {
+    std::vector<StateEvent*> ret;
+    if (s.is_start && q->type == Q_SEQUENCE && p.newAndEvery.empty() && p.pending.empty()) {
+      addState(i, new_state());
+    } else if (q->type == Q_SEQUENCE && !p.newAndEvery.empty()) {
+      resetState(i);
+    }
+    updateState(i);
+    for (auto it = p.pending.begin(); it != p.pending.end();) {
+      StateEvent* se = *it;
+      if (isExpired(i, se, currentTime)) {
+        it = p.pending.erase(it);
+        if (s.within_every >= 0) {
+          addEveryState(s.within_every, se);
+          updateState(s.within_every);
+        }
+        continue;
+      }
+      // waitingTimePassed:184-192
+      const bool passed = se->slots[i] == nullptr ? currentTime >= se->ts + w : currentTime >= se->slots[i]->ts + w;
+      if (!passed) { ++it; continue; }
+      it = p.pending.erase(it);
+      const bool partner = se->slots[s.partner] != nullptr;
+      if (s.ltype == L_OR && !partner) {
+        addDummyEvent(se, i);
+        ret.push_back(se);
+      } else if (s.ltype == L_AND && partner) {
+        ret.push_back(se);
+      } else if (s.ltype == L_AND && !partner) {
+        addDummyEvent(se, i);  // the partner may still proceed
+      }
+    }
+    notProcessed = ret.empty();
+    for (StateEvent* se : ret) absentLogicalSend(i, se);
+    p.lastArrivalTime = 0;
+  }
+  if (s.next_every >= 0 || (notProcessed && s.is_start)) {
+    const i64 nextBreak = p.lastArrivalTime == 0 ? actualCurrentTime + w : p.lastArrivalTime + w;
+    p.timers.push_back(nextBreak);
+  }
+}
+
+std::vector<StateEvent*> Runtime::absentLogicalProcessAndReturn(int i, i64 seq, i64 ts) {
+  const StateDef& s = S(i);
+  Pre& p = pres[i];
+  if (!p.active) return {};
+  p.iterating = true;
+  for (auto it = p.pending.begin(); it != p.pending.end();) {
+    StateEvent* se = *it;
+    if (isExpired(i, se, ts)) {
+      if (s.within_every >= 0) {
+        addEveryState(s.within_every, se);
+        updateState(s.within_every);
+      }
+      it = p.pending.erase(it);
+      continue;
+    }
+    if (s.ltype == L_OR && se->slots[s.partner] != nullptr) {
+      it = p.pending.erase(it);
+      continue;
+    }
+    StreamEvent* cur = se->slots[i];
+    se->slots[i] = eng->heap.copy(seq, ts);
+    process(i, se);
+    if (W(i) != -1 || (q->type == Q_SEQUENCE && s.ltype == L_AND && s.next_every >= 0)) se->slots[i] = cur;
+    bool removed = false;
+    if (posts[s.this_last].isEventReturned) {
+      posts[s.this_last].isEventReturned = false;
+      it = p.pending.erase(it);  // no longer an absent candidate
+      removed = true;
+      if (q->type == Q_SEQUENCE) {
+        auto& pp = pres[s.partner].pending;
+        for (auto jt = pp.begin(); jt != pp.end(); ++jt)
+          if (*jt == se) { pp.erase(jt); break; }
+      }
+    }
+    if (!p.stateChanged) {
+      se->slots[i] = cur;
+      if (q->type == Q_SEQUENCE) {
+        if (removed) throw std::runtime_error("IllegalStateException (double iterator.remove)");
+        it = p.pending.erase(it);
+        removed = true;
+      }
+    }
+    if (!removed) ++it;
+  }
+  p.iterating = false;
+  return {};
 }
 
 void Runtime::absentTimer(int i, i64 currentTime, i64 actualCurrentTime) {
@@ -1134,7 +1295,7 @@ int oracle_create(const void* blob, size_t len, OracleEngine** out) {
     e->part_inst.resize(e->prog.parts.size());
     e->key_order.resize(e->prog.parts.size());
     for (const auto& q : e->prog.queries)
-      for (const auto& st : q.states) e->has_absent |= st.kind == K_ABSENT;
+      for (const auto& st : q.states) e->has_absent |= st.kind == K_ABSENT || (st.kind == K_LOGICAL && st.waiting != -1);
     *out = e;
     return 0;
   } catch (const std::exception& ex) {

@@ -1303,6 +1303,8 @@ KPart kpart_shape(const kg::LProgram& P, int qi, const kg::GQuery& g) {
   KPart k;
   const kg::LQuery& q = P.q[qi];
   if (q.partition < 0 || q.type != kg::Q_PATTERN || q.st.size() != 3) return k;
+  for (const auto& x : q.st)
+    if (x.waiting != -1) return k;  // absent sides run on K_gen
   // start ids exist only with `within` (StateInputStreamParser.java:126-138): then e1 alone
   if (!(q.start_ids.empty() || (q.start_ids.size() == 1 && q.start_ids[0] == 0)) || g.max_depth > kg::RSTACK) return k;
   if (q.start_ids.empty() && q.within >= 0) return k;
@@ -2118,7 +2120,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   if (errs[1]) throw Error(SDH_E_REFERENCE, "the reference engine would throw on this stream "
                                             "(ConcurrentModification / IllegalState / NullPointer)");
   if (errs[0]) throw Error(SDH_E_CAPACITY, (errs[0] & kg::CAP_FIXED)
-                                               ? "K_gen compiled-in limit exceeded (GC pins or matches per processAndReturn)"
+                                               ? "K_gen compiled-in limit exceeded (GC pin depth)"
                                                : "K_gen instance pools could not grow further (4096 StateEvents / nodes per "
                                                  "instance, or device memory)");
   if (!any) nrec = used = 0;

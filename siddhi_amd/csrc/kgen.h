@@ -43,7 +43,6 @@ constexpr int GMAXCODE = 192;    // bytecode instructions per query
 constexpr int GMAXNA = 8;        // captured attributes per node (per stream)
 constexpr int GMAXSTREAM = 8;    // streams a query may read
 constexpr int GSTACK = 12;       // bytecode evaluation stack
-constexpr int GMAXRET = 64;      // matches one processAndReturn may return
 constexpr int GMAXNU = 4;        // node used-bitmask words the LDS hot cache holds (small pools)
 constexpr int GMAXPOOL = 4096;   // StateEvents / nodes per instance after growth (record <= ring margin)
 // the current event, not yet copied into the node pool: a stream / logical state's slot holds it
@@ -63,7 +62,7 @@ enum { R_SINGLE = 0, R_MULTI };
 // error codes (per lane, first one wins)
 enum { GE_OK = 0, GE_CAPACITY = 1, GE_REFERENCE = 2 };
 // capacity kinds: the pools and lists grow (the engine re-lays the arenas and re-runs the push);
-// CAP_FIXED limits (GC pins, matches one processAndReturn returns) are compiled in
+// CAP_FIXED: the GC pin stack depth (4) is compiled in
 enum { CAP_STATES = 1, CAP_NODES = 2, CAP_LIST = 4, CAP_FIXED = 8 };
 
 struct GInsn {
@@ -95,6 +94,7 @@ struct GLayout {
   // notification times o_tq [state][TQ] and lastScheduledTime o_lst (64-bit arena), ring head /
   // length o_tqh [state][2] (32-bit arena)
   int32_t TQ, o_tq, o_lst, o_tqh;
+  int32_t o_ret, pad2;  // the partials one processAndReturn / timer returns (LC entries: they grow with the lists)
 };
 
 // K_seq compare atoms: a state's filters as a conjunction of typed compares whose operands are a
@@ -451,14 +451,13 @@ struct Ctx {
   // GC roots outside the lists: partials unlinked or not yet linked while they are worked on
   int32_t* pins;  // [4] (stride hstride: LDS on the device)
   int32_t npin;
-  int32_t* ret;   // [GMAXRET]
-  int32_t n_ret;
+  int32_t n_ret;  // partials returned so far (arena ret_at: GC roots until handed on)
   // the count state's chain as process_and_return just extended it (its last node and length), so
   // CountPost does not walk it again; -1 = unknown
   int32_t cnt_tail = -1;
   int64_t cnt_len = 0;
-  // absent states: a timer of state timer_state is being processed (its matches are timer records,
-  // ordered by (timer_ts, query, timer_idx) before the triggering event's own matches)
+  // absent states: a timer is being processed (its matches are timer records, ordered by (timer_ts =
+  // the running max of the times fired so far, query, timer_idx) before the triggering event's own)
   bool in_timer = false;
   int64_t timer_ts = 0;
   int32_t timer_idx = 0;
@@ -472,6 +471,11 @@ struct Ctx {
 #endif
   KG_FN const GState& S(int i) const { return q->st[i]; }
   KG_FN int nS() const { return lay.S; }
+  // an absent side of a logical state (AbsentLogicalPre/PostStateProcessor); waiting -2 is a side
+  // without 'for' (the reference's waitingTime -1)
+  KG_FN bool absent_l(int i) const { return S(i).kind == K_LOGICAL && S(i).waiting != -1; }
+  KG_FN int64_t wait_of(int i) const { return S(i).waiting == -2 ? -1 : S(i).waiting; }
+  KG_FN bool absent_any(int i) const { return S(i).kind == K_ABSENT || absent_l(i); }
   KG_FN void bind(const GQuery* tmpl, const GQuery* own) {
     q = tmpl;
     ql = own;
@@ -507,6 +511,7 @@ struct Ctx {
   KG_FN int32_t& tq_head(int i) const { return i32(lay.o_tqh + 2 * i); }
   KG_FN int32_t& tq_len(int i) const { return i32(lay.o_tqh + 2 * i + 1); }
   KG_FN int64_t& lst(int i) const { return i64(lay.o_lst + i); }
+  KG_FN int32_t& ret_at(int k) const { return i32(lay.o_ret + k); }
   KG_FN void notify_at(int i, int64_t t) {  // Scheduler.notifyAt:118-126 (toNotifyQueue.put)
     const int n = tq_len(i);
     if (n >= lay.TQ) { cap_fail(CAP_LIST); return; }
@@ -586,7 +591,7 @@ struct Ctx {
       for (int k = 0; k < nn(i); ++k) mark_se(nl(i, k), m);
     }
     for (int k = 0; k < npin && k < 4; ++k) mark_se(pins[(int64_t)k * hstride], m);
-    for (int k = 0; k < n_ret; ++k) mark_se(ret[k], m);
+    for (int k = 0; k < n_ret; ++k) mark_se(ret_at(k), m);
   }
   KG_FN void gc() {
     KG_PHASE(1);
@@ -671,6 +676,31 @@ struct Ctx {
     return n;
   }
 
+  // StreamEventPool.borrowEvent()'s empty event (no data, timestamp -1) appended to slot i's chain
+  // (StateEvent.addEvent:212-222): an absent logical side whose wait has passed
+  KG_FN void add_dummy(int se, int i) {
+    pin(se);
+    int n = find_free_nd();
+    if (n < 0) {
+      gc();
+      n = find_free_nd();
+    }
+    unpin();
+    if (n < 0) { cap_fail(CAP_NODES); return; }
+    nd_used(n >> 6) = (int64_t)((uint64_t)nd_used(n >> 6) | (1ull << (n & 63)));
+    nd_seq(n) = -1;
+    nd_ts(n) = -1;
+    nd_next(n) = -1;
+    nd_null(n) = -1;  // every attribute null
+    if (slot(se, i) < 0) {
+      slot(se, i) = n;
+    } else {
+      int t = slot(se, i);
+      while (nd_next(t) >= 0) t = nd_next(t);
+      nd_next(t) = n;
+    }
+  }
+
   // ---- lists ----
   KG_FN void nae_push(int i, int se) {
     if (nn(i) >= lay.LC) { cap_fail(CAP_LIST); return; }
@@ -689,7 +719,7 @@ struct Ctx {
   // ---- pre processors ----
   KG_FN void init_pre(int i) {  // StreamPreStateProcessor.init:157-166
     const GState& s = S(i);
-    const bool absent_next = q->type == Q_SEQUENCE && s.next_pre >= 0 && S(s.next_pre).kind == K_ABSENT;
+    const bool absent_next = q->type == Q_SEQUENCE && s.next_pre >= 0 && absent_any(s.next_pre);
     if (s.is_start && (!(flags(i) & FL_INIT) || s.next_every >= 0 || absent_next)) {
       const int se = new_state();
       if (se < 0) return;
@@ -708,12 +738,17 @@ struct Ctx {
       const GState& s = S(i);
       if (s.kind == K_LOGICAL) {
         const int p = s.partner;
+        if (absent_l(i) && (flags(i) & FL_INACTIVE)) break;  // AbsentLogicalPre.addState:64-86
         if (s.is_start || q->type == Q_SEQUENCE) {
           if (nn(i) == 0) nae_push(i, se);
           if (nn(p) == 0) nae_push(p, se);
         } else {
           nae_push(i, se);
           nae_push(p, se);
+        }
+        if (absent_l(i) && !s.is_start && wait_of(i) != -1) {
+          notify_at(i, se_ts(se) + wait_of(i));
+          if (absent_l(p)) notify_at(p, se_ts(se) + wait_of(p));
         }
         break;
       }
@@ -750,6 +785,8 @@ struct Ctx {
     const int c = clone(se);
     if (c < 0) return;
     if (s.kind == K_LOGICAL) {
+      // AbsentLogicalPreStateProcessor.addEveryState:89-100 keeps the time of its own last event
+      if (absent_l(i) && slot(c, i) >= 0) se_ts(c) = nd_ts(slot(c, i));
       slot(c, i) = -1;
       nae_push(i, c);
       slot(c, s.partner) = -1;
@@ -921,10 +958,32 @@ struct Ctx {
       if (n == s.max) flags(i) |= FL_CHANGED;
     }
   }
+  // AbsentLogicalPreStateProcessor.partnerCanProceed:342-372 (asked by the partner's AND post)
+  KG_FN bool partner_can_proceed(int j, int se) {
+    const GState& a = S(j);
+    if (q->type == Q_SEQUENCE && a.next_every < 0 && lst(j) > 0) return false;
+    if (wait_of(j) == -1) {
+      if (a.next_every < 0) return slot(se, j) < 0;
+      if (lst(j) > 0) {
+        lst(j) = 0;
+        init_pre(j);
+        return false;
+      }
+      return true;
+    }
+    return slot(se, j) >= 0;
+  }
   KG_FN void logical_post(int i, int se) {  // LogicalPostStateProcessor.process:59-87
     const GState& s = S(i);
+    if (absent_l(i)) {  // AbsentLogicalPostStateProcessor.process:37-49 (lst = lastArrivalTime)
+      flags(i) |= FL_CHANGED;
+      flags(i) |= FL_RETURNED;
+      lst(i) = nd_ts(slot(se, i));
+      return;
+    }
     if (s.ltype == L_AND) {
-      if (slot(se, s.partner) >= 0) stream_post(i, se);
+      const bool go = absent_l(s.partner) ? partner_can_proceed(s.partner, se) : slot(se, s.partner) >= 0;
+      if (go) stream_post(i, se);
       else flags(i) |= FL_CHANGED;
     } else {
       stream_post(i, se);
@@ -969,8 +1028,65 @@ struct Ctx {
     return false;
   }
   KG_FN void push_ret(int se) {
-    if (n_ret >= GMAXRET) { cap_fail(CAP_FIXED); return; }
-    ret[n_ret++] = se;
+    if (n_ret >= lay.LC) { cap_fail(CAP_LIST); return; }
+    ret_at(n_ret++) = se;
+  }
+
+  // AbsentLogicalPreStateProcessor.processAndReturn:246-300: an arriving event of the absent side
+  // marks the partial (its lastArrivalTime moves); the chunk returned is always empty
+  KG_FN void absent_logical_par(int i) {
+    const GState& s = S(i);
+    if (flags(i) & FL_INACTIVE) return;
+    flags(i) |= FL_ITER;
+    int w = 0;
+    const int n0 = pn(i);
+    int k = 0;
+    for (; k < n0 && err == GE_OK; ++k) {
+      const int se = pl(i, k);
+      pin(se);
+      bool keep = true;
+      if (is_expired(i, se)) {
+        keep = false;
+        if (s.within_every >= 0) {
+          add_every_state(s.within_every, se);
+          update_state(s.within_every);
+        }
+      } else if (s.ltype == L_OR && slot(se, s.partner) >= 0) {
+        keep = false;
+      } else {
+        const int cur = slot(se, i);
+        slot(se, i) = VNODE;  // copied into the pool by process() once the filters pass
+        process(i, se, true);
+        if (wait_of(i) != -1 || (q->type == Q_SEQUENCE && s.ltype == L_AND && s.next_every >= 0)) slot(se, i) = cur;
+        bool removed = false;
+        if (take_returned(i)) {  // no longer an absent candidate
+          keep = false;
+          removed = true;
+          if (q->type == Q_SEQUENCE) remove_first(s.partner, se);
+        }
+        if (!(flags(i) & FL_CHANGED)) {
+          slot(se, i) = cur;
+          if (q->type == Q_SEQUENCE) {
+            if (removed) fail(GE_REFERENCE);  // IllegalStateException (second iterator.remove)
+            keep = false;
+          }
+        }
+      }
+      unpin();
+      if (keep) pl(i, w++) = se;
+    }
+    for (; k < n0; ++k) pl(i, w++) = pl(i, k);  // not visited (error): kept
+    pn(i) = w;
+    flags(i) &= ~FL_ITER;
+  }
+  KG_FN void remove_first(int j, int se) {  // pendingStateEventList.remove(Object)
+    const int n = pn(j);
+    for (int k = 0; k < n; ++k)
+      if (pl(j, k) == se) {
+        for (int m = k + 1; m < n; ++m) pl(j, m - 1) = pl(j, m);
+        pn(j) = n - 1;
+        return;
+      }
   }
 
   // processAndReturn: StreamPre:292-337, CountPre:53-93, LogicalPre:133-178. Emitted partials
@@ -979,6 +1095,7 @@ struct Ctx {
   KG_FN void process_and_return(int i) {
     const GState& s = S(i);
     if (s.kind == K_ABSENT && (flags(i) & FL_INACTIVE)) return;  // AbsentStreamPre.processAndReturn:231-244
+    if (absent_l(i)) { absent_logical_par(i); return; }
     flags(i) |= FL_ITER;
     int w = 0;
     const int nS_ = nS();
@@ -1072,7 +1189,7 @@ struct Ctx {
     for (int k = np - 1; k >= 0 && err == GE_OK; --k) {  // reverse registration order
       n_ret = 0;
       process_and_return(q->recv_procs[sidx][k]);
-      for (int r = 0; r < n_ret; ++r) em(*this, ret[r]);
+      for (int r = 0; r < n_ret; ++r) em(*this, ret_at(r));
       n_ret = 0;
     }
   }
@@ -1089,6 +1206,8 @@ struct Ctx {
         lst(i) = start_ts + s.waiting;
         notify_at(i, lst(i));
       }
+      // AbsentLogicalPreStateProcessor.start:320-330
+      if (absent_l(i) && s.is_start && wait_of(i) != -1 && !(flags(i) & FL_INACTIVE)) notify_at(i, start_ts + wait_of(i));
     }
   }
 
@@ -1144,13 +1263,83 @@ struct Ctx {
     pn(i) = w;
     if (s.within_every >= 0) update_state(s.within_every);
     const bool not_processed = n_ret == 0;
-    for (int r = 0; r < n_ret && err == GE_OK; ++r) absent_send(i, ret[r], em);
+    for (int r = 0; r < n_ret && err == GE_OK; ++r) absent_send(i, ret_at(r), em);
     n_ret = 0;
     if (actual > s.waiting + t) lst(i) = actual + s.waiting;
     if (not_processed && lst(i) < t) {
       lst(i) = t + s.waiting;
       notify_at(i, lst(i));
     }
+  }
+  // AbsentLogicalPreStateProcessor.sendEvent:225-244
+  template <class Emit>
+  KG_FN void absent_logical_send(int i, int se, Emit& em) {
+    const GState& s = S(i);
+    if (s.has_selector) em(*this, se);
+    if (s.next_pre >= 0) add_state(s.next_pre, se);
+    if (s.next_every >= 0) {
+      add_every_state(s.next_every, se);
+    } else if (s.is_start) {
+      flags(i) |= FL_INACTIVE;
+      if (s.ltype == L_OR && absent_l(s.partner)) flags(s.partner) |= FL_INACTIVE;
+    }
+    if (s.callback >= 0) start_state_reset(s.callback);
+  }
+  // AbsentLogicalPreStateProcessor.process:107-181: a timer of logical side i at time t
+  template <class Emit>
+  KG_FN void absent_logical_timer(int i, int64_t t, int64_t actual, Emit& em) {
+    const GState& s = S(i);
+    if (flags(i) & FL_INACTIVE) return;
+    const int64_t w = wait_of(i);
+    bool not_processed = true;
+    if (t >= lst(i) + w) {
+      if (s.is_start && q->type == Q_SEQUENCE && nn(i) == 0 && pn(i) == 0) {
+        const int se = new_state();
+        if (se < 0) return;
+        add_state(i, se);
+      } else if (q->type == Q_SEQUENCE && nn(i) > 0) {
+        reset_state(i);
+      }
+      update_state(i);
+      n_ret = 0;
+      int wr = 0;
+      const int n0 = pn(i);
+      int k = 0;
+      for (; k < n0 && err == GE_OK; ++k) {
+        const int se = pl(i, k);
+        if (is_expired(i, se)) {  // (ts == t here)
+          if (s.within_every >= 0) {
+            add_every_state(s.within_every, se);
+            update_state(s.within_every);
+          }
+          continue;
+        }
+        const int own = slot(se, i);
+        const bool passed = own < 0 ? t >= se_ts(se) + w : t >= nd_ts(own) + w;  // waitingTimePassed
+        if (!passed) {
+          pl(i, wr++) = se;
+          continue;
+        }
+        const bool partner = slot(se, s.partner) >= 0;
+        if (s.ltype == L_OR && !partner) {
+          add_dummy(se, i);
+          push_ret(se);
+        } else if (s.ltype == L_AND && partner) {
+          push_ret(se);
+        } else if (s.ltype == L_AND && !partner) {
+          pin(se);
+          add_dummy(se, i);  // the partner may still proceed
+          unpin();
+        }
+      }
+      for (; k < n0; ++k) pl(i, wr++) = pl(i, k);
+      pn(i) = wr;
+      not_processed = n_ret == 0;
+      for (int r = 0; r < n_ret && err == GE_OK; ++r) absent_logical_send(i, ret_at(r), em);
+      n_ret = 0;
+      lst(i) = 0;
+    }
+    if (s.next_every >= 0 || (not_processed && s.is_start)) notify_at(i, (lst(i) == 0 ? actual : lst(i)) + w);
   }
   // Scheduler.sendTimerEvents:186-214 of every absent state of the instance up to time `upto`: the
   // earliest queue head fires first (ties: lower state id). `playback`: the generator's time is
@@ -1159,11 +1348,15 @@ struct Ctx {
   KG_FN void fire_timers(int64_t upto, bool playback, Emit& em) {
     if (lay.TQ == 0) return;
     const int64_t ev_ts = ts;
+    // the sort key of this call's timer matches: the running max of the fired times. The oracle
+    // fires across instances by smallest queue head; a FIFO can hold a time behind a later one, and
+    // that one fires right after it, so (running max, query, fire order) is the global fire order
+    int64_t key = -0x7fffffffffffffffLL - 1;
     for (;;) {
       int bi = -1;
       int64_t bt = 0;
       for (int i = 0; i < lay.S; ++i) {
-        if (S(i).kind != K_ABSENT || tq_len(i) == 0) continue;
+        if (!absent_any(i) || tq_len(i) == 0) continue;
         const int64_t h = tq(i, tq_head(i));
         if (h > upto) continue;
         if (bi < 0 || h < bt) {
@@ -1175,9 +1368,11 @@ struct Ctx {
       tq_head(bi) = (tq_head(bi) + 1) % lay.TQ;
       tq_len(bi) -= 1;
       in_timer = true;
-      timer_ts = bt;
+      key = bt > key ? bt : key;
+      timer_ts = key;
       ts = bt;
-      absent_timer(bi, bt, playback ? upto : bt, em);
+      if (absent_l(bi)) absent_logical_timer(bi, bt, playback ? upto : bt, em);
+      else absent_timer(bi, bt, playback ? upto : bt, em);
       in_timer = false;
     }
     ts = ev_ts;
@@ -1206,6 +1401,8 @@ inline void make_layout(GLayout& L, int S, int R, int N, int LC, int NA, bool v3
   if (v32) { L.o_ndval = o; o += N * NA; }
   L.TQ = TQ;
   L.o_tqh = o; o += TQ > 0 ? 2 * S : 0;
+  L.o_ret = o; o += LC;
+  L.pad2 = 0;
   L.n32 = o;
   o = 0;
   L.o_seused = o; o += L.SU;

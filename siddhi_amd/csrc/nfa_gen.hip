@@ -83,10 +83,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   c.hstride = 64;
   c.hs = L.hot_s;
   c.load_hot();
-  int32_t ret[kg::GMAXRET];
   c.ev_val = evv;
   c.pins = c.h32 + (int64_t)3 * L.hot_s * 64;  // [4][lane] after the hot words
-  c.ret = ret;
   c.err = kg::GE_OK;
   c.capk = 0;
   c.npin = 0;

@@ -24,7 +24,8 @@ the CPU oracle (``oracle/oracle.cpp``)::
     state := kind stream_idx is_start min max logical_type partner next_pre next_every_pre
              within_every_pre callback_pre this_last_post has_selector waiting_ms
              n_filters { n_insn insn* }
-             (waiting_ms: the 'for' time of an absent state, -1 otherwise)
+             (waiting_ms: the 'for' time of an absent state or absent logical side; -2 for an
+              absent logical side without 'for'; -1 otherwise)
     node  := node_type a b pre
     insn  := w0 a b imm     w0 = op | ltype<<8 | rtype<<16 | restype<<24
 """

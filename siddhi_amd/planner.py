@@ -290,9 +290,21 @@ class _QueryPlanner:
             return self._new_node(NodeIR(N_EVERY, a=n, pre=f)), f, l
         if isinstance(e, ql.LogicalSE):
             lt = L_AND if e.type == "and" else L_OR
-            s2 = self._parse_stream(e.s2, is_start, K_LOGICAL, {"logical_type": lt})
+
+            def side(x):
+                # AbsentLogicalPre/PostStateProcessor sides (StateInputStreamParser.java:284-327):
+                # waiting_ms -2 encodes a side without 'for' (the reference's waitingTime -1)
+                if isinstance(x, ql.AbsentSE):
+                    if self.partitioned:
+                        raise SiddhiAppCreationException(
+                            "absent patterns inside a partition are not on the accelerated path")
+                    return x.stream, {"logical_type": lt, "waiting_ms": -2 if x.waiting_ms is None else x.waiting_ms}
+                return x, {"logical_type": lt}
+            st2, ex2 = side(e.s2)
+            st1, ex1 = side(e.s1)
+            s2 = self._parse_stream(st2, is_start, K_LOGICAL, ex2)
             pres.append(s2)
-            s1 = self._parse_stream(e.s1, is_start, K_LOGICAL, {"logical_type": lt})
+            s1 = self._parse_stream(st1, is_start, K_LOGICAL, ex1)
             pres.append(s1)
             self.states[s1].partner = s2
             self.states[s2].partner = s1

@@ -17,11 +17,12 @@ Covers the part of the SiddhiQL grammar that feeds the pattern/sequence (NFA) pa
 * ``partition with (attr of S, ...) begin <queries> end``
 
 * absent states ``not S[..] for T`` (``SiddhiQL.g4:263-268``, ``basic_absent_pattern_source``) in
-  pattern and sequence chains, with or without ``every``
+  pattern and sequence chains, with or without ``every``, and as sides of a logical state
+  (``e1=A and not B``, ``not A for T or e2=B``, ...; ``logical_absent_stateful_source``,
+  ``SiddhiQL.g4:251-260``)
 
-Logical absent states (``e1=A and not B``, ``SiddhiQL.g4:251-260``), windows, joins, functions,
-group-by and output rate limiting are outside the accelerated path and raise
-:class:`SiddhiParserException`.
+Windows, joins, functions, group-by and output rate limiting are outside the accelerated path and
+raise :class:`SiddhiParserException`.
 """
 from __future__ import annotations
 
@@ -103,9 +104,10 @@ class StreamSE:
 
 @dataclass
 class AbsentSE:
-    """``not S[..] for T`` (AbsentStreamStateElement; the stream carries no alias)."""
+    """``not S[..] for T`` (AbsentStreamStateElement; the stream carries no alias). waiting_ms is
+    None for a logical side written without 'for' (``e1=A and not B``)."""
     stream: StreamSE
-    waiting_ms: int
+    waiting_ms: Optional[int]
 
 
 @dataclass
@@ -525,28 +527,49 @@ class Parser:
             return self.absent()
         return self.source()
 
-    def absent(self):
-        """basic_absent_pattern_source: NOT basic_source for_time (SiddhiQL.g4:267-268)."""
+    def absent_side(self, need_for: bool):
+        """NOT basic_source [for_time] (SiddhiQL.g4:253-268)."""
         self.expect("not")
         s = self.std_source()
         if s.alias is not None:
             self.error("an absent stream ('not S') cannot carry an alias")
-        if self.at("and") or self.at("or"):
-            self.error("logical absent patterns ('not A and B') are outside the accelerated path")
-        if not self.accept("for"):
+        w = None
+        if self.accept("for"):
+            w = self.time_value()
+        elif need_for:
             self.error("an absent stream needs a 'for' waiting time")
-        w = self.time_value()
-        if self.at("and") or self.at("or"):
-            self.error("logical absent patterns ('not A for T and B') are outside the accelerated path")
         return AbsentSE(s, w)
+
+    def absent(self):
+        """basic_absent_pattern_source, or a logical_absent_stateful_source starting with one."""
+        a = self.absent_side(need_for=False)
+        if self.at("and") or self.at("or"):
+            ty = self.peek().text
+            self.i += 1
+            if ty == "or" and a.waiting_ms is None:
+                self.error("'not A or B' needs a 'for' time on the absent side")
+            # NOT basic_source AND standard | basic_absent AND|OR standard | basic_absent AND|OR basic_absent
+            if self.at("not"):
+                if a.waiting_ms is None:
+                    self.error("'not A and not B' needs 'for' times")
+                s2 = self.absent_side(need_for=True)
+            else:
+                s2 = self.std_source()
+            return LogicalSE(ty, a, s2)
+        if a.waiting_ms is None:
+            self.error("an absent stream needs a 'for' waiting time")
+        return a
 
     def source(self):
         s1 = self.std_source()
         if self.at("and") or self.at("or"):
             ty = self.peek().text
             self.i += 1
-            if self.at("not"):
-                self.error("logical absent patterns ('A and not B') are outside the accelerated path")
+            if self.at("not"):  # standard AND NOT basic_source [for T] | standard OR basic_absent
+                s2 = self.absent_side(need_for=(ty == "or"))
+                # the visitor puts the absent side first (State.logicalNotAnd / logicalOr(absent,
+                # present): SiddhiQLBaseVisitorImpl.visitLogical_absent_stateful_source:975-1017)
+                return LogicalSE(ty, s2, s1)
             s2 = self.std_source()
             return LogicalSE(ty, s1, s2)
         # count / kleene

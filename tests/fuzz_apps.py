@@ -123,6 +123,18 @@ def random_absent_app(seed, n_queries=4):
         for i in range(n):
             st = rng.choice("AB")
             pred = _pred(rng, aliases, st)
+            r = rng.random()
+            if r < 0.25 and i != absent_at:  # a logical state with an absent side
+                al = f"e{i}"
+                st2 = rng.choice("AB")
+                ab = f"not {st2}[{_pred(rng, aliases, st2)}]"
+                ty = rng.choice(["and", "or"])
+                if ty == "or" or rng.random() < 0.6:
+                    ab += f" for {rng.randint(2, 12)} milliseconds"
+                pres = f"{al}={st}[{pred}]"
+                parts.append(f"{pres} {ty} {ab}" if rng.random() < 0.5 else f"{ab} {ty} {pres}")
+                aliases.append(al)
+                continue
             if i == absent_at or (i > 0 and rng.random() < 0.15):
                 ab = f"not {st}[{pred}] for {rng.randint(2, 12)} milliseconds"
                 if rng.random() < 0.3 and (not seq or i == 0):  # sequences: `every` only at the start

@@ -94,10 +94,8 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
   c.load_hot();
   int64_t evv[GMAXNA];
   int32_t pins[4];
-  int32_t ret[GMAXRET];
   c.ev_val = evv;
   c.pins = pins;
-  c.ret = ret;
   c.npin = 0;
   c.n_ret = 0;
   c.err = GE_OK;

@@ -8,8 +8,9 @@ asserted in-event counts at each check), and the callback's ordered expected row
 starts at ts0 (playback apps: at 0, TimestampGeneratorImpl's initial time); time passes with the
 sleeps (a live runtime's schedulers fire meanwhile) or, in playback, with the events alone.
 
-Out of scope, and rejected at parse / plan time: logical absent states (`e1=A and not B`,
-`not A for T or e2=B`) and absent states inside a partition. Playback apps with a heartbeat
+Logical absent states (`e1=A and not B`, `not A for T or e2=B`: AbsentLogicalPre/PostStateProcessor)
+are in scope. Out of scope, and rejected at plan time: absent states inside a partition (2
+fixtures). Playback apps with a heartbeat
 (`@app:playback(idle.time=.., increment=..)`: event time advancing with the wall clock while idle)
 are not modelled and are skipped."""
 import json
@@ -95,4 +96,4 @@ def test_absent_kat_coverage():
     suites = {f["id"].split(".")[0] for f in FIXTURES}
     assert len(suites) == 8 and len(FIXTURES) >= 300
     in_scope = [f for f in FIXTURES if not out_of_scope(f)]
-    assert len(in_scope) >= 140
+    assert len(in_scope) >= 290

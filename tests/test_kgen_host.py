@@ -177,7 +177,7 @@ def run_timeline(src, seed, engine_factory=None):
     return app
 
 
-@pytest.mark.parametrize("seed", range(60))
+@pytest.mark.parametrize("seed", range(200))
 def test_kgen_host_absent_fuzz(seed):
     """Random absent patterns / sequences (any position, every, within, cross-references) over a
     random timeline of events and idle time: the host build of the device interpreter emits the

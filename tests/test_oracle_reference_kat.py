@@ -16,7 +16,6 @@ from siddhi_amd.ql import SiddhiAppCreationException, SiddhiParserException
 KAT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kat.json")))
 OUT_OF_SCOPE = {
     "CountPatternTestCase.testQuery14": "having",
-    "CountPatternTestCase.testQuery15": "absent pattern",
     "PatternPartitionTestCase.testPatternPartitionQuery30": "non-partitioned stream in partition",
     "PatternPartitionTestCase.testPatternPartitionQuery32": "inner stream",
     "PatternPartitionTestCase.testPatternPartitionQuery33": "plain stream query",
