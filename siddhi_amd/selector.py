@@ -134,7 +134,9 @@ def evaluate(code: List[Insn], slots: Sequence[Sequence[int]], log: EventLog, st
             st.append((_const(ins, dictionary, strings), ins.restype))
         elif op == OP_ATTR:
             seq = _chain_at(slots[ins.a], ins.b)
-            if seq is None or log.nulls[seq][ins.imm]:
+            # seq -1: the empty event an absent logical side borrows (StreamEventPool.borrowEvent:
+            # every attribute null)
+            if seq is None or seq < 0 or log.nulls[seq][ins.imm]:
                 st.append((None, ins.restype))
             else:
                 st.append((decode_value(int(log.vals[seq][ins.imm]), ins.restype, dictionary), ins.restype))
