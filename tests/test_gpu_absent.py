@@ -69,7 +69,7 @@ def test_absent_fuzz_on_gpu(seed, batch):
     assert g.matches == o.matches
 
 
-@pytest.mark.parametrize("seed", [1, 9, 12])
+@pytest.mark.parametrize("seed", [0, 3, 15])
 def test_absent_timer_queues_grow(seed):
     """Lists and scheduler queues that start at 2 entries overflow: the push is undone, the queues
     double with the lists (gen_remap_kernel rewrites each FIFO ring from its head) and the push
