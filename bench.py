@@ -7,8 +7,10 @@ P = 10,000 concurrent 2-state patterns per GPU
 over the seeded synthetic StockStream (20 B/event SoA), generated on the device and resident in HBM
 before the timed region. One step = one NFA-step pass (one sdh_engine_push) over a batch of B = 8M
 events; every match record is written to HBM (SDH_FLAG_DEVICE_MATCHES: counted, not polled).
-`--workload c3 | c4` runs the count/logical partitioned family or one GPU's shard of the fraud
-sequences instead.
+`--workload c3 | c4 | c5` runs the count/logical partitioned family, one GPU's shard of the fraud
+sequences, or the C5 family (four joined streams, mixed 2-4-state patterns under one `partition with`
+key, `within 1 hour`; one step = one batch per stream; reduced pattern / key counts)
+instead.
 
 Match expansion (`expansion` in the JSON line): a second engine in normal mode runs pushes of a
 smaller batch followed by sdh_engine_poll_device -- the device R18 sort and the gather of the ABI
@@ -36,6 +38,7 @@ DEFAULTS = {  # workload -> (patterns per GPU, events per step, keys)
     "c2": (10000, 1 << 23, 100),
     "c3": (1000, 1 << 20, 10000),
     "c4": (1250, 1 << 20, 100_000),
+    "c5": (256, 1 << 18, 32768),  # patterns, events per stream per step, accounts per GPU
 }
 
 
@@ -60,11 +63,11 @@ def parse():
 
 
 def app_source(workload, P, first):
-    from siddhi_amd.workloads import c2_app, c3_app, c4_app
-    return {"c2": c2_app, "c3": c3_app, "c4": c4_app}[workload](P, first=first)
+    from siddhi_amd.workloads import c2_app, c3_app, c4_app, c5_app
+    return {"c2": c2_app, "c3": c3_app, "c4": c4_app, "c5": c5_app}[workload](P, first=first)
 
 
-def make_engine(workload, P, first, K, device, flags, partials):
+def make_engine(workload, P, first, K, device, flags, partials, shard=(0, 1)):
     from siddhi_amd import ql
     from siddhi_amd.engine import HipEngine
     from siddhi_amd.planner import plan
@@ -72,6 +75,11 @@ def make_engine(workload, P, first, K, device, flags, partials):
     if workload == "c4":
         # a sequence instance holds at most one partial per state (R8): small pools
         return HipEngine(blob, device=device, flags=flags, gen_pool_states=8, gen_pool_nodes=32, gen_list_cap=8)
+    if workload == "c5":  # key sharding: every rank runs all patterns over its own accounts
+        pools = [int(x) for x in os.environ.get("SDH_C5_POOLS", "16,48,16").split(",")]
+        return HipEngine(blob, device=device, flags=flags, gen_pool_states=pools[0], gen_pool_nodes=pools[1],
+                         gen_list_cap=pools[2], gen_max_keys=max(1024, 2 * K), shard_rank=shard[0],
+                         shard_world=shard[1])
     if workload == "c3":
         pools = [int(x) for x in os.environ.get("SDH_C3_POOLS", "32,128,32").split(",")]
         return HipEngine(blob, device=device, flags=flags, gen_pool_states=pools[0], gen_pool_nodes=pools[1],
@@ -80,7 +88,14 @@ def make_engine(workload, P, first, K, device, flags, partials):
 
 
 def gen_batch(workload, start, n, K, dev):
-    from siddhi_amd.workloads import stock_events_torch, txn_events_torch
+    from siddhi_amd.workloads import c5_events_torch, stock_events_torch, txn_events_torch
+    if workload == "c5":  # one batch per stream: [(ts, acct, amount bits, code)] x 4
+        import torch
+        out = []
+        for si in range(4):
+            ts, a, b, c = c5_events_torch(si, start, n, K, dev)
+            out.append([ts, a, b.view(torch.int32), c])
+        return out
     gen = txn_events_torch if workload == "c4" else stock_events_torch
     ts, a, b, c = gen(start, n, K, dev)
     return [ts, a, b.view(__import__("torch").int32), c]
@@ -106,20 +121,22 @@ def _oracle_shard(workload, shard, P, n_symbols, budget_s):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from harness import App
     from siddhi_amd.workloads import stock_events, txn_events
+    from siddhi_amd.workloads import c5_events
     app = App(app_source(workload, P, shard * P))
     lib, h = app.engine.lib, app.engine.h
     gen = txn_events if workload == "c4" else stock_events
     done, start, n, matches = 0, 0, 20000, 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
-        ts, sym, price, vol = gen(start, n, n_symbols)
-        vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64),
-                         vol.astype(np.int64)], 1)
-        app.engine.send(0, ts, vals, None)
-        matches += lib.oracle_num_matches(h)
-        lib.oracle_clear_matches(h)
+        for si in range(4 if workload == "c5" else 1):  # C5: one batch per stream
+            ts, sym, price, vol = c5_events(si, start, n, n_symbols) if workload == "c5" else gen(start, n, n_symbols)
+            vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64),
+                             vol.astype(np.int64)], 1)
+            app.engine.send(si, ts, vals, None)
+            matches += lib.oracle_num_matches(h)
+            lib.oracle_clear_matches(h)
+            done += n
         start += n
-        done += n
     live = lib.oracle_live_partials(h)
     return done, time.perf_counter() - t0, matches, live
 
@@ -225,25 +242,35 @@ def main():
     P = args.patterns or P0
     B = args.batch or B0
     K = args.keys or K0
-    eng = make_engine(args.workload, P, rank * P, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials)
+    c5 = args.workload == "c5"
+    if c5:  # key sharding (weak scaling): every rank runs all P patterns over its K of K * world accounts,
+        # and each stream carries B events per GPU per step
+        eng = make_engine("c5", P, 0, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials, shard=(rank, world))
+        B, K_gen = B * world, K * world
+        args.no_expansion = args.no_ingest = True  # (single-stream helpers)
+    else:
+        eng = make_engine(args.workload, P, rank * P, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials)
+        K_gen = K
 
     n_batches = args.warmup + args.steps
     # synthetic batches generated on the device before the timed region (rank 0's copy is the
     # broadcast source in multi-GPU runs; the other ranks receive into their own buffers)
-    batches = [gen_batch(args.workload, s * B, B, K, dev) for s in range(n_batches)]
+    batches = [gen_batch(args.workload, s * B, B, K_gen, dev) for s in range(n_batches)]
     torch.cuda.synchronize()
     bcast = world > 1
 
     def step(i):
-        cols = batches[i]
-        if bcast:
-            for t in cols:
-                dist.broadcast(t if backend == "nccl" else t.cpu(), src=0)
-        eng.push_device(0, B, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
+        per_stream = batches[i] if c5 else [batches[i]]
+        for si, cols in enumerate(per_stream):
+            if bcast:
+                for t in cols:
+                    dist.broadcast(t if backend == "nccl" else t.cpu(), src=0)
+            eng.push_device(si, B, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
 
     for i in range(args.warmup):
         step(i)
     kern_ms, kern_bytes, matches = [], [], 0
+    pe0 = eng.stats().pattern_events
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -259,16 +286,19 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     live = eng.stats().live_partials
+    # C5: (event, pattern) evaluations the engine performed (each rank's own accounts' events
+    # against the patterns reading their stream)
+    pe = float(eng.stats().pattern_events - pe0)
     if world > 1:
         t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        mt = torch.tensor([matches, live], device=cdev, dtype=torch.float64)
+        mt = torch.tensor([matches, live, pe], device=cdev, dtype=torch.float64)
         dist.all_reduce(mt)
-        matches, live = int(mt[0].item()), int(mt[1].item())
+        matches, live, pe = int(mt[0].item()), int(mt[1].item()), float(mt[2].item())
     del batches
 
-    total_pe = float(B) * args.steps * P * world
+    total_pe = pe if c5 else float(B) * args.steps * P * world
     value = total_pe / elapsed
     avg_ms = float(np.mean(kern_ms))
     avg_bytes = float(np.mean(kern_bytes))
@@ -282,6 +312,11 @@ def main():
         wl = (f"C3: count <2:5> + logical and/or patterns, partition with (symbol) over {K} keys, "
               "within 10 sec")
         kernel = "sdh_part_spec"
+    elif c5:
+        wl = (f"C5 family (reduced): {P} mixed 2-4-state patterns (cross-stream reference, and, or, count) over 4 "
+              f"joined streams, partition with (acct) over {K} accounts per GPU of {K * world}, within 1 hour; "
+              f"{B} events per stream per step")
+        kernel = "nfa_gen_kernel"
     else:
         wl = ("C4: fraud-rule sequences every e1=Txn[..], e2=Txn[..e1.amount*M], e3=Txn[..] within 1 min "
               f"(strict contiguity), {K} accounts, pattern-set shard {rank * P}..{rank * P + P - 1}")
@@ -301,8 +336,10 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded splitmix64 StockStream / Txn stream, SURVEY §8(d)), generated in HBM",
-        "config": {"workload": wl, "patterns_per_gpu": P, "events_per_step": B, "timed_events": B * args.steps,
-                   "keys": K, "parallelism": f"pattern-set x{world}" + (" (RCCL event broadcast)" if bcast else ""),
+        "config": {"workload": wl, "patterns_per_gpu": P, "events_per_step": B * (4 if c5 else 1),
+                   "timed_events": B * args.steps * (4 if c5 else 1),
+                   "keys": K, "parallelism": (f"key shards x{world}" if c5 else f"pattern-set x{world}") +
+                   (" (RCCL event broadcast)" if bcast else ""),
                    "matches": matches, "matches_per_s": matches / elapsed, "live_partials": live,
                    "source_hash": source_hash(kernel)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",

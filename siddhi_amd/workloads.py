@@ -193,3 +193,69 @@ def txn_events_torch(start: int, n: int, n_accounts: int, device, seed: int = EV
     i, (h1, h2, h3) = _hashes_t(start, n, seed, device)
     amount = _umod_t(h1, 100000).to(torch.float32) / 100.0
     return TS0 + i, _umod_t(h3, n_accounts).to(torch.int32), amount, _umod_t(h2, 100).to(torch.int32)
+
+
+# ---- C5 family (BASELINE.json configs[4]): mixed 2-4-state patterns over four
+# joined streams, `partition with` one account key across all four, `within 1 hour` ----
+C5_STREAMS = ("Card", "Login", "Transfer", "Device")
+
+
+def c5_streams_def() -> str:
+    return " ".join(f"define stream {s} (acct int, amount float, code int);" for s in C5_STREAMS)
+
+
+def c5_query(p: int, seed: int = PATTERN_SEED) -> str:
+    """Pattern p of the C5 family: kind p % 4 (2-state cross-stream reference, logical and, logical
+    or, 4-state with a count state), streams and constants from splitmix64(seed ^ (p + 5000))."""
+    h = splitmix64(seed ^ (p + 5000))
+    sa, sb, sc, sd = (C5_STREAMS[(h >> (2 * k)) & 3] for k in range(4))
+    a = 600 + (h >> 8) % 390
+    m = ("1.01", "1.05", "1.1", "1.25")[(h >> 20) % 4]
+    c = (h >> 24) % 100
+    kind = p % 4
+    if kind == 0:
+        body = (f"every e1={sa}[amount > {a}] -> e2={sb}[amount > e1.amount * {m}] within 1 hour "
+                f"select e1.acct as k, e1.amount as a1, e2.amount as a2")
+    elif kind == 1:
+        body = (f"every e1={sa}[amount > {a}] -> e2={sb}[code == e1.code] and e3={sc}[amount < {1000 - a}] "
+                f"within 1 hour select e1.acct as k, e2.code as c2, e3.amount as a3")
+    elif kind == 2:
+        body = (f"every e1={sa}[amount > {a}] -> e2={sb}[amount > e1.amount] or e3={sc}[code > {c}] "
+                f"within 1 hour select e1.acct as k, e2.amount as a2, e3.code as c3")
+    else:
+        body = (f"every e1={sa}[amount > {a}] -> e2={sb}[amount < e1.amount]<1:3> -> "
+                f"e3={sc}[amount > e2[last].amount] -> e4={sd}[code == e1.code] within 1 hour "
+                f"select e1.acct as k, e2[0].amount as a2, e4.code as c4")
+    return f"@info(name='c5p{p}') from {body} insert into Alerts;"
+
+
+def c5_app(n_patterns: int, first: int = 0) -> str:
+    """C5 (BASELINE.json configs[4]): n_patterns mixed patterns in one `partition with (acct of
+    Card, acct of Login, acct of Transfer, acct of Device)`; a shard holds patterns first ..
+    first+n_patterns-1 (key sharding spreads the accounts over GPUs)."""
+    qs = " ".join(c5_query(p) for p in range(first, first + n_patterns))
+    keys = ", ".join(f"acct of {s}" for s in C5_STREAMS)
+    return f"{c5_streams_def()} partition with ({keys}) begin {qs} end;"
+
+
+def c5_events(stream: int, start: int, n: int, n_accounts: int, seed: int = EVENT_SEED):
+    """Events [start, start+n) of C5 stream `stream` (1 event / ms each): (ts int64, acct int32,
+    amount float32 in [0, 1000), code int32 in [0, 100))."""
+    i = np.arange(start, start + n, dtype=np.uint64)
+    s = np.uint64(seed ^ (0x5C5 + stream))
+    h1 = splitmix64_np(s ^ (i * np.uint64(4) + np.uint64(1)))
+    h2 = splitmix64_np(s ^ (i * np.uint64(4) + np.uint64(2)))
+    h3 = splitmix64_np(s ^ (i * np.uint64(4) + np.uint64(3)))
+    ts = (np.int64(TS0) + i.astype(np.int64)).astype(np.int64)
+    amount = (h1 % np.uint64(100000)).astype(np.float32) / np.float32(100.0)
+    code = (h2 % np.uint64(100)).astype(np.int32)
+    acct = (h3 % np.uint64(n_accounts)).astype(np.int32)
+    return ts, acct, amount.astype(np.float32), code
+
+
+def c5_events_torch(stream: int, start: int, n: int, n_accounts: int, device, seed: int = EVENT_SEED):
+    """c5_events as torch tensors on `device`."""
+    import torch
+    i, (h1, h2, h3) = _hashes_t(start, n, seed ^ (0x5C5 + stream), device)
+    amount = _umod_t(h1, 100000).to(torch.float32) / 100.0
+    return TS0 + i, _umod_t(h3, n_accounts).to(torch.int32), amount, _umod_t(h2, 100).to(torch.int32)

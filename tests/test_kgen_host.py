@@ -190,3 +190,12 @@ def test_kgen_host_absent_fuzz(seed):
         pytest.skip("the reference engine throws on this stream")
     g = run_timeline(src, seed, engine_factory=lambda blob: KGenHostEngine(blob, R=4096, N=4096, LC=4096))
     assert g.matches == o.matches
+
+
+def test_kgen_host_c5_family():
+    """The C5 family (4 joined streams, one partition key, mixed 2-4-state patterns) on the host
+    build of the K_gen interpreter equals the oracle."""
+    from c5_family import run_c5
+    o = run_c5(32, 200, 1500, 500)
+    g = run_c5(32, 200, 1500, 500, engine_factory=lambda blob: KGenHostEngine(blob, R=4096, N=4096, LC=4096))
+    assert g.matches == o.matches and len(o.matches) > 100
