@@ -38,7 +38,7 @@ DEFAULTS = {  # workload -> (patterns per GPU, events per step, keys)
     "c2": (10000, 1 << 23, 100),
     "c3": (1000, 1 << 20, 10000),
     "c4": (1250, 1 << 20, 100_000),
-    "c5": (256, 1 << 18, 32768),  # patterns, events per stream per step, accounts per GPU
+    "c5": (256, 1 << 16, 125_000),  # patterns, events per stream per step, accounts per GPU (8 GPUs: 1M)
 }
 
 
@@ -76,7 +76,7 @@ def make_engine(workload, P, first, K, device, flags, partials, shard=(0, 1)):
         # a sequence instance holds at most one partial per state (R8): small pools
         return HipEngine(blob, device=device, flags=flags, gen_pool_states=8, gen_pool_nodes=32, gen_list_cap=8)
     if workload == "c5":  # key sharding: every rank runs all patterns over its own accounts
-        pools = [int(x) for x in os.environ.get("SDH_C5_POOLS", "16,48,16").split(",")]
+        pools = [int(x) for x in os.environ.get("SDH_C5_POOLS", "8,24,8").split(",")]
         return HipEngine(blob, device=device, flags=flags, gen_pool_states=pools[0], gen_pool_nodes=pools[1],
                          gen_list_cap=pools[2], gen_max_keys=max(1024, 2 * K), shard_rank=shard[0],
                          shard_world=shard[1])

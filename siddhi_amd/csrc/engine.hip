@@ -2043,8 +2043,10 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   e->g_rec_next.ensure(1);
   const bool write = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) == 0;
   // arenas are backed up before the pass so that an overflow (match output, K_part tables, K_gen
-  // pools) can be undone and the push re-run exactly at the grown capacity
-  bool backed = gen_backup(e);
+  // pools) can be undone and the push re-run exactly at the grown capacity. The benchmark mode
+  // (SDH_FLAG_DEVICE_MATCHES: records wrap in a ring, nothing is polled) skips the copy unless K_part
+  // tables are present; there a K_gen pool overflow fails the push loudly (SDH_E_CAPACITY)
+  bool backed = (write || !e->psets.empty()) && gen_backup(e);
   double bytes = 0;
   int32_t tail_len = -1;
   bool any = false;

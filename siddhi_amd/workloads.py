@@ -206,25 +206,26 @@ def c5_streams_def() -> str:
 
 def c5_query(p: int, seed: int = PATTERN_SEED) -> str:
     """Pattern p of the C5 family: kind p % 4 (2-state cross-stream reference, logical and, logical
-    or, 4-state with a count state), streams and constants from splitmix64(seed ^ (p + 5000))."""
+    or, 4-state with a count state) over a fixed stream route per kind (so a kind is one shape and
+    64 patterns fill one wave), thresholds from splitmix64(seed ^ (p + 5000)). Start filters pass
+    0.1-5 % of events: fraud rules, with state sparse per account."""
     h = splitmix64(seed ^ (p + 5000))
-    sa, sb, sc, sd = (C5_STREAMS[(h >> (2 * k)) & 3] for k in range(4))
-    a = 600 + (h >> 8) % 390
+    a = 950 + (h >> 8) % 49
     m = ("1.01", "1.05", "1.1", "1.25")[(h >> 20) % 4]
     c = (h >> 24) % 100
     kind = p % 4
     if kind == 0:
-        body = (f"every e1={sa}[amount > {a}] -> e2={sb}[amount > e1.amount * {m}] within 1 hour "
+        body = (f"every e1=Card[amount > {a}] -> e2=Transfer[amount > e1.amount * {m}] within 1 hour "
                 f"select e1.acct as k, e1.amount as a1, e2.amount as a2")
     elif kind == 1:
-        body = (f"every e1={sa}[amount > {a}] -> e2={sb}[code == e1.code] and e3={sc}[amount < {1000 - a}] "
+        body = (f"every e1=Login[amount > {a}] -> e2=Transfer[code == e1.code] and e3=Device[amount < {1000 - a}] "
                 f"within 1 hour select e1.acct as k, e2.code as c2, e3.amount as a3")
     elif kind == 2:
-        body = (f"every e1={sa}[amount > {a}] -> e2={sb}[amount > e1.amount] or e3={sc}[code > {c}] "
+        body = (f"every e1=Card[amount > {a}] -> e2=Login[amount > e1.amount] or e3=Device[code > {c}] "
                 f"within 1 hour select e1.acct as k, e2.amount as a2, e3.code as c3")
     else:
-        body = (f"every e1={sa}[amount > {a}] -> e2={sb}[amount < e1.amount]<1:3> -> "
-                f"e3={sc}[amount > e2[last].amount] -> e4={sd}[code == e1.code] within 1 hour "
+        body = (f"every e1=Card[amount > {a}] -> e2=Transfer[amount < e1.amount]<1:3> -> "
+                f"e3=Device[amount > e2[last].amount] -> e4=Login[code == e1.code] within 1 hour "
                 f"select e1.acct as k, e2[0].amount as a2, e4.code as c4")
     return f"@info(name='c5p{p}') from {body} insert into Alerts;"
 

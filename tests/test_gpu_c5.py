@@ -21,7 +21,7 @@ def test_c5_family_equals_oracle(batch):
     o = run_c5(128, 2000, 8000, batch)
     g = run_c5(128, 2000, 8000, batch, engine_factory=lambda blob: _hip(blob, gen_pool_states=16,
                                                                          gen_pool_nodes=64, gen_list_cap=16))
-    assert g.matches == o.matches and len(o.matches) > 10000
+    assert g.matches == o.matches and len(o.matches) > 1000
 
 
 def test_c5_family_key_shards_merge():
@@ -31,4 +31,4 @@ def test_c5_family_key_shards_merge():
     parts = [run_c5(64, 1000, 4000, 1000, engine_factory=lambda blob, r=r: _hip(blob, shard_rank=r, shard_world=2))
              for r in range(2)]
     got = sorted(m for p in parts for m in p.matches)
-    assert got == sorted(o.matches) and all(p.matches for p in parts)
+    assert got == sorted(o.matches) and len(got) > 300 and all(p.matches for p in parts)
