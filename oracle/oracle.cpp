@@ -17,6 +17,7 @@
 // Garbage is reclaimed by a mark/sweep over all pending lists (the JVM's job in the reference).
 #include "oracle.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -834,20 +835,32 @@ struct Engine {
     if (!started) start(t);
     if (has_absent) {
       for (;;) {
+        // every scheduler in (query, key) order -- top-level runtimes and each partition's per-key
+        // clones (PartitionRuntime.cloneIfNotExist gives every key its own schedulers; clones are
+        // never start()ed) -- the earliest queue head fires first, ties in that order
         Runtime* best = nullptr;
         int bi = -1;
         i64 bt = 0;
-        for (auto& r : top) {
-          if (!r) continue;
+        auto consider = [&](Runtime* r) {
           for (size_t i = 0; i < r->pres.size(); ++i) {
             const Pre& p = r->pres[i];
             if (p.timers.empty() || p.timers.front() > t) continue;
             if (!best || p.timers.front() < bt) {
-              best = r.get();
+              best = r;
               bi = (int)i;
               bt = p.timers.front();
             }
           }
+        };
+        for (size_t qi = 0; qi < prog.queries.size(); ++qi) {
+          const int pi = prog.queries[qi].partition;
+          if (pi < 0) {
+            if (top[qi]) consider(top[qi].get());
+            continue;
+          }
+          const auto& qs = prog.parts[pi].queries;
+          const size_t slot = std::find(qs.begin(), qs.end(), (int)qi) - qs.begin();
+          for (auto& kv : part_inst[pi]) consider(kv.second[slot].get());
         }
         if (!best) break;
         best->pres[bi].timers.pop_front();

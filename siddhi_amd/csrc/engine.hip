@@ -823,7 +823,7 @@ void append_gen(sdh_engine* e) {
   HIPCHK(hipStreamSynchronize(e->stream));
   e->mt.n += n_rec;
   e->mt.nw += used;
-  e->mt.n_lo = std::max(e->mt.n_lo, e->has_absent ? 2 : 1);  // timer records: (fire order, time)
+  e->mt.n_lo = std::max(e->mt.n_lo, e->has_absent ? 3 : 1);  // timer records: (key, query, time)
 }
 
 void table_clear(sdh_engine* e) {
@@ -855,7 +855,7 @@ int64_t table_sort(sdh_engine* e, int64_t* total_words) {
   e->po_seq.ensure(n);
   e->po_len.ensure(n + 1);
   e->po_off.ensure(n + 1);
-  // timer records' tiebreaks are a full timestamp and (query << 32 | fire ordinal)
+  // timer records' tiebreaks are a full timestamp, the query and the partition key
   const int lo_bits = e->has_absent ? 64 : std::max(1, bits_of((uint64_t)std::max<int64_t>(e->seq, 1 << 16)));
   const int hi_bits = bits_of((uint64_t)(e->seq - e->seq_ref)) + RANK_BITS;
   int32_t* perm = nullptr;
@@ -1856,19 +1856,47 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
     }
   }
   // partitions: route the batch once (dense key ids, events grouped by key), then run the
-  // partition's K_gen set and its K_part sets over the same segments (a time advance has no
-  // events, and no partitioned query has absent states)
-  for (int pi = 0; pi < (int)e->routes.size() && n > 0; ++pi) {
+  // partition's K_gen set and its K_part sets over the same segments. A K_gen set with absent states
+  // runs as a timer sweep instead: every known key's clone walks the whole batch (time passes for it
+  // at every event of any key or stream) and processes its own key's events; a time advance, or a
+  // batch of a stream the partition does not key, sweeps with no own events
+  for (int pi = 0; pi < (int)e->routes.size(); ++pi) {
     if (!e->routes[pi]) continue;
     auto& rt = *e->routes[pi];
     const kg::LPart& pd = e->lp.parts[pi];
     int attr = -1;
     for (const auto& k : pd.keys)
       if (k.stream == stream) attr = (int)k.code[0].imm;
-    if (attr < 0) continue;
     sdh_engine::GenSet* gsp = nullptr;
     for (auto& up : e->gsets)
       if (up->partition == pi) gsp = up.get();
+    bool timed = false;
+    if (gsp)
+      for (int g = 0; g < gsp->n_groups; ++g) timed |= e->gq[e->group_tmpl[gsp->group_base + g]].lay.TQ > 0;
+    auto sweep = [&](const uint32_t* ev_kid, int64_t n_keys) {
+      auto& gs = *gsp;
+      sdh::GenLaunch L = gen_launch_base(e, gs, B, write);
+      L.a32 = gs.a32.p;
+      L.a64 = gs.a64.p;
+      L.key_of_id = rt.key_of_id.p;
+      L.sweep = 1;
+      L.ev_kid = ev_kid;
+      L.n_keys = n_keys;
+      L.n_items = (int32_t)(n_keys * gs.n_groups);
+      if (L.n_items > 0) HIPCHK(sdh_launch_gen(&L, e->stream));
+      e->stats.last_gen_items += L.n_items;
+      any = true;
+      bytes += (double)n * ev_bytes * gs.n_groups * (double)n_keys;
+    };
+    if (n == 0 || attr < 0) {
+      if (timed) {
+        int32_t nk = 0;
+        HIPCHK(hipMemcpyAsync(&nk, rt.n_keys.p, 4, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        sweep(nullptr, std::min<int64_t>(nk, gsp->key_cap));
+      }
+      continue;
+    }
     bool reads = gsp && gsp->n_groups > 0;
     for (auto& ps : e->psets)
       if (ps->partition == pi) reads = true;
@@ -1896,7 +1924,10 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
     if (hv[0] > rt.max_keys) throw Error(SDH_E_CAPACITY, "more partition keys than gen_max_keys");
     // routing (key column read, key/kid/idx written and sorted)
     bytes += (double)n * (8 + 8 + 4 + 4 + 2 * (4 + 4) + 3 * 4);
-    if (gsp && gsp->n_groups > 0) {
+    if (gsp && gsp->n_groups > 0 && timed) {
+      gen_grow(e, *gsp, hv[0]);
+      sweep(e->r_kid.p, hv[0]);
+    } else if (gsp && gsp->n_groups > 0) {
       auto& gs = *gsp;
       gen_grow(e, gs, hv[0]);
       sdh::GenLaunch L = gen_launch_base(e, gs, B, write);

@@ -283,7 +283,6 @@ inline GQuery lower_gen(const LProgram& P, int qi, const Sizing& sz) {
       if (g.cap_type[s][j] == T_LONG || g.cap_type[s][j] == T_DOUBLE) v32 = false;
   bool absent = false;  // absent states' scheduler queues hold up to one list's worth of times
   for (int i = 0; i < S; ++i) absent |= q.st[i].kind == K_ABSENT || (q.st[i].kind == K_LOGICAL && q.st[i].waiting != -1);
-  if (absent && q.partition >= 0) throw LowerError("absent states inside a partition");
   make_layout(g.lay, S, sz.R, sz.N, sz.LC, NA, v32, absent ? sz.LC : 0);
   lower_atoms_or_none(g);
   return g;

@@ -457,10 +457,10 @@ struct Ctx {
   int32_t cnt_tail = -1;
   int64_t cnt_len = 0;
   // absent states: a timer is being processed (its matches are timer records, ordered by (timer_ts =
-  // the running max of the times fired so far, query, timer_idx) before the triggering event's own)
+  // the running max of the times fired so far, query, partition key, emission order) before the
+  // triggering event's own)
   bool in_timer = false;
   int64_t timer_ts = 0;
-  int32_t timer_idx = 0;
 
 #ifdef KG_PROFILE  // host-only access census (tests/native, test infrastructure)
   int32_t& i32(int i) const { kg_prof_hit(lay, 0, i); return w32[(int64_t)i * stride]; }

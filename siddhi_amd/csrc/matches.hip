@@ -107,18 +107,20 @@ __global__ __launch_bounds__(256) void append_gen_kernel(const int64_t* __restri
   const int q = (int)r[1], stream = (int)((r[6] >> 16) & 0xFFFF);
   const int64_t row = row0 + i;
   T.seq[row] = r[4];
-#pragma unroll
-  for (int k = 2; k < MAXLO; ++k) T.lo[k][row] = 0ull;
+  static_assert(MAXLO >= 3, "timer tiebreaks");
   if (stream == 0xFFFF) {
     // an absent state's timer match (nfa_gen.hip): rank 0, before the trigger event's own matches;
-    // then by (timer time, query, fire ordinal) -- lo[1] is the more significant tiebreak
+    // then by (timer key, query, partition key) -- later lo passes are more significant -- and one
+    // instance's matches keep their emission order (the sort is stable, rows are appended in it)
     T.hi[row] = hi_key(r[4], seq_ref, 0);
-    T.lo[1][row] = (uint64_t)r[5] ^ 0x8000000000000000ull;
-    T.lo[0][row] = ((uint64_t)(uint32_t)q << 32) | (uint64_t)(uint32_t)(r[6] >> 32);
+    T.lo[2][row] = (uint64_t)r[5] ^ 0x8000000000000000ull;
+    T.lo[1][row] = (uint64_t)(uint32_t)q;
+    T.lo[0][row] = (uint64_t)r[2] ^ 0x8000000000000000ull;
   } else {
     T.hi[row] = hi_key(r[4], seq_ref, out_rank[(int64_t)q * n_streams + stream]);
     T.lo[0][row] = (uint64_t)r[5];
     T.lo[1][row] = 0ull;
+    T.lo[2][row] = 0ull;
   }
   T.q[row] = q;
   T.key[row] = r[2];

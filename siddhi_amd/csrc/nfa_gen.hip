@@ -37,7 +37,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   }
   int64_t e0 = 0, e1 = L.b.n;
   uint32_t kid = 0;
-  if (L.seg_begin) {
+  if (L.sweep) {  // every known key's clone walks the whole batch (timers), processing its own events
+    kid = (uint32_t)seg;
+    if ((int64_t)kid >= L.n_keys) return;
+  } else if (L.seg_begin) {
     kid = L.seg_kid[seg];
     if (kid == 0xFFFFFFFFu) return;  // events with a null partition key
     e0 = L.seg_begin[seg];
@@ -91,11 +94,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   c.n_ret = 0;
   c.stream = L.b.stream;
   const int64_t key = L.key_of_id ? L.key_of_id[kid] : -1;
-  if (c.i32(q->lay.o_init) == 0) {  // PartitionRuntime.cloneIfNotExist / QueryRuntime.init: seed
+  // PartitionRuntime.cloneIfNotExist / QueryRuntime.init: seed (a sweep seeds a clone at its key's
+  // first event); only top-level runtimes are start()ed (SiddhiAppRuntime.start)
+  auto seed = [&]() {
     c.init_instance();
-    c.start_instance(L.start_ts);
+    if (!L.key_of_id) c.start_instance(L.start_ts);
     c.i32(q->lay.o_init) = 1;
-  }
+  };
+  if (!L.sweep && c.i32(q->lay.o_init) == 0) seed();
   LaneOut o{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
   const int S = q->n_states;
   const int ncap = q->n_cap[c.stream];
@@ -103,7 +109,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   int64_t idx = 0;
   bool live = true;
   // a match record [len, qid, key, ts, trigger seq, idx, S | stream << 16, (count, seqs...) x S];
-  // a timer's record carries stream 0xFFFF, the timer time in idx and its fire ordinal in bits 32+
+  // a timer's record carries stream 0xFFFF and its sort time (kgen.h fire_timers) in idx
   auto emit = [&](const kg::Ctx& cx, int se) {
     if (!live) return;
     int words = 7;
@@ -122,7 +128,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     r[4] = cx.seq;
     if (cx.in_timer) {
       r[5] = cx.timer_ts;
-      r[6] = S | (0xFFFFll << 16) | ((int64_t)c.timer_idx++ << 32);
+      r[6] = S | (0xFFFFll << 16);
     } else {
       r[5] = idx++;
       r[6] = S | (c.stream << 16);
@@ -144,7 +150,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     c.seq = L.b.seq_base + e;
     c.ts = L.b.ts[e];
     idx = 0;
-    c.fire_timers(c.ts, L.playback != 0, emit);  // timers due by this event fire before it
+    const bool inited = !L.sweep || c.i32(q->lay.o_init) != 0;
+    if (inited) c.fire_timers(c.ts, L.playback != 0, emit);  // timers due by this event fire before it
+    if (L.sweep) {
+      if (!L.ev_kid || L.ev_kid[e] != kid) continue;  // another key's event: only time passed
+      if (!inited) seed();
+    }
     if (!reads) continue;
     c.ev_null = 0;
     for (int j = 0; j < ncap; ++j) {  // the event is the same for every lane: identical LDS stores
@@ -154,7 +165,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     }
     c.receive(emit);
   }
-  if (L.advance_to != INT64_MIN && c.err == kg::GE_OK) {  // time passes after the batch
+  if (L.advance_to != INT64_MIN && c.err == kg::GE_OK && c.i32(q->lay.o_init) != 0) {  // time passes after the batch
     live = true;
     c.seq = L.timer_seq;
     c.fire_timers(L.advance_to, L.playback != 0, emit);

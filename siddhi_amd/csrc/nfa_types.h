@@ -264,7 +264,12 @@ struct GenLaunch {
   int64_t advance_to;
   int64_t timer_seq;          // trigger seq of the timers fired after the last event
   int32_t playback;           // @app:playback: the generator's time is the event time while timers fire
-  int32_t pad_t;
+  // timer sweep of a partition set with absent states: item = (kid, group) over every known key; the
+  // item walks the whole batch in order, firing the clone's timers before each event and processing
+  // the events of its own key (ev_kid: each event's dense key id); clones seed at their first event
+  int32_t sweep;
+  const uint32_t* ev_kid;
+  int64_t n_keys;
 };
 
 // ------------------------------------------------------------------------------------------

@@ -268,9 +268,6 @@ class _QueryPlanner:
         if isinstance(e, ql.AbsentSE):
             # AbsentStreamStateElement: a stream state with the absent pre/post pair and its own
             # scheduler (StateInputStreamParser.java:174-200)
-            if self.partitioned:
-                raise SiddhiAppCreationException(
-                    "absent patterns inside a partition are not on the accelerated path")
             sid = self._parse_stream(e.stream, is_start, K_ABSENT, {"waiting_ms": e.waiting_ms})
             pres.append(sid)
             return self._new_node(NodeIR(N_STREAM, pre=sid)), sid, sid
@@ -295,9 +292,6 @@ class _QueryPlanner:
                 # AbsentLogicalPre/PostStateProcessor sides (StateInputStreamParser.java:284-327):
                 # waiting_ms -2 encodes a side without 'for' (the reference's waitingTime -1)
                 if isinstance(x, ql.AbsentSE):
-                    if self.partitioned:
-                        raise SiddhiAppCreationException(
-                            "absent patterns inside a partition are not on the accelerated path")
                     return x.stream, {"logical_type": lt, "waiting_ms": -2 if x.waiting_ms is None else x.waiting_ms}
                 return x, {"logical_type": lt}
             st2, ex2 = side(e.s2)

@@ -110,11 +110,13 @@ def random_seq_app(seed):
     return " ".join(qs)
 
 
-def random_absent_app(seed, n_queries=4):
-    """Unpartitioned patterns / sequences of 2-4 states with absent states (`not S[..] for T`, maybe
-    under `every`) at any position, over A and B (cross-references into earlier states, within)."""
+def random_absent_app(seed, n_queries=4, partition=False):
+    """Patterns / sequences of 2-4 states with absent states (`not S[..] for T`, maybe under
+    `every`) at any position and absent logical sides, over A and B (cross-references into earlier
+    states, within); `partition`: some of them inside `partition with (k of A, k of B)`."""
     rng = random.Random(seed)
     qs = [STREAMS]
+    body = []
     for qn in range(n_queries):
         seq = rng.random() < 0.35
         n = rng.randint(2, 4)
@@ -151,8 +153,14 @@ def random_absent_app(seed, n_queries=4):
             parts[0] = "every " + parts[0]
         w = f" within {rng.choice([8, 20, 60])} milliseconds" if rng.random() < 0.5 else ""
         sep = ", " if seq else " -> "
-        qs.append(f"@info(name='a{qn}') from {sep.join(parts)}{w} "
-                  f"select {aliases[0]}.v as a, {aliases[-1]}.v as b insert into Out;")
+        body.append(f"@info(name='a{qn}') from {sep.join(parts)}{w} "
+                    f"select {aliases[0]}.v as a, {aliases[-1]}.v as b insert into Out;")
+    if partition:
+        np_ = rng.randint(1, n_queries)
+        qs.append("partition with (k of A, k of B) begin " + " ".join(body[:np_]) + " end;")
+        qs += body[np_:]
+    else:
+        qs += body
     return " ".join(qs)
 
 

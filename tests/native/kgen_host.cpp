@@ -104,7 +104,7 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
     c.ts = ts;
     c.stream = stream;
     c.init_instance();
-    c.start_instance(h->start_ts);
+    if (in->key == -1 && h->gq[in->qi].partition < 0) c.start_instance(h->start_ts);  // clones never start
     in->init = true;
   }
   c.seq = seq;
@@ -153,6 +153,7 @@ void sort_out(Host* h) {
     if (a.rank != b.rank) return a.rank < b.rank;
     if (a.rank == -1 && a.tts != b.tts) return a.tts < b.tts;
     if (a.rank == -1 && a.query != b.query) return a.query < b.query;
+    if (a.rank == -1 && a.key != b.key) return a.key < b.key;
     return a.idx < b.idx;
   });
 }
@@ -249,24 +250,31 @@ int kgh_send(void* hp, int stream, int64_t n, int64_t seq0, const int64_t* ts, c
         if (e1 == n && fresh) in = std::move(fresh);
       }
     }
+    // partitions: each event goes to its key's clones (created at the key's first event); every
+    // other key's clones with absent states only see time pass (their timers due by the event fire)
     for (size_t pi = 0; pi < h->P.parts.size(); ++pi) {
       const LPart& pd = h->P.parts[pi];
-      for (const auto& key : pd.keys) {
-        if (key.stream != stream) continue;
-        const int attr = (int)key.code[0].imm;
-        const int type = h->P.stream_types[stream][attr];
-        for (int64_t k = 0; k < n; ++k) {
-          if (nulls && nulls[k * na + attr]) continue;  // null key drops the event
-          const int64_t kv = key_of_raw(type, vals[k * na + attr]);
-          auto it = h->part[pi].find(kv);
-          if (it == h->part[pi].end()) {
+      int attr = -1;
+      for (const auto& key : pd.keys)
+        if (key.stream == stream) attr = (int)key.code[0].imm;
+      for (int64_t k = 0; k < n; ++k) {
+        bool has_key = attr >= 0 && !(nulls && nulls[k * na + attr]);  // a null key drops the event
+        int64_t kv = 0;
+        if (has_key) {
+          kv = key_of_raw(h->P.stream_types[stream][attr], vals[k * na + attr]);
+          if (h->part[pi].find(kv) == h->part[pi].end()) {
             std::vector<std::unique_ptr<Inst>> v;
             for (int pq : pd.queries) v.emplace_back(make_inst(h, pq, kv));
-            it = h->part[pi].emplace(kv, std::move(v)).first;
+            h->part[pi].emplace(kv, std::move(v));
           }
-          for (auto& in : it->second)
-            run(h, in.get(), stream, seq0 + k, ts[k], vals + k * na, nulls ? nulls + k * na : nullptr);
         }
+        for (auto& kvp : h->part[pi])
+          for (auto& in : kvp.second) {
+            if (has_key && kvp.first == kv)
+              run(h, in.get(), stream, seq0 + k, ts[k], vals + k * na, nulls ? nulls + k * na : nullptr);
+            else if (in->init && h->gq[in->qi].lay.TQ > 0)
+              run(h, in.get(), stream, seq0 + k, ts[k], nullptr, nullptr, true, false, ts[k]);
+          }
       }
     }
     if (h->window) {
@@ -321,6 +329,10 @@ int kgh_advance(void* hp, int64_t t, int64_t seq) {
     }
     for (auto& in : h->top)
       if (in && h->gq[in->qi].lay.TQ > 0) run(h, in.get(), 0, seq, t, nullptr, nullptr, true, false, t);
+    for (auto& pm : h->part)
+      for (auto& kvp : pm)
+        for (auto& in : kvp.second)
+          if (in->init && h->gq[in->qi].lay.TQ > 0) run(h, in.get(), 0, seq, t, nullptr, nullptr, true, false, t);
     sort_out(h);
     return 0;
   } catch (const std::exception& ex) {

@@ -9,8 +9,8 @@ starts at ts0 (playback apps: at 0, TimestampGeneratorImpl's initial time); time
 sleeps (a live runtime's schedulers fire meanwhile) or, in playback, with the events alone.
 
 Logical absent states (`e1=A and not B`, `not A for T or e2=B`: AbsentLogicalPre/PostStateProcessor)
-are in scope. Out of scope, and rejected at plan time: absent states inside a partition (2
-fixtures). Playback apps with a heartbeat
+and absent states inside a partition (per-key clones with their own schedulers, never start()ed)
+are in scope. Playback apps with a heartbeat
 (`@app:playback(idle.time=.., increment=..)`: event time advancing with the wall clock while idle)
 are not modelled and are skipped."""
 import json
@@ -96,4 +96,4 @@ def test_absent_kat_coverage():
     suites = {f["id"].split(".")[0] for f in FIXTURES}
     assert len(suites) == 8 and len(FIXTURES) >= 300
     in_scope = [f for f in FIXTURES if not out_of_scope(f)]
-    assert len(in_scope) >= 290
+    assert len(in_scope) >= 300

@@ -1,7 +1,8 @@
 """GPU parity of absent patterns (`not S[..] for T`) against the CPU oracle: the
 reference's own absent-suite timelines (tests/golden/reference_absent_kat.json), seeded random
 absent apps over timelines of events and idle time, batched pushes (timers firing between the events
-of one push), pool / timer-queue growth and snapshot/restore of pending timers.
+of one push), absent states inside partitions (per-key clones swept over every event), pool /
+timer-queue growth and snapshot/restore of pending timers.
 
 The device runs each absent state's scheduler inside K_gen (kgen.h fire_timers): the timers due by
 an event fire before it, sdh_engine_advance_time fires those due by a time with no event, and the
@@ -60,7 +61,7 @@ def _timeline(src, seed, factory=None, batch=False):
 @pytest.mark.parametrize("batch", [False, True], ids=["per_event", "batched"])
 @pytest.mark.parametrize("seed", range(30))
 def test_absent_fuzz_on_gpu(seed, batch):
-    src = random_absent_app(seed)
+    src = random_absent_app(seed, partition=seed % 3 == 0)  # partitions run as timer sweeps
     try:
         o = _timeline(src, seed)
     except OracleError:

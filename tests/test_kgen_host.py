@@ -183,7 +183,7 @@ def test_kgen_host_absent_fuzz(seed):
     random timeline of events and idle time: the host build of the device interpreter emits the
     oracle's matches in the oracle's order."""
     from fuzz_apps import random_absent_app
-    src = random_absent_app(seed)
+    src = random_absent_app(seed, partition=seed % 3 == 0)
     try:
         o = run_timeline(src, seed)
     except OracleError:
