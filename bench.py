@@ -396,7 +396,9 @@ def expansion(args, P, rank, K, local, dev, world, cdev, dist):
     R18-sorted tuples are then gathered to rank 0 over RCCL and merged there (siddhi_amd/dist.py)."""
     import torch
     from siddhi_amd import dist as sdist
-    E = args.expansion_batch
+    # with N GPUs every rank's tuples are gathered to rank 0: at 10K patterns per rank a 64K-event
+    # batch is ~280M matches per rank, so the multi-GPU gather runs on 2K-event batches
+    E = args.expansion_batch if world == 1 else min(args.expansion_batch, 2048)
     eng = make_engine(args.workload, P, rank * P, K, local, 0, args.partials)
     steps, warm = 4, 1
     bs = [gen_batch(args.workload, s * E, E, K, dev) for s in range(steps + warm)]
