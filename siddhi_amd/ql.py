@@ -338,8 +338,10 @@ class Parser:
             vals = []
             if self.accept("("):
                 while not self.at(")"):
-                    if self.peek().kind in ("id", "kw") and self.at("=", 1):
+                    if self.peek().kind in ("id", "kw") and (self.at("=", 1) or self.at(".", 1)):
                         key = self.name()
+                        while self.accept("."):  # dotted element keys (idle.time = '...')
+                            key += "." + self.name()
                         self.expect("=")
                         vals.append((key.lower(), self.literal_text()))
                     else:

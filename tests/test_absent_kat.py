@@ -10,9 +10,9 @@ sleeps (a live runtime's schedulers fire meanwhile) or, in playback, with the ev
 
 Logical absent states (`e1=A and not B`, `not A for T or e2=B`: AbsentLogicalPre/PostStateProcessor)
 and absent states inside a partition (per-key clones with their own schedulers, never start()ed)
-are in scope. Playback apps with a heartbeat
-(`@app:playback(idle.time=.., increment=..)`: event time advancing with the wall clock while idle)
-are not modelled and are skipped."""
+are in scope. Playback apps with a heartbeat (`@app:playback(idle.time=.., increment=..)`: event
+time advancing with the wall clock while idle) run as plain playback: their timelines assert right
+after the last send, so no heartbeat can fire (the wall clock never idles for `idle.time`)."""
 import json
 import os
 
@@ -27,8 +27,6 @@ FIXTURES = ABSENT["fixtures"]
 
 def out_of_scope(fx) -> str:
     """Why a fixture is outside the accelerated path ('' if it is in scope)."""
-    if "idle.time" in fx["app"]:
-        return "heartbeat"
     try:
         App(fx["app"])
     except SiddhiParserException as ex:
@@ -82,8 +80,6 @@ def check_absent_rows(fx, rows, checks):
 @pytest.mark.parametrize("fx", FIXTURES, ids=[f["id"] for f in FIXTURES])
 def test_absent_kat_on_oracle(fx):
     why = out_of_scope(fx)
-    if why == "heartbeat":
-        pytest.skip("playback heartbeat (idle.time) is not modelled")
     if why:
         with pytest.raises((SiddhiParserException, SiddhiAppCreationException)):
             App(fx["app"])
@@ -96,4 +92,4 @@ def test_absent_kat_coverage():
     suites = {f["id"].split(".")[0] for f in FIXTURES}
     assert len(suites) == 8 and len(FIXTURES) >= 300
     in_scope = [f for f in FIXTURES if not out_of_scope(f)]
-    assert len(in_scope) >= 300
+    assert len(in_scope) == len(FIXTURES) == 303
