@@ -412,7 +412,7 @@ __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {  // b >= 0
 }
 
 template <int KK, int XM, bool FULL, int NF>
-__global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
   using U = typename KT<KK>::U;
   constexpr bool W64 = KT<KK>::W64;
   const int lane = threadIdx.x;
@@ -704,19 +704,24 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   refresh_top();
   refresh_bottom();
 
-  int blk = -1, fill = 0;
-  unsigned long long n_emit = 0;  // records of this wave (ring mode: the blocks wrap)
-  uint2* wp = nullptr;  // next record of the wave's current output block
-  const int rsh = L.wide ? 1 : 0;  // record size: 8 B << rsh
+  // output block state: fill >= FULL_FILL forces the block check, which also catches a full output
+  constexpr int FULL_FILL = 1 << 30;
+  int blk = -1, fill = FULL_FILL;
+  unsigned long long n_emit = 0;  // records of this wave's closed blocks (ring mode: the blocks wrap)
+  uint2* wb = nullptr;            // the wave's current output block
   int64_t prev_tile_ts = (W.c0 == 0) ? L.b.prev_ts : L.b.ts[W.c0 - 1];
 
   // one record per lane with `mt` (ballot m): per-wave output blocks (one atomic per block), ranks
-  // by mbcnt. e2 = batch event `off`; e1 = the partial with low seq bits q1
+  // by mbcnt. e2 = batch event `off`; e1 = the partial with low seq bits q1. The common case costs
+  // one compare-and-branch of bookkeeping (the record index is block base + fill + rank).
   auto emit = [&](bool mt, uint64_t m, uint32_t off, uint32_t q1) {
-    if (mover) return;
     const int c = __popcll(m);
-    if (blk < 0 || fill + c > L.blk_recs) {
-      if (blk >= 0 && lane == 0) L.blk_count[blk] = fill;
+    if (fill + c > L.blk_recs) {
+      if (mover) return;
+      if (blk >= 0) {
+        if (lane == 0) L.blk_count[blk] = fill;
+        n_emit += (unsigned long long)fill;
+      }
       int nb = 0;
       if (lane == 0) nb = atomicAdd(L.blk_next, 1);
       nb = __builtin_amdgcn_readfirstlane(nb);
@@ -724,21 +729,20 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
       if (nb >= L.n_blocks) {
         blk = -1;
         mover = true;
+        fill = FULL_FILL;
         return;
       }
       if (lane == 0) L.blk_group[nb] = W.g;
       blk = nb;
       fill = 0;
-      wp = reinterpret_cast<uint2*>(L.match) + ((size_t)blk * L.blk_recs << rsh);
+      wb = reinterpret_cast<uint2*>(L.match) + ((size_t)blk * L.blk_recs << (L.wide ? 1 : 0));
     }
     if (mt) {
-      const int r = wave_mbcnt(m);
-      if (!L.wide) wp[r] = make_uint2(off | ((uint32_t)lane << 26), q1);
-      else reinterpret_cast<uint4*>(wp)[r] = make_uint4(off, (uint32_t)lane, q1, 0u);
+      const int r = fill + wave_mbcnt(m);
+      if (!L.wide) wb[r] = make_uint2(off | ((uint32_t)lane << 26), q1);
+      else reinterpret_cast<uint4*>(wb)[r] = make_uint4(off, (uint32_t)lane, q1, 0u);
     }
-    wp += (size_t)c << rsh;
     fill += c;
-    n_emit += (unsigned long long)c;
   };
 
   // ---- forward NFA step over the events this item emits for. Fast path: straight-line per
@@ -837,7 +841,7 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
             refresh_top();
           }
         }
-        if (p > 0 && D.n() == 0) bdead = INT64_MAX;
+        bdead = (p > 0 && D.n() == 0) ? INT64_MAX : bdead;
         // more matches are possible only where four were popped or the top was refilled
         mt = fix && x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey);
         m = __ballot(mt);
@@ -862,10 +866,9 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
       }
       const bool push = f && D.ln < ML;
       if (push) D.lput_ks(D.li(D.lbot + D.ln), x, slo);  // ts0 = ts of this batch event
-      if (push && D.n() == 0) {
-        bseq = slo;
-        bdead = sat_add(tt, within);
-      }
+      const bool first = push && D.n() == 0;
+      bseq = first ? slo : bseq;
+      bdead = first ? sat_add(tt, within) : bdead;
       D.ln += push ? 1 : 0;
       tkey = push ? x : tkey;
       tseq = push ? slo : tseq;
@@ -873,7 +876,10 @@ __global__ __launch_bounds__(64) void nfa_ratchet_kernel(RatchetLaunch L, int ML
   }
 
   // ---- outputs ----
-  if (blk >= 0 && lane == 0) L.blk_count[blk] = fill;
+  if (blk >= 0) {
+    if (lane == 0) L.blk_count[blk] = fill;
+    n_emit += (unsigned long long)fill;
+  }
   const uint64_t any_over = __ballot(overflow), any_unord = __ballot(unordered), any_aged = __ballot(aged);
   if (lane == 0) {
     if (L.ring && n_emit) atomicAdd(L.rec_total, n_emit);
