@@ -777,9 +777,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void nf
       const bool x_ok = vb & 1u;
 
       // ---- 1. lazy `within` expiry (oldest first) ----
-      if (has_within) {
+      if (!FULL || has_within) {
         if constexpr (!FULL) {
-          // timestamps non-decreasing: expired(bts, tt) <=> tt > bts + within
+          // timestamps non-decreasing: expired(bts, tt) <=> tt > bts + within. Lanes without
+          // `within` hold within = INT64_MAX, so their deadline saturates and never passes: the
+          // check needs no group-level flag (one compare and branch per event)
           if (__ballot(tt > bdead) != 0) {
             while (true) {
               const bool ex = D.n() > 0 && tt > bdead;

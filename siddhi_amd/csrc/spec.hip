@@ -31,6 +31,15 @@ std::string fmt(const char* f, ...) {
   return buf;
 }
 
+// register budget of a shape-compiled kernel: SDH_SEQ_WPE / SDH_PART_WPE = N asks for N resident
+// waves per SIMD (amdgpu_waves_per_eu); unset or 0 leaves the compiler's choice
+std::string wpe_attr(const char* env, int dflt) {
+  const char* v = getenv(env);
+  const int n = v && *v ? atoi(v) : dflt;
+  return n > 0 ? fmt("__attribute__((amdgpu_waves_per_eu(%d))) ", std::min(n, 8)) : std::string();
+}
+
+
 // hiprtc has no system headers: the fixed-width types and limits kgen.h / nfa_types.h use
 const char* const kPrelude =
     "typedef __hip_internal::int8_t int8_t;\n"
@@ -154,7 +163,8 @@ std::string seq_source(const kg::GQuery& g) {
        "int64_t within, const W& w) {\n    (void)k;\n    (void)within;\n    bool ok = true;\n";
   s += body;
   s += "    return ok;\n  }\n};\n\n";
-  s += "extern \"C\" __global__ __launch_bounds__(64) void sdh_seq_spec(sdh::SeqLaunch L) { sdh::seq_body<SpecSeq>(L); }\n";
+  s += "extern \"C\" __global__ __launch_bounds__(64) " + wpe_attr("SDH_SEQ_WPE", 0) +
+       "void sdh_seq_spec(sdh::SeqLaunch L) { sdh::seq_body<SpecSeq>(L); }\n";
   return s;
 }
 
@@ -226,9 +236,9 @@ std::string part_source(const kg::GQuery& g, const PartLayout& lay) {
   s += ld.substr(ld.find('\n') + 1);  // (load's body, with the launch argument added)
   s += fns;
   s += "};\n\n";
-  s += fmt("extern \"C\" __global__ __launch_bounds__(64) void sdh_part_spec(sdh::PartLaunch L) {\n"
+  s += fmt("extern \"C\" __global__ __launch_bounds__(64) %svoid sdh_part_spec(sdh::PartLaunch L) {\n"
            "  sdh::part_body<%d, SpecPart>(L);\n}\n",
-           lay.kind);
+           wpe_attr("SDH_PART_WPE", 0).c_str(), lay.kind);
   return s;
 }
 
