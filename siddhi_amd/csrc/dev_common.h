@@ -48,6 +48,26 @@ struct LaneOut {
   unsigned long long* rec_next;
   bool over = false;
   __device__ void close() {}
+  // nl records of `words` words each, contiguous
+  __device__ int64_t* reserve_n(int nl, int words) {
+    const int64_t tw = (int64_t)nl * words;
+    const unsigned long long o = atomicAdd(next, (unsigned long long)tw);
+    if (ring) {
+      if (tw > GEN_RING_MARGIN) return nullptr;  // (the margin holds any record the ring wraps)
+      return out + (int64_t)(o % (unsigned long long)(cap - GEN_RING_MARGIN));
+    }
+    if ((int64_t)(o + tw) > cap) {
+      over = true;
+      return nullptr;
+    }
+    const unsigned long long r = atomicAdd(rec_next, (unsigned long long)nl);
+    if ((int64_t)(r + nl) > rec_cap) {
+      over = true;
+      return nullptr;
+    }
+    for (int i = 0; i < nl; ++i) rec_off[r + i] = (int64_t)o + (int64_t)i * words;
+    return out + o;
+  }
   __device__ int64_t* reserve(int words) {
     const unsigned long long o = atomicAdd(next, (unsigned long long)words);
     if (ring) return out + (int64_t)(o % (unsigned long long)(cap - GEN_RING_MARGIN));
@@ -74,8 +94,12 @@ struct LaneOut {
 // divergent atomic add into a loop over the active lanes). Records of one call land in lane order;
 // the device match table orders rows by their keys anyway (R18). A call whose records cannot fit an
 // empty buffer reserves globally per lane, as LaneOut does.
-struct WaveOut {
-  static constexpr int CAPW = 512;             // words in the LDS buffer (4 KiB: occupancy)
+// CAPW_: words in the LDS buffer. Every flush takes two atomics on the chip-wide counters, which
+// serialise once the match rate is high (C3: 512 words -> 42 ms/step, 1536 -> 24), while a larger
+// buffer costs resident waves (4096 -> 38 ms); K_part uses 1536, K_seq 1024 (measured)
+template <int CAPW_>
+struct WaveOutT {
+  static constexpr int CAPW = CAPW_;
   static constexpr int CAPR = CAPW / 7 + 1;    // records (>= 7 words each)
   struct Shared {
     int64_t buf[CAPW];
@@ -92,6 +116,10 @@ struct WaveOut {
   LaneOut g;
   Shared* sh;
   bool over = false;
+  // ordering of the wave's own LDS accesses across lanes. The work group is one wave and a wave's
+  // LDS operations complete in issue order, so only the compiler must not move them (a wavefront-
+  // scope fence emits no wait)
+  __device__ static void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
   __device__ static unsigned long long active() { return __ballot(1); }
   __device__ static unsigned long long below() { return (1ull << __lane_id()) - 1ull; }
   __device__ void init() {
@@ -99,11 +127,11 @@ struct WaveOut {
       st(sh->used, 0);
       st(sh->nrec, 0);
     }
-    __threadfence_block();
+    wave_fence();
   }
   // copy the buffer out (active lanes cooperate)
   __device__ void flush() {
-    __threadfence_block();  // the records' LDS words are written
+    wave_fence();  // the records' LDS words are written
     const unsigned long long m = active();
     const int cnt = __popcll(m), me = __popcll(m & below()), lead = __ffsll((long long)m) - 1;
     const int n = ld(sh->used), nr = ld(sh->nrec);
@@ -120,7 +148,7 @@ struct WaveOut {
       st(sh->base, base);
       st(sh->rbase, rbase);
     }
-    __threadfence_block();
+    wave_fence();
     const int64_t base = ld(sh->base), rbase = ld(sh->rbase);
     if (base < 0) {
       g.over = true;
@@ -131,66 +159,73 @@ struct WaveOut {
       for (int i = me; i < n; i += cnt) g.out[base + i] = sh->buf[i];
       for (int i = me; i < nr; i += cnt) g.rec_off[rbase + i] = base + sh->roff[i];
     }
-    __threadfence_block();
+    wave_fence();
     st(sh->used, 0);  // (every active lane writes the same values)
     st(sh->nrec, 0);
-    __threadfence_block();
+    wave_fence();
   }
-  // this lane's record of `words` words, written by fill(int64_t* r): into the LDS buffer, or for
-  // an oversized call straight into the global buffer (two instantiations, so the LDS stores are
-  // ds_ writes, not flat ones); skipped once the global buffer overflowed
+  // `nl` records of `words` words each for this lane (collective over the active lanes: they all
+  // call it at the same point), written by fill(int64_t* r): record i at r + i * words, into the LDS
+  // buffer. A call larger than the buffer's free room goes in rounds: each round places the lanes
+  // (in lane order) whose words and records fit, then the buffer is flushed. Only a lane whose own
+  // records exceed the whole buffer reserves globally, as LaneOut does.
+  template <class F>
+  __device__ void emit_n(int nl, int words, F&& fill) {
+    const unsigned long long lt = below();
+    const bool big = nl * words > CAPW || nl > CAPR;
+    const int mtw = big ? 0 : nl * words, mnl = big ? 0 : nl;
+    int wpre = 0, wtot = 0, rpre = 0;  // exclusive lane prefixes, total words (ballot bits)
+#pragma unroll
+    for (int b = 0; b < 13; ++b) {  // mtw <= CAPW
+      const unsigned long long mb = __ballot((mtw >> b) & 1);
+      wpre += __popcll(mb & lt) << b;
+      wtot += __popcll(mb) << b;
+    }
+#pragma unroll
+    for (int b = 0; b < 10; ++b) {  // mnl <= CAPR
+      const unsigned long long mb = __ballot((mnl >> b) & 1);
+      rpre += __popcll(mb & lt) << b;
+    }
+    int wdone = 0, rdone = 0;  // (uniform) words / records of this call placed so far
+    while (wdone < wtot) {
+      const int used = ld(sh->used), nr = ld(sh->nrec);
+      const bool fits = mnl > 0 && wpre >= wdone && wpre + mtw - wdone <= CAPW - used &&
+                        rpre + mnl - rdone <= CAPR - nr;
+      const unsigned long long fm = __ballot(fits);
+      if (!fm) {  // not even the first pending lane fits: empty the buffer
+        flush();
+        continue;
+      }
+      // the fitting lanes are a prefix of the pending ones (the prefix sums are monotone)
+      const int hi = 63 - __builtin_clzll(fm);
+      const int wend = __builtin_amdgcn_readlane(wpre + mtw, hi), rend = __builtin_amdgcn_readlane(rpre + mnl, hi);
+      const int off = used + wpre - wdone, r0 = nr + rpre - rdone;
+      if (fits)
+        for (int i = 0; i < mnl; ++i) sh->roff[r0 + i] = off + i * words;
+      wave_fence();
+      st(sh->used, used + wend - wdone);  // (every active lane writes the same values)
+      st(sh->nrec, nr + rend - rdone);
+      if (fits) fill(sh->buf + off);
+      wdone = wend;
+      rdone = rend;
+    }
+    if (big) {
+      int64_t* r = g.reserve_n(nl, words);
+      if (r) fill(r);
+    }
+  }
+  // this lane's record of `words` words, written by fill(int64_t* r)
   template <class F>
   __device__ void emit(int words, F&& fill) {
-    const unsigned long long m = active(), lt = below();
-    const int cnt = __popcll(m), rank = __popcll(m & lt);
-    int prefix = 0, total = 0;
-#pragma unroll
-    for (int b = 0; b < 6; ++b) {
-      const unsigned long long mb = __ballot((words >> b) & 1);
-      prefix += __popcll(mb & lt) << b;
-      total += __popcll(mb) << b;
-    }
-    if (__ballot(words >= 64) || total > CAPW || cnt > CAPR) {  // (uniform)
-      int64_t* r = g.reserve(words);
-      if (r) fill(r);
-      return;
-    }
-    if (ld(sh->used) + total > CAPW || ld(sh->nrec) + cnt > CAPR) flush();
-    const int base = ld(sh->used), nr = ld(sh->nrec);
-    const int off = base + prefix;
-    sh->roff[nr + rank] = off;
-    __threadfence_block();
-    st(sh->used, base + total);  // (every active lane writes the same values)
-    st(sh->nrec, nr + cnt);
-    fill(sh->buf + off);
-  }
-  // room for this lane's record of `words` words: a pointer into the LDS buffer (or, for an
-  // oversized call, into the global buffer); nullptr once the global buffer overflowed
-  __device__ int64_t* reserve(int words) {
-    const unsigned long long m = active(), lt = below();
-    const int cnt = __popcll(m), rank = __popcll(m & lt);
-    int prefix = 0, total = 0;
-#pragma unroll
-    for (int b = 0; b < 6; ++b) {
-      const unsigned long long mb = __ballot((words >> b) & 1);
-      prefix += __popcll(mb & lt) << b;
-      total += __popcll(mb) << b;
-    }
-    if (__ballot(words >= 64) || total > CAPW || cnt > CAPR) return g.reserve(words);  // (uniform)
-    if (ld(sh->used) + total > CAPW || ld(sh->nrec) + cnt > CAPR) flush();
-    const int base = ld(sh->used), nr = ld(sh->nrec);
-    const int off = base + prefix;
-    sh->roff[nr + rank] = off;
-    __threadfence_block();
-    st(sh->used, base + total);  // (every active lane writes the same values)
-    st(sh->nrec, nr + cnt);
-    return sh->buf + off;
+    emit_n(1, words, fill);
   }
   __device__ void close() {
     flush();
     over |= g.over;
   }
 };
+using WaveOut = WaveOutT<1536>;    // K_part
+using SeqWaveOut = WaveOutT<1024>; // K_seq
 
 __device__ __forceinline__ bool expired(int64_t ts1, int64_t ts, int64_t within) {
   if (within < 0) return false;

@@ -184,6 +184,10 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
   const int stream = L.b.stream;
   const int ncap = q->n_cap[stream];
   const int64_t within = ql->within;
+  // loaded once: a per-lane global load inside the event loop would wait (vmcnt is in order) for
+  // every record store issued before it
+  const int64_t qid = ql->qid;
+  const int cmin = q->st[1].min, cmax = q->st[1].max;  // PK_COUNT: this shape's <min:max>
   const int64_t key = L.key_of_id[kid];
   const int ew = RC > 0 ? EW : L.ew;
   const int64_t bw = PK_HDR + (int64_t)L.cap * ew;
@@ -266,54 +270,69 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
           F = Fw;
           if (F == 0) side = 0;
         }
-        auto emit = [&](int64_t e1seq, int64_t a_seq, int64_t b_seq) {  // a_seq / b_seq: -1 = empty slot
-          ++nrec;
-          if (!L.write_records) return;
-          const int words = 7 + 2 + (a_seq >= 0 ? 2 : 1) + (b_seq >= 0 ? 2 : 1);
-          const int64_t my_idx = idx++;
-          o.emit(words, [&](int64_t* r) {
-            r[0] = words;
-            r[1] = ql->qid;
-            r[2] = key;
-            r[3] = ts;
-            r[4] = seq;
-            r[5] = my_idx;
-            r[6] = 3 | (stream << 16);
-            int p = 7;
-            for (int s = 0; s < 3; ++s) {
-              const int64_t v = s == 0 ? e1seq : s == sA ? a_seq : b_seq;
-              if (v >= 0) {
-                r[p++] = 1;
-                r[p++] = v;
-              } else {
-                r[p++] = 0;
-              }
+        // one match record at r: [words, qid, key, ts, seq, idx, 3 | stream, (1, seq) | (0) per slot]
+        // (a_seq / b_seq -1: empty slot)
+        auto put_rec = [&](int64_t* r, int words, int64_t my_idx, int64_t e1seq, int64_t a_seq, int64_t b_seq) {
+          r[0] = words;
+          r[1] = qid;
+          r[2] = key;
+          r[3] = ts;
+          r[4] = seq;
+          r[5] = my_idx;
+          r[6] = 3 | (stream << 16);
+          int p = 7;
+          for (int s = 0; s < 3; ++s) {
+            const int64_t v = s == 0 ? e1seq : s == sA ? a_seq : b_seq;
+            if (v >= 0) {
+              r[p++] = 1;
+              r[p++] = v;
+            } else {
+              r[p++] = 0;
             }
-          });
+          }
         };
+        // The lane's matches of this event are the first c partials of its list (see the two cases
+        // below): their records go out in one collective reservation, record kk at r0 + kk * words
+        // with emission index kk (the pending-list order)
+        (void)idx;
         if constexpr (KIND == PK_OR) {
           // side B first (its processor runs first), then side A; either empties the list
           if (fb || fa) {
-            tab.each(n, [&](int, const auto& e) { emit(e.get(1), fb ? -1 : seq, fb ? seq : -1); });
+            nrec += n;
+            if (L.write_records) {
+              const int64_t as = fb ? -1 : seq, bs = fb ? seq : -1;  // words: 7 + 2 + 2 + 1
+              o.emit_n(n, 12, [&](int64_t* r0) {
+                tab.each(n, [&](int kk, const auto& e) { put_rec(r0 + kk * 12, 12, kk, e.get(1), as, bs); });
+              });
+            }
             n = 0;
           }
         } else if (fb || fa) {
           // AND. B pass: partials filled on A complete (a = fill, b = x); empty ones get b = x.
           // A pass: partials filled on B (old and new) complete (a = x). Both passes walk the list
-          // in creation order and every completed partial precedes every surviving one, so one walk
-          // in list order emits in the reference's order.
+          // in creation order and every completed partial precedes every surviving one: with both
+          // sides passing all n complete, with one side the F partials filled on the other side.
+          const int c = (fa && fb) ? n : ((fb && side == 1) || (fa && side == 2)) ? F : 0;
+          nrec += c;
+          if (L.write_records) {
+            o.emit_n(c, 13, [&](int64_t* r0) {  // words: 7 + 2 + 2 + 2
+              tab.each(c, [&](int kk, const auto& e) {
+                const bool filled = kk < F;
+                const int64_t aseq = (filled && side == 1) ? e.get(2) : seq;
+                const int64_t bseq = (filled && side == 2) ? e.get(2) : seq;
+                put_rec(r0 + kk * 13, 13, kk, e.get(1), aseq, bseq);
+              });
+            });
+          }
           int w = 0;
           tab.each(n, [&](int kk, const auto& e) {
+            if (kk < c) return;
             const bool filled = kk < F;
             int64_t aseq = -1, bseq = -1;
             if (filled && side == 1) aseq = e.get(2);
             if (filled && side == 2) bseq = e.get(2);
             if (fb && bseq < 0) bseq = seq;  // B pass: the partials whose B slot is empty
             if (fa && aseq < 0) aseq = seq;  // A pass: those whose A slot is empty (B-filled too)
-            if (aseq >= 0 && bseq >= 0) {
-              emit(e.get(1), aseq, bseq);
-              return;
-            }
             // survivor: exactly one side filled
             e.set(2, aseq >= 0 ? aseq : bseq);
             if (w != kk) tab.put(w, e, 3);
@@ -335,7 +354,6 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
         }
       } else {  // PK_COUNT
         const bool f2 = Spec::f2(k, q, ql, L, ev);
-        const int cmin = q->st[1].min, cmax = q->st[1].max;  // this shape's <min:max>
         const int ewc = 3 + of.cmax + of.n_e1 + of.n_first + of.n_last;
         int w = 0;
         tab.each(n, [&](int kk, const auto& e) {
@@ -354,7 +372,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
                 const int64_t my_idx = idx++;
                 o.emit(words, [&](int64_t* r) {
                   r[0] = words;
-                  r[1] = ql->qid;
+                  r[1] = qid;
                   r[2] = key;
                   r[3] = ts;
                   r[4] = seq;

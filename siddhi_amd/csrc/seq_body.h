@@ -40,6 +40,7 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
   const int stream = L.b.stream;
   const int na = q->n_cap[stream];
   const int64_t within = ql->within;
+  const int64_t qid = ql->qid;  // (a per-lane load in the loop would wait for the record stores)
   // window index w: tail rows 0 .. tail_len-1, then batch event w - tail_len. Start s is evaluated
   // by the batch holding its last event s + S - 1.
   const int64_t W = L.tail_len + L.b.n;
@@ -47,8 +48,8 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
   const int64_t s_end = W - S + 1;
   int64_t lo = s_begin + (int64_t)chunk * L.chunk_len;
   int64_t hi = lo + L.chunk_len < s_end ? lo + L.chunk_len : s_end;
-  __shared__ dev::WaveOut::Shared out_sh;
-  dev::WaveOut o;
+  __shared__ dev::SeqWaveOut::Shared out_sh;
+  dev::SeqWaveOut o;
   o.g = dev::LaneOut{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
   o.sh = &out_sh;
   o.init();
@@ -105,7 +106,7 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
     const int words = 7 + 2 * S;
     o.emit(words, [&](int64_t* r) {
       r[0] = words;
-      r[1] = ql->qid;
+      r[1] = qid;
       r[2] = -1;
       r[3] = wv.base[(S - 1) * SEQ_ROW];      // ts of the last event
       r[4] = wv.base[(S - 1) * SEQ_ROW + 1];  // the triggering event's seq
