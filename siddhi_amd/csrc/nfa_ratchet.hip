@@ -412,7 +412,7 @@ __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {  // b >= 0
 }
 
 template <int KK, int XM, bool FULL, int NF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
   using U = typename KT<KK>::U;
   constexpr bool W64 = KT<KK>::W64;
   const int lane = threadIdx.x;
