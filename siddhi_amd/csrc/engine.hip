@@ -1076,6 +1076,14 @@ int64_t ratchet_count_matches(sdh_engine* e) {
 // one NFA step of every ratchet group fed by `stream` over batch B (exact re-runs on overflow /
 // out-of-order timestamps: the groups' input deques are double-buffered and untouched until the
 // launch succeeds)
+// f0 atoms a K_ratchet launch variant must handle: the one-atom variant assumes a constant
+// interval, so a group with a two-column atom (`cur.a OP cur.b`) takes the general variant
+int ratchet_nf(const sdh::RatchetGroup& g) {
+  for (int a = 0; a < g.n_f0; ++a)
+    if (g.f0[a].cur2) return sdh::RMAXF0;
+  return g.n_f0;
+}
+
 void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2]) {
   e->r_blocks_used = 0;
   e->r_matches = 0;
@@ -1117,7 +1125,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       size_t i1 = i0;
       int nf = 0;
       while (i1 < order.size() && e->rg[order[i1]].key_kind == G0.key_kind && e->rg[order[i1]].xmask == G0.xmask)
-        nf = std::max(nf, e->rg[order[i1++]].n_f0);
+        nf = std::max(nf, ratchet_nf(e->rg[order[i1++]]));
       double slots = e->r_waves;
       if (slots <= 0) {
         const int occ = sdh_ratchet_occupancy(G0.key_kind, full, nf, e->rML);
@@ -1210,7 +1218,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       Ls.items = e->d_ritems.p + i0;
       Ls.n_items = i1 - i0;
       int nf = 0;
-      for (int i = i0; i < i1; ++i) nf = std::max(nf, e->rg[e->ritems[i].g].n_f0);
+      for (int i = i0; i < i1; ++i) nf = std::max(nf, ratchet_nf(e->rg[e->ritems[i].g]));
       // spill regions are indexed by the item's position in its launch
       Ls.spillA = e->d_rspillA.p + (size_t)i0 * e->rSC * WAVE;
       Ls.lds_ts = e->d_rlts.p + (size_t)i0 * e->rML * WAVE;

@@ -441,6 +441,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
   const int n_f0 = G->n_f0;
   const int xmask = G->xmask, kconv = G->key_conv, kattr = G->key_attr;
   const bool is_max = (xmask & CM_GT) != 0;
+  // one-atom launches carry only constant-interval atoms (the host routes groups with a two-column
+  // atom to the general variant), so their per-event start filter has no operand-kind branch
+  constexpr bool IV = (NF == 1);
   // f0 atoms: constant atoms become per-lane intervals of sortable keys; two-column atoms stay
   // generic compares. Operand columns are resolved once (wave-uniform).
   int64_t f_lo[NF], f_hi[NF];
@@ -497,7 +500,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
       if (a < n_f0 && live) {
         r.f[a] = load_raw(f_ptr[a], f_w[a], e);
         bool n1 = f_nul[a] && f_nul[a][e];
-        if (f_cur2[a]) {
+        if (!IV && f_cur2[a]) {
           r.f2[a] = load_raw(f_ptr2[a], f_w2[a], e);
           n1 = n1 || (f_nul2[a] && f_nul2[a][e]);
         }
@@ -516,7 +519,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
       fk2[a] = 0;
       if (a < n_f0 && r.live) {
         const int64_t k1 = to_key(r.f[a], f_conv[a]);
-        if (f_cur2[a]) {
+        if (!IV && f_cur2[a]) {
           fk[a] = k1;
           fk2[a] = to_key(r.f2[a], f_conv2[a]);
         } else {
@@ -540,7 +543,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
         const int64_t v = readlane64(fk[a], k);
         const bool cn = (vb >> (1 + a)) & 1u;
         bool r;
-        if (f_cur2[a]) r = cmp_keys(f_mask[a], f_f64[a], v, readlane64(fk2[a], k));
+        if (!IV && f_cur2[a]) r = cmp_keys(f_mask[a], f_f64[a], v, readlane64(fk2[a], k));
         else r = ((v >= f_lo[a]) && (v <= f_hi[a])) != f_neg[a];
         ok = ok && !cn && r;
       }
