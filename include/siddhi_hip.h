@@ -138,6 +138,7 @@ typedef struct sdh_stats {
                              /* SDH_SPEC=0 off, 1 every shape, default shapes of >= 128 queries) */
   int64_t pool_regrows;      /* K_gen pool / list growths (each re-lays the arenas and re-runs   */
                              /* the push that overflowed; the reference's lists are unbounded)   */
+  int64_t last_slab_items;   /* K_slab work items of the last push: key segments x groups         */
 } sdh_stats;
 
 int sdh_engine_create(const void* ir_blob, size_t len, const sdh_config* cfg, sdh_engine** out);
@@ -157,6 +158,10 @@ int sdh_engine_pending_matches(sdh_engine* e, int64_t* n);
 int sdh_engine_start(sdh_engine* e, int64_t t);
 int sdh_engine_advance_time(sdh_engine* e, int64_t t);
 int sdh_engine_stats(sdh_engine* e, sdh_stats* out);
+/* Device memory of the sparse per-partial state (K_slab: partitioned distinct-stream patterns,
+ * state only for instances that hold partials -- PartitionRuntime.java:257-306 clones per key
+ * lazily): live entry bytes, reserved slab bytes, directory bytes. */
+int sdh_engine_state_bytes(sdh_engine* e, int64_t* live_bytes, int64_t* reserved_bytes, int64_t* dir_bytes);
 int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len);
 int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len);
 void sdh_free(void* p);

@@ -22,11 +22,22 @@
 #include "../../include/siddhi_hip.h"
 #include "gen_lower.h"
 #include "nfa_types.h"
+#include "slab_lower.h"
 #include "spec.h"
 
 extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s);
 extern "C" hipError_t sdh_launch_part(const sdh::PartLaunch* L, hipStream_t s);
 extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, hipStream_t s);
+extern "C" hipError_t sdh_launch_slab(const sdh::SlabLaunch* L, hipStream_t s);
+extern "C" hipError_t sdh_slab_rollback(uint64_t* dir, const uint64_t* journal, const uint64_t* journal_idx, int64_t n,
+                                        const long long* live_bak, long long* live, hipStream_t s);
+extern "C" hipError_t sdh_slab_move(uint64_t* dir, int64_t n_dir, int groups, const int32_t* group_ew,
+                                    const uint32_t* src, int64_t src_cap, const unsigned long long* src_tail,
+                                    const unsigned long long* limit, uint32_t* dst, int64_t dst_cap, int dst_nsub,
+                                    unsigned long long* dst_head, const unsigned long long* dst_tail, int32_t* err,
+                                    hipStream_t s);
+extern "C" hipError_t sdh_slab_live_words(const uint64_t* dir, int64_t n_dir, int groups, const int32_t* group_ew,
+                                          unsigned long long* acc, hipStream_t s);
 extern "C" hipError_t sdh_seq_tail(const sdh::StreamBatch* b, int64_t* tail, int32_t tail_len, int32_t new_tail_len,
                                    hipStream_t s);
 extern "C" hipError_t sdh_route_partition(const sdh::StreamBatch* B, int attr, int type, unsigned long long* tkey,
@@ -661,6 +672,35 @@ struct sdh_engine {
     std::map<int, hipFunction_t> spec;  // shape template -> shape-compiled kernel (spec.h)
   };
   std::vector<std::unique_ptr<PartSet>> psets;
+  // K_slab (nfa_slab.hip): one set per partition; its queries' partials as sparse entries, one block
+  // per (key, group) in nsub sub-rings of a slab, found through the directory [key][group]
+  struct SlabSet {
+    int partition = -1;
+    int group_base = 0, n_groups = 0;
+    int64_t key_cap = 0;
+    std::vector<slab::Shape> shapes;
+    std::vector<int32_t> group_shape, group_ew;
+    DevBuf<slab::Shape> d_shapes;
+    DevBuf<int32_t> d_group_shape, d_group_ew;
+    std::vector<std::vector<int32_t>> glist;  // [stream] set groups reading it
+    std::vector<DevBuf<int32_t>> d_glist;
+    DevBuf<uint64_t> dir;                     // [key_cap * n_groups]
+    DevBuf<uint32_t> slab;                    // nsub * sub_cap words
+    int nsub = 256;
+    int64_t sub_cap = 0;
+    DevBuf<unsigned long long> head, tail, head_bak;
+    std::vector<unsigned long long> h_head, h_tail;
+    DevBuf<long long> live, live_bak;
+    DevBuf<unsigned long long> traffic;       // block bytes read + written by the last launch
+    DevBuf<uint64_t> journal, journal_idx;
+    int64_t items = 0;                        // items of this pass's launch (0: not launched)
+    int lds_words = 4096;
+    int64_t last_alloc = 0;                   // largest one-push allocation of a sub-ring (words)
+    int64_t cleanings = 0, growths = 0;
+  };
+  std::vector<std::unique_ptr<SlabSet>> ssets;
+  DevBuf<int32_t> d_serr;            // per K_slab set: [0] LDS capacity, [1] slab space, [2] output overflow
+  int64_t slab_items = 0;            // K_slab work items of the last push
   DevBuf<int32_t> d_perr;            // per K_part set: [0] entry capacity, [2] output overflow
   DevBuf<unsigned long long> d_pprof;  // SDH_PART_PROF measurement builds: phase clocks
   DevBuf<int64_t> r_key;
@@ -1416,6 +1456,151 @@ void spec_build(sdh_engine* e) {
   e->stats.spec_kernels = n;
 }
 
+// ------------------------------------------------------------------------------------------
+// K_slab host side (nfa_slab.hip): directory growth with the key table, slab space (reclaiming a
+// sub-ring's oldest half, growing), rollback of a failed push
+// ------------------------------------------------------------------------------------------
+void slab_heads(sdh_engine* e, sdh_engine::SlabSet& ss) {
+  ss.h_head.resize(ss.nsub);
+  HIPCHK(hipMemcpyAsync(ss.h_head.data(), ss.head.p, ss.nsub * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+}
+
+// a fresh, empty slab of nsub sub-rings of `sub_cap` words
+void slab_init(sdh_engine* e, sdh_engine::SlabSet& ss, int64_t sub_cap) {
+  ss.sub_cap = (sub_cap + 3) & ~3ll;
+  ss.slab.ensure((size_t)ss.nsub * ss.sub_cap);
+  ss.head.ensure(ss.nsub);
+  ss.tail.ensure(ss.nsub);
+  ss.head_bak.ensure(ss.nsub);
+  HIPCHK(hipMemset(ss.head.p, 0, ss.nsub * 8));
+  HIPCHK(hipMemset(ss.tail.p, 0, ss.nsub * 8));
+  ss.h_head.assign(ss.nsub, 0);
+  ss.h_tail.assign(ss.nsub, 0);
+  ss.live.ensure(256);
+  ss.live_bak.ensure(256);
+  ss.traffic.ensure(256);
+  HIPCHK(hipMemset(ss.live.p, 0, 256 * 8));
+  (void)e;
+}
+
+// directory room for `keys` keys (key-major: the old entries are a prefix; new keys' blocks empty)
+void slab_grow_keys(sdh_engine* e, sdh_engine::SlabSet& ss, int64_t keys) {
+  if (keys <= ss.key_cap) return;
+  int64_t cap = std::max<int64_t>(64, ss.key_cap);
+  while (cap < keys) cap *= 2;
+  const size_t old_n = (size_t)ss.key_cap * ss.n_groups, new_n = (size_t)cap * ss.n_groups;
+  DevBuf<uint64_t> nd;
+  if (hipMalloc(&nd.p, new_n * 8) != hipSuccess)
+    throw Error(SDH_E_CAPACITY, fmt("device memory exhausted growing the K_slab directory to %lld keys", (long long)cap));
+  nd.n = new_n;
+  HIPCHK(hipMemsetAsync(nd.p + old_n, 0, (new_n - old_n) * 8, e->stream));
+  if (old_n) HIPCHK(hipMemcpyAsync(nd.p, ss.dir.p, old_n * 8, hipMemcpyDeviceToDevice, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  std::swap(ss.dir.p, nd.p);
+  std::swap(ss.dir.n, nd.n);
+  ss.key_cap = cap;
+}
+
+// move the live blocks at sub-ring positions < limit[sub] to the head of their destination ring;
+// false when a destination ring ran out of room (nothing is lost: a block keeps its old place
+// until its directory entry moves)
+bool slab_move(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<unsigned long long>& limit, uint32_t* dst,
+               int64_t dst_cap, int dst_nsub, unsigned long long* dst_head, const unsigned long long* dst_tail,
+               uint64_t* dir = nullptr, const uint32_t* src = nullptr, int64_t src_cap = 0,
+               const unsigned long long* src_tail = nullptr) {
+  DevBuf<unsigned long long> d_lim;
+  d_lim.ensure(limit.size());
+  HIPCHK(hipMemcpyAsync(d_lim.p, limit.data(), limit.size() * 8, hipMemcpyHostToDevice, e->stream));
+  e->d_err.ensure(4);
+  HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
+  HIPCHK(sdh_slab_move(dir ? dir : ss.dir.p, ss.key_cap * ss.n_groups, ss.n_groups, ss.d_group_ew.p,
+                       src ? src : ss.slab.p, src ? src_cap : ss.sub_cap, src ? src_tail : ss.tail.p, d_lim.p, dst,
+                       dst_cap, dst_nsub, dst_head, dst_tail, e->d_err.p, e->stream));
+  int32_t err = 0;
+  HIPCHK(hipMemcpyAsync(&err, e->d_err.p, 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return err == 0;
+}
+
+// a slab of sub-rings of (at least) want words each, holding every live block
+void slab_grow(sdh_engine* e, sdh_engine::SlabSet& ss, int64_t want) {
+  const int64_t nc = (std::max<int64_t>(want, 2 * ss.sub_cap) + 3) & ~3ll;
+  DevBuf<uint32_t> ns;
+  DevBuf<unsigned long long> nh, nt;
+  if (hipMalloc(&ns.p, (size_t)ss.nsub * nc * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    throw Error(SDH_E_CAPACITY, fmt("device memory exhausted growing the K_slab slab to %.1f GB",
+                                    (double)ss.nsub * nc * 4 / 1e9));
+  }
+  ns.n = (size_t)ss.nsub * nc;
+  nh.ensure(ss.nsub);
+  nt.ensure(ss.nsub);
+  HIPCHK(hipMemsetAsync(nh.p, 0, ss.nsub * 8, e->stream));
+  HIPCHK(hipMemsetAsync(nt.p, 0, ss.nsub * 8, e->stream));
+  std::vector<unsigned long long> all(ss.nsub, ~0ull);
+  if (!slab_move(e, ss, all, ns.p, nc, ss.nsub, nh.p, nt.p))
+    throw Error(SDH_E_CAPACITY, "K_slab: a sub-ring overflowed while the slab grew");
+  std::swap(ss.slab.p, ns.p);
+  std::swap(ss.slab.n, ns.n);
+  std::swap(ss.head.p, nh.p);
+  std::swap(ss.tail.p, nt.p);
+  ss.sub_cap = nc;
+  ss.h_tail.assign(ss.nsub, 0);
+  slab_heads(e, ss);
+  ++ss.growths;
+}
+
+// room for the next push: a sub-ring with less than `reserve` words free has its oldest half
+// reclaimed (its live blocks move to its head); if that is not enough the slab grows
+void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss) {
+  const int64_t reserve = std::max<int64_t>(2 * ss.last_alloc, 4096);
+  auto free_min = [&]() {
+    int64_t f = INT64_MAX, used = 0;
+    for (int r = 0; r < ss.nsub; ++r) {
+      const int64_t u = (int64_t)(ss.h_head[r] - ss.h_tail[r]);
+      f = std::min(f, ss.sub_cap - u);
+      used = std::max(used, u);
+    }
+    return std::make_pair(f, used);
+  };
+  auto [f, used] = free_min();
+  if (f >= reserve) return;
+  std::vector<unsigned long long> limit(ss.nsub);
+  for (int r = 0; r < ss.nsub; ++r) limit[r] = ss.h_tail[r] + (ss.h_head[r] - ss.h_tail[r]) / 2;
+  bool ok = ss.sub_cap >= 2 * reserve && slab_move(e, ss, limit, ss.slab.p, ss.sub_cap, ss.nsub, ss.head.p, ss.tail.p);
+  if (ok) {
+    ss.h_tail = limit;
+    HIPCHK(hipMemcpyAsync(ss.tail.p, limit.data(), ss.nsub * 8, hipMemcpyHostToDevice, e->stream));
+    slab_heads(e, ss);
+    ++ss.cleanings;
+    std::tie(f, used) = free_min();
+    if (f >= reserve && used <= ss.sub_cap / 2) return;
+  } else {
+    slab_heads(e, ss);
+    std::tie(f, used) = free_min();
+  }
+  slab_grow(e, ss, 2 * (used + reserve));
+}
+
+// undo this pass's launch of the set (its directory changes; its allocations are dropped)
+void slab_rollback(sdh_engine* e, sdh_engine::SlabSet& ss) {
+  if (ss.items <= 0) return;
+  HIPCHK(sdh_slab_rollback(ss.dir.p, ss.journal.p, ss.journal_idx.p, ss.items, ss.live_bak.p, ss.live.p, e->stream));
+  HIPCHK(hipMemcpyAsync(ss.head.p, ss.head_bak.p, ss.nsub * 8, hipMemcpyDeviceToDevice, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  ss.items = 0;
+}
+
+int64_t slab_live_partials(sdh_engine* e, const sdh_engine::SlabSet& ss) {
+  long long v[256];
+  HIPCHK(hipMemcpyAsync(v, ss.live.p, sizeof v, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  int64_t n = 0;
+  for (long long x : v) n += x;
+  return n;
+}
+
 void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   kg::Sizing sz;
   if (e->cfg.gen_pool_states > 0) sz.R = std::min(kg::GMAXPOOL, e->cfg.gen_pool_states);
@@ -1424,7 +1609,9 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   e->gsz = sz;
   std::vector<int> gidx(e->lp.q.size(), -1);
   std::vector<KPart> kpart(e->lp.q.size());
+  std::vector<char> is_slab(e->lp.q.size(), 0);
   const bool use_part = !(e->cfg.flags & SDH_FLAG_FORCE_GEN) && !getenv("SDH_NO_KPART");
+  const bool use_slab = !(e->cfg.flags & SDH_FLAG_FORCE_GEN) && !getenv("SDH_NO_KSLAB");
   for (int qi : qis) {
     try {
       kg::GQuery g = kg::lower_gen(e->lp, qi, sz);
@@ -1433,9 +1620,13 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
       gidx[qi] = (int)e->gq.size();
       e->gq.push_back(g);
       if (use_part) kpart[qi] = kpart_shape(e->lp, qi, g);
-      e->gq_arena.push_back(kpart[qi].kind < 0);
+      if (use_slab && kpart[qi].kind < 0) {
+        slab::Shape sh;
+        is_slab[qi] = slab::shape_of_query(e->lp, qi, g, &sh, nullptr) ? 1 : 0;
+      }
+      e->gq_arena.push_back(kpart[qi].kind < 0 && !is_slab[qi]);
       e->has_absent |= g.lay.TQ > 0;
-      if (kpart[qi].kind >= 0) continue;  // K_part: no K_gen arena
+      if (kpart[qi].kind >= 0 || is_slab[qi]) continue;  // K_part / K_slab: no K_gen arena
       e->gB32 = std::max(e->gB32, g.lay.n32);
       e->gB64 = std::max(e->gB64, g.lay.n64);
       e->gHotS = std::max(e->gHotS, g.lay.S);
@@ -1518,13 +1709,63 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
       e->psets.push_back(std::move(ps));
     }
   };
+  // K_slab: a partition's distinct-stream patterns in one set (slab.h), groups bucketed by shape
+  auto add_slab_set = [&](int partition, const std::vector<int>& members) {
+    std::vector<int> m;
+    for (int qi : members)
+      if (is_slab[qi]) m.push_back(qi);
+    if (m.empty()) return;
+    route_of(partition);
+    auto ss = std::make_unique<sdh_engine::SlabSet>();
+    ss->partition = partition;
+    ss->group_base = (int)(e->lane_q.size() / 64);
+    ss->n_groups = add_groups(m, false);
+    std::map<int, int> shape_of_tmpl;
+    for (int g = 0; g < ss->n_groups; ++g) {
+      const int t = e->group_tmpl[ss->group_base + g];
+      auto it = shape_of_tmpl.find(t);
+      if (it == shape_of_tmpl.end()) {
+        slab::Shape sh;
+        std::string why;
+        if (!slab::shape_of_query(e->lp, e->gq[t].qid, e->gq[t], &sh, &why))
+          throw Error(SDH_E_UNSUPPORTED, "K_slab shape: " + why);
+        it = shape_of_tmpl.emplace(t, (int)ss->shapes.size()).first;
+        ss->shapes.push_back(sh);
+      }
+      ss->group_shape.push_back(it->second);
+      ss->group_ew.push_back(ss->shapes[it->second].EW);
+    }
+    const int ns = (int)e->prog.stream_types.size();
+    ss->glist.assign(ns, {});
+    ss->d_glist.resize(ns);
+    for (int g = 0; g < ss->n_groups; ++g)
+      for (int st = 0; st < ns && st < kg::GMAXSTREAM; ++st)
+        if (ss->shapes[ss->group_shape[g]].proc[st] >= 0) ss->glist[st].push_back(g);
+    for (int st = 0; st < ns; ++st) {
+      ss->d_glist[st].ensure(std::max<size_t>(1, ss->glist[st].size()));
+      if (!ss->glist[st].empty())
+        HIPCHK(hipMemcpy(ss->d_glist[st].p, ss->glist[st].data(), ss->glist[st].size() * 4, hipMemcpyHostToDevice));
+    }
+    ss->d_shapes.ensure(ss->shapes.size());
+    HIPCHK(hipMemcpy(ss->d_shapes.p, ss->shapes.data(), ss->shapes.size() * sizeof(slab::Shape), hipMemcpyHostToDevice));
+    ss->d_group_shape.ensure(ss->n_groups);
+    HIPCHK(hipMemcpy(ss->d_group_shape.p, ss->group_shape.data(), ss->n_groups * 4, hipMemcpyHostToDevice));
+    ss->d_group_ew.ensure(ss->n_groups);
+    HIPCHK(hipMemcpy(ss->d_group_ew.p, ss->group_ew.data(), ss->n_groups * 4, hipMemcpyHostToDevice));
+    if (const char* v = getenv("SDH_SLAB_LDS_WORDS")) ss->lds_words = std::max(64, atoi(v));
+    int64_t sub = 1 << 16;  // words per sub-ring; grows on demand (slab_prepare)
+    if (const char* v = getenv("SDH_SLAB_SUB_WORDS")) sub = std::max<int64_t>(64, atoll(v));
+    slab_init(e, *ss, sub);
+    e->ssets.push_back(std::move(ss));
+  };
   // sets: the unpartitioned queries, then one per partition; 64 queries per group (wave)
   auto add_set = [&](int partition, const std::vector<int>& members) {
     if (members.empty()) return;
     std::vector<int> gen_m;
     for (int qi : members)
-      if (kpart[qi].kind < 0) gen_m.push_back(qi);
+      if (kpart[qi].kind < 0 && !is_slab[qi]) gen_m.push_back(qi);
     if (partition >= 0) add_part_sets(partition, members);
+    if (partition >= 0) add_slab_set(partition, members);
     if (gen_m.empty()) return;
     auto gs = std::make_unique<sdh_engine::GenSet>();
     gs->partition = partition;
@@ -1572,6 +1813,7 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   e->g_out_next.ensure(1);
   e->g_nrec.ensure(1);
   e->d_perr.ensure(std::max<size_t>(1, e->psets.size()) * 4);
+  e->d_serr.ensure(std::max<size_t>(1, e->ssets.size()) * 4);
 }
 
 // grow a partition set's instance arena to hold `keys` keys (blocks are key-major: a prefix copy)
@@ -1908,6 +2150,8 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
     bool reads = gsp && gsp->n_groups > 0;
     for (auto& ps : e->psets)
       if (ps->partition == pi) reads = true;
+    for (auto& ss : e->ssets)
+      if (ss->partition == pi && !ss->glist[stream].empty()) reads = true;
     if (!reads) continue;
     const int type = e->lp.stream_types[stream][attr];
     e->r_key.ensure(n);
@@ -2029,6 +2273,66 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       any = true;
       bytes += (double)n * ev_bytes * ps.n_groups;
     }
+    // K_slab: item = (key segment, group whose shape reads this stream)
+    for (size_t si = 0; si < e->ssets.size(); ++si) {
+      auto& ss = *e->ssets[si];
+      if (ss.partition != pi) continue;
+      const auto& gl = ss.glist[stream];
+      if (gl.empty() || hv[1] == 0) continue;
+      slab_grow_keys(e, ss, hv[0]);
+      const int64_t items = (int64_t)hv[1] * (int64_t)gl.size();
+      if (items > INT32_MAX) throw Error(SDH_E_UNSUPPORTED, "K_slab launch beyond 2^31 work items (split the batch)");
+      ss.journal.ensure((size_t)items);
+      ss.journal_idx.ensure((size_t)items);
+      HIPCHK(hipMemsetAsync(ss.journal_idx.p, 0xff, (size_t)items * 8, e->stream));
+      HIPCHK(hipMemcpyAsync(ss.head_bak.p, ss.head.p, ss.nsub * 8, hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(hipMemcpyAsync(ss.live_bak.p, ss.live.p, 256 * 8, hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(hipMemsetAsync(ss.traffic.p, 0, 256 * 8, e->stream));
+      sdh::SlabLaunch S{};
+      S.queries = e->d_gq.p;
+      S.lane_q = e->d_lane_q.p;
+      S.group_tmpl = e->d_group_tmpl.p;
+      S.shapes = ss.d_shapes.p;
+      S.group_shape = ss.d_group_shape.p;
+      S.b = B;
+      S.seg_begin = e->r_off.p;
+      S.seg_len = e->r_cnt.p;
+      S.seg_kid = e->r_uniq.p;
+      S.key_of_id = rt.key_of_id.p;
+      S.ev_idx = e->r_idx_s.p;
+      S.glist = ss.d_glist[stream].p;
+      S.n_glist = (int32_t)gl.size();
+      S.n_items = (int32_t)items;
+      S.groups = ss.n_groups;
+      S.group_base = ss.group_base;
+      S.dir = ss.dir.p;
+      S.journal = ss.journal.p;
+      S.journal_idx = ss.journal_idx.p;
+      S.slab = ss.slab.p;
+      S.head = ss.head.p;
+      S.tail = ss.tail.p;
+      S.sub_cap = ss.sub_cap;
+      S.nsub = ss.nsub;
+      S.lds_words = ss.lds_words;
+      S.live = ss.live.p;
+      S.traffic = ss.traffic.p;
+      S.out = e->g_out.p;
+      S.out_cap = e->g_out_cap;
+      S.out_next = e->g_out_next.p;
+      S.rec_count = e->g_nrec.p;
+      S.rec_off = e->g_rec_off.p;
+      S.rec_cap = e->g_out_cap / 7 + 1;
+      S.rec_next = e->g_rec_next.p;
+      S.write_records = write ? 1 : 2;
+      S.err = e->d_serr.p + 4 * si;
+      HIPCHK(sdh_launch_slab(&S, e->stream));
+      ss.items = items;
+      e->slab_items += items;
+      any = true;
+      // every item reads its directory word and its key's events; the block bytes it moves are
+      // counted by the kernel (added once the pass has run)
+      bytes += (double)n * ev_bytes * gl.size() + (double)items * 8;
+    }
   }
   *bytes_out = bytes;
   return any;
@@ -2074,7 +2378,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   *bytes_out = 0;
   e->stats.last_gen_items = 0;
   e->stats.last_seq_items = 0;
-  if (e->gsets.empty() && e->psets.empty()) return;
+  if (e->gsets.empty() && e->psets.empty() && e->ssets.empty()) return;
   const int64_t n = B.n;
   e->g_out_cap = std::max<int64_t>(e->g_out_cap, std::max<int64_t>(1 << 22, n * 64));
   static_assert((1 << 22) > 2 * GEN_RING_MARGIN, "ring capacity");
@@ -2085,7 +2389,10 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   // pools) can be undone and the push re-run exactly at the grown capacity. The benchmark mode
   // (SDH_FLAG_DEVICE_MATCHES: records wrap in a ring, nothing is polled) skips the copy unless K_part
   // tables are present; there a K_gen pool overflow fails the push loudly (SDH_E_CAPACITY)
-  bool backed = (write || !e->psets.empty()) && gen_backup(e);
+  bool backed = (write || !e->psets.empty() || !e->ssets.empty()) && gen_backup(e);
+  for (auto& ss : e->ssets) slab_prepare(e, *ss);
+  const size_t nss = e->ssets.size();
+  std::vector<int32_t> serr(4 * std::max<size_t>(1, nss), 0);
   double bytes = 0;
   int32_t tail_len = -1;
   bool any = false;
@@ -2099,6 +2406,8 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     e->g_rec_off.ensure((size_t)(e->g_out_cap / 7 + 1));  // a record has at least 7 words
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
     HIPCHK(hipMemsetAsync(e->d_perr.p, 0, perr.size() * 4, e->stream));
+    HIPCHK(hipMemsetAsync(e->d_serr.p, 0, serr.size() * 4, e->stream));
+    e->slab_items = 0;
     HIPCHK(hipMemsetAsync(e->g_out_next.p, 0, 8, e->stream));
     HIPCHK(hipMemsetAsync(e->g_nrec.p, 0, 8, e->stream));
     HIPCHK(hipMemsetAsync(e->g_rec_next.p, 0, 8, e->stream));
@@ -2107,24 +2416,43 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     HIPCHK(hipEventRecord(e->ev1, e->stream));
     HIPCHK(hipMemcpyAsync(errs, e->d_err.p, 16, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(perr.data(), e->d_perr.p, perr.size() * 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(serr.data(), e->d_serr.p, serr.size() * 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&nrec, e->g_nrec.p, 8, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&used, e->g_out_next.p, 8, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
-    bool out_over = errs[2] != 0, part_over = false;
+    bool out_over = errs[2] != 0, part_over = false, slab_over = false;
     for (size_t i = 0; i < nps; ++i) {
       out_over |= perr[4 * i + 2] != 0;
       part_over |= perr[4 * i] != 0;
     }
+    for (size_t i = 0; i < nss; ++i) {
+      out_over |= serr[4 * i + 2] != 0;
+      slab_over |= serr[4 * i] != 0 || serr[4 * i + 1] != 0;
+    }
     kg::Sizing grown;
     const bool pools_over = errs[0] != 0 && gen_grown_sizing(e, errs[0], &grown);
-    if ((out_over || part_over || pools_over) && backed && attempt < 24 && (!errs[0] || pools_over) && !errs[1] &&
-        !errs[3]) {
+    if ((out_over || part_over || pools_over || slab_over) && backed && attempt < 24 && (!errs[0] || pools_over) &&
+        !errs[1] && !errs[3]) {
       // undo the pass (K_gen arenas from the backup; K_part tables are double-buffered and their
       // per-key selectors are swapped only after success) and re-run it with room for every match
       // record (out_next counts the words every record asked for), every K_part partial and the
       // K_gen pools / lists that overflowed
       gen_restore_backup(e);
+      for (size_t i = 0; i < nss; ++i) {
+        auto& ss = *e->ssets[i];
+        slab_rollback(e, ss);
+        if (serr[4 * i]) {  // a block outgrew the LDS staging area
+          if (ss.lds_words >= 13312) throw Error(SDH_E_CAPACITY, "K_slab: more partials in one (key, group) block "
+                                                                 "than the LDS staging area holds");
+          ss.lds_words = std::min(13312, 2 * ss.lds_words);
+        }
+        if (serr[4 * i + 1]) {  // a sub-ring ran out of room: plan for a push twice as large
+          ss.last_alloc = std::max<int64_t>(2 * ss.last_alloc, ss.sub_cap / 4);
+          slab_heads(e, ss);
+          slab_prepare(e, ss);
+        }
+      }
       if (pools_over) {
         gen_relayout(e, grown, true);
         ++e->gen_regrows;
@@ -2142,7 +2470,22 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     }
     if (part_over)
       throw Error(SDH_E_CAPACITY, "K_part partial table overflow (no room for an exact re-run)");
+    if (slab_over) throw Error(SDH_E_CAPACITY, "K_slab capacity (no room for an exact re-run)");
     break;
+  }
+  // the push succeeded: its K_slab allocations are committed (the heads tell the next push's room)
+  for (auto& up : e->ssets) {
+    auto& ss = *up;
+    if (ss.items <= 0) continue;
+    const std::vector<unsigned long long> before = ss.h_head;
+    slab_heads(e, ss);
+    int64_t alloc = 0;
+    for (int r = 0; r < ss.nsub; ++r) alloc = std::max<int64_t>(alloc, (int64_t)(ss.h_head[r] - before[r]));
+    ss.last_alloc = alloc;
+    unsigned long long tr[256];
+    HIPCHK(hipMemcpy(tr, ss.traffic.p, sizeof tr, hipMemcpyDeviceToHost));
+    for (unsigned long long x : tr) bytes += (double)x;
+    ss.items = 0;
   }
   // the push succeeded: the K_part tables it wrote become current
   for (auto& pp : e->psets)
@@ -2626,8 +2969,10 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
         if (e->rcur[g] == b)
           for (int l = 0; l < e->rg[g].n_lanes; ++l) live += rs[g].n[l];
     }
+    for (auto& ss : e->ssets) live += slab_live_partials(e, *ss);
     e->stats.live_partials = live;
     e->stats.pool_regrows = e->gen_regrows;
+    e->stats.last_slab_items = e->slab_items;
     *out = e->stats;
     return SDH_OK;
   });
@@ -2637,7 +2982,33 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
 // then per query
 // header + table, ratchet deques, K_gen arenas + key tables, K_seq tails
 constexpr int64_t SNAP_MAGIC = 0x5344485350415254LL;
-constexpr int64_t SNAP_VERSION = 5;
+constexpr int64_t SNAP_VERSION = 6;
+// Device memory of the sparse K_slab state: the live blocks' bytes, the slab's reserved bytes (live
+// blocks, not yet reclaimed superseded ones, and free room) and the directory's
+int sdh_engine_state_bytes(sdh_engine* e, int64_t* live_bytes, int64_t* reserved_bytes, int64_t* dir_bytes) {
+  if (!e) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    int64_t lb = 0, rb = 0, db = 0;
+    DevBuf<unsigned long long> acc;
+    acc.ensure(1);
+    for (auto& up : e->ssets) {
+      auto& ss = *up;
+      HIPCHK(hipMemsetAsync(acc.p, 0, 8, e->stream));
+      HIPCHK(sdh_slab_live_words(ss.dir.p, ss.key_cap * ss.n_groups, ss.n_groups, ss.d_group_ew.p, acc.p, e->stream));
+      unsigned long long w = 0;
+      HIPCHK(hipMemcpyAsync(&w, acc.p, 8, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipStreamSynchronize(e->stream));
+      lb += (int64_t)w * 4;
+      rb += (int64_t)ss.nsub * ss.sub_cap * 4;
+      db += ss.key_cap * ss.n_groups * 8;
+    }
+    if (live_bytes) *live_bytes = lb;
+    if (reserved_bytes) *reserved_bytes = rb;
+    if (dir_bytes) *dir_bytes = db;
+    return SDH_OK;
+  });
+}
+
 int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
   if (!e || !blob || !len) return SDH_E_INVALID;
   return guard(e, [&]() {
@@ -2723,6 +3094,39 @@ int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
     for (size_t st = 0; st < e->seq_tail.size(); ++st) {
       w.push_back(e->seq_tail_len[st]);
       put_dev(e->seq_tail[st].p, SEQ_TMAX * SEQ_TW * 8);
+    }
+    // K_slab: the live blocks packed into one ring, the directory pointing into it, the counters
+    w.push_back((int64_t)e->ssets.size());
+    for (auto& up : e->ssets) {
+      auto& ss = *up;
+      const int64_t n_dir = ss.key_cap * ss.n_groups;
+      DevBuf<unsigned long long> acc, ph, pt;
+      acc.ensure(1);
+      ph.ensure(1);
+      pt.ensure(1);
+      HIPCHK(hipMemset(acc.p, 0, 8));
+      HIPCHK(hipMemset(ph.p, 0, 8));
+      HIPCHK(hipMemset(pt.p, 0, 8));
+      HIPCHK(sdh_slab_live_words(ss.dir.p, n_dir, ss.n_groups, ss.d_group_ew.p, acc.p, e->stream));
+      unsigned long long words = 0;
+      HIPCHK(hipMemcpyAsync(&words, acc.p, 8, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipStreamSynchronize(e->stream));
+      DevBuf<uint64_t> dcopy;
+      DevBuf<uint32_t> packed;
+      dcopy.ensure(std::max<int64_t>(1, n_dir));
+      packed.ensure(std::max<size_t>(1, (size_t)words));
+      if (n_dir) HIPCHK(hipMemcpy(dcopy.p, ss.dir.p, n_dir * 8, hipMemcpyDeviceToDevice));
+      if (words && !slab_move(e, ss, std::vector<unsigned long long>(ss.nsub, ~0ull), packed.p, (int64_t)words, 1, ph.p,
+                              pt.p, dcopy.p))
+        throw Error(SDH_E_DEVICE, "K_slab snapshot: packing failed");
+      w.push_back(ss.partition);
+      w.push_back(ss.key_cap);
+      w.push_back(ss.n_groups);
+      w.push_back(ss.lds_words);
+      w.push_back((int64_t)words);
+      put_dev(dcopy.p, (size_t)n_dir * 8);
+      put_dev(packed.p, (size_t)words * 4);
+      put_dev(ss.live.p, 256 * 8);
     }
     *len = w.size() * 8;
     *blob = malloc(*len);
@@ -2861,6 +3265,35 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
       if (tl < 0 || tl > SEQ_TMAX) throw Error(SDH_E_INVALID, "bad snapshot tail length");
       e->seq_tail_len[st] = (int32_t)tl;
       get_dev(e->seq_tail[st].p, SEQ_TMAX * SEQ_TW * 8);
+    }
+    if ((size_t)nx() != e->ssets.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
+    for (auto& up : e->ssets) {
+      auto& ss = *up;
+      if (nx() != ss.partition) throw Error(SDH_E_INVALID, "snapshot of a different program");
+      const int64_t key_cap = nx(), ng = nx(), lds = nx(), words = nx();
+      if (ng != ss.n_groups || key_cap < 0 || key_cap > ((int64_t)1 << 32) || words < 0 || lds < 64 || lds > 13312)
+        throw Error(SDH_E_INVALID, "bad snapshot K_slab set");
+      ss.lds_words = (int)lds;
+      ss.key_cap = 0;
+      ss.dir.n = 0;
+      if (ss.dir.p) HIPCHK(hipFree(ss.dir.p));
+      ss.dir.p = nullptr;
+      slab_grow_keys(e, ss, key_cap);
+      if (ss.key_cap != key_cap) throw Error(SDH_E_INVALID, "snapshot key capacity mismatch");
+      get_dev(ss.dir.p, (size_t)key_cap * ng * 8);
+      DevBuf<uint32_t> packed;
+      packed.ensure(std::max<int64_t>(1, words));
+      get_dev(packed.p, (size_t)words * 4);
+      slab_init(e, ss, std::max<int64_t>(1 << 16, 2 * (words / ss.nsub) + 65536));
+      get_dev(ss.live.p, 256 * 8);
+      DevBuf<unsigned long long> zt;
+      zt.ensure(1);
+      HIPCHK(hipMemset(zt.p, 0, 8));
+      if (words && !slab_move(e, ss, std::vector<unsigned long long>(1, ~0ull), ss.slab.p, ss.sub_cap, ss.nsub,
+                              ss.head.p, ss.tail.p, nullptr, packed.p, words, zt.p))
+        throw Error(SDH_E_CAPACITY, "K_slab restore: a sub-ring overflowed");
+      slab_heads(e, ss);
+      ss.last_alloc = 0;
     }
     e->g_dev_matches = 0;
     e->device_matches = 0;

@@ -323,6 +323,54 @@ struct PartLaunch {
 };
 
 // ------------------------------------------------------------------------------------------
+// K_slab launch (nfa_slab.hip): distinct-stream patterns on sparse per-partial entries (slab.h)
+// item = (key segment of the pushed stream, group from glist); block (kid, g) = dir[kid * groups + g]
+//   dir word: offset / 4 (bits 0-39) | entries (40-55) | states with a non-empty list (56-63)
+// ------------------------------------------------------------------------------------------
+namespace slab {
+struct Shape;
+}
+
+struct SlabLaunch {
+  const kg::GQuery* queries;
+  const int32_t* lane_q;      // [group][64]
+  const int32_t* group_tmpl;  // [group]
+  const slab::Shape* shapes;  // per shape
+  const int32_t* group_shape; // [set group] -> shape
+  StreamBatch b;
+  const int32_t* seg_begin;   // partition routing (as GenLaunch)
+  const int32_t* seg_len;
+  const uint32_t* seg_kid;
+  const int64_t* key_of_id;
+  const int32_t* ev_idx;
+  const int32_t* glist;       // set groups that read the pushed stream; item = seg * n_glist + j
+  int32_t n_glist;
+  int32_t n_items;
+  int32_t groups;             // groups of the set (directory stride)
+  int32_t group_base;         // first row of lane_q / group_tmpl of the set
+  uint64_t* dir;              // [key_cap * groups]
+  uint64_t* journal;          // [item] the directory value a changed item replaced
+  uint64_t* journal_idx;      // [item] its directory index (~0: unchanged; the host clears them)
+  uint32_t* slab;             // nsub sub-rings of sub_cap words
+  unsigned long long* head;   // [nsub] logical allocation heads (monotone)
+  const unsigned long long* tail;  // [nsub] oldest live logical word
+  int64_t sub_cap;
+  int32_t nsub;
+  int32_t lds_words;          // dynamic LDS (uint32 words) for a block's entries
+  long long* live;            // [256] live-partial counters (sum = live partials)
+  unsigned long long* traffic;  // [256] block bytes read + written (the launch's state traffic)
+  int64_t* out;               // K_gen-format match records, as GenLaunch
+  int64_t out_cap;
+  unsigned long long* out_next;
+  unsigned long long* rec_count;
+  int64_t* rec_off;
+  int64_t rec_cap;
+  unsigned long long* rec_next;
+  int32_t write_records;
+  int32_t* err;               // [0] LDS capacity, [1] slab space, [2] output overflow
+};
+
+// ------------------------------------------------------------------------------------------
 // K_seq launch (nfa_gen.hip): every-start single-stream sequences of stream states evaluated as
 // windows of S consecutive events (kg::seq_window); item = (start chunk, group of 64 queries)
 // ------------------------------------------------------------------------------------------

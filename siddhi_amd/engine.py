@@ -54,12 +54,12 @@ class SdhStats(ctypes.Structure):
                 ("last_gen_items", ctypes.c_int64), ("last_seq_items", ctypes.c_int64),
                 ("last_part_items", ctypes.c_int64), ("last_ingest_ms", ctypes.c_double),
                 ("ingest_bytes", ctypes.c_int64), ("spec_kernels", ctypes.c_int64),
-                ("pool_regrows", ctypes.c_int64)]
+                ("pool_regrows", ctypes.c_int64), ("last_slab_items", ctypes.c_int64)]
 
 
 EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engine_poll", "sdh_engine_poll_device",
            "sdh_engine_pending_matches", "sdh_engine_start", "sdh_engine_advance_time", "sdh_engine_stats",
-           "sdh_engine_snapshot",
+           "sdh_engine_snapshot", "sdh_engine_state_bytes",
            "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version"]
 
 _lib = None
@@ -85,6 +85,8 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_engine_start.argtypes = [P, ctypes.c_int64]
     lib.sdh_engine_advance_time.argtypes = [P, ctypes.c_int64]
     lib.sdh_engine_stats.argtypes = [P, ctypes.POINTER(SdhStats)]
+    I64P = ctypes.POINTER(ctypes.c_int64)
+    lib.sdh_engine_state_bytes.argtypes = [P, I64P, I64P, I64P]
     lib.sdh_engine_snapshot.argtypes = [P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
     lib.sdh_engine_restore.argtypes = [P, ctypes.c_void_p, ctypes.c_size_t]
     lib.sdh_free.argtypes = [P]
@@ -229,6 +231,12 @@ class HipEngine:
         s = SdhStats()
         self._check(self.lib.sdh_engine_stats(self.h, ctypes.byref(s)))
         return s
+
+    def state_bytes(self):
+        """(live, reserved, directory) bytes of the sparse K_slab state (sdh_engine_state_bytes)."""
+        a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.sdh_engine_state_bytes(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
 
     def snapshot(self) -> bytes:
         p = ctypes.c_void_p()

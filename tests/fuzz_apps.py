@@ -173,3 +173,107 @@ def random_timeline(seed, n=200):
             out.append(("advance", None, t - 1 if t > 0 else 0))
         out.append((stream, row, t))
     return out
+
+
+# ---- distinct-stream patterns (the K_slab class, siddhi_amd/csrc/slab.h): every state reads its own
+# stream, inside `partition with` one key over all streams ----
+SLAB_STREAMS = tuple(f"S{i}" for i in range(6))
+
+
+def slab_streams_def():
+    return " ".join(f"define stream {s} (k int, a float, b int, s string);" for s in SLAB_STREAMS)
+
+
+def _slab_pred(rng, refs, own=None):
+    """A filter over the current event, constants and earlier slots (refs: (alias, is_count));
+    own: this state's alias when it is a count state (its own [last] reads the previous event)."""
+    def operand():
+        r = rng.random()
+        if refs and r < 0.5:
+            al, cnt = rng.choice(refs)
+            idx = rng.choice(["", "[0]", "[last]"]) if cnt else ""
+            return f"{al}{idx}.{rng.choice('ab')}"
+        if own and r < 0.6:
+            return f"{own}[last].{rng.choice('ab')}"
+        return None
+    terms = []
+    for _ in range(rng.choice([1, 1, 2])):
+        attr = rng.choice("ab")
+        op = rng.choice([">", "<", ">=", "<=", "==", "!="])
+        rhs = operand()
+        if rhs is None:
+            if rng.random() < 0.1:
+                terms.append(f"s == '{rng.choice('xyz')}'")
+                continue
+            c = rng.randint(0, 9)
+            rhs = f"{c}.5" if attr == "a" and rng.random() < 0.5 else str(c)
+        elif rng.random() < 0.25:
+            rhs = f"{rhs} {rng.choice(['+', '*', '-'])} {rng.choice(['1', '2', '0.5'])}"
+        terms.append(f"{attr} {op} {rhs}")
+    if len(terms) == 2 and rng.random() < 0.3:
+        return f"{terms[0]} or {terms[1]}"
+    if rng.random() < 0.08 and refs:
+        al, cnt = rng.choice([x for x in refs if not x[1]] or refs)
+        if not cnt:
+            return f"not ({terms[0]}) and {al}.b is null" if rng.random() < 0.5 else f"{terms[0]} or {al}.b is null"
+    return " and ".join(terms)
+
+
+def random_slab_query(rng, name):
+    streams = list(SLAB_STREAMS)
+    rng.shuffle(streams)
+    n_el = rng.randint(2, 4)
+    parts, refs, sel = [], [], []
+    prev_count = False
+    for i in range(n_el):
+        r = rng.random()
+        if i > 0 and r < 0.3 and len(streams) >= 2:
+            s1, s2 = streams.pop(), streams.pop()
+            a1, a2 = f"e{i}", f"e{i}x"
+            p1, p2 = _slab_pred(rng, refs), _slab_pred(rng, refs)
+            parts.append(f"{a1}={s1}[{p1}] {rng.choice(['and', 'or'])} {a2}={s2}[{p2}]")
+            refs += [(a1, False), (a2, False)]
+            sel.append(a1)
+            prev_count = False
+            continue
+        st = streams.pop()
+        al = f"e{i}"
+        if i > 0 and r < 0.55 and not prev_count:
+            mn = rng.randint(1, 3)
+            mx = mn + rng.randint(0, 3)
+            cnt = rng.choice([f"<{mn}:{mx}>", f"<{mx}>", f"<{mn}:{mx}>"])
+            parts.append(f"{al}={st}[{_slab_pred(rng, refs, own=al if rng.random() < 0.3 else None)}]{cnt}")
+            refs.append((al, True))
+            sel.append(al)
+            prev_count = True
+            continue
+        parts.append(f"{al}={st}[{_slab_pred(rng, refs)}]")
+        refs.append((al, False))
+        sel.append(al)
+        prev_count = False
+    if rng.random() < 0.8:
+        parts[0] = "every " + parts[0]
+    within = f" within {rng.choice([5, 12, 30, 80])} milliseconds" if rng.random() < 0.7 else ""
+    return (f"@info(name='{name}') from {' -> '.join(parts)}{within} "
+            f"select {sel[0]}.a as x, {sel[-1]}.b as y insert into Out;")
+
+
+def random_slab_app(seed, n_queries=6):
+    rng = random.Random(seed)
+    body = " ".join(random_slab_query(rng, f"q{i}") for i in range(n_queries))
+    keys = ", ".join(f"k of {s}" for s in SLAB_STREAMS)
+    return f"{slab_streams_def()} partition with ({keys}) begin {body} end;"
+
+
+def random_slab_events(seed, n=600, keys=4):
+    """(stream, row, ts) with rows (k, a, b, s); timestamps non-decreasing, now and then a null."""
+    rng = np.random.default_rng(seed)
+    ev, t = [], 0
+    for _ in range(n):
+        t += int(rng.integers(0, 3))
+        row = [int(rng.integers(0, keys)), float(np.float32(rng.integers(0, 20) / 2.0)), int(rng.integers(0, 10)),
+               str(rng.choice(list("xyz")))]
+        if rng.random() < 0.02:
+            row[int(rng.integers(1, 4))] = None
+        ev.append((SLAB_STREAMS[int(rng.integers(0, len(SLAB_STREAMS)))], row, t))
+    return ev
