@@ -38,8 +38,9 @@ DEFAULTS = {  # workload -> (patterns per GPU, events per step, keys)
     "c2": (10000, 1 << 23, 100),
     "c3": (1000, 1 << 20, 10000),
     "c4": (1250, 1 << 20, 100_000),
-    "c5": (256, 1 << 16, 125_000),  # patterns, events per stream per step, accounts per GPU (8 GPUs: 1M)
+    "c5": (100_000, 1 << 16, 125_000),  # patterns, events per stream per GPU per step, accounts per GPU
 }
+C5_NODE = 8  # BASELINE configs[4] is one 8-GPU node: every rank is one of 8 key shards of 1M accounts
 
 
 def parse():
@@ -75,10 +76,8 @@ def make_engine(workload, P, first, K, device, flags, partials, shard=(0, 1)):
     if workload == "c4":
         # a sequence instance holds at most one partial per state (R8): small pools
         return HipEngine(blob, device=device, flags=flags, gen_pool_states=8, gen_pool_nodes=32, gen_list_cap=8)
-    if workload == "c5":  # key sharding: every rank runs all patterns over its own accounts
-        pools = [int(x) for x in os.environ.get("SDH_C5_POOLS", "8,24,8").split(",")]
-        return HipEngine(blob, device=device, flags=flags, gen_pool_states=pools[0], gen_pool_nodes=pools[1],
-                         gen_list_cap=pools[2], gen_max_keys=max(1024, 2 * K), shard_rank=shard[0],
+    if workload == "c5":  # key sharding: every rank runs all patterns over its own accounts (K_slab)
+        return HipEngine(blob, device=device, flags=flags, gen_max_keys=max(1024, 2 * K), shard_rank=shard[0],
                          shard_world=shard[1])
     if workload == "c3":
         pools = [int(x) for x in os.environ.get("SDH_C3_POOLS", "32,128,32").split(",")]
@@ -179,6 +178,8 @@ KERNEL_SOURCES = {  # what a kernel's code and launch configuration are built fr
     # shape-compiled kernels (spec.hip generates and compiles them with hiprtc at engine creation)
     "sdh_part_spec": ["spec.hip", "part_body.h", "dev_common.h", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
     "sdh_seq_spec": ["spec.hip", "seq_body.h", "dev_common.h", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
+    "nfa_slab_kernel": ["nfa_slab.hip", "slab.h", "slab_lower.h", "dev_common.h", "kgen.h", "gen_lower.h",
+                        "nfa_types.h", "engine.hip"],
 }
 
 
@@ -243,10 +244,17 @@ def main():
     B = args.batch or B0
     K = args.keys or K0
     c5 = args.workload == "c5"
-    if c5:  # key sharding (weak scaling): every rank runs all P patterns over its K of K * world accounts,
-        # and each stream carries B events per GPU per step
-        eng = make_engine("c5", P, 0, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials, shard=(rank, world))
-        B, K_gen = B * world, K * world
+    if c5:  # key sharding (weak scaling): rank r is shard r of the 8-GPU node's 1M accounts; every step
+        # each stream carries the node's B * 8 events (generated by rank 0, broadcast) and a rank
+        # evaluates the ~B of them whose account it owns against all P patterns
+        if world > C5_NODE:
+            raise SystemExit(f"--workload c5 models one {C5_NODE}-GPU node")
+        t_build = time.perf_counter()
+        eng = make_engine("c5", P, 0, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials, shard=(rank, C5_NODE))
+        t_build = time.perf_counter() - t_build
+        B, K_gen = B * C5_NODE, K * C5_NODE
+        # `within 1 hour` of event time: the untimed warm-up covers an hour (the state's steady size)
+        args.warmup = max(args.warmup, -(-3_600_000 // B) + 1)
         args.no_expansion = args.no_ingest = True  # (single-stream helpers)
     else:
         eng = make_engine(args.workload, P, rank * P, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials)
@@ -255,17 +263,43 @@ def main():
     n_batches = args.warmup + args.steps
     # synthetic batches generated on the device before the timed region (rank 0's copy is the
     # broadcast source in multi-GPU runs; the other ranks receive into their own buffers)
-    batches = [gen_batch(args.workload, s * B, B, K_gen, dev) for s in range(n_batches)]
+    batches = [gen_batch(args.workload, s * B, B, K_gen, dev) for s in range(n_batches)] if not c5 else None
     torch.cuda.synchronize()
     bcast = world > 1
 
+    def bcast_into(t):
+        if backend == "nccl":
+            dist.broadcast(t, src=0)
+        else:  # gloo rehearsal: the collective runs on a host copy, received back into t
+            tc = t.cpu()
+            dist.broadcast(tc, src=0)
+            t.copy_(tc)
+
+    if c5:
+        # rank 0's batches of the timed steps are generated before the timed region; the other
+        # ranks receive them into zeroed buffers (a missing broadcast shows as wrong matches)
+        def c5_batch(i):
+            cols = gen_batch("c5", i * B, B, K_gen, dev)
+            return cols if rank == 0 or not bcast else [[torch.zeros_like(t) for t in c] for c in cols]
+        c5_pre = [c5_batch(i) for i in range(args.warmup, n_batches)]
+
     def step(i):
-        per_stream = batches[i] if c5 else [batches[i]]
+        """One step: every stream's batch pushed once; returns (kernel ms, algorithmic bytes, matches)
+        summed over the step's pushes."""
+        per_stream = ((c5_batch(i) if i < args.warmup else c5_pre[i - args.warmup]) if c5 else [batches[i]])
+        ms = by = 0.0
+        nm = 0
         for si, cols in enumerate(per_stream):
             if bcast:
                 for t in cols:
-                    dist.broadcast(t if backend == "nccl" else t.cpu(), src=0)
+                    bcast_into(t)
             eng.push_device(si, B, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
+            if len(per_stream) > 1 or i >= args.warmup:
+                st = eng.stats()
+                ms += st.last_kernel_ms
+                by += st.last_kernel_bytes
+                nm += eng.pending_matches()
+        return ms, by, nm
 
     for i in range(args.warmup):
         step(i)
@@ -276,11 +310,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.warmup, n_batches):
-        step(i)
-        st = eng.stats()
-        kern_ms.append(st.last_kernel_ms)
-        kern_bytes.append(st.last_kernel_bytes)
-        matches += eng.pending_matches()
+        ms, by, nm = step(i)
+        kern_ms.append(ms)
+        kern_bytes.append(by)
+        matches += nm
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -313,10 +346,10 @@ def main():
               "within 10 sec")
         kernel = "sdh_part_spec"
     elif c5:
-        wl = (f"C5 family (reduced): {P} mixed 2-4-state patterns (cross-stream reference, and, or, count) over 4 "
-              f"joined streams, partition with (acct) over {K} accounts per GPU of {K * world}, within 1 hour; "
-              f"{B} events per stream per step")
-        kernel = "nfa_gen_kernel"
+        wl = (f"C5: {P} mixed 2-4-state patterns (cross-stream reference, and, or, count) over 4 joined streams, "
+              f"partition with (acct) over {K * C5_NODE} accounts, within 1 hour; this GPU is key shard(s) "
+              f"{list(range(world))} of {C5_NODE} ({K} accounts each); {B} node events per stream per step")
+        kernel = "nfa_slab_kernel"
     else:
         wl = ("C4: fraud-rule sequences every e1=Txn[..], e2=Txn[..e1.amount*M], e3=Txn[..] within 1 min "
               f"(strict contiguity), {K} accounts, pattern-set shard {rank * P}..{rank * P + P - 1}")
@@ -347,10 +380,16 @@ def main():
                      "kernel": kernel, "kernel_ms": avg_ms,
                      # measured HBM rate (PMC traffic / live kernel time); below `achieved` when the
                      # device record is narrower than §8(d)'s 32-B match unit
-                     "traffic_gbps": (traffic / (avg_ms * 1e-3) / 1e9) if traffic else None},
+                     # measured HBM rate: PMC bytes per launch / the profile's average launch time
+                     "traffic_gbps": (traffic / (prof["kernel_ns_avg"] * 1e-9) / 1e9) if traffic else None},
     }
     if prof:
         result["roofline"]["counters"] = {k: v for k, v in prof.items() if k != "traffic_bytes"}
+    if c5:  # the sparse state (K_slab): bytes per live partial, engine build time
+        lb, rb, db = eng.state_bytes()
+        result["config"].update({"state_live_bytes": lb, "state_slab_bytes": rb, "state_dir_bytes": db,
+                                 "bytes_per_live_partial": (lb + db) / max(1, live),
+                                 "engine_build_s": t_build, "warmup_event_hours": args.warmup * B / 3.6e6})
     if not args.no_expansion:
         result["expansion"] = expansion(args, P, rank, K, local, dev, world, cdev, dist)
     if not args.no_ingest and world == 1:

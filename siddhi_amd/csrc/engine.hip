@@ -32,10 +32,11 @@ extern "C" hipError_t sdh_launch_slab(const sdh::SlabLaunch* L, hipStream_t s);
 extern "C" hipError_t sdh_slab_rollback(uint64_t* dir, const uint64_t* journal, const uint64_t* journal_idx, int64_t n,
                                         const long long* live_bak, long long* live, hipStream_t s);
 extern "C" hipError_t sdh_slab_move(uint64_t* dir, int64_t n_dir, int groups, const int32_t* group_ew,
-                                    const uint32_t* src, int64_t src_cap, const unsigned long long* src_tail,
-                                    const unsigned long long* limit, uint32_t* dst, int64_t dst_cap, int dst_nsub,
-                                    unsigned long long* dst_head, const unsigned long long* dst_tail, int32_t* err,
-                                    hipStream_t s);
+                                    uint32_t* const* src_ring, const int64_t* src_cap,
+                                    const unsigned long long* src_tail, int src_nsub, const unsigned long long* limit,
+                                    const uint8_t* active, uint32_t* const* dst_ring, const int64_t* dst_cap,
+                                    unsigned long long* dst_head, const unsigned long long* dst_tail, int dst_nsub,
+                                    int32_t* err, hipStream_t s);
 extern "C" hipError_t sdh_slab_live_words(const uint64_t* dir, int64_t n_dir, int groups, const int32_t* group_ew,
                                           unsigned long long* acc, hipStream_t s);
 extern "C" hipError_t sdh_seq_tail(const sdh::StreamBatch* b, int64_t* tail, int32_t tail_len, int32_t new_tail_len,
@@ -685,22 +686,28 @@ struct sdh_engine {
     std::vector<std::vector<int32_t>> glist;  // [stream] set groups reading it
     std::vector<DevBuf<int32_t>> d_glist;
     DevBuf<uint64_t> dir;                     // [key_cap * n_groups]
-    DevBuf<uint32_t> slab;                    // nsub * sub_cap words
-    int nsub = 256;
-    int64_t sub_cap = 0;
+    int nsub = 256;                           // sub-rings (separate buffers: they grow one at a time)
+    std::vector<uint32_t*> ring;
+    std::vector<int64_t> cap;                 // words per ring
+    DevBuf<uint32_t*> d_ring;
+    DevBuf<int64_t> d_cap;
     DevBuf<unsigned long long> head, tail, head_bak;
-    std::vector<unsigned long long> h_head, h_tail;
+    std::vector<unsigned long long> h_head, h_tail, h_push0;  // h_push0: heads before the last push
+    ~SlabSet() {
+      for (uint32_t* p : ring)
+        if (p) (void)hipFree(p);
+    }
     DevBuf<long long> live, live_bak;
     DevBuf<unsigned long long> traffic;       // block bytes read + written by the last launch
     DevBuf<uint64_t> journal, journal_idx;
     int64_t items = 0;                        // items of this pass's launch (0: not launched)
     int lds_words = 4096;
-    int64_t last_alloc = 0;                   // largest one-push allocation of a sub-ring (words)
     int64_t cleanings = 0, growths = 0;
   };
   std::vector<std::unique_ptr<SlabSet>> ssets;
   DevBuf<int32_t> d_serr;            // per K_slab set: [0] LDS capacity, [1] slab space, [2] output overflow
   int64_t slab_items = 0;            // K_slab work items of the last push
+  std::vector<int64_t> part_kept;    // per partition: events of the last push routed to a key here
   DevBuf<int32_t> d_perr;            // per K_part set: [0] entry capacity, [2] output overflow
   DevBuf<unsigned long long> d_pprof;  // SDH_PART_PROF measurement builds: phase clocks
   DevBuf<int64_t> r_key;
@@ -1466,10 +1473,31 @@ void slab_heads(sdh_engine* e, sdh_engine::SlabSet& ss) {
   HIPCHK(hipStreamSynchronize(e->stream));
 }
 
-// a fresh, empty slab of nsub sub-rings of `sub_cap` words
-void slab_init(sdh_engine* e, sdh_engine::SlabSet& ss, int64_t sub_cap) {
-  ss.sub_cap = (sub_cap + 3) & ~3ll;
-  ss.slab.ensure((size_t)ss.nsub * ss.sub_cap);
+void slab_upload_rings(sdh_engine::SlabSet& ss) {
+  HIPCHK(hipMemcpy(ss.d_ring.p, ss.ring.data(), ss.nsub * sizeof(uint32_t*), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ss.d_cap.p, ss.cap.data(), ss.nsub * 8, hipMemcpyHostToDevice));
+}
+
+uint32_t* ring_malloc(int64_t words) {
+  void* p = nullptr;
+  if (hipMalloc(&p, (size_t)words * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    throw Error(SDH_E_CAPACITY, fmt("device memory exhausted allocating a %.2f GB K_slab ring", words * 4.0 / 1e9));
+  }
+  return (uint32_t*)p;
+}
+
+// fresh, empty sub-rings of `cap` words each
+void slab_init(sdh_engine* e, sdh_engine::SlabSet& ss, int64_t cap) {
+  for (uint32_t* p : ss.ring)
+    if (p) HIPCHK(hipFree(p));
+  cap = (cap + 3) & ~3ll;
+  ss.ring.assign(ss.nsub, nullptr);
+  ss.cap.assign(ss.nsub, cap);
+  for (auto& p : ss.ring) p = ring_malloc(cap);
+  ss.d_ring.ensure(ss.nsub);
+  ss.d_cap.ensure(ss.nsub);
+  slab_upload_rings(ss);
   ss.head.ensure(ss.nsub);
   ss.tail.ensure(ss.nsub);
   ss.head_bak.ensure(ss.nsub);
@@ -1477,6 +1505,7 @@ void slab_init(sdh_engine* e, sdh_engine::SlabSet& ss, int64_t sub_cap) {
   HIPCHK(hipMemset(ss.tail.p, 0, ss.nsub * 8));
   ss.h_head.assign(ss.nsub, 0);
   ss.h_tail.assign(ss.nsub, 0);
+  ss.h_push0.assign(ss.nsub, 0);
   ss.live.ensure(256);
   ss.live_bak.ensure(256);
   ss.traffic.ensure(256);
@@ -1502,85 +1531,121 @@ void slab_grow_keys(sdh_engine* e, sdh_engine::SlabSet& ss, int64_t keys) {
   ss.key_cap = cap;
 }
 
-// move the live blocks at sub-ring positions < limit[sub] to the head of their destination ring;
-// false when a destination ring ran out of room (nothing is lost: a block keeps its old place
-// until its directory entry moves)
-bool slab_move(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<unsigned long long>& limit, uint32_t* dst,
-               int64_t dst_cap, int dst_nsub, unsigned long long* dst_head, const unsigned long long* dst_tail,
-               uint64_t* dir = nullptr, const uint32_t* src = nullptr, int64_t src_cap = 0,
-               const unsigned long long* src_tail = nullptr) {
+// One directory pass moving blocks (nfa_slab.hip slab_move_kernel); false if a destination ring
+// ran out of room (nothing is lost: a block keeps its old place until its directory word moves)
+bool slab_move_raw(sdh_engine* e, sdh_engine::SlabSet& ss, uint64_t* dir, uint32_t* const* src_ring,
+                   const int64_t* src_cap, const unsigned long long* src_tail, int src_nsub,
+                   const std::vector<unsigned long long>& limit, const std::vector<uint8_t>& active,
+                   uint32_t* const* dst_ring, const int64_t* dst_cap, unsigned long long* dst_head,
+                   const unsigned long long* dst_tail, int dst_nsub) {
   DevBuf<unsigned long long> d_lim;
+  DevBuf<uint8_t> d_act;
   d_lim.ensure(limit.size());
   HIPCHK(hipMemcpyAsync(d_lim.p, limit.data(), limit.size() * 8, hipMemcpyHostToDevice, e->stream));
+  if (!active.empty()) {
+    d_act.ensure(active.size());
+    HIPCHK(hipMemcpyAsync(d_act.p, active.data(), active.size(), hipMemcpyHostToDevice, e->stream));
+  }
   e->d_err.ensure(4);
   HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
-  HIPCHK(sdh_slab_move(dir ? dir : ss.dir.p, ss.key_cap * ss.n_groups, ss.n_groups, ss.d_group_ew.p,
-                       src ? src : ss.slab.p, src ? src_cap : ss.sub_cap, src ? src_tail : ss.tail.p, d_lim.p, dst,
-                       dst_cap, dst_nsub, dst_head, dst_tail, e->d_err.p, e->stream));
+  HIPCHK(sdh_slab_move(dir, ss.key_cap * ss.n_groups, ss.n_groups, ss.d_group_ew.p, src_ring, src_cap, src_tail,
+                       src_nsub, d_lim.p, active.empty() ? nullptr : d_act.p, dst_ring, dst_cap, dst_head, dst_tail,
+                       dst_nsub, e->d_err.p, e->stream));
   int32_t err = 0;
   HIPCHK(hipMemcpyAsync(&err, e->d_err.p, 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return err == 0;
 }
 
-// a slab of sub-rings of (at least) want words each, holding every live block
-void slab_grow(sdh_engine* e, sdh_engine::SlabSet& ss, int64_t want) {
-  const int64_t nc = (std::max<int64_t>(want, 2 * ss.sub_cap) + 3) & ~3ll;
-  DevBuf<uint32_t> ns;
-  DevBuf<unsigned long long> nh, nt;
-  if (hipMalloc(&ns.p, (size_t)ss.nsub * nc * 4) != hipSuccess) {
-    (void)hipGetLastError();
-    throw Error(SDH_E_CAPACITY, fmt("device memory exhausted growing the K_slab slab to %.1f GB",
-                                    (double)ss.nsub * nc * 4 / 1e9));
+// rings `which` into new buffers of new_cap[r] words holding their live blocks (a batch at a time,
+// so the extra memory is a batch's worth)
+void slab_grow(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int>& which,
+               const std::vector<int64_t>& new_cap) {
+  const int BATCH = 32;
+  for (size_t b0 = 0; b0 < which.size(); b0 += BATCH) {
+    std::vector<uint32_t*> nring(ss.ring);
+    std::vector<int64_t> ncap(ss.cap);
+    std::vector<uint8_t> active(ss.nsub, 0);
+    for (size_t k = b0; k < std::min(which.size(), b0 + BATCH); ++k) {
+      const int r = which[k];
+      ncap[r] = (new_cap[k] + 3) & ~3ll;
+      nring[r] = ring_malloc(ncap[r]);
+      active[r] = 1;
+    }
+    DevBuf<uint32_t*> d_nr;
+    DevBuf<int64_t> d_nc;
+    DevBuf<unsigned long long> nh, nt;
+    d_nr.ensure(ss.nsub);
+    d_nc.ensure(ss.nsub);
+    nh.ensure(ss.nsub);
+    nt.ensure(ss.nsub);
+    HIPCHK(hipMemcpy(d_nr.p, nring.data(), ss.nsub * sizeof(uint32_t*), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_nc.p, ncap.data(), ss.nsub * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(nh.p, 0, ss.nsub * 8));
+    HIPCHK(hipMemset(nt.p, 0, ss.nsub * 8));
+    if (!slab_move_raw(e, ss, ss.dir.p, ss.d_ring.p, ss.d_cap.p, ss.tail.p, ss.nsub,
+                       std::vector<unsigned long long>(ss.nsub, ~0ull), active, d_nr.p, d_nc.p, nh.p, nt.p, ss.nsub))
+      throw Error(SDH_E_CAPACITY, "K_slab: a ring overflowed while growing");
+    std::vector<unsigned long long> moved(ss.nsub);
+    HIPCHK(hipMemcpy(moved.data(), nh.p, ss.nsub * 8, hipMemcpyDeviceToHost));
+    for (int r = 0; r < ss.nsub; ++r) {
+      if (!active[r]) continue;
+      HIPCHK(hipFree(ss.ring[r]));
+      ss.ring[r] = nring[r];
+      ss.cap[r] = ncap[r];
+      ss.h_head[r] = moved[r];
+      ss.h_tail[r] = 0;
+      ss.h_push0[r] = 0;
+    }
+    slab_upload_rings(ss);
+    HIPCHK(hipMemcpy(ss.head.p, ss.h_head.data(), ss.nsub * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ss.tail.p, ss.h_tail.data(), ss.nsub * 8, hipMemcpyHostToDevice));
+    ss.growths += (int64_t)std::min<size_t>(BATCH, which.size() - b0);
   }
-  ns.n = (size_t)ss.nsub * nc;
-  nh.ensure(ss.nsub);
-  nt.ensure(ss.nsub);
-  HIPCHK(hipMemsetAsync(nh.p, 0, ss.nsub * 8, e->stream));
-  HIPCHK(hipMemsetAsync(nt.p, 0, ss.nsub * 8, e->stream));
-  std::vector<unsigned long long> all(ss.nsub, ~0ull);
-  if (!slab_move(e, ss, all, ns.p, nc, ss.nsub, nh.p, nt.p))
-    throw Error(SDH_E_CAPACITY, "K_slab: a sub-ring overflowed while the slab grew");
-  std::swap(ss.slab.p, ns.p);
-  std::swap(ss.slab.n, ns.n);
-  std::swap(ss.head.p, nh.p);
-  std::swap(ss.tail.p, nt.p);
-  ss.sub_cap = nc;
-  ss.h_tail.assign(ss.nsub, 0);
-  slab_heads(e, ss);
-  ++ss.growths;
 }
 
-// room for the next push: a sub-ring with less than `reserve` words free has its oldest half
-// reclaimed (its live blocks move to its head); if that is not enough the slab grows
-void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss) {
-  const int64_t reserve = std::max<int64_t>(2 * ss.last_alloc, 4096);
-  auto free_min = [&]() {
-    int64_t f = INT64_MAX, used = 0;
-    for (int r = 0; r < ss.nsub; ++r) {
-      const int64_t u = (int64_t)(ss.h_head[r] - ss.h_tail[r]);
-      f = std::min(f, ss.sub_cap - u);
-      used = std::max(used, u);
-    }
-    return std::make_pair(f, used);
-  };
-  auto [f, used] = free_min();
-  if (f >= reserve) return;
+// Room for the next push in every ring. A ring with less free room than twice what it took in the
+// last push is reclaimed: every block written before that push moves to its head (the blocks of
+// the last push are current, so the ring then holds live blocks only). A ring still short, or more
+// than 3/4 full, grows to 1.5x (or to what it needs).
+// demand: words a failed push tried to take per ring (room for 1.25x that is made instead)
+void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int64_t>* demand = nullptr) {
+  std::vector<int64_t> need(ss.nsub);
   std::vector<unsigned long long> limit(ss.nsub);
-  for (int r = 0; r < ss.nsub; ++r) limit[r] = ss.h_tail[r] + (ss.h_head[r] - ss.h_tail[r]) / 2;
-  bool ok = ss.sub_cap >= 2 * reserve && slab_move(e, ss, limit, ss.slab.p, ss.sub_cap, ss.nsub, ss.head.p, ss.tail.p);
-  if (ok) {
-    ss.h_tail = limit;
-    HIPCHK(hipMemcpyAsync(ss.tail.p, limit.data(), ss.nsub * 8, hipMemcpyHostToDevice, e->stream));
-    slab_heads(e, ss);
-    ++ss.cleanings;
-    std::tie(f, used) = free_min();
-    if (f >= reserve && used <= ss.sub_cap / 2) return;
-  } else {
-    slab_heads(e, ss);
-    std::tie(f, used) = free_min();
+  std::vector<uint8_t> clean(ss.nsub, 0);
+  bool any = false;
+  for (int r = 0; r < ss.nsub; ++r) {
+    const int64_t alloc = (int64_t)(ss.h_head[r] - ss.h_push0[r]);
+    need[r] = std::max<int64_t>(2 * alloc, 4096);
+    if (demand) need[r] = std::max<int64_t>(need[r], (*demand)[r] + (*demand)[r] / 4);
+    const int64_t used = (int64_t)(ss.h_head[r] - ss.h_tail[r]);
+    if (ss.cap[r] - used >= need[r]) continue;
+    limit[r] = ss.h_push0[r] > ss.h_tail[r] ? ss.h_push0[r] : ss.h_head[r];
+    clean[r] = 1;
+    any = true;
   }
-  slab_grow(e, ss, 2 * (used + reserve));
+  std::vector<int> grow;
+  std::vector<int64_t> gcap;
+  if (any) {
+    const bool ok = slab_move_raw(e, ss, ss.dir.p, ss.d_ring.p, ss.d_cap.p, ss.tail.p, ss.nsub, limit, clean,
+                                  ss.d_ring.p, ss.d_cap.p, ss.head.p, ss.tail.p, ss.nsub);
+    slab_heads(e, ss);
+    if (ok) {
+      for (int r = 0; r < ss.nsub; ++r)
+        if (clean[r]) ss.h_tail[r] = limit[r];
+      HIPCHK(hipMemcpy(ss.tail.p, ss.h_tail.data(), ss.nsub * 8, hipMemcpyHostToDevice));
+      ++ss.cleanings;
+    }
+    for (int r = 0; r < ss.nsub; ++r) {
+      if (!clean[r]) continue;
+      const int64_t used = (int64_t)(ss.h_head[r] - ss.h_tail[r]);
+      if (ok && ss.cap[r] - used >= need[r] && 4 * used <= 3 * ss.cap[r]) continue;
+      grow.push_back(r);
+      gcap.push_back(std::max<int64_t>(ss.cap[r] + ss.cap[r] / 2, 3 * (used + need[r]) / 2));
+    }
+  }
+  if (!grow.empty()) slab_grow(e, ss, grow, gcap);
+  ss.h_push0 = ss.h_head;
 }
 
 // undo this pass's launch of the set (its directory changes; its allocations are dropped)
@@ -1590,6 +1655,7 @@ void slab_rollback(sdh_engine* e, sdh_engine::SlabSet& ss) {
   HIPCHK(hipMemcpyAsync(ss.head.p, ss.head_bak.p, ss.nsub * 8, hipMemcpyDeviceToDevice, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   ss.items = 0;
+  slab_heads(e, ss);
 }
 
 int64_t slab_live_partials(sdh_engine* e, const sdh_engine::SlabSet& ss) {
@@ -2174,6 +2240,16 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
     HIPCHK(hipMemcpyAsync(&hv[1], e->r_nruns.p, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (hv[0] > rt.max_keys) throw Error(SDH_E_CAPACITY, "more partition keys than gen_max_keys");
+    // events this engine keeps (null keys and, with key sharding, other ranks' keys sort last)
+    if (hv[1] > 0) {
+      uint32_t last_kid = 0;
+      int32_t last_cnt = 0;
+      HIPCHK(hipMemcpyAsync(&last_kid, e->r_uniq.p + hv[1] - 1, 4, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipMemcpyAsync(&last_cnt, e->r_cnt.p + hv[1] - 1, 4, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipStreamSynchronize(e->stream));
+      if ((int)e->part_kept.size() <= pi) e->part_kept.resize(pi + 1, 0);
+      e->part_kept[pi] = n - (last_kid == 0xFFFFFFFFu ? last_cnt : 0);
+    }
     // routing (key column read, key/kid/idx written and sorted)
     bytes += (double)n * (8 + 8 + 4 + 4 + 2 * (4 + 4) + 3 * 4);
     if (gsp && gsp->n_groups > 0 && timed) {
@@ -2308,10 +2384,10 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       S.dir = ss.dir.p;
       S.journal = ss.journal.p;
       S.journal_idx = ss.journal_idx.p;
-      S.slab = ss.slab.p;
+      S.ring = ss.d_ring.p;
+      S.ring_cap = ss.d_cap.p;
       S.head = ss.head.p;
       S.tail = ss.tail.p;
-      S.sub_cap = ss.sub_cap;
       S.nsub = ss.nsub;
       S.lds_words = ss.lds_words;
       S.live = ss.live.p;
@@ -2441,17 +2517,19 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
       gen_restore_backup(e);
       for (size_t i = 0; i < nss; ++i) {
         auto& ss = *e->ssets[i];
+        std::vector<int64_t> demand(ss.nsub, 0);
+        if (serr[4 * i + 1] && ss.items > 0) {  // what the push tried to take from each ring
+          std::vector<unsigned long long> h(ss.nsub);
+          HIPCHK(hipMemcpy(h.data(), ss.head.p, ss.nsub * 8, hipMemcpyDeviceToHost));
+          for (int r = 0; r < ss.nsub; ++r) demand[r] = (int64_t)(h[r] - ss.h_push0[r]);
+        }
         slab_rollback(e, ss);
         if (serr[4 * i]) {  // a block outgrew the LDS staging area
           if (ss.lds_words >= 13312) throw Error(SDH_E_CAPACITY, "K_slab: more partials in one (key, group) block "
                                                                  "than the LDS staging area holds");
           ss.lds_words = std::min(13312, 2 * ss.lds_words);
         }
-        if (serr[4 * i + 1]) {  // a sub-ring ran out of room: plan for a push twice as large
-          ss.last_alloc = std::max<int64_t>(2 * ss.last_alloc, ss.sub_cap / 4);
-          slab_heads(e, ss);
-          slab_prepare(e, ss);
-        }
+        if (serr[4 * i + 1]) slab_prepare(e, ss, &demand);  // a ring ran out of room: reclaim / grow
       }
       if (pools_over) {
         gen_relayout(e, grown, true);
@@ -2477,11 +2555,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   for (auto& up : e->ssets) {
     auto& ss = *up;
     if (ss.items <= 0) continue;
-    const std::vector<unsigned long long> before = ss.h_head;
     slab_heads(e, ss);
-    int64_t alloc = 0;
-    for (int r = 0; r < ss.nsub; ++r) alloc = std::max<int64_t>(alloc, (int64_t)(ss.h_head[r] - before[r]));
-    ss.last_alloc = alloc;
     unsigned long long tr[256];
     HIPCHK(hipMemcpy(tr, ss.traffic.p, sizeof tr, hipMemcpyDeviceToHost));
     for (unsigned long long x : tr) bytes += (double)x;
@@ -2637,6 +2711,7 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   e->g_dev_matches = 0;
   e->g_used = 0;
   e->g_out_lost = false;
+  for (auto& k : e->part_kept) k = b->n;
   try {
     if (!qs.empty()) {
       bool unordered = false;
@@ -2668,10 +2743,16 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     e->broken = ex.what();
     throw;
   }
+  // (event, query) evaluations: a partition's queries see only the events routed to a key of this
+  // engine (null keys and other ranks' keys are not evaluated)
+  int64_t pe = b->n * consumers;
   for (const auto& g : e->gq)
-    if (g.recv_n[stream] > 0) consumers += 1;
+    if (g.recv_n[stream] > 0) {
+      ++consumers;
+      pe += g.partition >= 0 && g.partition < (int)e->part_kept.size() ? e->part_kept[g.partition] : b->n;
+    }
   if (consumers) {
-    e->stats.pattern_events += b->n * consumers;
+    e->stats.pattern_events += pe;
     e->stats.matches += e->device_matches + e->r_matches;
     e->stats.last_kernel_ms = ms;
     e->stats.last_kernel_bytes = bytes;
@@ -2999,7 +3080,7 @@ int sdh_engine_state_bytes(sdh_engine* e, int64_t* live_bytes, int64_t* reserved
       HIPCHK(hipMemcpyAsync(&w, acc.p, 8, hipMemcpyDeviceToHost, e->stream));
       HIPCHK(hipStreamSynchronize(e->stream));
       lb += (int64_t)w * 4;
-      rb += (int64_t)ss.nsub * ss.sub_cap * 4;
+      for (int64_t c : ss.cap) rb += c * 4;
       db += ss.key_cap * ss.n_groups * 8;
     }
     if (live_bytes) *live_bytes = lb;
@@ -3116,8 +3197,15 @@ int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
       dcopy.ensure(std::max<int64_t>(1, n_dir));
       packed.ensure(std::max<size_t>(1, (size_t)words));
       if (n_dir) HIPCHK(hipMemcpy(dcopy.p, ss.dir.p, n_dir * 8, hipMemcpyDeviceToDevice));
-      if (words && !slab_move(e, ss, std::vector<unsigned long long>(ss.nsub, ~0ull), packed.p, (int64_t)words, 1, ph.p,
-                              pt.p, dcopy.p))
+      DevBuf<uint32_t*> pr;
+      DevBuf<int64_t> pc;
+      pr.ensure(1);
+      pc.ensure(1);
+      const int64_t pcap = std::max<int64_t>(4, (int64_t)words);
+      HIPCHK(hipMemcpy(pr.p, &packed.p, sizeof(uint32_t*), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(pc.p, &pcap, 8, hipMemcpyHostToDevice));
+      if (words && !slab_move_raw(e, ss, dcopy.p, ss.d_ring.p, ss.d_cap.p, ss.tail.p, ss.nsub,
+                                  std::vector<unsigned long long>(ss.nsub, ~0ull), {}, pr.p, pc.p, ph.p, pt.p, 1))
         throw Error(SDH_E_DEVICE, "K_slab snapshot: packing failed");
       w.push_back(ss.partition);
       w.push_back(ss.key_cap);
@@ -3287,13 +3375,20 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
       slab_init(e, ss, std::max<int64_t>(1 << 16, 2 * (words / ss.nsub) + 65536));
       get_dev(ss.live.p, 256 * 8);
       DevBuf<unsigned long long> zt;
+      DevBuf<uint32_t*> pr;
+      DevBuf<int64_t> pc;
       zt.ensure(1);
+      pr.ensure(1);
+      pc.ensure(1);
+      const int64_t pcap = std::max<int64_t>(4, words);
       HIPCHK(hipMemset(zt.p, 0, 8));
-      if (words && !slab_move(e, ss, std::vector<unsigned long long>(1, ~0ull), ss.slab.p, ss.sub_cap, ss.nsub,
-                              ss.head.p, ss.tail.p, nullptr, packed.p, words, zt.p))
-        throw Error(SDH_E_CAPACITY, "K_slab restore: a sub-ring overflowed");
+      HIPCHK(hipMemcpy(pr.p, &packed.p, sizeof(uint32_t*), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(pc.p, &pcap, 8, hipMemcpyHostToDevice));
+      if (words && !slab_move_raw(e, ss, ss.dir.p, pr.p, pc.p, zt.p, 1, std::vector<unsigned long long>(1, ~0ull), {},
+                                  ss.d_ring.p, ss.d_cap.p, ss.head.p, ss.tail.p, ss.nsub))
+        throw Error(SDH_E_CAPACITY, "K_slab restore: a ring overflowed");
       slab_heads(e, ss);
-      ss.last_alloc = 0;
+      ss.h_push0 = ss.h_head;
     }
     e->g_dev_matches = 0;
     e->device_matches = 0;

@@ -33,14 +33,14 @@ __device__ __forceinline__ uint32_t sub_of(uint64_t dir_idx, int nsub) {
   return (uint32_t)(((dir_idx * 0x9E3779B97F4A7C15ull) >> 32) % (uint64_t)nsub);
 }
 
-// words [o, o + words) of sub-ring `sub`, or -1 when the sub-ring is full (a block never wraps: an
-// allocation that would straddle the ring's end is wasted and taken again)
+// words [o, o + words) of sub-ring `sub` (o: offset in its buffer), or -1 when the ring is full (a
+// block never wraps: an allocation that would straddle the ring's end is wasted and taken again)
 __device__ __forceinline__ int64_t ring_alloc(unsigned long long* head, uint64_t tail, int64_t cap, uint32_t sub,
                                               int64_t words) {
   unsigned long long o = atomicAdd(&head[sub], (unsigned long long)words);
   if ((int64_t)(o % (unsigned long long)cap) + words > cap) o = atomicAdd(&head[sub], (unsigned long long)words);
   if ((int64_t)(o + words - tail) > cap || (int64_t)(o % (unsigned long long)cap) + words > cap) return -1;
-  return (int64_t)sub * cap + (int64_t)(o % (unsigned long long)cap);
+  return (int64_t)(o % (unsigned long long)cap);
 }
 
 __device__ __forceinline__ int wave_prefix(int v, int bits, int* total) {
@@ -93,8 +93,9 @@ __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
     return;
   }
   // the old block -> LDS (coalesced), then each lane's range (entries are sorted by lane)
-  const int64_t off_old = (int64_t)(d0 & ((1ull << 40) - 1)) * 4;
-  for (int w = lane; w < n_old * EW; w += 64) ent[w] = L.slab[off_old + w];
+  const uint32_t sub = sub_of(dir_idx, L.nsub);
+  const uint32_t* old_blk = L.ring[sub] + (int64_t)(d0 & 0xffffffffull) * 4;
+  for (int w = lane; w < n_old * EW; w += 64) ent[w] = old_blk[w];
   __syncthreads();
   int b_l = 0, e_l = 0;
   {
@@ -275,17 +276,14 @@ __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
   uint64_t dnew = 0;
   if (M > 0) {
     const int64_t words = ((int64_t)M * EW + 3) & ~3ll;
-    if (lane == 0) {
-      const uint32_t sub = sub_of(dir_idx, L.nsub);
-      sh_base = ring_alloc(L.head, L.tail[sub], L.sub_cap, sub, words);
-    }
+    if (lane == 0) sh_base = ring_alloc(L.head, L.tail[sub], L.ring_cap[sub], sub, words);
     __syncthreads();
     const int64_t base = sh_base;
     if (base < 0) {
       if (lane == 0) atomicOr(&L.err[1], 1);
       return;
     }
-    uint32_t* dst = L.slab + base + (int64_t)pre * EW;
+    uint32_t* dst = L.ring[sub] + base + (int64_t)pre * EW;
     int t = 0;
     for (int k = b_l; k < e_l; ++k) {
       const uint32_t* e = ent + k * EW;
@@ -324,33 +322,43 @@ __global__ void slab_rollback_kernel(uint64_t* dir, const uint64_t* journal, con
   if (journal_idx[i] != ~0ull) dir[journal_idx[i]] = journal[i];
 }
 
-// Move the blocks of the directory entries [0, n_dir) whose sub-ring position is before limit[sub]
-// (in the source slab) to the head of their sub-ring in the destination slab: reclaiming a sub-ring's
-// oldest part (src == dst), growing the slab (every block, into a larger one), or packing it for a
-// snapshot (dst: one ring). err[0] = 1 when a destination sub-ring is full.
+// Move the blocks of the directory entries [0, n_dir) of the sub-rings marked in `active` whose ring
+// position is before limit[sub] (in the source rings) to the head of their ring in the destination:
+// reclaiming a ring's oldest blocks (src == dst), growing rings (every block into larger buffers),
+// packing for a snapshot (dst_nsub == 1: one ring) or unpacking a snapshot (src_nsub == 1). A block
+// keeps its old place until its directory word moves; err[0] = 1 when a destination ring is full.
+struct SlabRings {
+  uint32_t* const* ring;
+  const int64_t* cap;
+  unsigned long long* head;
+  const unsigned long long* tail;
+  int32_t nsub;
+};
 __global__ void slab_move_kernel(uint64_t* dir, int64_t n_dir, int groups, const int32_t* __restrict__ group_ew,
-                                 const uint32_t* src, int64_t src_cap, const unsigned long long* src_tail,
-                                 const unsigned long long* limit, uint32_t* dst, int64_t dst_cap, int dst_nsub,
-                                 unsigned long long* dst_head, const unsigned long long* dst_tail, int32_t* err) {
+                                 SlabRings src, const unsigned long long* limit, const uint8_t* active, SlabRings dst,
+                                 int32_t* err) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (x >= n_dir) return;
   const uint64_t d = dir[x];
   const int n = (int)((d >> 40) & 0xffff);
   if (n == 0) return;
-  const int64_t off = (int64_t)(d & ((1ull << 40) - 1)) * 4;
-  const int64_t sub = off / src_cap, rel = off - sub * src_cap;
-  const uint64_t t = src_tail[sub];
-  const uint64_t logical = t + (uint64_t)((rel - (int64_t)(t % (uint64_t)src_cap) + src_cap) % src_cap);
-  if (logical >= limit[sub]) return;
+  const uint32_t ss = src.nsub == 1 ? 0u : sub_of((uint64_t)x, src.nsub);
+  if (active && !active[ss]) return;
+  const int64_t rel = (int64_t)(d & 0xffffffffull) * 4, cap = src.cap[ss];
+  const uint64_t t = src.tail[ss];
+  const uint64_t logical = t + (uint64_t)((rel - (int64_t)(t % (uint64_t)cap) + cap) % cap);
+  if (logical >= limit[ss]) return;
   const int64_t words = ((int64_t)n * group_ew[x % groups] + 3) & ~3ll;
-  const uint32_t ds = dst_nsub == 1 ? 0u : sub_of((uint64_t)x, dst_nsub);
-  const int64_t o = ring_alloc(dst_head, dst_tail[ds], dst_cap, ds, words);
+  const uint32_t ds = dst.nsub == 1 ? 0u : sub_of((uint64_t)x, dst.nsub);
+  const int64_t o = ring_alloc(dst.head, dst.tail[ds], dst.cap[ds], ds, words);
   if (o < 0) {
     atomicOr(err, 1);
     return;
   }
-  for (int64_t w = 0; w < words; ++w) dst[o + w] = src[off + w];
-  dir[x] = (uint64_t)(o / 4) | (d & ~((1ull << 40) - 1));
+  const uint32_t* from = src.ring[ss] + rel;
+  uint32_t* to = dst.ring[ds] + o;
+  for (int64_t w = 0; w < words; ++w) to[w] = from[w];
+  dir[x] = (uint64_t)(o / 4) | (d & ~0xffffffffull);
 }
 
 // live words of the blocks (stats: bytes per live partial)
@@ -385,13 +393,16 @@ extern "C" hipError_t sdh_slab_rollback(uint64_t* dir, const uint64_t* journal, 
 }
 
 extern "C" hipError_t sdh_slab_move(uint64_t* dir, int64_t n_dir, int groups, const int32_t* group_ew,
-                                    const uint32_t* src, int64_t src_cap, const unsigned long long* src_tail,
-                                    const unsigned long long* limit, uint32_t* dst, int64_t dst_cap, int dst_nsub,
-                                    unsigned long long* dst_head, const unsigned long long* dst_tail, int32_t* err,
-                                    hipStream_t s) {
+                                    uint32_t* const* src_ring, const int64_t* src_cap,
+                                    const unsigned long long* src_tail, int src_nsub, const unsigned long long* limit,
+                                    const uint8_t* active, uint32_t* const* dst_ring, const int64_t* dst_cap,
+                                    unsigned long long* dst_head, const unsigned long long* dst_tail, int dst_nsub,
+                                    int32_t* err, hipStream_t s) {
   if (n_dir <= 0) return hipSuccess;
+  const sdh::SlabRings S{src_ring, src_cap, nullptr, src_tail, src_nsub};
+  const sdh::SlabRings D{dst_ring, dst_cap, dst_head, dst_tail, dst_nsub};
   hipLaunchKernelGGL(sdh::slab_move_kernel, dim3((unsigned)((n_dir + 255) / 256)), dim3(256), 0, s, dir, n_dir, groups,
-                     group_ew, src, src_cap, src_tail, limit, dst, dst_cap, dst_nsub, dst_head, dst_tail, err);
+                     group_ew, S, limit, active, D, err);
   return hipGetLastError();
 }
 

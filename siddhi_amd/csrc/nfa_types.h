@@ -325,7 +325,8 @@ struct PartLaunch {
 // ------------------------------------------------------------------------------------------
 // K_slab launch (nfa_slab.hip): distinct-stream patterns on sparse per-partial entries (slab.h)
 // item = (key segment of the pushed stream, group from glist); block (kid, g) = dir[kid * groups + g]
-//   dir word: offset / 4 (bits 0-39) | entries (40-55) | states with a non-empty list (56-63)
+// in sub-ring sub_of(kid * groups + g) (a separately allocated ring buffer)
+//   dir word: offset / 4 in the sub-ring (bits 0-31) | entries (40-55) | states with a non-empty list (56-63)
 // ------------------------------------------------------------------------------------------
 namespace slab {
 struct Shape;
@@ -351,10 +352,10 @@ struct SlabLaunch {
   uint64_t* dir;              // [key_cap * groups]
   uint64_t* journal;          // [item] the directory value a changed item replaced
   uint64_t* journal_idx;      // [item] its directory index (~0: unchanged; the host clears them)
-  uint32_t* slab;             // nsub sub-rings of sub_cap words
+  uint32_t* const* ring;      // [nsub] sub-ring buffers
+  const int64_t* ring_cap;    // [nsub] words of each
   unsigned long long* head;   // [nsub] logical allocation heads (monotone)
   const unsigned long long* tail;  // [nsub] oldest live logical word
-  int64_t sub_cap;
   int32_t nsub;
   int32_t lds_words;          // dynamic LDS (uint32 words) for a block's entries
   long long* live;            // [256] live-partial counters (sum = live partials)
