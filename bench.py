@@ -1,25 +1,31 @@
 #!/usr/bin/env python3
-"""NFA-step throughput benchmark (BASELINE.json metric: events/s x active patterns, at 10K patterns).
+"""NFA-step throughput benchmark (BASELINE.json metric: events/s x active patterns, whole node, at 10K
+patterns).
 
 Workload (default; BASELINE.json configs[1] at the metric's 10K patterns, SURVEY §8(d) C2 family):
-P = 10,000 concurrent 2-state patterns per GPU
+P = 10,000 concurrent 2-state patterns in total
     every e1=StockStream[price > T_p] -> e2=StockStream[price > e1.price] within W_p
 over the seeded synthetic StockStream (20 B/event SoA), generated on the device and resident in HBM
-before the timed region. One step = one NFA-step pass (one sdh_engine_push) over a batch of B = 8M
-events; every match record is written to HBM (SDH_FLAG_DEVICE_MATCHES: counted, not polled).
-`--workload c3 | c4 | c5` runs the count/logical partitioned family, one GPU's shard of the fraud
-sequences, or the C5 family (four joined streams, mixed 2-4-state patterns under one `partition with`
-key, `within 1 hour`; one step = one batch per stream; reduced pattern / key counts)
-instead.
+before the timed region. One step = one NFA-step pass (one sdh_engine_push per GPU) over a batch of
+B = 8M events; every match record is written to HBM (SDH_FLAG_DEVICE_MATCHES: counted, not polled).
+`--workload c3 | c4 | c5` runs the count/logical partitioned family (1000 patterns x 10K keys), the
+10K fraud-rule sequences, or the C5 family (100K mixed patterns over four joined streams under one
+`partition with` key, `within 1 hour`; one step = one batch per stream; one GPU = one of the 8-GPU
+node's key shards).
+
+Multi-GPU (torchrun, one process per GPU). `--scaling strong` (default) measures the metric as
+defined, the whole node at 10K patterns: the P patterns are split over the N GPUs by pattern set
+(strided: rank r runs patterns r, r+N, ...; c3: the partition keys are split instead, rank r owning
+|String.valueOf(key).hashCode() % N| == r). `--scaling weak` gives every GPU P patterns; a strong N>1
+run appends that as a second line (`weak_scaling`). Rank 0 generates each batch and broadcasts it
+over RCCL (the event broadcast of SURVEY §8(e)) inside the timed region; the other ranks receive
+into zeroed buffers. `value` = pattern-events summed over ranks / the max over ranks of the timed
+region (barrier + device sync on both sides).
 
 Match expansion (`expansion` in the JSON line): a second engine in normal mode runs pushes of a
 smaller batch followed by sdh_engine_poll_device -- the device R18 sort and the gather of the ABI
-tuples (query, key, ts, off, words) in HBM -- and times both.
-
-Multi-GPU (torchrun, one process per GPU): weak scaling by pattern set -- rank r runs patterns
-r*P .. r*P+P-1 of the family. Rank 0 generates each batch and broadcasts it over RCCL (the event
-broadcast of SURVEY §8(e)) inside the timed region; match counts are all-reduced. Timing: barrier +
-device sync on both sides of the K timed steps, max over ranks.
+tuples (query, key, ts, off, words) in HBM; with N GPUs the tuples of every rank are then gathered to
+rank 0 over RCCL and k-way merged there (siddhi_amd/dist.py), timed per matched tuple.
 """
 import argparse
 import glob
@@ -34,10 +40,11 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-DEFAULTS = {  # workload -> (patterns per GPU, events per step, keys)
+DEFAULTS = {  # workload -> (patterns, events per step, keys); patterns are the node total under strong
+    # scaling and per GPU under weak scaling (c5: always per GPU, one of the 8-GPU node's key shards)
     "c2": (10000, 1 << 23, 100),
     "c3": (1000, 1 << 20, 10000),
-    "c4": (1250, 1 << 20, 100_000),
+    "c4": (10000, 1 << 20, 100_000),
     "c5": (100_000, 1 << 16, 125_000),  # patterns, events per stream per GPU per step, accounts per GPU
 }
 C5_NODE = 8  # BASELINE configs[4] is one 8-GPU node: every rank is one of 8 key shards of 1M accounts
@@ -49,10 +56,14 @@ def parse():
     ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=list(DEFAULTS), default="c2",
-                    help="c2: BASELINE configs[1] at 10K patterns (headline); c3: configs[2] (count/logical, "
-                         "partitioned); c4: configs[3] (fraud-rule sequences, one GPU's pattern-set shard)")
+                    help="c2: BASELINE configs[1] at the metric's 10K patterns (headline); c3: configs[2] "
+                         "(count/logical, partitioned); c4: configs[3] (10K fraud-rule sequences); c5: configs[4]")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong (default): the workload's patterns (c3: keys) are split over the N GPUs -- "
+                         "the metric's 'whole node at 10K patterns'; weak: every GPU runs that many patterns")
+    ap.add_argument("--no-weak-leg", action="store_true", help="N>1 strong runs: skip the weak-scaling line")
     ap.add_argument("--keys", type=int, default=0, help="partition keys / symbols (default per workload)")
-    ap.add_argument("--patterns", type=int, default=0, help="patterns per GPU (default per workload)")
+    ap.add_argument("--patterns", type=int, default=0, help="patterns (default per workload)")
     ap.add_argument("--batch", type=int, default=0, help="events per step (default per workload; C2: 12 steps x 8M = 1.0e8 timed events)")
     ap.add_argument("--partials", type=int, default=128)
     ap.add_argument("--expansion-batch", type=int, default=1 << 16)
@@ -63,26 +74,47 @@ def parse():
     return ap.parse_args()
 
 
-def app_source(workload, P, first):
+def app_source(workload, n, first, step=1):
     from siddhi_amd.workloads import c2_app, c3_app, c4_app, c5_app
-    return {"c2": c2_app, "c3": c3_app, "c4": c4_app, "c5": c5_app}[workload](P, first=first)
+    return {"c2": c2_app, "c3": c3_app, "c4": c4_app, "c5": c5_app}[workload](n, first=first, step=step)
 
 
-def make_engine(workload, P, first, K, device, flags, partials, shard=(0, 1)):
+class Shard:
+    """This rank's share of a workload: the patterns first, first+step, ... (n of them) and, for key
+    sharding, (rank, world) of the partition keys (sdh_config.shard_rank / shard_world)."""
+
+    def __init__(self, workload, scaling, P, rank, world):
+        self.keyed = (workload == "c5") or (workload == "c3" and scaling == "strong")
+        if workload == "c5":
+            self.first, self.step, self.n, self.key_shard = 0, 1, P, (rank, C5_NODE)
+        elif scaling == "weak":
+            self.first, self.step, self.n, self.key_shard = rank * P, 1, P, (0, 1)
+        elif workload == "c3":
+            self.first, self.step, self.n, self.key_shard = 0, 1, P, (rank, world)
+        else:  # pattern-set sharding, strided (balances the threshold / multiplier mix)
+            self.first, self.step, self.n, self.key_shard = rank, world, len(range(rank, P, world)), (0, 1)
+
+    def global_q(self, q):
+        """local query index (tensor) -> the full program's query index"""
+        return self.first + q * self.step
+
+
+def make_engine(workload, sh, K, device, flags, partials):
     from siddhi_amd import ql
     from siddhi_amd.engine import HipEngine
     from siddhi_amd.planner import plan
-    blob = plan(ql.parse(app_source(workload, P, first))).serialize()
+    blob = plan(ql.parse(app_source(workload, sh.n, sh.first, sh.step))).serialize()
+    kr, kw = sh.key_shard
     if workload == "c4":
         # a sequence instance holds at most one partial per state (R8): small pools
         return HipEngine(blob, device=device, flags=flags, gen_pool_states=8, gen_pool_nodes=32, gen_list_cap=8)
     if workload == "c5":  # key sharding: every rank runs all patterns over its own accounts (K_slab)
-        return HipEngine(blob, device=device, flags=flags, gen_max_keys=max(1024, 2 * K), shard_rank=shard[0],
-                         shard_world=shard[1])
+        return HipEngine(blob, device=device, flags=flags, gen_max_keys=max(1024, 2 * K), shard_rank=kr,
+                         shard_world=kw)
     if workload == "c3":
         pools = [int(x) for x in os.environ.get("SDH_C3_POOLS", "32,128,32").split(",")]
         return HipEngine(blob, device=device, flags=flags, gen_pool_states=pools[0], gen_pool_nodes=pools[1],
-                         gen_list_cap=pools[2], gen_max_keys=max(1024, 2 * K))
+                         gen_list_cap=pools[2], gen_max_keys=max(1024, 2 * K), shard_rank=kr, shard_world=kw)
     return HipEngine(blob, device=device, partials=partials, flags=flags)
 
 
@@ -98,6 +130,14 @@ def gen_batch(workload, start, n, K, dev):
     gen = txn_events_torch if workload == "c4" else stock_events_torch
     ts, a, b, c = gen(start, n, K, dev)
     return [ts, a, b.view(__import__("torch").int32), c]
+
+
+T_START = time.time()
+
+
+def log(msg):
+    """progress on stderr (the JSON line stays alone on stdout)"""
+    print(f"[bench {time.time() - T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def cpu_cores():
@@ -215,6 +255,62 @@ def profiled(kernel, workload, patterns, batch):
     return None, None
 
 
+def timed_steps(eng, step, warmup, steps, world, dist):
+    """W untimed steps, then K timed ones bracketed by barrier + device sync; returns (elapsed max over
+    ranks, per-step kernel ms, per-step algorithmic bytes, matches, pattern-events summed over ranks)."""
+    import torch
+    for i in range(warmup):
+        t = time.perf_counter()
+        step(i)
+        log(f"warm-up step {i + 1}/{warmup}: {(time.perf_counter() - t) * 1e3:.1f} ms, last kernel "
+            f"{eng.stats().last_kernel_ms:.1f} ms")
+    kern_ms, kern_bytes, matches = [], [], 0
+    pe0 = eng.stats().pattern_events
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(warmup, warmup + steps):
+        ms, by, nm = step(i)
+        kern_ms.append(ms)
+        kern_bytes.append(by)
+        matches += nm
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    log(f"{steps} timed steps: {elapsed * 1e3 / steps:.2f} ms/step")
+    # (event, pattern) evaluations the engine performed: B x patterns for pattern-set shards, each
+    # rank's own keys' events x patterns for key shards (sdh_stats.pattern_events)
+    pe = float(eng.stats().pattern_events - pe0)
+    return elapsed, kern_ms, kern_bytes, matches, pe
+
+
+def reduce_run(elapsed, matches, pe, live, world, dist, cdev):
+    import torch
+    if world > 1:
+        t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        mt = torch.tensor([matches, live, pe], device=cdev, dtype=torch.float64)
+        dist.all_reduce(mt)
+        matches, live, pe = int(mt[0].item()), int(mt[1].item()), float(mt[2].item())
+    return elapsed, matches, pe, live
+
+
+def launches_per_step(prof, prof_dir):
+    """Launches of the profiled kernel per bench step: its rocprof call count over the profiled run's
+    pushes (warm-up + steps of its recorded bench arguments)."""
+    if not prof:
+        return 1
+    try:
+        a = json.load(open(os.path.join(ROOT, prof_dir, "meta.json")))["bench_args"].split()
+        n = int(a[a.index("--steps") + 1]) + int(a[a.index("--warmup") + 1])
+        return max(1, round(prof["calls"] / n))
+    except (OSError, ValueError, KeyError, IndexError):
+        return 1
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,28 +340,39 @@ def main():
     B = args.batch or B0
     K = args.keys or K0
     c5 = args.workload == "c5"
+    scaling = "weak" if c5 else args.scaling
+    sh = Shard(args.workload, scaling, P, rank, world)
+    t_build = time.perf_counter()
     if c5:  # key sharding (weak scaling): rank r is shard r of the 8-GPU node's 1M accounts; every step
         # each stream carries the node's B * 8 events (generated by rank 0, broadcast) and a rank
         # evaluates the ~B of them whose account it owns against all P patterns
         if world > C5_NODE:
             raise SystemExit(f"--workload c5 models one {C5_NODE}-GPU node")
-        t_build = time.perf_counter()
-        eng = make_engine("c5", P, 0, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials, shard=(rank, C5_NODE))
-        t_build = time.perf_counter() - t_build
         B, K_gen = B * C5_NODE, K * C5_NODE
         # `within 1 hour` of event time: the untimed warm-up covers an hour (the state's steady size)
         args.warmup = max(args.warmup, -(-3_600_000 // B) + 1)
         args.no_expansion = args.no_ingest = True  # (single-stream helpers)
     else:
-        eng = make_engine(args.workload, P, rank * P, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials)
         K_gen = K
+    log(f"building the engine: {args.workload}, {sh.n} patterns on this GPU, {B} events per step")
+    eng = make_engine(args.workload, sh, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials)
+    t_build = time.perf_counter() - t_build
+    log(f"engine built in {t_build:.1f} s")
 
     n_batches = args.warmup + args.steps
     # synthetic batches generated on the device before the timed region (rank 0's copy is the
-    # broadcast source in multi-GPU runs; the other ranks receive into their own buffers)
-    batches = [gen_batch(args.workload, s * B, B, K_gen, dev) for s in range(n_batches)] if not c5 else None
-    torch.cuda.synchronize()
+    # broadcast source in multi-GPU runs; the other ranks receive into zeroed buffers, so a missing
+    # broadcast shows as wrong matches)
     bcast = world > 1
+
+    def local_batch(i):
+        cols = gen_batch(args.workload, i * B, B, K_gen, dev)
+        if c5:
+            return cols if rank == 0 or not bcast else [[torch.zeros_like(t) for t in c] for c in cols]
+        return [cols] if rank == 0 or not bcast else [[torch.zeros_like(t) for t in cols]]
+
+    pre = [local_batch(i) for i in range(args.warmup, n_batches)]
+    torch.cuda.synchronize()
 
     def bcast_into(t):
         if backend == "nccl":
@@ -275,75 +382,47 @@ def main():
             dist.broadcast(tc, src=0)
             t.copy_(tc)
 
-    if c5:
-        # rank 0's batches of the timed steps are generated before the timed region; the other
-        # ranks receive them into zeroed buffers (a missing broadcast shows as wrong matches)
-        def c5_batch(i):
-            cols = gen_batch("c5", i * B, B, K_gen, dev)
-            return cols if rank == 0 or not bcast else [[torch.zeros_like(t) for t in c] for c in cols]
-        c5_pre = [c5_batch(i) for i in range(args.warmup, n_batches)]
+    def make_step(engine, batches):
+        def step(i):
+            """One step: every stream's batch pushed once (broadcast from rank 0 first); returns
+            (kernel ms, algorithmic bytes, matches) summed over the step's pushes."""
+            if i < args.warmup:  # generated now (torch's stream): complete before the engine reads it
+                per_stream = local_batch(i)
+                torch.cuda.synchronize()
+            else:
+                per_stream = batches[i - args.warmup]
+            ms = by = 0.0
+            nm = 0
+            for si, cols in enumerate(per_stream):
+                if bcast:
+                    for t in cols:
+                        bcast_into(t)
+                engine.push_device(si, B, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
+                if len(per_stream) > 1 or i >= args.warmup:
+                    st = engine.stats()
+                    ms += st.last_kernel_ms
+                    by += st.last_kernel_bytes
+                    nm += engine.pending_matches()
+            return ms, by, nm
+        return step
 
-    def step(i):
-        """One step: every stream's batch pushed once; returns (kernel ms, algorithmic bytes, matches)
-        summed over the step's pushes."""
-        per_stream = ((c5_batch(i) if i < args.warmup else c5_pre[i - args.warmup]) if c5 else [batches[i]])
-        ms = by = 0.0
-        nm = 0
-        for si, cols in enumerate(per_stream):
-            if bcast:
-                for t in cols:
-                    bcast_into(t)
-            eng.push_device(si, B, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
-            if len(per_stream) > 1 or i >= args.warmup:
-                st = eng.stats()
-                ms += st.last_kernel_ms
-                by += st.last_kernel_bytes
-                nm += eng.pending_matches()
-        return ms, by, nm
-
-    for i in range(args.warmup):
-        step(i)
-    kern_ms, kern_bytes, matches = [], [], 0
-    pe0 = eng.stats().pattern_events
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.warmup, n_batches):
-        ms, by, nm = step(i)
-        kern_ms.append(ms)
-        kern_bytes.append(by)
-        matches += nm
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed, kern_ms, kern_bytes, matches, pe = timed_steps(eng, make_step(eng, pre), args.warmup, args.steps,
+                                                           world, dist)
     live = eng.stats().live_partials
-    # C5: (event, pattern) evaluations the engine performed (each rank's own accounts' events
-    # against the patterns reading their stream)
-    pe = float(eng.stats().pattern_events - pe0)
-    if world > 1:
-        t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        mt = torch.tensor([matches, live, pe], device=cdev, dtype=torch.float64)
-        dist.all_reduce(mt)
-        matches, live, pe = int(mt[0].item()), int(mt[1].item()), float(mt[2].item())
-    del batches
-
-    total_pe = pe if c5 else float(B) * args.steps * P * world
-    value = total_pe / elapsed
+    elapsed, matches, pe, live = reduce_run(elapsed, matches, pe, live, world, dist, cdev)
+    value = pe / elapsed
     avg_ms = float(np.mean(kern_ms))
     avg_bytes = float(np.mean(kern_bytes))
     achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
     peak = 8000.0
+    per_gpu = "per GPU" if scaling == "weak" else f"in total over {world} GPU(s)"
     if args.workload == "c2":
-        wl = (f"C2 at the metric's 10K patterns: {P} concurrent 2-state filter+reference patterns per GPU "
+        wl = (f"C2 at the metric's 10K patterns: {P} concurrent 2-state filter+reference patterns {per_gpu} "
               "(every e1[price>T_p] -> e2[price>e1.price] within W_p)")
         kernel = "nfa_ratchet_kernel"
     elif args.workload == "c3":
-        wl = (f"C3: count <2:5> + logical and/or patterns, partition with (symbol) over {K} keys, "
-              "within 10 sec")
+        wl = (f"C3: {P} count <2:5> + logical and/or patterns, partition with (symbol) over {K} keys, "
+              f"within 10 sec; " + (f"key shards x{world}" if sh.keyed else f"{P} patterns per GPU"))
         kernel = "sdh_part_spec"
     elif c5:
         wl = (f"C5: {P} mixed 2-4-state patterns (cross-stream reference, and, or, count) over 4 joined streams, "
@@ -351,11 +430,12 @@ def main():
               f"{list(range(world))} of {C5_NODE} ({K} accounts each); {B} node events per stream per step")
         kernel = "nfa_slab_kernel"
     else:
-        wl = ("C4: fraud-rule sequences every e1=Txn[..], e2=Txn[..e1.amount*M], e3=Txn[..] within 1 min "
-              f"(strict contiguity), {K} accounts, pattern-set shard {rank * P}..{rank * P + P - 1}")
+        wl = (f"C4: {P} fraud-rule sequences {per_gpu}: every e1=Txn[..], e2=Txn[..e1.amount*M], e3=Txn[..] "
+              f"within 1 min (strict contiguity), {K} accounts")
         kernel = "sdh_seq_spec"
-    prof, prof_dir = profiled(kernel, args.workload, P, B)
+    prof, prof_dir = profiled(kernel, args.workload, sh.n, B)
     traffic = prof.get("traffic_bytes") if prof else None
+    launches = launches_per_step(prof, prof_dir)
     result = {
         "metric": "events/sec x active patterns (whole node) at 10K patterns; achieved HBM GB/s",
         "value": value,
@@ -365,23 +445,26 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded splitmix64 StockStream / Txn stream, SURVEY §8(d)), generated in HBM",
-        "config": {"workload": wl, "patterns_per_gpu": P, "events_per_step": B * (4 if c5 else 1),
+        "data": "synthetic (seeded splitmix64 StockStream / Txn / C5 streams, SURVEY §8(d)), generated in HBM",
+        "config": {"workload": wl, "patterns_total": P * (world if scaling == "weak" else 1),
+                   "patterns_per_gpu": sh.n, "events_per_step": B * (4 if c5 else 1),
                    "timed_events": B * args.steps * (4 if c5 else 1),
-                   "keys": K, "parallelism": (f"key shards x{world}" if c5 else f"pattern-set x{world}") +
+                   "keys": K, "parallelism": (f"key shards x{world}" if sh.keyed else f"pattern-set x{world}") +
                    (" (RCCL event broadcast)" if bcast else ""),
                    "matches": matches, "matches_per_s": matches / elapsed, "live_partials": live,
                    "source_hash": source_hash(kernel)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic, "traffic_source": prof_dir,
                      "kernel": kernel, "kernel_ms": avg_ms,
-                     # measured HBM rate (PMC traffic / live kernel time); below `achieved` when the
-                     # device record is narrower than §8(d)'s 32-B match unit
-                     # measured HBM rate: PMC bytes per launch / the profile's average launch time
-                     "traffic_gbps": (traffic / (prof["kernel_ns_avg"] * 1e-9) / 1e9) if traffic else None},
+                     # measured HBM rate: the profile's PMC bytes per launch over its average launch
+                     # time (below `achieved` when the device record is narrower than §8(d)'s 32-B
+                     # match unit); per step: x launches per step
+                     "traffic_gbps": (traffic / (prof["kernel_ns_avg"] * 1e-9) / 1e9) if traffic else None,
+                     "launches_per_step": launches,
+                     "traffic_per_step": traffic * launches if traffic else None},
     }
     if prof:
         result["roofline"]["counters"] = {k: v for k, v in prof.items() if k != "traffic_bytes"}
@@ -390,11 +473,28 @@ def main():
         result["config"].update({"state_live_bytes": lb, "state_slab_bytes": rb, "state_dir_bytes": db,
                                  "bytes_per_live_partial": (lb + db) / max(1, live),
                                  "engine_build_s": t_build, "warmup_event_hours": args.warmup * B / 3.6e6})
+    del pre
+    if world > 1 and scaling == "strong" and not args.no_weak_leg:
+        # the second line: weak scaling, every GPU runs the workload's full pattern count
+        eng.close()
+        wsh = Shard(args.workload, "weak", P, rank, world)
+        weng = make_engine(args.workload, wsh, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials)
+        wsteps = max(2, args.steps // 3)
+        wpre = [local_batch(i) for i in range(args.warmup, args.warmup + wsteps)]
+        el, _, _, wm, wpe = timed_steps(weng, make_step(weng, wpre), args.warmup, wsteps, world, dist)
+        el, wm, wpe, _ = reduce_run(el, wm, wpe, 0, world, dist, cdev)
+        result["weak_scaling"] = {"value": wpe / el, "unit": "pattern-events/s", "patterns_per_gpu": wsh.n,
+                                  "steps": wsteps, "ms_per_step": el * 1e3 / wsteps, "matches": wm}
+        weng.close()
+        del wpre
     if not args.no_expansion:
-        result["expansion"] = expansion(args, P, rank, K, local, dev, world, cdev, dist)
+        log("expansion leg (normal mode + sdh_engine_poll_device)")
+        result["expansion"] = expansion(args, sh, K, local, dev, world, cdev, dist)
     if not args.no_ingest and world == 1:
+        log("host-ingest leg")
         result["host_ingest"] = host_ingest(args, eng, B, K, n_batches)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(args.workload, K, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -429,20 +529,23 @@ def eng_patterns(eng):
     return st.pattern_events / max(1, st.events)
 
 
-def expansion(args, P, rank, K, local, dev, world, cdev, dist):
+def expansion(args, sh, K, local, dev, world, cdev, dist):
     """Pushes of a smaller batch in normal mode, each followed by sdh_engine_poll_device (device R18
-    sort + gather of the ABI tuples in HBM): the NFA step with every match expanded. With N GPUs the
-    R18-sorted tuples are then gathered to rank 0 over RCCL and merged there (siddhi_amd/dist.py)."""
+    sort + gather of the ABI tuples in HBM): the NFA step with every match expanded. With N GPUs every
+    rank's R18-sorted tuples are then gathered to rank 0 over RCCL and merged there (siddhi_amd/dist.py:
+    a k-way merge of the sorted runs), timed per step."""
     import torch
     from siddhi_amd import dist as sdist
-    # with N GPUs every rank's tuples are gathered to rank 0: at 10K patterns per rank a 64K-event
-    # batch is ~280M matches per rank, so the multi-GPU gather runs on 2K-event batches
-    E = args.expansion_batch if world == 1 else min(args.expansion_batch, 2048)
-    eng = make_engine(args.workload, P, rank * P, K, local, 0, args.partials)
+    # with N GPUs every rank's tuples are gathered to rank 0: C2 at 10K patterns makes ~4,300 matches
+    # per event, so the multi-GPU gather runs on 8K-event batches
+    E = args.expansion_batch if world == 1 else min(args.expansion_batch, 8192)
+    eng = make_engine(args.workload, sh, K, local, 0, args.partials)
     steps, warm = 4, 1
     bs = [gen_batch(args.workload, s * E, E, K, dev) for s in range(steps + warm)]
-    log = sdist.StreamLog()
-    table = torch.arange(P * world, dtype=torch.int64)  # one stream, queries in definition order
+    slog = sdist.StreamLog()
+    # one stream: the receiver rank of a query is its index in the full program (every query of
+    # these families reads the one stream; c3's partition receivers are all multi-processor ones)
+    table = torch.arange((args.patterns or DEFAULTS[args.workload][0]) * world, dtype=torch.int64)
     torch.cuda.synchronize()
     push_ms, gather_ms, matches, merged = 0.0, 0.0, 0, 0
     for i, cols in enumerate(bs):
@@ -453,28 +556,32 @@ def expansion(args, P, rank, K, local, dev, world, cdev, dist):
             t0 = time.perf_counter()
         t1 = time.perf_counter()
         eng.push_device(0, E, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
-        log.push(0, E)
+        slog.push(0, E)
+        torch.cuda.synchronize()
         t2 = time.perf_counter()
-        if world > 1 and args.workload == "c2":
+        if world > 1:
             mc = sdist.columns_from_device(eng, dev)
-            mc["q"] += rank * P  # this rank's sub-app numbers its queries from 0
+            mc["q"] = sh.global_q(mc["q"])  # this rank's sub-app numbers its queries from 0
             if cdev.type != "cuda":  # gloo rehearsal: the collectives take host tensors
                 mc = {k: v.to(cdev) for k, v in mc.items()}
             t3 = time.perf_counter()
             per_rank = sdist.gather_columns(mc)
-            if rank == 0:
-                out = sdist.merge_columns(None, per_rank, log, table=table, n_streams=1)
+            if dist.get_rank() == 0:
+                out = sdist.merge_columns(None, per_rank, slog, table=table.to(cdev), n_streams=1)
                 merged += int(out["q"].numel())
             torch.cuda.synchronize()
             n_local = int(mc["q"].numel())
             t4 = time.perf_counter()
         else:
             n_local = eng.poll_device().n
+            torch.cuda.synchronize()
             t3 = t4 = time.perf_counter()
         if i >= warm:
             push_ms += (t2 - t1) * 1e3
             gather_ms += (t4 - t3) * 1e3
             matches += n_local
+        log(f"expansion push {i + 1}/{steps + warm}: {n_local} matches, push {(t2 - t1) * 1e3:.1f} ms, "
+            f"poll/gather {(time.perf_counter() - t2) * 1e3:.1f} ms")
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
@@ -483,13 +590,20 @@ def expansion(args, P, rank, K, local, dev, world, cdev, dist):
         mt = t[1:].clone()
         dist.all_reduce(mt)
         el, matches = float(t[0].item()), int(mt.item())
+    pe = eng.stats().pattern_events
     eng.close()
+    if world > 1:
+        x = torch.tensor([float(pe)], device=cdev, dtype=torch.float64)
+        dist.all_reduce(x)
+        pe = float(x.item())
+    pe_timed = pe * steps / (steps + warm)
     r = {"events_per_step": E, "steps": steps, "ms_per_step": el * 1e3 / steps,
-         "push_ms_per_step": push_ms / steps, "matches_per_step": matches / steps,
-         "pattern_events_per_s": E * steps * P * world / el, "matches_per_s": matches / el}
-    if world > 1 and args.workload == "c2":
+         "push_ms_per_step": push_ms / steps, "poll_ms_per_step": (el * 1e3 - push_ms - gather_ms) / steps,
+         "matches_per_step": matches / steps, "pattern_events_per_s": pe_timed / el, "matches_per_s": matches / el}
+    if world > 1:
         r["rccl_gather_merge_ms_per_step"] = gather_ms / steps
         r["merged_matches_per_step_rank0"] = merged / steps
+        r["gather_merge_ns_per_match"] = gather_ms * 1e6 / max(1, matches)
     return r
 
 

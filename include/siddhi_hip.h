@@ -89,8 +89,10 @@ typedef struct sdh_config {
  *   INT -> int32, LONG -> int64, FLOAT -> float, DOUBLE -> double, BOOL -> uint8,
  *   STRING -> int32 dictionary id (ids are assigned by the caller; equal strings, equal ids).
  * nulls[a] (optional, may be NULL or have NULL entries) is a uint8 mask, 1 = null.
- * on_device != 0: all pointers are HIP device pointers already resident in HBM; otherwise they
- * are host pointers (pinned memory recommended) and are copied before sdh_engine_push returns. */
+ * on_device != 0: all pointers are HIP device pointers already resident in HBM, and their contents
+ * complete (the engine runs on its own non-blocking stream: the caller synchronizes the stream that
+ * produced them); otherwise they are host pointers (pinned memory recommended) and are copied before
+ * sdh_engine_push returns. */
 typedef struct sdh_batch {
   int64_t n;
   const int64_t* ts;
@@ -109,6 +111,10 @@ typedef struct sdh_batch {
  * seq[i] is the sequence number of the event whose processing completed the match (the R18 order
  * is by that event first; a multi-GPU gather merges per-rank outputs on it).
  * Sequence numbers count pushed events from 0 across all streams in push order.
+ * tb[i] is INT64_MIN for a match completed by an event; for an absent state's timer match (fired
+ * before event seq[i], or by sdh_engine_advance_time) it is the instance's running max of the times
+ * fired so far: the timer matches of one seq precede its event matches, ordered by (tb, query, key)
+ * and then by emission (the order a multi-GPU merge needs, siddhi_amd/dist.py).
  * Buffers are owned by the engine and valid until the next push/poll/destroy. */
 typedef struct sdh_matches {
   int64_t n;
@@ -118,6 +124,7 @@ typedef struct sdh_matches {
   const int64_t* off;
   const int64_t* words;
   const int64_t* seq;
+  const int64_t* tb;
 } sdh_matches;
 
 typedef struct sdh_stats {
@@ -139,6 +146,8 @@ typedef struct sdh_stats {
   int64_t pool_regrows;      /* K_gen pool / list growths (each re-lays the arenas and re-runs   */
                              /* the push that overflowed; the reference's lists are unbounded)   */
   int64_t last_slab_items;   /* K_slab work items of the last push: key segments x groups         */
+  int64_t placed_pushes;     /* pushes whose matches (all K_ratchet) went straight to their R18   */
+                             /* rows (no sort at poll; matches.hip ratchet_place_kernel)          */
 } sdh_stats;
 
 int sdh_engine_create(const void* ir_blob, size_t len, const sdh_config* cfg, sdh_engine** out);
@@ -170,6 +179,10 @@ const char* sdh_last_error(sdh_engine* e);
 /* Diagnostic, no device needed: generate and compile (hiprtc, gfx950) the shape-compiled kernels of
  * representative K_seq / K_part shapes. Returns the number compiled, or -1 with the compiler log. */
 int sdh_spec_selftest(char* log, size_t cap);
+/* Test diagnostic: out[0] = the K_ratchet records the last push wrote, out[1] = an order-independent
+ * hash of them (e2 seq, query, e1 seq), in either output mode (SDH_FLAG_DEVICE_MATCHES included,
+ * unless its record ring wrapped: SDH_E_CAPACITY). */
+int sdh_engine_debug_digest(sdh_engine* e, uint64_t* out);
 /* Library version / build info string (static storage). */
 const char* sdh_version(void);
 

@@ -466,6 +466,11 @@ struct Match {
   i64 key;
   i64 ts;
   std::vector<std::vector<i64>> slots;
+  // merge metadata (multi-rank tests): the sequence number of the event whose processing produced
+  // the match (timers: the event they fire before, or the next sequence number on an advance), and
+  // for an absent state's timer match the instance's running max of fired times, else INT64_MIN
+  i64 seq = -1;
+  i64 tb = INT64_MIN;
 };
 
 struct Runtime;
@@ -800,7 +805,11 @@ struct Engine {
   std::vector<std::vector<i64>> key_order;          // creation order per partition
   std::vector<Match> matches;
   std::vector<std::pair<Runtime*, StateEvent*>> deferred;  // single-receiver chunk deferral
+  std::vector<i64> deferred_seq;
   std::string err;
+  i64 cur_seq = 0;             // the event being processed (Match::seq)
+  bool in_timer = false;       // a timer is firing (Match::tb = timer_key)
+  i64 timer_key = INT64_MIN;
   size_t gc_threshold = 1 << 20;
   // time (the runtime's TimestampGenerator): the last event's timestamp or an explicit advance;
   // absent processors' schedulers fire at their notification times as it passes them
@@ -834,6 +843,9 @@ struct Engine {
   void advance(i64 t) {
     if (!started) start(t);
     if (has_absent) {
+      // per instance, the running max of the times fired in this call (the device's timer tiebreak,
+      // kgen.h fire_timers)
+      std::map<Runtime*, i64> runmax;
       for (;;) {
         // every scheduler in (query, key) order -- top-level runtimes and each partition's per-key
         // clones (PartitionRuntime.cloneIfNotExist gives every key its own schedulers; clones are
@@ -865,8 +877,13 @@ struct Engine {
         if (!best) break;
         best->pres[bi].timers.pop_front();
         now = bt;
+        i64& rm = runmax.emplace(best, INT64_MIN).first->second;
+        rm = bt > rm ? bt : rm;
+        in_timer = true;
+        timer_key = rm;
         if (best->absentL(bi)) best->absentLogicalTimer(bi, bt, playback ? t : bt);
         else best->absentTimer(bi, bt, playback ? t : bt);
+        in_timer = false;
       }
     }
     if (t > now) now = t;
@@ -880,6 +897,8 @@ struct Engine {
     m.slots.resize(se->slots.size());
     for (size_t k = 0; k < se->slots.size(); ++k)
       for (StreamEvent* e = se->slots[k]; e; e = e->next) m.slots[k].push_back(e->seq);
+    m.seq = cur_seq;
+    m.tb = in_timer ? timer_key : INT64_MIN;
     matches.push_back(std::move(m));
   }
 
@@ -1189,6 +1208,7 @@ void Runtime::absentTimer(int i, i64 currentTime, i64 actualCurrentTime) {
 }
 
 void Runtime::receive(int stream, i64 seq, i64 ts) {
+  eng->cur_seq = seq;
   const RecvDef* rv = nullptr;
   for (auto& r : q->recvs)
     if (r.stream == stream) rv = &r;
@@ -1197,7 +1217,10 @@ void Runtime::receive(int stream, i64 seq, i64 ts) {
     // SingleProcessStreamReceiver.processAndClear:57-80 (selector deferred to chunk end)
     if (q->type == Q_SEQUENCE) { node_reset(0); node_update(0); }   // StateStreamRuntime.resetAndUpdate
     else updateState(rv->procs[0]);                                  // PatternSingle.stabilizeStates
-    for (StateEvent* se : processAndReturn(rv->procs[0], seq, ts)) eng->deferred.push_back({this, se});
+    for (StateEvent* se : processAndReturn(rv->procs[0], seq, ts)) {
+      eng->deferred.push_back({this, se});
+      eng->deferred_seq.push_back(seq);
+    }
   } else {
     // MultiProcessStreamReceiver.receive:268-279 + StateMultiProcessStreamReceiver.processAndClear:53-74
     if (q->type == Q_SEQUENCE) { node_reset(0); node_update(0); }
@@ -1230,8 +1253,12 @@ i64 key_of(const Value& v) {
 }
 
 void deliver_deferred(Engine* e) {
-  for (auto& pr : e->deferred) e->emit(pr.first, pr.second);
+  for (size_t i = 0; i < e->deferred.size(); ++i) {
+    e->cur_seq = e->deferred_seq[i];
+    e->emit(e->deferred[i].first, e->deferred[i].second);
+  }
   e->deferred.clear();
+  e->deferred_seq.clear();
 }
 
 // One junction subscriber (a top-level query, or a partition's PartitionStreamReceiver) receives
@@ -1334,6 +1361,7 @@ int oracle_send(OracleEngine* e, int32_t stream, int64_t n, const int64_t* ts, c
       e->log.push_back(std::move(ev));
       // timers due up to this event fire before it (playback order: TimestampGenerator time
       // change -> Scheduler.sendTimerEvents before the event reaches the junction)
+      e->cur_seq = seqs.back();
       if (!as_chunk || seqs.size() == 1) e->advance(ts[k]);
       if (!as_chunk) {
         send_chunk(e, stream, seqs);
@@ -1347,6 +1375,7 @@ int oracle_send(OracleEngine* e, int32_t stream, int64_t n, const int64_t* ts, c
   } catch (const std::exception& ex) {
     e->err = ex.what();
     e->deferred.clear();
+    e->deferred_seq.clear();
     return -1;
   }
 }
@@ -1378,6 +1407,15 @@ int oracle_get_matches(const OracleEngine* e, int64_t* query, int64_t* key, int6
   return 0;
 }
 
+// per match: the producing event's sequence number and the timer tiebreak (Match::seq, Match::tb)
+int oracle_get_match_meta(const OracleEngine* e, int64_t* seq, int64_t* tb) {
+  for (size_t i = 0; i < e->matches.size(); ++i) {
+    seq[i] = e->matches[i].seq;
+    tb[i] = e->matches[i].tb;
+  }
+  return 0;
+}
+
 void oracle_clear_matches(OracleEngine* e) { e->matches.clear(); }
 
 // the runtime starts at time t (SiddhiAppRuntime.start); without it the first event or advance starts it
@@ -1400,6 +1438,7 @@ int oracle_set_playback(OracleEngine* e, int on) {
 // time passes to t with no event (the scheduler thread of a live runtime; a playback heartbeat)
 int oracle_advance_time(OracleEngine* e, int64_t t) {
   try {
+    e->cur_seq = (i64)e->log.size();
     e->advance(t);
     e->gc();
     return 0;

@@ -36,6 +36,9 @@ int64_t oracle_match_words(const OracleEngine* e);
  * by c event sequence numbers (the slot's event chain at emission time). */
 int oracle_get_matches(const OracleEngine* e, int64_t* query, int64_t* key, int64_t* ts,
                        int64_t* off, int64_t* words);
+/* per match: the sequence number of the event whose processing produced it, and for an absent
+ * state's timer match the instance's running max of fired times (INT64_MIN for event matches) */
+int oracle_get_match_meta(const OracleEngine* e, int64_t* seq, int64_t* tb);
 void oracle_clear_matches(OracleEngine* e);
 /* Absent patterns' time: the runtime starts at t (SiddhiAppRuntime.start; else at the first event
  * or advance), and time passes to t with no event (the schedulers fire what falls due). */

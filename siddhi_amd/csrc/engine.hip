@@ -74,10 +74,31 @@ extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off,
                                      const int32_t* out_rank, int n_streams, sdh::MatchTable T, int64_t row0,
                                      int64_t word0, hipStream_t s);
 extern "C" size_t sdh_poll_temp_bytes(int64_t n);
+extern "C" size_t sdh_place_temp_bytes(int64_t cells);
+extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, const int32_t* blk_count,
+                                        const int32_t* blk_group, int n_blocks, const int32_t* gpos, int n_gpos,
+                                        int64_t n_events, int32_t* cnt, int32_t* flag, void* temp, size_t temp_bytes,
+                                        const sdh::RatchetGroup* groups, const int64_t* ts, int64_t seq_base,
+                                        int64_t row0, int64_t* oq, int64_t* okey, int64_t* ots, int64_t* oseq,
+                                        int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s);
+extern "C" hipError_t sdh_placed_to_table(const int64_t* q, const int64_t* ts, const int64_t* seq, const int64_t* words,
+                                          int64_t n, int64_t seq_ref, const int32_t* out_rank, const int32_t* qinfo,
+                                          int n_streams, sdh::MatchTable T, hipStream_t s);
+extern "C" hipError_t sdh_live_gen(const int32_t* a32, int64_t B32, int64_t blocks, int n_groups, int group_base,
+                                    const int32_t* lane_q, const int32_t* group_seq, const sdh::kg::GQuery* queries,
+                                    unsigned long long* acc, hipStream_t s);
+extern "C" hipError_t sdh_live_seq(const int64_t* tail, int tail_len, int stream, const int32_t* groups, int n_groups,
+                                   const int32_t* lane_q, const int32_t* group_tmpl, const sdh::kg::GQuery* queries,
+                                   unsigned long long* acc, hipStream_t s);
+extern "C" hipError_t sdh_live_part(const int64_t* st, const int32_t* cur, int64_t n_keys, int groups, int64_t blocks,
+                                    int64_t bw, unsigned long long* acc, hipStream_t s);
+extern "C" hipError_t sdh_digest_ratchet(const int64_t* match, int blk_recs, int wide, const int32_t* blk_count,
+                                         const int32_t* blk_group, const sdh::RatchetGroup* groups, int64_t seq_base,
+                                         int n_blocks, unsigned long long* acc, hipStream_t s);
 extern "C" hipError_t sdh_poll_sort(sdh::MatchTable T, int64_t n, int n_lo, int lo_bits, int hi_bits, uint64_t* kbuf,
                                     int32_t* pbuf, void* temp, size_t temp_bytes, int64_t* oq, int64_t* okey,
-                                    int64_t* ots, int64_t* oseq, int64_t* olen, int64_t* ooff, int32_t** perm_out,
-                                    int64_t* total_words, hipStream_t s);
+                                    int64_t* ots, int64_t* oseq, int64_t* otb, int64_t* olen, int64_t* ooff,
+                                    int32_t** perm_out, int64_t* total_words, hipStream_t s);
 extern "C" hipError_t sdh_poll_words(sdh::MatchTable T, const int32_t* perm, int64_t n, const int64_t* ooff,
                                      int64_t* owords, hipStream_t s);
 
@@ -603,6 +624,7 @@ struct sdh_engine {
     DevBuf<int64_t> seq, q, key, ts, woff, wlen, words;
     int64_t n = 0, nw = 0;           // rows / words used
     int n_lo = 0;                    // tiebreak passes the rows need
+    bool placed = false;             // the rows are K_ratchet matches already in R18 order in po_*
   } mt;
   int64_t seq_ref = 0;               // global seq at the last poll (<= every trigger seq in mt)
   DevBuf<int32_t> d_out_rank;        // [query][stream] R18 receiver rank
@@ -611,8 +633,8 @@ struct sdh_engine {
   DevBuf<uint64_t> p_keys;
   DevBuf<int32_t> p_perm;
   DevBuf<uint8_t> p_temp;
-  DevBuf<int64_t> po_q, po_key, po_ts, po_seq, po_len, po_off, po_words;
-  HostBuf<int64_t> ho_q, ho_key, ho_ts, ho_seq, ho_off, ho_words;
+  DevBuf<int64_t> po_q, po_key, po_ts, po_seq, po_tb, po_len, po_off, po_words;
+  HostBuf<int64_t> ho_q, ho_key, ho_ts, ho_seq, ho_tb, ho_off, ho_words;
   // ---- K_gen (general interpreter) ----
   kg::LProgram lp;                   // full IR (receivers, runtime tree, partitions)
   std::vector<int> out_rank;         // R18 rank per (query, stream)
@@ -738,6 +760,15 @@ struct sdh_engine {
   int64_t r_blocks = 0;              // capacity in blocks
   int r_blk_recs = 8192;
   int r_blocks_used = 0;             // of the last launch
+  int64_t r_blk_taken = 0;           // blocks the last launch took (ring mode: may exceed r_blocks)
+  // direct R18 placement (matches.hip ratchet_place_kernel): per group its position among its
+  // stream's groups in receiver-rank order; per stream the group count, or -1 when some group's lanes
+  // are not consecutive ranks
+  std::vector<int32_t> r_gpos;
+  std::vector<int> r_place_n;
+  DevBuf<int32_t> d_rgpos, p_cnt, p_flag;
+  DevBuf<uint8_t> p_ptemp;
+  int64_t r_seq_base = 0;            // seq of the last launch's first event
   std::vector<int32_t> r_blk_count;
   int rML = 8;                       // LDS ring entries per lane (power of two)
   double r_waves = 0;                // resident-wave target per launch (0: CUs x occupancy)
@@ -877,7 +908,89 @@ void table_clear(sdh_engine* e) {
   e->mt.n = 0;
   e->mt.nw = 0;
   e->mt.n_lo = 0;
+  e->mt.placed = false;
   e->seq_ref = e->seq;
+}
+
+// Direct R18 placement plan: a stream's K_ratchet matches can be placed without a sort when every
+// group's lanes are consecutive receiver ranks (queries of one shape defined in a row)
+void ratchet_place_plan(sdh_engine* e) {
+  const int ns = (int)e->prog.stream_types.size();
+  e->r_gpos.assign(e->rg.size(), -1);
+  e->r_place_n.assign(ns, 0);
+  for (int s = 0; s < ns; ++s) {
+    std::vector<std::pair<int, int>> gr;  // (first rank, group)
+    bool ok = true;
+    for (int g = 0; g < (int)e->rg.size(); ++g) {
+      const RatchetGroup& G = e->rg[g];
+      if (G.stream != s) continue;
+      const int r0 = e->out_rank[(size_t)G.qid[0] * ns + s];
+      for (int l = 1; l < G.n_lanes; ++l) ok &= e->out_rank[(size_t)G.qid[l] * ns + s] == r0 + l;
+      gr.push_back({r0, g});
+    }
+    std::sort(gr.begin(), gr.end());
+    for (size_t i = 0; i < gr.size(); ++i) e->r_gpos[gr[i].second] = (int32_t)i;
+    e->r_place_n[s] = ok ? (int)gr.size() : -1;
+  }
+  if (!e->r_gpos.empty()) {
+    e->d_rgpos.ensure(e->r_gpos.size());
+    HIPCHK(hipMemcpy(e->d_rgpos.p, e->r_gpos.data(), e->r_gpos.size() * 4, hipMemcpyHostToDevice));
+  }
+}
+
+// The last push's K_ratchet matches written straight to their R18 rows of the ABI outputs, after
+// the window's rows (matches.hip ratchet_place_kernel). False, with nothing written, when the push
+// does not qualify or a run split over two blocks: the caller appends to the table instead.
+bool place_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base, int64_t n_events, int stream) {
+  const int ng = e->r_place_n[stream];
+  const int64_t rows = e->r_matches, n0 = e->mt.n;
+  if (ng <= 0 || e->r_wide || e->r_blk_recs > 8192 || (double)n_events * ng > (double)(1 << 28) ||
+      n0 + rows >= INT32_MAX || getenv("SDH_NO_PLACE"))
+    return false;
+  const size_t keep = (size_t)n0, want = (size_t)(n0 + rows);
+  e->po_q.grow_keep(want, keep, e->stream);
+  e->po_key.grow_keep(want, keep, e->stream);
+  e->po_ts.grow_keep(want, keep, e->stream);
+  e->po_seq.grow_keep(want, keep, e->stream);
+  e->po_tb.grow_keep(want, keep, e->stream);
+  e->po_off.grow_keep(want + 1, keep, e->stream);
+  e->po_words.grow_keep(4 * want, 4 * keep, e->stream);
+  const int64_t cells = n_events * ng;
+  e->p_cnt.ensure((size_t)cells);
+  e->p_flag.ensure(1);
+  const size_t tb = sdh_place_temp_bytes(cells);
+  e->p_ptemp.ensure(tb);
+  const hipError_t r = sdh_place_ratchet(e->d_rmatch.p, e->r_blk_recs, e->d_blk_count.p, e->d_blk_group.p,
+                                         e->r_blocks_used, e->d_rgpos.p, ng, n_events, e->p_cnt.p, e->p_flag.p,
+                                         e->p_ptemp.p, e->p_ptemp.n, e->d_rg.p, ts_col, seq_base, n0, e->po_q.p,
+                                         e->po_key.p, e->po_ts.p, e->po_seq.p, e->po_tb.p, e->po_off.p, e->po_words.p,
+                                         e->stream);
+  if (r == hipErrorNotSupported) {
+    (void)hipGetLastError();
+    return false;
+  }
+  HIPCHK(r);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  e->mt.n += rows;
+  e->mt.placed = true;
+  ++e->stats.placed_pushes;
+  return true;
+}
+
+// placed rows -> general table rows (a later push of the window has other producers)
+void placed_to_table(sdh_engine* e) {
+  if (!e->mt.placed) return;
+  const int64_t n = e->mt.n;
+  e->mt.n = 0;
+  e->mt.nw = 0;
+  table_reserve(e, n, 4 * n);
+  HIPCHK(sdh_placed_to_table(e->po_q.p, e->po_ts.p, e->po_seq.p, e->po_words.p, n, e->seq_ref, e->d_out_rank.p,
+                             e->d_qinfo.p, (int)e->prog.stream_types.size(), table_view(e), e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  e->mt.n = n;
+  e->mt.nw = 4 * n;
+  e->mt.n_lo = std::max(e->mt.n_lo, 1);
+  e->mt.placed = false;
 }
 
 int bits_of(uint64_t v) {
@@ -900,6 +1013,7 @@ int64_t table_sort(sdh_engine* e, int64_t* total_words) {
   e->po_key.ensure(n);
   e->po_ts.ensure(n);
   e->po_seq.ensure(n);
+  e->po_tb.ensure(n);
   e->po_len.ensure(n + 1);
   e->po_off.ensure(n + 1);
   // timer records' tiebreaks are a full timestamp, the query and the partition key
@@ -907,8 +1021,8 @@ int64_t table_sort(sdh_engine* e, int64_t* total_words) {
   const int hi_bits = bits_of((uint64_t)(e->seq - e->seq_ref)) + RANK_BITS;
   int32_t* perm = nullptr;
   HIPCHK(sdh_poll_sort(table_view(e), n, e->mt.n_lo, lo_bits, hi_bits, e->p_keys.p, e->p_perm.p, e->p_temp.p,
-                       e->p_temp.n, e->po_q.p, e->po_key.p, e->po_ts.p, e->po_seq.p, e->po_len.p, e->po_off.p, &perm,
-                       total_words, e->stream));
+                       e->p_temp.n, e->po_q.p, e->po_key.p, e->po_ts.p, e->po_seq.p, e->po_tb.p, e->po_len.p,
+                       e->po_off.p, &perm, total_words, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   e->po_words.ensure((size_t)std::max<int64_t>(*total_words, 1));
   HIPCHK(sdh_poll_words(table_view(e), perm, n, e->po_off.p, e->po_words.p, e->stream));
@@ -1280,6 +1394,10 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     HIPCHK(hipStreamSynchronize(e->stream));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    if (getenv("SDH_TRACE"))
+      fprintf(stderr, "[sdh] ratchet stream %d n %lld attempt %d full %d items %d blocks %d/%lld errs %d %d %d %d: %.2f ms\n",
+              stream, (long long)n, attempt, (int)full, n_items, used, (long long)e->r_blocks, errs[0], errs[1], errs[2],
+              errs[3], ms);
     if (errs[3]) throw Error(SDH_E_CAPACITY, "a pending partial is more than 2^31 events old");
     if (errs[1] && !full) {  // timestamps out of order: exact re-run with the full expiry scan
       e->r_full_expiry[stream] = 1;
@@ -1299,6 +1417,8 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       continue;
     }
     for (int g : gs) e->rcur[g] ^= 1;
+    e->r_blk_taken = used;
+    e->r_seq_base = B.seq_base;
     if (ring) {  // counted, not collected
       unsigned long long tot = 0;
       HIPCHK(hipMemcpy(&tot, e->d_rtotal.p, 8, hipMemcpyDeviceToHost));
@@ -2707,6 +2827,7 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   e->work.clear();
   e->device_matches = 0;
   e->r_blocks_used = 0;
+  e->r_blk_taken = 0;
   e->r_matches = 0;
   e->g_dev_matches = 0;
   e->g_used = 0;
@@ -2760,11 +2881,18 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   e->prev_ts[stream] = t01[1];
   e->seq += b->n;
   e->stats.events += b->n;
-  // the push is committed; its matches join the device table (R18-sorted at poll)
+  // the push is committed; its matches join the device table (R18-sorted at poll), or, when they
+  // all come from K_ratchet, go straight to their R18 rows (no sort at poll)
   if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES)) {
-    append_chain(e);
-    append_ratchet(e, B.ts, B.seq_base);
-    append_gen(e);
+    const bool only_ratchet = e->device_matches == 0 && e->g_dev_matches == 0;
+    const bool placeable = only_ratchet && (e->mt.n == 0 || e->mt.placed);
+    if (!(only_ratchet && e->r_matches == 0) &&
+        !(placeable && place_ratchet(e, B.ts, B.seq_base, b->n, stream))) {
+      placed_to_table(e);
+      append_chain(e);
+      append_ratchet(e, B.ts, B.seq_base);
+      append_gen(e);
+    }
   }
   if (e->g_out_lost)
     throw Error(SDH_E_CAPACITY, "K_gen match output overflow: the push was applied but its K_gen matches were "
@@ -2795,12 +2923,21 @@ void check_usable(sdh_engine* e) {
 int do_poll(sdh_engine* e, sdh_matches* out, bool host) {
   check_usable(e);
   int64_t tw = 0;
-  const int64_t n = table_sort(e, &tw);
+  int64_t n = 0;
+  if (e->mt.placed) {  // already in R18 order (place_ratchet): 4 words per match
+    n = e->mt.n;
+    tw = 4 * n;
+    HIPCHK(hipMemcpyAsync(e->po_off.p + n, &tw, 8, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  } else {
+    n = table_sort(e, &tw);
+  }
   if (host) {
     e->ho_q.ensure(std::max<int64_t>(n, 1));
     e->ho_key.ensure(std::max<int64_t>(n, 1));
     e->ho_ts.ensure(std::max<int64_t>(n, 1));
     e->ho_seq.ensure(std::max<int64_t>(n, 1));
+    e->ho_tb.ensure(std::max<int64_t>(n, 1));
     e->ho_off.ensure(n + 1);
     e->ho_words.ensure(std::max<int64_t>(tw, 1));
     e->ho_off.p[0] = 0;
@@ -2809,6 +2946,7 @@ int do_poll(sdh_engine* e, sdh_matches* out, bool host) {
       HIPCHK(hipMemcpyAsync(e->ho_key.p, e->po_key.p, n * 8, hipMemcpyDeviceToHost, e->stream));
       HIPCHK(hipMemcpyAsync(e->ho_ts.p, e->po_ts.p, n * 8, hipMemcpyDeviceToHost, e->stream));
       HIPCHK(hipMemcpyAsync(e->ho_seq.p, e->po_seq.p, n * 8, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipMemcpyAsync(e->ho_tb.p, e->po_tb.p, n * 8, hipMemcpyDeviceToHost, e->stream));
       HIPCHK(hipMemcpyAsync(e->ho_off.p, e->po_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, e->stream));
       if (tw) HIPCHK(hipMemcpyAsync(e->ho_words.p, e->po_words.p, tw * 8, hipMemcpyDeviceToHost, e->stream));
       HIPCHK(hipStreamSynchronize(e->stream));
@@ -2817,6 +2955,7 @@ int do_poll(sdh_engine* e, sdh_matches* out, bool host) {
     out->key = e->ho_key.p;
     out->ts = e->ho_ts.p;
     out->seq = e->ho_seq.p;
+    out->tb = e->ho_tb.p;
     out->off = e->ho_off.p;
     out->words = e->ho_words.p;
   } else {
@@ -2829,6 +2968,7 @@ int do_poll(sdh_engine* e, sdh_matches* out, bool host) {
     out->key = e->po_key.p;
     out->ts = e->po_ts.p;
     out->seq = e->po_seq.p;
+    out->tb = e->po_tb.p;
     out->off = e->po_off.p;
     out->words = e->po_words.p;
   }
@@ -2915,6 +3055,7 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     ensure_state(e);
     ratchet_build(e, rplans);
     gen_build(e, gen_qs);
+    ratchet_place_plan(e);
     // R18 tables of the device match table: receiver rank per (query, stream), and per query its
     // state count and the stream of its last state (the trigger of a chain-plan match)
     const size_t nq_all = e->prog.q.size();
@@ -3008,7 +3149,10 @@ int sdh_engine_advance_time(sdh_engine* e, int64_t t) {
       throw;
     }
     e->advance_to = INT64_MIN;
-    if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES)) append_gen(e);
+    if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) && e->g_dev_matches) {
+      placed_to_table(e);
+      append_gen(e);
+    }
     if (e->g_out_lost)
       throw Error(SDH_E_CAPACITY, "K_gen match output overflow: the advance was applied but its matches were lost");
     return SDH_OK;
@@ -3031,6 +3175,73 @@ int sdh_engine_poll_device(sdh_engine* e, sdh_matches* out) {
   return guard(e, [&]() { return do_poll(e, out, false); });
 }
 
+// keys a partition has seen so far (its routing table's dense ids)
+int64_t route_keys(sdh_engine* e, int partition) {
+  if (partition < 0 || partition >= (int)e->routes.size() || !e->routes[partition]) return 0;
+  int32_t nk = 0;
+  d2h_sync(e, &nk, e->routes[partition]->n_keys.p, 4);
+  return nk;
+}
+
+// Live partials of K_gen arenas, K_part tables and K_seq windows: entries of the pending lists of
+// non-start states (oracle_live_partials counts every pending list, the start state's seed included)
+int64_t device_live_partials(sdh_engine* e) {
+  DevBuf<unsigned long long> acc;
+  acc.ensure(1);
+  HIPCHK(hipMemsetAsync(acc.p, 0, 8, e->stream));
+  DevBuf<int32_t> d_gseq;
+  if (!e->group_seq.empty()) {
+    d_gseq.ensure(e->group_seq.size());
+    HIPCHK(hipMemcpy(d_gseq.p, e->group_seq.data(), e->group_seq.size() * 4, hipMemcpyHostToDevice));
+  }
+  for (auto& up : e->gsets) {
+    auto& gs = *up;
+    if (!gs.a32.p || gs.n_groups == 0) continue;
+    const int64_t blocks = gs.partition < 0 ? gs.n_groups : std::min(gs.key_cap, route_keys(e, gs.partition)) * gs.n_groups;
+    HIPCHK(sdh_live_gen(gs.a32.p, e->gB32, blocks, gs.n_groups, gs.group_base, e->d_lane_q.p, d_gseq.p, e->d_gq.p, acc.p,
+                        e->stream));
+  }
+  for (auto& up : e->psets) {
+    auto& ps = *up;
+    if (!ps.st.p || ps.key_cap == 0) continue;
+    const int64_t nk = std::min(ps.key_cap, route_keys(e, ps.partition));
+    HIPCHK(sdh_live_part(ps.st.p, ps.cur.p, nk, ps.n_groups, ps.key_cap * ps.n_groups, ps.bw(), acc.p, e->stream));
+  }
+  for (int s = 0; s < (int)e->seq_tail.size(); ++s) {
+    std::vector<int32_t> gl;
+    for (int g = 0; g < (int)e->group_seq.size(); ++g)
+      if (e->group_seq[g] > 0 && e->gq[e->group_tmpl[g]].st[0].stream == s) gl.push_back(g);
+    if (gl.empty() || e->seq_tail_len[s] <= 0) continue;
+    DevBuf<int32_t> d_gl;
+    d_gl.ensure(gl.size());
+    HIPCHK(hipMemcpy(d_gl.p, gl.data(), gl.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(sdh_live_seq(e->seq_tail[s].p, e->seq_tail_len[s], s, d_gl.p, (int)gl.size(), e->d_lane_q.p,
+                        e->d_group_tmpl.p, e->d_gq.p, acc.p, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));  // (d_gl is freed at scope end)
+  }
+  unsigned long long v = 0;
+  d2h_sync(e, &v, acc.p, 8);
+  return (int64_t)v;
+}
+
+// Test diagnostic: (records, order-independent hash) of the last push's K_ratchet records as the
+// kernel wrote them, in either output mode (matches.hip digest_ratchet_kernel)
+int sdh_engine_debug_digest(sdh_engine* e, uint64_t* out) {
+  if (!e || !out) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    out[0] = out[1] = 0;
+    if (e->r_blk_taken > e->r_blocks)
+      throw Error(SDH_E_CAPACITY, "the last push's device-match records wrapped their ring");
+    DevBuf<unsigned long long> acc;
+    acc.ensure(2);
+    HIPCHK(hipMemsetAsync(acc.p, 0, 16, e->stream));
+    HIPCHK(sdh_digest_ratchet(e->d_rmatch.p, e->r_blk_recs, e->r_wide, e->d_blk_count.p, e->d_blk_group.p, e->d_rg.p,
+                              e->r_seq_base, (int)e->r_blk_taken, acc.p, e->stream));
+    d2h_sync(e, out, acc.p, 16);
+    return SDH_OK;
+  });
+}
+
 int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
   if (!e || !out) return SDH_E_INVALID;
   return guard(e, [&]() {
@@ -3051,6 +3262,7 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
           for (int l = 0; l < e->rg[g].n_lanes; ++l) live += rs[g].n[l];
     }
     for (auto& ss : e->ssets) live += slab_live_partials(e, *ss);
+    live += device_live_partials(e);
     e->stats.live_partials = live;
     e->stats.pool_regrows = e->gen_regrows;
     e->stats.last_slab_items = e->slab_items;

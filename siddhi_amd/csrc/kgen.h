@@ -1513,9 +1513,10 @@ KG_FN bool atoms_pass(const GQuery* q, const GQuery* ql, int i, const Win& w) {
   return true;
 }
 
+// (n_st >= 0: only states 0 .. n_st-1, i.e. a partial waiting at state n_st -- live-partial counts)
 template <class Win>
-KG_FN bool seq_match(const GQuery* q, const GQuery* ql, int64_t within, const Win& w) {
-  const int S = q->n_states;
+KG_FN bool seq_match(const GQuery* q, const GQuery* ql, int64_t within, const Win& w, int n_st = -1) {
+  const int S = n_st < 0 ? q->n_states : n_st;
   for (int i = 0; i < S; ++i) {
     if (i >= 1 && within >= 0) {  // StreamPreStateProcessor.isExpired:102-113 before the filter
       const int64_t d = (int64_t)((uint64_t)w.ts(0) - (uint64_t)w.ts(i));

@@ -65,6 +65,149 @@ __global__ __launch_bounds__(256) void append_ratchet_kernel(
   }
 }
 
+// Order-independent digest of the K_ratchet records of the last launch (both output modes write the
+// same per-wave blocks; SDH_FLAG_DEVICE_MATCHES lets the block index wrap): per record
+// mix64(e2 seq, query, e1 seq) summed mod 2^64, and the record count. Test diagnostics
+// (sdh_engine_debug_digest): normal and device-match modes must write the same records.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void digest_ratchet_kernel(const int64_t* __restrict__ match, int blk_recs, int wide,
+                                                             const int32_t* __restrict__ blk_count,
+                                                             const int32_t* __restrict__ blk_group,
+                                                             const RatchetGroup* __restrict__ groups, int64_t seq_base,
+                                                             unsigned long long* acc) {
+  const int b = blockIdx.x;
+  const int n = blk_count[b];
+  const RatchetGroup* G = groups + blk_group[b];
+  const uint2* R = reinterpret_cast<const uint2*>(match) + ((size_t)b * blk_recs << (wide ? 1 : 0));
+  unsigned long long h = 0, c = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t off, ln, q1;
+    if (!wide) {
+      const uint2 r = R[i];
+      off = r.x & ((1u << 26) - 1);
+      ln = r.x >> 26;
+      q1 = r.y;
+    } else {
+      const uint4 r = reinterpret_cast<const uint4*>(R)[i];
+      off = r.x;
+      ln = r.y & 63;
+      q1 = r.z;
+    }
+    const int64_t s = seq_base + (int64_t)off;
+    const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
+    h += mix64(mix64((uint64_t)s * 0x9E3779B97F4A7C15ull ^ (uint64_t)G->qid[ln]) ^ (uint64_t)s1);
+    ++c;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    h += __shfl_down(h, o);
+    c += __shfl_down(c, o);
+  }
+  if ((threadIdx.x & 63) == 0 && c) {
+    atomicAdd(&acc[0], c);
+    atomicAdd(&acc[1], h);
+  }
+}
+
+// ---- K_ratchet direct R18 placement (a push whose matches all come from K_ratchet) ----
+// A block holds one wave's records (one group of 64 queries, lane = query) in emission order: events
+// ascending; for one event -- its run, kept in one block by the kernel's level-0 reserve -- by pop
+// level, each level's lanes ascending (ballot compaction), level 0 the newest partial. R18 wants per
+// event the queries in receiver-rank order and per query its partials in pending-list order (e1 seq
+// ascending = pop level descending). When a group's lanes are consecutive receiver ranks, record i
+// of a run goes to
+//   base[event][group position] + #{k in run: lane_k < lane_i} + #{k in run, k > i: lane_k == lane_i}
+// where base is the exclusive scan of the run lengths over (event, groups in rank order). Pass 1
+// stores the run lengths (a run key seen twice = a run split over blocks: the caller falls back to
+// the sort); pass 2 writes the ABI tuples in place: no sort, one read of the records, one write of
+// the outputs.
+constexpr int PLACE_RECS = 8192;  // block records a workgroup stages in LDS (the host checks blk_recs)
+
+template <bool PLACE>
+__global__ __launch_bounds__(256) void ratchet_place_kernel(
+    const int64_t* __restrict__ match, int blk_recs, const int32_t* __restrict__ blk_count,
+    const int32_t* __restrict__ blk_group, const int32_t* __restrict__ gpos, int n_gpos, int32_t* __restrict__ cnt,
+    int32_t* __restrict__ split, const RatchetGroup* __restrict__ groups, const int64_t* __restrict__ ts,
+    int64_t seq_base, int64_t row0, int64_t* __restrict__ oq, int64_t* __restrict__ okey, int64_t* __restrict__ ots,
+    int64_t* __restrict__ oseq, int64_t* __restrict__ otb, int64_t* __restrict__ ooff, int64_t* __restrict__ owords) {
+  __shared__ uint32_t rx[PLACE_RECS];
+  const int b = blockIdx.x;
+  const int n = blk_count[b];
+  const int g = blk_group[b];
+  const int gp = gpos[g];
+  const uint2* R = reinterpret_cast<const uint2*>(match) + (size_t)b * blk_recs;
+  constexpr uint32_t OFF = (1u << 26) - 1;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) rx[i] = R[i].x;
+  __syncthreads();
+  const RatchetGroup* G = groups + g;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t x = rx[i], off = x & OFF, lane = x >> 26;
+    int lo = 0, hi = i;  // run start: first record of this event (records ascend by event)
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if ((rx[m] & OFF) < off) lo = m + 1;
+      else hi = m;
+    }
+    const int a = lo;
+    hi = n;
+    lo = i + 1;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if ((rx[m] & OFF) <= off) lo = m + 1;
+      else hi = m;
+    }
+    const int z = lo;  // one past the run
+    const int64_t cell = (int64_t)off * n_gpos + gp;
+    if constexpr (!PLACE) {
+      if (i == a && atomicAdd(&cnt[cell], z - a) != 0) atomicOr(split, 1);
+    } else {
+      int p = 0;
+      for (int k = a; k < z; ++k) {
+        const uint32_t lk = rx[k] >> 26;
+        p += (lk < lane || (k > i && lk == lane)) ? 1 : 0;
+      }
+      const int64_t P = row0 + (int64_t)cnt[cell] + p;
+      const uint32_t q1 = R[i].y;
+      const int64_t s = seq_base + (int64_t)off;
+      const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
+      oq[P] = G->qid[lane];
+      okey[P] = -1;
+      ots[P] = ts[off];
+      oseq[P] = s;
+      otb[P] = INT64_MIN;
+      ooff[P] = 4 * P;
+      reinterpret_cast<longlong2*>(owords + 4 * P)[0] = make_longlong2(1, s1);
+      reinterpret_cast<longlong2*>(owords + 4 * P)[1] = make_longlong2(1, s);
+    }
+  }
+}
+
+// placed rows [0, n) -> general table rows (a later push in the same poll window has other producers)
+__global__ __launch_bounds__(256) void placed_to_table_kernel(const int64_t* __restrict__ q, const int64_t* __restrict__ ts,
+                                                              const int64_t* __restrict__ seq,
+                                                              const int64_t* __restrict__ words, int64_t n,
+                                                              int64_t seq_ref, const int32_t* __restrict__ out_rank,
+                                                              const int32_t* __restrict__ qinfo, int n_streams,
+                                                              MatchTable T) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int qq = (int)q[i];
+  T.hi[i] = hi_key(seq[i], seq_ref, out_rank[(int64_t)qq * n_streams + qinfo[2 * qq + 1]]);
+  T.lo[0][i] = (uint64_t)words[4 * i + 1];
+#pragma unroll
+  for (int k = 1; k < MAXLO; ++k) T.lo[k][i] = 0ull;
+  T.seq[i] = seq[i];
+  T.q[i] = qq;
+  T.key[i] = -1;
+  T.ts[i] = ts[i];
+  T.woff[i] = 4 * i;
+  T.wlen[i] = 4;
+  for (int k = 0; k < 4; ++k) T.words[4 * i + k] = words[4 * i + k];
+}
+
 // K_chain segments (records {qid, ts, seq_0 .. seq_{S-1}} of rec_words) -> table rows
 __global__ __launch_bounds__(256) void append_chain_kernel(
     const int64_t* __restrict__ src, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ seg_count,
@@ -143,7 +286,7 @@ __global__ void gather_key_kernel(const uint64_t* __restrict__ key, const int32_
 // sorted row i <- table row perm[i]; len[n] = 0 so that an exclusive scan of n+1 gives off[n]
 __global__ void gather_rows_kernel(MatchTable T, const int32_t* __restrict__ perm, int64_t n, int64_t* __restrict__ oq,
                                    int64_t* __restrict__ okey, int64_t* __restrict__ ots, int64_t* __restrict__ oseq,
-                                   int64_t* __restrict__ olen) {
+                                   int64_t* __restrict__ otb, int64_t* __restrict__ olen) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i > n) return;
   if (i == n) {
@@ -155,6 +298,9 @@ __global__ void gather_rows_kernel(MatchTable T, const int32_t* __restrict__ per
   okey[i] = T.key[p];
   ots[i] = T.ts[p];
   oseq[i] = T.seq[p];
+  // timer rows rank 0 (append_gen_kernel) and carry their tiebreak time in lo[2]
+  const bool timer = (T.hi[p] & ((1ull << RANK_BITS) - 1)) == 0;
+  otb[i] = timer ? (int64_t)(T.lo[2][p] ^ 0x8000000000000000ull) : INT64_MIN;
   olen[i] = T.wlen[p];
 }
 
@@ -207,6 +353,62 @@ extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off,
   return hipGetLastError();
 }
 
+extern "C" hipError_t sdh_digest_ratchet(const int64_t* match, int blk_recs, int wide, const int32_t* blk_count,
+                                         const int32_t* blk_group, const sdh::RatchetGroup* groups, int64_t seq_base,
+                                         int n_blocks, unsigned long long* acc, hipStream_t s) {
+  if (n_blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::digest_ratchet_kernel, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, wide, blk_count,
+                     blk_group, groups, seq_base, acc);
+  return hipGetLastError();
+}
+
+// Direct R18 placement of the last push's K_ratchet blocks at rows row0.. of the ABI outputs (see
+// ratchet_place_kernel). cnt: n_events * n_gpos int32 (zeroed here; scanned in place). Returns
+// hipErrorNotSupported, with nothing written, when a run split over two blocks (use the sort).
+extern "C" size_t sdh_place_temp_bytes(int64_t cells) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum((void*)nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, (int)cells);
+  return b + 256;
+}
+extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, const int32_t* blk_count,
+                                        const int32_t* blk_group, int n_blocks, const int32_t* gpos, int n_gpos,
+                                        int64_t n_events, int32_t* cnt, int32_t* flag, void* temp, size_t temp_bytes,
+                                        const sdh::RatchetGroup* groups, const int64_t* ts, int64_t seq_base,
+                                        int64_t row0, int64_t* oq, int64_t* okey, int64_t* ots, int64_t* oseq,
+                                        int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s) {
+  using namespace sdh;
+  if (n_blocks <= 0) return hipSuccess;
+  if (blk_recs > PLACE_RECS) return hipErrorNotSupported;
+  const int64_t cells = n_events * n_gpos;
+  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)cells * 4, s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(flag, 0, 4, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ratchet_place_kernel<false>, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, blk_count, blk_group,
+                     gpos, n_gpos, cnt, flag, groups, ts, seq_base, row0, oq, okey, ots, oseq, otb, ooff, owords);
+  int32_t split = 0;
+  e = hipMemcpyAsync(&split, flag, 4, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  if (split) return hipErrorNotSupported;
+  size_t tb = temp_bytes;
+  e = hipcub::DeviceScan::ExclusiveSum(temp, tb, cnt, cnt, (int)cells, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ratchet_place_kernel<true>, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, blk_count, blk_group,
+                     gpos, n_gpos, cnt, flag, groups, ts, seq_base, row0, oq, okey, ots, oseq, otb, ooff, owords);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sdh_placed_to_table(const int64_t* q, const int64_t* ts, const int64_t* seq, const int64_t* words,
+                                          int64_t n, int64_t seq_ref, const int32_t* out_rank, const int32_t* qinfo,
+                                          int n_streams, MatchTable T, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::placed_to_table_kernel, dim3(sdh::grid(n, 256)), dim3(256), 0, s, q, ts, seq, words, n,
+                     seq_ref, out_rank, qinfo, n_streams, T);
+  return hipGetLastError();
+}
+
 // Scratch the poll needs for n rows (bytes): hipcub temp storage.
 extern "C" size_t sdh_poll_temp_bytes(int64_t n) {
   size_t a = 0, b = 0;
@@ -222,8 +424,8 @@ extern "C" size_t sdh_poll_temp_bytes(int64_t n) {
 // sorted permutation (inside pbuf) and *total_words (host) receives off[n] once the stream has run.
 extern "C" hipError_t sdh_poll_sort(MatchTable T, int64_t n, int n_lo, int lo_bits, int hi_bits, uint64_t* kbuf,
                                     int32_t* pbuf, void* temp, size_t temp_bytes, int64_t* oq, int64_t* okey,
-                                    int64_t* ots, int64_t* oseq, int64_t* olen, int64_t* ooff, int32_t** perm_out,
-                                    int64_t* total_words, hipStream_t s) {
+                                    int64_t* ots, int64_t* oseq, int64_t* otb, int64_t* olen, int64_t* ooff,
+                                    int32_t** perm_out, int64_t* total_words, hipStream_t s) {
   using namespace sdh;
   *total_words = 0;
   *perm_out = pbuf;
@@ -251,7 +453,8 @@ extern "C" hipError_t sdh_poll_sort(MatchTable T, int64_t n, int n_lo, int lo_bi
   hipError_t e = pass(T.hi, hi_bits);
   if (e != hipSuccess) return e;
   *perm_out = perm;
-  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid(n + 1, 256)), dim3(256), 0, s, T, perm, n, oq, okey, ots, oseq, olen);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid(n + 1, 256)), dim3(256), 0, s, T, perm, n, oq, okey, ots, oseq, otb,
+                     olen);
   size_t tb = temp_bytes;
   e = hipcub::DeviceScan::ExclusiveSum(temp, tb, olen, ooff, (int)(n + 1), s);
   if (e != hipSuccess) return e;

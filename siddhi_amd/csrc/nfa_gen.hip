@@ -216,6 +216,61 @@ __global__ void seq_tail_kernel(StreamBatch b, int64_t* tail, int32_t tail_len, 
   }
 }
 
+// ---- live partials (sdh_engine_stats): entries of the pending lists of non-start states ----
+__device__ __forceinline__ void acc_wave(unsigned long long v, unsigned long long* acc) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(acc, v);
+}
+
+// K_gen arenas: one thread per (block, lane); blocks [key][group] or [group]; K_seq groups skipped
+__global__ void gen_live_kernel(const int32_t* __restrict__ a32, int64_t B32, int64_t blocks, int n_groups, int group_base,
+                                const int32_t* __restrict__ lane_q, const int32_t* __restrict__ group_seq,
+                                const kg::GQuery* __restrict__ queries, unsigned long long* acc) {
+  const int64_t block = blockIdx.x;
+  const int lane = threadIdx.x;
+  unsigned long long v = 0;
+  const int g = (int)(block % n_groups);
+  const int qi = block < blocks ? lane_q[(int64_t)(group_base + g) * 64 + lane] : -1;
+  if (qi >= 0 && group_seq[group_base + g] == 0) {
+    const kg::GQuery& q = queries[qi];
+    const int32_t* w = a32 + block * B32 * 64 + lane;
+    if (w[(int64_t)q.lay.o_init * 64] != 0)
+      for (int s = 0; s < q.n_states; ++s)
+        if (!q.st[s].is_start) v += (unsigned long long)w[(int64_t)(q.lay.o_pn + s) * 64];
+  }
+  acc_wave(v, acc);
+}
+
+// K_seq: a sequence partial waits at state j (1 <= j < S) iff states 0 .. j-1 passed (with their
+// `within` checks) over the stream's last j events (seq_body.h: the window argument); one wave per
+// group of the stream, lane = query, over the carried tail
+struct TailWin {
+  static constexpr bool kStagedConsts = false;
+  const int64_t* base;  // row of window event 0
+  const int32_t* cap;   // the stream's captured attribute per capture index
+  __device__ int64_t lane_const(int) const { return 0; }
+  __device__ int64_t ts(int p) const { return base[p * SEQ_TW]; }
+  __device__ int64_t raw(int p, int j, bool = false) const { return base[p * SEQ_TW + 2 + cap[j]]; }
+  __device__ bool null(int p, int j, bool = false) const { return base[p * SEQ_TW + 2 + MAXATTR + cap[j]] != 0; }
+};
+__global__ void seq_live_kernel(const int64_t* __restrict__ tail, int tail_len, int stream,
+                                const int32_t* __restrict__ groups, const int32_t* __restrict__ lane_q,
+                                const int32_t* __restrict__ group_tmpl, const kg::GQuery* __restrict__ queries,
+                                unsigned long long* acc) {
+  const int g = groups[blockIdx.x];
+  const int lane = threadIdx.x;
+  const int qi = lane_q[(int64_t)g * 64 + lane];
+  unsigned long long v = 0;
+  if (qi >= 0) {
+    const kg::GQuery* q = queries + group_tmpl[g];
+    const kg::GQuery* ql = queries + qi;
+    for (int j = 1; j < q->n_states && j <= tail_len; ++j)
+      if (kg::seq_match(q, ql, ql->within, TailWin{tail + (int64_t)(tail_len - j) * SEQ_TW, q->cap_attr[stream]}, j))
+        ++v;
+  }
+  acc_wave(v, acc);
+}
+
 // ---- pool growth: one instance arena re-laid from layout `a` to layout `b` (kgen.h make_layout) ----
 // Pools and lists only grow, so every index an arena holds (StateEvent, node, list entry) stays
 // valid: each field is copied entry by entry to its new offset and the new entries stay zero (free
@@ -397,6 +452,24 @@ extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, hipStream_t s) {
 }
 
 // roll a stream's K_seq tail over batch b (after the push's K_seq launches have succeeded)
+extern "C" hipError_t sdh_live_gen(const int32_t* a32, int64_t B32, int64_t blocks, int n_groups, int group_base,
+                                    const int32_t* lane_q, const int32_t* group_seq, const sdh::kg::GQuery* queries,
+                                    unsigned long long* acc, hipStream_t s) {
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::gen_live_kernel, dim3((unsigned)blocks), dim3(64), 0, s, a32, B32, blocks, n_groups,
+                     group_base, lane_q, group_seq, queries, acc);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sdh_live_seq(const int64_t* tail, int tail_len, int stream, const int32_t* groups, int n_groups,
+                                   const int32_t* lane_q, const int32_t* group_tmpl, const sdh::kg::GQuery* queries,
+                                   unsigned long long* acc, hipStream_t s) {
+  if (n_groups <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::seq_live_kernel, dim3((unsigned)n_groups), dim3(64), 0, s, tail, tail_len, stream, groups,
+                     lane_q, group_tmpl, queries, acc);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t sdh_seq_tail(const sdh::StreamBatch* b, int64_t* tail, int32_t tail_len, int32_t new_tail_len,
                                    hipStream_t s) {
   hipLaunchKernelGGL(sdh::seq_tail_kernel, dim3(1), dim3(64), 0, s, *b, tail, tail_len, new_tail_len);

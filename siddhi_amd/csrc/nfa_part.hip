@@ -84,7 +84,31 @@ __global__ __launch_bounds__(64) void nfa_part_kernel(PartLaunch L) {
   part_body<KIND, PartInterp>(L);
 }
 
+// live partials (sdh_engine_stats): table entries in each key's current buffer; one thread per
+// (key, group, lane)
+__global__ void part_live_kernel(const int64_t* __restrict__ st, const int32_t* __restrict__ cur, int64_t n_keys,
+                                 int groups, int64_t blocks, int64_t bw, unsigned long long* acc) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t blk = x >> 6;
+  unsigned long long v = 0;
+  if (blk / groups < n_keys) {
+    const int64_t kid = blk / groups;
+    v = (unsigned long long)st[(((int64_t)cur[kid] * blocks + blk) * bw) * 64 + (x & 63)];
+  }
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(acc, v);
+}
+
 }  // namespace sdh
+
+extern "C" hipError_t sdh_live_part(const int64_t* st, const int32_t* cur, int64_t n_keys, int groups, int64_t blocks,
+                                    int64_t bw, unsigned long long* acc, hipStream_t s) {
+  const int64_t threads = n_keys * groups * 64;
+  if (threads <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::part_live_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, st, cur, n_keys,
+                     groups, blocks, bw, acc);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t sdh_launch_part(const sdh::PartLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;

@@ -15,9 +15,18 @@ Shard rule (mirrors sdh_engine_create and nfa_gen.hip key_shard):
 
 The gather moves device buffers: every rank's R18-sorted tuples stay in HBM
 (sdh_engine_poll_device), counts are all-gathered and the columns are sent to rank 0 point-to-point
-(RCCL over xGMI, or gloo on CPU tensors in the tests). The merge is a stable sort by
-(trigger sequence number, receiver rank): a query's matches for one event come from one rank (its
-pattern shard, or the owner of the event's key), so the sort keeps their pending-list order.
+(RCCL over xGMI, or gloo on CPU tensors in the tests).
+
+The merge. Every rank's stream is already in R18 order, i.e. sorted by the key (trigger sequence
+number, receiver rank) -- with the global receiver ranks of the full program, since a shard keeps its
+queries in definition order. A query's event matches for one event come from one rank (its pattern
+shard, or the owner of the event's key), so keys never tie across ranks and the merge is a k-way
+merge of sorted runs: each row's output position is its index in its own run plus, for every other
+run, the number of rows with a smaller key (torch.searchsorted), then one scatter -- no sort.
+Absent-state timer matches (tb != INT64_MIN) precede the event matches of their seq and are ordered
+by (tb, query, partition key), then emission order (matches.hip); timers of different keys /
+queries of one seq DO come from different ranks, so when any are present the merge is an exact
+stable lexicographic sort on those keys instead.
 """
 from __future__ import annotations
 
@@ -114,15 +123,21 @@ class StreamLog:
         self.streams.append(stream)
         self.next += n
 
-    def stream_of(self, seq):
-        """torch int64 tensor of seqs -> stream index tensor."""
+    def stream_of(self, seq, ignore=None):
+        """torch int64 tensor of seqs -> stream index tensor (0 where `ignore` is set: timer rows,
+        whose seq may be one past the last push, or precede every push)."""
         import torch
+        if not self.bases:
+            return torch.zeros_like(seq)
         b = torch.tensor(self.bases, dtype=torch.int64, device=seq.device)
         s = torch.tensor(self.streams, dtype=torch.int64, device=seq.device)
-        return s[torch.searchsorted(b, seq, right=True) - 1]
+        i = (torch.searchsorted(b, seq, right=True) - 1).clamp(min=0)
+        out = s[i]
+        return out if ignore is None else torch.where(ignore, torch.zeros_like(out), out)
 
 
-FIELDS = ("q", "key", "ts", "seq", "len", "words")
+FIELDS = ("q", "key", "ts", "seq", "tb", "len", "words")
+TB_EVENT = -(1 << 63)  # tb of a match completed by an event (include/siddhi_hip.h sdh_matches.tb)
 
 
 def columns_from_device(eng, device) -> Dict[str, "object"]:
@@ -133,7 +148,7 @@ def columns_from_device(eng, device) -> Dict[str, "object"]:
     n = m.n
     hip = _hip()
     out = {}
-    for name, ptr in (("q", m.query), ("key", m.key), ("ts", m.ts), ("seq", m.seq), ("off", m.off)):
+    for name, ptr in (("q", m.query), ("key", m.key), ("ts", m.ts), ("seq", m.seq), ("tb", m.tb), ("off", m.off)):
         t = torch.empty(n + 1 if name == "off" else n, dtype=torch.int64, device=device)
         if t.numel():
             _d2d(hip, t.data_ptr(), ptr, t.numel() * 8)
@@ -147,10 +162,12 @@ def columns_from_device(eng, device) -> Dict[str, "object"]:
     return out
 
 
-def columns_from_arrays(q, key, ts, off, words, seq, device="cpu"):
+def columns_from_arrays(q, key, ts, off, words, seq, tb=None, device="cpu"):
     import torch
     t = lambda a: torch.as_tensor(a, dtype=torch.int64).to(device)  # noqa: E731
-    return {"q": t(q), "key": t(key), "ts": t(ts), "seq": t(seq), "len": t(off).diff(), "words": t(words)}
+    tb = t(tb) if tb is not None else torch.full((len(q),), TB_EVENT, dtype=torch.int64, device=device)
+    return {"q": t(q), "key": t(key), "ts": t(ts), "seq": t(seq), "tb": tb, "len": t(off).diff(),
+            "words": t(words)}
 
 
 def gather_columns(cols, group=None) -> Optional[List[dict]]:
@@ -193,11 +210,37 @@ def rank_table(ir: ProgramIR):
     return table
 
 
+def merge_keys(cols, table, ns, stream_log: StreamLog):
+    """Primary merge key of each row: trigger seq << RANK_BITS | class, class 0 for a timer match and
+    1 + the global receiver rank of (query, stream) for an event match."""
+    import torch
+    timer = cols["tb"] != TB_EVENT
+    cls = table[cols["q"] * ns + stream_log.stream_of(cols["seq"], timer)] + 1
+    return (cols["seq"] << RANK_BITS) | torch.where(timer, torch.zeros_like(cls), cls), timer
+
+
+def merge_order(keys: Sequence["object"]):
+    """k-way merge of sorted int64 runs: (run index, position in the output) for every row of every
+    run. A row's position is its index in its run plus, per other run, the rows with a smaller key
+    (and, for an earlier run, equal keys too: ties keep run order, like a stable sort of the
+    concatenation)."""
+    import torch
+    pos = []
+    for r, k in enumerate(keys):
+        p = torch.arange(k.numel(), dtype=torch.int64, device=k.device)
+        for r2, k2 in enumerate(keys):
+            if r2 != r and k2.numel() and k.numel():
+                p += torch.searchsorted(k2, k, right=r2 < r)
+        pos.append(p)
+    return pos
+
+
 def merge_columns(ir: Optional[ProgramIR], per_rank: Sequence[dict], stream_log: StreamLog, table=None,
                   n_streams: int = 0) -> dict:
-    """Per-rank R18-ordered columns -> the single-engine order (stable sort by trigger seq, receiver
-    rank; rank-major concatenation keeps a query's own order). `table` (rank_table) may be given
-    instead of the program."""
+    """Per-rank R18-ordered columns -> the single-engine order: a k-way merge of the runs on (trigger
+    seq, receiver rank), or, when absent-state timer matches are present, a stable lexicographic sort
+    on (seq, class, tb, query, key) of the rank-major concatenation. `table` (rank_table) may be
+    given instead of the program."""
     import torch
     dev = per_rank[0]["q"].device
     cat = {f: torch.cat([c[f] for c in per_rank]) for f in FIELDS}
@@ -206,10 +249,20 @@ def merge_columns(ir: Optional[ProgramIR], per_rank: Sequence[dict], stream_log:
         return cat
     ns = n_streams or len(ir.streams)
     table = (rank_table(ir) if table is None else table).to(dev)
-    st = stream_log.stream_of(cat["seq"])
-    key = (cat["seq"] << RANK_BITS) | table[cat["q"] * ns + st]
-    perm = torch.sort(key, stable=True).indices
-    out = {f: cat[f][perm] for f in ("q", "key", "ts", "seq", "len")}
+    keys, timers = zip(*(merge_keys(c, table, ns, stream_log) for c in per_rank))
+    if not any(bool(t.any()) for t in timers):
+        pos = torch.cat(merge_order(keys))
+        perm = torch.empty_like(pos)
+        perm[pos] = torch.arange(n, dtype=torch.int64, device=dev)
+    else:  # LSD passes of a stable sort: key, query, tb (timer rows only), then the primary key
+        key = torch.cat(keys)
+        timer = torch.cat(timers)
+        zero = torch.zeros_like(key)
+        perm = torch.arange(n, dtype=torch.int64, device=dev)
+        for k in (torch.where(timer, cat["key"], zero), torch.where(timer, cat["q"], zero),
+                  torch.where(timer, cat["tb"], zero), key):
+            perm = perm[torch.sort(k[perm], stable=True).indices]
+    out = {f: cat[f][perm] for f in ("q", "key", "ts", "seq", "tb", "len")}
     starts = torch.cumsum(cat["len"], 0) - cat["len"]
     lens = out["len"]
     new_off = torch.cumsum(lens, 0) - lens

@@ -44,7 +44,7 @@ class SdhMatches(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("query", ctypes.POINTER(ctypes.c_int64)),
                 ("key", ctypes.POINTER(ctypes.c_int64)), ("ts", ctypes.POINTER(ctypes.c_int64)),
                 ("off", ctypes.POINTER(ctypes.c_int64)), ("words", ctypes.POINTER(ctypes.c_int64)),
-                ("seq", ctypes.POINTER(ctypes.c_int64))]
+                ("seq", ctypes.POINTER(ctypes.c_int64)), ("tb", ctypes.POINTER(ctypes.c_int64))]
 
 
 class SdhStats(ctypes.Structure):
@@ -54,13 +54,15 @@ class SdhStats(ctypes.Structure):
                 ("last_gen_items", ctypes.c_int64), ("last_seq_items", ctypes.c_int64),
                 ("last_part_items", ctypes.c_int64), ("last_ingest_ms", ctypes.c_double),
                 ("ingest_bytes", ctypes.c_int64), ("spec_kernels", ctypes.c_int64),
-                ("pool_regrows", ctypes.c_int64), ("last_slab_items", ctypes.c_int64)]
+                ("pool_regrows", ctypes.c_int64), ("last_slab_items", ctypes.c_int64),
+                ("placed_pushes", ctypes.c_int64)]
 
 
 EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engine_poll", "sdh_engine_poll_device",
            "sdh_engine_pending_matches", "sdh_engine_start", "sdh_engine_advance_time", "sdh_engine_stats",
            "sdh_engine_snapshot", "sdh_engine_state_bytes",
-           "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version"]
+           "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version",
+           "sdh_engine_debug_digest"]
 
 _lib = None
 
@@ -94,6 +96,7 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_last_error.argtypes = [P]
     lib.sdh_last_error.restype = ctypes.c_char_p
     lib.sdh_version.restype = ctypes.c_char_p
+    lib.sdh_engine_debug_digest.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
     _lib = lib
     return lib
 
@@ -178,20 +181,21 @@ class HipEngine:
         self.push_columns(stream, np.asarray(ts, dtype=np.int64), cols, nl)
 
     def poll(self, with_seq: bool = False):
-        """R18-ordered matches since the last poll as arrays (query, key, ts, off, words[, seq])."""
+        """R18-ordered matches since the last poll as arrays (query, key, ts, off, words[, seq, tb])."""
         m = SdhMatches()
         self._check(self.lib.sdh_engine_poll(self.h, ctypes.byref(m)))
         n = m.n
         if n == 0:
             z = np.zeros(0, np.int64)
-            return (z, z, z, np.zeros(1, np.int64), z) + ((z,) if with_seq else ())
+            return (z, z, z, np.zeros(1, np.int64), z) + ((z, z) if with_seq else ())
         q = np.ctypeslib.as_array(m.query, shape=(n,)).copy()
         k = np.ctypeslib.as_array(m.key, shape=(n,)).copy()
         ts = np.ctypeslib.as_array(m.ts, shape=(n,)).copy()
         off = np.ctypeslib.as_array(m.off, shape=(n + 1,)).copy()
         words = np.ctypeslib.as_array(m.words, shape=(int(off[-1]),)).copy() if off[-1] else np.zeros(0, np.int64)
         if with_seq:
-            return q, k, ts, off, words, np.ctypeslib.as_array(m.seq, shape=(n,)).copy()
+            return (q, k, ts, off, words, np.ctypeslib.as_array(m.seq, shape=(n,)).copy(),
+                    np.ctypeslib.as_array(m.tb, shape=(n,)).copy())
         return q, k, ts, off, words
 
     def poll_device(self) -> SdhMatches:
@@ -231,6 +235,13 @@ class HipEngine:
         s = SdhStats()
         self._check(self.lib.sdh_engine_stats(self.h, ctypes.byref(s)))
         return s
+
+    def debug_digest(self):
+        """(records, order-independent hash) of the last push's K_ratchet records as written, in either
+        output mode (sdh_engine_debug_digest)."""
+        out = (ctypes.c_uint64 * 2)()
+        self._check(self.lib.sdh_engine_debug_digest(self.h, out))
+        return int(out[0]), int(out[1])
 
     def state_bytes(self):
         """(live, reserved, directory) bytes of the sparse K_slab state (sdh_engine_state_bytes)."""

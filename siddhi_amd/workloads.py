@@ -75,11 +75,12 @@ def c2_within_sec(p: int, seed: int = PATTERN_SEED) -> int:
     return (1, 10, 60)[splitmix64(seed ^ p) % 3]
 
 
-def c2_app(n_patterns: int, within=None, first: int = 0) -> str:
+def c2_app(n_patterns: int, within=None, first: int = 0, step: int = 1) -> str:
     """1K concurrent 2-state filter+reference patterns (BASELINE.json configs[1]); a shard holds
-    patterns first .. first+n_patterns-1."""
+    patterns first, first+step, ... (n_patterns of them: a contiguous range, or with step = N the
+    strided shard of N GPUs, which balances the thresholds)."""
     qs = [STOCK_STREAM]
-    for p in range(first, first + n_patterns):
+    for p in range(first, first + n_patterns * step, step):
         w = c2_within_sec(p) if within is None else within
         qs.append(f"@info(name='p{p}') from every e1=StockStream[price > {c2_threshold_text(p)}] -> "
                   f"e2=StockStream[price > e1.price] within {w} sec "
@@ -110,10 +111,10 @@ def c3_query(p: int, seed: int = PATTERN_SEED) -> str:
     return f"@info(name='c3p{p}') from {body} insert into OutStream;"
 
 
-def c3_app(n_patterns: int, first: int = 0) -> str:
+def c3_app(n_patterns: int, first: int = 0, step: int = 1) -> str:
     """C3 (BASELINE.json configs[2]): count/kleene <2:5> plus logical and/or patterns,
     `partition with (symbol)` (keys = the stream's symbols)."""
-    qs = " ".join(c3_query(p) for p in range(first, first + n_patterns))
+    qs = " ".join(c3_query(p) for p in range(first, first + n_patterns * step, step))
     return f"{STOCK_STREAM} partition with (symbol of StockStream) begin {qs} end;"
 
 
@@ -146,10 +147,10 @@ def c4_query(p: int, seed: int = PATTERN_SEED) -> str:
             f"select e1.account as acct, e1.amount as a1, e3.amount as a3 insert into Alerts;")
 
 
-def c4_app(n_patterns: int, first: int = 0) -> str:
-    """C4 (BASELINE.json configs[3]): fraud-rule sequences; a shard holds patterns
-    first .. first+n_patterns-1 (pattern-set sharding across GPUs)."""
-    return " ".join([TXN_STREAM] + [c4_query(p) for p in range(first, first + n_patterns)])
+def c4_app(n_patterns: int, first: int = 0, step: int = 1) -> str:
+    """C4 (BASELINE.json configs[3]): fraud-rule sequences; a shard holds patterns first,
+    first+step, ... (pattern-set sharding across GPUs)."""
+    return " ".join([TXN_STREAM] + [c4_query(p) for p in range(first, first + n_patterns * step, step)])
 
 
 # ---- the same streams generated on a device with torch (int64 ops wrap like uint64; logical shifts
@@ -230,11 +231,11 @@ def c5_query(p: int, seed: int = PATTERN_SEED) -> str:
     return f"@info(name='c5p{p}') from {body} insert into Alerts;"
 
 
-def c5_app(n_patterns: int, first: int = 0) -> str:
+def c5_app(n_patterns: int, first: int = 0, step: int = 1) -> str:
     """C5 (BASELINE.json configs[4]): n_patterns mixed patterns in one `partition with (acct of
     Card, acct of Login, acct of Transfer, acct of Device)`; a shard holds patterns first ..
     first+n_patterns-1 (key sharding spreads the accounts over GPUs)."""
-    qs = " ".join(c5_query(p) for p in range(first, first + n_patterns))
+    qs = " ".join(c5_query(p) for p in range(first, first + n_patterns * step, step))
     keys = ", ".join(f"acct of {s}" for s in C5_STREAMS)
     return f"{c5_streams_def()} partition with ({keys}) begin {qs} end;"
 

@@ -39,6 +39,7 @@ def oracle_lib():
         lib.oracle_match_words.restype = I64
         lib.oracle_get_matches.argtypes = [P, VP, VP, VP, VP, VP]
         lib.oracle_clear_matches.argtypes = [P]
+        lib.oracle_get_match_meta.argtypes = [P, VP, VP]
         lib.oracle_live_partials.argtypes = [P]
         lib.oracle_live_partials.restype = I64
         lib.oracle_error.argtypes = [P]
@@ -100,7 +101,9 @@ class OracleEngine:
         if self.lib.oracle_advance_time(self.h, int(t)) != 0:
             raise OracleError(self.lib.oracle_error(self.h).decode())
 
-    def take_matches(self, n_slots_of):
+    def take_matches(self, n_slots_of, meta=None):
+        """Decoded matches (and, when `meta` is a list, (trigger seq, timer tiebreak) per match
+        appended to it), clearing them."""
         n = self.lib.oracle_num_matches(self.h)
         nw = self.lib.oracle_match_words(self.h)
         q = np.zeros(n, np.int64)
@@ -110,6 +113,11 @@ class OracleEngine:
         words = np.zeros(max(nw, 1), np.int64)
         self.lib.oracle_get_matches(self.h, q.ctypes.data, k.ctypes.data, ts.ctypes.data,
                                     off.ctypes.data, words.ctypes.data)
+        if meta is not None:
+            seq = np.zeros(max(n, 1), np.int64)
+            tb = np.zeros(max(n, 1), np.int64)
+            self.lib.oracle_get_match_meta(self.h, seq.ctypes.data, tb.ctypes.data)
+            meta.extend(zip(seq[:n].tolist(), tb[:n].tolist()))
         self.lib.oracle_clear_matches(self.h)
         return decode_matches(n, q, k, ts, off, words, n_slots_of)
 
@@ -150,6 +158,7 @@ class App:
             self.engine.set_playback(True)   # (the HIP engine takes SDH_FLAG_PLAYBACK at create)
         self.log = EventLog()
         self.matches: List[tuple] = []
+        self.meta: List[tuple] = []  # per match (trigger seq, timer tiebreak) when the engine has them
 
     def stream_types(self, name: str) -> List[int]:
         return self.ir.streams[self.ir.stream_index(name)].attr_types
@@ -159,7 +168,7 @@ class App:
         vals, nulls = encode_rows(rows, self.ir.streams[si].attr_types, self.dictionary)
         self.log.append(si, ts, vals, nulls)
         self.engine.send(si, ts, vals, nulls, as_chunk)
-        self.matches.extend(self.engine.take_matches(lambda q: len(self.ir.queries[q].states)))
+        self._take()
 
     def start(self, t: int):
         """SiddhiAppRuntime.start at time t (absent patterns schedule from it)."""
@@ -168,7 +177,14 @@ class App:
     def advance_time(self, t: int):
         """Time passes to t with no event: absent patterns' schedulers fire what falls due."""
         self.engine.advance_time(t)
-        self.matches.extend(self.engine.take_matches(lambda q: len(self.ir.queries[q].states)))
+        self._take()
+
+    def _take(self):
+        n_slots = lambda q: len(self.ir.queries[q].states)  # noqa: E731
+        if isinstance(self.engine, OracleEngine):
+            self.matches.extend(self.engine.take_matches(n_slots, self.meta))
+        else:
+            self.matches.extend(self.engine.take_matches(n_slots))
 
     def rows_for_query(self, qname: str):
         qi = self.ir.query_index(qname)

@@ -25,18 +25,25 @@ PART = [
     "@info(name='p0') from every e1=A[v > 4] -> e2=A[p > e1.p] within 50 milliseconds select e1.v as a insert into O;",
     "@info(name='p1') from every e1=B[v > 2] -> e2=A[v > e1.v] and e3=B[p < 2] within 60 milliseconds select e1.v as a insert into O;",
 ]
+# absent states inside the partition: timer matches of different keys fire before the same event
+# (the merge must order them by (tb, query, key) across ranks)
+PART_ABSENT = [
+    "@info(name='p2') from every e1=A[v > 6] -> not B[p > 8] for 15 milliseconds select e1.v as a insert into O;",
+    "@info(name='p3') from every e1=B[v > 7] -> not A[v < 2] for 9 milliseconds select e1.v as a insert into O;",
+]
 
 
-def full_src():
-    return " ".join([STREAMS, TOP[0], TOP[1], "partition with (k of A, k of B) begin", *PART, "end;", TOP[2], TOP[3]])
+def full_src(absent=False):
+    part = PART + (PART_ABSENT if absent else [])
+    return " ".join([STREAMS, TOP[0], TOP[1], "partition with (k of A, k of B) begin", *part, "end;", TOP[2], TOP[3]])
 
 
-def shard_src(ir, rank, world):
+def shard_src(ir, rank, world, absent=False):
     """Rank `rank`'s sub-app: its pattern shard of the unpartitioned queries plus the whole partition
     block (every rank runs the partition for the keys it owns)."""
     names = {ir.queries[q].name for q in range(len(ir.queries)) if sdist.shard_of(ir, q, world) in (rank, -1)}
     parts = [STREAMS] + [q for q in TOP[:2] if q.split("'")[1] in names]
-    parts += ["partition with (k of A, k of B) begin", *PART, "end;"]
+    parts += ["partition with (k of A, k of B) begin", *PART, *(PART_ABSENT if absent else []), "end;"]
     parts += [q for q in TOP[2:] if q.split("'")[1] in names]
     return " ".join(parts), names
 
@@ -51,7 +58,7 @@ def events(seed=3, n=400):
     return out
 
 
-def _worker(rank, world, port, results):
+def _worker(rank, world, port, results, absent=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -59,33 +66,39 @@ def _worker(rank, world, port, results):
     from siddhi_amd import ql
     from siddhi_amd.ir import T_INT
     from siddhi_amd.planner import plan
-    ir = plan(ql.parse(full_src()))
-    src, names = shard_src(ir, rank, world)
+    ir = plan(ql.parse(full_src(absent)))
+    src, names = shard_src(ir, rank, world, absent)
     local = App(src)
     log = sdist.StreamLog()
-    for stream, row, t in events():  # every rank sees the whole stream (the broadcast)
+    evs = events()
+    for stream, row, t in evs:  # every rank sees the whole stream (the broadcast)
         local.send(stream, [row], [t])
         log.push(ir.stream_index(stream), 1)
-    rows = []
-    for m in local.matches:
+    local.advance_time(evs[-1][2] + 100)  # trailing timers fire (seq = one past the last event)
+    rows, meta = [], []
+    for m, mt in zip(local.matches, local.meta):
         gq = ir.query_index(local.ir.queries[m[0]].name)  # local query index -> global
         if ir.queries[gq].partition_idx >= 0 and sdist.key_shard(m[1], T_INT, world) != rank:
             continue  # another rank owns this key (the device drops its events at routing)
         rows.append((gq,) + tuple(m[1:]))
+        meta.append(mt)
     q = [m[0] for m in rows]
     words, off = [], [0]
     for m in rows:
         for sl in m[3]:
             words += [len(sl), *sl]
         off.append(len(words))
-    seq = [max(x for sl in m[3] for x in sl) for m in rows]  # the triggering (newest) event
-    cols = sdist.columns_from_arrays(q, [m[1] for m in rows], [m[2] for m in rows], off, words, seq)
+    seq = [mt[0] for mt in meta]  # the event whose processing produced the match
+    tb = [mt[1] for mt in meta]
+    cols = sdist.columns_from_arrays(q, [m[1] for m in rows], [m[2] for m in rows], off, words, seq, tb)
     per_rank = sdist.gather_columns(cols)
     if rank == 0:
-        full = App(full_src())
-        for stream, row, t in events():
+        full = App(full_src(absent))
+        for stream, row, t in evs:
             full.send(stream, [row], [t])
+        full.advance_time(evs[-1][2] + 100)
         merged = sdist.columns_to_tuples(sdist.merge_columns(ir, per_rank, log))
+        results["timers"] = sum(1 for x in tb if x != sdist.TB_EVENT)
         results["ok"] = merged == full.matches
         results["n"] = len(full.matches)
         results["sizes"] = [int(c["q"].numel()) for c in per_rank]
@@ -103,16 +116,34 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_gather_merge_equals_single_engine(world):
-    """Pattern-set + key sharding, the column gather (gloo) and the R18 merge reproduce one engine."""
+@pytest.mark.parametrize("world,absent", [(2, False), (3, False), (2, True), (3, True)])
+def test_sharded_gather_merge_equals_single_engine(world, absent):
+    """Pattern-set + key sharding, the column gather (gloo) and the R18 merge reproduce one engine
+    (with absent states in the partition: timer matches of several ranks before one event)."""
     mgr = mp.Manager()
     results = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), results), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), results, absent), nprocs=world, join=True)
     assert results["n"] > 50
     assert all(s > 0 for s in results["sizes"])
     assert sum(1 for x in results["part_split"] if x > 0) >= 2  # partition keys really split
+    if absent:
+        assert results["timers"] > 10
     assert results["ok"]
+
+
+def test_merge_order_is_a_stable_kway_merge():
+    """merge_order over sorted runs equals a stable sort of the concatenation (ties in run order)."""
+    import torch
+    g = torch.Generator().manual_seed(5)
+    for _ in range(20):
+        runs = [torch.sort(torch.randint(0, 40, (int(torch.randint(0, 30, (1,), generator=g)),), generator=g)).values
+                for _ in range(int(torch.randint(1, 5, (1,), generator=g)))]
+        pos = torch.cat(sdist.merge_order(runs))
+        cat = torch.cat(runs)
+        want = torch.sort(cat, stable=True).indices
+        perm = torch.empty_like(pos)
+        perm[pos] = torch.arange(cat.numel())
+        assert torch.equal(perm, want)
 
 
 def test_shard_rule():

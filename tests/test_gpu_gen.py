@@ -196,32 +196,37 @@ def test_force_gen_matches_chain_plans_on_c2():
     assert len(a[0]) > 10000
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_engine_shards_merge_to_single_engine(world):
+@pytest.mark.parametrize("world,absent", [(2, False), (3, False), (2, True), (3, True)])
+def test_engine_shards_merge_to_single_engine(world, absent):
     """sdh_config.shard_rank/shard_world on the device: pattern-set sharding of the unpartitioned
     queries and key sharding of the partition (foreign keys dropped at routing); the union of the
     shards, merged by siddhi_amd.dist.merge_columns, equals one engine running every query (and the
-    oracle)."""
+    oracle). With absent states in the partition, timer matches of several ranks precede one event:
+    the merge orders them by the exported tiebreak (sdh_matches.tb)."""
     from siddhi_amd import dist as sdist
     from siddhi_amd.engine import HipEngine
     from siddhi_amd.ir import T_INT
     from test_dist import events, full_src
-    o = App(full_src())
+    o = App(full_src(absent))
     types = [s.attr_types for s in o.ir.streams]
     shards = [HipEngine(o.blob, stream_types=types, shard_rank=r, shard_world=world) for r in range(world)]
     log = sdist.StreamLog()
     from siddhi_amd.events import encode_rows
-    for stream, row, t in events():
+    evs = events()
+    for stream, row, t in evs:
         o.send(stream, [row], [t])
         si = o.ir.stream_index(stream)
         log.push(si, 1)
         vals, nulls = encode_rows([row], o.ir.streams[si].attr_types, o.dictionary)
         for sh in shards:  # every rank sees the whole stream
             sh.send(si, [t], vals, nulls)
+    o.advance_time(evs[-1][2] + 100)
+    for sh in shards:
+        sh.advance_time(evs[-1][2] + 100)
     per_rank = []
     for r, sh in enumerate(shards):
-        q, k, ts, off, words, seq = sh.poll(with_seq=True)
-        cols = sdist.columns_from_arrays(q, k, ts, off, words, seq)
+        q, k, ts, off, words, seq, tb = sh.poll(with_seq=True)
+        cols = sdist.columns_from_arrays(q, k, ts, off, words, seq, tb)
         for qi, key in zip(q.tolist(), k.tolist()):
             if o.ir.queries[qi].partition_idx >= 0:
                 assert sdist.key_shard(key, T_INT, world) == r

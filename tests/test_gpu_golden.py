@@ -66,6 +66,115 @@ def _hip():
     return lib
 
 
+def _d2h(hip, ptr, first, n):
+    out = np.zeros(n, np.int64)
+    if n:
+        addr = ctypes.cast(ptr, ctypes.c_void_p).value + first * 8
+        assert hip.hipMemcpy(out.ctypes.data, addr, n * 8, 2) == 0  # hipMemcpyDeviceToHost
+    return out
+
+
+def _digest_device_matches(eng, dig, chunk=1 << 24):
+    """sdh_engine_poll_device, then the R18-ordered tuples streamed to the host in slices into the
+    running digest (the digest is independent of how the stream is cut)."""
+    hip = _hip()
+    m = eng.poll_device()
+    for lo in range(0, m.n, chunk):
+        n = min(chunk, m.n - lo)
+        off = _d2h(hip, m.off, lo, n + 1)
+        words = _d2h(hip, m.words, int(off[0]), int(off[-1] - off[0]))
+        dig.update(_d2h(hip, m.query, lo, n), _d2h(hip, m.key, lo, n), _d2h(hip, m.ts, lo, n), off - off[0], words)
+    return m.n
+
+
+@pytest.mark.timeout(900)
+def test_headline_config_golden():
+    """The headline configuration itself (bench.py's default workload): 10,000 C2 patterns over 200K
+    events (~860M matches), pushed from HBM in 100K-event batches, against the oracle's golden
+    (tests/golden/large_c2h.json). The same pushes in SDH_FLAG_DEVICE_MATCHES mode (the bench's) write
+    the same K_ratchet records: equal counts and equal order-independent record hashes
+    (sdh_engine_debug_digest); and one 200K-event push in that mode produces the golden's count."""
+    import torch
+    from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES, HipEngine
+    cfg = CONFIGS["c2h"]
+    g = load("c2h")
+    app = App(app_source("c2h", cfg["patterns"]), engine_factory=lambda blob: None)
+    types = [s.attr_types for s in app.ir.streams]
+    dev = torch.device("cuda:0")
+
+    def batch(lo, n):
+        ts, cols, _ = events("c2h", lo, n)
+        t_ts = torch.from_numpy(ts).to(dev)
+        t_cols = [torch.from_numpy(np.ascontiguousarray(c).view(np.int32)).to(dev) for c in cols]
+        return t_ts, t_cols
+
+    normal = HipEngine(app.blob, stream_types=types)
+    ring = HipEngine(app.blob, stream_types=types, flags=SDH_FLAG_DEVICE_MATCHES)
+    dig = Digest(g["sample_stride"])
+    B = cfg["events"] // 2
+    for lo in range(0, cfg["events"], B):
+        t_ts, t_cols = batch(lo, B)
+        for e in (normal, ring):
+            e.push_device(0, B, t_ts.data_ptr(), [c.data_ptr() for c in t_cols])
+        dn, dr = normal.debug_digest(), ring.debug_digest()
+        assert dn == dr and dn[0] > 0, f"normal-mode records {dn} != device-match-mode records {dr}"
+        assert ring.pending_matches() == dn[0]
+        assert _digest_device_matches(normal, dig) == dn[0]
+    ring.close()
+    normal.close()
+    assert dig.n == g["n_matches"]
+    assert dig.first == g["sample_first"]
+    assert dig.strided == g["sample_strided"]
+    assert dig.n_words == g["n_words"]
+    assert dig.hexdigest() == g["digest"]
+    one = HipEngine(app.blob, stream_types=types, flags=SDH_FLAG_DEVICE_MATCHES)
+    t_ts, t_cols = batch(0, cfg["events"])
+    one.push_device(0, cfg["events"], t_ts.data_ptr(), [c.data_ptr() for c in t_cols])
+    assert one.pending_matches() == g["n_matches"]
+    assert one.debug_digest()[0] == g["n_matches"]
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_direct_placement_equals_sort(mixed):
+    """Pushes whose matches all come from K_ratchet go straight to their R18 rows (matches.hip
+    ratchet_place_kernel, no sort at poll). Against the same pushes with placement off
+    (SDH_NO_PLACE: the device table + radix sort): identical poll output, over polls after one push
+    and after several (placed windows), and -- `mixed` -- with chain / K_gen queries whose rare
+    matches turn a placed window back into table rows (placed_to_table)."""
+    import os
+    from siddhi_amd.engine import HipEngine
+    from siddhi_amd.workloads import c2_app, stock_events
+    src = c2_app(200)
+    if mixed:
+        src += (" @info(name='x3') from every e1=StockStream[price > 90] -> e2=StockStream[price < 10] "
+                "-> e3=StockStream[price > e1.price] within 1 sec select e1.price as a insert into O;"
+                " @info(name='xl') from every e1=StockStream[price > 98] -> e2=StockStream[volume > 990] "
+                "or e3=StockStream[price < 0.5] within 1 sec select e1.price as a insert into O;")
+    app = App(src, engine_factory=lambda blob: None)
+    types = [s.attr_types for s in app.ir.streams]
+    a, b = HipEngine(app.blob, stream_types=types), HipEngine(app.blob, stream_types=types)
+    sizes = [700, 9000, 5, 1300, 40000, 1, 2500, 800, 800, 800, 6000, 300] * 2
+    polls = {0, 2, 4, 5, 9, 10, 13, 17, 20, 23}
+    lo, n_total = 0, 0
+    for i, n in enumerate(sizes):
+        ts, sym, price, vol = stock_events(lo, n)
+        lo += n
+        cols = [sym, price.view(np.uint32), vol]
+        a.push_columns(0, ts, cols)
+        os.environ["SDH_NO_PLACE"] = "1"
+        try:
+            b.push_columns(0, ts, cols)
+        finally:
+            del os.environ["SDH_NO_PLACE"]
+        if i in polls:
+            ga, gb = a.poll(with_seq=True), b.poll(with_seq=True)
+            for x, y in zip(ga, gb):
+                assert np.array_equal(x, y)
+            n_total += len(ga[0])
+    assert n_total > 100000
+    assert a.stats().placed_pushes >= 8 and b.stats().placed_pushes == 0
+
+
 def test_poll_device_equals_poll():
     """sdh_engine_poll_device leaves the same R18-ordered tuples in HBM that sdh_engine_poll copies
     to the host (two engines over the same C2 stream: ratchet + chain + K_gen plans)."""
