@@ -69,6 +69,7 @@ def parse():
     ap.add_argument("--expansion-batch", type=int, default=1 << 16)
     ap.add_argument("--no-expansion", action="store_true")
     ap.add_argument("--no-ingest", action="store_true")
+    ap.add_argument("--no-latency", action="store_true", help="skip the small-push latency leg")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -493,6 +494,10 @@ def main():
     if not args.no_ingest and world == 1:
         log("host-ingest leg")
         result["host_ingest"] = host_ingest(args, eng, B, K, n_batches)
+    if not args.no_latency and world == 1 and not c5:
+        log("push-latency leg")
+        eng.close()
+        result["push_latency"] = push_latency(args, sh, K, local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(args.workload, K, args.cpu_seconds)
@@ -522,6 +527,36 @@ def host_ingest(args, eng, B, K, first_step):
     return {"events_per_step": B, "steps": steps, "ms_per_step": el * 1e3 / steps, "h2d_ms_per_step": ing / steps,
             "h2d_gbps": nbytes / (ing / steps * 1e-3) / 1e9 if ing else None,
             "pattern_events_per_s": B * steps * eng_patterns(eng) / el}
+
+
+def push_latency(args, sh, K, local):
+    """Latency of one small push + poll, the JNI seam's granularity (StreamJunction.Receiver.receive(
+    Event) / receive(Event[]) chunks, StreamJunction.java:376-389): host-resident events of 1, 64 and
+    4,096, normal mode (every match polled to the host in R18 order). Median and p99 over 50 pushes
+    after 5 warm-up pushes (4,096: 10 after 2; at 10K C2 patterns such a push carries ~17M matches),
+    continuing one stream."""
+    from siddhi_amd.workloads import stock_events, txn_events
+    eng = make_engine(args.workload, sh, K, local, 0, args.partials)
+    gen = txn_events if args.workload == "c4" else stock_events
+    out, lo = {}, 0
+    for bs in (1, 64, 4096):
+        lat, nm = [], 0
+        warm, reps = (5, 50) if bs < 4096 else (2, 10)
+        for i in range(warm + reps):
+            ts, a, b, c = gen(lo, bs, K)
+            lo += bs
+            cols = [a, b.view(np.uint32), c]
+            t0 = time.perf_counter()
+            eng.push_columns(0, ts, cols)
+            m = eng.poll()
+            if i >= warm:
+                lat.append((time.perf_counter() - t0) * 1e3)
+                nm += len(m[0])
+        lat.sort()
+        out[str(bs)] = {"median_ms": lat[len(lat) // 2], "p99_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))],
+                        "matches_per_push": nm / len(lat)}
+    eng.close()
+    return out
 
 
 def eng_patterns(eng):

@@ -53,8 +53,14 @@ struct LaneOut {
     const int64_t tw = (int64_t)nl * words;
     const unsigned long long o = atomicAdd(next, (unsigned long long)tw);
     if (ring) {
-      if (tw > GEN_RING_MARGIN) return nullptr;  // (the margin holds any record the ring wraps)
-      return out + (int64_t)(o % (unsigned long long)(cap - GEN_RING_MARGIN));
+      // the margin holds any record the ring wraps; a longer run of records wraps modulo the buffer
+      // less its own length (written, and counted, like any other: ADVICE r2)
+      const int64_t m = cap - (tw > GEN_RING_MARGIN ? tw : GEN_RING_MARGIN);
+      if (m <= 0) {
+        over = true;
+        return nullptr;
+      }
+      return out + (int64_t)(o % (unsigned long long)m);
     }
     if ((int64_t)(o + tw) > cap) {
       over = true;

@@ -74,13 +74,18 @@ extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off,
                                      const int32_t* out_rank, int n_streams, sdh::MatchTable T, int64_t row0,
                                      int64_t word0, hipStream_t s);
 extern "C" size_t sdh_poll_temp_bytes(int64_t n);
+extern "C" hipError_t sdh_gen_journal(int32_t* a32, int64_t* a64, int64_t B32, int64_t B64, int mode,
+                                       const int32_t* glist, const uint32_t* seg_kid, int groups, int64_t slots,
+                                       int32_t* j32, int64_t* j64, int64_t* jidx, int restore, hipStream_t s);
 extern "C" size_t sdh_place_temp_bytes(int64_t cells);
 extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, const int32_t* blk_count,
-                                        const int32_t* blk_group, int n_blocks, const int32_t* gpos, int n_gpos,
-                                        int64_t n_events, int32_t* cnt, int32_t* flag, void* temp, size_t temp_bytes,
-                                        const sdh::RatchetGroup* groups, const int64_t* ts, int64_t seq_base,
-                                        int64_t row0, int64_t* oq, int64_t* okey, int64_t* ots, int64_t* oseq,
-                                        int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s);
+                                        const int32_t* blk_group, const int32_t* blk_prev, int n_blocks,
+                                        int64_t rows, const int32_t* out_rank,
+                                        int n_streams, int n_ranks, int64_t n_events, int32_t* cnt, int32_t* flag,
+                                        void* temp, size_t temp_bytes, const sdh::RatchetGroup* groups,
+                                        const int64_t* ts, int64_t seq_base, int64_t row0, int64_t* oq, int64_t* okey,
+                                        int64_t* ots, int64_t* oseq, int64_t* otb, int64_t* ooff, int64_t* owords,
+                                        hipStream_t s);
 extern "C" hipError_t sdh_placed_to_table(const int64_t* q, const int64_t* ts, const int64_t* seq, const int64_t* words,
                                           int64_t n, int64_t seq_ref, const int32_t* out_rank, const int32_t* qinfo,
                                           int n_streams, sdh::MatchTable T, hipStream_t s);
@@ -667,9 +672,10 @@ struct sdh_engine {
     DevBuf<int64_t> a64;
     DevBuf<int32_t> s32;             // scratch arenas of event chunks 1.. (unpartitioned sets)
     DevBuf<int64_t> s64;
-    DevBuf<int32_t> bk32;            // the arenas before the current push (exact re-runs)
-    DevBuf<int64_t> bk64;
-    size_t bk_n32 = 0, bk_n64 = 0;
+    // exact re-runs: the blocks the current pass modifies, as they were before it (gen_journal)
+    DevBuf<int32_t> j32;
+    DevBuf<int64_t> j64, jidx;
+    int64_t jn = 0;
   };
   std::vector<std::unique_ptr<GenSet>> gsets;
   // per partition: PartitionRuntime's key -> instance map (dense key ids), shared by the
@@ -744,7 +750,7 @@ struct sdh_engine {
   DevBuf<unsigned long long> g_rec_next;
   int64_t g_dev_matches = 0;         // K_gen / K_seq matches of the last push
   int64_t g_used = 0;                // words of the last push's records in g_out (normal mode)
-  bool g_out_lost = false;           // the last push's records overflowed g_out (matches lost)
+  bool g_journal = false;            // the current K_gen pass journals the blocks it modifies
   // ---- K_ratchet groups ----
   std::vector<RatchetGroup> rg;
   std::vector<int> rcur;             // per group: buffer holding its deques
@@ -754,19 +760,15 @@ struct sdh_engine {
   DevBuf<RatchetItem> d_ritems;
   std::vector<RatchetItem> ritems;
   DevBuf<int64_t> d_rmatch;
-  DevBuf<int32_t> d_blk_count, d_blk_next, d_blk_group;
+  DevBuf<int32_t> d_blk_count, d_blk_next, d_blk_group, d_blk_prev;
   DevBuf<unsigned long long> d_rtotal;  // records written in ring mode (SDH_FLAG_DEVICE_MATCHES)
   int r_wide = 0;
   int64_t r_blocks = 0;              // capacity in blocks
   int r_blk_recs = 8192;
   int r_blocks_used = 0;             // of the last launch
   int64_t r_blk_taken = 0;           // blocks the last launch took (ring mode: may exceed r_blocks)
-  // direct R18 placement (matches.hip ratchet_place_kernel): per group its position among its
-  // stream's groups in receiver-rank order; per stream the group count, or -1 when some group's lanes
-  // are not consecutive ranks
-  std::vector<int32_t> r_gpos;
-  std::vector<int> r_place_n;
-  DevBuf<int32_t> d_rgpos, p_cnt, p_flag;
+  // direct R18 placement (matches.hip ratchet_place_kernel): the (event, query rank) count matrix
+  DevBuf<int32_t> p_cnt, p_flag;
   DevBuf<uint8_t> p_ptemp;
   int64_t r_seq_base = 0;            // seq of the last launch's first event
   std::vector<int32_t> r_blk_count;
@@ -912,40 +914,14 @@ void table_clear(sdh_engine* e) {
   e->seq_ref = e->seq;
 }
 
-// Direct R18 placement plan: a stream's K_ratchet matches can be placed without a sort when every
-// group's lanes are consecutive receiver ranks (queries of one shape defined in a row)
-void ratchet_place_plan(sdh_engine* e) {
-  const int ns = (int)e->prog.stream_types.size();
-  e->r_gpos.assign(e->rg.size(), -1);
-  e->r_place_n.assign(ns, 0);
-  for (int s = 0; s < ns; ++s) {
-    std::vector<std::pair<int, int>> gr;  // (first rank, group)
-    bool ok = true;
-    for (int g = 0; g < (int)e->rg.size(); ++g) {
-      const RatchetGroup& G = e->rg[g];
-      if (G.stream != s) continue;
-      const int r0 = e->out_rank[(size_t)G.qid[0] * ns + s];
-      for (int l = 1; l < G.n_lanes; ++l) ok &= e->out_rank[(size_t)G.qid[l] * ns + s] == r0 + l;
-      gr.push_back({r0, g});
-    }
-    std::sort(gr.begin(), gr.end());
-    for (size_t i = 0; i < gr.size(); ++i) e->r_gpos[gr[i].second] = (int32_t)i;
-    e->r_place_n[s] = ok ? (int)gr.size() : -1;
-  }
-  if (!e->r_gpos.empty()) {
-    e->d_rgpos.ensure(e->r_gpos.size());
-    HIPCHK(hipMemcpy(e->d_rgpos.p, e->r_gpos.data(), e->r_gpos.size() * 4, hipMemcpyHostToDevice));
-  }
-}
-
 // The last push's K_ratchet matches written straight to their R18 rows of the ABI outputs, after
 // the window's rows (matches.hip ratchet_place_kernel). False, with nothing written, when the push
 // does not qualify or a run split over two blocks: the caller appends to the table instead.
-bool place_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base, int64_t n_events, int stream) {
-  const int ng = e->r_place_n[stream];
+bool place_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base, int64_t n_events) {
+  const int nr = (int)e->prog.q.size();  // receiver ranks < queries
   const int64_t rows = e->r_matches, n0 = e->mt.n;
-  if (ng <= 0 || e->r_wide || e->r_blk_recs > 8192 || (double)n_events * ng > (double)(1 << 28) ||
-      n0 + rows >= INT32_MAX || getenv("SDH_NO_PLACE"))
+  if (e->r_wide || e->r_blk_recs > 8192 || (double)n_events * nr > (double)(1 << 30) || n0 + rows >= INT32_MAX ||
+      getenv("SDH_NO_PLACE"))
     return false;
   const size_t keep = (size_t)n0, want = (size_t)(n0 + rows);
   e->po_q.grow_keep(want, keep, e->stream);
@@ -955,13 +931,14 @@ bool place_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base, int64
   e->po_tb.grow_keep(want, keep, e->stream);
   e->po_off.grow_keep(want + 1, keep, e->stream);
   e->po_words.grow_keep(4 * want, 4 * keep, e->stream);
-  const int64_t cells = n_events * ng;
+  const int64_t cells = n_events * nr;
   e->p_cnt.ensure((size_t)cells);
   e->p_flag.ensure(1);
   const size_t tb = sdh_place_temp_bytes(cells);
   e->p_ptemp.ensure(tb);
   const hipError_t r = sdh_place_ratchet(e->d_rmatch.p, e->r_blk_recs, e->d_blk_count.p, e->d_blk_group.p,
-                                         e->r_blocks_used, e->d_rgpos.p, ng, n_events, e->p_cnt.p, e->p_flag.p,
+                                         e->d_blk_prev.p, e->r_blocks_used, rows, e->d_out_rank.p, (int)e->prog.stream_types.size(), nr,
+                                         n_events, e->p_cnt.p, e->p_flag.p,
                                          e->p_ptemp.p, e->p_ptemp.n, e->d_rg.p, ts_col, seq_base, n0, e->po_q.p,
                                          e->po_key.p, e->po_ts.p, e->po_seq.p, e->po_tb.p, e->po_off.p, e->po_words.p,
                                          e->stream);
@@ -1326,6 +1303,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     if (any64) e->d_rspillB.ensure((size_t)n_items * e->rSC * WAVE);
     e->d_blk_count.ensure((size_t)e->r_blocks);
     e->d_blk_group.ensure((size_t)e->r_blocks);
+    e->d_blk_prev.ensure((size_t)e->r_blocks);
     e->d_err.ensure(4);
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
     HIPCHK(hipMemsetAsync(e->d_blk_next.p, 0, 4, e->stream));
@@ -1363,6 +1341,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.match = e->d_rmatch.p;
     L.blk_count = e->d_blk_count.p;
     L.blk_group = e->d_blk_group.p;
+    L.blk_prev = e->d_blk_prev.p;
     L.wide = wide;
     L.blk_next = e->d_blk_next.p;
     L.n_blocks = (int32_t)std::min<int64_t>(e->r_blocks, INT32_MAX);
@@ -2087,6 +2066,53 @@ bool gen_grown_sizing(const sdh_engine* e, int capk, kg::Sizing* out) {
 }
 
 
+// Exact re-runs (the reference never drops a match): just before a K_gen launch modifies a set's
+// arena blocks, they are journaled (gen_journal_kernel); a pass whose match output, pools, K_part
+// tables or K_slab space overflowed is undone by copying them back, and re-run at the grown size.
+// The journal holds the blocks of this pass only -- the set's groups (unpartitioned), the pushed
+// keys' blocks (partitions), every known key's (a timer sweep) -- so its cost scales with the push,
+// not with the total state. mode / glist / seg_kid: as gen_journal_kernel.
+void gen_journal(sdh_engine* e, sdh_engine::GenSet& gs, int mode, const int32_t* glist, const uint32_t* seg_kid,
+                 int64_t slots) {
+  gs.jn = 0;
+  if (!e->g_journal || slots <= 0) return;
+  const size_t b32 = (size_t)e->gB32 * 64, b64 = (size_t)e->gB64 * 64;
+  gs.j32.ensure(b32 * slots);
+  gs.j64.ensure(b64 * slots);
+  gs.jidx.ensure((size_t)slots);
+  HIPCHK(sdh_gen_journal(gs.a32.p, gs.a64.p, e->gB32, e->gB64, mode, glist, seg_kid, gs.n_groups, slots, gs.j32.p,
+                         gs.j64.p, gs.jidx.p, 0, e->stream));
+  gs.jn = slots;
+}
+
+void gen_restore_journal(sdh_engine* e) {
+  for (auto& up : e->gsets) {
+    auto& gs = *up;
+    if (gs.jn > 0)
+      HIPCHK(sdh_gen_journal(gs.a32.p, gs.a64.p, e->gB32, e->gB64, 0, nullptr, nullptr, gs.n_groups, gs.jn, gs.j32.p,
+                             gs.j64.p, gs.jidx.p, 1, e->stream));
+    gs.jn = 0;
+  }
+  HIPCHK(hipStreamSynchronize(e->stream));
+}
+
+// Upper bound of the journal bytes a push of n events over `stream` needs; do_push splits a batch
+// whose bound does not fit a third of free HBM
+double gen_journal_bound(sdh_engine* e, int64_t n) {
+  double blocks = 0;
+  for (auto& up : e->gsets) {
+    auto& gs = *up;
+    if (gs.partition < 0) {
+      blocks += gs.n_groups;
+      continue;
+    }
+    bool timed = false;
+    for (int g = 0; g < gs.n_groups; ++g) timed |= e->gq[e->group_tmpl[gs.group_base + g]].lay.TQ > 0;
+    blocks += (double)gs.n_groups * (double)(timed ? gs.key_cap + n : n);
+  }
+  return blocks * ((double)e->gB32 * 64 * 4 + (double)e->gB64 * 64 * 8);
+}
+
 // one K_gen step for every set fed by `stream`
 sdh::GenLaunch gen_launch_base(sdh_engine* e, const sdh_engine::GenSet& gs, const StreamBatch& B, bool write) {
   sdh::GenLaunch L{};
@@ -2275,6 +2301,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
         L.s32 = gs.s32.p;
         L.s64 = gs.s64.p;
       }
+      gen_journal(e, gs, 0, L.glist, nullptr, (int64_t)gen_groups.size());
       HIPCHK(sdh_launch_gen(&L, e->stream));
       e->stats.last_gen_items += L.n_items;
       if (C > 1) {  // the last chunk's instances are the set's state after this batch
@@ -2319,6 +2346,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       L.ev_kid = ev_kid;
       L.n_keys = n_keys;
       L.n_items = (int32_t)(n_keys * gs.n_groups);
+      gen_journal(e, gs, 2, nullptr, nullptr, (int64_t)L.n_items);
       if (L.n_items > 0) HIPCHK(sdh_launch_gen(&L, e->stream));
       e->stats.last_gen_items += L.n_items;
       any = true;
@@ -2387,6 +2415,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       L.key_of_id = rt.key_of_id.p;
       L.ev_idx = e->r_idx_s.p;
       L.n_items = hv[1] * gs.n_groups;
+      gen_journal(e, gs, 1, nullptr, e->r_uniq.p, (int64_t)L.n_items);
       HIPCHK(sdh_launch_gen(&L, e->stream));
       e->stats.last_gen_items += L.n_items;
       any = true;
@@ -2534,40 +2563,6 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
   return any;
 }
 
-// arena state of every set a push over `stream` may touch, copied before the push so that a pass
-// whose match output overflowed can be undone and re-run exactly (normal mode only: in
-// SDH_FLAG_DEVICE_MATCHES mode records wrap in a ring and cannot overflow)
-bool gen_backup(sdh_engine* e) {
-  size_t total = 0;
-  for (auto& up : e->gsets) total += up->a32.n * 4 + up->a64.n * 8;
-  size_t fr = 0, tot = 0;
-  if (hipMemGetInfo(&fr, &tot) != hipSuccess || total > fr / 3) {
-    (void)hipGetLastError();
-    return false;
-  }
-  for (auto& up : e->gsets) {
-    auto& gs = *up;
-    gs.bk32.ensure(std::max<size_t>(1, gs.a32.n));
-    gs.bk64.ensure(std::max<size_t>(1, gs.a64.n));
-    gs.bk_n32 = gs.a32.n;
-    gs.bk_n64 = gs.a64.n;
-    if (gs.a32.n) HIPCHK(hipMemcpyAsync(gs.bk32.p, gs.a32.p, gs.a32.n * 4, hipMemcpyDeviceToDevice, e->stream));
-    if (gs.a64.n) HIPCHK(hipMemcpyAsync(gs.bk64.p, gs.a64.p, gs.a64.n * 8, hipMemcpyDeviceToDevice, e->stream));
-  }
-  return true;
-}
-
-void gen_restore_backup(sdh_engine* e) {
-  for (auto& up : e->gsets) {
-    auto& gs = *up;
-    // blocks added by arena growth during the undone pass are fresh again (zero: not yet seeded)
-    if (gs.a32.n > gs.bk_n32) HIPCHK(hipMemsetAsync(gs.a32.p + gs.bk_n32, 0, (gs.a32.n - gs.bk_n32) * 4, e->stream));
-    if (gs.a64.n > gs.bk_n64) HIPCHK(hipMemsetAsync(gs.a64.p + gs.bk_n64, 0, (gs.a64.n - gs.bk_n64) * 8, e->stream));
-    if (gs.bk_n32) HIPCHK(hipMemcpyAsync(gs.a32.p, gs.bk32.p, gs.bk_n32 * 4, hipMemcpyDeviceToDevice, e->stream));
-    if (gs.bk_n64) HIPCHK(hipMemcpyAsync(gs.a64.p, gs.bk64.p, gs.bk_n64 * 8, hipMemcpyDeviceToDevice, e->stream));
-  }
-}
-
 // one K_gen step for every set fed by `stream`
 void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out, double* bytes_out) {
   *ms_out = 0;
@@ -2581,11 +2576,12 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   e->d_err.ensure(4);
   e->g_rec_next.ensure(1);
   const bool write = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) == 0;
-  // arenas are backed up before the pass so that an overflow (match output, K_part tables, K_gen
-  // pools) can be undone and the push re-run exactly at the grown capacity. The benchmark mode
-  // (SDH_FLAG_DEVICE_MATCHES: records wrap in a ring, nothing is polled) skips the copy unless K_part
-  // tables are present; there a K_gen pool overflow fails the push loudly (SDH_E_CAPACITY)
-  bool backed = (write || !e->psets.empty() || !e->ssets.empty()) && gen_backup(e);
+  // the blocks a pass modifies are journaled so that an overflow (match output, K_part tables, K_gen
+  // pools, K_slab space) can be undone and the push re-run exactly at the grown capacity. The
+  // benchmark mode (SDH_FLAG_DEVICE_MATCHES: records wrap in a ring, nothing is polled) skips it
+  // unless K_part / K_slab sets are present; there a K_gen pool overflow fails the push loudly
+  e->g_journal = write || !e->psets.empty() || !e->ssets.empty();
+  for (auto& up : e->gsets) up->jn = 0;
   for (auto& ss : e->ssets) slab_prepare(e, *ss);
   const size_t nss = e->ssets.size();
   std::vector<int32_t> serr(4 * std::max<size_t>(1, nss), 0);
@@ -2628,13 +2624,13 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     }
     kg::Sizing grown;
     const bool pools_over = errs[0] != 0 && gen_grown_sizing(e, errs[0], &grown);
-    if ((out_over || part_over || pools_over || slab_over) && backed && attempt < 24 && (!errs[0] || pools_over) &&
-        !errs[1] && !errs[3]) {
-      // undo the pass (K_gen arenas from the backup; K_part tables are double-buffered and their
+    if ((out_over || part_over || pools_over || slab_over) && e->g_journal && attempt < 24 &&
+        (!errs[0] || pools_over) && !errs[1] && !errs[3]) {
+      // undo the pass (K_gen blocks from the journal; K_part tables are double-buffered and their
       // per-key selectors are swapped only after success) and re-run it with room for every match
       // record (out_next counts the words every record asked for), every K_part partial and the
       // K_gen pools / lists that overflowed
-      gen_restore_backup(e);
+      gen_restore_journal(e);
       for (size_t i = 0; i < nss; ++i) {
         auto& ss = *e->ssets[i];
         std::vector<int64_t> demand(ss.nsub, 0);
@@ -2652,9 +2648,8 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
         if (serr[4 * i + 1]) slab_prepare(e, ss, &demand);  // a ring ran out of room: reclaim / grow
       }
       if (pools_over) {
-        gen_relayout(e, grown, true);
+        gen_relayout(e, grown, true);  // (the next pass journals its blocks in the new layout)
         ++e->gen_regrows;
-        backed = gen_backup(e);  // the pre-push state in the new layout
       }
       if (out_over)
         while (e->g_out_cap < (int64_t)used + (int64_t)used / 4 + GEN_RING_MARGIN) e->g_out_cap *= 2;
@@ -2668,6 +2663,8 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     }
     if (part_over)
       throw Error(SDH_E_CAPACITY, "K_part partial table overflow (no room for an exact re-run)");
+    if (out_over)
+      throw Error(SDH_E_CAPACITY, "K_gen match output overflow (no room for an exact re-run)");
     if (slab_over) throw Error(SDH_E_CAPACITY, "K_slab capacity (no room for an exact re-run)");
     break;
   }
@@ -2705,17 +2702,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   *bytes_out += (double)nrec * 32.0;  // one (query, ts, seqs) record per match, as for K_ratchet
   e->stats.matches += (int64_t)nrec;
   e->g_dev_matches = (int64_t)nrec;
-  e->g_used = 0;
-  if (errs[2]) {
-    // the instances have consumed the batch (their arenas advance in place), so the push is
-    // committed and only the records that did not fit are lost; do_push reports it after the
-    // commit, and the next push gets a buffer that holds this one's records
-    while (e->g_out_cap < (int64_t)used + (int64_t)used / 2) e->g_out_cap *= 2;
-    e->g_out_lost = true;
-    e->g_dev_matches = 0;
-    return;
-  }
-  if (write) e->g_used = (int64_t)used;
+  e->g_used = write ? (int64_t)used : 0;
 }
 
 // Host-resident batch -> HBM (the StreamJunction -> receiver hand-off of north_star (2)): the
@@ -2789,6 +2776,36 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     throw Error(SDH_E_INVALID, "batch larger than max_batch");
   if (b->n == 0) return SDH_OK;
   HIPCHK(hipSetDevice(e->dev));
+  // an exact re-run needs the journal of the K_gen blocks the push modifies (gen_journal): a batch
+  // whose bound does not fit a third of free HBM is pushed as two halves -- the same events in the
+  // same order, so the same matches
+  const bool journaled = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) == 0 || !e->psets.empty() || !e->ssets.empty();
+  if (!e->gsets.empty() && journaled && b->n > 1) {
+    size_t fr = 0, tot = 0;
+    const char* jb = getenv("SDH_JOURNAL_BUDGET");  // (tests: force the split)
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && gen_journal_bound(e, b->n) > (jb ? atof(jb) : (double)fr / 3)) {
+      std::vector<const void*> c0(na), c1(na);
+      std::vector<const uint8_t*> n0(na), n1(na);
+      const int64_t h = b->n / 2;
+      for (int a = 0; a < na; ++a) {
+        c0[a] = b->cols[a];
+        c1[a] = (const uint8_t*)b->cols[a] + h * attr_width(types[a]);
+        n0[a] = b->nulls ? b->nulls[a] : nullptr;
+        n1[a] = (b->nulls && b->nulls[a]) ? b->nulls[a] + h : nullptr;
+      }
+      sdh_batch first = *b, second = *b;
+      first.n = h;
+      first.cols = c0.data();
+      first.nulls = b->nulls ? n0.data() : nullptr;
+      second.n = b->n - h;
+      second.ts = b->ts + h;
+      second.cols = c1.data();
+      second.nulls = b->nulls ? n1.data() : nullptr;
+      do_push(e, stream, &first);
+      return do_push(e, stream, &second);
+    }
+  }
+  (void)hipGetLastError();
   StreamBatch B{};
   B.n = b->n;
   B.n_attr = na;
@@ -2831,7 +2848,6 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   e->r_matches = 0;
   e->g_dev_matches = 0;
   e->g_used = 0;
-  e->g_out_lost = false;
   for (auto& k : e->part_kept) k = b->n;
   try {
     if (!qs.empty()) {
@@ -2887,16 +2903,13 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     const bool only_ratchet = e->device_matches == 0 && e->g_dev_matches == 0;
     const bool placeable = only_ratchet && (e->mt.n == 0 || e->mt.placed);
     if (!(only_ratchet && e->r_matches == 0) &&
-        !(placeable && place_ratchet(e, B.ts, B.seq_base, b->n, stream))) {
+        !(placeable && place_ratchet(e, B.ts, B.seq_base, b->n))) {
       placed_to_table(e);
       append_chain(e);
       append_ratchet(e, B.ts, B.seq_base);
       append_gen(e);
     }
   }
-  if (e->g_out_lost)
-    throw Error(SDH_E_CAPACITY, "K_gen match output overflow: the push was applied but its K_gen matches were "
-                                "lost (the output buffer has grown for the next push)");
   return SDH_OK;
 }
 
@@ -3055,7 +3068,6 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     ensure_state(e);
     ratchet_build(e, rplans);
     gen_build(e, gen_qs);
-    ratchet_place_plan(e);
     // R18 tables of the device match table: receiver rank per (query, stream), and per query its
     // state count and the stream of its last state (the trigger of a chain-plan match)
     const size_t nq_all = e->prog.q.size();
@@ -3138,7 +3150,6 @@ int sdh_engine_advance_time(sdh_engine* e, int64_t t) {
     e->r_matches = 0;
     e->g_dev_matches = 0;
     e->g_used = 0;
-    e->g_out_lost = false;
     double ms = 0, bytes = 0;
     e->advance_to = t;
     try {
@@ -3153,8 +3164,6 @@ int sdh_engine_advance_time(sdh_engine* e, int64_t t) {
       placed_to_table(e);
       append_gen(e);
     }
-    if (e->g_out_lost)
-      throw Error(SDH_E_CAPACITY, "K_gen match output overflow: the advance was applied but its matches were lost");
     return SDH_OK;
   });
 }

@@ -113,67 +113,77 @@ __global__ __launch_bounds__(256) void digest_ratchet_kernel(const int64_t* __re
 }
 
 // ---- K_ratchet direct R18 placement (a push whose matches all come from K_ratchet) ----
-// A block holds one wave's records (one group of 64 queries, lane = query) in emission order: events
-// ascending; for one event -- its run, kept in one block by the kernel's level-0 reserve -- by pop
-// level, each level's lanes ascending (ballot compaction), level 0 the newest partial. R18 wants per
-// event the queries in receiver-rank order and per query its partials in pending-list order (e1 seq
-// ascending = pop level descending). When a group's lanes are consecutive receiver ranks, record i
-// of a run goes to
-//   base[event][group position] + #{k in run: lane_k < lane_i} + #{k in run, k > i: lane_k == lane_i}
-// where base is the exclusive scan of the run lengths over (event, groups in rank order). Pass 1
-// stores the run lengths (a run key seen twice = a run split over blocks: the caller falls back to
-// the sort); pass 2 writes the ABI tuples in place: no sort, one read of the records, one write of
-// the outputs.
+// A block holds one wave's records (one group of up to 64 queries, one per lane) in emission order:
+// events ascending; for one event (its run) by pop level, each level's lanes ascending (ballot
+// compaction), level 0 the newest partial. A run may continue from the wave's previous block
+// (blk_prev). R18 wants per event the queries in receiver-rank order and per query its partials in
+// pending-list order (e1 seq ascending = pop level descending). Pass 1 adds, per (event, query
+// rank) cell, the query's records of each block's run; an exclusive scan over the cells gives each
+// cell's first row; pass 2 writes a record of level L (the lane's earlier records at that event, in
+// this block and in the wave's previous blocks) to
+//   row0 + base[cell] + count[cell] - 1 - L
+// as the ABI tuples, in place: no sort, one read of the records, one write of the outputs (plus the
+// count matrix: 4 B per (event, query) cell).
 constexpr int PLACE_RECS = 8192;  // block records a workgroup stages in LDS (the host checks blk_recs)
 
 template <bool PLACE>
 __global__ __launch_bounds__(256) void ratchet_place_kernel(
     const int64_t* __restrict__ match, int blk_recs, const int32_t* __restrict__ blk_count,
-    const int32_t* __restrict__ blk_group, const int32_t* __restrict__ gpos, int n_gpos, int32_t* __restrict__ cnt,
-    int32_t* __restrict__ split, const RatchetGroup* __restrict__ groups, const int64_t* __restrict__ ts,
-    int64_t seq_base, int64_t row0, int64_t* __restrict__ oq, int64_t* __restrict__ okey, int64_t* __restrict__ ots,
-    int64_t* __restrict__ oseq, int64_t* __restrict__ otb, int64_t* __restrict__ ooff, int64_t* __restrict__ owords) {
+    const int32_t* __restrict__ blk_group, const int32_t* __restrict__ blk_prev, int64_t rows,
+    const int32_t* __restrict__ out_rank, int n_streams, int n_ranks, int64_t cells, int32_t* __restrict__ cnt,
+    const RatchetGroup* __restrict__ groups, const int64_t* __restrict__ ts, int64_t seq_base, int64_t row0,
+    int64_t* __restrict__ oq, int64_t* __restrict__ okey, int64_t* __restrict__ ots, int64_t* __restrict__ oseq,
+    int64_t* __restrict__ otb, int64_t* __restrict__ ooff, int64_t* __restrict__ owords) {
   __shared__ uint32_t rx[PLACE_RECS];
   const int b = blockIdx.x;
   const int n = blk_count[b];
-  const int g = blk_group[b];
-  const int gp = gpos[g];
+  const RatchetGroup* G = groups + blk_group[b];
   const uint2* R = reinterpret_cast<const uint2*>(match) + (size_t)b * blk_recs;
   constexpr uint32_t OFF = (1u << 26) - 1;
   for (int i = threadIdx.x; i < n; i += blockDim.x) rx[i] = R[i].x;
   __syncthreads();
-  const RatchetGroup* G = groups + g;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const uint32_t x = rx[i], off = x & OFF, lane = x >> 26;
-    int lo = 0, hi = i;  // run start: first record of this event (records ascend by event)
+    int lo = 0, hi = i;  // run start: first record of this event in the block (records ascend by event)
     while (lo < hi) {
       const int m = (lo + hi) >> 1;
       if ((rx[m] & OFF) < off) lo = m + 1;
       else hi = m;
     }
     const int a = lo;
-    hi = n;
-    lo = i + 1;
-    while (lo < hi) {
-      const int m = (lo + hi) >> 1;
-      if ((rx[m] & OFF) <= off) lo = m + 1;
-      else hi = m;
-    }
-    const int z = lo;  // one past the run
-    const int64_t cell = (int64_t)off * n_gpos + gp;
+    const int q = G->qid[lane];
+    const int64_t cell = (int64_t)off * n_ranks + (out_rank[(int64_t)q * n_streams + G->stream] - 1);
     if constexpr (!PLACE) {
-      if (i == a && atomicAdd(&cnt[cell], z - a) != 0) atomicOr(split, 1);
-    } else {
-      int p = 0;
-      for (int k = a; k < z; ++k) {
-        const uint32_t lk = rx[k] >> 26;
-        p += (lk < lane || (k > i && lk == lane)) ? 1 : 0;
+      bool last = true;  // the lane's last record of the run in this block adds the block's count
+      int c = 0;
+      for (int k = a; k < n && (rx[k] & OFF) == off; ++k) {
+        const bool same = (rx[k] >> 26) == lane;
+        c += same ? 1 : 0;
+        if (k > i && same) last = false;
       }
-      const int64_t P = row0 + (int64_t)cnt[cell] + p;
+      if (last) atomicAdd(&cnt[cell], c);
+    } else {
+      int level = 0;  // the lane's records at this event emitted before this one
+      for (int k = a; k < i; ++k) level += (rx[k] >> 26) == lane ? 1 : 0;
+      if (a == 0) {  // the run may have begun in the wave's previous block(s)
+        for (int pb = blk_prev[b]; pb >= 0; pb = blk_prev[pb]) {
+          const uint2* PR = reinterpret_cast<const uint2*>(match) + (size_t)pb * blk_recs;
+          int k = blk_count[pb] - 1;
+          for (; k >= 0; --k) {
+            const uint32_t y = PR[k].x;
+            if ((y & OFF) != off) break;
+            level += (y >> 26) == lane ? 1 : 0;
+          }
+          if (k >= 0) break;  // the run began in that block
+        }
+      }
+      const int64_t base = cnt[cell], next = cell + 1 < cells ? (int64_t)cnt[cell + 1] : rows;
+      const int64_t P = row0 + next - 1 - level;
+      (void)base;
       const uint32_t q1 = R[i].y;
       const int64_t s = seq_base + (int64_t)off;
       const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
-      oq[P] = G->qid[lane];
+      oq[P] = q;
       okey[P] = -1;
       ots[P] = ts[off];
       oseq[P] = s;
@@ -363,40 +373,35 @@ extern "C" hipError_t sdh_digest_ratchet(const int64_t* match, int blk_recs, int
 }
 
 // Direct R18 placement of the last push's K_ratchet blocks at rows row0.. of the ABI outputs (see
-// ratchet_place_kernel). cnt: n_events * n_gpos int32 (zeroed here; scanned in place). Returns
-// hipErrorNotSupported, with nothing written, when a run split over two blocks (use the sort).
+// ratchet_place_kernel). cnt: n_events * n_ranks int32 (zeroed here, scanned in place).
 extern "C" size_t sdh_place_temp_bytes(int64_t cells) {
   size_t b = 0;
   (void)hipcub::DeviceScan::ExclusiveSum((void*)nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, (int)cells);
   return b + 256;
 }
 extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, const int32_t* blk_count,
-                                        const int32_t* blk_group, int n_blocks, const int32_t* gpos, int n_gpos,
-                                        int64_t n_events, int32_t* cnt, int32_t* flag, void* temp, size_t temp_bytes,
-                                        const sdh::RatchetGroup* groups, const int64_t* ts, int64_t seq_base,
-                                        int64_t row0, int64_t* oq, int64_t* okey, int64_t* ots, int64_t* oseq,
-                                        int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s) {
+                                        const int32_t* blk_group, const int32_t* blk_prev, int n_blocks,
+                                        int64_t rows, const int32_t* out_rank, int n_streams, int n_ranks,
+                                        int64_t n_events, int32_t* cnt, int32_t* flag, void* temp,
+                                        size_t temp_bytes, const sdh::RatchetGroup* groups, const int64_t* ts,
+                                        int64_t seq_base, int64_t row0, int64_t* oq, int64_t* okey, int64_t* ots,
+                                        int64_t* oseq, int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s) {
   using namespace sdh;
+  (void)flag;
   if (n_blocks <= 0) return hipSuccess;
   if (blk_recs > PLACE_RECS) return hipErrorNotSupported;
-  const int64_t cells = n_events * n_gpos;
+  const int64_t cells = n_events * n_ranks;
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)cells * 4, s);
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(flag, 0, 4, s);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(ratchet_place_kernel<false>, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, blk_count, blk_group,
-                     gpos, n_gpos, cnt, flag, groups, ts, seq_base, row0, oq, okey, ots, oseq, otb, ooff, owords);
-  int32_t split = 0;
-  e = hipMemcpyAsync(&split, flag, 4, hipMemcpyDeviceToHost, s);
-  if (e != hipSuccess) return e;
-  e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return e;
-  if (split) return hipErrorNotSupported;
+                     blk_prev, rows, out_rank, n_streams, n_ranks, cells, cnt, groups, ts, seq_base, row0, oq, okey,
+                     ots, oseq, otb, ooff, owords);
   size_t tb = temp_bytes;
   e = hipcub::DeviceScan::ExclusiveSum(temp, tb, cnt, cnt, (int)cells, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(ratchet_place_kernel<true>, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, blk_count, blk_group,
-                     gpos, n_gpos, cnt, flag, groups, ts, seq_base, row0, oq, okey, ots, oseq, otb, ooff, owords);
+                     blk_prev, rows, out_rank, n_streams, n_ranks, cells, cnt, groups, ts, seq_base, row0, oq, okey,
+                     ots, oseq, otb, ooff, owords);
   return hipGetLastError();
 }
 

@@ -216,6 +216,44 @@ __global__ void seq_tail_kernel(StreamBatch b, int64_t* tail, int32_t tail_len, 
   }
 }
 
+// ---- exact re-runs: the arena blocks a pass is about to modify, journaled just before it runs ----
+// Slot x journals block: mode 0, glist[x] (an unpartitioned set's groups); mode 1, seg_kid[x /
+// groups] * groups + x % groups (a partition's key segments; dropped events have no block); mode 2,
+// x (a timer sweep over every known key). restore != 0 copies the journaled blocks back.
+__global__ void gen_journal_kernel(int32_t* __restrict__ a32, int64_t* __restrict__ a64, int64_t B32, int64_t B64,
+                                   int mode, const int32_t* __restrict__ glist, const uint32_t* __restrict__ seg_kid,
+                                   int groups, int32_t* __restrict__ j32, int64_t* __restrict__ j64,
+                                   int64_t* __restrict__ jidx, int restore) {
+  const int64_t x = blockIdx.x;
+  int64_t b;
+  if (restore) {
+    b = jidx[x];
+  } else {
+    if (mode == 0) {
+      b = glist[x];
+    } else if (mode == 1) {
+      const uint32_t kid = seg_kid[x / groups];
+      b = kid == 0xFFFFFFFFu ? -1 : (int64_t)kid * groups + x % groups;
+    } else {
+      b = x;
+    }
+    if (threadIdx.x == 0) jidx[x] = b;
+  }
+  if (b < 0) return;
+  int32_t* s32 = a32 + b * B32 * 64;
+  int32_t* d32 = j32 + x * B32 * 64;
+  int64_t* s64 = a64 + b * B64 * 64;
+  int64_t* d64 = j64 + x * B64 * 64;
+  for (int64_t i = threadIdx.x; i < B32 * 64; i += blockDim.x) {
+    if (restore) s32[i] = d32[i];
+    else d32[i] = s32[i];
+  }
+  for (int64_t i = threadIdx.x; i < B64 * 64; i += blockDim.x) {
+    if (restore) s64[i] = d64[i];
+    else d64[i] = s64[i];
+  }
+}
+
 // ---- live partials (sdh_engine_stats): entries of the pending lists of non-start states ----
 __device__ __forceinline__ void acc_wave(unsigned long long v, unsigned long long* acc) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
@@ -452,6 +490,15 @@ extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, hipStream_t s) {
 }
 
 // roll a stream's K_seq tail over batch b (after the push's K_seq launches have succeeded)
+extern "C" hipError_t sdh_gen_journal(int32_t* a32, int64_t* a64, int64_t B32, int64_t B64, int mode,
+                                       const int32_t* glist, const uint32_t* seg_kid, int groups, int64_t slots,
+                                       int32_t* j32, int64_t* j64, int64_t* jidx, int restore, hipStream_t s) {
+  if (slots <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::gen_journal_kernel, dim3((unsigned)slots), dim3(256), 0, s, a32, a64, B32, B64, mode, glist,
+                     seg_kid, groups, j32, j64, jidx, restore);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t sdh_live_gen(const int32_t* a32, int64_t B32, int64_t blocks, int n_groups, int group_base,
                                     const int32_t* lane_q, const int32_t* group_seq, const sdh::kg::GQuery* queries,
                                     unsigned long long* acc, hipStream_t s) {

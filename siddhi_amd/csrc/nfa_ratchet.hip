@@ -714,15 +714,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
   uint2* wb = nullptr;            // the wave's current output block
   int64_t prev_tile_ts = (W.c0 == 0) ? L.b.prev_ts : L.b.ts[W.c0 - 1];
 
-  // one record per lane with `mt` (ballot m): per-wave output blocks (one atomic per block), ranks
-  // by mbcnt. e2 = batch event `off`; e1 = the partial with low seq bits q1. The common case costs
-  // one compare-and-branch of bookkeeping (the record index is block base + fill + rank). An event's
-  // first emit (level 0) switches blocks unless four levels of a full wave fit, so one event's
-  // records of a wave stay in one block (the poll's direct R18 placement, matches.hip, relies on
-  // it and falls back to the sort when a longer run splits).
-  auto emit = [&](bool mt, uint64_t m, uint32_t off, uint32_t q1, bool first) {
+  // one record per lane with `mt` (ballot m): per-wave output blocks (one atomic per block, chained
+  // to the wave's previous block for the direct R18 placement, matches.hip), ranks by mbcnt. e2 =
+  // batch event `off`; e1 = the partial with low seq bits q1. The common case costs one
+  // compare-and-branch of bookkeeping (the record index is block base + fill + rank).
+  auto emit = [&](bool mt, uint64_t m, uint32_t off, uint32_t q1) {
     const int c = __popcll(m);
-    if (fill + (first ? 4 * WAVE : c) > L.blk_recs) {
+    if (fill + c > L.blk_recs) {
       if (mover) return;
       if (blk >= 0) {
         if (lane == 0) L.blk_count[blk] = fill;
@@ -738,7 +736,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
         fill = FULL_FILL;
         return;
       }
-      if (lane == 0) L.blk_group[nb] = W.g;
+      if (lane == 0) {
+        L.blk_group[nb] = W.g;
+        L.blk_prev[nb] = blk;
+      }
       blk = nb;
       fill = 0;
       wb = reinterpret_cast<uint2*>(L.match) + ((size_t)blk * L.blk_recs << (L.wide ? 1 : 0));
@@ -826,15 +827,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
         const bool c2 = c1 && D.ln > 2 && xop<KK, XM>(xmask, x, k2);
         const bool c3 = c2 && D.ln > 3 && xop<KK, XM>(xmask, x, k3);
         const uint32_t off = (uint32_t)(t + k);
-        emit(mt, m, off, tseq, true);
+        emit(mt, m, off, tseq);
         const uint64_t m1 = __ballot(c1);
         if (m1) {
-          emit(c1, m1, off, q1, false);
+          emit(c1, m1, off, q1);
           const uint64_t m2 = __ballot(c2);
           if (m2) {
-            emit(c2, m2, off, q2, false);
+            emit(c2, m2, off, q2);
             const uint64_t m3 = __ballot(c3);
-            if (m3) emit(c3, m3, off, q3, false);
+            if (m3) emit(c3, m3, off, q3);
           }
         }
         const int p = (int)mt + (int)c1 + (int)c2 + (int)c3;

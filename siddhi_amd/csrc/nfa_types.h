@@ -201,6 +201,7 @@ struct RatchetLaunch {
   int64_t* match;
   int32_t* blk_count;           // records written per block
   int32_t* blk_group;           // group of the wave that owns the block
+  int32_t* blk_prev;            // the wave's previous block (-1: its first), for the direct R18 placement
   int32_t* blk_next;            // [0] next free block
   int32_t n_blocks, blk_recs;
   int32_t wide;

@@ -157,12 +157,26 @@ class StreamIR:
 
 
 @dataclass
+class ChainIR:
+    """A plain query over a pattern query's inner-stream output (``from #X[f] select ... insert into
+    Y`` inside the partition): part of the host selector (selector.stream_rows), not of the device
+    program. Its expressions read the one-event row of #X (slot 0)."""
+    name: str
+    input: str                  # '#X'
+    input_types: List[int]      # #X's schema: the producing query's output types
+    filters: List[List[Insn]]
+    outputs: List[OutputIR]     # empty: select *
+    output_stream: str
+
+
+@dataclass
 class ProgramIR:
     name: str
     streams: List[StreamIR]
     strings: List[str]
     queries: List[QueryIR]
     partitions: List[PartitionIR]
+    chains: List[ChainIR] = field(default_factory=list)
 
     def stream_index(self, name: str) -> int:
         for i, s in enumerate(self.streams):

@@ -36,7 +36,7 @@ from .ir import (AR_CODE, CMP_CODE, INT_MAX, K_ABSENT, K_COUNT, K_LOGICAL, K_STR
                  N_EVERY, N_LOGICAL, N_NEXT, N_STREAM, OP_AND, OP_ARITH, OP_ATTR, OP_CMP, OP_CONST,
                  OP_IS_NULL, OP_NOT, OP_OR, OP_STREAM_IS_NULL, Q_PATTERN, Q_SEQUENCE, R_MULTI,
                  R_SINGLE, T_BOOL, T_DOUBLE, T_FLOAT, T_INT, T_LONG, T_STRING, TYPE_CODE, Insn,
-                 NodeIR, OutputIR, PartitionIR, PartitionKeyIR, ProgramIR, QueryIR, ReceiverIR,
+                 ChainIR, NodeIR, OutputIR, PartitionIR, PartitionKeyIR, ProgramIR, QueryIR, ReceiverIR,
                  StateIR, StreamIR)
 from .ql import SiddhiAppCreationException
 
@@ -364,13 +364,194 @@ class _QueryPlanner:
                        partition_idx=self.partition_idx, output_stream=self.q.output_stream or "")
 
 
+# ---- inner streams (`#X`, partition-local) on the pattern path ----------------------------------
+# (1) A projection feeding a pattern: `from S[f] select a, b as c insert into #X` with S a partitioned
+#     stream, read by pattern states `e=#X[g]`. The inner stream carries exactly the S events that
+#     pass f, delivered while the projection query processes them (PartitionRuntime.clonePartition
+#     subscribes the local junction #X+key; QueryRuntime -> InsertIntoStreamCallback), so the state is
+#     the same state over S with filter f AND g and #X's attribute names mapped back to S's: the fold
+#     rewrites the pattern's AST and the device never sees #X. R18 order is unchanged when no other
+#     query of the partition reads S (the pattern then receives S events at the projection's place).
+# (2) A selector chain over a pattern's output: the pattern inserts its rows into #X and plain
+#     queries `from #X[f] select ... insert into Y` re-project them (ChainIR, applied by the host
+#     selector in match order: each row passes through the chain when its match is delivered).
+def _walk_expr(e, fn):
+    e = fn(e)
+    if isinstance(e, ql.IsNull):
+        return ql.IsNull(_walk_expr(e.expr, fn))
+    if isinstance(e, ql.Not):
+        return ql.Not(_walk_expr(e.expr, fn))
+    if isinstance(e, ql.BinOp):
+        return ql.BinOp(e.op, _walk_expr(e.left, fn), _walk_expr(e.right, fn))
+    return e
+
+
+def _fold_projection(q: ql.Query, folds: dict) -> ql.Query:
+    """Pattern query q with its states over folded inner streams rewritten onto their source streams."""
+    import copy
+    q = copy.deepcopy(q)
+    alias_map = {}  # alias of a folded state -> {#X attribute: S attribute}
+
+    def amap_of(p):
+        if p.select is None:
+            return None
+        return {(oa.rename or oa.expr.attr): oa.expr.attr for oa in p.select}
+
+    def rename_own(amap):
+        def fn(e):
+            if isinstance(e, ql.Var) and e.stream_ref is None and amap is not None:
+                return ql.Var(None, e.index, amap.get(e.attr, e.attr))
+            return e
+        return fn
+
+    def fix_stream(se: ql.StreamSE):
+        p = folds.get(se.stream)
+        if p is None:
+            if se.stream.startswith("#"):
+                raise SiddhiAppCreationException(f"inner stream '{se.stream}' has no projection to fold")
+            return se
+        amap = amap_of(p)
+        if se.alias is not None:
+            alias_map[se.alias] = amap
+        own = [_walk_expr(f, rename_own(amap)) for f in se.filters]
+        return ql.StreamSE(se.alias, p.stream, list(p.filters) + own)
+
+    def fix_elem(e):
+        if isinstance(e, ql.StreamSE):
+            return fix_stream(e)
+        if isinstance(e, ql.AbsentSE):
+            return ql.AbsentSE(fix_stream(e.stream), e.waiting_ms)
+        if isinstance(e, ql.NextSE):
+            return ql.NextSE(fix_elem(e.first), fix_elem(e.next))
+        if isinstance(e, ql.EverySE):
+            return ql.EverySE(fix_elem(e.inner))
+        if isinstance(e, ql.LogicalSE):
+            return ql.LogicalSE(e.type, fix_elem(e.s1), fix_elem(e.s2))
+        if isinstance(e, ql.CountSE):
+            return ql.CountSE(fix_stream(e.stream), e.min, e.max)
+        raise SiddhiAppCreationException(f"unsupported state element {e!r}")
+
+    q.input.element = fix_elem(q.input.element)
+
+    def rename_ref(e):
+        if isinstance(e, ql.Var) and e.stream_ref in alias_map and alias_map[e.stream_ref] is not None:
+            return ql.Var(e.stream_ref, e.index, alias_map[e.stream_ref].get(e.attr, e.attr))
+        return e
+
+    def fix_refs(e):
+        if isinstance(e, (ql.StreamSE,)):
+            e.filters = [_walk_expr(f, rename_ref) for f in e.filters]
+        elif isinstance(e, ql.AbsentSE):
+            fix_refs(e.stream)
+        elif isinstance(e, ql.NextSE):
+            fix_refs(e.first)
+            fix_refs(e.next)
+        elif isinstance(e, ql.EverySE):
+            fix_refs(e.inner)
+        elif isinstance(e, ql.LogicalSE):
+            fix_refs(e.s1)
+            fix_refs(e.s2)
+        elif isinstance(e, ql.CountSE):
+            fix_refs(e.stream)
+
+    fix_refs(q.input.element)
+    if q.select is not None:
+        renamed = any(m is not None and any(k != v for k, v in m.items()) for m in alias_map.values())
+        for oa in q.select:
+            if renamed and any(isinstance(x, ql.Var) and x.stream_ref is None for x in _vars(oa.expr)):
+                raise SiddhiAppCreationException("unqualified attribute over a renamed inner stream")
+            oa.expr = _walk_expr(oa.expr, rename_ref)
+    return q
+
+
+def _vars(e):
+    out = []
+    _walk_expr(e, lambda x: (out.append(x), x)[1])
+    return out
+
+
+def _state_streams(e, acc):
+    if isinstance(e, ql.StreamSE):
+        acc.append(e.stream)
+    elif isinstance(e, ql.AbsentSE):
+        acc.append(e.stream.stream)
+    elif isinstance(e, ql.NextSE):
+        _state_streams(e.first, acc)
+        _state_streams(e.next, acc)
+    elif isinstance(e, ql.EverySE):
+        _state_streams(e.inner, acc)
+    elif isinstance(e, ql.LogicalSE):
+        _state_streams(e.s1, acc)
+        _state_streams(e.s2, acc)
+    elif isinstance(e, ql.CountSE):
+        acc.append(e.stream.stream)
+    return acc
+
+
+def _plan_inner_streams(app: ql.App, part: ql.Partition, part_streams: set):
+    """(pattern queries with folded projections, plain chain queries) of one partition."""
+    pattern = [q for q in part.queries if isinstance(q, ql.Query)]
+    plain = [q for q in part.queries if isinstance(q, ql.PlainQuery)]
+    producers = {}
+    for q in part.queries:
+        if q.output_stream and q.output_stream.startswith("#"):
+            producers.setdefault(q.output_stream, []).append(q)
+    folds, chains = {}, []
+    for p in plain:
+        if p.stream.startswith("#"):
+            if not all(isinstance(x, ql.Query) for x in producers.get(p.stream, [])) or p.stream not in producers:
+                raise SiddhiAppCreationException(f"inner stream '{p.stream}' must be a pattern query's output")
+            chains.append(p)
+        elif p.output_stream and p.output_stream.startswith("#") and p.stream in part_streams:
+            if len(producers[p.output_stream]) != 1:
+                raise SiddhiAppCreationException(f"inner stream '{p.output_stream}' has several producers")
+            if p.select is not None and not all(isinstance(oa.expr, ql.Var) and oa.expr.stream_ref is None and
+                                                oa.expr.index is None for oa in p.select):
+                raise SiddhiAppCreationException("only attribute projections feed a pattern through an inner stream")
+            folds[p.output_stream] = p
+        else:
+            raise SiddhiAppCreationException("plain stream queries are outside the accelerated path")
+    for x, p in folds.items():
+        readers = [q for q in pattern if p.stream in _state_streams(q.input.element, [])]
+        readers += [c for c in plain if c is not p and c.stream == p.stream]
+        if readers:
+            raise SiddhiAppCreationException(f"stream '{p.stream}' feeds a pattern both directly and through '{x}'")
+        if any(c.stream == x for c in chains):
+            raise SiddhiAppCreationException(f"inner stream '{x}' feeds both a pattern and a plain query")
+    return [_fold_projection(q, folds) if folds else q for q in pattern], chains
+
+
+def _plan_chain(pb: "_ProgramBuilder", c: ql.PlainQuery, src: QueryIR) -> ChainIR:
+    """A plain query over the inner stream `src` writes: compiled against #X's schema (src's outputs)."""
+    rev = {v: k for k, v in TYPE_CODE.items()}
+    sd = ql.StreamDef(c.stream, [(o.name, rev[o.type]) for o in src.outputs])
+    comp = _ExprCompiler(pb, [(None, sd)], 0, CURRENT)
+    filters = []
+    for f in c.filters:
+        code, t = comp.compile(f)
+        if t != T_BOOL:
+            raise SiddhiAppCreationException("filter expression must return BOOL")
+        filters.append(code)
+    outputs = []
+    for oa in c.select or []:
+        code, t = comp.compile(oa.expr)
+        nm = oa.rename or (oa.expr.attr if isinstance(oa.expr, ql.Var) else None)
+        if nm is None:
+            raise SiddhiAppCreationException("output attribute needs a name ('as')")
+        outputs.append(OutputIR(nm, t, code))
+    return ChainIR(c.name, c.stream, [o.type for o in src.outputs], filters, outputs, c.output_stream or "")
+
+
 def plan(app: ql.App) -> ProgramIR:
     """Lower a parsed app to the pattern IR."""
     pb = _ProgramBuilder(app)
     queries: List[QueryIR] = []
     partitions: List[PartitionIR] = []
+    chains: List[ChainIR] = []
     for kind, obj in app.order:
         if kind == "query":
+            if isinstance(obj, ql.PlainQuery):
+                raise SiddhiAppCreationException("plain stream queries are outside the accelerated path")
             queries.append(_QueryPlanner(pb, obj, -1).build())
         else:
             pidx = len(partitions)
@@ -391,7 +572,8 @@ def plan(app: ql.App) -> ProgramIR:
             if len(kclass) > 1:
                 raise SiddhiAppCreationException("mixed-type partition keys are not supported")
             qidx = []
-            for q in obj.queries:
+            pattern_qs, chain_qs = _plan_inner_streams(app, obj, part_streams)
+            for q in pattern_qs:
                 qp = _QueryPlanner(pb, q, pidx)
                 qir = qp.build()
                 for st in qir.states:
@@ -400,12 +582,17 @@ def plan(app: ql.App) -> ProgramIR:
                             "non-partitioned streams inside a partition are not on the accelerated path")
                 qidx.append(len(queries))
                 queries.append(qir)
+            for c in chain_qs:
+                src = [queries[i] for i in qidx if queries[i].output_stream == c.stream]
+                chains.append(_plan_chain(pb, c, src[0]))
+                if any([o.type for o in s.outputs] != chains[-1].input_types for s in src[1:]):
+                    raise SiddhiAppCreationException(f"producers of '{c.stream}' disagree on its schema")
             partitions.append(PartitionIR(keys, qidx))
     names = [q.name for q in queries]
     if len(set(names)) != len(names):
         raise SiddhiAppCreationException("duplicate query names")
     return ProgramIR(name=app.name, streams=pb.streams, strings=pb.strings, queries=queries,
-                     partitions=partitions)
+                     partitions=partitions, chains=chains)
 
 
 def compile_app(src: str) -> ProgramIR:

@@ -158,6 +158,20 @@ class Query:
 
 
 @dataclass
+class PlainQuery:
+    """``from S[f] select ... insert into T`` (no state element). Only the inner-stream forms that
+    chain to the pattern path are planned (planner.py): a projection feeding a pattern's state
+    (folded into the state on the device) and a selector chain over a pattern's inner-stream
+    output (host selector, selector.py)."""
+    name: str
+    stream: str                          # '#X' for an inner stream
+    filters: List[object]
+    select: Optional[List[OutputAttr]]   # None == select *
+    output_stream: Optional[str]
+    annotations: dict = field(default_factory=dict)
+
+
+@dataclass
 class PartitionKey:
     expr: object
     stream: str
@@ -405,8 +419,13 @@ class Parser:
         return Partition(keys, qs)
 
     # query -----------------------------------------------------------------------------------
-    def query(self, anns: dict) -> Query:
+    def query(self, anns: dict):
         self.expect("from")
+        start = self.i
+        plain = self._plain_source()
+        if plain is not None:
+            return self._plain_query(anns, plain)
+        self.i = start
         inp = self.state_input()
         select = None
         if self.accept("select"):
@@ -445,6 +464,49 @@ class Parser:
         self.query_counter += 1
         name = anns.get("info.name") or f"query_{self.query_counter}"
         return Query(name=name, input=inp, select=select, output_stream=out, annotations=anns)
+
+    def _plain_source(self):
+        """A plain stream source (no alias, no state operator), or None."""
+        if self.peek().kind in ("id", "kw") and self.at("=", 1):
+            return None
+        if self.at("every") or self.at("not") or self.at("("):
+            return None
+        try:
+            se = self.std_source()
+        except SiddhiParserException:
+            return None
+        if not (self.at("select") or self.at("insert") or self.at("return")):
+            return None
+        return se
+
+    def _plain_query(self, anns: dict, se) -> "PlainQuery":
+        select = None
+        if self.accept("select"):
+            if not self.accept("*"):
+                select = []
+                while True:
+                    e = self.expression()
+                    rn = self.name() if self.accept("as") else None
+                    select.append(OutputAttr(e, rn))
+                    if not self.accept(","):
+                        break
+            for kw in ("group", "having", "order", "limit", "offset"):
+                if self.at(kw):
+                    self.error(f"'{kw}' is outside the accelerated path")
+        if self.at("output"):
+            self.error("output rate limiting is outside the accelerated path")
+        out = None
+        if self.accept("insert"):
+            if self.accept("all") or self.accept("expired") or self.accept("current"):
+                self.expect("events")
+            self.expect("into")
+            out = ("#" + self.name()) if self.accept("#") else self.name()
+        elif not self.accept("return"):
+            self.error("expected 'insert into' or 'return'")
+        self.query_counter += 1
+        name = anns.get("info.name") or f"query_{self.query_counter}"
+        return PlainQuery(name=name, stream=se.stream, filters=se.filters, select=select, output_stream=out,
+                          annotations=anns)
 
     def state_input(self) -> StateInput:
         start = self.i
@@ -613,9 +675,7 @@ class Parser:
         if self.peek().kind in ("id", "kw") and self.at("=", 1):
             alias = self.name()
             self.expect("=")
-        if self.accept("#"):
-            self.error("inner streams are outside the accelerated path")
-        stream = self.name()
+        stream = ("#" + self.name()) if self.accept("#") else self.name()
         filters = []
         while self.at("[") or self.at("#"):
             if self.at("#"):

@@ -170,3 +170,36 @@ def evaluate(code: List[Insn], slots: Sequence[Sequence[int]], log: EventLog, st
 def project(query_ir, match_slots, log: EventLog, stream_types, dictionary, strings):
     return [evaluate(o.code, match_slots, log, stream_types, dictionary, strings)
             for o in query_ir.outputs]
+
+
+def stream_rows(ir, matches, log: EventLog, dictionary, strings, stream: str) -> List[list]:
+    """Rows arriving on `stream` in delivery order: each match's projected row goes to its query's
+    output stream when the match is delivered (R18 order), and through every selector chain reading
+    that stream (ir.chains: plain queries over a pattern's inner-stream output, in definition order
+    -- the subscription order of StreamJunction.sendEvent:185-205), whose filters and projections see
+    the row as a one-event #X stream."""
+    from .events import encode_rows
+    by_input = {}
+    for c in getattr(ir, "chains", []):
+        by_input.setdefault(c.input, []).append(c)
+    out: List[list] = []
+
+    def deliver(row, types, target):
+        if target == stream:
+            out.append(row)
+        for c in by_input.get(target, []):
+            vals, nulls = encode_rows([row], types, dictionary)
+            one = EventLog()
+            one.append(-1, [0], vals, nulls)
+            if not all(evaluate(f, [[0]], one, None, dictionary, strings) is True for f in c.filters):
+                continue
+            if c.outputs:
+                deliver([evaluate(o.code, [[0]], one, None, dictionary, strings) for o in c.outputs],
+                        [o.type for o in c.outputs], c.output_stream)
+            else:
+                deliver(list(row), types, c.output_stream)
+
+    for m in matches:
+        q = ir.queries[m[0]]
+        deliver(project(q, m[3], log, None, dictionary, strings), [o.type for o in q.outputs], q.output_stream)
+    return out

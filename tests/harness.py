@@ -16,7 +16,7 @@ from siddhi_amd import ql
 from siddhi_amd.events import EventLog, StringDictionary, encode_rows
 from siddhi_amd.ir import T_BOOL, T_DOUBLE, T_FLOAT, T_INT, T_LONG, T_STRING
 from siddhi_amd.planner import plan
-from siddhi_amd.selector import project
+from siddhi_amd.selector import project, stream_rows
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
@@ -193,12 +193,7 @@ class App:
                 for m in self.matches if m[0] == qi]
 
     def rows_for_stream(self, stream: str):
-        out = []
-        for m in self.matches:
-            q = self.ir.queries[m[0]]
-            if q.output_stream == stream:
-                out.append(project(q, m[3], self.log, None, self.dictionary, self.ir.strings))
-        return out
+        return stream_rows(self.ir, self.matches, self.log, self.dictionary, self.ir.strings, stream)
 
 
 def values_equal(expected_tok: str, actual) -> bool:

@@ -430,3 +430,30 @@ def test_gen_output_overflow_reruns_exactly():
         om = o.engine.take_matches(lambda q: 2)
         gm = g.engine.take_matches(lambda q: 2)
         assert gm == om and len(om) > 100000
+
+
+def test_journal_budget_splits_the_push_exactly():
+    """The K_gen journal (the blocks a pass modifies, saved so that an overflow re-runs exactly) must
+    fit a third of free HBM; a push whose bound does not is split into halves. With the budget forced
+    to nothing (SDH_JOURNAL_BUDGET) every push of a partitioned K_gen app splits down to single
+    events, and with tiny pools every one of those re-runs from the journal: the matches equal the
+    oracle's."""
+    import os
+    from siddhi_amd.workloads import c3_app, stock_events
+    src = c3_app(12)
+    o = App(src)
+    g = hip_app(src, flags=SDH_FLAG_FORCE_GEN, gen_pool_states=2, gen_pool_nodes=4, gen_list_cap=2,
+                gen_max_keys=1024)
+    os.environ["SDH_JOURNAL_BUDGET"] = "1"
+    try:
+        for lo, n in ((0, 700), (700, 1300)):
+            ts, sym, price, vol = stock_events(lo, n, 40)
+            vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64), vol.astype(np.int64)], 1)
+            o.engine.send(0, ts, vals, None)
+            g.engine.push_columns(0, ts, [sym, price.view(np.uint32), vol])
+            om = o.engine.take_matches(lambda q: 3)
+            gm = g.engine.take_matches(lambda q: 3)
+            assert gm == om and len(om) > 50
+    finally:
+        del os.environ["SDH_JOURNAL_BUDGET"]
+    assert g.engine.stats().pool_regrows > 0

@@ -17,8 +17,6 @@ KAT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "referenc
 OUT_OF_SCOPE = {
     "CountPatternTestCase.testQuery14": "having",
     "PatternPartitionTestCase.testPatternPartitionQuery30": "non-partitioned stream in partition",
-    "PatternPartitionTestCase.testPatternPartitionQuery32": "inner stream",
-    "PatternPartitionTestCase.testPatternPartitionQuery33": "plain stream query",
     "IsNullTestCase.isNullTest1": "plain stream query (runs as a one-state pattern in test_filter_kat.py)",
 }
 
