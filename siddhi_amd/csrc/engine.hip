@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <tuple>
 #include <array>
 #include <cmath>
 #include <map>
@@ -55,9 +56,9 @@ extern "C" hipError_t sdh_gen_remap(const int32_t* lane_q, int group_base, int n
 
 extern "C" hipError_t sdh_launch_chain(int n_states, int k, const sdh::ChainLaunch* L, int n_blocks,
                                        size_t lds, hipStream_t s);
-extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int nf, int ML, int SC,
+extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int nf, int sim, int ML, int SC,
                                          const sdh::RatchetLaunch* L, hipStream_t s);
-extern "C" int sdh_ratchet_occupancy(int key_kind, int full, int nf, int ML);
+extern "C" int sdh_ratchet_occupancy(int key_kind, int full, int nf, int ML, int sim);
 extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::StreamBatch* B, int attr, int conv,
                                                  int64_t n_tiles, uint64_t* tmax, uint64_t* tmin, uint8_t* thas,
                                                  hipStream_t s);
@@ -1126,6 +1127,8 @@ void launch(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2
 // ------------------------------------------------------------------------------------------
 // K_ratchet host side
 // ------------------------------------------------------------------------------------------
+int ratchet_sim(const sdh::RatchetGroup& g);
+
 void ratchet_build(sdh_engine* e, std::vector<std::pair<RatchetPlan, int>>& plans) {
   std::stable_sort(plans.begin(), plans.end(), [](const auto& a, const auto& b) {
     const auto sa = a.first.sig(), sb = b.first.sig();
@@ -1146,6 +1149,7 @@ void ratchet_build(sdh_engine* e, std::vector<std::pair<RatchetPlan, int>>& plan
     g.xmask = P.xmask;
     g.n_f0 = (int)P.f0.size();
     for (int a = 0; a < g.n_f0; ++a) g.f0[a] = P.f0[a];
+    g.sim = ratchet_sim(g);
     g.wmax = -1;
     for (int l = 0; l < 64; ++l) {
       const size_t k = i + std::min<size_t>(l, j - i - 1);  // idle lanes mirror the last pattern
@@ -1222,6 +1226,17 @@ int ratchet_nf(const sdh::RatchetGroup& g) {
   return g.n_f0;
 }
 
+// the SIM form (nfa_ratchet.hip): float keys from a float column, one start atom over that same
+// column compared in the float / double domain against a constant, without negation
+int ratchet_sim(const sdh::RatchetGroup& g) {
+  if (getenv("SDH_RATCHET_NO_SIM")) return 0;
+  if (g.key_kind != sdh::KK_F32 || g.key_conv == sdh::CV_F32_INT || g.key_conv == sdh::CV_F32_LONG || g.n_f0 != 1)
+    return 0;
+  const sdh::RatchetAtom& A = g.f0[0];
+  return (A.attr == g.key_attr && !A.cur2 && A.f64 && (A.conv == sdh::CV_F32_FLOAT || A.conv == sdh::CV_F64_FLOAT) &&
+          !(A.mask & sdh::CM_NOT)) ? 1 : 0;
+}
+
 void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2]) {
   e->r_blocks_used = 0;
   e->r_matches = 0;
@@ -1255,18 +1270,18 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : 2048;
     e->ritems.clear();
     std::vector<int> order(gs);
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-      return std::make_pair(e->rg[a].key_kind, e->rg[a].xmask) < std::make_pair(e->rg[b].key_kind, e->rg[b].xmask);
-    });
+    // launches: one per (key kind, orientation, SIM form); SIM also needs the key column null-free
+    // in this batch
+    auto lsim = [&](int g) { return e->rg[g].sim && !B.nul[e->rg[g].key_attr] ? 1 : 0; };
+    auto lkey = [&](int g) { return std::make_tuple(e->rg[g].key_kind, e->rg[g].xmask, lsim(g)); };
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return lkey(a) < lkey(b); });
     for (size_t i0 = 0; i0 < order.size();) {
-      const RatchetGroup& G0 = e->rg[order[i0]];
       size_t i1 = i0;
       int nf = 0;
-      while (i1 < order.size() && e->rg[order[i1]].key_kind == G0.key_kind && e->rg[order[i1]].xmask == G0.xmask)
-        nf = std::max(nf, ratchet_nf(e->rg[order[i1++]]));
+      while (i1 < order.size() && lkey(order[i1]) == lkey(order[i0])) nf = std::max(nf, ratchet_nf(e->rg[order[i1++]]));
       double slots = e->r_waves;
       if (slots <= 0) {
-        const int occ = sdh_ratchet_occupancy(G0.key_kind, full, nf, e->rML);
+        const int occ = sdh_ratchet_occupancy(e->rg[order[i0]].key_kind, full, nf, e->rML, lsim(order[i0]));
         slots = (double)e->n_cu * std::max(1, occ);
       }
       const double len = std::max((double)min_chunk, (double)n * (double)(i1 - i0) / slots);
@@ -1351,9 +1366,10 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.err = e->d_err.p;
     HIPCHK(hipEventRecord(e->ev0, e->stream));
     for (int i0 = 0; i0 < n_items;) {
-      const int kk = e->rg[e->ritems[i0].g].key_kind, xm = e->rg[e->ritems[i0].g].xmask;
+      const int g0 = e->ritems[i0].g;
+      const int kk = e->rg[g0].key_kind, xm = e->rg[g0].xmask, sim = lsim(g0);
       int i1 = i0;
-      while (i1 < n_items && e->rg[e->ritems[i1].g].key_kind == kk && e->rg[e->ritems[i1].g].xmask == xm) ++i1;
+      while (i1 < n_items && lkey(e->ritems[i1].g) == lkey(g0)) ++i1;
       RatchetLaunch Ls = L;
       Ls.items = e->d_ritems.p + i0;
       Ls.n_items = i1 - i0;
@@ -1363,7 +1379,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       Ls.spillA = e->d_rspillA.p + (size_t)i0 * e->rSC * WAVE;
       Ls.lds_ts = e->d_rlts.p + (size_t)i0 * e->rML * WAVE;
       Ls.spillB = any64 ? e->d_rspillB.p + (size_t)i0 * e->rSC * WAVE : nullptr;
-      HIPCHK(sdh_launch_ratchet(kk, xm, full, nf, e->rML, e->rSC, &Ls, e->stream));
+      HIPCHK(sdh_launch_ratchet(kk, xm, full, nf, full ? 0 : sim, e->rML, e->rSC, &Ls, e->stream));
       i0 = i1;
     }
     HIPCHK(hipEventRecord(e->ev1, e->stream));

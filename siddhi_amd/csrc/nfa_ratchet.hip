@@ -411,7 +411,12 @@ __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {  // b >= 0
   return a > INT64_MAX - b ? INT64_MAX : a + b;
 }
 
-template <int KK, int XM, bool FULL, int NF>
+// SIM (the C2 family's form): 32-bit float keys, one start atom on the key's own float column with a
+// plain interval (no negation), no null masks. The start filter is then two float compares of the
+// event key against per-lane float bounds, and NaN keys fail every compare by themselves, so the
+// per-event validity bits are not read; an empty deque's top key is NaN, so the match test needs no
+// length check; a non-pushing lane writes its LDS entry to a dummy row instead of branching.
+template <int KK, int XM, bool FULL, int NF, bool SIM = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
   using U = typename KT<KK>::U;
   constexpr bool W64 = KT<KK>::W64;
@@ -472,6 +477,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
     f_ptr[a] = pick(L.b.col, A0.attr); f_w[a] = pick(L.b.width, A0.attr); f_nul[a] = pick(L.b.nul, A0.attr);
     f_ptr2[a] = pick(L.b.col, A0.attr2); f_w2[a] = pick(L.b.width, A0.attr2); f_nul2[a] = pick(L.b.nul, A0.attr2);
   }
+  // SIM: the start atom's interval of sortable binary64 keys as binary32 bounds (x in [flo, fhi] iff
+  // the widened key is in the interval; idle lanes get an empty one)
+  float flo = 0.f, fhi = 0.f;
+  if constexpr (SIM) {
+    auto unsort = [](int64_t v) { return __longlong_as_double(v >= 0 ? v : (v ^ INT64_MAX)); };
+    if (!active || f_lo[0] > f_hi[0]) {
+      flo = __int_as_float(0x7f800000);   // +inf
+      fhi = __int_as_float((int)0xff800000u);  // -inf
+    } else {
+      const double lo = f_lo[0] <= INT64_MIN + 1 ? -__longlong_as_double(0x7ff0000000000000ll) : unsort(f_lo[0]);
+      const double hi = f_hi[0] == INT64_MAX ? __longlong_as_double(0x7ff0000000000000ll) : unsort(f_hi[0]);
+      // the least float >= lo and the greatest float <= hi (one ulp step from the nearest; from +-0
+      // the step is the least denormal of the right sign)
+      flo = (float)lo;
+      if (flo == 0.f && lo > 0.0) flo = __int_as_float(1);
+      else if ((double)flo < lo) flo = __int_as_float(__float_as_int(flo) + (flo > 0.f ? 1 : -1));
+      fhi = (float)hi;
+      if (fhi == 0.f && hi < 0.0) fhi = __int_as_float((int)0x80000001u);
+      else if ((double)fhi > hi) fhi = __int_as_float(__float_as_int(fhi) + (fhi > 0.f ? -1 : 1));
+    }
+  }
+  const U TSENT = SIM ? (U)0x7fc00000u : (U)0;  // SIM: the top key of an empty deque (NaN)
   const void* k_ptr = pick(L.b.col, kattr);
   const uint8_t* k_nul = pick(L.b.nul, kattr);
   const int k_w = pick(L.b.width, kattr);
@@ -694,6 +721,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
   int64_t bdead = INT64_MAX;
   auto refresh_top = [&]() {
     if (D.ln > 0) D.lget_ks(D.li(D.lbot + D.ln - 1), tkey, tseq);
+    else if (SIM) tkey = TSENT;
   };
   auto refresh_bottom = [&]() {
     bdead = INT64_MAX;
@@ -779,9 +807,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
       const int64_t tt = readlane64(ets, k);
       const int64_t s = seq_base + t + k;
       const uint32_t slo = (uint32_t)s;
-      const uint32_t vb = __builtin_amdgcn_readlane(vbits, k);
+      const uint32_t vb = SIM ? 1u : __builtin_amdgcn_readlane(vbits, k);
       const U x = rlane(xk, k);
-      const bool x_ok = vb & 1u;
+      const bool x_ok = SIM || (vb & 1u);
 
       // ---- 1. lazy `within` expiry (oldest first) ----
       if (!FULL || has_within) {
@@ -798,6 +826,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
                 refill();
                 refresh_bottom();
                 if (D.n() == 0) bdead = INT64_MAX;
+                if (SIM && D.ln == 0) tkey = TSENT;
               }
             }
           }
@@ -813,7 +842,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
       }
 
       // ---- 2. matches: the newest partials whose key satisfies `cur OP key` ----
-      bool mt = x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey);
+      bool mt = SIM ? xop<KK, XM>(xmask, x, tkey) : (x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey));
       uint64_t m = __ballot(mt);
       while (m) {
         // the three LDS entries under the top, read unconditionally (in-bounds ring slots)
@@ -852,12 +881,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
         }
         bdead = (p > 0 && D.n() == 0) ? INT64_MAX : bdead;
         // more matches are possible only where four were popped or the top was refilled
-        mt = fix && x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey);
+        mt = SIM ? (fix && xop<KK, XM>(xmask, x, tkey)) : (fix && x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey));
         m = __ballot(mt);
       }
 
       // ---- 3. start state: every event passing f0 opens a partial (pending from j+1) ----
-      const bool f = f0_pass(k, vb);
+      bool f;
+      if constexpr (SIM) {
+        const float xf = __uint_as_float((uint32_t)x);
+        f = xf >= flo && xf <= fhi;
+      } else {
+        f = f0_pass(k, vb);
+      }
       if (__ballot(f && D.ln == ML) != 0) {
         // LDS ring full: move its oldest entry to the spill ring (rare)
         if (f && D.ln == ML) {
@@ -874,7 +909,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
         }
       }
       const bool push = f && D.ln < ML;
-      if (push) D.lput_ks(D.li(D.lbot + D.ln), x, slo);  // ts0 = ts of this batch event
+      if constexpr (SIM) D.lput_ks(push ? D.li(D.lbot + D.ln) : ML * WAVE + lane, x, slo);  // (dummy row)
+      else if (push) D.lput_ks(D.li(D.lbot + D.ln), x, slo);  // ts0 = ts of this batch event
       const bool first = push && D.n() == 0;
       bseq = first ? slo : bseq;
       bdead = first ? sat_add(tt, within) : bdead;
@@ -977,35 +1013,47 @@ extern "C" hipError_t sdh_launch_ratchet_summary(int key_kind, const sdh::Stream
   return hipGetLastError();
 }
 
-template <int KK, int XM, bool FULL, int NF>
+template <int KK, int XM, bool FULL, int NF, bool SIM = false>
 static void launch_one(const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {
   const bool w64 = (KK == sdh::KK_F64 || KK == sdh::KK_I64);
-  const size_t lds = (size_t)ML * 64 * (w64 ? 16 : 8);
-  hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF>), dim3(L->n_items), dim3(64), lds, s, *L, ML, SC);
+  const size_t lds = (size_t)(ML + (SIM ? 1 : 0)) * 64 * (w64 ? 16 : 8);  // (SIM: + the dummy row)
+  hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM>), dim3(L->n_items), dim3(64), lds, s, *L, ML, SC);
 }
 
-template <int KK, int XM, bool FULL, int NF>
+template <int KK, int XM, bool FULL, int NF, bool SIM = false>
 static int occupancy_one(int ML) {
   const bool w64 = (KK == sdh::KK_F64 || KK == sdh::KK_I64);
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sdh::nfa_ratchet_kernel<KK, XM, FULL, NF>, 64,
-                                                   (size_t)ML * 64 * (w64 ? 16 : 8)) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM>, 64,
+                                                   (size_t)(ML + (SIM ? 1 : 0)) * 64 * (w64 ? 16 : 8)) != hipSuccess)
     return 0;
   return nb;
 }
 
 template <int KK>
-static int occupancy_kk(bool full, int nf, int ML) {
+static int occupancy_kk(bool full, int nf, int ML, bool sim) {
   // the four orientations share one register allocation; XM = 0 stands for all
   if (full) return occupancy_one<KK, -1, true, sdh::RMAXF0>(ML);
+  if constexpr (KK == sdh::KK_F32)
+    if (sim && nf <= 1) return occupancy_one<KK, 0, false, 1, true>(ML);
   return nf <= 1 ? occupancy_one<KK, 0, false, 1>(ML) : occupancy_one<KK, 0, false, sdh::RMAXF0>(ML);
 }
 
 // nf: max f0 atoms over the launched groups (one-atom start filters get a leaner register set)
 template <int KK>
-static hipError_t launch_kk(int xm, bool full, int nf, const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {
+static hipError_t launch_kk(int xm, bool full, int nf, bool sim, const sdh::RatchetLaunch* L, int ML, int SC,
+                            hipStream_t s) {
   if (full) {
     launch_one<KK, -1, true, sdh::RMAXF0>(L, ML, SC, s);
+  } else if (KK == sdh::KK_F32 && sim && nf <= 1) {
+    if constexpr (KK == sdh::KK_F32) {
+      switch (xm) {
+        case 0: launch_one<KK, 0, false, 1, true>(L, ML, SC, s); break;
+        case 1: launch_one<KK, 1, false, 1, true>(L, ML, SC, s); break;
+        case 2: launch_one<KK, 2, false, 1, true>(L, ML, SC, s); break;
+        default: launch_one<KK, 3, false, 1, true>(L, ML, SC, s); break;
+      }
+    }
   } else if (nf <= 1) {
     switch (xm) {
       case 0: launch_one<KK, 0, false, 1>(L, ML, SC, s); break;
@@ -1025,27 +1073,27 @@ static hipError_t launch_kk(int xm, bool full, int nf, const sdh::RatchetLaunch*
 }
 
 // resident waves per CU of the K_ratchet instantiation (chunk planning fills the chip in one round)
-extern "C" int sdh_ratchet_occupancy(int key_kind, int full, int nf, int ML) {
+extern "C" int sdh_ratchet_occupancy(int key_kind, int full, int nf, int ML, int sim) {
   switch (key_kind) {
-    case sdh::KK_F32: return occupancy_kk<sdh::KK_F32>(full, nf, ML);
-    case sdh::KK_I32: return occupancy_kk<sdh::KK_I32>(full, nf, ML);
-    case sdh::KK_F64: return occupancy_kk<sdh::KK_F64>(full, nf, ML);
-    default: return occupancy_kk<sdh::KK_I64>(full, nf, ML);
+    case sdh::KK_F32: return occupancy_kk<sdh::KK_F32>(full, nf, ML, sim != 0);
+    case sdh::KK_I32: return occupancy_kk<sdh::KK_I32>(full, nf, ML, false);
+    case sdh::KK_F64: return occupancy_kk<sdh::KK_F64>(full, nf, ML, false);
+    default: return occupancy_kk<sdh::KK_I64>(full, nf, ML, false);
   }
 }
 
 // xmask: normalized `cur OP key` CmpMask of the launched groups (all equal); nf: max f0 atoms;
 // ML, SC powers of two
-extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int nf, int ML, int SC,
+extern "C" hipError_t sdh_launch_ratchet(int key_kind, int xmask, int full, int nf, int sim, int ML, int SC,
                                          const sdh::RatchetLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
   if (ML < 4 || (ML & (ML - 1)) || SC < 1 || (SC & (SC - 1)) || nf > sdh::RMAXF0) return hipErrorInvalidValue;
   const int xm = xmask == sdh::CM_GT ? 0 : xmask == (sdh::CM_GT | sdh::CM_EQ) ? 1 : xmask == sdh::CM_LT ? 2 : 3;
   switch (key_kind) {
-    case sdh::KK_F32: return launch_kk<sdh::KK_F32>(xm, full, nf, L, ML, SC, s);
-    case sdh::KK_I32: return launch_kk<sdh::KK_I32>(xm, full, nf, L, ML, SC, s);
-    case sdh::KK_F64: return launch_kk<sdh::KK_F64>(xm, full, nf, L, ML, SC, s);
-    case sdh::KK_I64: return launch_kk<sdh::KK_I64>(xm, full, nf, L, ML, SC, s);
+    case sdh::KK_F32: return launch_kk<sdh::KK_F32>(xm, full, nf, sim != 0, L, ML, SC, s);
+    case sdh::KK_I32: return launch_kk<sdh::KK_I32>(xm, full, nf, false, L, ML, SC, s);
+    case sdh::KK_F64: return launch_kk<sdh::KK_F64>(xm, full, nf, false, L, ML, SC, s);
+    case sdh::KK_I64: return launch_kk<sdh::KK_I64>(xm, full, nf, false, L, ML, SC, s);
     default: return hipErrorInvalidValue;
   }
 }

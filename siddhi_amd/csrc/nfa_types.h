@@ -156,6 +156,7 @@ struct RatchetGroup {
   int32_t xmask;                          // normalized `cur OP key` CmpMask (never EQ/NE)
   int32_t n_f0;
   int32_t sum_slot;                       // row of the launch's per-tile x-summaries (host-set)
+  int32_t sim;                            // the SIM kernel form applies (nfa_ratchet.hip; host-set)
   RatchetAtom f0[RMAXF0];
   int64_t wmax;                           // max within over lanes (-1: none)
   int32_t qid[64];

@@ -172,7 +172,10 @@ def test_direct_placement_equals_sort(mixed):
                 assert np.array_equal(x, y)
             n_total += len(ga[0])
     assert n_total > 100000
-    assert a.stats().placed_pushes >= 8 and b.stats().placed_pushes == 0
+    placed = a.stats().placed_pushes
+    assert b.stats().placed_pushes == 0
+    # (mixed: pushes where the chain / K_gen queries match go through the table)
+    assert (0 < placed < len(sizes)) if mixed else placed >= len(sizes) // 2
 
 
 def test_poll_device_equals_poll():
