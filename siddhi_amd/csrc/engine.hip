@@ -79,6 +79,11 @@ extern "C" hipError_t sdh_gen_journal(int32_t* a32, int64_t* a64, int64_t B32, i
                                        const int32_t* glist, const uint32_t* seg_kid, int groups, int64_t slots,
                                        int32_t* j32, int64_t* j64, int64_t* jidx, int restore, hipStream_t s);
 extern "C" size_t sdh_place_temp_bytes(int64_t cells);
+extern "C" size_t sdh_prefix_max_temp_bytes(int64_t n);
+extern "C" hipError_t sdh_prefix_max(const int64_t* ts, int64_t n, int64_t* pm, int32_t* unordered, void* temp,
+                                     size_t temp_bytes, hipStream_t s);
+extern "C" hipError_t sdh_key_segments(const uint32_t* uniq, const int32_t* nruns, int64_t max_runs, int64_t n_keys,
+                                       int32_t* kseg, hipStream_t s);
 extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, const int32_t* blk_count,
                                         const int32_t* blk_group, const int32_t* blk_prev, int n_blocks,
                                         int64_t rows, const int32_t* out_rank,
@@ -740,6 +745,9 @@ struct sdh_engine {
   DevBuf<int32_t> d_perr;            // per K_part set: [0] entry capacity, [2] output overflow
   DevBuf<unsigned long long> d_pprof;  // SDH_PART_PROF measurement builds: phase clocks
   DevBuf<int64_t> r_key;
+  DevBuf<int64_t> t_pm;              // indexed timer sweep: the batch's timestamp prefix max
+  DevBuf<int32_t> t_kseg, t_flag;    // per known key its routed segment; ts-order flag
+  DevBuf<uint8_t> t_temp;
   DevBuf<uint32_t> r_kid, r_kid_s, r_uniq;
   DevBuf<int32_t> r_idx, r_idx_s, r_cnt, r_off, r_nruns;
   DevBuf<uint8_t> r_temp;
@@ -2352,7 +2360,20 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
     bool timed = false;
     if (gsp)
       for (int g = 0; g < gsp->n_groups; ++g) timed |= e->gq[e->group_tmpl[gsp->group_base + g]].lay.TQ > 0;
-    auto sweep = [&](const uint32_t* ev_kid, int64_t n_keys) {
+    // an ordered batch takes the indexed sweep (each key walks its own events; its timers fire at the
+    // first event whose time reaches them, found by binary search), else every key walks the batch
+    auto ordered = [&]() {
+      if (n <= 0 || getenv("SDH_NO_TIMER_INDEX")) return false;
+      e->t_pm.ensure((size_t)n);
+      e->t_flag.ensure(1);
+      e->t_temp.ensure(sdh_prefix_max_temp_bytes(n));
+      HIPCHK(sdh_prefix_max(B.ts, n, e->t_pm.p, e->t_flag.p, e->t_temp.p, e->t_temp.n, e->stream));
+      int32_t un = 1;
+      HIPCHK(hipMemcpyAsync(&un, e->t_flag.p, 4, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipStreamSynchronize(e->stream));
+      return un == 0;
+    };
+    auto sweep = [&](const uint32_t* ev_kid, int64_t n_keys, bool indexed = false, bool own = false) {
       auto& gs = *gsp;
       sdh::GenLaunch L = gen_launch_base(e, gs, B, write);
       L.a32 = gs.a32.p;
@@ -2361,19 +2382,32 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       L.sweep = 1;
       L.ev_kid = ev_kid;
       L.n_keys = n_keys;
+      if (indexed) {
+        L.pm = e->t_pm.p;
+        if (own) {  // the keys' own events: the routed segments
+          e->t_kseg.ensure((size_t)std::max<int64_t>(1, n_keys));
+          HIPCHK(sdh_key_segments(e->r_uniq.p, e->r_nruns.p, n, n_keys, e->t_kseg.p, e->stream));
+          L.kseg = e->t_kseg.p;
+          L.seg_begin = e->r_off.p;
+          L.seg_len = e->r_cnt.p;
+          L.ev_idx = e->r_idx_s.p;
+        }
+      }
       L.n_items = (int32_t)(n_keys * gs.n_groups);
       gen_journal(e, gs, 2, nullptr, nullptr, (int64_t)L.n_items);
       if (L.n_items > 0) HIPCHK(sdh_launch_gen(&L, e->stream));
       e->stats.last_gen_items += L.n_items;
       any = true;
-      bytes += (double)n * ev_bytes * gs.n_groups * (double)n_keys;
+      // indexed: each key reads its own events and binary-searches pm per timer stop
+      bytes += (double)n * ev_bytes * gs.n_groups * (indexed ? 1.0 : (double)n_keys);
     };
     if (n == 0 || attr < 0) {
       if (timed) {
         int32_t nk = 0;
         HIPCHK(hipMemcpyAsync(&nk, rt.n_keys.p, 4, hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
-        sweep(nullptr, std::min<int64_t>(nk, gsp->key_cap));
+        const bool ix = ordered();
+        sweep(nullptr, std::min<int64_t>(nk, gsp->key_cap), ix, false);
       }
       continue;
     }
@@ -2418,7 +2452,8 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
     bytes += (double)n * (8 + 8 + 4 + 4 + 2 * (4 + 4) + 3 * 4);
     if (gsp && gsp->n_groups > 0 && timed) {
       gen_grow(e, *gsp, hv[0]);
-      sweep(e->r_kid.p, hv[0]);
+      const bool ix = ordered();
+      sweep(e->r_kid.p, hv[0], ix, true);
     } else if (gsp && gsp->n_groups > 0) {
       auto& gs = *gsp;
       gen_grow(e, gs, hv[0]);

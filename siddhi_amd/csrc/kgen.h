@@ -1341,6 +1341,17 @@ struct Ctx {
     }
     if (s.next_every >= 0 || (not_processed && s.is_start)) notify_at(i, (lst(i) == 0 ? actual : lst(i)) + w);
   }
+  // the earliest pending notification time of the instance's schedulers (INT64_MAX: none)
+  KG_FN int64_t next_due() const {
+    int64_t d = 0x7fffffffffffffffLL;
+    if (lay.TQ == 0) return d;
+    for (int i = 0; i < lay.S; ++i) {
+      if (!absent_any(i) || tq_len(i) == 0) continue;
+      const int64_t h = tq(i, tq_head(i));
+      d = h < d ? h : d;
+    }
+    return d;
+  }
   // Scheduler.sendTimerEvents:186-214 of every absent state of the instance up to time `upto`: the
   // earliest queue head fires first (ties: lower state id). `playback`: the generator's time is
   // `upto` while the timers fire; else each timer's own time.

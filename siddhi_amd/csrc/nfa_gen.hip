@@ -144,24 +144,59 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
       r[cw] = cnt;
     }
   };
-  for (int64_t k = w0; k < e1 && c.err == kg::GE_OK; ++k) {
-    live = k >= e0;
-    const int64_t e = L.ev_idx ? L.ev_idx[k] : k;
+  // One walk, one call site each for the timers and the interpreter (the interpreter is inlined per
+  // call site). Plain: the key's events [w0, e1). Whole-batch sweep: every batch event passes time,
+  // the key's own events are received. Indexed sweep (ordered batch, pm = ts): only the key's own
+  // events and the timer stops -- a timer due at d fires at the first batch event whose time reaches
+  // d (binary search of pm), with that event's seq and time, exactly where the whole walk fires it.
+  const bool indexed = L.sweep && L.pm;
+  const int32_t sg = indexed && L.kseg ? L.kseg[kid] : -1;
+  const int64_t sb = sg >= 0 ? L.seg_begin[sg] : 0, sl = sg >= 0 ? L.seg_len[sg] : 0;
+  int64_t j = 0, pos = 0;  // indexed: next own event, first batch event not passed yet
+  for (int64_t k = w0; c.err == kg::GE_OK;) {
+    int64_t e;
+    bool own;
+    const bool inited = !L.sweep || c.i32(q->lay.o_init) != 0;
+    if (indexed) {
+      const int64_t eo = j < sl ? L.ev_idx[sb + j] : L.b.n - 1;
+      if (eo < 0) break;  // (an empty batch)
+      const int64_t d = inited ? c.next_due() : 0x7fffffffffffffffLL;
+      if (d <= L.b.ts[eo]) {  // a timer stop at or before the next own event
+        int64_t lo = pos, hi = eo;
+        while (lo < hi) {
+          const int64_t m = (lo + hi) >> 1;
+          if (L.pm[m] < d) lo = m + 1;
+          else hi = m;
+        }
+        e = lo;
+        own = false;
+      } else if (j < sl) {
+        e = eo;
+        own = true;
+        ++j;
+      } else {
+        break;
+      }
+      pos = e;
+    } else {
+      if (k >= e1) break;
+      live = k >= e0;
+      e = L.ev_idx ? L.ev_idx[k] : k;
+      ++k;
+      own = !L.sweep || (L.ev_kid && L.ev_kid[e] == kid);  // a sweep passes time at other keys' events
+    }
     c.seq = L.b.seq_base + e;
     c.ts = L.b.ts[e];
     idx = 0;
-    const bool inited = !L.sweep || c.i32(q->lay.o_init) != 0;
     if (inited) c.fire_timers(c.ts, L.playback != 0, emit);  // timers due by this event fire before it
-    if (L.sweep) {
-      if (!L.ev_kid || L.ev_kid[e] != kid) continue;  // another key's event: only time passed
-      if (!inited) seed();
-    }
+    if (!own) continue;
+    if (!inited) seed();
     if (!reads) continue;
     c.ev_null = 0;
-    for (int j = 0; j < ncap; ++j) {  // the event is the same for every lane: identical LDS stores
+    for (int jj = 0; jj < ncap; ++jj) {  // the event is the same for every lane: identical LDS stores
       bool nl;
-      evv[j] = raw_word(L.b, q->cap_attr[c.stream][j], e, nl);
-      if (nl) c.ev_null |= 1u << j;
+      evv[jj] = raw_word(L.b, q->cap_attr[c.stream][jj], e, nl);
+      if (nl) c.ev_null |= 1u << jj;
     }
     c.receive(emit);
   }
@@ -214,6 +249,20 @@ __global__ void seq_tail_kernel(StreamBatch b, int64_t* tail, int32_t tail_len, 
       }
     }
   }
+}
+
+// ---- indexed timer sweep inputs: the batch's timestamp prefix max (and whether it is ordered), and
+// each known key's routed segment ----
+__global__ void ts_order_kernel(const int64_t* __restrict__ ts, int64_t n, int32_t* unordered) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > 0 && i < n && ts[i] < ts[i - 1]) atomicOr(unordered, 1);
+}
+__global__ void key_segment_kernel(const uint32_t* __restrict__ uniq, const int32_t* __restrict__ nruns,
+                                   int64_t n_keys, int32_t* __restrict__ kseg) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= *nruns) return;
+  const uint32_t kid = uniq[s];
+  if (kid != 0xFFFFFFFFu && (int64_t)kid < n_keys) kseg[kid] = (int32_t)s;
 }
 
 // ---- exact re-runs: the arena blocks a pass is about to modify, journaled just before it runs ----
@@ -490,6 +539,36 @@ extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, hipStream_t s) {
 }
 
 // roll a stream's K_seq tail over batch b (after the push's K_seq launches have succeeded)
+// pm = inclusive prefix max of ts; *unordered (device) = 1 when ts decreases somewhere
+extern "C" size_t sdh_prefix_max_temp_bytes(int64_t n) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::InclusiveScan((void*)nullptr, b, (const int64_t*)nullptr, (int64_t*)nullptr,
+                                          hipcub::Max(), (int)n);
+  return b + 256;
+}
+extern "C" hipError_t sdh_prefix_max(const int64_t* ts, int64_t n, int64_t* pm, int32_t* unordered, void* temp,
+                                     size_t temp_bytes, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(unordered, 0, 4, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sdh::ts_order_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ts, n, unordered);
+  size_t tb = temp_bytes;
+  e = hipcub::DeviceScan::InclusiveScan(temp, tb, ts, pm, hipcub::Max(), (int)n, s);
+  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+// kseg[kid] = the routed segment of key kid in this batch, -1 without events
+extern "C" hipError_t sdh_key_segments(const uint32_t* uniq, const int32_t* nruns, int64_t max_runs, int64_t n_keys,
+                                       int32_t* kseg, hipStream_t s) {
+  if (n_keys <= 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(kseg, 0xFF, (size_t)n_keys * 4, s);
+  if (e != hipSuccess) return e;
+  if (max_runs > 0)
+    hipLaunchKernelGGL(sdh::key_segment_kernel, dim3((unsigned)((max_runs + 255) / 256)), dim3(256), 0, s, uniq, nruns,
+                       n_keys, kseg);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t sdh_gen_journal(int32_t* a32, int64_t* a64, int64_t B32, int64_t B64, int mode,
                                        const int32_t* glist, const uint32_t* seg_kid, int groups, int64_t slots,
                                        int32_t* j32, int64_t* j64, int64_t* jidx, int restore, hipStream_t s) {

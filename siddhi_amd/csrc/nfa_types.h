@@ -266,6 +266,12 @@ struct GenLaunch {
   int64_t advance_to;
   int64_t timer_seq;          // trigger seq of the timers fired after the last event
   int32_t playback;           // @app:playback: the generator's time is the event time while timers fire
+  // indexed timer sweep (pm != nullptr; batches with ordered timestamps): item = (kid, group) over
+  // every known key walks only its own events (the routed segment kseg[kid] of seg_begin / seg_len /
+  // ev_idx, -1: none) and fires each due timer at the first batch event whose ts reaches it (binary
+  // search in the prefix max pm) -- O(own events + firings) instead of O(batch) per key
+  const int64_t* pm;          // [n] prefix max of the batch timestamps
+  const int32_t* kseg;        // [known keys] segment of the key's events in this batch, or -1
   // timer sweep of a partition set with absent states: item = (kid, group) over every known key; the
   // item walks the whole batch in order, firing the clone's timers before each event and processing
   // the events of its own key (ev_kid: each event's dense key id); clones seed at their first event

@@ -110,3 +110,42 @@ def test_absent_snapshot_restore_keeps_pending_timers():
             x.send(s, [r], [t])
         x.advance_time(t0 + 400)
     assert b.matches == o.matches and len(o.matches) >= 2
+
+
+@pytest.mark.parametrize("seed", [0, 3, 6, 9, 12])
+def test_absent_partition_indexed_sweep(seed):
+    """Partitioned absent states over many keys and long ordered pushes take the indexed timer sweep
+    (nfa_gen.hip: each key's clone walks its own routed events; a timer fires at the first batch event
+    whose time reaches it, by binary search of the batch's time prefix max). Against the oracle, and
+    equal to the whole-batch sweep (SDH_NO_TIMER_INDEX) push for push."""
+    import os
+    import numpy as np
+    from fuzz_apps import random_events
+    src = random_absent_app(seed, partition=True)
+    rng = np.random.default_rng(seed)
+    ev = [("A" if rng.random() < 0.9 else "B", row, t) for _, row, t in random_events(seed, n=3000, keys=60)]
+    apps = [App(src), App(src, hip_factory(src)), App(src, hip_factory(src))]
+    try:
+        for a in apps:
+            a.start(0)
+        i = 0
+        while i < len(ev):
+            j = i + 1
+            while j < len(ev) and ev[j][0] == ev[i][0] and j - i < 500:
+                j += 1
+            rows, ts = [r for _, r, _ in ev[i:j]], [t for _, _, t in ev[i:j]]
+            for k, a in enumerate(apps):
+                if k == 2:
+                    os.environ["SDH_NO_TIMER_INDEX"] = "1"
+                try:
+                    a.send(ev[i][0], rows, ts)
+                finally:
+                    os.environ.pop("SDH_NO_TIMER_INDEX", None)
+            i = j
+        for a in apps:
+            a.advance_time(ev[-1][2] + 50)
+    except OracleError:
+        pytest.skip("the reference engine throws on this stream")
+    o, g, w = apps
+    assert g.matches == w.matches
+    assert g.matches == o.matches and len(o.matches) > 0
