@@ -540,7 +540,7 @@ def push_latency(args, sh, K, local):
     gen = txn_events if args.workload == "c4" else stock_events
     out, lo = {}, 0
     for bs in (1, 64, 4096):
-        lat, nm = [], 0
+        lat, plat, nm = [], [], 0
         warm, reps = (5, 50) if bs < 4096 else (2, 10)
         for i in range(warm + reps):
             ts, a, b, c = gen(lo, bs, K)
@@ -548,12 +548,19 @@ def push_latency(args, sh, K, local):
             cols = [a, b.view(np.uint32), c]
             t0 = time.perf_counter()
             eng.push_columns(0, ts, cols)
+            t1 = time.perf_counter()
             m = eng.poll()
             if i >= warm:
                 lat.append((time.perf_counter() - t0) * 1e3)
+                plat.append((t1 - t0) * 1e3)
                 nm += len(m[0])
         lat.sort()
+        plat.sort()
+        # push: host batch in, NFA step, matches placed in HBM in R18 order; poll: the tuples copied
+        # to host arrays (PCIe and host copies, ~72 B per match)
         out[str(bs)] = {"median_ms": lat[len(lat) // 2], "p99_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))],
+                        "push_median_ms": plat[len(plat) // 2],
+                        "push_p99_ms": plat[min(len(plat) - 1, int(len(plat) * 0.99))],
                         "matches_per_push": nm / len(lat)}
     eng.close()
     return out

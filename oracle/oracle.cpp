@@ -78,9 +78,15 @@ struct PartKey {
   int stream;
   Code code;
 };
+struct FanOut {  // a stream the partition's queries read but no key covers
+  int stream;
+  int32_t id_hash;  // String.hashCode of the stream id
+  int id_len;
+};
 struct PartDef {
   std::vector<PartKey> keys;
   std::vector<int> queries;
+  std::vector<FanOut> fanout;
 };
 struct Program {
   std::vector<std::vector<int>> stream_types;
@@ -169,7 +175,124 @@ Program parse_ir(const void* blob, size_t len) {
     pd.queries.resize(r.next());
     for (auto& x : pd.queries) x = (int)r.next();
   }
+  if (r.i < r.n)  // trailer: the partitions' fan-out streams
+    for (auto& pd : p.parts) {
+      pd.fanout.resize(r.next());
+      for (auto& f : pd.fanout) {
+        f.stream = (int)r.next();
+        f.id_hash = (int32_t)r.next();
+        f.id_len = (int)r.next();
+      }
+    }
   return p;
+}
+
+// ------------------------------------------------------------------------------------------
+// java.util.concurrent.ConcurrentHashMap (JDK 8, the reference's runtime; not in /root/reference --
+// restated from its published algorithm): the iteration order of a map filled by put() in a given
+// order, single-threaded. PartitionStreamReceiver.send(ComplexEvent):277-281 walks its
+// cachedStreamJunctionMap.values() in this order. Parity of multi-key orders is unpinned (the
+// reference KAT, PatternPartitionTestCase query 30, has one key).
+// ------------------------------------------------------------------------------------------
+struct JavaCHM {
+  struct Node {
+    int32_t hash;  // spread(h)
+    int id;
+  };
+  struct Bin {
+    std::vector<Node> nodes;  // list order (a TreeBin: its `first` list order)
+    bool tree = false;
+  };
+  std::vector<Bin> tab;
+  int64_t size_ctl = 0, count = 0;
+  static int32_t spread(int32_t h) { return (int32_t)(((uint32_t)h ^ ((uint32_t)h >> 16)) & 0x7fffffffu); }
+  // transfer:2330-2470 to a table twice as large: a list bin splits at its lastRun -- the nodes
+  // before it are prepended to their half (reversed), the run keeps its order; a TreeBin splits in
+  // order and untreeifies at <= 6 nodes (UNTREEIFY_THRESHOLD)
+  void transfer() {
+    const size_t n = tab.size();
+    std::vector<Bin> nt(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+      Bin& b = tab[i];
+      if (b.nodes.empty()) continue;
+      std::vector<Node> lo, hi;
+      if (!b.tree) {
+        size_t last = 0;
+        int run = b.nodes[0].hash & (int)n;
+        for (size_t k = 1; k < b.nodes.size(); ++k)
+          if ((b.nodes[k].hash & (int)n) != run) {
+            run = b.nodes[k].hash & (int)n;
+            last = k;
+          }
+        std::vector<Node>& tail = run == 0 ? lo : hi;
+        tail.assign(b.nodes.begin() + (long)last, b.nodes.end());
+        for (size_t k = 0; k < last; ++k) {
+          std::vector<Node>& dst = (b.nodes[k].hash & (int)n) == 0 ? lo : hi;
+          dst.insert(dst.begin(), b.nodes[k]);
+        }
+        nt[i].nodes = lo;
+        nt[i + n].nodes = hi;
+      } else {
+        for (const Node& x : b.nodes) ((x.hash & (int)n) == 0 ? lo : hi).push_back(x);
+        nt[i].nodes = lo;
+        nt[i].tree = lo.size() > 6;
+        nt[i + n].nodes = hi;
+        nt[i + n].tree = hi.size() > 6;
+      }
+    }
+    tab.swap(nt);
+    size_ctl = (int64_t)(2 * n) - (int64_t)(n >> 1);
+  }
+  static int64_t table_size_for(int64_t c) {
+    int64_t n = 1;
+    while (n < c) n <<= 1;
+    return n;
+  }
+  // tryPresize:2262-2300 (treeifyBin on a table shorter than MIN_TREEIFY_CAPACITY)
+  void try_presize(int64_t size) {
+    const int64_t c = table_size_for(size + (size >> 1) + 1);
+    while (c > size_ctl) transfer();
+  }
+  // putVal:1010-1060 + addCount:2230-2260
+  void put(int32_t h, int id) {
+    if (tab.empty()) {
+      tab.resize(16);  // DEFAULT_CAPACITY
+      size_ctl = 12;
+    }
+    const int32_t hs = spread(h);
+    const size_t i = (size_t)hs & (tab.size() - 1);
+    Bin& b = tab[i];
+    int64_t bin_count = 0;
+    if (b.nodes.empty()) {
+      b.nodes.push_back({hs, id});
+    } else if (b.tree) {
+      bin_count = 2;
+      b.nodes.insert(b.nodes.begin(), Node{hs, id});  // putTreeVal: the new node becomes `first`
+    } else {
+      bin_count = (int64_t)b.nodes.size();
+      b.nodes.push_back({hs, id});
+      if (bin_count >= 8) {  // TREEIFY_THRESHOLD -> treeifyBin
+        if (tab.size() < 64) try_presize((int64_t)tab.size() << 1);
+        else tab[i].tree = true;
+      }
+    }
+    ++count;
+    if (bin_count >= 0)
+      while (count >= size_ctl) transfer();
+  }
+  std::vector<int> order() const {
+    std::vector<int> o;
+    for (const Bin& b : tab)
+      for (const Node& x : b.nodes) o.push_back(x.id);
+    return o;
+  }
+};
+
+// String.hashCode of `prefix + s` from the prefix's hash and the UTF-16 (here ASCII) units of s
+int32_t java_hash_append(int32_t h, const std::string& s) {
+  uint32_t u = (uint32_t)h;
+  for (unsigned char c : s) u = 31u * u + c;
+  return (int32_t)u;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -803,6 +926,7 @@ struct Engine {
   // per partition: key -> instance runtimes (one per partition query)
   std::vector<std::map<i64, std::vector<std::unique_ptr<Runtime>>>> part_inst;
   std::vector<std::vector<i64>> key_order;          // creation order per partition
+  std::vector<int> key_type;                        // per partition: the keys' value type
   std::vector<Match> matches;
   std::vector<std::pair<Runtime*, StateEvent*>> deferred;  // single-receiver chunk deferral
   std::vector<i64> deferred_seq;
@@ -1275,6 +1399,26 @@ void deliver_to(Engine* e, int qi, int stream, const std::vector<i64>& seqs) {
   }
   const int pi = q.partition;
   const PartDef& pd = P.parts[pi];
+  for (const FanOut& fo : pd.fanout) {
+    if (fo.stream != stream) continue;
+    // PartitionStreamReceiver.receive:83-92 (no executor for this stream) -> send(ComplexEvent):
+    // 277-281: every key's junction "streamId + key" in its cachedStreamJunctionMap's order; keys
+    // joined it at clonePartition (updatePartitionStreamReceivers:312-316), in creation order
+    const auto& ko = e->key_order[pi];
+    auto value_of = [&](i64 k) {  // String.valueOf (ValuePartitionExecutor.java:34-40)
+      if (e->key_type[pi] == T_BOOL) return std::string(k ? "true" : "false");
+      return std::to_string((long long)k);
+    };
+    for (i64 seq : seqs) {
+      JavaCHM m;
+      for (size_t k = 0; k < ko.size(); ++k) m.put(java_hash_append(fo.id_hash, value_of(ko[k])), (int)k);
+      for (int k : m.order()) {
+        for (auto& rt : e->part_inst[pi].at(ko[(size_t)k])) rt->receive(stream, seq, e->log[seq].ts);
+        deliver_deferred(e);
+      }
+    }
+    return;
+  }
   for (i64 seq : seqs) {
     for (const PartKey& k : pd.keys) {
       if (k.stream != stream) continue;
@@ -1296,6 +1440,7 @@ void deliver_to(Engine* e, int qi, int stream, const std::vector<i64>& seqs) {
         }
         it = inst.emplace(key, std::move(rts)).first;
         e->key_order[pi].push_back(key);
+        e->key_type[pi] = kv.type;
       }
       for (auto& rt : it->second) rt->receive(stream, seq, e->log[seq].ts);
       deliver_deferred(e);
@@ -1334,6 +1479,7 @@ int oracle_create(const void* blob, size_t len, OracleEngine** out) {
     }
     e->part_inst.resize(e->prog.parts.size());
     e->key_order.resize(e->prog.parts.size());
+    e->key_type.resize(e->prog.parts.size(), T_INT);
     for (const auto& q : e->prog.queries)
       for (const auto& st : q.states) e->has_absent |= st.kind == K_ABSENT || (st.kind == K_LOGICAL && st.waiting != -1);
     *out = e;

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/siddhi_hip.h"
+#include "chm_order.h"
 #include "gen_lower.h"
 #include "nfa_types.h"
 #include "slab_lower.h"
@@ -72,8 +73,11 @@ extern "C" hipError_t sdh_append_chain(const int64_t* src, const int64_t* seg_of
                                        int64_t seq_ref, const int32_t* out_rank, int n_streams, sdh::MatchTable T,
                                        int64_t row0, int64_t word0, hipStream_t s);
 extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t seq_ref,
-                                     const int32_t* out_rank, int n_streams, sdh::MatchTable T, int64_t row0,
-                                     int64_t word0, hipStream_t s);
+                                     const int32_t* out_rank, const int32_t* fan_rank, int n_streams,
+                                     sdh::MatchTable T, int64_t row0, int64_t word0, hipStream_t s);
+extern "C" hipError_t sdh_new_keys(const uint32_t* uniq, const int32_t* nruns, int64_t max_runs, const int32_t* off,
+                                   const int32_t* idx_s, const int64_t* key_of_id, int64_t old_n, int64_t new_n,
+                                   int64_t* out, hipStream_t s);
 extern "C" size_t sdh_poll_temp_bytes(int64_t n);
 extern "C" hipError_t sdh_gen_journal(int32_t* a32, int64_t* a64, int64_t B32, int64_t B64, int mode,
                                        const int32_t* glist, const uint32_t* seg_kid, int groups, int64_t slots,
@@ -85,13 +89,11 @@ extern "C" hipError_t sdh_prefix_max(const int64_t* ts, int64_t n, int64_t* pm, 
 extern "C" hipError_t sdh_key_segments(const uint32_t* uniq, const int32_t* nruns, int64_t max_runs, int64_t n_keys,
                                        int32_t* kseg, hipStream_t s);
 extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, const int32_t* blk_count,
-                                        const int32_t* blk_group, const int32_t* blk_prev, int n_blocks,
-                                        int64_t rows, const int32_t* out_rank,
-                                        int n_streams, int n_ranks, int64_t n_events, int32_t* cnt, int32_t* flag,
-                                        void* temp, size_t temp_bytes, const sdh::RatchetGroup* groups,
-                                        const int64_t* ts, int64_t seq_base, int64_t row0, int64_t* oq, int64_t* okey,
-                                        int64_t* ots, int64_t* oseq, int64_t* otb, int64_t* ooff, int64_t* owords,
-                                        hipStream_t s);
+                                        const int32_t* blk_group, int n_blocks, int64_t rows, const int32_t* out_rank,
+                                        int n_streams, int n_ranks, int64_t n_events, int32_t* cnt, void* temp,
+                                        size_t temp_bytes, const sdh::RatchetGroup* groups, const int64_t* ts,
+                                        int64_t seq_base, int64_t row0, int64_t* oq, int64_t* okey, int64_t* ots,
+                                        int64_t* oseq, int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s);
 extern "C" hipError_t sdh_placed_to_table(const int64_t* q, const int64_t* ts, const int64_t* seq, const int64_t* words,
                                           int64_t n, int64_t seq_ref, const int32_t* out_rank, const int32_t* qinfo,
                                           int n_streams, sdh::MatchTable T, hipStream_t s);
@@ -667,6 +669,8 @@ struct sdh_engine {
   bool started = false;
   int64_t start_ts = 0;
   bool has_absent = false;
+  bool has_fanout = false;           // a partition query reads a stream the partition does not key
+  DevBuf<int32_t> d_fan_rank;        // [query][stream] its rank within the partition (fan-out), -1
   int64_t advance_to = INT64_MIN;    // set while a time advance runs (sdh_engine_advance_time)
   std::vector<char> gq_arena;        // [gq] the query runs on K_gen (has an instance arena)
   int64_t gen_regrows = 0;           // pool growths so far (sdh_stats)
@@ -691,6 +695,16 @@ struct sdh_engine {
     DevBuf<int32_t> tid, n_keys;
     DevBuf<int64_t> key_of_id;
     int64_t tmask = 0, max_keys = 0;
+    // fan-out partitions: keys in creation order (dense id, value), for the junction-map order
+    bool track = false, kbool = false;
+    int64_t nk_seen = 0;
+    std::vector<int64_t> korder_kid, korder_key;
+    DevBuf<int64_t> nk_tmp;
+    struct Fan {
+      int64_t n = -1;  // keys the positions cover
+      DevBuf<int32_t> pos;
+    };
+    std::map<int, Fan> fan;  // [stream] per-kid positions in that stream's junction map
   };
   std::vector<std::unique_ptr<Route>> routes;  // [partition] (null: no device set uses it)
   // K_part (nfa_part.hip): one set per (partition, kind); state blocks (key, group) double-buffered
@@ -769,7 +783,7 @@ struct sdh_engine {
   DevBuf<RatchetItem> d_ritems;
   std::vector<RatchetItem> ritems;
   DevBuf<int64_t> d_rmatch;
-  DevBuf<int32_t> d_blk_count, d_blk_next, d_blk_group, d_blk_prev;
+  DevBuf<int32_t> d_blk_count, d_blk_next, d_blk_group;
   DevBuf<unsigned long long> d_rtotal;  // records written in ring mode (SDH_FLAG_DEVICE_MATCHES)
   int r_wide = 0;
   int64_t r_blocks = 0;              // capacity in blocks
@@ -777,7 +791,8 @@ struct sdh_engine {
   int r_blocks_used = 0;             // of the last launch
   int64_t r_blk_taken = 0;           // blocks the last launch took (ring mode: may exceed r_blocks)
   // direct R18 placement (matches.hip ratchet_place_kernel): the (event, query rank) count matrix
-  DevBuf<int32_t> p_cnt, p_flag;
+  DevBuf<int32_t> p_cnt;            // direct placement: the (event, rank) count matrix
+  bool r_placing = false;            //   the last K_ratchet launch wrote it (PLACE variant)
   DevBuf<uint8_t> p_ptemp;
   int64_t r_seq_base = 0;            // seq of the last launch's first event
   std::vector<int32_t> r_blk_count;
@@ -908,11 +923,13 @@ void append_gen(sdh_engine* e) {
   table_reserve(e, n_rec, used);
   HIPCHK(hipMemcpyAsync(e->mt.words.p + e->mt.nw, e->g_out.p, (size_t)used * 8, hipMemcpyDeviceToDevice, e->stream));
   HIPCHK(sdh_append_gen(e->g_out.p, e->g_rec_off.p, n_rec, e->seq_ref, e->d_out_rank.p,
-                        (int)e->prog.stream_types.size(), table_view(e), e->mt.n, e->mt.nw, e->stream));
+                        e->has_fanout ? e->d_fan_rank.p : nullptr, (int)e->prog.stream_types.size(), table_view(e),
+                        e->mt.n, e->mt.nw, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   e->mt.n += n_rec;
   e->mt.nw += used;
-  e->mt.n_lo = std::max(e->mt.n_lo, e->has_absent ? 3 : 1);  // timer records: (key, query, time)
+  // timer records: (key, query, time); fan-out records: (position, rank, emission)
+  e->mt.n_lo = std::max(e->mt.n_lo, e->has_absent || e->has_fanout ? 3 : 1);
 }
 
 void table_clear(sdh_engine* e) {
@@ -923,15 +940,60 @@ void table_clear(sdh_engine* e) {
   e->seq_ref = e->seq;
 }
 
-// The last push's K_ratchet matches written straight to their R18 rows of the ABI outputs, after
-// the window's rows (matches.hip ratchet_place_kernel). False, with nothing written, when the push
-// does not qualify or a run split over two blocks: the caller appends to the table instead.
-bool place_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base, int64_t n_events) {
+// keys this push created (ids [nk_seen, new_n)), in the order of their first events: the order
+// PartitionRuntime.clonePartition adds them to every receiver's junction map
+void track_new_keys(sdh_engine* e, sdh_engine::Route& rt, int64_t new_n, int64_t nruns, bool kbool) {
+  const int64_t m = new_n - rt.nk_seen;
+  rt.nk_tmp.ensure((size_t)(2 * m));
+  HIPCHK(sdh_new_keys(e->r_uniq.p, e->r_nruns.p, nruns, e->r_off.p, e->r_idx_s.p, rt.key_of_id.p, rt.nk_seen, new_n,
+                      rt.nk_tmp.p, e->stream));
+  std::vector<int64_t> v((size_t)(2 * m));
+  HIPCHK(hipMemcpyAsync(v.data(), rt.nk_tmp.p, v.size() * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  std::vector<int64_t> ord((size_t)m);
+  for (int64_t k = 0; k < m; ++k) ord[(size_t)k] = k;
+  std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return v[(size_t)(2 * a)] < v[(size_t)(2 * b)]; });
+  for (int64_t k : ord) {
+    rt.korder_kid.push_back(rt.nk_seen + k);
+    rt.korder_key.push_back(v[(size_t)(2 * k + 1)]);
+  }
+  rt.kbool = kbool;
+  rt.nk_seen = new_n;
+}
+
+// per known key its position in the fan-out stream's junction map of "streamId + key" strings
+// (chm_order.h), on the device; rebuilt when keys were added
+const int32_t* fan_positions(sdh_engine* e, sdh_engine::Route& rt, const kg::LFanOut& fo, int64_t nk) {
+  auto& f = rt.fan[fo.stream];
+  if (f.n != nk) {
+    const size_t m = std::min<size_t>((size_t)nk, rt.korder_key.size());
+    std::vector<int32_t> hs(m), byk((size_t)std::max<int64_t>(1, nk), 0);
+    for (size_t j = 0; j < m; ++j) hs[j] = sdh::java_hash_cat(fo.id_hash, sdh::java_value_of(rt.kbool, rt.korder_key[j]));
+    const std::vector<int32_t> pos = sdh::ChmOrder().positions(hs);
+    for (size_t j = 0; j < m; ++j) byk[(size_t)rt.korder_kid[j]] = pos[j];
+    f.pos.ensure(byk.size());
+    HIPCHK(hipMemcpy(f.pos.p, byk.data(), byk.size() * 4, hipMemcpyHostToDevice));
+    f.n = nk;
+  }
+  return f.pos.p;
+}
+
+// A normal-mode push places its K_ratchet matches directly (the PLACE variant counts them per
+// (event, rank) cell) when the count matrix stays within 2^30 cells and timestamps are in order.
+bool ratchet_placeable(const sdh_engine* e, int64_t n_events, bool full) {
   const int nr = (int)e->prog.q.size();  // receiver ranks < queries
+  return !(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) && !full && n_events > 0 &&
+         (double)n_events * nr <= (double)(1 << 30) && !getenv("SDH_NO_PLACE");
+}
+
+// The last push's K_ratchet matches written straight to their R18 rows of the ABI outputs, after
+// the window's rows (matches.hip ratchet_place_kernel). False, with nothing written, when the launch
+// did not count them (ratchet_placeable) or the rows would pass 2^31: the caller appends to the
+// table instead.
+bool place_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base, int64_t n_events) {
+  const int nr = (int)e->prog.q.size();
   const int64_t rows = e->r_matches, n0 = e->mt.n;
-  if (e->r_wide || e->r_blk_recs > 8192 || (double)n_events * nr > (double)(1 << 30) || n0 + rows >= INT32_MAX ||
-      getenv("SDH_NO_PLACE"))
-    return false;
+  if (!e->r_placing || n0 + rows >= INT32_MAX) return false;
   const size_t keep = (size_t)n0, want = (size_t)(n0 + rows);
   e->po_q.grow_keep(want, keep, e->stream);
   e->po_key.grow_keep(want, keep, e->stream);
@@ -941,21 +1003,12 @@ bool place_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base, int64
   e->po_off.grow_keep(want + 1, keep, e->stream);
   e->po_words.grow_keep(4 * want, 4 * keep, e->stream);
   const int64_t cells = n_events * nr;
-  e->p_cnt.ensure((size_t)cells);
-  e->p_flag.ensure(1);
   const size_t tb = sdh_place_temp_bytes(cells);
   e->p_ptemp.ensure(tb);
-  const hipError_t r = sdh_place_ratchet(e->d_rmatch.p, e->r_blk_recs, e->d_blk_count.p, e->d_blk_group.p,
-                                         e->d_blk_prev.p, e->r_blocks_used, rows, e->d_out_rank.p, (int)e->prog.stream_types.size(), nr,
-                                         n_events, e->p_cnt.p, e->p_flag.p,
-                                         e->p_ptemp.p, e->p_ptemp.n, e->d_rg.p, ts_col, seq_base, n0, e->po_q.p,
-                                         e->po_key.p, e->po_ts.p, e->po_seq.p, e->po_tb.p, e->po_off.p, e->po_words.p,
-                                         e->stream);
-  if (r == hipErrorNotSupported) {
-    (void)hipGetLastError();
-    return false;
-  }
-  HIPCHK(r);
+  HIPCHK(sdh_place_ratchet(e->d_rmatch.p, e->r_blk_recs, e->d_blk_count.p, e->d_blk_group.p, e->r_blocks_used, rows,
+                           e->d_out_rank.p, (int)e->prog.stream_types.size(), nr, n_events, e->p_cnt.p, e->p_ptemp.p,
+                           e->p_ptemp.n, e->d_rg.p, ts_col, seq_base, n0, e->po_q.p, e->po_key.p, e->po_ts.p,
+                           e->po_seq.p, e->po_tb.p, e->po_off.p, e->po_words.p, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   e->mt.n += rows;
   e->mt.placed = true;
@@ -1246,6 +1299,7 @@ int ratchet_sim(const sdh::RatchetGroup& g) {
 }
 
 void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2]) {
+  e->r_placing = false;
   e->r_blocks_used = 0;
   e->r_matches = 0;
   e->r_kernel_ms = 0;
@@ -1315,8 +1369,10 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     e->d_ritems.ensure(n_items);
     HIPCHK(hipMemcpyAsync(e->d_ritems.p, e->ritems.data(), n_items * sizeof(RatchetItem),
                           hipMemcpyHostToDevice, e->stream));
-    // 8-B records address e2 by a 26-bit batch offset; larger batches use 16-B records
-    const int wide = n > ((int64_t)1 << 26) ? 1 : 0;
+    // 8-B records address e2 by a 26-bit batch offset; larger batches, and placing launches (the
+    // record carries its pop level), use 16-B records
+    const bool placing = ratchet_placeable(e, n, full);
+    const int wide = (n > ((int64_t)1 << 26) || placing) ? 1 : 0;
     if (n > ((int64_t)1 << 32)) throw Error(SDH_E_INVALID, "batch larger than 2^32 events");
     e->d_rmatch.ensure((size_t)e->r_blocks * e->r_blk_recs * (wide ? 2 : 1));
     e->d_rspillA.ensure((size_t)n_items * e->rSC * WAVE);
@@ -1326,7 +1382,6 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     if (any64) e->d_rspillB.ensure((size_t)n_items * e->rSC * WAVE);
     e->d_blk_count.ensure((size_t)e->r_blocks);
     e->d_blk_group.ensure((size_t)e->r_blocks);
-    e->d_blk_prev.ensure((size_t)e->r_blocks);
     e->d_err.ensure(4);
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
     HIPCHK(hipMemsetAsync(e->d_blk_next.p, 0, 4, e->stream));
@@ -1364,7 +1419,6 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.match = e->d_rmatch.p;
     L.blk_count = e->d_blk_count.p;
     L.blk_group = e->d_blk_group.p;
-    L.blk_prev = e->d_blk_prev.p;
     L.wide = wide;
     L.blk_next = e->d_blk_next.p;
     L.n_blocks = (int32_t)std::min<int64_t>(e->r_blocks, INT32_MAX);
@@ -1372,6 +1426,16 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.ring = ring ? 1 : 0;
     L.rec_total = e->d_rtotal.p;
     L.err = e->d_err.p;
+    if (placing) {
+      const int nr = (int)e->prog.q.size();
+      e->p_cnt.ensure((size_t)(n * nr));
+      HIPCHK(hipMemsetAsync(e->p_cnt.p, 0, (size_t)(n * nr) * 4, e->stream));
+      L.pcnt = e->p_cnt.p;
+      L.out_rank = e->d_out_rank.p;
+      L.n_ranks = nr;
+      L.n_streams = (int32_t)e->prog.stream_types.size();
+    }
+    e->r_placing = false;
     HIPCHK(hipEventRecord(e->ev0, e->stream));
     for (int i0 = 0; i0 < n_items;) {
       const int g0 = e->ritems[i0].g;
@@ -1420,6 +1484,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       continue;
     }
     for (int g : gs) e->rcur[g] ^= 1;
+    e->r_placing = placing;
     e->r_blk_taken = used;
     e->r_seq_base = B.seq_base;
     if (ring) {  // counted, not collected
@@ -1808,8 +1873,10 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
       if (7 + g.lay.S + g.lay.N > GEN_RING_MARGIN) throw kg::LowerError("match record longer than the ring margin");
       gidx[qi] = (int)e->gq.size();
       e->gq.push_back(g);
-      if (use_part) kpart[qi] = kpart_shape(e->lp, qi, g);
-      if (use_slab && kpart[qi].kind < 0) {
+      const bool fan = kg::reads_fanout(e->lp, qi);  // fan-out streams run on K_gen (the sweep)
+      e->has_fanout |= fan;
+      if (use_part && !fan) kpart[qi] = kpart_shape(e->lp, qi, g);
+      if (use_slab && !fan && kpart[qi].kind < 0) {
         slab::Shape sh;
         is_slab[qi] = slab::shape_of_query(e->lp, qi, g, &sh, nullptr) ? 1 : 0;
       }
@@ -1868,6 +1935,9 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
     r->n_keys.ensure(1);
     HIPCHK(hipMemset(r->n_keys.p, 0, 4));
     r->key_of_id.ensure(r->max_keys);
+    r->track = !e->lp.parts[partition].fanout.empty();
+    if (r->track && e->cfg.shard_world > 1)
+      throw Error(SDH_E_UNSUPPORTED, "a non-partitioned stream inside a partition with key sharding");
     e->routes[partition] = std::move(r);
   };
   auto add_part_sets = [&](int partition, const std::vector<int>& members) {
@@ -2373,7 +2443,8 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       HIPCHK(hipStreamSynchronize(e->stream));
       return un == 0;
     };
-    auto sweep = [&](const uint32_t* ev_kid, int64_t n_keys, bool indexed = false, bool own = false) {
+    auto sweep = [&](const uint32_t* ev_kid, int64_t n_keys, bool indexed = false, bool own = false,
+                     const int32_t* fan_pos = nullptr) {
       auto& gs = *gsp;
       sdh::GenLaunch L = gen_launch_base(e, gs, B, write);
       L.a32 = gs.a32.p;
@@ -2382,6 +2453,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       L.sweep = 1;
       L.ev_kid = ev_kid;
       L.n_keys = n_keys;
+      L.fan_pos = fan_pos;
       if (indexed) {
         L.pm = e->t_pm.p;
         if (own) {  // the keys' own events: the routed segments
@@ -2401,17 +2473,21 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       // indexed: each key reads its own events and binary-searches pm per timer stop
       bytes += (double)n * ev_bytes * gs.n_groups * (indexed ? 1.0 : (double)n_keys);
     };
+    // a stream the partition does not key reaches every known key's clones (PartitionStreamReceiver
+    // .send(ComplexEvent):277-281), ordered by the junction map (fan_positions)
+    const kg::LFanOut* fo = n > 0 && attr < 0 && gsp && gsp->n_groups > 0 ? pd.fan(stream) : nullptr;
     if (n == 0 || attr < 0) {
-      if (timed) {
+      if (timed || fo) {
         int32_t nk = 0;
         HIPCHK(hipMemcpyAsync(&nk, rt.n_keys.p, 4, hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
-        const bool ix = ordered();
-        sweep(nullptr, std::min<int64_t>(nk, gsp->key_cap), ix, false);
+        const int64_t nks = std::min<int64_t>(nk, gsp->key_cap);
+        if (fo) sweep(nullptr, nks, false, false, fan_positions(e, rt, *fo, nks));
+        else sweep(nullptr, nks, ordered(), false);
       }
       continue;
     }
-    bool reads = gsp && gsp->n_groups > 0;
+    bool reads = (gsp && gsp->n_groups > 0) || rt.track;  // (fan-out: every key's creation counts)
     for (auto& ps : e->psets)
       if (ps->partition == pi) reads = true;
     for (auto& ss : e->ssets)
@@ -2448,6 +2524,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       if ((int)e->part_kept.size() <= pi) e->part_kept.resize(pi + 1, 0);
       e->part_kept[pi] = n - (last_kid == 0xFFFFFFFFu ? last_cnt : 0);
     }
+    if (rt.track && hv[0] > rt.nk_seen) track_new_keys(e, rt, hv[0], hv[1], type == kg::T_BOOL);
     // routing (key column read, key/kid/idx written and sorted)
     bytes += (double)n * (8 + 8 + 4 + 4 + 2 * (4 + 4) + 3 * 4);
     if (gsp && gsp->n_groups > 0 && timed) {
@@ -3126,10 +3203,25 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     // device ranks are out_rank + 1: rank 0 orders the absent states' timer matches before the
     // triggering event's own
     e->d_out_rank.ensure(std::max<size_t>(1, e->out_rank.size()));
+    e->d_fan_rank.ensure(std::max<size_t>(1, e->out_rank.size()));
     if (!e->out_rank.empty()) {
-      std::vector<int32_t> r1(e->out_rank.size());
+      std::vector<int32_t> r1(e->out_rank.size()), fr(e->out_rank.size(), -1);
       for (size_t k = 0; k < r1.size(); ++k) r1[k] = e->out_rank[k] + 1;
+      // fan-out (query, stream): the partition's first rank for that stream, and the query's rank
+      // within it as a tiebreak below the key's junction-map position (the key-major order of
+      // PartitionStreamReceiver.send(ComplexEvent))
+      const size_t ns = e->prog.stream_types.size();
+      for (const auto& pd : e->lp.parts)
+        for (const auto& f : pd.fanout) {
+          int base = INT32_MAX;
+          for (int pq : pd.queries) base = std::min(base, e->out_rank[(size_t)pq * ns + f.stream]);
+          for (int pq : pd.queries) {
+            fr[(size_t)pq * ns + f.stream] = e->out_rank[(size_t)pq * ns + f.stream] - base;
+            r1[(size_t)pq * ns + f.stream] = base + 1;
+          }
+        }
       HIPCHK(hipMemcpy(e->d_out_rank.p, r1.data(), r1.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(e->d_fan_rank.p, fr.data(), fr.size() * 4, hipMemcpyHostToDevice));
     }
     std::vector<int32_t> qinfo(std::max<size_t>(1, 2 * nq_all), 0);
     for (size_t q = 0; q < nq_all; ++q) {
@@ -3335,7 +3427,7 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
 // then per query
 // header + table, ratchet deques, K_gen arenas + key tables, K_seq tails
 constexpr int64_t SNAP_MAGIC = 0x5344485350415254LL;
-constexpr int64_t SNAP_VERSION = 6;
+constexpr int64_t SNAP_VERSION = 7;
 // Device memory of the sparse K_slab state: the live blocks' bytes, the slab's reserved bytes (live
 // blocks, not yet reclaimed superseded ones, and free room) and the directory's
 int sdh_engine_state_bytes(sdh_engine* e, int64_t* live_bytes, int64_t* reserved_bytes, int64_t* dir_bytes) {
@@ -3430,6 +3522,14 @@ int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
       put_dev(rp->tid.p, slots * 4);
       put_dev(rp->n_keys.p, 4);
       put_dev(rp->key_of_id.p, (size_t)rp->max_keys * 8);
+      // fan-out partitions: the keys' creation order (the junction maps' insertion order)
+      w.push_back(rp->kbool ? 1 : 0);
+      w.push_back(rp->nk_seen);
+      w.push_back((int64_t)rp->korder_kid.size());
+      for (size_t j = 0; j < rp->korder_kid.size(); ++j) {
+        w.push_back(rp->korder_kid[j]);
+        w.push_back(rp->korder_key[j]);
+      }
     }
     // K_part tables: both buffers and the per-key selector
     w.push_back((int64_t)e->psets.size());
@@ -3601,6 +3701,17 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
       get_dev(rp->tid.p, slots * 4);
       get_dev(rp->n_keys.p, 4);
       get_dev(rp->key_of_id.p, (size_t)rp->max_keys * 8);
+      rp->kbool = nx() != 0;
+      rp->nk_seen = nx();
+      const int64_t nko = nx();
+      if (nko < 0 || nko > rp->max_keys) throw Error(SDH_E_INVALID, "bad snapshot key order");
+      rp->korder_kid.resize((size_t)nko);
+      rp->korder_key.resize((size_t)nko);
+      for (int64_t j = 0; j < nko; ++j) {
+        rp->korder_kid[(size_t)j] = nx();
+        rp->korder_key[(size_t)j] = nx();
+      }
+      rp->fan.clear();
     }
     if ((size_t)nx() != e->psets.size()) throw Error(SDH_E_INVALID, "snapshot of a different program");
     for (auto& pp : e->psets) {

@@ -47,9 +47,20 @@ struct LPartKey {
   int stream;
   LCode code;
 };
+struct LFanOut {  // a stream the partition's queries read but no key covers (every key sees it)
+  int stream;
+  int32_t id_hash;  // String.hashCode of the stream id
+  int id_len;
+};
 struct LPart {
   std::vector<LPartKey> keys;
   std::vector<int> queries;
+  std::vector<LFanOut> fanout;
+  const LFanOut* fan(int stream) const {
+    for (const auto& f : fanout)
+      if (f.stream == stream) return &f;
+    return nullptr;
+  }
 };
 struct LProgram {
   std::vector<std::vector<int>> stream_types;
@@ -139,7 +150,25 @@ inline LProgram read_program(const void* blob, size_t len) {
     pd.queries.resize((size_t)nx());
     for (auto& x : pd.queries) x = (int)nx();
   }
+  if (i < n)  // trailer: the partitions' fan-out streams
+    for (auto& pd : p.parts) {
+      pd.fanout.resize((size_t)nx());
+      for (auto& f : pd.fanout) {
+        f.stream = (int)nx();
+        f.id_hash = (int32_t)nx();
+        f.id_len = (int)nx();
+      }
+    }
   return p;
+}
+
+// a partition query that reads a fan-out stream (it runs on K_gen)
+inline bool reads_fanout(const LProgram& P, int qi) {
+  const int pi = P.q[qi].partition;
+  if (pi < 0) return false;
+  for (const auto& s : P.q[qi].st)
+    if (P.parts[pi].fan(s.stream)) return true;
+  return false;
 }
 
 enum { N_STREAM = 0, N_NEXT, N_EVERY, N_LOGICAL, N_COUNT };

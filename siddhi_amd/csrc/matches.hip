@@ -113,86 +113,62 @@ __global__ __launch_bounds__(256) void digest_ratchet_kernel(const int64_t* __re
 }
 
 // ---- K_ratchet direct R18 placement (a push whose matches all come from K_ratchet) ----
-// A block holds one wave's records (one group of up to 64 queries, one per lane) in emission order:
-// events ascending; for one event (its run) by pop level, each level's lanes ascending (ballot
-// compaction), level 0 the newest partial. A run may continue from the wave's previous block
-// (blk_prev). R18 wants per event the queries in receiver-rank order and per query its partials in
-// pending-list order (e1 seq ascending = pop level descending). Pass 1 adds, per (event, query
-// rank) cell, the query's records of each block's run; an exclusive scan over the cells gives each
-// cell's first row; pass 2 writes a record of level L (the lane's earlier records at that event, in
-// this block and in the wave's previous blocks) to
-//   row0 + base[cell] + count[cell] - 1 - L
-// as the ABI tuples, in place: no sort, one read of the records, one write of the outputs (plus the
-// count matrix: 4 B per (event, query) cell).
-constexpr int PLACE_RECS = 8192;  // block records a workgroup stages in LDS (the host checks blk_recs)
-
-template <bool PLACE>
+// R18 wants per event the queries in receiver-rank order and per query its partials in pending-list
+// order (e1 seq ascending = pop level descending, level 0 the newest partial). K_ratchet's PLACE
+// variant (nfa_ratchet.hip) stored each (event, query rank) cell's match count and each record's
+// pop level; an exclusive scan over the cells gives each cell's first row, and a record of level L
+// goes to
+//   P = row0 + base[cell] + count[cell] - 1 - L = row0 + base[cell + 1] - 1 - L.
+// Two passes, no sort. Scattered 8-B stores would each dirty a separate 32-B sector of six output
+// columns, so pass 1 (record order) writes only the row's aligned 32-B word quadruple, carrying the
+// query in place of its first count word: {q, e1 seq, 1, e2 seq}; pass 2 (row order, coalesced)
+// reads it back and writes every ABI column of the row.
 __global__ __launch_bounds__(256) void ratchet_place_kernel(
     const int64_t* __restrict__ match, int blk_recs, const int32_t* __restrict__ blk_count,
-    const int32_t* __restrict__ blk_group, const int32_t* __restrict__ blk_prev, int64_t rows,
-    const int32_t* __restrict__ out_rank, int n_streams, int n_ranks, int64_t cells, int32_t* __restrict__ cnt,
-    const RatchetGroup* __restrict__ groups, const int64_t* __restrict__ ts, int64_t seq_base, int64_t row0,
-    int64_t* __restrict__ oq, int64_t* __restrict__ okey, int64_t* __restrict__ ots, int64_t* __restrict__ oseq,
-    int64_t* __restrict__ otb, int64_t* __restrict__ ooff, int64_t* __restrict__ owords) {
-  __shared__ uint32_t rx[PLACE_RECS];
+    const int32_t* __restrict__ blk_group, int64_t rows, const int32_t* __restrict__ out_rank, int n_streams,
+    int n_ranks, int64_t cells, const int32_t* __restrict__ base, const RatchetGroup* __restrict__ groups,
+    int64_t seq_base, int64_t row0, int64_t* __restrict__ owords) {
+  __shared__ int32_t s_q[64], s_rank[64];
   const int b = blockIdx.x;
   const int n = blk_count[b];
   const RatchetGroup* G = groups + blk_group[b];
-  const uint2* R = reinterpret_cast<const uint2*>(match) + (size_t)b * blk_recs;
-  constexpr uint32_t OFF = (1u << 26) - 1;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) rx[i] = R[i].x;
-  __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint32_t x = rx[i], off = x & OFF, lane = x >> 26;
-    int lo = 0, hi = i;  // run start: first record of this event in the block (records ascend by event)
-    while (lo < hi) {
-      const int m = (lo + hi) >> 1;
-      if ((rx[m] & OFF) < off) lo = m + 1;
-      else hi = m;
-    }
-    const int a = lo;
-    const int q = G->qid[lane];
-    const int64_t cell = (int64_t)off * n_ranks + (out_rank[(int64_t)q * n_streams + G->stream] - 1);
-    if constexpr (!PLACE) {
-      bool last = true;  // the lane's last record of the run in this block adds the block's count
-      int c = 0;
-      for (int k = a; k < n && (rx[k] & OFF) == off; ++k) {
-        const bool same = (rx[k] >> 26) == lane;
-        c += same ? 1 : 0;
-        if (k > i && same) last = false;
-      }
-      if (last) atomicAdd(&cnt[cell], c);
-    } else {
-      int level = 0;  // the lane's records at this event emitted before this one
-      for (int k = a; k < i; ++k) level += (rx[k] >> 26) == lane ? 1 : 0;
-      if (a == 0) {  // the run may have begun in the wave's previous block(s)
-        for (int pb = blk_prev[b]; pb >= 0; pb = blk_prev[pb]) {
-          const uint2* PR = reinterpret_cast<const uint2*>(match) + (size_t)pb * blk_recs;
-          int k = blk_count[pb] - 1;
-          for (; k >= 0; --k) {
-            const uint32_t y = PR[k].x;
-            if ((y & OFF) != off) break;
-            level += (y >> 26) == lane ? 1 : 0;
-          }
-          if (k >= 0) break;  // the run began in that block
-        }
-      }
-      const int64_t base = cnt[cell], next = cell + 1 < cells ? (int64_t)cnt[cell + 1] : rows;
-      const int64_t P = row0 + next - 1 - level;
-      (void)base;
-      const uint32_t q1 = R[i].y;
-      const int64_t s = seq_base + (int64_t)off;
-      const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
-      oq[P] = q;
-      okey[P] = -1;
-      ots[P] = ts[off];
-      oseq[P] = s;
-      otb[P] = INT64_MIN;
-      ooff[P] = 4 * P;
-      reinterpret_cast<longlong2*>(owords + 4 * P)[0] = make_longlong2(1, s1);
-      reinterpret_cast<longlong2*>(owords + 4 * P)[1] = make_longlong2(1, s);
-    }
+  if (threadIdx.x < 64) {
+    const int q = threadIdx.x < G->n_lanes ? G->qid[threadIdx.x] : 0;
+    s_q[threadIdx.x] = q;
+    s_rank[threadIdx.x] = out_rank[(int64_t)q * n_streams + G->stream] - 1;
   }
+  __syncthreads();
+  const uint4* R = reinterpret_cast<const uint4*>(match) + (size_t)b * blk_recs;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint4 r = R[i];
+    const uint32_t off = r.x, lane = r.y & 63, q1 = r.z, level = r.w;
+    const int64_t cell = (int64_t)off * n_ranks + s_rank[lane];
+    const int64_t next = cell + 1 < cells ? (int64_t)base[cell + 1] : rows;
+    const int64_t P = row0 + next - 1 - (int64_t)level;
+    const int64_t s = seq_base + (int64_t)off;
+    const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
+    reinterpret_cast<longlong2*>(owords + 4 * P)[0] = make_longlong2(s_q[lane], s1);
+    reinterpret_cast<longlong2*>(owords + 4 * P)[1] = make_longlong2(1, s);
+  }
+}
+
+__global__ __launch_bounds__(256) void placed_fill_kernel(int64_t row0, int64_t rows, const int64_t* __restrict__ ts,
+                                                          int64_t seq_base, int64_t* __restrict__ oq,
+                                                          int64_t* __restrict__ okey, int64_t* __restrict__ ots,
+                                                          int64_t* __restrict__ oseq, int64_t* __restrict__ otb,
+                                                          int64_t* __restrict__ ooff, int64_t* __restrict__ owords) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows) return;
+  const int64_t P = row0 + i;
+  longlong2* w = reinterpret_cast<longlong2*>(owords + 4 * P);
+  const longlong2 a = w[0], b = w[1];
+  oq[P] = a.x;
+  okey[P] = -1;
+  ots[P] = ts[b.y - seq_base];
+  oseq[P] = b.y;
+  otb[P] = INT64_MIN;
+  ooff[P] = 4 * P;
+  w[0] = make_longlong2(1, a.y);
 }
 
 // placed rows [0, n) -> general table rows (a later push in the same poll window has other producers)
@@ -252,7 +228,8 @@ __global__ __launch_bounds__(256) void append_chain_kernel(
 __global__ __launch_bounds__(256) void append_gen_kernel(const int64_t* __restrict__ out,
                                                          const int64_t* __restrict__ rec_off, int64_t n_rec,
                                                          int64_t seq_ref, const int32_t* __restrict__ out_rank,
-                                                         int n_streams, MatchTable T, int64_t row0, int64_t word0) {
+                                                         const int32_t* __restrict__ fan_rank, int n_streams,
+                                                         MatchTable T, int64_t row0, int64_t word0) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_rec) return;
   const int64_t o = rec_off[i];
@@ -269,6 +246,13 @@ __global__ __launch_bounds__(256) void append_gen_kernel(const int64_t* __restri
     T.lo[2][row] = (uint64_t)r[5] ^ 0x8000000000000000ull;
     T.lo[1][row] = (uint64_t)(uint32_t)q;
     T.lo[0][row] = (uint64_t)r[2] ^ 0x8000000000000000ull;
+  } else if (fan_rank && fan_rank[(int64_t)q * n_streams + stream] >= 0) {
+    // a fan-out stream's match (PartitionStreamReceiver.send(ComplexEvent)): the partition's
+    // rank, then the key's junction-map position, the query's rank in the partition, emission
+    T.hi[row] = hi_key(r[4], seq_ref, out_rank[(int64_t)q * n_streams + stream]);
+    T.lo[2][row] = (uint64_t)r[5] >> 32;
+    T.lo[1][row] = (uint64_t)fan_rank[(int64_t)q * n_streams + stream];
+    T.lo[0][row] = (uint64_t)r[5] & 0xFFFFFFFFull;
   } else {
     T.hi[row] = hi_key(r[4], seq_ref, out_rank[(int64_t)q * n_streams + stream]);
     T.lo[0][row] = (uint64_t)r[5];
@@ -355,11 +339,11 @@ extern "C" hipError_t sdh_append_chain(const int64_t* src, const int64_t* seg_of
 }
 
 extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t seq_ref,
-                                     const int32_t* out_rank, int n_streams, MatchTable T, int64_t row0,
-                                     int64_t word0, hipStream_t s) {
+                                     const int32_t* out_rank, const int32_t* fan_rank, int n_streams, MatchTable T,
+                                     int64_t row0, int64_t word0, hipStream_t s) {
   if (n_rec <= 0) return hipSuccess;
   hipLaunchKernelGGL(sdh::append_gen_kernel, dim3(sdh::grid(n_rec, 256)), dim3(256), 0, s, out, rec_off, n_rec,
-                     seq_ref, out_rank, n_streams, T, row0, word0);
+                     seq_ref, out_rank, fan_rank, n_streams, T, row0, word0);
   return hipGetLastError();
 }
 
@@ -379,29 +363,24 @@ extern "C" size_t sdh_place_temp_bytes(int64_t cells) {
   (void)hipcub::DeviceScan::ExclusiveSum((void*)nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, (int)cells);
   return b + 256;
 }
+// cnt: the (event, rank) match counts K_ratchet's PLACE variant stored (scanned in place)
 extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, const int32_t* blk_count,
-                                        const int32_t* blk_group, const int32_t* blk_prev, int n_blocks,
-                                        int64_t rows, const int32_t* out_rank, int n_streams, int n_ranks,
-                                        int64_t n_events, int32_t* cnt, int32_t* flag, void* temp,
+                                        const int32_t* blk_group, int n_blocks, int64_t rows, const int32_t* out_rank,
+                                        int n_streams, int n_ranks, int64_t n_events, int32_t* cnt, void* temp,
                                         size_t temp_bytes, const sdh::RatchetGroup* groups, const int64_t* ts,
                                         int64_t seq_base, int64_t row0, int64_t* oq, int64_t* okey, int64_t* ots,
                                         int64_t* oseq, int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s) {
   using namespace sdh;
-  (void)flag;
   if (n_blocks <= 0) return hipSuccess;
-  if (blk_recs > PLACE_RECS) return hipErrorNotSupported;
   const int64_t cells = n_events * n_ranks;
-  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)cells * 4, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(ratchet_place_kernel<false>, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, blk_count, blk_group,
-                     blk_prev, rows, out_rank, n_streams, n_ranks, cells, cnt, groups, ts, seq_base, row0, oq, okey,
-                     ots, oseq, otb, ooff, owords);
   size_t tb = temp_bytes;
-  e = hipcub::DeviceScan::ExclusiveSum(temp, tb, cnt, cnt, (int)cells, s);
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, tb, cnt, cnt, (int)cells, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(ratchet_place_kernel<true>, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, blk_count, blk_group,
-                     blk_prev, rows, out_rank, n_streams, n_ranks, cells, cnt, groups, ts, seq_base, row0, oq, okey,
-                     ots, oseq, otb, ooff, owords);
+  hipLaunchKernelGGL(ratchet_place_kernel, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, blk_count, blk_group,
+                     rows, out_rank, n_streams, n_ranks, cells, cnt, groups, seq_base, row0, owords);
+  if (rows > 0)
+    hipLaunchKernelGGL(placed_fill_kernel, dim3(grid(rows, 256)), dim3(256), 0, s, row0, rows, ts, seq_base, oq, okey,
+                       ots, oseq, otb, ooff, owords);
   return hipGetLastError();
 }
 

@@ -107,6 +107,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   const int ncap = q->n_cap[c.stream];
   unsigned long long nrec = 0;
   int64_t idx = 0;
+  const int64_t fpos = L.fan_pos ? (int64_t)L.fan_pos[kid] << 32 : 0;
   bool live = true;
   // a match record [len, qid, key, ts, trigger seq, idx, S | stream << 16, (count, seqs...) x S];
   // a timer's record carries stream 0xFFFF and its sort time (kgen.h fire_timers) in idx
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
       r[5] = cx.timer_ts;
       r[6] = S | (0xFFFFll << 16);
     } else {
-      r[5] = idx++;
+      r[5] = fpos | idx++;
       r[6] = S | (c.stream << 16);
     }
     int w = 7;
@@ -183,7 +184,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
       live = k >= e0;
       e = L.ev_idx ? L.ev_idx[k] : k;
       ++k;
-      own = !L.sweep || (L.ev_kid && L.ev_kid[e] == kid);  // a sweep passes time at other keys' events
+      // a sweep passes time at other keys' events; a fan-out stream's events are every key's
+      own = !L.sweep || L.fan_pos || (L.ev_kid && L.ev_kid[e] == kid);
     }
     c.seq = L.b.seq_base + e;
     c.ts = L.b.ts[e];
@@ -263,6 +265,21 @@ __global__ void key_segment_kernel(const uint32_t* __restrict__ uniq, const int3
   if (s >= *nruns) return;
   const uint32_t kid = uniq[s];
   if (kid != 0xFFFFFFFFu && (int64_t)kid < n_keys) kseg[kid] = (int32_t)s;
+}
+
+// ---- keys created by this batch (ids [old_n, new_n)): their first event and value, for the
+// creation order of the fan-out junction maps (PartitionRuntime.clonePartition at the key's first
+// event) ----
+__global__ void new_keys_kernel(const uint32_t* __restrict__ uniq, const int32_t* __restrict__ nruns,
+                                const int32_t* __restrict__ off, const int32_t* __restrict__ idx_s,
+                                const int64_t* __restrict__ key_of_id, int64_t old_n, int64_t new_n,
+                                int64_t* __restrict__ out) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= *nruns) return;
+  const uint32_t kid = uniq[s];
+  if (kid == 0xFFFFFFFFu || (int64_t)kid < old_n || (int64_t)kid >= new_n) return;
+  out[2 * (kid - old_n)] = idx_s[off[s]];  // segments list a key's events in batch order
+  out[2 * (kid - old_n) + 1] = key_of_id[kid];
 }
 
 // ---- exact re-runs: the arena blocks a pass is about to modify, journaled just before it runs ----
@@ -538,7 +555,6 @@ extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, hipStream_t s) {
   return hipGetLastError();
 }
 
-// roll a stream's K_seq tail over batch b (after the push's K_seq launches have succeeded)
 // pm = inclusive prefix max of ts; *unordered (device) = 1 when ts decreases somewhere
 extern "C" size_t sdh_prefix_max_temp_bytes(int64_t n) {
   size_t b = 0;
@@ -555,6 +571,14 @@ extern "C" hipError_t sdh_prefix_max(const int64_t* ts, int64_t n, int64_t* pm, 
   size_t tb = temp_bytes;
   e = hipcub::DeviceScan::InclusiveScan(temp, tb, ts, pm, hipcub::Max(), (int)n, s);
   if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+extern "C" hipError_t sdh_new_keys(const uint32_t* uniq, const int32_t* nruns, int64_t max_runs, const int32_t* off,
+                                   const int32_t* idx_s, const int64_t* key_of_id, int64_t old_n, int64_t new_n,
+                                   int64_t* out, hipStream_t s) {
+  if (max_runs <= 0 || new_n <= old_n) return hipSuccess;
+  hipLaunchKernelGGL(sdh::new_keys_kernel, dim3((unsigned)((max_runs + 255) / 256)), dim3(256), 0, s, uniq, nruns, off,
+                     idx_s, key_of_id, old_n, new_n, out);
   return hipGetLastError();
 }
 // kseg[kid] = the routed segment of key kid in this batch, -1 without events
@@ -596,6 +620,7 @@ extern "C" hipError_t sdh_live_seq(const int64_t* tail, int tail_len, int stream
   return hipGetLastError();
 }
 
+// roll a stream's K_seq tail over batch b (after the push's K_seq launches have succeeded)
 extern "C" hipError_t sdh_seq_tail(const sdh::StreamBatch* b, int64_t* tail, int32_t tail_len, int32_t new_tail_len,
                                    hipStream_t s) {
   hipLaunchKernelGGL(sdh::seq_tail_kernel, dim3(1), dim3(64), 0, s, *b, tail, tail_len, new_tail_len);

@@ -416,7 +416,10 @@ __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {  // b >= 0
 // event key against per-lane float bounds, and NaN keys fail every compare by themselves, so the
 // per-event validity bits are not read; an empty deque's top key is NaN, so the match test needs no
 // length check; a non-pushing lane writes its LDS entry to a dummy row instead of branching.
-template <int KK, int XM, bool FULL, int NF, bool SIM = false>
+// PLACE (normal-mode pushes that qualify for the direct R18 placement, matches.hip): 16-B records
+// carry the record's pop level at its event, and every (event, lane) with matches stores its match
+// count into the (event, receiver rank) count matrix -- one plain store per cell, no atomics
+template <int KK, int XM, bool FULL, int NF, bool SIM = false, bool PLACE = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
   using U = typename KT<KK>::U;
   constexpr bool W64 = KT<KK>::W64;
@@ -742,10 +745,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
   uint2* wb = nullptr;            // the wave's current output block
   int64_t prev_tile_ts = (W.c0 == 0) ? L.b.prev_ts : L.b.ts[W.c0 - 1];
 
-  // one record per lane with `mt` (ballot m): per-wave output blocks (one atomic per block, chained
-  // to the wave's previous block for the direct R18 placement, matches.hip), ranks by mbcnt. e2 =
+  // one record per lane with `mt` (ballot m): per-wave output blocks (one atomic per block), ranks
+  // by mbcnt. e2 =
   // batch event `off`; e1 = the partial with low seq bits q1. The common case costs one
   // compare-and-branch of bookkeeping (the record index is block base + fill + rank).
+  int32_t* const pcell = PLACE && active ? L.pcnt + (L.out_rank[(int64_t)G->qid[lane] * L.n_streams + G->stream] - 1)
+                                         : nullptr;
+  uint32_t lv = 0;  // PLACE: the lane's records at the current event so far (the next one's level)
   auto emit = [&](bool mt, uint64_t m, uint32_t off, uint32_t q1) {
     const int c = __popcll(m);
     if (fill + c > L.blk_recs) {
@@ -764,19 +770,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
         fill = FULL_FILL;
         return;
       }
-      if (lane == 0) {
-        L.blk_group[nb] = W.g;
-        L.blk_prev[nb] = blk;
-      }
+      if (lane == 0) L.blk_group[nb] = W.g;
       blk = nb;
       fill = 0;
       wb = reinterpret_cast<uint2*>(L.match) + ((size_t)blk * L.blk_recs << (L.wide ? 1 : 0));
     }
     if (mt) {
       const int r = fill + wave_mbcnt(m);
-      if (!L.wide) wb[r] = make_uint2(off | ((uint32_t)lane << 26), q1);
-      else reinterpret_cast<uint4*>(wb)[r] = make_uint4(off, (uint32_t)lane, q1, 0u);
+      if (!PLACE && !L.wide) wb[r] = make_uint2(off | ((uint32_t)lane << 26), q1);
+      else reinterpret_cast<uint4*>(wb)[r] = make_uint4(off, (uint32_t)lane, q1, PLACE ? lv : 0u);
     }
+    if constexpr (PLACE) lv += mt ? 1u : 0u;
     fill += c;
   };
 
@@ -844,6 +848,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
       // ---- 2. matches: the newest partials whose key satisfies `cur OP key` ----
       bool mt = SIM ? xop<KK, XM>(xmask, x, tkey) : (x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey));
       uint64_t m = __ballot(mt);
+      if constexpr (PLACE) lv = 0;
       while (m) {
         // the three LDS entries under the top, read unconditionally (in-bounds ring slots)
         const int topl = D.lbot + D.ln - 1;
@@ -884,6 +889,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
         mt = SIM ? (fix && xop<KK, XM>(xmask, x, tkey)) : (fix && x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey));
         m = __ballot(mt);
       }
+      if constexpr (PLACE)
+        if (lv) pcell[(int64_t)(t + k) * L.n_ranks] = (int32_t)lv;  // (lanes with matches are active)
 
       // ---- 3. start state: every event passing f0 opens a partial (pending from j+1) ----
       bool f;
@@ -1017,6 +1024,13 @@ template <int KK, int XM, bool FULL, int NF, bool SIM = false>
 static void launch_one(const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {
   const bool w64 = (KK == sdh::KK_F64 || KK == sdh::KK_I64);
   const size_t lds = (size_t)(ML + (SIM ? 1 : 0)) * 64 * (w64 ? 16 : 8);  // (SIM: + the dummy row)
+  if constexpr (!FULL) {
+    if (L->pcnt) {
+      hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM, true>), dim3(L->n_items), dim3(64), lds, s, *L,
+                         ML, SC);
+      return;
+    }
+  }
   hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM>), dim3(L->n_items), dim3(64), lds, s, *L, ML, SC);
 }
 

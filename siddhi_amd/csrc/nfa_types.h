@@ -197,12 +197,11 @@ struct RatchetLaunch {
   uint32_t* spillB;             //   (seq words of 64-bit-key entries)
   // match records, in per-wave blocks of blk_recs records. Narrow (wide == 0, batches of at most
   // 2^26 events): 8 B {e2 batch offset | lane << 26, low 32 bits of e1's seq}; wide: 16 B
-  // {e2 batch offset, lane, low 32 bits of e1's seq, 0}. The block's group is blk_group[block];
+  // {e2 batch offset, lane, low 32 bits of e1's seq, pop level (placement) or 0}. The block's group is blk_group[block];
   // sdh_launch_ratchet_decode expands records to (qid, ts, seq1, seq2)
   int64_t* match;
   int32_t* blk_count;           // records written per block
   int32_t* blk_group;           // group of the wave that owns the block
-  int32_t* blk_prev;            // the wave's previous block (-1: its first), for the direct R18 placement
   int32_t* blk_next;            // [0] next free block
   int32_t n_blocks, blk_recs;
   int32_t wide;
@@ -210,6 +209,11 @@ struct RatchetLaunch {
                                 //   written, none is read back); rec_total counts them
   unsigned long long* rec_total;
   int32_t* err;                 // [0] deque overflow, [1] unordered ts, [2] match overflow
+  // direct R18 placement (non-null pcnt; wide records, w = the record's pop level at its event):
+  // pcnt[event * n_ranks + out_rank(query, stream) - 1] = the query's matches at that event
+  int32_t* pcnt;
+  const int32_t* out_rank;
+  int32_t n_ranks, n_streams;
 };
 
 // ------------------------------------------------------------------------------------------
@@ -278,6 +282,10 @@ struct GenLaunch {
   int32_t sweep;
   const uint32_t* ev_kid;
   int64_t n_keys;
+  // fan-out (a stream the partition does not key; with sweep): every event is every key's own; a
+  // match record's idx word carries the key's position in the reference's junction map
+  // (chm_order.h) above the emission index: fan_pos[kid] << 32 | idx
+  const int32_t* fan_pos;
 };
 
 // ------------------------------------------------------------------------------------------

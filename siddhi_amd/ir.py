@@ -147,6 +147,9 @@ class PartitionKeyIR:
 class PartitionIR:
     keys: List[PartitionKeyIR]
     query_idx: List[int]
+    # streams its queries read but no key covers: (stream, String.hashCode of the stream id, id
+    # length) -- every event reaches every key's instance (the order: PartitionStreamReceiver.send)
+    fanout: List[tuple] = field(default_factory=list)
 
 
 @dataclass
@@ -248,4 +251,9 @@ class ProgramIR:
                 code(k.code)
             w.append(len(p.query_idx))
             w.extend(p.query_idx)
+        # trailer (readers that predate it stop before it): per partition its fan-out streams
+        for p in self.partitions:
+            w.append(len(p.fanout))
+            for f in p.fanout:
+                w.extend(f)
         return MAGIC + struct.pack(f"<{len(w)}q", *w)

@@ -542,6 +542,15 @@ def _plan_chain(pb: "_ProgramBuilder", c: ql.PlainQuery, src: QueryIR) -> ChainI
     return ChainIR(c.name, c.stream, [o.type for o in src.outputs], filters, outputs, c.output_stream or "")
 
 
+def java_string_hash(s: str) -> int:
+    """java.lang.String.hashCode over the UTF-16 code units (int32 wrap)."""
+    h = 0
+    data = s.encode("utf-16-le")
+    for k in range(0, len(data), 2):
+        h = (31 * h + (data[k] | data[k + 1] << 8)) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= 1 << 31 else h
+
+
 def plan(app: ql.App) -> ProgramIR:
     """Lower a parsed app to the pattern IR."""
     pb = _ProgramBuilder(app)
@@ -572,14 +581,24 @@ def plan(app: ql.App) -> ProgramIR:
             if len(kclass) > 1:
                 raise SiddhiAppCreationException("mixed-type partition keys are not supported")
             qidx = []
+            fanout = []
             pattern_qs, chain_qs = _plan_inner_streams(app, obj, part_streams)
             for q in pattern_qs:
                 qp = _QueryPlanner(pb, q, pidx)
                 qir = qp.build()
                 for st in qir.states:
-                    if pb.streams[st.stream_idx].name not in part_streams:
+                    name = pb.streams[st.stream_idx].name
+                    if name in part_streams or st.stream_idx in [f[0] for f in fanout]:
+                        continue
+                    # a stream the partition does not key reaches every key's instance, in the order
+                    # of its receiver's ConcurrentHashMap of "streamId + key" junctions
+                    # (PartitionStreamReceiver.java:271-275); the engine restates that order for
+                    # String.valueOf of int / long / bool keys
+                    if kclass - {"num", T_BOOL}:
                         raise SiddhiAppCreationException(
-                            "non-partitioned streams inside a partition are not on the accelerated path")
+                            "a non-partitioned stream inside a partition keyed by string / float / double "
+                            "values is not on the accelerated path")
+                    fanout.append((st.stream_idx, java_string_hash(name), len(name)))
                 qidx.append(len(queries))
                 queries.append(qir)
             for c in chain_qs:
@@ -587,7 +606,7 @@ def plan(app: ql.App) -> ProgramIR:
                 chains.append(_plan_chain(pb, c, src[0]))
                 if any([o.type for o in s.outputs] != chains[-1].input_types for s in src[1:]):
                     raise SiddhiAppCreationException(f"producers of '{c.stream}' disagree on its schema")
-            partitions.append(PartitionIR(keys, qidx))
+            partitions.append(PartitionIR(keys, qidx, fanout))
     names = [q.name for q in queries]
     if len(set(names)) != len(names):
         raise SiddhiAppCreationException("duplicate query names")

@@ -277,3 +277,49 @@ def random_slab_events(seed, n=600, keys=4):
             row[int(rng.integers(1, 4))] = None
         ev.append((SLAB_STREAMS[int(rng.integers(0, len(SLAB_STREAMS)))], row, t))
     return ev
+
+
+# ---- a stream the partition does not key (fan-out to every key's instances in the reference's
+# ConcurrentHashMap order, PartitionStreamReceiver.java:277-281) ----
+FAN_STREAMS = ("define stream A (k {kt}, v int, p float, s string); "
+               "define stream B (k int, v int, p float, s string);")
+
+
+def fanout_app(seed, key_type="int"):
+    """Partition keyed by A.k only; its patterns read B too (every key's instance sees every B
+    event): starts on A or on B, 2-3 states, cross-references, within, a sequence."""
+    rng = random.Random(seed)
+    qs = [FAN_STREAMS.format(kt=key_type), "partition with (k of A) begin"]
+    forms = [
+        "from every e1=A[v > {a}] -> e2=B[p > e1.p] within {w} milliseconds",
+        "from e1=A[v < {a}] -> e2=B[v == e1.v or v > 8]",
+        "from every e1=B[v > {a}] -> e2=A[p < e1.p] within {w} milliseconds",
+        "from every e1=A[v > {a}], e2=B[v >= {b}]",
+        "from every e1=B[v > {a}] -> e2=B[v < e1.v] -> e3=A[v > {b}] within {w} milliseconds",
+        "from every e1=A[v > {a}] -> e2=B[v > {b}] or e3=A[v < {b}] within {w} milliseconds",
+    ]
+    picks = rng.sample(range(len(forms)), 4)
+    for qn, f in enumerate(picks):
+        body = forms[f].format(a=rng.randint(1, 7), b=rng.randint(1, 7), w=rng.randint(5, 40))
+        qs.append(f"@info(name='f{qn}') {body} select e1.v as x insert into O;")
+    qs.append("end;")
+    return " ".join(qs)
+
+
+def fanout_events(seed, n=600, keys=40, key_type="int"):
+    rng = np.random.default_rng(seed)
+    out, t = [], 0
+    for _ in range(n):
+        t += int(rng.integers(0, 3))
+        k = int(rng.integers(0, keys))
+        if key_type == "long":
+            k = k * 1_000_003 - 7_000_000_000 if k % 2 else k
+        elif key_type == "bool":
+            k = bool(k % 2)
+        row = [k, int(rng.integers(0, 10)), float(np.float32(rng.integers(0, 20) / 2.0)),
+               str(rng.choice(list("xyz")))]
+        st = "A" if rng.random() < 0.6 else "B"
+        if st == "B":
+            row[0] = int(rng.integers(0, 5))  # (B.k is an int nobody partitions by)
+        out.append((st, row, t))
+    return out

@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "../../siddhi_amd/csrc/chm_order.h"
 #include "../../siddhi_amd/csrc/gen_lower.h"
 
 using namespace sdh::kg;
@@ -19,6 +20,7 @@ namespace {
 struct Rec {
   int64_t seq, rank, idx;
   int64_t tts = 0;  // timer records (rank -1): the timer's time, ordered before idx
+  int64_t fpos = -1, frank = 0;  // fan-out records: the key's map position, the query's rank in it
   int64_t query, key, ts;
   std::vector<std::vector<int64_t>> slots;
 };
@@ -38,6 +40,8 @@ struct Host {
   std::vector<int> rank;
   std::vector<std::unique_ptr<Inst>> top;                       // unpartitioned instances
   std::vector<std::map<int64_t, std::vector<std::unique_ptr<Inst>>>> part;
+  std::vector<std::vector<int64_t>> korder;  // per partition: keys in creation order
+  std::vector<char> kbool;                   //   bool-valued keys
   std::vector<Rec> out;
   std::string err;
   int64_t chunk_len = 0;  // >0: unpartitioned instances with a bounded look-back run event chunks
@@ -78,7 +82,7 @@ Inst* make_inst(Host* h, int qi, int64_t key) {
 // run one event through one instance (what one lane does for one event): the absent states'
 // timers due by the event fire first (nfa_gen.hip); event == false: only time passes, to `upto`
 void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* vals, const uint8_t* nulls,
-         bool live = true, bool event = true, int64_t upto = 0) {
+         bool live = true, bool event = true, int64_t upto = 0, int64_t fpos = -1) {
   const GQuery& q = h->gq[in->qi];
   Ctx c{};
   c.bind(&q, &q);
@@ -128,6 +132,14 @@ void run(Host* h, Inst* in, int stream, int64_t seq, int64_t ts, const int64_t* 
     } else {
       r.rank = h->rank[(size_t)in->qi * h->P.stream_types.size() + stream];
       r.idx = idx++;
+      if (fpos >= 0) {  // fan-out: (partition's first rank, key position, rank in the partition)
+        const int ns = (int)h->P.stream_types.size();
+        int base = r.rank;
+        for (int pq : h->P.parts[h->P.q[in->qi].partition].queries) base = std::min(base, h->rank[(size_t)pq * ns + stream]);
+        r.frank = r.rank - base;
+        r.rank = base;
+        r.fpos = fpos;
+      }
     }
     r.query = in->qi;
     r.key = in->key;
@@ -154,6 +166,8 @@ void sort_out(Host* h) {
     if (a.rank == -1 && a.tts != b.tts) return a.tts < b.tts;
     if (a.rank == -1 && a.query != b.query) return a.query < b.query;
     if (a.rank == -1 && a.key != b.key) return a.key < b.key;
+    if (a.fpos != b.fpos) return a.fpos < b.fpos;
+    if (a.frank != b.frank) return a.frank < b.frank;
     return a.idx < b.idx;
   });
 }
@@ -176,6 +190,8 @@ void* kgh_create(const void* blob, size_t len, int R, int N, int LC) {
     for (int qi = 0; qi < (int)h->P.q.size(); ++qi)
       if (h->P.q[qi].partition < 0) h->top[qi].reset(make_inst(h, qi, -1));
     h->part.resize(h->P.parts.size());
+    h->korder.resize(h->P.parts.size());
+    h->kbool.resize(h->P.parts.size(), 0);
     return h;
   } catch (const std::exception&) {
     return nullptr;
@@ -257,6 +273,18 @@ int kgh_send(void* hp, int stream, int64_t n, int64_t seq0, const int64_t* ts, c
       int attr = -1;
       for (const auto& key : pd.keys)
         if (key.stream == stream) attr = (int)key.code[0].imm;
+      if (const LFanOut* fo = pd.fan(stream)) {  // every key's instances, in the map's order
+        std::vector<int32_t> hs;
+        for (int64_t kv : h->korder[pi])
+          hs.push_back(sdh::java_hash_cat(fo->id_hash, sdh::java_value_of(h->kbool[pi] != 0, kv)));
+        const std::vector<int32_t> pos = sdh::ChmOrder().positions(hs);
+        for (int64_t k = 0; k < n; ++k)
+          for (size_t j = 0; j < h->korder[pi].size(); ++j)
+            for (auto& in : h->part[pi].at(h->korder[pi][j]))
+              run(h, in.get(), stream, seq0 + k, ts[k], vals + k * na, nulls ? nulls + k * na : nullptr, true, true, 0,
+                  pos[j]);
+        continue;
+      }
       for (int64_t k = 0; k < n; ++k) {
         bool has_key = attr >= 0 && !(nulls && nulls[k * na + attr]);  // a null key drops the event
         int64_t kv = 0;
@@ -266,6 +294,8 @@ int kgh_send(void* hp, int stream, int64_t n, int64_t seq0, const int64_t* ts, c
             std::vector<std::unique_ptr<Inst>> v;
             for (int pq : pd.queries) v.emplace_back(make_inst(h, pq, kv));
             h->part[pi].emplace(kv, std::move(v));
+            h->korder[pi].push_back(kv);
+            h->kbool[pi] = h->P.stream_types[stream][attr] == T_BOOL;
           }
         }
         for (auto& kvp : h->part[pi])

@@ -199,3 +199,19 @@ def test_kgen_host_c5_family():
     o = run_c5(32, 200, 1500, 500)
     g = run_c5(32, 200, 1500, 500, engine_factory=lambda blob: KGenHostEngine(blob, R=4096, N=4096, LC=4096))
     assert g.matches == o.matches and len(o.matches) > 100
+
+
+@pytest.mark.parametrize("key_type", ["int", "long", "bool"])
+@pytest.mark.parametrize("seed", range(8))
+def test_kgen_host_fanout(seed, key_type):
+    """A stream the partition does not key reaches every key's instances in the order of the
+    reference's ConcurrentHashMap of "streamId + key" (chm_order.h vs the oracle's own restatement):
+    up to 60 keys, so the map resizes past 64 bins and bins collide."""
+    from fuzz_apps import fanout_app, fanout_events
+    src = fanout_app(seed, key_type)
+    o, g = App(src), App(src, engine_factory=lambda blob: KGenHostEngine(blob, R=4096, N=4096, LC=4096))
+    for stream, row, t in fanout_events(seed, keys=20 + 5 * seed, key_type=key_type):
+        o.send(stream, [row], [t])
+        g.send(stream, [row], [t])
+    assert len(o.matches) > 20
+    assert g.matches == o.matches

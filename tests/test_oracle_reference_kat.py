@@ -3,8 +3,7 @@
 tests/golden/reference_kat.json is transcribed from the reference's TestNG suites by
 tests/golden/extract_reference_tests.py (queries, events with cumulative-sleep timestamps,
 hand-asserted expected rows and counts). Fixtures that use features outside the accelerated path
-(absent patterns, having, inner streams, plain queries, non-partitioned streams inside a
-partition) must be rejected at plan time rather than mis-executed."""
+(having, plain queries) must be rejected at plan time rather than mis-executed.""" 
 import json
 import os
 
@@ -16,7 +15,6 @@ from siddhi_amd.ql import SiddhiAppCreationException, SiddhiParserException
 KAT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kat.json")))
 OUT_OF_SCOPE = {
     "CountPatternTestCase.testQuery14": "having",
-    "PatternPartitionTestCase.testPatternPartitionQuery30": "non-partitioned stream in partition",
     "IsNullTestCase.isNullTest1": "plain stream query (runs as a one-state pattern in test_filter_kat.py)",
 }
 
