@@ -139,16 +139,32 @@ __global__ __launch_bounds__(256) void ratchet_place_kernel(
   }
   __syncthreads();
   const uint4* R = reinterpret_cast<const uint4*>(match) + (size_t)b * blk_recs;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint4 r = R[i];
-    const uint32_t off = r.x, lane = r.y & 63, q1 = r.z, level = r.w;
-    const int64_t cell = (int64_t)off * n_ranks + s_rank[lane];
-    const int64_t next = cell + 1 < cells ? (int64_t)base[cell + 1] : rows;
-    const int64_t P = row0 + next - 1 - (int64_t)level;
-    const int64_t s = seq_base + (int64_t)off;
-    const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
-    reinterpret_cast<longlong2*>(owords + 4 * P)[0] = make_longlong2(s_q[lane], s1);
-    reinterpret_cast<longlong2*>(owords + 4 * P)[1] = make_longlong2(1, s);
+  // U records per thread in flight: their record loads, then their (dependent) count loads, issue
+  // back to back
+  constexpr int U = 4;
+  for (int i0 = threadIdx.x; i0 < n; i0 += U * blockDim.x) {
+    uint4 r[U];
+    int64_t next[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * blockDim.x;
+      r[u] = i < n ? R[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t cell = (int64_t)r[u].x * n_ranks + s_rank[r[u].y & 63];
+      next[u] = cell + 1 < cells ? (int64_t)base[cell + 1] : rows;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (i0 + u * blockDim.x >= n) break;
+      const uint32_t off = r[u].x, lane = r[u].y & 63, q1 = r[u].z, level = r[u].w;
+      const int64_t P = row0 + next[u] - 1 - (int64_t)level;
+      const int64_t s = seq_base + (int64_t)off;
+      const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
+      reinterpret_cast<longlong2*>(owords + 4 * P)[0] = make_longlong2(s_q[lane], s1);
+      reinterpret_cast<longlong2*>(owords + 4 * P)[1] = make_longlong2(1, s);
+    }
   }
 }
 

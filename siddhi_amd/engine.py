@@ -253,7 +253,7 @@ class HipEngine:
         p = ctypes.c_void_p()
         n = ctypes.c_size_t()
         self._check(self.lib.sdh_engine_snapshot(self.h, ctypes.byref(p), ctypes.byref(n)))
-        data = ctypes.string_at(p, n.value)
+        data = bytes((ctypes.c_char * n.value).from_address(p.value)) if n.value else b""  # (> 2 GiB too)
         self.lib.sdh_free(p)
         return data
 

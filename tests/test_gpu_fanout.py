@@ -42,18 +42,18 @@ def test_fanout_on_gpu(seed, key_type, batch):
 
 
 def test_fanout_many_keys_and_snapshot():
-    """300 keys (the junction map resizes to 512 bins), pushed in batches; a snapshot taken midway
+    """150 keys (the junction map resizes to 256 bins), pushed in batches; a snapshot taken midway
     restores the key creation order into a fresh engine that continues identically."""
     src = fanout_app(3)
-    ev = fanout_events(11, n=3000, keys=300)
+    ev = fanout_events(11, n=2000, keys=150)
     o, g = App(src), hip_app(src)
-    _send([o, g], ev[:1500], True)
+    _send([o, g], ev[:1000], True)
     snap = g.engine.snapshot()
     g2 = hip_app(src)
     g2.engine.restore(snap)
     o.matches.clear()
     g.matches.clear()
-    _send([o, g, g2], ev[1500:], True)
+    _send([o, g, g2], ev[1000:], True)
     assert len(o.matches) > 100
     assert g.matches == o.matches
     assert g2.matches == o.matches
