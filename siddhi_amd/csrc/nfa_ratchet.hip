@@ -420,7 +420,9 @@ __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {  // b >= 0
 // carry the record's pop level at its event, and every (event, lane) with matches stores its match
 // count into the (event, receiver rank) count matrix -- one plain store per cell, no atomics
 template <int KK, int XM, bool FULL, int NF, bool SIM = false, bool PLACE = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
+// occupancy: the general forms at 7 waves per SIMD (72 VGPRs), the SIM form at 8 (64 VGPRs, a few
+// spills; the LDS rings allow 8 at ML = 8). SIM at 10K C2 patterns: 7 waves 167.9 ms, 8 waves 156.1
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7))) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
   using U = typename KT<KK>::U;
   constexpr bool W64 = KT<KK>::W64;
   const int lane = threadIdx.x;
@@ -787,11 +789,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void nf
   // ---- forward NFA step over the events this item emits for. Fast path: straight-line per
   // event (expiry check, up to four pops from one LDS round trip, push); rare cases (expiry,
   // spill refill / eviction, a fifth pop) branch to slow paths on a wave-uniform ballot ----
-  Raw nxt;
-  load(W.c0 + lane, W.c0 + lane < W.c1, nxt);
+  // The tile is loaded at its start, not prefetched during the previous tile: a load still in flight
+  // inside the event loop made the compiler wait for the vector-memory counter to drain (the match
+  // records' stores included) at every event that writes its destination registers (C2 10K SIM:
+  // prefetch 176.2 ms, load at tile start 167.8; the other resident waves cover the load)
   for (int64_t t = W.c0; t < W.c1; t += WAVE) {
-    const Raw cur = nxt;
-    if (t + WAVE < W.c1) load(t + WAVE + lane, t + WAVE + lane < W.c1, nxt);  // prefetch
+    Raw cur;
+    load(t + lane, t + lane < W.c1, cur);
     int64_t ets;
     U xk;
     uint32_t vbits;

@@ -12,4 +12,5 @@ for wl in "${@:-c2 c5}"; do
   bash profiles/collect.sh gpurun_out/prof_$wl "$args" $kern > gpurun_out/prof_$wl.log 2>&1 || { tail -20 gpurun_out/prof_$wl.log; exit 1; }
   python3 profiles/summarize.py gpurun_out/prof_$wl gpurun_out/r3_$wl $kern $wl $pat $batch > gpurun_out/sum_$wl.log 2>&1 || { tail -20 gpurun_out/sum_$wl.log; exit 1; }
   tail -25 gpurun_out/sum_$wl.log
+  rm -rf gpurun_out/prof_$wl  # (raw traces: the summary is in gpurun_out/r3_$wl; keeps the copy-back small)
 done
