@@ -1639,7 +1639,8 @@ void spec_build(sdh_engine* e) {
       if (mode == 1 && ng < 2) continue;
       // register-resident entries per lane: the first few partials of a (query, key) instance
       // stay in VGPRs across the key's events (C3 instances hold a handful at a time)
-      int regs = ps.kind == PK_COUNT ? 3 : 8;
+      // (C3 at 1000 x 10K keys, or/and entries: 8 26.0 ms/step, 6 25.4, 5 25.1, 4 24.6, 3 24.4, 2 32.8)
+      int regs = ps.kind == PK_COUNT ? 3 : 3;
       if (const char* v = getenv(ps.kind == PK_COUNT ? "SDH_KPART_REGS_COUNT" : "SDH_KPART_REGS")) regs = std::max(0, atoi(v));
       const sdh::spec::PartLayout lay{ps.kind, ps.sA, ps.sB, ps.cmax, ps.n_e1, ps.n_first, ps.n_last, ps.ew, regs};
       std::string err;

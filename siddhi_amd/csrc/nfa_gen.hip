@@ -219,6 +219,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
 // ---- K_seq (seq_body.h) with the interpreted window test: the shape's atoms, else its bytecode ----
 struct SeqInterp {
   static constexpr bool kBranchFree = false;
+  static constexpr int kRow = SEQ_ROW, kOutW = 1024;
   struct K {};
   __device__ static void load(K&, const kg::GQuery*) {}
   template <class Win>

@@ -215,10 +215,13 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
 
   // the key's events, staged 64 at a time (one coalesced index load and one gather per lane), then
   // read by broadcast: ts, seq, null bits and the captured words
-  __shared__ int64_t t_ts[64], t_seq[64], t_w[kg::GMAXNA][64];
+  // (LDS per wave bounds the resident waves: the staging holds the shape's captured words only, and
+  // the Spec sizes the output buffer)
+  using Out = dev::WaveOutT<Spec::kOutW>;
+  __shared__ int64_t t_ts[64], t_seq[64], t_w[Spec::kNA][64];
   __shared__ uint32_t t_nul[64];
-  __shared__ dev::WaveOut::Shared out_sh;
-  dev::WaveOut o;
+  __shared__ typename Out::Shared out_sh;
+  Out o;
   o.g = dev::LaneOut{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
   o.sh = &out_sh;
   o.init();
@@ -240,7 +243,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
       uint32_t nb = 0;
       for (int j = 0; j < ncap; ++j) {
         bool nl;
-        t_w[j][lane] = dev::raw_word(L.b, q->cap_attr[stream][j], e, nl);
+        if (j < Spec::kNA) t_w[j][lane] = dev::raw_word(L.b, q->cap_attr[stream][j], e, nl);
         if (nl) nb |= 1u << j;
       }
       t_nul[lane] = nb;

@@ -14,20 +14,26 @@
 namespace sdh {
 
 constexpr int SEQ_TILE = 64;
-constexpr int SEQ_ROW = 3 + kg::GMAXNA;  // ts, seq, null bits, raw words
+constexpr int SEQ_ROW = 3 + kg::GMAXNA;  // ts, seq, null bits, raw words (the widest row)
 
-struct LdsWin {
+// a window over LDS rows of ROW words; a Spec sets kRow = 3 + the attributes its shape captures (the
+// LDS a wave takes bounds the resident waves: C4's rows are 5 words, not 11)
+template <int ROW>
+struct LdsWinT {
   static constexpr bool kStagedConsts = false;
   const int64_t* base;  // row of window event 0
   __device__ int64_t lane_const(int) const { return 0; }
-  __device__ int64_t ts(int p) const { return base[p * SEQ_ROW]; }
-  __device__ int64_t raw(int p, int j, bool = false) const { return base[p * SEQ_ROW + 3 + j]; }
-  __device__ bool null(int p, int j, bool = false) const { return (base[p * SEQ_ROW + 2] >> j) & 1; }
+  __device__ int64_t ts(int p) const { return base[p * ROW]; }
+  __device__ int64_t raw(int p, int j, bool = false) const { return base[p * ROW + 3 + j]; }
+  __device__ bool null(int p, int j, bool = false) const { return (base[p * ROW + 2] >> j) & 1; }
 };
+using LdsWin = LdsWinT<SEQ_ROW>;
 
 template <class Spec>
 __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
-  __shared__ int64_t win[(SEQ_TILE + 8 + kg::GMAXS) * SEQ_ROW];  // (+8: masked starts of the last group)
+  constexpr int ROW = Spec::kRow;
+  using Win = LdsWinT<ROW>;
+  __shared__ int64_t win[(SEQ_TILE + 8 + kg::GMAXS) * ROW];  // (+8: masked starts of the last group)
   const int lane = threadIdx.x;
   const int gi = L.glist[blockIdx.x % L.n_glist];
   const int chunk = blockIdx.x / L.n_glist;
@@ -48,8 +54,9 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
   const int64_t s_end = W - S + 1;
   int64_t lo = s_begin + (int64_t)chunk * L.chunk_len;
   int64_t hi = lo + L.chunk_len < s_end ? lo + L.chunk_len : s_end;
-  __shared__ dev::SeqWaveOut::Shared out_sh;
-  dev::SeqWaveOut o;
+  using Out = dev::WaveOutT<Spec::kOutW>;
+  __shared__ typename Out::Shared out_sh;
+  Out o;
   o.g = dev::LaneOut{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
   o.sh = &out_sh;
   o.init();
@@ -86,13 +93,13 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
     }
   };
   auto put = [&](int p, const Row& r) {
-    int64_t* row = win + p * SEQ_ROW;
+    int64_t* row = win + p * ROW;
     row[0] = r.ts;
     row[1] = r.seq;
     row[2] = r.nb;
 #pragma unroll
     for (int j = 0; j < kg::GMAXNA; ++j)
-      if (j < na) row[3 + j] = r.v[j];
+      if (j < na && j < ROW - 3) row[3 + j] = r.v[j];
   };
   // rows t0 + p for p = lane (and lane + 64 for the S - 1 rows past the tile) that exist
   const int64_t rows_end = hi + S - 1;  // one past the last window row any start of the chunk reads
@@ -100,7 +107,7 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
   if (lo + lane < rows_end) fetch(lo + lane, ra);
   if (lane < S - 1 && lo + 64 + lane < rows_end) fetch(lo + 64 + lane, rb);
   auto emit = [&](int s) {
-    const LdsWin wv{win + s * SEQ_ROW};
+    const Win wv{win + s * ROW};
     ++nrec;
     if (!L.write_records) return;
     const int words = 7 + 2 * S;
@@ -108,13 +115,13 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
       r[0] = words;
       r[1] = qid;
       r[2] = -1;
-      r[3] = wv.base[(S - 1) * SEQ_ROW];      // ts of the last event
-      r[4] = wv.base[(S - 1) * SEQ_ROW + 1];  // the triggering event's seq
+      r[3] = wv.base[(S - 1) * ROW];      // ts of the last event
+      r[4] = wv.base[(S - 1) * ROW + 1];  // the triggering event's seq
       r[5] = 0;                               // one match per event per query
       r[6] = S | (stream << 16);
       for (int i = 0; i < S; ++i) {
         r[7 + 2 * i] = 1;
-        r[8 + 2 * i] = wv.base[i * SEQ_ROW + 1];
+        r[8 + 2 * i] = wv.base[i * ROW + 1];
       }
     });
   };
@@ -136,7 +143,7 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
           uint32_t m = 0;
 #pragma unroll
           for (int u = 0; u < 8; ++u)
-            m |= (Spec::match(k, q, ql, within, LdsWin{win + (s0 + u) * SEQ_ROW}) ? 1u : 0u) << u;
+            m |= (Spec::match(k, q, ql, within, Win{win + (s0 + u) * ROW}) ? 1u : 0u) << u;
           if (cnt - s0 < 8) m &= (1u << (cnt - s0)) - 1u;
           while (m) {
             const int u = __builtin_ctz(m);
@@ -146,7 +153,7 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
         }
       } else {
         for (int s = 0; s < cnt; ++s)
-          if (Spec::match(k, q, ql, within, LdsWin{win + s * SEQ_ROW})) emit(s);
+          if (Spec::match(k, q, ql, within, Win{win + s * ROW})) emit(s);
       }
     }
     __syncthreads();

@@ -31,6 +31,13 @@ std::string fmt(const char* f, ...) {
   return buf;
 }
 
+// an integer knob from the environment, clamped (tuning A/Bs of the generated kernels)
+int env_int(const char* env, int dflt, int lo, int hi) {
+  const char* v = getenv(env);
+  const int n = v && *v ? atoi(v) : dflt;
+  return n < lo ? lo : n > hi ? hi : n;
+}
+
 // register budget of a shape-compiled kernel: SDH_SEQ_WPE / SDH_PART_WPE = N asks for N resident
 // waves per SIMD (amdgpu_waves_per_eu); unset or 0 leaves the compiler's choice
 std::string wpe_attr(const char* env, int dflt) {
@@ -156,7 +163,11 @@ std::string seq_source(const kg::GQuery& g) {
   }
   // branch-free: every state is evaluated (filters are pure and total -- /0 is null, no traps), so
   // seq_body can test several window starts at once with their LDS reads in flight together
+  int na = 1;  // LDS row: ts, seq, null bits and the captured words
+  for (int st = 0; st < kg::GMAXSTREAM; ++st) na = std::max(na, (int)g.n_cap[st]);
   std::string s = header() + "#include \"seq_body.h\"\n\nstruct SpecSeq {\n  static constexpr bool kBranchFree = true;\n";
+  s += fmt("  static constexpr int kRow = %d, kOutW = %d;\n", 3 + std::min(na, kg::GMAXNA),
+           env_int("SDH_KSEQ_OUTW", 1024, 256, 4096));
   s += K.decl();
   s += K.load();
   s += "  template <class W>\n  __device__ static bool match(const K& k, const sdh::kg::GQuery*, const sdh::kg::GQuery*, "
@@ -227,7 +238,10 @@ std::string part_source(const kg::GQuery& g, const PartLayout& lay) {
   }
   fns += "    return ok;\n  }\n";
   std::string s = header() + "#include \"part_body.h\"\n\nstruct SpecPart {\n";
-  s += fmt("  static constexpr int kRegEntries = %d, kEW = %d;\n", lay.reg_entries, lay.ew);
+  int na = 1;  // captured words the tile staging holds
+  for (int st = 0; st < kg::GMAXSTREAM; ++st) na = std::max(na, (int)g.n_cap[st]);
+  s += fmt("  static constexpr int kRegEntries = %d, kEW = %d, kNA = %d, kOutW = %d;\n", lay.reg_entries, lay.ew,
+           std::min(na, kg::GMAXNA), env_int("SDH_KPART_OUTW", 1536, 256, 4096));
   s += fmt("  __device__ static sdh::PartOffs offs(const sdh::PartLaunch&) { return sdh::PartOffs{%d, %d, %d, %d}; }\n",
            lay.cmax, lay.n_e1, lay.n_first, lay.n_last);
   s += K.decl();
