@@ -103,6 +103,12 @@ struct LaneOut {
 // CAPW_: words in the LDS buffer. Every flush takes two atomics on the chip-wide counters, which
 // serialise once the match rate is high (C3: 512 words -> 42 ms/step, 1536 -> 24), while a larger
 // buffer costs resident waves (4096 -> 38 ms); K_part uses 1536, K_seq 1024 (measured)
+// Ring mode (SDH_FLAG_DEVICE_MATCHES) reserves SDH_RING_CHUNK buffers' worth of the ring per atomic:
+// the flush's round trip on the chip-wide counter stalls the whole wave (C3 ring chunk 1: 23.4
+// ms/step, 4: 20.7, 16: 20.7; C4 27.3 / 25.9 / 26.1)
+#ifndef SDH_RING_CHUNK
+#define SDH_RING_CHUNK 4
+#endif
 template <int CAPW_>
 struct WaveOutT {
   static constexpr int CAPW = CAPW_;
@@ -112,6 +118,7 @@ struct WaveOutT {
     int32_t roff[CAPR];
     int64_t base, rbase;
     int32_t used, nrec;
+    int64_t cbase, cleft;  // ring mode: the wave's reserved run of the ring (SDH_RING_CHUNK)
   };
   // the wave's shared counters: relaxed atomics, so no lane keeps a stale copy in a register (other
   // lanes update them) and, unlike volatile, the accesses stay ds_ operations
@@ -132,6 +139,7 @@ struct WaveOutT {
     if (__lane_id() == 0) {
       st(sh->used, 0);
       st(sh->nrec, 0);
+      st(sh->cleft, (int64_t)0);
     }
     wave_fence();
   }
@@ -143,7 +151,24 @@ struct WaveOutT {
     const int n = ld(sh->used), nr = ld(sh->nrec);
     if (n == 0) return;
     if (__lane_id() == lead) {
+#if SDH_RING_CHUNK > 1
+      // ring mode: one reservation per SDH_RING_CHUNK buffers' worth of words (the ring is written,
+      // never read back, so the run's unused tail costs nothing)
+      unsigned long long o;
+      if (g.ring) {
+        if (ld(sh->cleft) < n) {
+          st(sh->cbase, (int64_t)atomicAdd(g.next, (unsigned long long)(SDH_RING_CHUNK * CAPW)));
+          st(sh->cleft, (int64_t)(SDH_RING_CHUNK * CAPW));
+        }
+        o = (unsigned long long)ld(sh->cbase);
+        st(sh->cbase, ld(sh->cbase) + n);
+        st(sh->cleft, ld(sh->cleft) - n);
+      } else {
+        o = atomicAdd(g.next, (unsigned long long)n);
+      }
+#else
       const unsigned long long o = atomicAdd(g.next, (unsigned long long)n);
+#endif
       int64_t base = (int64_t)o, rbase = 0;
       if (!g.ring) {
         if ((int64_t)(o + n) > g.cap) base = -1;

@@ -31,6 +31,12 @@ std::string fmt(const char* f, ...) {
   return buf;
 }
 
+// tuning macros the generated kernels see (SDH_RING_CHUNK: ring-mode output reservations)
+std::string tuning_defines() {
+  const char* v = getenv("SDH_RING_CHUNK");
+  return v && *v ? fmt("#define SDH_RING_CHUNK %d\n", atoi(v)) : std::string();
+}
+
 // an integer knob from the environment, clamped (tuning A/Bs of the generated kernels)
 int env_int(const char* env, int dflt, int lo, int hi) {
   const char* v = getenv(env);
@@ -165,7 +171,7 @@ std::string seq_source(const kg::GQuery& g) {
   // seq_body can test several window starts at once with their LDS reads in flight together
   int na = 1;  // LDS row: ts, seq, null bits and the captured words
   for (int st = 0; st < kg::GMAXSTREAM; ++st) na = std::max(na, (int)g.n_cap[st]);
-  std::string s = header() + "#include \"seq_body.h\"\n\nstruct SpecSeq {\n  static constexpr bool kBranchFree = true;\n";
+  std::string s = tuning_defines() + header() + "#include \"seq_body.h\"\n\nstruct SpecSeq {\n  static constexpr bool kBranchFree = true;\n";
   s += fmt("  static constexpr int kRow = %d, kOutW = %d;\n", 3 + std::min(na, kg::GMAXNA),
            env_int("SDH_KSEQ_OUTW", 1024, 256, 4096));
   s += K.decl();
@@ -237,7 +243,7 @@ std::string part_source(const kg::GQuery& g, const PartLayout& lay) {
     fns += "    ok = false;\n";
   }
   fns += "    return ok;\n  }\n";
-  std::string s = header() + "#include \"part_body.h\"\n\nstruct SpecPart {\n";
+  std::string s = tuning_defines() + header() + "#include \"part_body.h\"\n\nstruct SpecPart {\n";
   int na = 1;  // captured words the tile staging holds
   for (int st = 0; st < kg::GMAXSTREAM; ++st) na = std::max(na, (int)g.n_cap[st]);
   s += fmt("  static constexpr int kRegEntries = %d, kEW = %d, kNA = %d, kOutW = %d;\n", lay.reg_entries, lay.ew,
