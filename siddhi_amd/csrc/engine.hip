@@ -1626,7 +1626,11 @@ void spec_build(sdh_engine* e) {
   for (const auto& [t, ng] : groups) {
     if (mode == 1 && ng < 2) continue;
     std::string err;
-    hipFunction_t f = sdh::spec::get_kernel(sdh::spec::seq_source(e->gq[t]), "sdh_seq_spec", &err);
+    // ring-mode output reserves the ring in chunks (dev_common.h SDH_RING_CHUNK), so its flushes are
+    // cheap and a smaller LDS buffer buys resident waves (C4 ring: 1024 words 25.9 ms/step, 768 22.9,
+    // 512 23.7); normal-mode flushes take two atomics each and keep the larger buffer
+    const int seq_w = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) ? 768 : 0;
+    hipFunction_t f = sdh::spec::get_kernel(sdh::spec::seq_source(e->gq[t], seq_w), "sdh_seq_spec", &err);
     if (!f && mode == 3) throw Error(SDH_E_DEVICE, "shape-compiled K_seq kernel: " + err);
     if (f) e->seq_spec[t] = f;
   }
@@ -1642,7 +1646,9 @@ void spec_build(sdh_engine* e) {
       // (C3 at 1000 x 10K keys, or/and entries: 8 26.0 ms/step, 6 25.4, 5 25.1, 4 24.6, 3 24.4, 2 32.8)
       int regs = ps.kind == PK_COUNT ? 3 : 3;
       if (const char* v = getenv(ps.kind == PK_COUNT ? "SDH_KPART_REGS_COUNT" : "SDH_KPART_REGS")) regs = std::max(0, atoi(v));
-      const sdh::spec::PartLayout lay{ps.kind, ps.sA, ps.sB, ps.cmax, ps.n_e1, ps.n_first, ps.n_last, ps.ew, regs};
+      sdh::spec::PartLayout lay{ps.kind, ps.sA, ps.sB, ps.cmax, ps.n_e1, ps.n_first, ps.n_last, ps.ew, regs};
+      // (C3 ring: 1536 words 20.7 ms/step, 1024 17.5, 768 18.0, 2048 21.8)
+      if (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) lay.out_w = 1024;
       std::string err;
       hipFunction_t f = sdh::spec::get_kernel(sdh::spec::part_source(e->gq[t], lay), "sdh_part_spec", &err);
       if (!f && mode == 3) throw Error(SDH_E_DEVICE, "shape-compiled K_part kernel: " + err);

@@ -20,7 +20,8 @@ namespace sdh {
 namespace spec {
 
 // K_seq (seq_body.h) for windows of shape g: source of kernel "sdh_seq_spec"
-std::string seq_source(const kg::GQuery& g);
+// out_w: words of the wave's LDS output buffer (0: the default for normal-mode output)
+std::string seq_source(const kg::GQuery& g, int out_w = 0);
 
 // K_part (part_body.h) of kind `kind` for shape g with the set's side / entry layout: source of
 // kernel "sdh_part_spec"
@@ -28,6 +29,7 @@ struct PartLayout {
   int kind, sA, sB, cmax, n_e1, n_first, n_last;
   int ew;            // words per entry
   int reg_entries;   // entries of a lane's table kept in registers
+  int out_w = 0;     // words of the wave's LDS output buffer (0: the default for normal-mode output)
 };
 std::string part_source(const kg::GQuery& g, const PartLayout& lay);
 

@@ -148,7 +148,7 @@ struct Loaded {
 // K_seq window test (kg::seq_match over a window of one-event slots): state i's filters see slots
 // 0 .. i at chain index 0 / CURRENT, every other reference is null; a step i >= 1 whose event is
 // more than `within` from the start event fails first (StreamPreStateProcessor.isExpired:102-113)
-std::string seq_source(const kg::GQuery& g) {
+std::string seq_source(const kg::GQuery& g, int out_w) {
   Consts K;
   std::string body;
   for (int i = 0; i < g.n_states; ++i) {
@@ -173,7 +173,7 @@ std::string seq_source(const kg::GQuery& g) {
   for (int st = 0; st < kg::GMAXSTREAM; ++st) na = std::max(na, (int)g.n_cap[st]);
   std::string s = tuning_defines() + header() + "#include \"seq_body.h\"\n\nstruct SpecSeq {\n  static constexpr bool kBranchFree = true;\n";
   s += fmt("  static constexpr int kRow = %d, kOutW = %d;\n", 3 + std::min(na, kg::GMAXNA),
-           env_int("SDH_KSEQ_OUTW", 1024, 256, 4096));
+           env_int("SDH_KSEQ_OUTW", out_w > 0 ? out_w : 1024, 256, 4096));
   s += K.decl();
   s += K.load();
   s += "  template <class W>\n  __device__ static bool match(const K& k, const sdh::kg::GQuery*, const sdh::kg::GQuery*, "
@@ -247,7 +247,7 @@ std::string part_source(const kg::GQuery& g, const PartLayout& lay) {
   int na = 1;  // captured words the tile staging holds
   for (int st = 0; st < kg::GMAXSTREAM; ++st) na = std::max(na, (int)g.n_cap[st]);
   s += fmt("  static constexpr int kRegEntries = %d, kEW = %d, kNA = %d, kOutW = %d;\n", lay.reg_entries, lay.ew,
-           std::min(na, kg::GMAXNA), env_int("SDH_KPART_OUTW", 1536, 256, 4096));
+           std::min(na, kg::GMAXNA), env_int("SDH_KPART_OUTW", lay.out_w > 0 ? lay.out_w : 1536, 256, 4096));
   s += fmt("  __device__ static sdh::PartOffs offs(const sdh::PartLaunch&) { return sdh::PartOffs{%d, %d, %d, %d}; }\n",
            lay.cmax, lay.n_e1, lay.n_first, lay.n_last);
   s += K.decl();
