@@ -2674,6 +2674,10 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       S.tail = ss.tail.p;
       S.nsub = ss.nsub;
       S.lds_words = ss.lds_words;
+      S.max_na = 1;
+      for (int g = 0; g < ss.n_groups; ++g)
+        for (int st = 0; st < kg::GMAXSTREAM; ++st)
+          S.max_na = std::max<int32_t>(S.max_na, e->gq[e->group_tmpl[ss.group_base + g]].n_cap[st]);
       S.live = ss.live.p;
       S.traffic = ss.traffic.p;
       S.out = e->g_out.p;

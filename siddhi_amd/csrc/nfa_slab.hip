@@ -57,6 +57,9 @@ __device__ __forceinline__ int wave_prefix(int v, int bits, int* total) {
 
 }  // namespace
 
+// NAX: the captured words the event staging holds (the launch's widest shape); LDS bounds the resident
+// waves of this kernel
+template <int NAX>
 __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
   using namespace slab;
   const int lane = threadIdx.x;
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
   const int ncap = q->n_cap[stream];
 
   extern __shared__ uint32_t slab_lds[];  // [lcap][EW] entries: the old block, then new partials
-  __shared__ int64_t t_ts[64], t_seq[64], t_w[kg::GMAXNA][64];
+  __shared__ int64_t t_ts[64], t_seq[64], t_w[NAX][64];
   __shared__ uint32_t t_nul[64];
   __shared__ SlabWaveOut::Shared out_sh;
   __shared__ int64_t sh_base;
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
       uint32_t nb = 0;
       for (int j = 0; j < ncap; ++j) {
         bool nl;
-        t_w[j][lane] = dev::raw_word(L.b, q->cap_attr[stream][j], ev, nl);
+        if (j < NAX) t_w[j][lane] = dev::raw_word(L.b, q->cap_attr[stream][j], ev, nl);
         if (nl) nb |= 1u << j;
       }
       t_nul[lane] = nb;
@@ -380,7 +383,8 @@ __global__ void slab_live_words_kernel(const uint64_t* dir, int64_t n_dir, int g
 extern "C" hipError_t sdh_launch_slab(const sdh::SlabLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
   const size_t lds = (size_t)L->lds_words * 4;
-  hipLaunchKernelGGL(sdh::nfa_slab_kernel, dim3((unsigned)L->n_items), dim3(64), lds, s, *L);
+  if (L->max_na <= 4) hipLaunchKernelGGL(sdh::nfa_slab_kernel<4>, dim3((unsigned)L->n_items), dim3(64), lds, s, *L);
+  else hipLaunchKernelGGL(sdh::nfa_slab_kernel<sdh::kg::GMAXNA>, dim3((unsigned)L->n_items), dim3(64), lds, s, *L);
   return hipGetLastError();
 }
 

@@ -374,6 +374,7 @@ struct SlabLaunch {
   const unsigned long long* tail;  // [nsub] oldest live logical word
   int32_t nsub;
   int32_t lds_words;          // dynamic LDS (uint32 words) for a block's entries
+  int32_t max_na;             // the widest captured-word count of the set's shapes (event staging)
   long long* live;            // [256] live-partial counters (sum = live partials)
   unsigned long long* traffic;  // [256] block bytes read + written (the launch's state traffic)
   int64_t* out;               // K_gen-format match records, as GenLaunch
