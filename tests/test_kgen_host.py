@@ -215,3 +215,31 @@ def test_kgen_host_fanout(seed, key_type):
         g.send(stream, [row], [t])
     assert len(o.matches) > 20
     assert g.matches == o.matches
+
+
+@pytest.mark.parametrize("key_type", ["string", "float", "double"])
+def test_fanout_refused_for_text_keys(key_type):
+    """The junction-map order needs String.valueOf of the key: string / float / double keys (the
+    dictionary id, Java's float formatting) are refused at plan time for fan-out partitions, while the
+    same partition without the unkeyed stream plans."""
+    from fuzz_apps import fanout_app
+    from siddhi_amd.planner import compile_app
+    from siddhi_amd.ql import SiddhiAppCreationException
+    src = fanout_app(0, key_type)
+    with pytest.raises(SiddhiAppCreationException):
+        compile_app(src)
+    keyed = src.replace("partition with (k of A)", "partition with (k of A, k of B)")
+    if key_type == "string":
+        keyed = keyed.replace("define stream B (k int", "define stream B (k string")
+    elif key_type in ("float", "double"):
+        keyed = keyed.replace("define stream B (k int", f"define stream B (k {key_type}")
+    compile_app(keyed)
+
+
+def test_java_string_hash_matches_known_values():
+    from siddhi_amd.planner import java_string_hash
+    # published String.hashCode values: "", "hello", "true", "false"
+    assert java_string_hash("") == 0
+    assert java_string_hash("hello") == 99162322
+    assert java_string_hash("true") == 3569038
+    assert java_string_hash("false") == 97196323
