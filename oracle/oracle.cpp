@@ -1528,6 +1528,15 @@ int oracle_send(OracleEngine* e, int32_t stream, int64_t n, const int64_t* ts, c
 
 int64_t oracle_num_matches(const OracleEngine* e) { return (int64_t)e->matches.size(); }
 
+// test hook: the iteration position of each of n keys (String.hashCode values, inserted in order)
+// in the restated ConcurrentHashMap
+void oracle_chm_positions(const int32_t* hashes, int64_t n, int32_t* pos) {
+  JavaCHM m;
+  for (int64_t k = 0; k < n; ++k) m.put(hashes[k], (int)k);
+  const std::vector<int> o = m.order();
+  for (size_t r = 0; r < o.size(); ++r) pos[o[r]] = (int32_t)r;
+}
+
 int64_t oracle_match_words(const OracleEngine* e) {
   int64_t w = 0;
   for (auto& m : e->matches)

@@ -29,6 +29,7 @@ int oracle_create(const void* ir_blob, size_t len, OracleEngine** out);
 int oracle_send(OracleEngine* e, int32_t stream, int64_t n, const int64_t* ts, const int64_t* vals,
                 const uint8_t* nulls, int as_chunk);
 int64_t oracle_num_matches(const OracleEngine* e);
+void oracle_chm_positions(const int32_t* hashes, int64_t n, int32_t* pos);  // (test hook)
 /* Total int64 words needed for the slot encoding of all matches. */
 int64_t oracle_match_words(const OracleEngine* e);
 /* Copy matches out in delivery order. For match i: query[i], key[i] (partition instance key id,

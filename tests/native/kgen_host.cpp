@@ -176,6 +176,13 @@ void sort_out(Host* h) {
 
 extern "C" {
 
+// test hook: chm_order.h positions of n keys inserted in order
+void kgh_chm_positions(const int32_t* hashes, int64_t n, int32_t* pos) {
+  const std::vector<int32_t> p = sdh::ChmOrder().positions(std::vector<int32_t>(hashes, hashes + n));
+  for (int64_t k = 0; k < n; ++k) pos[k] = p[(size_t)k];
+}
+
+
 void* kgh_create(const void* blob, size_t len, int R, int N, int LC) {
   try {
     auto* h = new Host;
