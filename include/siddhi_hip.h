@@ -21,10 +21,11 @@
  *   sdh_last_error      <- Java exceptions (SiddhiAppCreationException, OperationNotSupportedException)
  *
  * Conventions: plain C, no exceptions cross the ABI, every call returns 0 on success and a
- * negative SDH_E* code on failure; sdh_last_error() then describes it. A push that fails after its
- * kernels ran leaves the engine unusable (later calls fail with SDH_E_CAPACITY until
- * sdh_engine_restore), except a K_gen match-output overflow: that push is applied, only its K_gen
- * matches are lost, and the engine stays usable. One producer thread per
+ * negative SDH_E* code on failure; sdh_last_error() then describes it. Capacity overflows inside a
+ * push (pools, lists, tables, slab rings, match output) grow the buffer and re-run the push exactly
+ * from a journal, so no push drops a match. A push that fails after its kernels ran (device memory
+ * exhausted while growing, a HIP error, SDH_E_REFERENCE) leaves the engine unusable: later calls
+ * fail with SDH_E_CAPACITY until sdh_engine_restore. One producer thread per
  * engine (the reference serialises receivers on a monitor, SingleProcessStreamReceiver.java:59).
  * There is NO CPU fallback: an engine that cannot run a query on the GPU fails at create time.
  */
@@ -92,7 +93,16 @@ typedef struct sdh_config {
  * on_device != 0: all pointers are HIP device pointers already resident in HBM, and their contents
  * complete (the engine runs on its own non-blocking stream: the caller synchronizes the stream that
  * produced them); otherwise they are host pointers (pinned memory recommended) and are copied before
- * sdh_engine_push returns. */
+ * sdh_engine_push returns.
+ * chunk != 0: the batch is ONE chunk, InputHandler.send(Event[]) (stream/input/InputHandler.java:77-85)
+ * -> StreamJunction.sendEvent(Event[]) (stream/StreamJunction.java:218-236): every junction
+ * subscriber (a query, or a partition) receives the whole chunk before the next one; a partition
+ * splits it into runs of consecutive same-key events, each run going to its key's clones in turn
+ * (partition/PartitionStreamReceiver.java:214-239), or sends all of it to every key for a stream it
+ * does not key (:200-213, 277-281); a single-stream receiver calls its selector at the end of its
+ * chunk (query/input/SingleProcessStreamReceiver.java:57-80). Time moves once, to the chunk's last
+ * timestamp, before the chunk: the absent states' timers due by then fire first, none inside it.
+ * chunk == 0: n single-event sends (InputHandler.send(Event) per event). */
 typedef struct sdh_batch {
   int64_t n;
   const int64_t* ts;
@@ -100,10 +110,13 @@ typedef struct sdh_batch {
   const uint8_t* const* nulls;
   int32_t n_cols;
   int32_t on_device;
+  int32_t chunk;
+  int32_t reserved;          /* 0 */
 } sdh_batch;
 
 /* Matches, in the reference's delivery order (per input event; per query; per state processor
- * in reverse registration order; per pending partial in insertion order -- SURVEY R18). The
+ * in reverse registration order; per pending partial in insertion order -- SURVEY R18; for a chunk
+ * push: per junction subscriber, per same-key run or key, per query, per event, ...). The
  * order is established on the device (a stable radix sort of the matches since the last poll).
  * Match i: query[i], key[i] (partition key id, -1 if unpartitioned), ts[i] (the StateEvent
  * timestamp); words[off[i] .. off[i+1]) holds, per state slot, a count c followed by c global

@@ -1385,67 +1385,90 @@ void deliver_deferred(Engine* e) {
   e->deferred_seq.clear();
 }
 
+// One receiver (a query, or a partition key's clone of it) processes its chunk event by event
+// (ProcessStreamReceiver.receive(Event[]):137-151 / receive(ComplexEvent):105-119 build one
+// ComplexEventChunk); a single-stream receiver hands its matches to the selector at the end of its
+// chunk (SingleProcessStreamReceiver.processAndClear:57-80), a multi-stream one as they complete
+// (StateMultiProcessStreamReceiver.processAndClear:53-74, Runtime::receive). A per-event send is a
+// chunk of one event.
+void run_chunk(Engine* e, Runtime* rt, int stream, const std::vector<i64>& seqs) {
+  for (i64 seq : seqs) rt->receive(stream, seq, e->log[seq].ts);
+  deliver_deferred(e);
+}
+
 // One junction subscriber (a top-level query, or a partition's PartitionStreamReceiver) receives
-// the whole chunk before the next subscriber does (StreamJunction.sendEvent:185-205 loops over
-// receivers in subscription order); single-stream receivers hand their matches to the selector at
-// the end of their chunk (SingleProcessStreamReceiver.processAndClear:57-80).
+// the whole chunk before the next subscriber does (StreamJunction.sendEvent(Event[]):218-236 loops
+// over its receivers in subscription order). Inside a partition the key's junction holds the clones
+// in the partition's query order (PartitionRuntime.clonePartition:270 iterates metaQueryRuntimeMap,
+// a ConcurrentHashMap of query names: the planner emits PartDef::queries in that order).
 void deliver_to(Engine* e, int qi, int stream, const std::vector<i64>& seqs) {
   const Program& P = e->prog;
   const QueryDef& q = P.queries[qi];
   if (q.partition < 0) {
-    for (i64 seq : seqs) e->top[qi]->receive(stream, seq, e->log[seq].ts);
-    deliver_deferred(e);
+    run_chunk(e, e->top[qi].get(), stream, seqs);
     return;
   }
   const int pi = q.partition;
   const PartDef& pd = P.parts[pi];
   for (const FanOut& fo : pd.fanout) {
     if (fo.stream != stream) continue;
-    // PartitionStreamReceiver.receive:83-92 (no executor for this stream) -> send(ComplexEvent):
-    // 277-281: every key's junction "streamId + key" in its cachedStreamJunctionMap's order; keys
-    // joined it at clonePartition (updatePartitionStreamReceivers:312-316), in creation order
+    // PartitionStreamReceiver.receive(Event[]):200-213 / receive(Event):166-175 with no executor
+    // for this stream -> send(ComplexEvent):277-281: the whole chunk to every key's junction
+    // "streamId + key" in its cachedStreamJunctionMap's order; keys joined it at clonePartition
+    // (updatePartitionStreamReceivers:312-316), in creation order
     const auto& ko = e->key_order[pi];
     auto value_of = [&](i64 k) {  // String.valueOf (ValuePartitionExecutor.java:34-40)
       if (e->key_type[pi] == T_BOOL) return std::string(k ? "true" : "false");
       return std::to_string((long long)k);
     };
-    for (i64 seq : seqs) {
-      JavaCHM m;
-      for (size_t k = 0; k < ko.size(); ++k) m.put(java_hash_append(fo.id_hash, value_of(ko[k])), (int)k);
-      for (int k : m.order()) {
-        for (auto& rt : e->part_inst[pi].at(ko[(size_t)k])) rt->receive(stream, seq, e->log[seq].ts);
-        deliver_deferred(e);
-      }
-    }
+    JavaCHM m;
+    for (size_t k = 0; k < ko.size(); ++k) m.put(java_hash_append(fo.id_hash, value_of(ko[k])), (int)k);
+    for (int k : m.order())
+      for (auto& rt : e->part_inst[pi].at(ko[(size_t)k])) run_chunk(e, rt.get(), stream, seqs);
     return;
   }
-  for (i64 seq : seqs) {
-    for (const PartKey& k : pd.keys) {
-      if (k.stream != stream) continue;
-      EvalCtx cx{&e->log, &P.stream_types};
-      std::vector<StreamEvent*> slots(1);
-      StreamEvent tmp{seq, e->log[seq].ts};
-      slots[0] = &tmp;
-      Value kv = run_code(cx, k.code, slots);
-      if (kv.null) continue;  // PartitionStreamReceiver.send: null key drops the event
-      i64 key = key_of(kv);
-      auto& inst = e->part_inst[pi];
-      auto it = inst.find(key);
-      if (it == inst.end()) {
-        // PartitionRuntime.clonePartition:263-306 -> per-key QueryRuntime clones, seeded at init
-        std::vector<std::unique_ptr<Runtime>> rts;
-        for (int pq : pd.queries) {
-          rts.emplace_back(new Runtime(e, pq, key, &P.queries[pq]));
-          rts.back()->node_init(0);
-        }
-        it = inst.emplace(key, std::move(rts)).first;
-        e->key_order[pi].push_back(key);
-        e->key_type[pi] = kv.type;
+  const PartKey* pk = nullptr;  // (the planner allows one key per stream and partition)
+  for (const PartKey& k : pd.keys)
+    if (k.stream == stream) pk = &k;
+  if (!pk) return;
+  // PartitionStreamReceiver.receive(Event[]):214-239: the chunk splits into runs of consecutive
+  // events with equal keys (an event whose key is null is skipped and does not end a run); each run
+  // goes to its key's junction (send(String, ComplexEvent):270-275), the key's clones created on
+  // its first run (PartitionRuntime.cloneIfNotExist:257-306, seeded at init)
+  std::vector<i64> run;
+  i64 run_key = 0;
+  int run_type = T_INT;
+  auto flush = [&]() {
+    if (run.empty()) return;
+    auto& inst = e->part_inst[pi];
+    auto it = inst.find(run_key);
+    if (it == inst.end()) {
+      std::vector<std::unique_ptr<Runtime>> rts;
+      for (int pq : pd.queries) {
+        rts.emplace_back(new Runtime(e, pq, run_key, &P.queries[pq]));
+        rts.back()->node_init(0);
       }
-      for (auto& rt : it->second) rt->receive(stream, seq, e->log[seq].ts);
-      deliver_deferred(e);
+      it = inst.emplace(run_key, std::move(rts)).first;
+      e->key_order[pi].push_back(run_key);
+      e->key_type[pi] = run_type;
     }
+    for (auto& rt : it->second) run_chunk(e, rt.get(), stream, run);
+    run.clear();
+  };
+  for (i64 seq : seqs) {
+    EvalCtx cx{&e->log, &P.stream_types};
+    std::vector<StreamEvent*> slots(1);
+    StreamEvent tmp{seq, e->log[seq].ts};
+    slots[0] = &tmp;
+    Value kv = run_code(cx, pk->code, slots);
+    if (kv.null) continue;  // ValuePartitionExecutor.execute: a null value has no key
+    const i64 key = key_of(kv);
+    if (!run.empty() && key != run_key) flush();
+    run_key = key;
+    run_type = kv.type;
+    run.push_back(seq);
   }
+  flush();
 }
 
 void send_chunk(Engine* e, int stream, const std::vector<i64>& seqs) {
@@ -1505,17 +1528,25 @@ int oracle_send(OracleEngine* e, int32_t stream, int64_t n, const int64_t* ts, c
       else ev.nulls.assign(na, 0);
       seqs.push_back((i64)e->log.size());
       e->log.push_back(std::move(ev));
+      if (as_chunk) continue;
       // timers due up to this event fire before it (playback order: TimestampGenerator time
       // change -> Scheduler.sendTimerEvents before the event reaches the junction)
       e->cur_seq = seqs.back();
-      if (!as_chunk || seqs.size() == 1) e->advance(ts[k]);
-      if (!as_chunk) {
-        send_chunk(e, stream, seqs);
-        seqs.clear();
-        e->gc();
-      }
+      e->advance(ts[k]);
+      send_chunk(e, stream, seqs);
+      seqs.clear();
+      e->gc();
     }
-    if (!seqs.empty()) send_chunk(e, stream, seqs);
+    if (!seqs.empty()) {
+      // InputHandler.send(Event[]):77-85: the generator's time moves once, to the chunk's last
+      // timestamp, before the chunk reaches the junction -- the timers due by then fire first (with
+      // the chunk's first seq), none fire inside the chunk. A runtime not started yet starts with
+      // the chunk's first event, as with single events.
+      e->cur_seq = seqs.front();
+      if (!e->started) e->start(ts[0]);
+      e->advance(ts[n - 1]);
+      send_chunk(e, stream, seqs);
+    }
     e->gc();
     return 0;
   } catch (const std::exception& ex) {

@@ -108,10 +108,14 @@ extern "C" hipError_t sdh_live_part(const int64_t* st, const int32_t* cur, int64
 extern "C" hipError_t sdh_digest_ratchet(const int64_t* match, int blk_recs, int wide, const int32_t* blk_count,
                                          const int32_t* blk_group, const sdh::RatchetGroup* groups, int64_t seq_base,
                                          int n_blocks, unsigned long long* acc, hipStream_t s);
-extern "C" hipError_t sdh_poll_sort(sdh::MatchTable T, int64_t n, int n_lo, int lo_bits, int hi_bits, uint64_t* kbuf,
-                                    int32_t* pbuf, void* temp, size_t temp_bytes, int64_t* oq, int64_t* okey,
-                                    int64_t* ots, int64_t* oseq, int64_t* otb, int64_t* olen, int64_t* ooff,
-                                    int32_t** perm_out, int64_t* total_words, hipStream_t s);
+extern "C" hipError_t sdh_poll_sort(sdh::MatchTable T, int64_t n, int n_lo, int lo_bits, int hi_bits, int clo_bits,
+                                    uint64_t* kbuf, int32_t* pbuf, void* temp, size_t temp_bytes, int64_t* oq,
+                                    int64_t* okey, int64_t* ots, int64_t* oseq, int64_t* otb, int64_t* olen,
+                                    int64_t* ooff, int32_t** perm_out, int64_t* total_words, hipStream_t s);
+extern "C" hipError_t sdh_chunk_keys(sdh::MatchTable T, int64_t r0, int64_t r1, int chunk, int64_t cseq,
+                                     int64_t first_seq, int stream, int n_streams, const int32_t* major,
+                                     const int32_t* minor, const int32_t* qslot, const int32_t* runs,
+                                     int64_t n_events, hipStream_t s);
 extern "C" hipError_t sdh_poll_words(sdh::MatchTable T, const int32_t* perm, int64_t n, const int64_t* ooff,
                                      int64_t* owords, hipStream_t s);
 
@@ -638,7 +642,22 @@ struct sdh_engine {
     int64_t n = 0, nw = 0;           // rows / words used
     int n_lo = 0;                    // tiebreak passes the rows need
     bool placed = false;             // the rows are K_ratchet matches already in R18 order in po_*
+    // chunk delivery keys (nfa_types.h): allocated once a chunk push joins the window; rows
+    // [0, ck_n) have theirs, the rest are single-event rows filled at the poll
+    DevBuf<uint64_t> chi, clo;
+    bool chunked = false;
+    int64_t ck_n = 0;
+    int64_t max_run = 0;             // largest run start / key position a chunk row carries
   } mt;
+  // the chunk push in progress (sdh_batch.chunk): its first event's seq, its length, and per
+  // partition keyed on its stream each event's same-key run start (ck_runs[slot][event])
+  struct Chunk {
+    bool active = false;
+    int64_t first_seq = 0, n = 0;
+    int stream = -1;
+  } ck;
+  DevBuf<int32_t> ck_runs, d_ck_major, d_ck_minor, d_ck_qslot;
+  std::vector<int32_t> ck_major, ck_minor;  // [query][stream] subscriber rank (+1), rank in partition
   int64_t seq_ref = 0;               // global seq at the last poll (<= every trigger seq in mt)
   DevBuf<int32_t> d_out_rank;        // [query][stream] R18 receiver rank
   DevBuf<int32_t> d_qinfo;           // [query] (states, stream of the last state)
@@ -851,6 +870,8 @@ sdh::MatchTable table_view(sdh_engine* e) {
   T.woff = t.woff.p;
   T.wlen = t.wlen.p;
   T.words = t.words.p;
+  T.chi = t.chi.p;
+  T.clo = t.clo.p;
   return T;
 }
 
@@ -937,7 +958,33 @@ void table_clear(sdh_engine* e) {
   e->mt.nw = 0;
   e->mt.n_lo = 0;
   e->mt.placed = false;
+  e->mt.chunked = false;
+  e->mt.ck_n = 0;
+  e->mt.max_run = 0;
   e->seq_ref = e->seq;
+}
+
+// chunk keys of rows [ck_n, r1): single-event rows (chunk = false), or the rows the chunk push in
+// progress appended (matches.hip chunk_keys_kernel)
+void chunk_keys(sdh_engine* e, int64_t r1, bool chunk) {
+  auto& t = e->mt;
+  if (r1 <= t.ck_n) return;
+  t.chi.grow_keep((size_t)r1, (size_t)t.ck_n, e->stream);
+  t.clo.grow_keep((size_t)r1, (size_t)t.ck_n, e->stream);
+  const int ns = (int)e->prog.stream_types.size();
+  HIPCHK(sdh_chunk_keys(table_view(e), t.ck_n, r1, chunk ? 1 : 0, e->ck.first_seq - e->seq_ref, e->ck.first_seq,
+                        e->ck.stream, ns, e->d_ck_major.p, e->d_ck_minor.p, e->d_ck_qslot.p, e->ck_runs.p, e->ck.n,
+                        e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  t.ck_n = r1;
+}
+
+// the rows a sub-push of the chunk in progress appended, from row n0 on
+void chunk_rows(sdh_engine* e, int64_t n0) {
+  if (e->mt.n <= n0) return;
+  e->mt.chunked = true;
+  chunk_keys(e, n0, false);
+  chunk_keys(e, e->mt.n, true);
 }
 
 // keys this push created (ids [nk_seen, new_n)), in the order of their first events: the order
@@ -1058,10 +1105,15 @@ int64_t table_sort(sdh_engine* e, int64_t* total_words) {
   // timer records' tiebreaks are a full timestamp, the query and the partition key
   const int lo_bits = e->has_absent ? 64 : std::max(1, bits_of((uint64_t)std::max<int64_t>(e->seq, 1 << 16)));
   const int hi_bits = bits_of((uint64_t)(e->seq - e->seq_ref)) + RANK_BITS;
+  int clo_bits = 0;
+  if (e->mt.chunked) {  // the window holds chunk rows: the single-event rows' chunk keys, 2 passes more
+    chunk_keys(e, n, false);
+    clo_bits = bits_of((uint64_t)e->mt.max_run) + RANK_BITS;
+  }
   int32_t* perm = nullptr;
-  HIPCHK(sdh_poll_sort(table_view(e), n, e->mt.n_lo, lo_bits, hi_bits, e->p_keys.p, e->p_perm.p, e->p_temp.p,
-                       e->p_temp.n, e->po_q.p, e->po_key.p, e->po_ts.p, e->po_seq.p, e->po_tb.p, e->po_len.p,
-                       e->po_off.p, &perm, total_words, e->stream));
+  HIPCHK(sdh_poll_sort(table_view(e), n, e->mt.n_lo, lo_bits, hi_bits, clo_bits, e->p_keys.p, e->p_perm.p,
+                       e->p_temp.p, e->p_temp.n, e->po_q.p, e->po_key.p, e->po_ts.p, e->po_seq.p, e->po_tb.p,
+                       e->po_len.p, e->po_off.p, &perm, total_words, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   e->po_words.ensure((size_t)std::max<int64_t>(*total_words, 1));
   HIPCHK(sdh_poll_words(table_view(e), perm, n, e->po_off.p, e->po_words.p, e->stream));
@@ -2240,6 +2292,7 @@ sdh::GenLaunch gen_launch_base(sdh_engine* e, const sdh_engine::GenSet& gs, cons
   L.advance_to = e->advance_to;
   L.timer_seq = e->seq + B.n;
   L.playback = (e->cfg.flags & SDH_FLAG_PLAYBACK) ? 1 : 0;
+  L.no_timers = e->ck.active ? 1 : 0;
   return L;
 }
 
@@ -3040,13 +3093,15 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   // all come from K_ratchet, go straight to their R18 rows (no sort at poll)
   if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES)) {
     const bool only_ratchet = e->device_matches == 0 && e->g_dev_matches == 0;
-    const bool placeable = only_ratchet && (e->mt.n == 0 || e->mt.placed);
+    const bool placeable = only_ratchet && !e->ck.active && (e->mt.n == 0 || e->mt.placed);
     if (!(only_ratchet && e->r_matches == 0) &&
         !(placeable && place_ratchet(e, B.ts, B.seq_base, b->n))) {
       placed_to_table(e);
+      const int64_t n0 = e->mt.n;
       append_chain(e);
       append_ratchet(e, B.ts, B.seq_base);
       append_gen(e);
+      if (e->ck.active) chunk_rows(e, n0);
     }
   }
   return SDH_OK;
@@ -3126,6 +3181,137 @@ int do_poll(sdh_engine* e, sdh_matches* out, bool host) {
   }
   out->n = n;
   table_clear(e);
+  return SDH_OK;
+}
+
+// the absent states' timers due by t fire, with the next event's seq (sdh_engine_advance_time, and
+// a chunk push before its first event)
+void time_advance(sdh_engine* e, int64_t t) {
+  if (!e->has_absent) return;
+  HIPCHK(hipSetDevice(e->dev));
+  StreamBatch B{};
+  B.n = 0;
+  B.stream = 0;
+  B.n_attr = (int)e->prog.stream_types[0].size();
+  B.seq_base = e->seq;
+  B.prev_ts = e->prev_ts[0];
+  e->work.clear();
+  e->device_matches = 0;
+  e->r_blocks_used = 0;
+  e->r_matches = 0;
+  e->g_dev_matches = 0;
+  e->g_used = 0;
+  double ms = 0, bytes = 0;
+  e->advance_to = t;
+  try {
+    launch_gen(e, 0, B, &ms, &bytes);
+  } catch (const std::exception& ex) {
+    e->advance_to = INT64_MIN;
+    e->broken = ex.what();
+    throw;
+  }
+  e->advance_to = INT64_MIN;
+  if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) && e->g_dev_matches) {
+    placed_to_table(e);
+    append_gen(e);
+  }
+}
+
+// A chunk push (sdh_batch.chunk; include/siddhi_hip.h): per partition keyed on the stream, each
+// event's same-key run start (PartitionStreamReceiver.receive(Event[]):214-239 -- runs of
+// consecutive events with equal String.valueOf keys; an event with a null key is skipped and does
+// not end a run), and per query the run table it reads (-1: none, -2: fan-out, by key position).
+// Computed on the host from the key columns (copied back for a device-resident batch).
+void chunk_begin(sdh_engine* e, int stream, const sdh_batch* b) {
+  const int64_t n = b->n;
+  const size_t nq = e->prog.q.size();
+  std::vector<int32_t> qslot(std::max<size_t>(1, nq), -1), runs;
+  int slots = 0;
+  bool fan = false;
+  for (const auto& pd : e->lp.parts) {
+    int attr = -1;
+    for (const auto& k : pd.keys)
+      if (k.stream == stream) attr = (int)k.code[0].imm;
+    if (attr < 0) {
+      if (pd.fan(stream)) {
+        fan = true;
+        for (int pq : pd.queries) qslot[(size_t)pq] = -2;
+      }
+      continue;
+    }
+    for (int pq : pd.queries) qslot[(size_t)pq] = slots;
+    const int type = e->lp.stream_types[stream][attr];
+    const int w = attr_width(type);
+    std::vector<uint8_t> col((size_t)n * w), nul;
+    const bool has_nul = b->nulls && b->nulls[attr];
+    if (has_nul) nul.resize((size_t)n);
+    if (b->on_device) {
+      d2h_sync(e, col.data(), b->cols[attr], col.size());
+      if (has_nul) d2h_sync(e, nul.data(), b->nulls[attr], nul.size());
+    } else {
+      memcpy(col.data(), b->cols[attr], col.size());
+      if (has_nul) memcpy(nul.data(), b->nulls[attr], nul.size());
+    }
+    runs.resize((size_t)(slots + 1) * n, 0);
+    int32_t* r = runs.data() + (size_t)slots * n;
+    int64_t prev = 0, start = 0;
+    bool have = false;
+    for (int64_t i = 0; i < n; ++i) {
+      if (has_nul && nul[(size_t)i]) continue;
+      int64_t raw;
+      if (w == 8) memcpy(&raw, col.data() + (size_t)i * 8, 8);
+      else if (w == 4) {
+        int32_t v;
+        memcpy(&v, col.data() + (size_t)i * 4, 4);
+        raw = v;
+      } else raw = col[(size_t)i];
+      const int64_t k = kg::key_of_raw(type, raw);
+      if (!have || k != prev) start = i;
+      have = true;
+      prev = k;
+      r[i] = (int32_t)start;
+    }
+    ++slots;
+  }
+  e->ck_runs.ensure(std::max<size_t>(1, runs.size()));
+  if (!runs.empty()) HIPCHK(hipMemcpy(e->ck_runs.p, runs.data(), runs.size() * 4, hipMemcpyHostToDevice));
+  e->d_ck_qslot.ensure(qslot.size());
+  HIPCHK(hipMemcpy(e->d_ck_qslot.p, qslot.data(), qslot.size() * 4, hipMemcpyHostToDevice));
+  e->mt.max_run = std::max<int64_t>(e->mt.max_run, fan ? (int64_t)INT32_MAX : n);
+}
+
+int push_chunk(sdh_engine* e, int32_t stream, const sdh_batch* b) {
+  if (stream < 0 || stream >= (int)e->prog.stream_types.size() || b->n_cols != (int)e->prog.stream_types[stream].size())
+    throw Error(SDH_E_INVALID, "bad stream or batch");
+  if (e->cfg.max_batch > 0 && b->n > e->cfg.max_batch) throw Error(SDH_E_INVALID, "batch larger than max_batch");
+  if (b->n >= INT32_MAX) throw Error(SDH_E_INVALID, "a chunk of 2^31 events or more");
+  HIPCHK(hipSetDevice(e->dev));
+  int64_t t01[2];
+  if (b->on_device) {
+    d2h_sync(e, &t01[0], b->ts, 8);
+    d2h_sync(e, &t01[1], b->ts + (b->n - 1), 8);
+  } else {
+    t01[0] = b->ts[0];
+    t01[1] = b->ts[b->n - 1];
+  }
+  chunk_begin(e, stream, b);
+  // InputHandler.send(Event[]):77-85: time moves once, to the last timestamp, before the chunk
+  if (!e->started) {
+    e->started = true;
+    e->start_ts = t01[0];
+  }
+  time_advance(e, t01[1]);
+  e->ck.active = true;
+  e->ck.first_seq = e->seq;
+  e->ck.n = b->n;
+  e->ck.stream = stream;
+  try {
+    do_push(e, stream, b);
+  } catch (...) {
+    e->ck.active = false;
+    throw;
+  }
+  e->ck.active = false;
   return SDH_OK;
 }
 
@@ -3233,6 +3419,23 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
         }
       HIPCHK(hipMemcpy(e->d_out_rank.p, r1.data(), r1.size() * 4, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(e->d_fan_rank.p, fr.data(), fr.size() * 4, hipMemcpyHostToDevice));
+      // chunk delivery (matches.hip chunk_keys_kernel): a query's junction subscriber rank (+1) --
+      // its partition's first rank on the stream -- and its rank inside the partition
+      e->ck_major = r1;
+      e->ck_minor.assign(r1.size(), 0);
+      for (const auto& pd : e->lp.parts)
+        for (size_t st = 0; st < ns; ++st) {
+          int base = INT32_MAX;
+          for (int pq : pd.queries) base = std::min(base, e->out_rank[(size_t)pq * ns + st]);
+          for (int pq : pd.queries) {
+            e->ck_major[(size_t)pq * ns + st] = base + 1;
+            e->ck_minor[(size_t)pq * ns + st] = e->out_rank[(size_t)pq * ns + st] - base;
+          }
+        }
+      e->d_ck_major.ensure(r1.size());
+      e->d_ck_minor.ensure(r1.size());
+      HIPCHK(hipMemcpy(e->d_ck_major.p, e->ck_major.data(), r1.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(e->d_ck_minor.p, e->ck_minor.data(), r1.size() * 4, hipMemcpyHostToDevice));
     }
     std::vector<int32_t> qinfo(std::max<size_t>(1, 2 * nq_all), 0);
     for (size_t q = 0; q < nq_all; ++q) {
@@ -3256,6 +3459,7 @@ int sdh_engine_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   if (!e) return SDH_E_INVALID;
   return guard(e, [&]() {
     check_usable(e);
+    if (b && b->chunk && b->n > 1) return push_chunk(e, stream, b);
     return do_push(e, stream, b);
   });
 }
@@ -3290,34 +3494,7 @@ int sdh_engine_advance_time(sdh_engine* e, int64_t t) {
       e->started = true;
       e->start_ts = t;
     }
-    if (!e->has_absent) return SDH_OK;
-    HIPCHK(hipSetDevice(e->dev));
-    StreamBatch B{};
-    B.n = 0;
-    B.stream = 0;
-    B.n_attr = (int)e->prog.stream_types[0].size();
-    B.seq_base = e->seq;
-    B.prev_ts = e->prev_ts[0];
-    e->work.clear();
-    e->device_matches = 0;
-    e->r_blocks_used = 0;
-    e->r_matches = 0;
-    e->g_dev_matches = 0;
-    e->g_used = 0;
-    double ms = 0, bytes = 0;
-    e->advance_to = t;
-    try {
-      launch_gen(e, 0, B, &ms, &bytes);
-    } catch (const std::exception& ex) {
-      e->advance_to = INT64_MIN;
-      e->broken = ex.what();
-      throw;
-    }
-    e->advance_to = INT64_MIN;
-    if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) && e->g_dev_matches) {
-      placed_to_table(e);
-      append_gen(e);
-    }
+    time_advance(e, t);
     return SDH_OK;
   });
 }

@@ -318,18 +318,13 @@ inline GQuery lower_gen(const LProgram& P, int qi, const Sizing& sz) {
 }
 
 // Output order of the matches of one event across queries (R18): junction subscribers in
-// definition order (a partition subscribes at its first query); inside a partition the queries'
-// multi-processor receivers emit while the event is delivered and the single-processor receivers'
-// deferred selector calls follow at the end of the delivery (oracle: deliver_to/deliver_deferred).
-// Returns rank[q * n_streams + stream].
+// definition order (a partition subscribes at its first query); inside a partition a key's junction
+// holds the clones in the partition's query order -- the planner emits LPart::queries in
+// PartitionRuntime.metaQueryRuntimeMap order -- and each clone's receiver emits at the end of its own
+// chunk (oracle: deliver_to / run_chunk). Returns rank[q * n_streams + stream].
 inline std::vector<int> output_ranks(const LProgram& P) {
   const int nq = (int)P.q.size(), ns = (int)P.stream_types.size();
   std::vector<int> rank((size_t)nq * ns, 0);
-  auto multi = [&](int q, int s) {
-    for (const auto& rv : P.q[q].recvs)
-      if (rv.stream == s) return rv.kind == R_MULTI;
-    return false;
-  };
   for (int s = 0; s < ns; ++s) {
     std::vector<char> done(P.parts.size(), 0);
     int r = 0;
@@ -341,9 +336,7 @@ inline std::vector<int> output_ranks(const LProgram& P) {
       }
       if (done[pi]) continue;
       done[pi] = 1;
-      for (int pass = 0; pass < 2; ++pass)
-        for (int pq : P.parts[pi].queries)
-          if ((pass == 0) == multi(pq, s)) rank[(size_t)pq * ns + s] = r++;
+      for (int pq : P.parts[pi].queries) rank[(size_t)pq * ns + s] = r++;
     }
   }
   return rank;

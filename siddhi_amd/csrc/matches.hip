@@ -282,6 +282,39 @@ __global__ __launch_bounds__(256) void append_gen_kernel(const int64_t* __restri
   T.wlen[row] = r[0] - 7;
 }
 
+// Chunk delivery keys (nfa_types.h MatchTable chi / clo) of rows [r0, r1).
+// chunk == 0: single-event rows -- chi = their hi with the rank cleared, clo = 0, so the final
+// (chi, clo) passes keep their (seq, rank, tiebreak) order.
+// chunk != 0: rows of a chunk push over stream `stream` whose first event has seq first_seq. The
+// reference hands the whole chunk to one junction subscriber after another; a partition splits it
+// into same-key runs (each run to every clone of its key, one clone after another) or, for a stream
+// it does not key, gives all of it to every key in junction-map order; inside a clone the events
+// go in order. So a row sorts by (chunk, subscriber rank major[q], run start runs[slot][event] or
+// key position lo[2] (fan-out rows, append_gen_kernel), its query's rank in the partition minor[q],
+// then its single-event key). Timer rows (rank 0: fired before the chunk) come first.
+__global__ void chunk_keys_kernel(MatchTable T, int64_t r0, int64_t r1, int chunk, int64_t cseq, int64_t first_seq,
+                                  int stream, int n_streams, const int32_t* __restrict__ major,
+                                  const int32_t* __restrict__ minor, const int32_t* __restrict__ qslot,
+                                  const int32_t* __restrict__ runs, int64_t n_events) {
+  const int64_t row = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= r1) return;
+  const uint64_t hi = T.hi[row];
+  const uint64_t rmask = (1ull << RANK_BITS) - 1;
+  if (!chunk || (hi & rmask) == 0) {
+    T.chi[row] = chunk ? (uint64_t)cseq << RANK_BITS : hi & ~rmask;
+    T.clo[row] = 0;
+    return;
+  }
+  const int64_t q = T.q[row];
+  const int64_t qs = q * n_streams + stream;
+  const int slot = qslot[q];
+  uint64_t run = 0;
+  if (slot >= 0) run = (uint64_t)runs[(int64_t)slot * n_events + (T.seq[row] - first_seq)];
+  else if (slot == -2) run = T.lo[2][row];  // fan-out: the key's junction-map position
+  T.chi[row] = ((uint64_t)cseq << RANK_BITS) | (uint64_t)major[qs];
+  T.clo[row] = (run << RANK_BITS) | (uint64_t)minor[qs];
+}
+
 __global__ void iota_kernel(int32_t* p, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = (int32_t)i;
@@ -422,10 +455,20 @@ extern "C" size_t sdh_poll_temp_bytes(int64_t n) {
 // pointers; off has n+1 entries). n_lo tiebreak passes; lo_bits / hi_bits bound the key bits that
 // vary. kbuf: 2 x n keys, pbuf: 2 x n permutation entries, olen: n + 1. On return *perm_out is the
 // sorted permutation (inside pbuf) and *total_words (host) receives off[n] once the stream has run.
-extern "C" hipError_t sdh_poll_sort(MatchTable T, int64_t n, int n_lo, int lo_bits, int hi_bits, uint64_t* kbuf,
-                                    int32_t* pbuf, void* temp, size_t temp_bytes, int64_t* oq, int64_t* okey,
-                                    int64_t* ots, int64_t* oseq, int64_t* otb, int64_t* olen, int64_t* ooff,
-                                    int32_t** perm_out, int64_t* total_words, hipStream_t s) {
+extern "C" hipError_t sdh_chunk_keys(MatchTable T, int64_t r0, int64_t r1, int chunk, int64_t cseq, int64_t first_seq,
+                                     int stream, int n_streams, const int32_t* major, const int32_t* minor,
+                                     const int32_t* qslot, const int32_t* runs, int64_t n_events, hipStream_t s) {
+  if (r1 <= r0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::chunk_keys_kernel, dim3(sdh::grid(r1 - r0, 256)), dim3(256), 0, s, T, r0, r1, chunk, cseq,
+                     first_seq, stream, n_streams, major, minor, qslot, runs, n_events);
+  return hipGetLastError();
+}
+
+// clo_bits > 0: the window holds chunk rows, two more passes (clo, then chi) after hi
+extern "C" hipError_t sdh_poll_sort(MatchTable T, int64_t n, int n_lo, int lo_bits, int hi_bits, int clo_bits,
+                                    uint64_t* kbuf, int32_t* pbuf, void* temp, size_t temp_bytes, int64_t* oq,
+                                    int64_t* okey, int64_t* ots, int64_t* oseq, int64_t* otb, int64_t* olen,
+                                    int64_t* ooff, int32_t** perm_out, int64_t* total_words, hipStream_t s) {
   using namespace sdh;
   *total_words = 0;
   *perm_out = pbuf;
@@ -452,6 +495,12 @@ extern "C" hipError_t sdh_poll_sort(MatchTable T, int64_t n, int n_lo, int lo_bi
   }
   hipError_t e = pass(T.hi, hi_bits);
   if (e != hipSuccess) return e;
+  if (clo_bits > 0) {
+    e = pass(T.clo, clo_bits);
+    if (e != hipSuccess) return e;
+    e = pass(T.chi, hi_bits);
+    if (e != hipSuccess) return e;
+  }
   *perm_out = perm;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(grid(n + 1, 256)), dim3(256), 0, s, T, perm, n, oq, okey, ots, oseq, otb,
                      olen);

@@ -151,9 +151,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   // events and the timer stops -- a timer due at d fires at the first batch event whose time reaches
   // d (binary search of pm), with that event's seq and time, exactly where the whole walk fires it.
   const bool indexed = L.sweep && L.pm;
+  const bool timers = !L.no_timers;  // (a chunk push fired its timers before its first event)
   const int32_t sg = indexed && L.kseg ? L.kseg[kid] : -1;
   const int64_t sb = sg >= 0 ? L.seg_begin[sg] : 0, sl = sg >= 0 ? L.seg_len[sg] : 0;
-  int64_t j = 0, pos = 0;  // indexed: next own event, first batch event not passed yet
+  int64_t j = 0, pos = 0;  // indexed: next own event, first batch event whose timers may still fire
   for (int64_t k = w0; c.err == kg::GE_OK;) {
     int64_t e;
     bool own;
@@ -161,8 +162,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     if (indexed) {
       const int64_t eo = j < sl ? L.ev_idx[sb + j] : L.b.n - 1;
       if (eo < 0) break;  // (an empty batch)
-      const int64_t d = inited ? c.next_due() : 0x7fffffffffffffffLL;
-      if (d <= L.b.ts[eo]) {  // a timer stop at or before the next own event
+      const int64_t d = inited && timers ? c.next_due() : 0x7fffffffffffffffLL;
+      if (d <= L.b.ts[eo] && pos <= eo) {  // a timer stop at or before the next own event
         int64_t lo = pos, hi = eo;
         while (lo < hi) {
           const int64_t m = (lo + hi) >> 1;
@@ -171,14 +172,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
         }
         e = lo;
         own = false;
+        pos = e;
       } else if (j < sl) {
         e = eo;
         own = true;
         ++j;
+        // a timer the event itself schedules fires at a later event (the whole-batch walk fires
+        // timers before it receives), never at this one
+        pos = e + 1;
       } else {
         break;
       }
-      pos = e;
     } else {
       if (k >= e1) break;
       live = k >= e0;
@@ -190,7 +194,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     c.seq = L.b.seq_base + e;
     c.ts = L.b.ts[e];
     idx = 0;
-    if (inited) c.fire_timers(c.ts, L.playback != 0, emit);  // timers due by this event fire before it
+    if (inited && timers) c.fire_timers(c.ts, L.playback != 0, emit);  // timers due by this event fire before it
     if (!own) continue;
     if (!inited) seed();
     if (!reads) continue;

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
       t_seq[lane] = L.b.seq_base + ev;
       uint32_t nb = 0;
       for (int j = 0; j < ncap; ++j) {
-        bool nl;
+        bool nl = false;
         if (j < NAX) t_w[j][lane] = dev::raw_word(L.b, q->cap_attr[stream][j], ev, nl);
         if (nl) nb |= 1u << j;
       }

@@ -270,6 +270,7 @@ struct GenLaunch {
   int64_t advance_to;
   int64_t timer_seq;          // trigger seq of the timers fired after the last event
   int32_t playback;           // @app:playback: the generator's time is the event time while timers fire
+  int32_t no_timers;          // a chunk push: its timers fired before it (time moved once), none inside
   // indexed timer sweep (pm != nullptr; batches with ordered timestamps): item = (kid, group) over
   // every known key walks only its own events (the routed segment kseg[kid] of seg_begin / seg_len /
   // ev_idx, -1: none) and fires each due timer at the first batch event whose ts reaches it (binary
@@ -427,6 +428,10 @@ struct SeqLaunch {
 //           seq; K_chain slot k's seq (k = 0 .. S-2; slot S-2 is compared first); K_gen the
 //           emission index within its processAndReturn chunk
 // words[woff .. woff+wlen) = per state slot a count c then c event sequence numbers.
+// A poll window holding chunk pushes (sdh_batch.chunk) sorts by two more significant keys first:
+//   chi = (chunk's first seq - seq_ref) << RANK_BITS | junction subscriber rank
+//   clo = (same-key run start | fan-out key position) << RANK_BITS | the query's rank in its partition
+// (single-event rows and timer rows: chi = their hi with rank 0, clo = 0; matches.hip chunk_keys).
 // ------------------------------------------------------------------------------------------
 constexpr int MAXLO = MAXS - 1;
 constexpr int RANK_BITS = 20;
@@ -434,6 +439,8 @@ constexpr int RANK_BITS = 20;
 struct MatchTable {
   uint64_t* hi;
   uint64_t* lo[MAXLO];
+  uint64_t* chi;
+  uint64_t* clo;
   int64_t* seq;         // trigger event sequence number
   int64_t* q;
   int64_t* key;

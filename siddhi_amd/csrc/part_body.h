@@ -242,7 +242,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
       t_seq[lane] = L.b.seq_base + e;
       uint32_t nb = 0;
       for (int j = 0; j < ncap; ++j) {
-        bool nl;
+        bool nl = false;
         if (j < Spec::kNA) t_w[j][lane] = dev::raw_word(L.b, q->cap_attr[stream][j], e, nl);
         if (nl) nb |= 1u << j;
       }

@@ -33,7 +33,7 @@ from __future__ import annotations
 import ctypes
 from typing import Dict, List, Optional, Sequence, Tuple
 
-from .ir import R_MULTI, T_BOOL, T_INT, T_LONG, ProgramIR
+from .ir import T_BOOL, T_INT, T_LONG, ProgramIR
 
 RANK_BITS = 20  # as nfa_types.h
 
@@ -79,14 +79,11 @@ def key_shard(raw: int, attr_type: int, world: int) -> int:
 def output_ranks(ir: ProgramIR) -> Dict[Tuple[int, int], int]:
     """R18 order of the matches of one event across queries, per (query, stream): junction
     subscribers in definition order (a partition subscribes at its first query); inside a partition
-    the multi-processor receivers emit while the event is delivered, the single-processor
-    receivers' deferred selector calls follow (siddhi_amd/csrc/gen_lower.h output_ranks)."""
+    a key's junction holds the clones in the partition's query order (the planner emits
+    ``query_idx`` in ``metaQueryRuntimeMap`` order), each emitting at the end of its own chunk
+    (siddhi_amd/csrc/gen_lower.h output_ranks)."""
     nq, ns = len(ir.queries), len(ir.streams)
     rank: Dict[Tuple[int, int], int] = {}
-
-    def multi(q, s):
-        return any(r.stream_idx == s and r.kind == R_MULTI for r in ir.queries[q].receivers)
-
     for s in range(ns):
         done, r = set(), 0
         for q in range(nq):
@@ -98,11 +95,9 @@ def output_ranks(ir: ProgramIR) -> Dict[Tuple[int, int], int]:
             if pi in done:
                 continue
             done.add(pi)
-            for want_multi in (True, False):
-                for pq in ir.partitions[pi].query_idx:
-                    if multi(pq, s) == want_multi:
-                        rank[(pq, s)] = r
-                        r += 1
+            for pq in ir.partitions[pi].query_idx:
+                rank[(pq, s)] = r
+                r += 1
     return rank
 
 

@@ -37,7 +37,7 @@ class SdhConfig(ctypes.Structure):
 class SdhBatch(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("ts", ctypes.c_void_p), ("cols", ctypes.POINTER(ctypes.c_void_p)),
                 ("nulls", ctypes.POINTER(ctypes.c_void_p)), ("n_cols", ctypes.c_int32),
-                ("on_device", ctypes.c_int32)]
+                ("on_device", ctypes.c_int32), ("chunk", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class SdhMatches(ctypes.Structure):
@@ -152,7 +152,8 @@ class HipEngine:
             raise EngineError(rc, self.lib.sdh_last_error(self.h).decode())
 
     def push_columns(self, stream: int, ts: np.ndarray, cols: Sequence[np.ndarray],
-                     nulls: Optional[Sequence[Optional[np.ndarray]]] = None):
+                     nulls: Optional[Sequence[Optional[np.ndarray]]] = None, chunk: bool = False):
+        """Push host columns: n single-event sends, or (chunk) one ``InputHandler.send(Event[])``."""
         ts = np.ascontiguousarray(ts, dtype=np.int64)
         keep = [ts] + list(cols)
         cp = (ctypes.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
@@ -161,14 +162,15 @@ class HipEngine:
             nl = [None if x is None else np.ascontiguousarray(x, dtype=np.uint8) for x in nulls]
             keep += [x for x in nl if x is not None]
             nptr = (ctypes.c_void_p * len(cols))(*[0 if x is None else x.ctypes.data for x in nl])
-        b = SdhBatch(n=len(ts), ts=ts.ctypes.data, cols=cp, nulls=nptr, n_cols=len(cols), on_device=0)
+        b = SdhBatch(n=len(ts), ts=ts.ctypes.data, cols=cp, nulls=nptr, n_cols=len(cols), on_device=0,
+                     chunk=int(chunk))
         self._check(self.lib.sdh_engine_push(self.h, stream, ctypes.byref(b)))
         del keep
 
-    def push_device(self, stream: int, n: int, ts_ptr: int, col_ptrs: Sequence[int]):
+    def push_device(self, stream: int, n: int, ts_ptr: int, col_ptrs: Sequence[int], chunk: bool = False):
         """Push a batch whose columns are already resident in HBM (e.g. torch CUDA tensors)."""
         cp = (ctypes.c_void_p * len(col_ptrs))(*col_ptrs)
-        b = SdhBatch(n=n, ts=ts_ptr, cols=cp, nulls=None, n_cols=len(col_ptrs), on_device=1)
+        b = SdhBatch(n=n, ts=ts_ptr, cols=cp, nulls=None, n_cols=len(col_ptrs), on_device=1, chunk=int(chunk))
         self._check(self.lib.sdh_engine_push(self.h, stream, ctypes.byref(b)))
 
     # interface used by tests/harness.App -------------------------------------------------------
@@ -178,7 +180,7 @@ class HipEngine:
         nl = None
         if nulls is not None and np.any(nulls):
             nl = [np.ascontiguousarray(nulls[:, j]) for j in range(len(types))]
-        self.push_columns(stream, np.asarray(ts, dtype=np.int64), cols, nl)
+        self.push_columns(stream, np.asarray(ts, dtype=np.int64), cols, nl, chunk=as_chunk)
 
     def poll(self, with_seq: bool = False):
         """R18-ordered matches since the last poll as arrays (query, key, ts, off, words[, seq, tb])."""

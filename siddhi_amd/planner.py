@@ -31,7 +31,7 @@ from __future__ import annotations
 import struct
 from typing import List, Optional
 
-from . import ql
+from . import chm, ql
 from .ir import (AR_CODE, CMP_CODE, INT_MAX, K_ABSENT, K_COUNT, K_LOGICAL, K_STREAM, L_AND, L_OR, N_COUNT,
                  N_EVERY, N_LOGICAL, N_NEXT, N_STREAM, OP_AND, OP_ARITH, OP_ATTR, OP_CMP, OP_CONST,
                  OP_IS_NULL, OP_NOT, OP_OR, OP_STREAM_IS_NULL, Q_PATTERN, Q_SEQUENCE, R_MULTI,
@@ -575,6 +575,8 @@ def plan(app: ql.App) -> ProgramIR:
                         "only value partitions on a plain attribute are on the accelerated path")
                 comp = _ExprCompiler(pb, [(None, sd)], 0, CURRENT)
                 code, t = comp.compile(k.expr)
+                if k.stream in part_streams:
+                    raise SiddhiAppCreationException(f"stream '{k.stream}' is keyed twice in one partition")
                 keys.append(PartitionKeyIR(pb.stream_idx[k.stream], code, t))
                 part_streams.add(k.stream)
             kclass = {("num" if kk.type in (T_INT, T_LONG) else kk.type) for kk in keys}
@@ -606,6 +608,13 @@ def plan(app: ql.App) -> ProgramIR:
                 chains.append(_plan_chain(pb, c, src[0]))
                 if any([o.type for o in s.outputs] != chains[-1].input_types for s in src[1:]):
                     raise SiddhiAppCreationException(f"producers of '{c.stream}' disagree on its schema")
+            # a key's junction holds the clones in PartitionRuntime.metaQueryRuntimeMap order
+            # (clonePartition iterates its values(), PartitionRuntime.java:270; addStreamJunction
+            # subscribes them in that order, PartitionStreamReceiver.java:300-307): a
+            # ConcurrentHashMap keyed by query name (:177), holding every query of the partition
+            names = [q.name for q in obj.queries]
+            pos = chm.positions([java_string_hash(nm) for nm in names])
+            qidx.sort(key=lambda i: pos[names.index(queries[i].name)])
             partitions.append(PartitionIR(keys, qidx, fanout))
     names = [q.name for q in queries]
     if len(set(names)) != len(names):
