@@ -610,7 +610,8 @@ def expansion(args, sh, K, local, dev, world, cdev, dist):
             per_rank = sdist.gather_columns(mc)
             if dist.get_rank() == 0:
                 out = sdist.merge_columns(None, per_rank, slog, table=table.to(cdev), n_streams=1)
-                merged += int(out["q"].numel())
+                if i >= warm:  # (timed pushes only, as `matches`)
+                    merged += int(out["q"].numel())
             torch.cuda.synchronize()
             n_local = int(mc["q"].numel())
             t4 = time.perf_counter()
@@ -643,6 +644,8 @@ def expansion(args, sh, K, local, dev, world, cdev, dist):
          "push_ms_per_step": push_ms / steps, "poll_ms_per_step": (el * 1e3 - push_ms - gather_ms) / steps,
          "matches_per_step": matches / steps, "pattern_events_per_s": pe_timed / el, "matches_per_s": matches / el}
     if world > 1:
+        if dist.get_rank() == 0 and merged != matches:
+            raise RuntimeError(f"the gather merged {merged} matches, the ranks produced {matches}")
         r["rccl_gather_merge_ms_per_step"] = gather_ms / steps
         r["merged_matches_per_step_rank0"] = merged / steps
         r["gather_merge_ns_per_match"] = gather_ms * 1e6 / max(1, matches)

@@ -811,6 +811,8 @@ struct sdh_engine {
   int64_t r_blk_taken = 0;           // blocks the last launch took (ring mode: may exceed r_blocks)
   // direct R18 placement (matches.hip ratchet_place_kernel): the (event, query rank) count matrix
   DevBuf<int32_t> p_cnt;            // direct placement: the (event, rank) count matrix
+  DevBuf<int32_t> d_place_rank;     // [query][stream] 1 + its rank among the stream's K_ratchet queries
+  std::vector<int> place_nr;        // [stream] K_ratchet queries reading it
   bool r_placing = false;            //   the last K_ratchet launch wrote it (PLACE variant)
   DevBuf<uint8_t> p_ptemp;
   int64_t r_seq_base = 0;            // seq of the last launch's first event
@@ -1026,10 +1028,13 @@ const int32_t* fan_positions(sdh_engine* e, sdh_engine::Route& rt, const kg::LFa
 }
 
 // A normal-mode push places its K_ratchet matches directly (the PLACE variant counts them per
-// (event, rank) cell) when the count matrix stays within 2^30 cells and timestamps are in order.
-bool ratchet_placeable(const sdh_engine* e, int64_t n_events, bool full) {
-  const int nr = (int)e->prog.q.size();  // receiver ranks < queries
-  return !(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) && !full && n_events > 0 &&
+// (event, rank) cell, the ranks being the stream's K_ratchet queries in R18 order: place_rank) when
+// the count matrix stays within 2^30 cells and the launch runs without the full-expiry re-run (the
+// PLACE variant's pop levels assume the chunked launch's deques; a full-expiry launch appends to
+// the table instead).
+bool ratchet_placeable(const sdh_engine* e, int stream, int64_t n_events, bool full) {
+  const int nr = e->place_nr[(size_t)stream];
+  return !(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) && !full && n_events > 0 && !e->ck.active &&
          (double)n_events * nr <= (double)(1 << 30) && !getenv("SDH_NO_PLACE");
 }
 
@@ -1037,8 +1042,8 @@ bool ratchet_placeable(const sdh_engine* e, int64_t n_events, bool full) {
 // the window's rows (matches.hip ratchet_place_kernel). False, with nothing written, when the launch
 // did not count them (ratchet_placeable) or the rows would pass 2^31: the caller appends to the
 // table instead.
-bool place_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base, int64_t n_events) {
-  const int nr = (int)e->prog.q.size();
+bool place_ratchet(sdh_engine* e, int stream, const int64_t* ts_col, int64_t seq_base, int64_t n_events) {
+  const int nr = e->place_nr[(size_t)stream];
   const int64_t rows = e->r_matches, n0 = e->mt.n;
   if (!e->r_placing || n0 + rows >= INT32_MAX) return false;
   const size_t keep = (size_t)n0, want = (size_t)(n0 + rows);
@@ -1053,7 +1058,7 @@ bool place_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base, int64
   const size_t tb = sdh_place_temp_bytes(cells);
   e->p_ptemp.ensure(tb);
   HIPCHK(sdh_place_ratchet(e->d_rmatch.p, e->r_blk_recs, e->d_blk_count.p, e->d_blk_group.p, e->r_blocks_used, rows,
-                           e->d_out_rank.p, (int)e->prog.stream_types.size(), nr, n_events, e->p_cnt.p, e->p_ptemp.p,
+                           e->d_place_rank.p, (int)e->prog.stream_types.size(), nr, n_events, e->p_cnt.p, e->p_ptemp.p,
                            e->p_ptemp.n, e->d_rg.p, ts_col, seq_base, n0, e->po_q.p, e->po_key.p, e->po_ts.p,
                            e->po_seq.p, e->po_tb.p, e->po_off.p, e->po_words.p, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
@@ -1423,7 +1428,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
                           hipMemcpyHostToDevice, e->stream));
     // 8-B records address e2 by a 26-bit batch offset; larger batches, and placing launches (the
     // record carries its pop level), use 16-B records
-    const bool placing = ratchet_placeable(e, n, full);
+    const bool placing = ratchet_placeable(e, stream, n, full);
     const int wide = (n > ((int64_t)1 << 26) || placing) ? 1 : 0;
     if (n > ((int64_t)1 << 32)) throw Error(SDH_E_INVALID, "batch larger than 2^32 events");
     e->d_rmatch.ensure((size_t)e->r_blocks * e->r_blk_recs * (wide ? 2 : 1));
@@ -1479,11 +1484,11 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.rec_total = e->d_rtotal.p;
     L.err = e->d_err.p;
     if (placing) {
-      const int nr = (int)e->prog.q.size();
+      const int nr = e->place_nr[(size_t)stream];
       e->p_cnt.ensure((size_t)(n * nr));
       HIPCHK(hipMemsetAsync(e->p_cnt.p, 0, (size_t)(n * nr) * 4, e->stream));
       L.pcnt = e->p_cnt.p;
-      L.out_rank = e->d_out_rank.p;
+      L.out_rank = e->d_place_rank.p;
       L.n_ranks = nr;
       L.n_streams = (int32_t)e->prog.stream_types.size();
     }
@@ -3095,7 +3100,7 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     const bool only_ratchet = e->device_matches == 0 && e->g_dev_matches == 0;
     const bool placeable = only_ratchet && !e->ck.active && (e->mt.n == 0 || e->mt.placed);
     if (!(only_ratchet && e->r_matches == 0) &&
-        !(placeable && place_ratchet(e, B.ts, B.seq_base, b->n))) {
+        !(placeable && place_ratchet(e, stream, B.ts, B.seq_base, b->n))) {
       placed_to_table(e);
       const int64_t n0 = e->mt.n;
       append_chain(e);
@@ -3436,6 +3441,23 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
       e->d_ck_minor.ensure(r1.size());
       HIPCHK(hipMemcpy(e->d_ck_major.p, e->ck_major.data(), r1.size() * 4, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(e->d_ck_minor.p, e->ck_minor.data(), r1.size() * 4, hipMemcpyHostToDevice));
+    }
+    // direct placement ranks: per stream its K_ratchet queries in R18 (out_rank) order
+    {
+      const size_t ns = e->prog.stream_types.size();
+      std::vector<int32_t> pr(std::max<size_t>(1, nq_all * ns), 0);
+      e->place_nr.assign(ns, 0);
+      for (size_t st = 0; st < ns; ++st) {
+        std::vector<int> qs;
+        for (const auto& g : e->rg)
+          if (g.stream == (int)st)
+            for (int l = 0; l < g.n_lanes; ++l) qs.push_back(g.qid[l]);
+        std::sort(qs.begin(), qs.end(), [&](int a, int b) { return e->out_rank[a * ns + st] < e->out_rank[b * ns + st]; });
+        for (size_t k = 0; k < qs.size(); ++k) pr[(size_t)qs[k] * ns + st] = (int32_t)k + 1;
+        e->place_nr[st] = (int)qs.size();
+      }
+      e->d_place_rank.ensure(pr.size());
+      HIPCHK(hipMemcpy(e->d_place_rank.p, pr.data(), pr.size() * 4, hipMemcpyHostToDevice));
     }
     std::vector<int32_t> qinfo(std::max<size_t>(1, 2 * nq_all), 0);
     for (size_t q = 0; q < nq_all; ++q) {

@@ -205,13 +205,17 @@ def rank_table(ir: ProgramIR):
     return table
 
 
-def merge_keys(cols, table, ns, stream_log: StreamLog):
-    """Primary merge key of each row: trigger seq << RANK_BITS | class, class 0 for a timer match and
-    1 + the global receiver rank of (query, stream) for an event match."""
+def merge_keys(cols, table, ns, stream_log: StreamLog, seq_ref: int = 0):
+    """Primary merge key of each row: (trigger seq - seq_ref) << RANK_BITS | class, class 0 for a
+    timer match and 1 + the global receiver rank of (query, stream) for an event match. seq_ref is
+    the window's smallest trigger seq (as the engine's hi keys subtract its last poll's seq)."""
     import torch
     timer = cols["tb"] != TB_EVENT
     cls = table[cols["q"] * ns + stream_log.stream_of(cols["seq"], timer)] + 1
-    return (cols["seq"] << RANK_BITS) | torch.where(timer, torch.zeros_like(cls), cls), timer
+    rel = cols["seq"] - seq_ref
+    if rel.numel() and (int(rel.min()) < 0 or int(rel.max()) >= 1 << (63 - RANK_BITS)):
+        raise ValueError("trigger seqs outside the merge window")
+    return (rel << RANK_BITS) | torch.where(timer, torch.zeros_like(cls), cls), timer
 
 
 def merge_order(keys: Sequence["object"]):
@@ -244,7 +248,8 @@ def merge_columns(ir: Optional[ProgramIR], per_rank: Sequence[dict], stream_log:
         return cat
     ns = n_streams or len(ir.streams)
     table = (rank_table(ir) if table is None else table).to(dev)
-    keys, timers = zip(*(merge_keys(c, table, ns, stream_log) for c in per_rank))
+    seq_ref = min(int(c["seq"].min()) for c in per_rank if c["seq"].numel())
+    keys, timers = zip(*(merge_keys(c, table, ns, stream_log, seq_ref) for c in per_rank))
     if not any(bool(t.any()) for t in timers):
         pos = torch.cat(merge_order(keys))
         perm = torch.empty_like(pos)
