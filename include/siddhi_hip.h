@@ -184,6 +184,14 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out);
  * state only for instances that hold partials -- PartitionRuntime.java:257-306 clones per key
  * lazily): live entry bytes, reserved slab bytes, directory bytes. */
 int sdh_engine_state_bytes(sdh_engine* e, int64_t* live_bytes, int64_t* reserved_bytes, int64_t* dir_bytes);
+/* The text behind string dictionary ids, as String.hashCode and UTF-16 length per id. Needed only by
+ * a partition keyed by a string attribute whose queries also read a stream it does not key: that
+ * stream reaches every key's junction in the order of a ConcurrentHashMap of "streamId" +
+ * String.valueOf(key) (partition/PartitionStreamReceiver.java:277-281), which hashes the key's text.
+ * Register every id such a key can take (a later call may add ids) before the push that needs it,
+ * and again after sdh_engine_restore; a missing id fails that push with SDH_E_INVALID. */
+int sdh_engine_set_strings(sdh_engine* e, int64_t n, const int32_t* ids, const int32_t* java_hash,
+                           const int32_t* utf16_len);
 int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len);
 int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len);
 void sdh_free(void* p);

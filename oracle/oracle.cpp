@@ -932,6 +932,7 @@ struct Engine {
   std::vector<i64> deferred_seq;
   std::string err;
   i64 cur_seq = 0;             // the event being processed (Match::seq)
+  std::map<i64, std::pair<int32_t, int64_t>> str_info;  // dictionary id -> (String.hashCode, length)
   bool in_timer = false;       // a timer is firing (Match::tb = timer_key)
   i64 timer_key = INT64_MIN;
   size_t gc_threshold = 1 << 20;
@@ -1421,8 +1422,17 @@ void deliver_to(Engine* e, int qi, int stream, const std::vector<i64>& seqs) {
       if (e->key_type[pi] == T_BOOL) return std::string(k ? "true" : "false");
       return std::to_string((long long)k);
     };
+    // a string key's String.valueOf is its text: "streamId" + text hashes as id_hash * 31^len + hash
+    auto key_hash = [&](i64 k) -> int32_t {
+      if (e->key_type[pi] != T_STRING) return java_hash_append(fo.id_hash, value_of(k));
+      auto it = e->str_info.find(k);
+      if (it == e->str_info.end()) throw std::runtime_error("partition key string id without its text hash");
+      uint32_t h = (uint32_t)fo.id_hash;
+      for (int64_t c = 0; c < it->second.second; ++c) h *= 31u;
+      return (int32_t)(h + (uint32_t)it->second.first);
+    };
     JavaCHM m;
-    for (size_t k = 0; k < ko.size(); ++k) m.put(java_hash_append(fo.id_hash, value_of(ko[k])), (int)k);
+    for (size_t k = 0; k < ko.size(); ++k) m.put(key_hash(ko[k]), (int)k);
     for (int k : m.order())
       for (auto& rt : e->part_inst[pi].at(ko[(size_t)k])) run_chunk(e, rt.get(), stream, seqs);
     return;
@@ -1558,6 +1568,12 @@ int oracle_send(OracleEngine* e, int32_t stream, int64_t n, const int64_t* ts, c
 }
 
 int64_t oracle_num_matches(const OracleEngine* e) { return (int64_t)e->matches.size(); }
+
+// the text of string dictionary ids as (String.hashCode, UTF-16 length): a string partition key's
+// String.valueOf (the fan-out order hashes it)
+void oracle_set_strings(OracleEngine* e, int64_t n, const int32_t* ids, const int32_t* hash, const int32_t* len) {
+  for (int64_t i = 0; i < n; ++i) e->str_info[ids[i]] = {hash[i], (int64_t)len[i]};
+}
 
 // test hook: the iteration position of each of n keys (String.hashCode values, inserted in order)
 // in the restated ConcurrentHashMap

@@ -46,6 +46,9 @@ void oracle_clear_matches(OracleEngine* e);
 int oracle_start(OracleEngine* e, int64_t t);
 int oracle_advance_time(OracleEngine* e, int64_t t);
 int oracle_set_playback(OracleEngine* e, int on);
+/* String dictionary ids' text as (String.hashCode, UTF-16 length): the fan-out order of a partition
+ * keyed by a string attribute hashes String.valueOf(key). */
+void oracle_set_strings(OracleEngine* e, int64_t n, const int32_t* ids, const int32_t* hash, const int32_t* len);
 /* Partial matches held in the pending lists of every pre-processor (after the last send). */
 int64_t oracle_live_partials(const OracleEngine* e);
 const char* oracle_error(const OracleEngine* e);

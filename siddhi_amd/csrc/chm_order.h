@@ -21,6 +21,17 @@ inline int32_t java_hash_cat(int32_t prefix_hash, const std::string& s) {
   return (int32_t)h;
 }
 
+// String.hashCode of prefix + s from s's own hashCode and UTF-16 length:
+// h(p + s) = h(p) * 31^len(s) + h(s) (mod 2^32)
+inline int32_t java_hash_cat_hashed(int32_t prefix_hash, int32_t s_hash, int64_t s_len) {
+  uint32_t m = 1, b = 31;
+  for (int64_t e = s_len; e > 0; e >>= 1) {
+    if (e & 1) m *= b;
+    b *= b;
+  }
+  return (int32_t)((uint32_t)prefix_hash * m + (uint32_t)s_hash);
+}
+
 // String.valueOf of a partition key's value (ValuePartitionExecutor.java:34-40): int / long in
 // decimal, bool as true / false
 inline std::string java_value_of(bool is_bool, int64_t v) {

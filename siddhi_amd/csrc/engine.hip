@@ -12,6 +12,7 @@
 #include <array>
 #include <cmath>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <cstdarg>
 #include <cstdio>
@@ -715,7 +716,8 @@ struct sdh_engine {
     DevBuf<int64_t> key_of_id;
     int64_t tmask = 0, max_keys = 0;
     // fan-out partitions: keys in creation order (dense id, value), for the junction-map order
-    bool track = false, kbool = false;
+    bool track = false;
+    int kkind = 0;                   // key values: 0 int / long, 1 bool, 2 string (dictionary ids)
     int64_t nk_seen = 0;
     std::vector<int64_t> korder_kid, korder_key;
     DevBuf<int64_t> nk_tmp;
@@ -813,6 +815,9 @@ struct sdh_engine {
   DevBuf<int32_t> p_cnt;            // direct placement: the (event, rank) count matrix
   DevBuf<int32_t> d_place_rank;     // [query][stream] 1 + its rank among the stream's K_ratchet queries
   std::vector<int> place_nr;        // [stream] K_ratchet queries reading it
+  // string dictionary ids -> (String.hashCode, UTF-16 length) of their text (sdh_engine_set_strings):
+  // the fan-out order of partitions keyed by a string attribute
+  std::unordered_map<int32_t, std::pair<int32_t, int64_t>> str_info;
   bool r_placing = false;            //   the last K_ratchet launch wrote it (PLACE variant)
   DevBuf<uint8_t> p_ptemp;
   int64_t r_seq_base = 0;            // seq of the last launch's first event
@@ -991,7 +996,7 @@ void chunk_rows(sdh_engine* e, int64_t n0) {
 
 // keys this push created (ids [nk_seen, new_n)), in the order of their first events: the order
 // PartitionRuntime.clonePartition adds them to every receiver's junction map
-void track_new_keys(sdh_engine* e, sdh_engine::Route& rt, int64_t new_n, int64_t nruns, bool kbool) {
+void track_new_keys(sdh_engine* e, sdh_engine::Route& rt, int64_t new_n, int64_t nruns, int kkind) {
   const int64_t m = new_n - rt.nk_seen;
   rt.nk_tmp.ensure((size_t)(2 * m));
   HIPCHK(sdh_new_keys(e->r_uniq.p, e->r_nruns.p, nruns, e->r_off.p, e->r_idx_s.p, rt.key_of_id.p, rt.nk_seen, new_n,
@@ -1006,7 +1011,7 @@ void track_new_keys(sdh_engine* e, sdh_engine::Route& rt, int64_t new_n, int64_t
     rt.korder_kid.push_back(rt.nk_seen + k);
     rt.korder_key.push_back(v[(size_t)(2 * k + 1)]);
   }
-  rt.kbool = kbool;
+  rt.kkind = kkind;
   rt.nk_seen = new_n;
 }
 
@@ -1017,7 +1022,17 @@ const int32_t* fan_positions(sdh_engine* e, sdh_engine::Route& rt, const kg::LFa
   if (f.n != nk) {
     const size_t m = std::min<size_t>((size_t)nk, rt.korder_key.size());
     std::vector<int32_t> hs(m), byk((size_t)std::max<int64_t>(1, nk), 0);
-    for (size_t j = 0; j < m; ++j) hs[j] = sdh::java_hash_cat(fo.id_hash, sdh::java_value_of(rt.kbool, rt.korder_key[j]));
+    for (size_t j = 0; j < m; ++j) {
+      const int64_t k = rt.korder_key[j];
+      if (rt.kkind == 2) {  // String.valueOf of a string is its text: its registered hash and length
+        auto it = e->str_info.find((int32_t)k);
+        if (it == e->str_info.end())
+          throw Error(SDH_E_INVALID, fmt("partition key string id %lld has no text hash (sdh_engine_set_strings)", (long long)k));
+        hs[j] = sdh::java_hash_cat_hashed(fo.id_hash, it->second.first, it->second.second);
+      } else {
+        hs[j] = sdh::java_hash_cat(fo.id_hash, sdh::java_value_of(rt.kkind == 1, k));
+      }
+    }
     const std::vector<int32_t> pos = sdh::ChmOrder().positions(hs);
     for (size_t j = 0; j < m; ++j) byk[(size_t)rt.korder_kid[j]] = pos[j];
     f.pos.ensure(byk.size());
@@ -2589,7 +2604,8 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       if ((int)e->part_kept.size() <= pi) e->part_kept.resize(pi + 1, 0);
       e->part_kept[pi] = n - (last_kid == 0xFFFFFFFFu ? last_cnt : 0);
     }
-    if (rt.track && hv[0] > rt.nk_seen) track_new_keys(e, rt, hv[0], hv[1], type == kg::T_BOOL);
+    if (rt.track && hv[0] > rt.nk_seen)
+      track_new_keys(e, rt, hv[0], hv[1], type == kg::T_BOOL ? 1 : type == kg::T_STRING ? 2 : 0);
     // routing (key column read, key/kid/idx written and sorted)
     bytes += (double)n * (8 + 8 + 4 + 4 + 2 * (4 + 4) + 3 * 4);
     if (gsp && gsp->n_groups > 0 && timed) {
@@ -3664,6 +3680,18 @@ int sdh_engine_state_bytes(sdh_engine* e, int64_t* live_bytes, int64_t* reserved
   });
 }
 
+int sdh_engine_set_strings(sdh_engine* e, int64_t n, const int32_t* ids, const int32_t* java_hash,
+                           const int32_t* utf16_len) {
+  if (!e || n < 0 || (n > 0 && (!ids || !java_hash || !utf16_len))) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    for (int64_t i = 0; i < n; ++i) {
+      if (utf16_len[i] < 0) throw Error(SDH_E_INVALID, "negative string length");
+      e->str_info[ids[i]] = {java_hash[i], (int64_t)utf16_len[i]};
+    }
+    return SDH_OK;
+  });
+}
+
 int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
   if (!e || !blob || !len) return SDH_E_INVALID;
   return guard(e, [&]() {
@@ -3733,7 +3761,7 @@ int sdh_engine_snapshot(sdh_engine* e, void** blob, size_t* len) {
       put_dev(rp->n_keys.p, 4);
       put_dev(rp->key_of_id.p, (size_t)rp->max_keys * 8);
       // fan-out partitions: the keys' creation order (the junction maps' insertion order)
-      w.push_back(rp->kbool ? 1 : 0);
+      w.push_back(rp->kkind);
       w.push_back(rp->nk_seen);
       w.push_back((int64_t)rp->korder_kid.size());
       for (size_t j = 0; j < rp->korder_kid.size(); ++j) {
@@ -3911,7 +3939,7 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len) {
       get_dev(rp->tid.p, slots * 4);
       get_dev(rp->n_keys.p, 4);
       get_dev(rp->key_of_id.p, (size_t)rp->max_keys * 8);
-      rp->kbool = nx() != 0;
+      rp->kkind = (int)nx();
       rp->nk_seen = nx();
       const int64_t nko = nx();
       if (nko < 0 || nko > rp->max_keys) throw Error(SDH_E_INVALID, "bad snapshot key order");

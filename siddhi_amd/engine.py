@@ -62,7 +62,7 @@ EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engi
            "sdh_engine_pending_matches", "sdh_engine_start", "sdh_engine_advance_time", "sdh_engine_stats",
            "sdh_engine_snapshot", "sdh_engine_state_bytes",
            "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version",
-           "sdh_engine_debug_digest"]
+           "sdh_engine_debug_digest", "sdh_engine_set_strings"]
 
 _lib = None
 
@@ -97,6 +97,7 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_last_error.restype = ctypes.c_char_p
     lib.sdh_version.restype = ctypes.c_char_p
     lib.sdh_engine_debug_digest.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
+    lib.sdh_engine_set_strings.argtypes = [P, ctypes.c_int64, P, P, P]
     _lib = lib
     return lib
 
@@ -219,6 +220,14 @@ class HipEngine:
                 j += 1 + c
             out.append((int(q[i]), int(k[i]), int(ts[i]), tuple(slots)))
         return out
+
+    def set_strings(self, ids, texts):
+        """The String.hashCode and UTF-16 length of each dictionary id's text (sdh_engine_set_strings)."""
+        from .planner import java_string_hash
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        h = np.array([java_string_hash(t) for t in texts], dtype=np.int32)
+        ln = np.array([len(t.encode("utf-16-le")) // 2 for t in texts], dtype=np.int32)
+        self._check(self.lib.sdh_engine_set_strings(self.h, len(ids), ids.ctypes.data, h.ctypes.data, ln.ctypes.data))
 
     def start(self, t: int):
         """SiddhiAppRuntime.start at time t (absent states schedule their first checks from it)."""

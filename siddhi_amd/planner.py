@@ -596,9 +596,9 @@ def plan(app: ql.App) -> ProgramIR:
                     # of its receiver's ConcurrentHashMap of "streamId + key" junctions
                     # (PartitionStreamReceiver.java:271-275); the engine restates that order for
                     # String.valueOf of int / long / bool keys
-                    if kclass - {"num", T_BOOL}:
+                    if kclass - {"num", T_BOOL, T_STRING}:
                         raise SiddhiAppCreationException(
-                            "a non-partitioned stream inside a partition keyed by string / float / double "
+                            "a non-partitioned stream inside a partition keyed by float / double "
                             "values is not on the accelerated path")
                     fanout.append((st.stream_idx, java_string_hash(name), len(name)))
                 qidx.append(len(queries))

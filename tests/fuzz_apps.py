@@ -316,6 +316,8 @@ def fanout_events(seed, n=600, keys=40, key_type="int"):
             k = k * 1_000_003 - 7_000_000_000 if k % 2 else k
         elif key_type == "bool":
             k = bool(k % 2)
+        elif key_type == "string":  # texts of several lengths (the map hashes "A" + the text)
+            k = ("IBM", "WSO2", "ORCL", "é", "")[k % 5] + "x" * (k // 5)
         row = [k, int(rng.integers(0, 10)), float(np.float32(rng.integers(0, 20) / 2.0)),
                str(rng.choice(list("xyz")))]
         st = "A" if rng.random() < 0.6 else "B"

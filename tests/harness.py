@@ -48,6 +48,7 @@ def oracle_lib():
         lib.oracle_start.argtypes = [P, I64]
         lib.oracle_advance_time.argtypes = [P, I64]
         lib.oracle_set_playback.argtypes = [P, ctypes.c_int]
+        lib.oracle_set_strings.argtypes = [P, I64, VP, VP, VP]
         _lib = lib
     return _lib
 
@@ -92,6 +93,13 @@ class OracleEngine:
 
     def set_playback(self, on: bool):
         self.lib.oracle_set_playback(self.h, int(on))
+
+    def set_strings(self, ids, texts):
+        from siddhi_amd.planner import java_string_hash
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        h = np.array([java_string_hash(t) for t in texts], dtype=np.int32)
+        ln = np.array([len(t.encode("utf-16-le")) // 2 for t in texts], dtype=np.int32)
+        self.lib.oracle_set_strings(self.h, len(ids), ids.ctypes.data, h.ctypes.data, ln.ctypes.data)
 
     def start(self, t: int):
         if self.lib.oracle_start(self.h, int(t)) != 0:
@@ -157,6 +165,7 @@ class App:
         if self.playback and hasattr(self.engine, "set_playback"):
             self.engine.set_playback(True)   # (the HIP engine takes SDH_FLAG_PLAYBACK at create)
         self.log = EventLog()
+        self._strings_sent = 0  # dictionary ids whose text the engine has (set_strings)
         self.matches: List[tuple] = []
         self.meta: List[tuple] = []  # per match (trigger seq, timer tiebreak) when the engine has them
 
@@ -167,6 +176,11 @@ class App:
         si = self.ir.stream_index(stream)
         vals, nulls = encode_rows(rows, self.ir.streams[si].attr_types, self.dictionary)
         self.log.append(si, ts, vals, nulls)
+        n = len(self.dictionary)
+        if n > self._strings_sent and hasattr(self.engine, "set_strings"):
+            ids = list(range(self._strings_sent, n))
+            self.engine.set_strings(ids, [self.dictionary.lookup(i) for i in ids])
+            self._strings_sent = n
         self.engine.send(si, ts, vals, nulls, as_chunk)
         self._take()
 

@@ -99,7 +99,7 @@ def test_absent_timelines_as_chunks(seed):
     assert g.matches == o.matches
 
 
-@pytest.mark.parametrize("key_type", ["int", "bool"])
+@pytest.mark.parametrize("key_type", ["int", "bool", "string"])
 @pytest.mark.parametrize("seed", range(4))
 def test_fanout_as_chunks(seed, key_type):
     src = fanout_app(seed, key_type)

@@ -217,11 +217,12 @@ def test_kgen_host_fanout(seed, key_type):
     assert g.matches == o.matches
 
 
-@pytest.mark.parametrize("key_type", ["string", "float", "double"])
-def test_fanout_refused_for_text_keys(key_type):
-    """The junction-map order needs String.valueOf of the key: string / float / double keys (the
-    dictionary id, Java's float formatting) are refused at plan time for fan-out partitions, while the
-    same partition without the unkeyed stream plans."""
+@pytest.mark.parametrize("key_type", ["float", "double"])
+def test_fanout_refused_for_float_keys(key_type):
+    """The junction-map order needs String.valueOf of the key: float / double keys (Java's float
+    formatting) are refused at plan time for fan-out partitions, while the same partition without the
+    unkeyed stream plans. String keys plan: the caller registers each id's text hash
+    (sdh_engine_set_strings; test_gpu_fanout.py)."""
     from fuzz_apps import fanout_app
     from siddhi_amd.planner import compile_app
     from siddhi_amd.ql import SiddhiAppCreationException
@@ -229,17 +230,17 @@ def test_fanout_refused_for_text_keys(key_type):
     with pytest.raises(SiddhiAppCreationException):
         compile_app(src)
     keyed = src.replace("partition with (k of A)", "partition with (k of A, k of B)")
-    if key_type == "string":
-        keyed = keyed.replace("define stream B (k int", "define stream B (k string")
-    elif key_type in ("float", "double"):
-        keyed = keyed.replace("define stream B (k int", f"define stream B (k {key_type}")
+    keyed = keyed.replace("define stream B (k int", f"define stream B (k {key_type}")
     compile_app(keyed)
+    compile_app(fanout_app(0, "string"))
 
 
-def test_java_string_hash_matches_known_values():
-    from siddhi_amd.planner import java_string_hash
-    # published String.hashCode values: "", "hello", "true", "false"
-    assert java_string_hash("") == 0
-    assert java_string_hash("hello") == 99162322
-    assert java_string_hash("true") == 3569038
-    assert java_string_hash("false") == 97196323
+def test_fanout_string_keys_on_the_oracle():
+    """String keys: the oracle orders the fan-out by "A" + the key's text (its registered
+    String.hashCode and UTF-16 length), so the order differs from the int ids'."""
+    from fuzz_apps import fanout_app, fanout_events
+    src = fanout_app(2, "string")
+    o = App(src)
+    for stream, row, t in fanout_events(2, keys=30, key_type="string"):
+        o.send(stream, [row], [t])
+    assert len(o.matches) > 20
