@@ -289,6 +289,204 @@ struct JavaCHM {
 };
 
 // String.hashCode of `prefix + s` from the prefix's hash and the UTF-16 (here ASCII) units of s
+// Java 8 Float.toString / Double.toString (sun.misc.FloatingDecimal; the JDK is outside the
+// reference tree): String.valueOf of a float / double partition key. The oracle's own restatement
+// (the engine has csrc/java_fmt.h, the tests tests/java_fmt.py; test_java_fmt.py compares the three).
+// Magnitudes: base-2^32 little-endian limbs.
+using Mag = std::vector<uint32_t>;
+Mag mag_of(uint64_t v, int p5, int p2) {
+  Mag m;
+  for (; v; v >>= 32) m.push_back((uint32_t)v);
+  for (int k = 0; k < p5; ++k) {
+    uint64_t c = 0;
+    for (auto& x : m) { c += (uint64_t)x * 5; x = (uint32_t)c; c >>= 32; }
+    if (c) m.push_back((uint32_t)c);
+  }
+  for (int k = 0; k < p2; ++k) {
+    uint32_t c = 0;
+    for (auto& x : m) { uint32_t nc = x >> 31; x = (x << 1) | c; c = nc; }
+    if (c) m.push_back(c);
+  }
+  return m;
+}
+int mag_cmp(Mag a, Mag b) {
+  while (!a.empty() && !a.back()) a.pop_back();
+  while (!b.empty() && !b.back()) b.pop_back();
+  if (a.size() != b.size()) return a.size() < b.size() ? -1 : 1;
+  for (size_t i = a.size(); i-- > 0;) if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+  return 0;
+}
+Mag mag_add(const Mag& a, const Mag& b) {
+  Mag r(std::max(a.size(), b.size()) + 1, 0);
+  uint64_t c = 0;
+  for (size_t i = 0; i < r.size(); ++i) {
+    c += (uint64_t)(i < a.size() ? a[i] : 0) + (i < b.size() ? b[i] : 0);
+    r[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return r;
+}
+void mag_sub(Mag& a, const Mag& b) {
+  int64_t br = 0;
+  for (size_t i = 0; i < a.size(); ++i) {
+    int64_t d = (int64_t)a[i] - (i < b.size() ? b[i] : 0) - br;
+    br = d < 0;
+    a[i] = (uint32_t)(d + (br << 32));
+  }
+}
+Mag mag_mul10(const Mag& a) {
+  Mag r = mag_add(a, a), r4 = mag_add(r, r);
+  return mag_add(mag_add(r4, r4), r);  // 8a + 2a
+}
+
+std::string java_fp_string(uint64_t raw, bool dbl) {
+  const int MB = dbl ? 52 : 23, EB = dbl ? 11 : 8, bias = dbl ? 1023 : 127;
+  const bool neg = (raw >> (MB + EB)) & 1;
+  uint64_t f = raw & ((1ull << MB) - 1);
+  int be = (int)((raw >> MB) & ((1u << EB) - 1));
+  if (be == (1 << EB) - 1) return f ? "NaN" : neg ? "-Infinity" : "Infinity";
+  int nsig;
+  if (be == 0) {
+    if (!f) return neg ? "-0.0" : "0.0";
+    int width = 0;
+    for (uint64_t t = f; t; t >>= 1) ++width;
+    const int shift = MB + 1 - width;  // normalise the denormal
+    f <<= shift;
+    be = 1 - shift;
+    nsig = width;
+  } else {
+    f |= 1ull << MB;
+    nsig = MB + 1;
+  }
+  be -= bias;
+  f <<= 52 - MB;
+  std::vector<int> dg;
+  int decexp;  // value = 0.dg x 10^decexp
+  int tz = 0;
+  while (!((f >> tz) & 1)) ++tz;
+  const int nfb = 53 - tz, tiny = std::max(0, nfb - be - 1);
+  static const int n5[27] = {0, 3, 5, 7, 10, 12, 14, 17, 19, 21, 24, 26, 28, 31, 33, 35, 38, 40, 42, 45, 47, 49, 52, 54, 56, 59, 61};
+  if (be >= -21 && be <= 62 && tiny == 0) {
+    // an integer in a long: its digits, the digits past the float's precision rounded away
+    uint64_t v = be >= 52 ? f << (be - 52) : f >> (52 - be);
+    int drop = 0;
+    if (be > nsig) {
+      const int p = be - nsig - 1;
+      if (p > 1 && p < 64) drop = (int)std::floor(p * 0.30102999566398119521);  // digits of 2^p - 1
+    }
+    decexp = drop;
+    if (drop) {
+      uint64_t t = 1;
+      for (int i = 0; i < drop; ++i) t *= 10;
+      const uint64_t rem = v % t;
+      v = v / t + (rem >= t / 2 ? 1 : 0);
+    }
+    std::string s = std::to_string((unsigned long long)v);
+    while (s.size() > 1 && s.back() == '0') { s.pop_back(); ++decexp; }
+    for (char c : s) dg.push_back(c - '0');
+    decexp += (int)dg.size();
+  } else {
+    double d2;
+    const uint64_t b2 = 0x3FF0000000000000ull | (f & 0xFFFFFFFFFFFFFull);
+    std::memcpy(&d2, &b2, 8);
+    int de = (int)std::floor((d2 - 1.5) * 0.289529654 + 0.176091259 + (double)be * 0.301029995663981);
+    const int B5 = std::max(0, -de), S5 = std::max(0, de);
+    int B2 = B5 + tiny + be, S2 = S5 + tiny, M2 = B2 - nsig;
+    const uint64_t fr = f >> tz;
+    B2 -= nfb - 1;
+    const int common = std::min(B2, S2);
+    B2 -= common; S2 -= common; M2 -= common;
+    if (nfb == 1) --M2;
+    if (M2 < 0) { B2 -= M2; S2 -= M2; M2 = 0; }
+    const int bbits = nfb + B2 + (B5 < 27 ? n5[B5] : B5 * 3);
+    const int tbits = S2 + 1 + (S5 + 1 < 27 ? n5[S5 + 1] : (S5 + 1) * 3);
+    bool low, high;
+    int ldiff;  // sign of 2B - 10S where it decides the last digit
+    if (bbits < 64 && tbits < 64) {
+      const int W = bbits < 32 && tbits < 32 ? 32 : 64;  // Java int / long arithmetic, wrapping
+      auto wr = [W](unsigned __int128 x) -> int64_t {
+        return W == 32 ? (int64_t)(int32_t)(uint32_t)x : (int64_t)(uint64_t)x;
+      };
+      unsigned __int128 p5b = 1, p5s = 1;
+      for (int i = 0; i < B5; ++i) p5b *= 5;
+      for (int i = 0; i < S5; ++i) p5s *= 5;
+      int64_t b = wr((unsigned __int128)(uint64_t)wr((unsigned __int128)fr * p5b) << B2);
+      const int64_t sv = wr(p5s << S2);
+      int64_t m = wr(p5b << M2);  // (M5 = B5)
+      const int64_t tens = wr((unsigned __int128)(uint64_t)sv * 10);
+      int64_t q = b / sv;
+      b = wr((unsigned __int128)(uint64_t)(b % sv) * 10);
+      m = wr((unsigned __int128)(uint64_t)m * 10);
+      low = b < m;
+      high = wr((unsigned __int128)(uint64_t)b + (uint64_t)m) > tens;
+      if (q == 0 && !high) --de;
+      else dg.push_back((int)q);
+      if (de < -3 || de >= 8) low = high = false;
+      while (!low && !high) {
+        q = b / sv;
+        b = wr((unsigned __int128)(uint64_t)(b % sv) * 10);
+        m = wr((unsigned __int128)(uint64_t)m * 10);
+        if (m > 0) {
+          low = b < m;
+          high = wr((unsigned __int128)(uint64_t)b + (uint64_t)m) > tens;
+        } else {
+          low = high = true;
+        }
+        dg.push_back((int)q);
+      }
+      const int64_t diff = wr((unsigned __int128)(uint64_t)wr((unsigned __int128)(uint64_t)b << 1) - (uint64_t)tens);
+      ldiff = diff > 0 ? 1 : diff < 0 ? -1 : 0;
+    } else {
+      const Mag S = mag_of(1, S5, S2), T = mag_of(1, S5 + 1, S2 + 1);
+      Mag B = mag_of(fr, B5, B2), M = mag_of(1, B5 + 1, M2 + 1);
+      auto step = [&]() {
+        int q = 0;
+        while (mag_cmp(B, S) >= 0) { mag_sub(B, S); ++q; }
+        B = mag_mul10(B);
+        return q;
+      };
+      int q = step();
+      low = mag_cmp(B, M) < 0;
+      high = mag_cmp(mag_add(B, M), T) >= 0;
+      if (q == 0 && !high) --de;
+      else dg.push_back(q);
+      if (de < -3 || de >= 8) low = high = false;
+      while (!low && !high) {
+        q = step();
+        M = mag_mul10(M);
+        low = mag_cmp(B, M) < 0;
+        high = mag_cmp(mag_add(B, M), T) >= 0;
+        dg.push_back(q);
+      }
+      ldiff = high && low ? mag_cmp(mag_add(B, B), T) : 0;
+    }
+    decexp = de + 1;
+    const bool up = high && (!low || ldiff > 0 || (ldiff == 0 && (dg.back() & 1)));
+    if (up) {  // roundup: the digit count stays
+      size_t i = dg.size() - 1;
+      while (dg[i] == 9 && i > 0) dg[i--] = 0;
+      if (dg[i] == 9) { dg[0] = 1; ++decexp; }
+      else ++dg[i];
+    }
+  }
+  std::string ds;
+  for (int x : dg) ds.push_back((char)('0' + x));
+  std::string out = neg ? "-" : "";
+  const int n = (int)ds.size();
+  if (decexp > 0 && decexp < 8) {
+    const int c = std::min(n, decexp);
+    out += ds.substr(0, c);
+    if (c < decexp) out += std::string(decexp - c, '0') + ".0";
+    else out += "." + (c < n ? ds.substr(c) : std::string("0"));
+  } else if (decexp <= 0 && decexp > -3) {
+    out += "0." + std::string(-decexp, '0') + ds;
+  } else {
+    out += ds.substr(0, 1) + "." + (n > 1 ? ds.substr(1) : std::string("0")) + "E" +
+           (decexp <= 0 ? "-" + std::to_string(1 - decexp) : std::to_string(decexp - 1));
+  }
+  return out;
+}
+
 int32_t java_hash_append(int32_t h, const std::string& s) {
   uint32_t u = (uint32_t)h;
   for (unsigned char c : s) u = 31u * u + c;
@@ -1420,6 +1618,8 @@ void deliver_to(Engine* e, int qi, int stream, const std::vector<i64>& seqs) {
     const auto& ko = e->key_order[pi];
     auto value_of = [&](i64 k) {  // String.valueOf (ValuePartitionExecutor.java:34-40)
       if (e->key_type[pi] == T_BOOL) return std::string(k ? "true" : "false");
+      if (e->key_type[pi] == T_FLOAT) return java_fp_string((uint64_t)(uint32_t)k, false);
+      if (e->key_type[pi] == T_DOUBLE) return java_fp_string((uint64_t)k, true);
       return std::to_string((long long)k);
     };
     // a string key's String.valueOf is its text: "streamId" + text hashes as id_hash * 31^len + hash
@@ -1573,6 +1773,14 @@ int64_t oracle_num_matches(const OracleEngine* e) { return (int64_t)e->matches.s
 // String.valueOf (the fan-out order hashes it)
 void oracle_set_strings(OracleEngine* e, int64_t n, const int32_t* ids, const int32_t* hash, const int32_t* len) {
   for (int64_t i = 0; i < n; ++i) e->str_info[ids[i]] = {hash[i], (int64_t)len[i]};
+}
+
+// test hook: Java 8 Float / Double.toString of raw bits (java_fp_string)
+int oracle_java_fmt(uint64_t bits, int is_double, char* out, int cap) {
+  const std::string t = java_fp_string(bits, is_double != 0);
+  if ((int)t.size() >= cap) return -1;
+  std::memcpy(out, t.c_str(), t.size() + 1);
+  return (int)t.size();
 }
 
 // test hook: the iteration position of each of n keys (String.hashCode values, inserted in order)

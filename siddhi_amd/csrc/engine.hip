@@ -23,6 +23,7 @@
 
 #include "../../include/siddhi_hip.h"
 #include "chm_order.h"
+#include "java_fmt.h"
 #include "gen_lower.h"
 #include "nfa_types.h"
 #include "slab_lower.h"
@@ -717,7 +718,8 @@ struct sdh_engine {
     int64_t tmask = 0, max_keys = 0;
     // fan-out partitions: keys in creation order (dense id, value), for the junction-map order
     bool track = false;
-    int kkind = 0;                   // key values: 0 int / long, 1 bool, 2 string (dictionary ids)
+    int kkind = 0;                   // key values: 0 int / long, 1 bool, 2 string (dictionary ids),
+                                     // 3 float, 4 double (raw bits; NaN canonical)
     int64_t nk_seen = 0;
     std::vector<int64_t> korder_kid, korder_key;
     DevBuf<int64_t> nk_tmp;
@@ -1029,6 +1031,9 @@ const int32_t* fan_positions(sdh_engine* e, sdh_engine::Route& rt, const kg::LFa
         if (it == e->str_info.end())
           throw Error(SDH_E_INVALID, fmt("partition key string id %lld has no text hash (sdh_engine_set_strings)", (long long)k));
         hs[j] = sdh::java_hash_cat_hashed(fo.id_hash, it->second.first, it->second.second);
+      } else if (rt.kkind == 3 || rt.kkind == 4) {  // Float / Double.toString (java_fmt.h)
+        hs[j] = sdh::java_hash_cat(fo.id_hash, rt.kkind == 3 ? sdh::jfmt::float_to_string((uint32_t)k)
+                                                             : sdh::jfmt::double_to_string((uint64_t)k));
       } else {
         hs[j] = sdh::java_hash_cat(fo.id_hash, sdh::java_value_of(rt.kkind == 1, k));
       }
@@ -2605,7 +2610,8 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       e->part_kept[pi] = n - (last_kid == 0xFFFFFFFFu ? last_cnt : 0);
     }
     if (rt.track && hv[0] > rt.nk_seen)
-      track_new_keys(e, rt, hv[0], hv[1], type == kg::T_BOOL ? 1 : type == kg::T_STRING ? 2 : 0);
+      track_new_keys(e, rt, hv[0], hv[1],
+                     type == kg::T_BOOL ? 1 : type == kg::T_STRING ? 2 : type == kg::T_FLOAT ? 3 : type == kg::T_DOUBLE ? 4 : 0);
     // routing (key column read, key/kid/idx written and sorted)
     bytes += (double)n * (8 + 8 + 4 + 4 + 2 * (4 + 4) + 3 * 4);
     if (gsp && gsp->n_groups > 0 && timed) {

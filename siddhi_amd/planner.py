@@ -594,12 +594,9 @@ def plan(app: ql.App) -> ProgramIR:
                         continue
                     # a stream the partition does not key reaches every key's instance, in the order
                     # of its receiver's ConcurrentHashMap of "streamId + key" junctions
-                    # (PartitionStreamReceiver.java:271-275); the engine restates that order for
-                    # String.valueOf of int / long / bool keys
-                    if kclass - {"num", T_BOOL, T_STRING}:
-                        raise SiddhiAppCreationException(
-                            "a non-partitioned stream inside a partition keyed by float / double "
-                            "values is not on the accelerated path")
+                    # (PartitionStreamReceiver.java:277-281); the engine restates that order over
+                    # String.valueOf of the key: int / long / bool text, a string's registered text
+                    # hash (sdh_engine_set_strings), Java 8 Float / Double.toString (java_fmt.h)
                     fanout.append((st.stream_idx, java_string_hash(name), len(name)))
                 qidx.append(len(queries))
                 queries.append(qir)

@@ -318,6 +318,8 @@ def fanout_events(seed, n=600, keys=40, key_type="int"):
             k = bool(k % 2)
         elif key_type == "string":  # texts of several lengths (the map hashes "A" + the text)
             k = ("IBM", "WSO2", "ORCL", "é", "")[k % 5] + "x" * (k // 5)
+        elif key_type in ("float", "double"):  # Float / Double.toString forms: plain, E-notation, NaN, -0.0
+            k = (0.1 * k, k * 1.0e9, -k / 3.0, 2.0 ** -(k + 130), float("nan"), -0.0, 1.0e-5 * k, 2.0e23)[k % 8]
         row = [k, int(rng.integers(0, 10)), float(np.float32(rng.integers(0, 20) / 2.0)),
                str(rng.choice(list("xyz")))]
         st = "A" if rng.random() < 0.6 else "B"

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../siddhi_amd/csrc/chm_order.h"
+#include "../../siddhi_amd/csrc/java_fmt.h"
 #include "../../siddhi_amd/csrc/gen_lower.h"
 
 using namespace sdh::kg;
@@ -41,7 +42,7 @@ struct Host {
   std::vector<std::unique_ptr<Inst>> top;                       // unpartitioned instances
   std::vector<std::map<int64_t, std::vector<std::unique_ptr<Inst>>>> part;
   std::vector<std::vector<int64_t>> korder;  // per partition: keys in creation order
-  std::vector<char> kbool;                   //   bool-valued keys
+  std::vector<char> kkind;                   //   key values: 0 int / long, 1 bool, 3 float, 4 double
   std::vector<Rec> out;
   std::string err;
   int64_t chunk_len = 0;  // >0: unpartitioned instances with a bounded look-back run event chunks
@@ -198,7 +199,7 @@ void* kgh_create(const void* blob, size_t len, int R, int N, int LC) {
       if (h->P.q[qi].partition < 0) h->top[qi].reset(make_inst(h, qi, -1));
     h->part.resize(h->P.parts.size());
     h->korder.resize(h->P.parts.size());
-    h->kbool.resize(h->P.parts.size(), 0);
+    h->kkind.resize(h->P.parts.size(), 0);
     return h;
   } catch (const std::exception&) {
     return nullptr;
@@ -282,8 +283,11 @@ int kgh_send(void* hp, int stream, int64_t n, int64_t seq0, const int64_t* ts, c
         if (key.stream == stream) attr = (int)key.code[0].imm;
       if (const LFanOut* fo = pd.fan(stream)) {  // every key's instances, in the map's order
         std::vector<int32_t> hs;
+        const int kk = h->kkind[pi];
         for (int64_t kv : h->korder[pi])
-          hs.push_back(sdh::java_hash_cat(fo->id_hash, sdh::java_value_of(h->kbool[pi] != 0, kv)));
+          hs.push_back(sdh::java_hash_cat(fo->id_hash, kk == 3   ? sdh::jfmt::float_to_string((uint32_t)kv)
+                                                       : kk == 4 ? sdh::jfmt::double_to_string((uint64_t)kv)
+                                                                 : sdh::java_value_of(kk == 1, kv)));
         const std::vector<int32_t> pos = sdh::ChmOrder().positions(hs);
         for (int64_t k = 0; k < n; ++k)
           for (size_t j = 0; j < h->korder[pi].size(); ++j)
@@ -302,7 +306,8 @@ int kgh_send(void* hp, int stream, int64_t n, int64_t seq0, const int64_t* ts, c
             for (int pq : pd.queries) v.emplace_back(make_inst(h, pq, kv));
             h->part[pi].emplace(kv, std::move(v));
             h->korder[pi].push_back(kv);
-            h->kbool[pi] = h->P.stream_types[stream][attr] == T_BOOL;
+            const int ty = h->P.stream_types[stream][attr];
+            h->kkind[pi] = ty == T_BOOL ? 1 : ty == T_FLOAT ? 3 : ty == T_DOUBLE ? 4 : 0;
           }
         }
         for (auto& kvp : h->part[pi])
@@ -409,3 +414,11 @@ extern "C" void kgh_prof(int64_t* out) {
   for (int k = 0; k < 16; ++k) { out[k] = sdh::kg::g_prof[k]; sdh::kg::g_prof[k] = 0; }
 }
 #endif
+
+// test hook: Java 8 Float / Double.toString of raw bits (java_fmt.h), into out (cap bytes)
+extern "C" int kgh_java_fmt(uint64_t bits, int is_double, char* out, int cap) {
+  const std::string t = is_double ? sdh::jfmt::double_to_string(bits) : sdh::jfmt::float_to_string((uint32_t)bits);
+  if ((int)t.size() >= cap) return -1;
+  std::memcpy(out, t.c_str(), t.size() + 1);
+  return (int)t.size();
+}

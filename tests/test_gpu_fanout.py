@@ -31,7 +31,7 @@ def _send(apps, ev, batch):
 
 
 @pytest.mark.parametrize("batch", [False, True], ids=["per_event", "batched"])
-@pytest.mark.parametrize("key_type", ["int", "long", "bool", "string"])
+@pytest.mark.parametrize("key_type", ["int", "long", "bool", "string", "float", "double"])
 @pytest.mark.parametrize("seed", range(6))
 def test_fanout_on_gpu(seed, key_type, batch):
     src = fanout_app(seed, key_type)

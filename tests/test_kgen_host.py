@@ -217,22 +217,14 @@ def test_kgen_host_fanout(seed, key_type):
     assert g.matches == o.matches
 
 
-@pytest.mark.parametrize("key_type", ["float", "double"])
-def test_fanout_refused_for_float_keys(key_type):
-    """The junction-map order needs String.valueOf of the key: float / double keys (Java's float
-    formatting) are refused at plan time for fan-out partitions, while the same partition without the
-    unkeyed stream plans. String keys plan: the caller registers each id's text hash
-    (sdh_engine_set_strings; test_gpu_fanout.py)."""
+def test_fanout_plans_for_every_key_type():
+    """The junction-map order needs String.valueOf of the key: int / long / bool text, a string's
+    registered text (sdh_engine_set_strings), Java 8 Float / Double.toString (java_fmt.h): every key
+    type plans for fan-out partitions."""
     from fuzz_apps import fanout_app
     from siddhi_amd.planner import compile_app
-    from siddhi_amd.ql import SiddhiAppCreationException
-    src = fanout_app(0, key_type)
-    with pytest.raises(SiddhiAppCreationException):
-        compile_app(src)
-    keyed = src.replace("partition with (k of A)", "partition with (k of A, k of B)")
-    keyed = keyed.replace("define stream B (k int", f"define stream B (k {key_type}")
-    compile_app(keyed)
-    compile_app(fanout_app(0, "string"))
+    for key_type in ("int", "long", "bool", "string", "float", "double"):
+        assert compile_app(fanout_app(0, key_type)).partitions[0].fanout
 
 
 def test_fanout_string_keys_on_the_oracle():
