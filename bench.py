@@ -72,6 +72,7 @@ def parse():
     ap.add_argument("--no-latency", action="store_true", help="skip the small-push latency leg")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-calibrate", action="store_true", help="skip the HBM copy / read ceiling measurement")
     return ap.parse_args()
 
 
@@ -469,6 +470,25 @@ def main():
     }
     if prof:
         result["roofline"]["counters"] = {k: v for k, v in prof.items() if k != "traffic_bytes"}
+        # issue roofline: the profile's wave-instructions per pattern-event at this run's kernel rate,
+        # against the issue capacity at the profile's clock (a wave64 VALU op holds a SIMD32 for 2
+        # cycles, 1024 SIMDs; one scalar issue per CU and cycle, 256 CUs; profiles/summarize.py)
+        pe_kernel = pe / max(1e-12, sum(kern_ms) * 1e-3) / max(1, world)  # per GPU, per kernel-second
+        clk = prof["clock_ghz"] * 1e9
+        result["roofline"]["issue"] = {
+            "valu_frac": prof["valu_insts_per_pe"] * pe_kernel * 2.0 / (1024.0 * clk),
+            "salu_frac": prof["salu_insts_per_pe"] * pe_kernel / (256.0 * clk),
+            "valu_insts_per_pe": prof["valu_insts_per_pe"], "salu_insts_per_pe": prof["salu_insts_per_pe"],
+            "clock_ghz": prof["clock_ghz"]}
+    if rank == 0 and not args.no_calibrate:
+        from siddhi_amd.engine import calibrate_hbm
+        copy_gbps, read_gbps = calibrate_hbm(local)
+        rf = result["roofline"]
+        rf["measured_peak"] = {"copy": copy_gbps, "read": read_gbps, "unit": "GB/s",
+                               "how": "best of 5 streaming 4 GiB copies / reads (csrc/calib.hip)"}
+        rf["frac_measured"] = achieved / copy_gbps
+        if traffic:
+            rf["traffic_frac_measured"] = rf["traffic_gbps"] / copy_gbps
     if c5:  # the sparse state (K_slab): bytes per live partial, engine build time
         lb, rb, db = eng.state_bytes()
         result["config"].update({"state_live_bytes": lb, "state_slab_bytes": rb, "state_dir_bytes": db,

@@ -204,6 +204,10 @@ int sdh_spec_selftest(char* log, size_t cap);
  * hash of them (e2 seq, query, e1 seq), in either output mode (SDH_FLAG_DEVICE_MATCHES included,
  * unless its record ring wrapped: SDH_E_CAPACITY). */
 int sdh_engine_debug_digest(sdh_engine* e, uint64_t* out);
+/* Diagnostic: best-of-`iters` HBM bandwidth of a streaming copy (bytes read + written) and a
+ * streaming read over `bytes`-sized buffers on `device`, in GB/s -- the measured ceiling the bench
+ * reports its roofline fraction against beside the 8 TB/s peak. */
+int sdh_calibrate_hbm(int32_t device, int64_t bytes, int32_t iters, double* copy_gbps, double* read_gbps);
 /* Library version / build info string (static storage). */
 const char* sdh_version(void);
 

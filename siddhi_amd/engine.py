@@ -62,7 +62,7 @@ EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engi
            "sdh_engine_pending_matches", "sdh_engine_start", "sdh_engine_advance_time", "sdh_engine_stats",
            "sdh_engine_snapshot", "sdh_engine_state_bytes",
            "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version",
-           "sdh_engine_debug_digest", "sdh_engine_set_strings"]
+           "sdh_engine_debug_digest", "sdh_engine_set_strings", "sdh_calibrate_hbm"]
 
 _lib = None
 
@@ -98,6 +98,8 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_version.restype = ctypes.c_char_p
     lib.sdh_engine_debug_digest.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
     lib.sdh_engine_set_strings.argtypes = [P, ctypes.c_int64, P, P, P]
+    D = ctypes.POINTER(ctypes.c_double)
+    lib.sdh_calibrate_hbm.argtypes = [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, D, D]
     _lib = lib
     return lib
 
@@ -282,3 +284,13 @@ class HipEngine:
             self.close()
         except Exception:  # noqa: BLE001
             pass
+
+
+def calibrate_hbm(device: int = 0, nbytes: int = 4 << 30, iters: int = 5):
+    """(copy GB/s, read GB/s): the measured HBM ceiling (sdh_calibrate_hbm)."""
+    lib = load_library()
+    c, r = ctypes.c_double(), ctypes.c_double()
+    rc = lib.sdh_calibrate_hbm(device, nbytes, iters, ctypes.byref(c), ctypes.byref(r))
+    if rc != SDH_OK:
+        raise EngineError(rc, "sdh_calibrate_hbm failed")
+    return c.value, r.value
