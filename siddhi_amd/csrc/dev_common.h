@@ -20,6 +20,18 @@ __device__ __forceinline__ T gpick(const T (&arr)[N], int idx) {
   return v;
 }
 
+// The logical item of this workgroup. Observed dispatch deals workgroups round-robin over the 8
+// XCDs, blocks b and b + 8 sharing one (MI355X_MICROARCH.md; speed only, never correctness). With
+// `xcd` set the launch pads its grid to a multiple of 8 and each XCD takes one contiguous range of
+// items, so neighbouring items -- one key's groups, one event chunk's groups -- read the inputs they
+// share (the key's events, a tile, directory lines) through one XCD's L2 instead of all eight.
+// Items at or past the launch's count return.
+__device__ __forceinline__ int64_t grid_item(int xcd) {
+  const int64_t b = blockIdx.x;
+  if (!xcd) return b;
+  return (b & 7) * (int64_t)(gridDim.x >> 3) + (b >> 3);
+}
+
 // attribute word `attr` of batch event e: int / string id sign-extended, float bits, long / double
 // bits, bool byte; *isnull from the column's null bytes
 __device__ __forceinline__ int64_t raw_word(const StreamBatch& b, int attr, int64_t e, bool& isnull) {

@@ -824,6 +824,8 @@ struct sdh_engine {
   DevBuf<uint8_t> p_ptemp;
   int64_t r_seq_base = 0;            // seq of the last launch's first event
   std::vector<int32_t> r_blk_count;
+  int xcd = 1;                       // per-XCD item ranges in the K_gen / K_seq / K_part / K_slab launches
+                                     // (dev::grid_item; SDH_XCD=0 turns them off for A/B runs)
   int rML = 8;                       // LDS ring entries per lane (power of two)
   double r_waves = 0;                // resident-wave target per launch (0: CUs x occupancy)
   int n_cu = 256;
@@ -2318,6 +2320,7 @@ sdh::GenLaunch gen_launch_base(sdh_engine* e, const sdh_engine::GenSet& gs, cons
   L.timer_seq = e->seq + B.n;
   L.playback = (e->cfg.flags & SDH_FLAG_PLAYBACK) ? 1 : 0;
   L.no_timers = e->ck.active ? 1 : 0;
+  L.xcd = e->xcd;
   return L;
 }
 
@@ -2412,6 +2415,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
         for (r1 = r0 + 1; r1 < seq_rows.size() && e->group_tmpl[seq_rows[r1]] == tmpl;) ++r1;
         const int nrows = (int)(r1 - r0);
         sdh::SeqLaunch Q{};
+        Q.xcd = e->xcd;
         Q.queries = e->d_gq.p;
         Q.lane_q = e->d_lane_q.p;
         Q.group_tmpl = e->d_group_tmpl.p;
@@ -2438,8 +2442,9 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
         auto sp = e->seq_spec.find(tmpl);
         if (sp != e->seq_spec.end()) {
           void* args[] = {&Q};
-          HIPCHK(hipModuleLaunchKernel(sp->second, (unsigned)(Q.n_glist * Q.n_chunks), 1, 1, 64, 1, 1, 0, e->stream, args,
-                                       nullptr));
+          const int64_t items = (int64_t)Q.n_glist * Q.n_chunks;
+          HIPCHK(hipModuleLaunchKernel(sp->second, (unsigned)(Q.xcd ? (items + 7) & ~7ll : items), 1, 1, 64, 1, 1, 0,
+                                       e->stream, args, nullptr));
         } else {
           HIPCHK(sdh_launch_seq(&Q, e->stream));
         }
@@ -2641,6 +2646,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       if (ps.partition != pi) continue;
       part_grow(e, ps, hv[0]);
       sdh::PartLaunch P{};
+      P.xcd = e->xcd;
       P.queries = e->d_gq.p;
       P.lane_q = e->d_lane_q.p;
       P.group_tmpl = e->d_group_tmpl.p;
@@ -2694,7 +2700,8 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
         if (sp != ps.spec.end()) {
           if (P.n_items > 0) {
             void* args[] = {&P};
-            HIPCHK(hipModuleLaunchKernel(sp->second, (unsigned)P.n_items, 1, 1, 64, 1, 1, 0, e->stream, args, nullptr));
+            HIPCHK(hipModuleLaunchKernel(sp->second, (unsigned)(P.xcd ? (P.n_items + 7) & ~7 : P.n_items), 1, 1, 64, 1,
+                                         1, 0, e->stream, args, nullptr));
           }
         } else {
           HIPCHK(sdh_launch_part(&P, e->stream));
@@ -2729,6 +2736,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       HIPCHK(hipMemcpyAsync(ss.live_bak.p, ss.live.p, 256 * 8, hipMemcpyDeviceToDevice, e->stream));
       HIPCHK(hipMemsetAsync(ss.traffic.p, 0, 256 * 8, e->stream));
       sdh::SlabLaunch S{};
+      S.xcd = e->xcd;
       S.queries = e->d_gq.p;
       S.lane_q = e->d_lane_q.p;
       S.group_tmpl = e->d_group_tmpl.p;
@@ -3377,6 +3385,7 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     // tuning overrides for kernel experiments: K_ratchet LDS ring depth and waves per launch
     if (const char* v = getenv("SDH_RATCHET_ML")) e->rML = std::max(4, atoi(v));
     if (const char* v = getenv("SDH_RATCHET_WAVES")) e->r_waves = atof(v);
+    if (const char* v = getenv("SDH_XCD")) e->xcd = atoi(v) != 0;
     e->out_rank = kg::output_ranks(e->lp);
     // plan selection per query: K_ratchet (2-state threshold ratchet) > K_chain (stream-state
     // chains) > K_gen (everything else: count, logical, sequences, partitions, general predicates)

@@ -28,7 +28,7 @@ using dev::raw_word;
 template <int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void nfa_gen_kernel(GenLaunch L) {
   const int lane = threadIdx.x;
-  const int item = blockIdx.x;
+  const int item = (int)dev::grid_item(L.xcd);
   if (item >= L.n_items) return;
   int seg = item / L.groups, g = item % L.groups;
   if (L.glist) {  // unpartitioned: a subset of the set's groups (K_seq runs the others)
@@ -550,13 +550,14 @@ extern "C" hipError_t sdh_launch_gen(const sdh::GenLaunch* L, hipStream_t s) {
   // 4 waves/SIMD (116 VGPRs, no spills): on C3, 5 (96 VGPRs + spills) is level and 6 / 8 are
   // 10-30 % slower
   const size_t lds = (size_t)(sdh::kg::GMAXNA + (1 + L->hot_nu) * 64) * 8 + (size_t)(3 * L->hot_s + 4) * 64 * 4;
-  hipLaunchKernelGGL(sdh::nfa_gen_kernel<4>, dim3(L->n_items), dim3(64), lds, s, *L);
+  hipLaunchKernelGGL(sdh::nfa_gen_kernel<4>, dim3(L->xcd ? (L->n_items + 7) & ~7 : L->n_items), dim3(64), lds, s, *L);
   return hipGetLastError();
 }
 
 extern "C" hipError_t sdh_launch_seq(const sdh::SeqLaunch* L, hipStream_t s) {
   if (L->n_glist > 0 && L->n_chunks > 0)
-    hipLaunchKernelGGL(sdh::nfa_seq_kernel, dim3(L->n_glist * L->n_chunks), dim3(64), 0, s, *L);
+    hipLaunchKernelGGL(sdh::nfa_seq_kernel, dim3(L->xcd ? (L->n_glist * L->n_chunks + 7) & ~7 : L->n_glist * L->n_chunks),
+                       dim3(64), 0, s, *L);
   return hipGetLastError();
 }
 

@@ -113,10 +113,11 @@ extern "C" hipError_t sdh_live_part(const int64_t* st, const int32_t* cur, int64
 
 extern "C" hipError_t sdh_launch_part(const sdh::PartLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
+  const dim3 grid(L->xcd ? (L->n_items + 7) & ~7 : L->n_items);
   switch (L->kind) {
-    case sdh::PK_OR: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_OR>, dim3(L->n_items), dim3(64), 0, s, *L); break;
-    case sdh::PK_AND: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_AND>, dim3(L->n_items), dim3(64), 0, s, *L); break;
-    default: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_COUNT>, dim3(L->n_items), dim3(64), 0, s, *L);
+    case sdh::PK_OR: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_OR>, grid, dim3(64), 0, s, *L); break;
+    case sdh::PK_AND: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_AND>, grid, dim3(64), 0, s, *L); break;
+    default: hipLaunchKernelGGL(sdh::nfa_part_kernel<sdh::PK_COUNT>, grid, dim3(64), 0, s, *L);
   }
   return hipGetLastError();
 }

@@ -63,7 +63,7 @@ template <int NAX>
 __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
   using namespace slab;
   const int lane = threadIdx.x;
-  const int item = blockIdx.x;
+  const int item = (int)dev::grid_item(L.xcd);
   if (item >= L.n_items) return;
   const int seg = item / L.n_glist, g = L.glist[item % L.n_glist];
   const uint32_t kid = L.seg_kid[seg];
@@ -383,8 +383,9 @@ __global__ void slab_live_words_kernel(const uint64_t* dir, int64_t n_dir, int g
 extern "C" hipError_t sdh_launch_slab(const sdh::SlabLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
   const size_t lds = (size_t)L->lds_words * 4;
-  if (L->max_na <= 4) hipLaunchKernelGGL(sdh::nfa_slab_kernel<4>, dim3((unsigned)L->n_items), dim3(64), lds, s, *L);
-  else hipLaunchKernelGGL(sdh::nfa_slab_kernel<sdh::kg::GMAXNA>, dim3((unsigned)L->n_items), dim3(64), lds, s, *L);
+  const unsigned grid = (unsigned)(L->xcd ? (L->n_items + 7) & ~7 : L->n_items);
+  if (L->max_na <= 4) hipLaunchKernelGGL(sdh::nfa_slab_kernel<4>, dim3(grid), dim3(64), lds, s, *L);
+  else hipLaunchKernelGGL(sdh::nfa_slab_kernel<sdh::kg::GMAXNA>, dim3(grid), dim3(64), lds, s, *L);
   return hipGetLastError();
 }
 

@@ -271,6 +271,7 @@ struct GenLaunch {
   int64_t timer_seq;          // trigger seq of the timers fired after the last event
   int32_t playback;           // @app:playback: the generator's time is the event time while timers fire
   int32_t no_timers;          // a chunk push: its timers fired before it (time moved once), none inside
+  int32_t xcd;                // items in per-XCD ranges (as PartLaunch)
   // indexed timer sweep (pm != nullptr; batches with ordered timestamps): item = (kid, group) over
   // every known key walks only its own events (the routed segment kseg[kid] of seg_begin / seg_len /
   // ev_idx, -1: none) and fires each due timer at the first batch event whose ts reaches it (binary
@@ -335,6 +336,7 @@ struct PartLaunch {
   int64_t rec_cap;
   unsigned long long* rec_next;
   int32_t write_records;
+  int32_t xcd;                // items in per-XCD ranges (dev::grid_item; the grid is padded to a multiple of 8)
   int32_t* err;               // [0] entry capacity, [2] output overflow
   unsigned long long* prof;   // SDH_PART_PROF builds: per-phase clock sums (part_body.h), else null
 };
@@ -386,6 +388,7 @@ struct SlabLaunch {
   int64_t rec_cap;
   unsigned long long* rec_next;
   int32_t write_records;
+  int32_t xcd;                // items in per-XCD ranges (as PartLaunch)
   int32_t* err;               // [0] LDS capacity, [1] slab space, [2] output overflow
 };
 
@@ -416,7 +419,7 @@ struct SeqLaunch {
   int64_t rec_cap;
   unsigned long long* rec_next;
   int32_t* err;               // [2] output overflow
-  int32_t pad;
+  int32_t xcd;                // items in per-XCD ranges (as PartLaunch)
 };
 
 // ------------------------------------------------------------------------------------------

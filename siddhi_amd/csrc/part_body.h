@@ -169,7 +169,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
   PPROF_T(c_start);
   constexpr int RC = Spec::kRegEntries, EW = Spec::kEW;
   const int lane = threadIdx.x;
-  const int item = blockIdx.x;
+  const int item = (int)dev::grid_item(L.xcd);
   if (item >= L.n_items) return;
   const int seg = item / L.gn, g = L.g0 + item % L.gn;
   const uint32_t kid = L.seg_kid[seg];

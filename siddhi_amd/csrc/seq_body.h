@@ -35,8 +35,10 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
   using Win = LdsWinT<ROW>;
   __shared__ int64_t win[(SEQ_TILE + 8 + kg::GMAXS) * ROW];  // (+8: masked starts of the last group)
   const int lane = threadIdx.x;
-  const int gi = L.glist[blockIdx.x % L.n_glist];
-  const int chunk = blockIdx.x / L.n_glist;
+  const int64_t it = dev::grid_item(L.xcd);  // (chunk-major: one chunk's groups are neighbours)
+  if (it >= (int64_t)L.n_glist * L.n_chunks) return;
+  const int gi = L.glist[it % L.n_glist];
+  const int chunk = (int)(it / L.n_glist);
   const int qi = L.lane_q[(int64_t)gi * 64 + lane];
   const kg::GQuery* __restrict__ q = L.queries + L.group_tmpl[gi];
   const kg::GQuery* __restrict__ ql = L.queries + (qi >= 0 ? qi : L.group_tmpl[gi]);

@@ -20,7 +20,7 @@ the work is cut into (pattern shard x key class) tasks, each an oracle fed only 
 A task's match seqs are mapped back to global seqs, and the tasks' outputs merge into the one-engine
 R18 order by a stable sort on (trigger seq, receiver rank): every slot event of a match precedes or is
 its trigger (no absent states), so the trigger is the match's largest seq; all C5 receivers are single-
-processor receivers, so the rank is the query's index in the partition; and one (event, query) pair's
+processor receivers, so the rank is the query's position in the partition's name map (chm.py); and one (event, query) pair's
 matches all come from one task, in its emission order. Before the full run the merge is checked
 against an unsharded oracle over a small pattern set (`--check`).
 
@@ -127,7 +127,12 @@ def run(cfg_name, threads, patterns=None, check=False, log=True):
     w = np.concatenate(words)
     tr = np.asarray(trig, np.int64)
     starts = np.concatenate([[0], np.cumsum(ln)[:-1]])
-    perm = np.lexsort((q, tr))  # stable: trigger seq, then the query (= receiver rank)
+    # stable: trigger seq, then the receiver rank -- the query's position on a key's junction, the
+    # order of PartitionRuntime.metaQueryRuntimeMap, a ConcurrentHashMap of the names c5p0 ..
+    from siddhi_amd import chm
+    from siddhi_amd.planner import java_string_hash
+    rank = np.asarray(chm.positions([java_string_hash(f"c5p{p}") for p in range(P)]), np.int64)
+    perm = np.lexsort((rank[q], tr))
     ln_s = ln[perm]
     off = np.concatenate([[0], np.cumsum(ln_s)])
     src = np.repeat(starts[perm] - off[:-1], ln_s) + np.arange(off[-1])

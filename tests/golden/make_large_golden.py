@@ -45,7 +45,18 @@ def raw_matches(app):
     return q, k, ts, off, words
 
 
-def merge(parts, firsts):
+def receiver_ranks(cfg_name, P):
+    """Per global query its receiver rank on the one stream (dist.output_ranks of the full app): the
+    query index, except inside C3's partition, whose clones sit on a key's junction in the order of
+    PartitionRuntime.metaQueryRuntimeMap (a ConcurrentHashMap of the names c3p0 .. c3p{P-1})."""
+    from siddhi_amd import chm
+    from siddhi_amd.planner import java_string_hash
+    if cfg_name != "c3":
+        return np.arange(P, dtype=np.int64)
+    return np.asarray(chm.positions([java_string_hash(f"c3p{p}") for p in range(P)]), np.int64)
+
+
+def merge(parts, firsts, rank):
     """Shard outputs of one batch -> one R18-ordered set of columns (query ids made global)."""
     qs, ks, tss, lens, words = [], [], [], [], []
     for (q, k, ts, off, w), first in zip(parts, firsts):
@@ -62,9 +73,8 @@ def merge(parts, firsts):
     ln = np.concatenate(lens)
     w = np.concatenate(words)
     starts = np.concatenate([[0], np.cumsum(ln)[:-1]])
-    # receiver rank = query index for every config here (single stream; C3's partition queries all
-    # have multi-processor receivers, kg::output_ranks), checked by the unsharded comparison
-    perm = np.lexsort((q, ts))  # stable: primary ts, then rank; shard order kept within a query
+    # receiver rank per query (receiver_ranks), checked by the unsharded comparison
+    perm = np.lexsort((rank[q], ts))  # stable: primary ts, then rank; shard order kept within a query
     ln_s = ln[perm]
     off = np.concatenate([[0], np.cumsum(ln_s)])
     src = np.repeat(starts[perm] - off[:-1], ln_s) + np.arange(off[-1])
@@ -79,6 +89,7 @@ def run(cfg_name, n_events, threads, stride, log=True):
     apps = [App(app_source(cfg_name, bounds[i + 1] - bounds[i], first=bounds[i])) if cfg_name != "c1"
             else App(app_source("c1", 1)) for i in range(T)]
     dig = Digest(stride)
+    rank = receiver_ranks(cfg_name, P)
     B = cfg["batch"]
     t0 = time.time()
     with ThreadPoolExecutor(T) as ex:
@@ -90,7 +101,7 @@ def run(cfg_name, n_events, threads, stride, log=True):
                 apps[i].engine.send(0, ts, vals, None)
                 return raw_matches(apps[i])
             parts = list(ex.map(one, range(T)))
-            dig.update(*merge(parts, bounds[:T]))
+            dig.update(*merge(parts, bounds[:T], rank))
             if log and (lo // B) % 4 == 0:
                 print(f"  {cfg_name}: {lo + n}/{n_events} events, {dig.n} matches, {time.time() - t0:.0f} s",
                       flush=True)
