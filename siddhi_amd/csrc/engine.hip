@@ -824,8 +824,8 @@ struct sdh_engine {
   DevBuf<uint8_t> p_ptemp;
   int64_t r_seq_base = 0;            // seq of the last launch's first event
   std::vector<int32_t> r_blk_count;
-  int xcd = 1;                       // per-XCD item ranges in the K_gen / K_seq / K_part / K_slab launches
-                                     // (dev::grid_item; SDH_XCD=0 turns them off for A/B runs)
+  int xcd = 0;                       // per-XCD item ranges in the K_gen / K_seq / K_part / K_slab launches
+                                     // (dev::grid_item; SDH_XCD=1: measured neutral)
   int rML = 8;                       // LDS ring entries per lane (power of two)
   double r_waves = 0;                // resident-wave target per launch (0: CUs x occupancy)
   int n_cu = 256;
@@ -2136,9 +2136,14 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
     if (e->lp.q[qi].partition < 0) top.push_back(qi);
   add_set(-1, top);
   for (int pi = 0; pi < (int)e->lp.parts.size(); ++pi) {
+    // lanes in definition order, not the partition's receiver order (LPart::queries is the
+    // metaQueryRuntimeMap order, which scatters a family's neighbouring queries): lane order is free
+    // (the match table orders rows by rank), and neighbouring definitions share a wave's control
+    // flow more often (C3: 20.9 ms/step in receiver order)
     std::vector<int> m;
     for (int qi : e->lp.parts[pi].queries)
       if (gidx[qi] >= 0) m.push_back(qi);
+    std::sort(m.begin(), m.end());
     add_set(pi, m);
   }
   e->d_gq.ensure(e->gq.size());
@@ -3668,7 +3673,7 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
 // then per query
 // header + table, ratchet deques, K_gen arenas + key tables, K_seq tails
 constexpr int64_t SNAP_MAGIC = 0x5344485350415254LL;
-constexpr int64_t SNAP_VERSION = 7;
+constexpr int64_t SNAP_VERSION = 8;
 // Device memory of the sparse K_slab state: the live blocks' bytes, the slab's reserved bytes (live
 // blocks, not yet reclaimed superseded ones, and free room) and the directory's
 int sdh_engine_state_bytes(sdh_engine* e, int64_t* live_bytes, int64_t* reserved_bytes, int64_t* dir_bytes) {

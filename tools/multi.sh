@@ -2,7 +2,7 @@
 # Multi-rank rehearsal on a 1-GPU box: 2 ranks on device 0 over gloo (the driver's 8-GPU runs use
 # RCCL, one rank per GPU). Strong scaling (the metric's 10K patterns split over the ranks) with the
 # weak-scaling line, and the expansion leg's gather + k-way merge timed per matched tuple.
-# Usage: tools/r3_multi.sh [c2] [c3] [c4]
+# Usage: tools/multi.sh [c2] [c3] [c4]
 set -o pipefail
 mkdir -p gpurun_out
 export SDH_BENCH_BACKEND=gloo SDH_BENCH_DEVICE=0
