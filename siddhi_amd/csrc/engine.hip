@@ -676,6 +676,8 @@ struct sdh_engine {
   DevBuf<kg::GQuery> d_gq;
   std::vector<int32_t> lane_q;       // [group][64]
   DevBuf<int32_t> d_lane_q;
+  DevBuf<int64_t> d_lconst;          // [group][lc_slots][64] lane constants (kg::LaneConsts)
+  int lc_slots = kg::LC_FIRST;
   std::vector<int32_t> group_tmpl;   // [group] shape template (a member query)
   DevBuf<int32_t> d_group_tmpl;
   std::vector<int32_t> group_seq;    // [group] window length S when the group runs on K_seq, else 0
@@ -2148,6 +2150,32 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   }
   e->d_gq.ensure(e->gq.size());
   HIPCHK(hipMemcpy(e->d_gq.p, e->gq.data(), e->gq.size() * sizeof(kg::GQuery), hipMemcpyHostToDevice));
+  // the groups' lane-constant table (kg::LaneConsts): [group][slot][64], slot 0 query id, 1 within,
+  // 2 + k the k-th CONST instruction of the group's shape; idle lanes repeat the template's values
+  {
+    const size_t n_groups = e->group_tmpl.size();
+    int slots = kg::LC_FIRST;
+    std::vector<std::vector<int>> pcs(n_groups);
+    for (size_t g = 0; g < n_groups; ++g) {
+      const kg::GQuery& t = e->gq[e->group_tmpl[g]];
+      for (int pc = 0; pc < t.n_code; ++pc)
+        if (t.code[pc].op == kg::OP_CONST) pcs[g].push_back(pc);
+      slots = std::max(slots, kg::LC_FIRST + (int)pcs[g].size());
+    }
+    std::vector<int64_t> lc(std::max<size_t>(1, n_groups * slots * 64), 0);
+    for (size_t g = 0; g < n_groups; ++g)
+      for (int l = 0; l < 64; ++l) {
+        const int qi = e->lane_q[g * 64 + l];
+        const kg::GQuery& x = e->gq[qi >= 0 ? qi : e->group_tmpl[g]];
+        int64_t* row = lc.data() + g * slots * 64 + l;
+        row[kg::LC_QID * 64] = x.qid;
+        row[kg::LC_WITHIN * 64] = x.within;
+        for (size_t k = 0; k < pcs[g].size(); ++k) row[(kg::LC_FIRST + k) * 64] = x.code[pcs[g][k]].imm;
+      }
+    e->lc_slots = slots;
+    e->d_lconst.ensure(lc.size());
+    HIPCHK(hipMemcpy(e->d_lconst.p, lc.data(), lc.size() * 8, hipMemcpyHostToDevice));
+  }
   e->d_lane_q.ensure(e->lane_q.size());
   HIPCHK(hipMemcpy(e->d_lane_q.p, e->lane_q.data(), e->lane_q.size() * 4, hipMemcpyHostToDevice));
   e->seq_tail.resize(e->prog.stream_types.size());
@@ -2652,6 +2680,8 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       part_grow(e, ps, hv[0]);
       sdh::PartLaunch P{};
       P.xcd = e->xcd;
+      P.lconst = e->d_lconst.p;
+      P.lc_slots = e->lc_slots;
       P.queries = e->d_gq.p;
       P.lane_q = e->d_lane_q.p;
       P.group_tmpl = e->d_group_tmpl.p;
@@ -2742,6 +2772,8 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       HIPCHK(hipMemsetAsync(ss.traffic.p, 0, 256 * 8, e->stream));
       sdh::SlabLaunch S{};
       S.xcd = e->xcd;
+      S.lconst = e->d_lconst.p;
+      S.lc_slots = e->lc_slots;
       S.queries = e->d_gq.p;
       S.lane_q = e->d_lane_q.p;
       S.group_tmpl = e->d_group_tmpl.p;

@@ -345,14 +345,16 @@ KG_UNROLL
   KG_FN Val result() const { return sp == 1 ? s[0] : Val{T_BOOL, 1, 0}; }
 };
 
-template <class Stack = ArrStack, class Attr, class StreamNull>
-KG_FN Val eval_code(const GQuery* q, const GQuery* ql, int b, int e, Attr attr, StreamNull stream_null) {
+// imm(pc): the lane's constant of CONST instruction pc (its own query's, or its column of a
+// lane-interleaved constant table: kg::LaneConsts)
+template <class Stack = ArrStack, class Imm, class Attr, class StreamNull>
+KG_FN Val eval_code_imm(const GQuery* q, Imm imm_of, int b, int e, Attr attr, StreamNull stream_null) {
   Stack stk;
   for (int pc = b; pc < e; ++pc) {
     const GInsn& in = q->code[pc];
     switch (in.op) {
       case OP_CONST: {  // constants differ within a shape: the lane's own query
-        const int64_t imm = ql->code[pc].imm;
+        const int64_t imm = imm_of(pc);
         Val v{in.res, 0, 0};
         if (in.res == T_FLOAT) v.bits = (int64_t)(uint32_t)imm;
         else if (in.res == T_INT) v.bits = (int32_t)imm;
@@ -408,6 +410,35 @@ KG_FN Val eval_code(const GQuery* q, const GQuery* ql, int b, int e, Attr attr, 
   }
   return stk.result();
 }
+
+template <class Stack = ArrStack, class Attr, class StreamNull>
+KG_FN Val eval_code(const GQuery* q, const GQuery* ql, int b, int e, Attr attr, StreamNull stream_null) {
+  return eval_code_imm<Stack>(q, [&](int pc) { return ql->code[pc].imm; }, b, e, attr, stream_null);
+}
+
+// A lane's per-query values, read from the group's lane-interleaved constant table
+// [group][slot][64] (engine.hip lane_consts): slot 0 the query id, 1 `within`, 2 + k the k-th CONST
+// instruction of the shape in program order. A wave's 64 lanes read one slot as one coalesced 512-B
+// row instead of 64 scattered lines of 64 different GQuery structs (K_slab and K_part read them per
+// work item). col == nullptr: the lane's own query (host builds).
+constexpr int LC_QID = 0, LC_WITHIN = 1, LC_FIRST = 2;
+struct LaneConsts {
+  const GQuery* ql;
+  const int64_t* col;  // table + (group * slots) * 64 + lane
+  KG_FN int64_t qid() const { return col ? col[LC_QID * 64] : (int64_t)ql->qid; }
+  KG_FN int64_t within() const { return col ? col[LC_WITHIN * 64] : ql->within; }
+  // k: the instruction's rank among the shape's CONST instructions
+  KG_FN int64_t imm(int pc, int k) const { return col ? col[(LC_FIRST + k) * 64] : ql->code[pc].imm; }
+};
+
+#ifndef __HIPCC_RTC__
+// per instruction its rank among the CONST instructions of the code (-1: not a CONST)
+inline void const_ranks(const GQuery& g, int8_t* rank, int* n) {
+  int k = 0;
+  for (int pc = 0; pc < GMAXCODE; ++pc) rank[pc] = (pc < g.n_code && g.code[pc].op == OP_CONST) ? (int8_t)k++ : -1;
+  *n = k;
+}
+#endif
 
 struct Emitter;  // defined by the caller: void emit(const Ctx&, int se)
 #ifdef KG_PROFILE

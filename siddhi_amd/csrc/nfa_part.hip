@@ -42,7 +42,7 @@ struct PartInterp {
   static constexpr int kRegEntries = 0, kEW = 1;  // the whole table in the global state block
   static constexpr int kNA = kg::GMAXNA, kOutW = 1536;
   struct K {};
-  __device__ static void load(K&, const kg::GQuery*, const PartLaunch&) {}
+  __device__ static void load(K&, const kg::GQuery*, const PartLaunch&, const int64_t*) {}
   __device__ static PartOffs offs(const PartLaunch& L) { return PartOffs{L.cmax, L.n_e1, L.n_first, L.n_last}; }
   __device__ static bool f1(const K&, const kg::GQuery* q, const kg::GQuery* ql, const PartLaunch&, const PartEv& ev) {
     return ev_filter(q, ql, 0, ev);

@@ -79,7 +79,9 @@ __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
   const int qi = L.lane_q[(int64_t)(L.group_base + g) * 64 + lane];
   const bool live = qi >= 0;
   const kg::GQuery* __restrict__ q = L.queries + L.group_tmpl[L.group_base + g];
-  const kg::GQuery* __restrict__ ql = L.queries + (live ? qi : L.group_tmpl[L.group_base + g]);
+  // the lane's query id, `within` and filter constants: one coalesced row per value of the group's
+  // lane-constant table (a lane reading its own GQuery instead touched 64 scattered lines per value)
+  const kg::LaneConsts lk{nullptr, L.lconst + ((int64_t)(L.group_base + g) * L.lc_slots) * 64 + lane};
   const int EW = sh.EW;
   const int64_t e0 = L.seg_begin[seg], e1 = e0 + L.seg_len[seg];
   const int ncap = q->n_cap[stream];
@@ -121,8 +123,8 @@ __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
   o.g = dev::LaneOut{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
   o.sh = &out_sh;
   o.init();
-  const int64_t within = ql->within;
-  const int64_t qid = ql->qid;
+  const int64_t within = lk.within();
+  const int64_t qid = lk.qid();
   const int64_t key = L.key_of_id[kid];
   unsigned long long nrec = 0;
   bool changed = false, lds_over = false;
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
     for (int te = 0; te < cnt; ++te) {
       const Ev ev{t_ts[te], t_seq[te], &t_w[0][te], 64, t_nul[te]};
       if (st == 0) {  // e1: every passing lane opens a partial (and a non-every start disarms)
-        const bool pass = armed && start_pass(sh, q, ql, ev);
+        const bool pass = armed && start_pass(sh, q, lk, ev);
         const int need = pass ? (sh.every ? 1 : 2) : 0;
         int tot = 0;
         const int pre = wave_prefix(need, 2, &tot);
@@ -195,7 +197,7 @@ __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
       bool moved = false;
       for (int k = b_l; k < e_l; ++k) {
         uint32_t* e = ent + k * EW;
-        const int r = step(sh, q, ql, st, e, ev, within);
+        const int r = step(sh, q, lk, st, e, ev, within);
         changed |= r != 0;
         const bool em = (r & R_EMIT) != 0;
         if (em) ++nrec;

@@ -339,6 +339,9 @@ struct PartLaunch {
   int32_t xcd;                // items in per-XCD ranges (dev::grid_item; the grid is padded to a multiple of 8)
   int32_t* err;               // [0] entry capacity, [2] output overflow
   unsigned long long* prof;   // SDH_PART_PROF builds: per-phase clock sums (part_body.h), else null
+  const int64_t* lconst;      // [group][lc_slots][64] the lanes' query ids, withins, constants (kg::LaneConsts)
+  int32_t lc_slots;
+  int32_t pad_lc;
 };
 
 // ------------------------------------------------------------------------------------------
@@ -390,6 +393,9 @@ struct SlabLaunch {
   int32_t write_records;
   int32_t xcd;                // items in per-XCD ranges (as PartLaunch)
   int32_t* err;               // [0] LDS capacity, [1] slab space, [2] output overflow
+  const int64_t* lconst;      // [group][lc_slots][64] the lanes' query ids, withins, constants (kg::LaneConsts)
+  int32_t lc_slots;
+  int32_t pad_lc;
 };
 
 // ------------------------------------------------------------------------------------------

@@ -178,15 +178,17 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
   const int qi = L.lane_q[(int64_t)(L.group_base + g) * 64 + lane];
   const kg::GQuery* __restrict__ q = L.queries + L.group_tmpl[L.group_base + g];  // wave-uniform shape
   const kg::GQuery* __restrict__ ql = L.queries + (qi >= 0 ? qi : L.group_tmpl[L.group_base + g]);
+  // the lane's query id, `within` and constants from the group's lane-constant table (one coalesced
+  // row per value; kg::LaneConsts), loaded once: a per-lane global load inside the event loop would
+  // wait (vmcnt is in order) for every record store issued before it
+  const int64_t* __restrict__ lcol = L.lconst + ((int64_t)(L.group_base + g) * L.lc_slots) * 64 + lane;
   typename Spec::K k;
-  Spec::load(k, ql, L);
+  Spec::load(k, ql, L, lcol);
   const PartOffs of = Spec::offs(L);
   const int stream = L.b.stream;
   const int ncap = q->n_cap[stream];
-  const int64_t within = ql->within;
-  // loaded once: a per-lane global load inside the event loop would wait (vmcnt is in order) for
-  // every record store issued before it
-  const int64_t qid = ql->qid;
+  const int64_t within = lcol[kg::LC_WITHIN * 64];
+  const int64_t qid = lcol[kg::LC_QID * 64];
   const int cmin = q->st[1].min, cmax = q->st[1].max;  // PK_COUNT: this shape's <min:max>
   const int64_t key = L.key_of_id[kid];
   const int ew = RC > 0 ? EW : L.ew;

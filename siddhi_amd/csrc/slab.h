@@ -75,6 +75,7 @@ struct Shape {
   int32_t nb_f[SL_MAXS], nb_l[SL_MAXS];  // first null bit of those copies
   int32_t ncap[SL_MAXS];        // captured words per copy (the state stream's kg::GQuery::n_cap)
   int32_t pad[2];
+  int8_t crank[kg::GMAXCODE];   // per instruction its rank among the shape's CONST ones (kg::LaneConsts)
 };
 
 // ---- entry accessors (E: uint32 pointer of one entry, contiguous words) ----
@@ -160,12 +161,12 @@ KG_FN int slot_ref(const Shape& sh, const uint32_t* e, int st, int len, int a, i
 }
 
 // state st's filters (FilterProcessor.process:55-66 over the typed bytecode)
-KG_FN bool filters_pass(const Shape& sh, const kg::GQuery* q, const kg::GQuery* ql, int st, const uint32_t* e,
+KG_FN bool filters_pass(const Shape& sh, const kg::GQuery* q, const kg::LaneConsts& lk, int st, const uint32_t* e,
                         int len, const Ev& ev) {
   const kg::GState& gs = q->st[st];
   for (int f = 0; f < gs.n_filt; ++f) {
-    const kg::Val v = kg::eval_code<kg::RegStack>(
-        q, ql, gs.fb[f], gs.fe[f],
+    const kg::Val v = kg::eval_code_imm<kg::RegStack>(
+        q, [&](int pc) { return lk.imm(pc, sh.crank[pc]); }, gs.fb[f], gs.fe[f],
         [&](const kg::GInsn& in) {
           int o = 0, nb = 0;
           const int w = slot_ref(sh, e, st, len, in.a, in.b, &o, &nb);
@@ -183,9 +184,9 @@ KG_FN bool filters_pass(const Shape& sh, const kg::GQuery* q, const kg::GQuery* 
 }
 
 // the start state: does e1's filter pass the event? (its slot is the event; nothing else is read)
-KG_FN bool start_pass(const Shape& sh, const kg::GQuery* q, const kg::GQuery* ql, const Ev& ev) {
+KG_FN bool start_pass(const Shape& sh, const kg::GQuery* q, const kg::LaneConsts& lk, const Ev& ev) {
   uint32_t dummy[SL_HDR] = {0, 0, 0, 0, 0, 0};
-  return filters_pass(sh, q, ql, 0, dummy, 0, ev);
+  return filters_pass(sh, q, lk, 0, dummy, 0, ev);
 }
 
 // A new partial opened by e1 at event ev: it joins the next element's lists at position `pos`
@@ -223,13 +224,13 @@ KG_FN void drop_counts(const Shape& sh, uint32_t* e, int st) {
 // One partial at one event of the stream that feeds state st (st > 0, the partial in st's list).
 // Returns R_* bits: R_EMIT (the query's last post returned it: a match, trigger = this event),
 // R_MOVE (it arrives in the next element's lists), R_CHANGED (the entry changed).
-KG_FN int step(const Shape& sh, const kg::GQuery* q, const kg::GQuery* ql, int st, uint32_t* e, const Ev& ev,
+KG_FN int step(const Shape& sh, const kg::GQuery* q, const kg::LaneConsts& lk, int st, uint32_t* e, const Ev& ev,
                int64_t within) {
   if (!(e[0] & in_bit(st))) return 0;
   const int kind = sh.kind[st];
   if (kind == kg::K_COUNT) {  // CountPreStateProcessor.processAndReturn:53-93 + CountPost.process:45-71
     const int len = count_len(sh, e, st);
-    if (!filters_pass(sh, q, ql, st, e, len, ev)) return 0;  // removeLastEvent: chain unchanged
+    if (!filters_pass(sh, q, lk, st, e, len, ev)) return 0;  // removeLastEvent: chain unchanged
     set64(e, sh.o_seq[st] + 2 * len, ev.seq);
     if (len == 0 && sh.o_cf[st] >= 0) capture(e, sh.o_cf[st], sh.nb_f[st], sh.ncap[st], ev);
     if (sh.o_cl[st] >= 0) capture(e, sh.o_cl[st], sh.nb_l[st], sh.ncap[st], ev);
@@ -253,7 +254,7 @@ KG_FN int step(const Shape& sh, const kg::GQuery* q, const kg::GQuery* ql, int s
     e[0] &= ~in_bit(st);
     return R_CHANGED;
   }
-  if (!filters_pass(sh, q, ql, st, e, 0, ev)) return 0;  // slot cleared, kept (PATTERN)
+  if (!filters_pass(sh, q, lk, st, e, 0, ev)) return 0;  // slot cleared, kept (PATTERN)
   e[0] &= ~in_bit(st);  // stateChanged: removed from this list
   fill_slot(sh, e, st, ev);
   drop_counts(sh, e, st);

@@ -176,6 +176,8 @@ inline bool shape_of_query(const kg::LProgram& P, int qi, const kg::GQuery& g, S
   if (nb > 32) return no("captured words");
   if (o > SL_MAXEW) return no("entry words");
   sh.EW = o;
+  int n_const = 0;
+  kg::const_ranks(g, sh.crank, &n_const);
   *out = sh;
   return true;
 }

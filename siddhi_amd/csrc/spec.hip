@@ -83,6 +83,18 @@ struct Consts {
     for (size_t i = 0; i < pcs.size(); ++i) s += fmt("    k.c[%zu] = ql->code[%d].imm;\n", i, pcs[i]);
     return s + "  }\n";
   }
+  // from the group's lane-constant table column lc (kg::LaneConsts: slot LC_FIRST + the instruction's
+  // rank among the shape's CONST instructions; one coalesced row per constant)
+  std::string load_table(const kg::GQuery& g, const std::string& sig) const {
+    int8_t rank[kg::GMAXCODE];
+    int n = 0;
+    kg::const_ranks(g, rank, &n);
+    std::string s = "  __device__ static void load(K& k, const sdh::kg::GQuery* ql, " + sig + ", const int64_t* lc) {\n";
+    if (pcs.empty()) s += "    k.c[0] = 0;\n";
+    for (size_t i = 0; i < pcs.size(); ++i)
+      s += fmt("    k.c[%zu] = lc[%d * 64];\n", i, kg::LC_FIRST + (int)rank[pcs[i]]);
+    return s + "  }\n";
+  }
 };
 
 // One filter (bytecode range [b, e) of g) as statements; returns the variable holding its kg::Val.
@@ -251,9 +263,7 @@ std::string part_source(const kg::GQuery& g, const PartLayout& lay) {
   s += fmt("  __device__ static sdh::PartOffs offs(const sdh::PartLaunch&) { return sdh::PartOffs{%d, %d, %d, %d}; }\n",
            lay.cmax, lay.n_e1, lay.n_first, lay.n_last);
   s += K.decl();
-  s += "  __device__ static void load(K& k, const sdh::kg::GQuery* ql, const sdh::PartLaunch&) {\n";
-  std::string ld = K.load();
-  s += ld.substr(ld.find('\n') + 1);  // (load's body, with the launch argument added)
+  s += K.load_table(g, "const sdh::PartLaunch&");
   s += fns;
   s += "};\n\n";
   s += fmt("extern \"C\" __global__ __launch_bounds__(64) %svoid sdh_part_spec(sdh::PartLaunch L) {\n"

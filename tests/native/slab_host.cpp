@@ -65,7 +65,7 @@ void step_instance(Host* h, int qi, int64_t key, std::vector<uint32_t>& ent, int
       }
     }
     if (!(sh.every || !marker)) return;
-    if (!start_pass(sh, &q, &q, ev)) return;
+    if (!start_pass(sh, &q, kg::LaneConsts{&q, nullptr}, ev)) return;
     ent.resize(ent.size() + EW);
     open_partial(sh, &ent[(size_t)n * EW], 0, any ? mx + 1 : 0, ev);
     if (!sh.every) {
@@ -77,7 +77,7 @@ void step_instance(Host* h, int qi, int64_t key, std::vector<uint32_t>& ent, int
   bool moved = false;
   for (int k = 0; k < n; ++k) {
     uint32_t* e = &ent[(size_t)k * EW];
-    const int r = step(sh, &q, &q, st, e, ev, q.within);
+    const int r = step(sh, &q, kg::LaneConsts{&q, nullptr}, st, e, ev, q.within);
     if (r & R_EMIT) {
       const int words = record_words(sh, e, st);
       std::vector<int64_t> rr(words);
