@@ -774,7 +774,9 @@ struct sdh_engine {
     DevBuf<unsigned long long> traffic;       // block bytes read + written by the last launch
     DevBuf<uint64_t> journal, journal_idx;
     int64_t items = 0;                        // items of this pass's launch (0: not launched)
-    int lds_words = 4096;
+    int lds_words = 4096;                     // LDS rows (uint32 words) of the large tier
+    DevBuf<int32_t> defer, defer_n;           // items deferred to the large tier (nfa_slab.hip)
+    int64_t deferred = 0;
     int64_t cleanings = 0, growths = 0;
   };
   std::vector<std::unique_ptr<SlabSet>> ssets;
@@ -826,6 +828,7 @@ struct sdh_engine {
   DevBuf<uint8_t> p_ptemp;
   int64_t r_seq_base = 0;            // seq of the last launch's first event
   std::vector<int32_t> r_blk_count;
+  int slab_lds_small = 1024;          // K_slab small-tier LDS rows (SDH_SLAB_LDS_SMALL)
   int xcd = 0;                       // per-XCD item ranges in the K_gen / K_seq / K_part / K_slab launches
                                      // (dev::grid_item; SDH_XCD=1: measured neutral)
   int rML = 8;                       // LDS ring entries per lane (power of two)
@@ -2814,7 +2817,32 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       S.rec_next = e->g_rec_next.p;
       S.write_records = write ? 1 : 2;
       S.err = e->d_serr.p + 4 * si;
+      // two LDS tiers: every item first with small rows (more resident waves); the few whose block
+      // outgrows them are deferred to a second launch with the set's full rows
+      const int small = std::min(ss.lds_words, e->slab_lds_small);
+      if (small < ss.lds_words) {
+        ss.defer.ensure((size_t)items);
+        ss.defer_n.ensure(1);
+        HIPCHK(hipMemsetAsync(ss.defer_n.p, 0, 4, e->stream));
+        S.lds_words = small;
+        S.defer_cap = (int32_t)items;
+        S.defer = ss.defer.p;
+        S.defer_n = ss.defer_n.p;
+      }
       HIPCHK(sdh_launch_slab(&S, e->stream));
+      if (small < ss.lds_words) {
+        int32_t nd = 0;
+        d2h_sync(e, &nd, ss.defer_n.p, 4);
+        if (nd > 0) {
+          sdh::SlabLaunch D = S;
+          D.lds_words = ss.lds_words;
+          D.defer_cap = 0;
+          D.item_list = ss.defer.p;
+          D.n_items = std::min<int32_t>(nd, (int32_t)items);
+          HIPCHK(sdh_launch_slab(&D, e->stream));
+        }
+        ss.deferred += nd;
+      }
       ss.items = items;
       e->slab_items += items;
       any = true;
@@ -3423,6 +3451,7 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     if (const char* v = getenv("SDH_RATCHET_ML")) e->rML = std::max(4, atoi(v));
     if (const char* v = getenv("SDH_RATCHET_WAVES")) e->r_waves = atof(v);
     if (const char* v = getenv("SDH_XCD")) e->xcd = atoi(v) != 0;
+    if (const char* v = getenv("SDH_SLAB_LDS_SMALL")) e->slab_lds_small = std::max(64, atoi(v));
     e->out_rank = kg::output_ranks(e->lp);
     // plan selection per query: K_ratchet (2-state threshold ratchet) > K_chain (stream-state
     // chains) > K_gen (everything else: count, logical, sequences, partitions, general predicates)

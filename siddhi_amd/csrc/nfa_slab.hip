@@ -25,7 +25,8 @@
 
 namespace sdh {
 
-using SlabWaveOut = dev::WaveOutT<768>;
+// (C5 emits ~0.6 records per work item: a small output buffer leaves LDS for resident waves)
+using SlabWaveOut = dev::WaveOutT<256>;
 
 namespace {
 
@@ -63,8 +64,9 @@ template <int NAX>
 __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
   using namespace slab;
   const int lane = threadIdx.x;
-  const int item = (int)dev::grid_item(L.xcd);
-  if (item >= L.n_items) return;
+  const int gi = (int)dev::grid_item(L.xcd);
+  if (gi >= L.n_items) return;
+  const int item = L.item_list ? L.item_list[gi] : gi;
   const int seg = item / L.n_glist, g = L.glist[item % L.n_glist];
   const uint32_t kid = L.seg_kid[seg];
   if (kid == 0xFFFFFFFFu) return;  // null / foreign partition keys
@@ -93,8 +95,22 @@ __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
   __shared__ int64_t sh_base;
   uint32_t* ent = slab_lds;
   const int cap_ent = L.lds_words / EW;  // entries this shape's rows fit in the launch's LDS
+  // a block that outgrows this launch's rows: deferred to the large-LDS launch (two tiers keep most
+  // waves small, so more of them are resident), or, in that launch, the push re-runs with more LDS.
+  // A deferred item has changed nothing (an e1 item that grows emits nothing before its write-back)
+  auto outgrown = [&]() {
+    if (lane != 0) return;
+    if (L.defer_cap > 0) {
+      const int d = atomicAdd(L.defer_n, 1);
+      if (d < L.defer_cap) {
+        L.defer[d] = item;
+        return;
+      }
+    }
+    atomicOr(&L.err[0], 1);
+  };
   if (n_old > cap_ent) {
-    if (lane == 0) atomicOr(&L.err[0], 1);
+    outgrown();
     return;
   }
   // the old block -> LDS (coalesced), then each lane's range (entries are sorted by lane)
@@ -246,13 +262,13 @@ __global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
     __syncthreads();  // the tile is rewritten next
   }
   o.close();
+  if (lds_over) {  // only e1 items grow (they emit nothing)
+    outgrown();
+    return;
+  }
   if (lane == 0 && n_old) atomicAdd(&L.traffic[item & 255], (unsigned long long)n_old * EW * 4);
   if (nrec) atomicAdd(L.rec_count, nrec);
   if (o.over) atomicOr(&L.err[2], 1);
-  if (lds_over) {  // only e1 items grow (they emit nothing): the push is undone and re-run
-    if (lane == 0) atomicOr(&L.err[0], 1);
-    return;
-  }
   if (!__ballot(changed)) return;
   // write-back: the lane's surviving entries (old ones still in a list, markers) then its new ones
   int m_l = 0, parts_old = 0, parts_new = 0;

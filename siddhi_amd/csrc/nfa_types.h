@@ -395,7 +395,10 @@ struct SlabLaunch {
   int32_t* err;               // [0] LDS capacity, [1] slab space, [2] output overflow
   const int64_t* lconst;      // [group][lc_slots][64] the lanes' query ids, withins, constants (kg::LaneConsts)
   int32_t lc_slots;
-  int32_t pad_lc;
+  int32_t defer_cap;          // two-tier LDS: room in defer (0: no deferral, an oversized block sets err[0])
+  int32_t* defer;             // items whose block outgrew this launch's LDS rows (re-run with more LDS)
+  int32_t* defer_n;
+  const int32_t* item_list;   // the deferred launch: its items (nullptr: items 0 .. n_items-1)
 };
 
 // ------------------------------------------------------------------------------------------
