@@ -20,6 +20,8 @@
 // oldest half to its head (slab_move_kernel), or by moving everything into a larger slab.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "dev_common.h"
 #include "slab.h"
 
@@ -60,8 +62,8 @@ __device__ __forceinline__ int wave_prefix(int v, int bits, int* total) {
 
 // NAX: the captured words the event staging holds (the launch's widest shape); LDS bounds the resident
 // waves of this kernel
-template <int NAX>
-__global__ __launch_bounds__(64) void nfa_slab_kernel(SlabLaunch L) {
+template <int NAX, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void nfa_slab_kernel(SlabLaunch L) {
   using namespace slab;
   const int lane = threadIdx.x;
   const int gi = (int)dev::grid_item(L.xcd);
@@ -402,8 +404,15 @@ extern "C" hipError_t sdh_launch_slab(const sdh::SlabLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
   const size_t lds = (size_t)L->lds_words * 4;
   const unsigned grid = (unsigned)(L->xcd ? (L->n_items + 7) & ~7 : L->n_items);
-  if (L->max_na <= 4) hipLaunchKernelGGL(sdh::nfa_slab_kernel<4>, dim3(grid), dim3(64), lds, s, *L);
-  else hipLaunchKernelGGL(sdh::nfa_slab_kernel<sdh::kg::GMAXNA>, dim3(grid), dim3(64), lds, s, *L);
+  // waves per SIMD the register allocation aims at (SDH_SLAB_WPE; LDS allows ~4 at the small tier)
+  static const int wpe = getenv("SDH_SLAB_WPE") ? atoi(getenv("SDH_SLAB_WPE")) : 4;
+  if (L->max_na <= 4) {
+    if (wpe >= 6) hipLaunchKernelGGL((sdh::nfa_slab_kernel<4, 6>), dim3(grid), dim3(64), lds, s, *L);
+    else if (wpe == 5) hipLaunchKernelGGL((sdh::nfa_slab_kernel<4, 5>), dim3(grid), dim3(64), lds, s, *L);
+    else hipLaunchKernelGGL((sdh::nfa_slab_kernel<4, 1>), dim3(grid), dim3(64), lds, s, *L);
+  } else {
+    hipLaunchKernelGGL((sdh::nfa_slab_kernel<sdh::kg::GMAXNA, 1>), dim3(grid), dim3(64), lds, s, *L);
+  }
   return hipGetLastError();
 }
 
