@@ -663,6 +663,8 @@ def expansion(args, sh, K, local, dev, world, cdev, dist):
     r = {"events_per_step": E, "steps": steps, "ms_per_step": el * 1e3 / steps,
          "push_ms_per_step": push_ms / steps, "poll_ms_per_step": (el * 1e3 - push_ms - gather_ms) / steps,
          "matches_per_step": matches / steps, "pattern_events_per_s": pe_timed / el, "matches_per_s": matches / el}
+    if world == 1:
+        r["compact"] = compact_leg(args, sh, K, local, bs, E, warm, matches)
     if world > 1:
         if dist.get_rank() == 0 and merged != matches:
             raise RuntimeError(f"the gather merged {merged} matches, the ranks produced {matches}")
@@ -670,6 +672,39 @@ def expansion(args, sh, K, local, dev, world, cdev, dist):
         r["merged_matches_per_step_rank0"] = merged / steps
         r["gather_merge_ns_per_match"] = gather_ms * 1e6 / max(1, matches)
     return r
+
+
+def compact_leg(args, sh, K, local, bs, E, warm, want):
+    """The expansion pushes again on a fresh engine, each followed by sdh_engine_poll_compact(device):
+    the same R18-ordered matches as compact int32 rows (a window placed by K_ratchet is handed out as
+    it is: no sort, no gather). Workloads whose matches the form cannot express (count chains,
+    partition keys) report why."""
+    import torch
+    from siddhi_amd.engine import EngineError
+    eng = make_engine(args.workload, sh, K, local, 0, args.partials)
+    matches, width = 0, 0
+    try:
+        for i, cols in enumerate(bs):
+            if i == warm:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            eng.push_device(0, E, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
+            m = eng.poll_compact(device=True)
+            if i >= warm:
+                matches += m.n
+                width = m.width
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    except EngineError as ex:
+        return {"unsupported": str(ex)}
+    finally:
+        eng.close()
+    if matches != want:
+        raise RuntimeError(f"poll_compact delivered {matches} matches, sdh_engine_poll_device {want}")
+    steps = len(bs) - warm
+    log(f"compact leg: {matches} matches in {el * 1e3:.1f} ms (width {width})")
+    return {"ms_per_step": el * 1e3 / steps, "matches_per_s": matches / el, "width": width,
+            "bytes_per_match": 4 * width}
 
 
 if __name__ == "__main__":

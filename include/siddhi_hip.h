@@ -170,6 +170,26 @@ int sdh_engine_poll(sdh_engine* e, sdh_matches* out);
 /* As sdh_engine_poll, but every sdh_matches pointer is a HIP device pointer into engine-owned HBM
  * (valid until the next push/poll/destroy): no copy to the host. */
 int sdh_engine_poll_device(sdh_engine* e, sdh_matches* out);
+/* The same matches in the same order as compact int32 rows (4 * width bytes per match),
+ * for consumers that hold their own events and want the match relation only: row i is
+ * rows[i * width .. (i + 1) * width) =
+ *   { query, seq_i - seq_base, then per state slot seq_i - the slot's event seq (0 for the event
+ *     that completed the match), or INT32_MIN for an empty slot / a slot the query lacks },
+ * where seq_i is sdh_matches.seq[i]; width = 2 + the most states any query of the engine has.
+ * A window whose matches came straight from K_ratchet placement is handed out without a sort or a
+ * gather (4 int32 per match instead of 8 int64 + 4 words). Matches this form cannot express (a slot
+ * holding a chain of several events -- count states --, a partition key, an absent state's timer
+ * match, seq distances past 2^31) fail with SDH_E_UNSUPPORTED and stay pending: poll them with
+ * sdh_engine_poll. device != 0 leaves rows in engine-owned HBM (valid until the next
+ * push/poll/destroy); otherwise they are copied to an engine-owned host buffer. */
+typedef struct sdh_matches_compact {
+  int64_t n;
+  int64_t seq_base;
+  int32_t width;
+  int32_t flags;             /* 0 */
+  const int32_t* rows;
+} sdh_matches_compact;
+int sdh_engine_poll_compact(sdh_engine* e, int32_t device, sdh_matches_compact* out);
 /* Device-resident match count of the last push (no host copy of the matches). */
 int sdh_engine_pending_matches(sdh_engine* e, int64_t* n);
 /* Absent patterns (`not S[..] for T`) and time. The runtime starts at t (SiddhiAppRuntime.start:

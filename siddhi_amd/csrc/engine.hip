@@ -93,12 +93,16 @@ extern "C" hipError_t sdh_key_segments(const uint32_t* uniq, const int32_t* nrun
 extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, const int32_t* blk_count,
                                         const int32_t* blk_group, int n_blocks, int64_t rows, const int32_t* out_rank,
                                         int n_streams, int n_ranks, int64_t n_events, int32_t* cnt, void* temp,
-                                        size_t temp_bytes, const sdh::RatchetGroup* groups, const int64_t* ts,
-                                        int64_t seq_base, int64_t row0, int64_t* oq, int64_t* okey, int64_t* ots,
-                                        int64_t* oseq, int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s);
-extern "C" hipError_t sdh_placed_to_table(const int64_t* q, const int64_t* ts, const int64_t* seq, const int64_t* words,
-                                          int64_t n, int64_t seq_ref, const int32_t* out_rank, const int32_t* qinfo,
+                                        size_t temp_bytes, const sdh::RatchetGroup* groups, int64_t seq_base,
+                                        int64_t seq_ref, int64_t row0, int width, int32_t* crow, hipStream_t s);
+extern "C" hipError_t sdh_compact_fill(const int32_t* crow, int width, int64_t rows, const int64_t* ts_log,
+                                       int64_t seq_ref, int64_t* oq, int64_t* okey, int64_t* ots, int64_t* oseq,
+                                       int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s);
+extern "C" hipError_t sdh_placed_to_table(const int32_t* crow, int width, int64_t n, const int64_t* ts_log,
+                                          int64_t seq_ref, const int32_t* out_rank, const int32_t* qinfo,
                                           int n_streams, sdh::MatchTable T, hipStream_t s);
+extern "C" hipError_t sdh_table_compact(sdh::MatchTable T, const int32_t* perm, int64_t n, int width, int64_t seq_ref,
+                                        int32_t* crow, int32_t* err, hipStream_t s);
 extern "C" hipError_t sdh_live_gen(const int32_t* a32, int64_t B32, int64_t blocks, int n_groups, int group_base,
                                     const int32_t* lane_q, const int32_t* group_seq, const sdh::kg::GQuery* queries,
                                     unsigned long long* acc, hipStream_t s);
@@ -669,6 +673,13 @@ struct sdh_engine {
   DevBuf<uint8_t> p_temp;
   DevBuf<int64_t> po_q, po_key, po_ts, po_seq, po_tb, po_len, po_off, po_words;
   HostBuf<int64_t> ho_q, ho_key, ho_ts, ho_seq, ho_tb, ho_off, ho_words;
+  // compact rows (sdh_matches_compact): a placed window's rows live here (the ABI columns are
+  // filled from them at a full poll), with the window's event times ts_log[seq - seq_ref]; cw =
+  // 2 + the most states any query has
+  DevBuf<int32_t> pc_rows, pc_err;
+  DevBuf<int64_t> ts_log;
+  HostBuf<int32_t> hc_rows;
+  int cw = 4;
   // ---- K_gen (general interpreter) ----
   kg::LProgram lp;                   // full IR (receivers, runtime tree, partitions)
   std::vector<int> out_rank;         // R18 rank per (query, stream)
@@ -1072,22 +1083,20 @@ bool ratchet_placeable(const sdh_engine* e, int stream, int64_t n_events, bool f
 bool place_ratchet(sdh_engine* e, int stream, const int64_t* ts_col, int64_t seq_base, int64_t n_events) {
   const int nr = e->place_nr[(size_t)stream];
   const int64_t rows = e->r_matches, n0 = e->mt.n;
-  if (!e->r_placing || n0 + rows >= INT32_MAX) return false;
-  const size_t keep = (size_t)n0, want = (size_t)(n0 + rows);
-  e->po_q.grow_keep(want, keep, e->stream);
-  e->po_key.grow_keep(want, keep, e->stream);
-  e->po_ts.grow_keep(want, keep, e->stream);
-  e->po_seq.grow_keep(want, keep, e->stream);
-  e->po_tb.grow_keep(want, keep, e->stream);
-  e->po_off.grow_keep(want + 1, keep, e->stream);
-  e->po_words.grow_keep(4 * want, 4 * keep, e->stream);
+  if (!e->r_placing || n0 + rows >= INT32_MAX || seq_base + n_events - e->seq_ref >= INT32_MAX) return false;
+  const int w = e->cw;
+  e->pc_rows.grow_keep((size_t)((n0 + rows) * w), (size_t)(n0 * w), e->stream);
+  // the window's event times: the compact rows carry seqs only
+  const int64_t t0 = seq_base - e->seq_ref;
+  e->ts_log.grow_keep((size_t)(t0 + n_events), (size_t)t0, e->stream);
+  if (n_events)
+    HIPCHK(hipMemcpyAsync(e->ts_log.p + t0, ts_col, (size_t)n_events * 8, hipMemcpyDeviceToDevice, e->stream));
   const int64_t cells = n_events * nr;
   const size_t tb = sdh_place_temp_bytes(cells);
   e->p_ptemp.ensure(tb);
   HIPCHK(sdh_place_ratchet(e->d_rmatch.p, e->r_blk_recs, e->d_blk_count.p, e->d_blk_group.p, e->r_blocks_used, rows,
                            e->d_place_rank.p, (int)e->prog.stream_types.size(), nr, n_events, e->p_cnt.p, e->p_ptemp.p,
-                           e->p_ptemp.n, e->d_rg.p, ts_col, seq_base, n0, e->po_q.p, e->po_key.p, e->po_ts.p,
-                           e->po_seq.p, e->po_tb.p, e->po_off.p, e->po_words.p, e->stream));
+                           e->p_ptemp.n, e->d_rg.p, seq_base, e->seq_ref, n0, w, e->pc_rows.p, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   e->mt.n += rows;
   e->mt.placed = true;
@@ -1102,8 +1111,8 @@ void placed_to_table(sdh_engine* e) {
   e->mt.n = 0;
   e->mt.nw = 0;
   table_reserve(e, n, 4 * n);
-  HIPCHK(sdh_placed_to_table(e->po_q.p, e->po_ts.p, e->po_seq.p, e->po_words.p, n, e->seq_ref, e->d_out_rank.p,
-                             e->d_qinfo.p, (int)e->prog.stream_types.size(), table_view(e), e->stream));
+  HIPCHK(sdh_placed_to_table(e->pc_rows.p, e->cw, n, e->ts_log.p, e->seq_ref, e->d_out_rank.p, e->d_qinfo.p,
+                             (int)e->prog.stream_types.size(), table_view(e), e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   e->mt.n = n;
   e->mt.nw = 4 * n;
@@ -1117,23 +1126,29 @@ int bits_of(uint64_t v) {
   return b;
 }
 
-// R18 sort of the table and gather of the ABI arrays in HBM (po_*); returns the match count
-int64_t table_sort(sdh_engine* e, int64_t* total_words) {
+// the ABI output arrays in HBM for n matches of tw words (po_*; off and len have n + 1 entries)
+void poll_reserve(sdh_engine* e, int64_t n, int64_t tw) {
+  const size_t m = (size_t)std::max<int64_t>(n, 1);
+  e->po_q.ensure(m);
+  e->po_key.ensure(m);
+  e->po_ts.ensure(m);
+  e->po_seq.ensure(m);
+  e->po_tb.ensure(m);
+  e->po_len.ensure(n + 1);
+  e->po_off.ensure(n + 1);
+  e->po_words.ensure((size_t)std::max<int64_t>(tw, 1));
+}
+
+// R18 sort of the table's n > 0 rows and gather of the ABI arrays except the words; returns the
+// sorted order (perm[i] = the table row of match i)
+int32_t* table_order(sdh_engine* e, int64_t* total_words) {
   const int64_t n = e->mt.n;
-  *total_words = 0;
-  if (n == 0) return 0;
   if (n >= INT32_MAX) throw Error(SDH_E_CAPACITY, "more than 2^31 matches between two polls");
   e->p_keys.ensure((size_t)n * 2);
   e->p_perm.ensure((size_t)n * 2);
   const size_t tb = sdh_poll_temp_bytes(n);
   e->p_temp.ensure(tb);
-  e->po_q.ensure(n);
-  e->po_key.ensure(n);
-  e->po_ts.ensure(n);
-  e->po_seq.ensure(n);
-  e->po_tb.ensure(n);
-  e->po_len.ensure(n + 1);
-  e->po_off.ensure(n + 1);
+  poll_reserve(e, n, 0);
   // timer records' tiebreaks are a full timestamp, the query and the partition key
   const int lo_bits = e->has_absent ? 64 : std::max(1, bits_of((uint64_t)std::max<int64_t>(e->seq, 1 << 16)));
   const int hi_bits = bits_of((uint64_t)(e->seq - e->seq_ref)) + RANK_BITS;
@@ -1147,6 +1162,15 @@ int64_t table_sort(sdh_engine* e, int64_t* total_words) {
                        e->p_temp.p, e->p_temp.n, e->po_q.p, e->po_key.p, e->po_ts.p, e->po_seq.p, e->po_tb.p,
                        e->po_len.p, e->po_off.p, &perm, total_words, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  return perm;
+}
+
+// R18 sort of the table and gather of the ABI arrays in HBM (po_*); returns the match count
+int64_t table_sort(sdh_engine* e, int64_t* total_words) {
+  const int64_t n = e->mt.n;
+  *total_words = 0;
+  if (n == 0) return 0;
+  int32_t* perm = table_order(e, total_words);
   e->po_words.ensure((size_t)std::max<int64_t>(*total_words, 1));
   HIPCHK(sdh_poll_words(table_view(e), perm, n, e->po_off.p, e->po_words.p, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
@@ -3231,10 +3255,12 @@ int do_poll(sdh_engine* e, sdh_matches* out, bool host) {
   check_usable(e);
   int64_t tw = 0;
   int64_t n = 0;
-  if (e->mt.placed) {  // already in R18 order (place_ratchet): 4 words per match
+  if (e->mt.placed) {  // compact rows already in R18 order (place_ratchet): 4 words per match
     n = e->mt.n;
     tw = 4 * n;
-    HIPCHK(hipMemcpyAsync(e->po_off.p + n, &tw, 8, hipMemcpyHostToDevice, e->stream));
+    poll_reserve(e, n, tw);
+    HIPCHK(sdh_compact_fill(e->pc_rows.p, e->cw, n, e->ts_log.p, e->seq_ref, e->po_q.p, e->po_key.p, e->po_ts.p,
+                            e->po_seq.p, e->po_tb.p, e->po_off.p, e->po_words.p, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
   } else {
     n = table_sort(e, &tw);
@@ -3280,6 +3306,43 @@ int do_poll(sdh_engine* e, sdh_matches* out, bool host) {
     out->words = e->po_words.p;
   }
   out->n = n;
+  table_clear(e);
+  return SDH_OK;
+}
+
+// the window's matches as compact rows (sdh_engine_poll_compact): a placed window hands out its rows
+// as they are; otherwise the table is R18-sorted and converted, and a row the form cannot express
+// fails the call with the window left pending
+int do_poll_compact(sdh_engine* e, sdh_matches_compact* out, bool device) {
+  check_usable(e);
+  const int64_t n = e->mt.n;
+  const int w = e->cw;
+  if (!e->mt.placed && n) {
+    if (e->seq - e->seq_ref >= INT32_MAX) throw Error(SDH_E_UNSUPPORTED, "compact rows: seq span past 2^31");
+    int64_t tw = 0;
+    const int32_t* perm = table_order(e, &tw);
+    e->pc_rows.ensure((size_t)(n * w));
+    e->pc_err.ensure(1);
+    HIPCHK(hipMemsetAsync(e->pc_err.p, 0, 4, e->stream));
+    HIPCHK(sdh_table_compact(table_view(e), perm, n, w, e->seq_ref, e->pc_rows.p, e->pc_err.p, e->stream));
+    int32_t bad = 0;
+    d2h_sync(e, &bad, e->pc_err.p, 4);
+    if (bad)
+      throw Error(SDH_E_UNSUPPORTED, "compact rows: a match has a count-state chain, a partition key or a timer "
+                                     "(poll it with sdh_engine_poll)");
+  }
+  e->pc_rows.ensure(1);
+  out->n = n;
+  out->seq_base = e->seq_ref;
+  out->width = w;
+  out->flags = 0;
+  if (device) {
+    out->rows = e->pc_rows.p;
+  } else {
+    e->hc_rows.ensure((size_t)std::max<int64_t>(n * w, 1));
+    if (n) d2h_sync(e, e->hc_rows.p, e->pc_rows.p, (size_t)(n * w) * 4);
+    out->rows = e->hc_rows.p;
+  }
   table_clear(e);
   return SDH_OK;
 }
@@ -3563,6 +3626,7 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     }
     e->d_qinfo.ensure(qinfo.size());
     HIPCHK(hipMemcpy(e->d_qinfo.p, qinfo.data(), qinfo.size() * 4, hipMemcpyHostToDevice));
+    for (size_t q = 0; q < nq_all; ++q) e->cw = std::max(e->cw, 2 + qinfo[2 * q]);
     return SDH_OK;
   });
   if (rc != SDH_OK) {
@@ -3632,6 +3696,11 @@ int sdh_engine_poll(sdh_engine* e, sdh_matches* out) {
 int sdh_engine_poll_device(sdh_engine* e, sdh_matches* out) {
   if (!e || !out) return SDH_E_INVALID;
   return guard(e, [&]() { return do_poll(e, out, false); });
+}
+
+int sdh_engine_poll_compact(sdh_engine* e, int32_t device, sdh_matches_compact* out) {
+  if (!e || !out) return SDH_E_INVALID;
+  return guard(e, [&]() { return do_poll_compact(e, out, device != 0); });
 }
 
 // keys a partition has seen so far (its routing table's dense ids)

@@ -119,15 +119,15 @@ __global__ __launch_bounds__(256) void digest_ratchet_kernel(const int64_t* __re
 // pop level; an exclusive scan over the cells gives each cell's first row, and a record of level L
 // goes to
 //   P = row0 + base[cell] + count[cell] - 1 - L = row0 + base[cell + 1] - 1 - L.
-// Two passes, no sort. Scattered 8-B stores would each dirty a separate 32-B sector of six output
-// columns, so pass 1 (record order) writes only the row's aligned 32-B word quadruple, carrying the
-// query in place of its first count word: {q, e1 seq, 1, e2 seq}; pass 2 (row order, coalesced)
-// reads it back and writes every ABI column of the row.
+// One pass, no sort: each record becomes its row of the window's COMPACT rows (sdh_matches_compact,
+// `width` int32: query, e2 seq - seq_ref, per slot the trigger seq minus the slot's seq -- e2 - e1,
+// 0 -- then INT32_MIN for slots the engine's wider queries have), one 16-B store for width 4. The
+// ABI columns are built from them only when a poll asks for the full tuples (compact_fill_kernel).
 __global__ __launch_bounds__(256) void ratchet_place_kernel(
     const int64_t* __restrict__ match, int blk_recs, const int32_t* __restrict__ blk_count,
     const int32_t* __restrict__ blk_group, int64_t rows, const int32_t* __restrict__ out_rank, int n_streams,
     int n_ranks, int64_t cells, const int32_t* __restrict__ base, const RatchetGroup* __restrict__ groups,
-    int64_t seq_base, int64_t row0, int64_t* __restrict__ owords) {
+    int64_t seq_base, int64_t seq_ref, int64_t row0, int width, int32_t* __restrict__ crow) {
   __shared__ int32_t s_q[64], s_rank[64];
   const int b = blockIdx.x;
   const int n = blk_count[b];
@@ -161,53 +161,105 @@ __global__ __launch_bounds__(256) void ratchet_place_kernel(
       const uint32_t off = r[u].x, lane = r[u].y & 63, q1 = r[u].z, level = r[u].w;
       const int64_t P = row0 + next[u] - 1 - (int64_t)level;
       const int64_t s = seq_base + (int64_t)off;
-      const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
-      reinterpret_cast<longlong2*>(owords + 4 * P)[0] = make_longlong2(s_q[lane], s1);
-      reinterpret_cast<longlong2*>(owords + 4 * P)[1] = make_longlong2(1, s);
+      const int32_t d0 = (int32_t)((uint32_t)s - q1);  // e2 - e1 (< 2^31: the kernel's aged check)
+      const int32_t rel = (int32_t)(s - seq_ref);
+      int32_t* o = crow + P * width;
+      if (width == 4) {
+        *reinterpret_cast<int4*>(o) = make_int4(s_q[lane], rel, d0, 0);
+      } else {
+        o[0] = s_q[lane];
+        o[1] = rel;
+        o[2] = d0;
+        o[3] = 0;
+        for (int k = 4; k < width; ++k) o[k] = INT32_MIN;
+      }
     }
   }
 }
 
-__global__ __launch_bounds__(256) void placed_fill_kernel(int64_t row0, int64_t rows, const int64_t* __restrict__ ts,
-                                                          int64_t seq_base, int64_t* __restrict__ oq,
-                                                          int64_t* __restrict__ okey, int64_t* __restrict__ ots,
-                                                          int64_t* __restrict__ oseq, int64_t* __restrict__ otb,
-                                                          int64_t* __restrict__ ooff, int64_t* __restrict__ owords) {
+// compact rows of a placed window (K_ratchet: two one-event slots) -> the ABI columns of rows
+// [0, rows): words {1, e1, 1, e2} per row, ts from the window's event-time log (ts_log[seq - seq_ref])
+__global__ __launch_bounds__(256) void compact_fill_kernel(const int32_t* __restrict__ crow, int width, int64_t rows,
+                                                           const int64_t* __restrict__ ts_log, int64_t seq_ref,
+                                                           int64_t* __restrict__ oq, int64_t* __restrict__ okey,
+                                                           int64_t* __restrict__ ots, int64_t* __restrict__ oseq,
+                                                           int64_t* __restrict__ otb, int64_t* __restrict__ ooff,
+                                                           int64_t* __restrict__ owords) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= rows) return;
-  const int64_t P = row0 + i;
-  longlong2* w = reinterpret_cast<longlong2*>(owords + 4 * P);
-  const longlong2 a = w[0], b = w[1];
-  oq[P] = a.x;
-  okey[P] = -1;
-  ots[P] = ts[b.y - seq_base];
-  oseq[P] = b.y;
-  otb[P] = INT64_MIN;
-  ooff[P] = 4 * P;
-  w[0] = make_longlong2(1, a.y);
+  if (i > rows) return;
+  if (i == rows) {
+    ooff[rows] = 4 * rows;
+    return;
+  }
+  const int32_t* r = crow + i * width;
+  const int64_t e2 = seq_ref + (int64_t)r[1], e1 = e2 - (int64_t)r[2];
+  oq[i] = r[0];
+  okey[i] = -1;
+  ots[i] = ts_log[r[1]];
+  oseq[i] = e2;
+  otb[i] = INT64_MIN;
+  ooff[i] = 4 * i;
+  reinterpret_cast<longlong2*>(owords + 4 * i)[0] = make_longlong2(1, e1);
+  reinterpret_cast<longlong2*>(owords + 4 * i)[1] = make_longlong2(1, e2);
 }
 
-// placed rows [0, n) -> general table rows (a later push in the same poll window has other producers)
-__global__ __launch_bounds__(256) void placed_to_table_kernel(const int64_t* __restrict__ q, const int64_t* __restrict__ ts,
-                                                              const int64_t* __restrict__ seq,
-                                                              const int64_t* __restrict__ words, int64_t n,
-                                                              int64_t seq_ref, const int32_t* __restrict__ out_rank,
+// placed compact rows [0, n) -> general table rows (a later push in the same poll window has other
+// producers)
+__global__ __launch_bounds__(256) void placed_to_table_kernel(const int32_t* __restrict__ crow, int width, int64_t n,
+                                                              const int64_t* __restrict__ ts_log, int64_t seq_ref,
+                                                              const int32_t* __restrict__ out_rank,
                                                               const int32_t* __restrict__ qinfo, int n_streams,
                                                               MatchTable T) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int qq = (int)q[i];
-  T.hi[i] = hi_key(seq[i], seq_ref, out_rank[(int64_t)qq * n_streams + qinfo[2 * qq + 1]]);
-  T.lo[0][i] = (uint64_t)words[4 * i + 1];
+  const int32_t* r = crow + i * width;
+  const int qq = r[0];
+  const int64_t e2 = seq_ref + (int64_t)r[1], e1 = e2 - (int64_t)r[2];
+  T.hi[i] = hi_key(e2, seq_ref, out_rank[(int64_t)qq * n_streams + qinfo[2 * qq + 1]]);
+  T.lo[0][i] = (uint64_t)e1;
 #pragma unroll
   for (int k = 1; k < MAXLO; ++k) T.lo[k][i] = 0ull;
-  T.seq[i] = seq[i];
+  T.seq[i] = e2;
   T.q[i] = qq;
   T.key[i] = -1;
-  T.ts[i] = ts[i];
+  T.ts[i] = ts_log[r[1]];
   T.woff[i] = 4 * i;
   T.wlen[i] = 4;
-  for (int k = 0; k < 4; ++k) T.words[4 * i + k] = words[4 * i + k];
+  reinterpret_cast<longlong2*>(T.words + 4 * i)[0] = make_longlong2(1, e1);
+  reinterpret_cast<longlong2*>(T.words + 4 * i)[1] = make_longlong2(1, e2);
+}
+
+// R18-sorted table rows -> compact rows (sdh_engine_poll_compact on a window with other producers):
+// [query, trigger seq - seq_ref, per slot trigger seq - its event's seq (INT32_MIN: empty)].
+// err[0] = 1 when a row does not fit the form: a slot with a chain of several events (count
+// states), a partition key, a timer match, or a seq distance past int32.
+__global__ __launch_bounds__(256) void table_compact_kernel(MatchTable T, const int32_t* __restrict__ perm, int64_t n,
+                                                            int width, int64_t seq_ref, int32_t* __restrict__ crow,
+                                                            int32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t p = perm[i];
+  int32_t* o = crow + i * width;
+  const int64_t sq = T.seq[p];
+  bool bad = T.key[p] != -1 || (T.hi[p] & ((1ull << RANK_BITS) - 1)) == 0 || sq - seq_ref > INT32_MAX;
+  o[0] = (int32_t)T.q[p];
+  o[1] = (int32_t)(sq - seq_ref);
+  const int64_t* w = T.words + T.woff[p];
+  const int64_t len = T.wlen[p];
+  int slot = 0;
+  for (int64_t j = 0; j < len && !bad; ++slot) {
+    const int64_t c = w[j];
+    if (c > 1 || 2 + slot >= width) {
+      bad = true;
+      break;
+    }
+    const int64_t d = c == 1 ? sq - w[j + 1] : 0;
+    if (d < 0 || d > INT32_MAX) bad = true;
+    o[2 + slot] = c == 1 ? (int32_t)d : INT32_MIN;
+    j += 1 + c;
+  }
+  for (int k = 2 + slot; k < width; ++k) o[k] = INT32_MIN;
+  if (bad) atomicOr(err, 1);
 }
 
 // K_chain segments (records {qid, ts, seq_0 .. seq_{S-1}} of rec_words) -> table rows
@@ -412,13 +464,13 @@ extern "C" size_t sdh_place_temp_bytes(int64_t cells) {
   (void)hipcub::DeviceScan::ExclusiveSum((void*)nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, (int)cells);
   return b + 256;
 }
-// cnt: the (event, rank) match counts K_ratchet's PLACE variant stored (scanned in place)
+// cnt: the (event, rank) match counts K_ratchet's PLACE variant stored (scanned in place); the
+// records become compact rows row0.. of crow (width int32 each)
 extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, const int32_t* blk_count,
                                         const int32_t* blk_group, int n_blocks, int64_t rows, const int32_t* out_rank,
                                         int n_streams, int n_ranks, int64_t n_events, int32_t* cnt, void* temp,
-                                        size_t temp_bytes, const sdh::RatchetGroup* groups, const int64_t* ts,
-                                        int64_t seq_base, int64_t row0, int64_t* oq, int64_t* okey, int64_t* ots,
-                                        int64_t* oseq, int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s) {
+                                        size_t temp_bytes, const sdh::RatchetGroup* groups, int64_t seq_base,
+                                        int64_t seq_ref, int64_t row0, int width, int32_t* crow, hipStream_t s) {
   using namespace sdh;
   if (n_blocks <= 0) return hipSuccess;
   const int64_t cells = n_events * n_ranks;
@@ -426,19 +478,35 @@ extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, cons
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, tb, cnt, cnt, (int)cells, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(ratchet_place_kernel, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, blk_count, blk_group,
-                     rows, out_rank, n_streams, n_ranks, cells, cnt, groups, seq_base, row0, owords);
-  if (rows > 0)
-    hipLaunchKernelGGL(placed_fill_kernel, dim3(grid(rows, 256)), dim3(256), 0, s, row0, rows, ts, seq_base, oq, okey,
-                       ots, oseq, otb, ooff, owords);
+                     rows, out_rank, n_streams, n_ranks, cells, cnt, groups, seq_base, seq_ref, row0, width, crow);
   return hipGetLastError();
 }
 
-extern "C" hipError_t sdh_placed_to_table(const int64_t* q, const int64_t* ts, const int64_t* seq, const int64_t* words,
-                                          int64_t n, int64_t seq_ref, const int32_t* out_rank, const int32_t* qinfo,
+// the ABI columns of a placed window's compact rows (po_* arrays; off has rows + 1 entries)
+extern "C" hipError_t sdh_compact_fill(const int32_t* crow, int width, int64_t rows, const int64_t* ts_log,
+                                       int64_t seq_ref, int64_t* oq, int64_t* okey, int64_t* ots, int64_t* oseq,
+                                       int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s) {
+  hipLaunchKernelGGL(sdh::compact_fill_kernel, dim3(sdh::grid(rows + 1, 256)), dim3(256), 0, s, crow, width, rows,
+                     ts_log, seq_ref, oq, okey, ots, oseq, otb, ooff, owords);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sdh_placed_to_table(const int32_t* crow, int width, int64_t n, const int64_t* ts_log,
+                                          int64_t seq_ref, const int32_t* out_rank, const int32_t* qinfo,
                                           int n_streams, MatchTable T, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(sdh::placed_to_table_kernel, dim3(sdh::grid(n, 256)), dim3(256), 0, s, q, ts, seq, words, n,
+  hipLaunchKernelGGL(sdh::placed_to_table_kernel, dim3(sdh::grid(n, 256)), dim3(256), 0, s, crow, width, n, ts_log,
                      seq_ref, out_rank, qinfo, n_streams, T);
+  return hipGetLastError();
+}
+
+// the R18-sorted table rows (perm from sdh_poll_sort) as compact rows; *err (device) = 1 when some
+// row does not fit the compact form
+extern "C" hipError_t sdh_table_compact(MatchTable T, const int32_t* perm, int64_t n, int width, int64_t seq_ref,
+                                        int32_t* crow, int32_t* err, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::table_compact_kernel, dim3(sdh::grid(n, 256)), dim3(256), 0, s, T, perm, n, width, seq_ref,
+                     crow, err);
   return hipGetLastError();
 }
 

@@ -47,6 +47,11 @@ class SdhMatches(ctypes.Structure):
                 ("seq", ctypes.POINTER(ctypes.c_int64)), ("tb", ctypes.POINTER(ctypes.c_int64))]
 
 
+class SdhMatchesCompact(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("seq_base", ctypes.c_int64), ("width", ctypes.c_int32),
+                ("flags", ctypes.c_int32), ("rows", ctypes.POINTER(ctypes.c_int32))]
+
+
 class SdhStats(ctypes.Structure):
     _fields_ = [("events", ctypes.c_int64), ("pattern_events", ctypes.c_int64),
                 ("matches", ctypes.c_int64), ("live_partials", ctypes.c_int64),
@@ -59,6 +64,7 @@ class SdhStats(ctypes.Structure):
 
 
 EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engine_poll", "sdh_engine_poll_device",
+           "sdh_engine_poll_compact",
            "sdh_engine_pending_matches", "sdh_engine_start", "sdh_engine_advance_time", "sdh_engine_stats",
            "sdh_engine_snapshot", "sdh_engine_state_bytes",
            "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version",
@@ -83,6 +89,7 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_engine_flush.argtypes = [P]
     lib.sdh_engine_poll.argtypes = [P, ctypes.POINTER(SdhMatches)]
     lib.sdh_engine_poll_device.argtypes = [P, ctypes.POINTER(SdhMatches)]
+    lib.sdh_engine_poll_compact.argtypes = [P, ctypes.c_int32, ctypes.POINTER(SdhMatchesCompact)]
     lib.sdh_engine_pending_matches.argtypes = [P, ctypes.POINTER(ctypes.c_int64)]
     lib.sdh_engine_start.argtypes = [P, ctypes.c_int64]
     lib.sdh_engine_advance_time.argtypes = [P, ctypes.c_int64]
@@ -209,6 +216,17 @@ class HipEngine:
         m = SdhMatches()
         self._check(self.lib.sdh_engine_poll_device(self.h, ctypes.byref(m)))
         return m
+
+    def poll_compact(self, device: bool = False):
+        """The same matches as compact int32 rows (sdh_engine_poll_compact): (seq_base, rows[n, width])
+        on the host, or the SdhMatchesCompact struct (rows a device pointer) when device is set."""
+        m = SdhMatchesCompact()
+        self._check(self.lib.sdh_engine_poll_compact(self.h, int(device), ctypes.byref(m)))
+        if device:
+            return m
+        if m.n == 0:
+            return m.seq_base, np.zeros((0, m.width), np.int32)
+        return m.seq_base, np.ctypeslib.as_array(m.rows, shape=(m.n, m.width)).copy()
 
     def take_matches(self, n_slots_of):
         q, k, ts, off, words = self.poll()
