@@ -90,11 +90,9 @@ extern "C" hipError_t sdh_prefix_max(const int64_t* ts, int64_t n, int64_t* pm, 
                                      size_t temp_bytes, hipStream_t s);
 extern "C" hipError_t sdh_key_segments(const uint32_t* uniq, const int32_t* nruns, int64_t max_runs, int64_t n_keys,
                                        int32_t* kseg, hipStream_t s);
-extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, const int32_t* blk_count,
-                                        const int32_t* blk_group, int n_blocks, int64_t rows, const int32_t* out_rank,
-                                        int n_streams, int n_ranks, int64_t n_events, int32_t* cnt, void* temp,
-                                        size_t temp_bytes, const sdh::RatchetGroup* groups, int64_t seq_base,
-                                        int64_t seq_ref, int64_t row0, int width, int32_t* crow, hipStream_t s);
+extern "C" hipError_t sdh_digest_compact(const int32_t* crow, int width, int64_t row0, int64_t n, int64_t seq_ref,
+                                         unsigned long long* acc, hipStream_t s);
+extern "C" hipError_t sdh_place_scan(int32_t* cnt, int64_t cells, void* temp, size_t temp_bytes, hipStream_t s);
 extern "C" hipError_t sdh_compact_fill(const int32_t* crow, int width, int64_t rows, const int64_t* ts_log,
                                        int64_t seq_ref, int64_t* oq, int64_t* okey, int64_t* ots, int64_t* oseq,
                                        int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s);
@@ -828,14 +826,14 @@ struct sdh_engine {
   int r_blk_recs = 8192;
   int r_blocks_used = 0;             // of the last launch
   int64_t r_blk_taken = 0;           // blocks the last launch took (ring mode: may exceed r_blocks)
-  // direct R18 placement (matches.hip ratchet_place_kernel): the (event, query rank) count matrix
-  DevBuf<int32_t> p_cnt;            // direct placement: the (event, rank) count matrix
-  DevBuf<int32_t> d_place_rank;     // [query][stream] 1 + its rank among the stream's K_ratchet queries
-  std::vector<int> place_nr;        // [stream] K_ratchet queries reading it
+  // direct R18 placement (nfa_ratchet.hip PM): the (event, group cell) match counts, scanned
+  DevBuf<int32_t> p_cnt;
+  std::vector<int> place_cells;     // [stream] K_ratchet groups reading it (0: not placeable)
   // string dictionary ids -> (String.hashCode, UTF-16 length) of their text (sdh_engine_set_strings):
   // the fan-out order of partitions keyed by a string attribute
   std::unordered_map<int32_t, std::pair<int32_t, int64_t>> str_info;
-  bool r_placing = false;            //   the last K_ratchet launch wrote it (PLACE variant)
+  bool r_placing = false;            // the last K_ratchet launch placed its matches (compact rows)
+  int64_t r_place_row0 = 0;          //   from this row of pc_rows
   DevBuf<uint8_t> p_ptemp;
   int64_t r_seq_base = 0;            // seq of the last launch's first event
   std::vector<int32_t> r_blk_count;
@@ -989,6 +987,7 @@ void table_clear(sdh_engine* e) {
   e->mt.ck_n = 0;
   e->mt.max_run = 0;
   e->seq_ref = e->seq;
+  e->r_placing = false;  // (the placed rows are gone)
 }
 
 // chunk keys of rows [ck_n, r1): single-event rows (chunk = false), or the rows the chunk push in
@@ -1065,43 +1064,30 @@ const int32_t* fan_positions(sdh_engine* e, sdh_engine::Route& rt, const kg::LFa
   return f.pos.p;
 }
 
-// A normal-mode push places its K_ratchet matches directly (the PLACE variant counts them per
-// (event, rank) cell, the ranks being the stream's K_ratchet queries in R18 order: place_rank) when
-// the count matrix stays within 2^30 cells and the launch runs without the full-expiry re-run (the
-// PLACE variant's pop levels assume the chunked launch's deques; a full-expiry launch appends to
-// the table instead).
-bool ratchet_placeable(const sdh_engine* e, int stream, int64_t n_events, bool full) {
-  const int nr = e->place_nr[(size_t)stream];
-  return !(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) && !full && n_events > 0 && !e->ck.active &&
-         (double)n_events * nr <= (double)(1 << 30) && !getenv("SDH_NO_PLACE");
+// A normal-mode push places its K_ratchet matches directly (nfa_ratchet.hip PM: COUNT per (event,
+// group) cell, scan, WRITE as compact rows after the window's rows) when they are its only matches
+// -- the chain and K_gen launches ran first and produced none, and the window holds no table rows
+// --, the stream's groups are rank-ordered (place_cells), the cells stay within 2^30, the seqs of
+// the window within 2^31 of seq_ref, and the launch runs without the full-expiry scan.
+bool ratchet_placeable(const sdh_engine* e, int stream, int64_t seq_base, int64_t n_events, bool full) {
+  const int nc = e->place_cells[(size_t)stream];
+  return nc > 0 && !(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) && !full && n_events > 0 && !e->ck.active &&
+         e->device_matches == 0 && e->g_dev_matches == 0 && (e->mt.n == 0 || e->mt.placed) &&
+         (double)n_events * nc < (double)(1 << 30) && seq_base + n_events - e->seq_ref < INT32_MAX &&
+         !getenv("SDH_NO_PLACE");
 }
 
-// The last push's K_ratchet matches written straight to their R18 rows of the ABI outputs, after
-// the window's rows (matches.hip ratchet_place_kernel). False, with nothing written, when the launch
-// did not count them (ratchet_placeable) or the rows would pass 2^31: the caller appends to the
-// table instead.
-bool place_ratchet(sdh_engine* e, int stream, const int64_t* ts_col, int64_t seq_base, int64_t n_events) {
-  const int nr = e->place_nr[(size_t)stream];
-  const int64_t rows = e->r_matches, n0 = e->mt.n;
-  if (!e->r_placing || n0 + rows >= INT32_MAX || seq_base + n_events - e->seq_ref >= INT32_MAX) return false;
-  const int w = e->cw;
-  e->pc_rows.grow_keep((size_t)((n0 + rows) * w), (size_t)(n0 * w), e->stream);
-  // the window's event times: the compact rows carry seqs only
+// a placed push joins the window: its rows are already in pc_rows; the compact rows carry seqs
+// only, so the window keeps the pushed events' times (ts_log[seq - seq_ref])
+void place_commit(sdh_engine* e, const int64_t* ts_col, int64_t seq_base, int64_t n_events) {
+  e->mt.placed = true;
+  if (e->r_matches == 0) return;  // (rows reference their own push's events only)
   const int64_t t0 = seq_base - e->seq_ref;
   e->ts_log.grow_keep((size_t)(t0 + n_events), (size_t)t0, e->stream);
-  if (n_events)
-    HIPCHK(hipMemcpyAsync(e->ts_log.p + t0, ts_col, (size_t)n_events * 8, hipMemcpyDeviceToDevice, e->stream));
-  const int64_t cells = n_events * nr;
-  const size_t tb = sdh_place_temp_bytes(cells);
-  e->p_ptemp.ensure(tb);
-  HIPCHK(sdh_place_ratchet(e->d_rmatch.p, e->r_blk_recs, e->d_blk_count.p, e->d_blk_group.p, e->r_blocks_used, rows,
-                           e->d_place_rank.p, (int)e->prog.stream_types.size(), nr, n_events, e->p_cnt.p, e->p_ptemp.p,
-                           e->p_ptemp.n, e->d_rg.p, seq_base, e->seq_ref, n0, w, e->pc_rows.p, e->stream));
+  HIPCHK(hipMemcpyAsync(e->ts_log.p + t0, ts_col, (size_t)n_events * 8, hipMemcpyDeviceToDevice, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
-  e->mt.n += rows;
-  e->mt.placed = true;
+  e->mt.n += e->r_matches;
   ++e->stats.placed_pushes;
-  return true;
 }
 
 // placed rows -> general table rows (a later push of the window has other producers)
@@ -1299,10 +1285,18 @@ void launch(sdh_engine* e, int stream, const StreamBatch& B, const int64_t t01[2
 int ratchet_sim(const sdh::RatchetGroup& g);
 
 void ratchet_build(sdh_engine* e, std::vector<std::pair<RatchetPlan, int>>& plans) {
-  std::stable_sort(plans.begin(), plans.end(), [](const auto& a, const auto& b) {
+  // lanes: normal mode in receiver-rank order (a wave's lanes are then consecutive ranks, which the
+  // direct placement needs: place_cells); SDH_FLAG_DEVICE_MATCHES mode by `within`, so that similar
+  // warm-up windows share a wave (SDH_RATCHET_LANES=rank|within overrides)
+  const char* lo = getenv("SDH_RATCHET_LANES");
+  const bool by_rank = lo ? strcmp(lo, "rank") == 0 : !(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES);
+  const size_t ns = e->prog.stream_types.size();
+  auto rank = [&](const std::pair<RatchetPlan, int>& p) { return e->out_rank[(size_t)p.second * ns + p.first.stream]; };
+  std::stable_sort(plans.begin(), plans.end(), [&](const auto& a, const auto& b) {
     const auto sa = a.first.sig(), sb = b.first.sig();
     if (sa != sb) return sa < sb;
-    return a.first.within < b.first.within;  // similar warm-up windows share a wave
+    if (by_rank) return rank(a) < rank(b);
+    return a.first.within < b.first.within;
   });
   for (size_t i = 0; i < plans.size();) {
     size_t j = i;
@@ -1427,6 +1421,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
   }
   e->d_rtotal.ensure(1);
   (void)t01;
+  bool no_place = false;
   for (int attempt = 0; attempt < 40; ++attempt) {
     // out-of-order timestamps seen on this stream, or timestamps so extreme that `ts0 + within`
     // could wrap: exact per-entry expiry scan, no chunking
@@ -1477,10 +1472,10 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     e->d_ritems.ensure(n_items);
     HIPCHK(hipMemcpyAsync(e->d_ritems.p, e->ritems.data(), n_items * sizeof(RatchetItem),
                           hipMemcpyHostToDevice, e->stream));
-    // 8-B records address e2 by a 26-bit batch offset; larger batches, and placing launches (the
-    // record carries its pop level), use 16-B records
-    const bool placing = ratchet_placeable(e, stream, n, full);
-    const int wide = (n > ((int64_t)1 << 26) || placing) ? 1 : 0;
+    // 8-B records address e2 by a 26-bit batch offset; larger batches use 16-B records. A placing
+    // launch writes no records: COUNT, scan, WRITE (compact rows)
+    const bool placing = !no_place && ratchet_placeable(e, stream, B.seq_base, n, full);
+    const int wide = n > ((int64_t)1 << 26) ? 1 : 0;
     if (n > ((int64_t)1 << 32)) throw Error(SDH_E_INVALID, "batch larger than 2^32 events");
     e->d_rmatch.ensure((size_t)e->r_blocks * e->r_blk_recs * (wide ? 2 : 1));
     e->d_rspillA.ensure((size_t)n_items * e->rSC * WAVE);
@@ -1534,34 +1529,37 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.ring = ring ? 1 : 0;
     L.rec_total = e->d_rtotal.p;
     L.err = e->d_err.p;
+    const int nc = e->place_cells[(size_t)stream];
+    const int64_t cells = n * nc + 1;  // (+1: the scan's total)
     if (placing) {
-      const int nr = e->place_nr[(size_t)stream];
-      e->p_cnt.ensure((size_t)(n * nr));
-      HIPCHK(hipMemsetAsync(e->p_cnt.p, 0, (size_t)(n * nr) * 4, e->stream));
+      e->p_cnt.ensure((size_t)cells);
+      HIPCHK(hipMemsetAsync(e->p_cnt.p + cells - 1, 0, 4, e->stream));
       L.pcnt = e->p_cnt.p;
-      L.out_rank = e->d_place_rank.p;
-      L.n_ranks = nr;
-      L.n_streams = (int32_t)e->prog.stream_types.size();
+      L.n_cells = nc;
     }
     e->r_placing = false;
+    // one launch per (key kind, orientation, SIM form)
+    auto run = [&](const RatchetLaunch& L0) {
+      for (int i0 = 0; i0 < n_items;) {
+        const int g0 = e->ritems[i0].g;
+        const int kk = e->rg[g0].key_kind, xm = e->rg[g0].xmask, sim = lsim(g0);
+        int i1 = i0;
+        while (i1 < n_items && lkey(e->ritems[i1].g) == lkey(g0)) ++i1;
+        RatchetLaunch Ls = L0;
+        Ls.items = e->d_ritems.p + i0;
+        Ls.n_items = i1 - i0;
+        int nf = 0;
+        for (int i = i0; i < i1; ++i) nf = std::max(nf, ratchet_nf(e->rg[e->ritems[i].g]));
+        // spill regions are indexed by the item's position in its launch
+        Ls.spillA = e->d_rspillA.p + (size_t)i0 * e->rSC * WAVE;
+        Ls.lds_ts = e->d_rlts.p + (size_t)i0 * e->rML * WAVE;
+        Ls.spillB = any64 ? e->d_rspillB.p + (size_t)i0 * e->rSC * WAVE : nullptr;
+        HIPCHK(sdh_launch_ratchet(kk, xm, full, nf, full ? 0 : sim, e->rML, e->rSC, &Ls, e->stream));
+        i0 = i1;
+      }
+    };
     HIPCHK(hipEventRecord(e->ev0, e->stream));
-    for (int i0 = 0; i0 < n_items;) {
-      const int g0 = e->ritems[i0].g;
-      const int kk = e->rg[g0].key_kind, xm = e->rg[g0].xmask, sim = lsim(g0);
-      int i1 = i0;
-      while (i1 < n_items && lkey(e->ritems[i1].g) == lkey(g0)) ++i1;
-      RatchetLaunch Ls = L;
-      Ls.items = e->d_ritems.p + i0;
-      Ls.n_items = i1 - i0;
-      int nf = 0;
-      for (int i = i0; i < i1; ++i) nf = std::max(nf, ratchet_nf(e->rg[e->ritems[i].g]));
-      // spill regions are indexed by the item's position in its launch
-      Ls.spillA = e->d_rspillA.p + (size_t)i0 * e->rSC * WAVE;
-      Ls.lds_ts = e->d_rlts.p + (size_t)i0 * e->rML * WAVE;
-      Ls.spillB = any64 ? e->d_rspillB.p + (size_t)i0 * e->rSC * WAVE : nullptr;
-      HIPCHK(sdh_launch_ratchet(kk, xm, full, nf, full ? 0 : sim, e->rML, e->rSC, &Ls, e->stream));
-      i0 = i1;
-    }
+    run(L);
     HIPCHK(hipEventRecord(e->ev1, e->stream));
     int32_t errs[4], used = 0;
     HIPCHK(hipMemcpyAsync(errs, e->d_err.p, 16, hipMemcpyDeviceToHost, e->stream));
@@ -1591,11 +1589,45 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       e->r_blocks *= 2;
       continue;
     }
+    int64_t placed_rows = 0;
+    if (placing) {
+      // the (event, cell) counts -> each cell's first row; then the same items again, writing
+      e->p_ptemp.ensure(sdh_place_temp_bytes(cells));
+      HIPCHK(sdh_place_scan(e->p_cnt.p, cells, e->p_ptemp.p, e->p_ptemp.n, e->stream));
+      int32_t tot = 0;
+      HIPCHK(hipMemcpyAsync(&tot, e->p_cnt.p + cells - 1, 4, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipStreamSynchronize(e->stream));
+      placed_rows = tot;
+      const int64_t n0 = e->mt.n;
+      if (tot < 0 || n0 + placed_rows >= INT32_MAX) {  // (rows past 2^31: records for the table)
+        no_place = true;
+        continue;
+      }
+      e->pc_rows.grow_keep((size_t)((n0 + placed_rows) * e->cw), (size_t)(n0 * e->cw), e->stream);
+      RatchetLaunch W = L;
+      W.pcnt = nullptr;
+      W.pbase = e->p_cnt.p;
+      W.crow = e->pc_rows.p;
+      W.cw = e->cw;
+      W.row0 = n0;
+      e->r_place_row0 = n0;
+      W.seq_ref = e->seq_ref;
+      float ms2 = 0;
+      HIPCHK(hipEventRecord(e->ev0, e->stream));
+      run(W);
+      HIPCHK(hipEventRecord(e->ev1, e->stream));
+      HIPCHK(hipEventSynchronize(e->ev1));
+      HIPCHK(hipEventElapsedTime(&ms2, e->ev0, e->ev1));
+      ms += ms2;
+    }
     for (int g : gs) e->rcur[g] ^= 1;
     e->r_placing = placing;
     e->r_blk_taken = used;
     e->r_seq_base = B.seq_base;
-    if (ring) {  // counted, not collected
+    if (placing) {
+      e->r_blocks_used = 0;
+      e->r_matches = placed_rows;
+    } else if (ring) {  // counted, not collected
       unsigned long long tot = 0;
       HIPCHK(hipMemcpy(&tot, e->d_rtotal.p, 8, hipMemcpyDeviceToHost));
       e->r_blocks_used = 0;
@@ -3177,17 +3209,18 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
       bytes += e->stats.last_kernel_bytes;
       consumers += (int64_t)qs.size();
     }
-    launch_ratchet(e, stream, B, t01);
-    for (const auto& g : e->rg)
-      if (g.stream == stream) consumers += g.n_lanes;
-    ms += e->r_kernel_ms;
-    bytes += e->r_kernel_bytes;
+    // K_gen before K_ratchet: a push whose only matches are K_ratchet's places them directly
     double gms = 0, gbytes = 0;
     e->stats.last_gen_items = 0;
     e->stats.last_seq_items = 0;
     launch_gen(e, stream, B, &gms, &gbytes);
     ms += gms;
     bytes += gbytes;
+    launch_ratchet(e, stream, B, t01);
+    for (const auto& g : e->rg)
+      if (g.stream == stream) consumers += g.n_lanes;
+    ms += e->r_kernel_ms;
+    bytes += e->r_kernel_bytes;
   } catch (const std::exception& ex) {
     // kernels may already have advanced part of the state: the engine no longer mirrors the
     // reference, so every later call fails (restore a snapshot or recreate)
@@ -3214,12 +3247,12 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   e->seq += b->n;
   e->stats.events += b->n;
   // the push is committed; its matches join the device table (R18-sorted at poll), or, when they
-  // all come from K_ratchet, go straight to their R18 rows (no sort at poll)
+  // all come from K_ratchet, are already at their R18 rows (placed by the launch: no sort at poll)
   if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES)) {
     const bool only_ratchet = e->device_matches == 0 && e->g_dev_matches == 0;
-    const bool placeable = only_ratchet && !e->ck.active && (e->mt.n == 0 || e->mt.placed);
-    if (!(only_ratchet && e->r_matches == 0) &&
-        !(placeable && place_ratchet(e, stream, B.ts, B.seq_base, b->n))) {
+    if (e->r_placing) {
+      place_commit(e, B.ts, B.seq_base, b->n);
+    } else if (!(only_ratchet && e->r_matches == 0)) {
       placed_to_table(e);
       const int64_t n0 = e->mt.n;
       append_chain(e);
@@ -3602,22 +3635,31 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
       HIPCHK(hipMemcpy(e->d_ck_major.p, e->ck_major.data(), r1.size() * 4, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(e->d_ck_minor.p, e->ck_minor.data(), r1.size() * 4, hipMemcpyHostToDevice));
     }
-    // direct placement ranks: per stream its K_ratchet queries in R18 (out_rank) order
+    // direct placement cells: a stream qualifies when its K_ratchet groups, each in lane order, are
+    // consecutive runs of its K_ratchet queries in receiver-rank order (a placed push has no other
+    // producer); cell = the group's run position
     {
       const size_t ns = e->prog.stream_types.size();
-      std::vector<int32_t> pr(std::max<size_t>(1, nq_all * ns), 0);
-      e->place_nr.assign(ns, 0);
+      e->place_cells.assign(ns, 0);
+      for (auto& g : e->rg) g.cell = -1;
       for (size_t st = 0; st < ns; ++st) {
-        std::vector<int> qs;
-        for (const auto& g : e->rg)
-          if (g.stream == (int)st)
-            for (int l = 0; l < g.n_lanes; ++l) qs.push_back(g.qid[l]);
-        std::sort(qs.begin(), qs.end(), [&](int a, int b) { return e->out_rank[a * ns + st] < e->out_rank[b * ns + st]; });
-        for (size_t k = 0; k < qs.size(); ++k) pr[(size_t)qs[k] * ns + st] = (int32_t)k + 1;
-        e->place_nr[st] = (int)qs.size();
+        std::vector<int> gs;
+        for (int g = 0; g < (int)e->rg.size(); ++g)
+          if (e->rg[g].stream == (int)st && e->rg[g].n_lanes > 0) gs.push_back(g);
+        if (gs.empty()) continue;
+        auto rk = [&](int g, int l) { return e->out_rank[(size_t)e->rg[g].qid[l] * ns + st]; };
+        std::sort(gs.begin(), gs.end(), [&](int a, int b) { return rk(a, 0) < rk(b, 0); });
+        std::vector<int> ranks;
+        for (int g : gs)
+          for (int l = 0; l < e->rg[g].n_lanes; ++l) ranks.push_back(rk(g, l));
+        bool ok = true;
+        for (size_t k = 1; k < ranks.size(); ++k) ok = ok && ranks[k - 1] < ranks[k];
+        if (!ok) continue;
+        for (size_t c = 0; c < gs.size(); ++c) e->rg[gs[c]].cell = (int)c;
+        e->place_cells[st] = (int)gs.size();
       }
-      e->d_place_rank.ensure(pr.size());
-      HIPCHK(hipMemcpy(e->d_place_rank.p, pr.data(), pr.size() * 4, hipMemcpyHostToDevice));
+      if (!e->rg.empty())
+        HIPCHK(hipMemcpy(e->d_rg.p, e->rg.data(), e->rg.size() * sizeof(RatchetGroup), hipMemcpyHostToDevice));
     }
     std::vector<int32_t> qinfo(std::max<size_t>(1, 2 * nq_all), 0);
     for (size_t q = 0; q < nq_all; ++q) {
@@ -3763,8 +3805,11 @@ int sdh_engine_debug_digest(sdh_engine* e, uint64_t* out) {
     DevBuf<unsigned long long> acc;
     acc.ensure(2);
     HIPCHK(hipMemsetAsync(acc.p, 0, 16, e->stream));
-    HIPCHK(sdh_digest_ratchet(e->d_rmatch.p, e->r_blk_recs, e->r_wide, e->d_blk_count.p, e->d_blk_group.p, e->d_rg.p,
-                              e->r_seq_base, (int)e->r_blk_taken, acc.p, e->stream));
+    if (e->r_placing)  // the last push placed its matches: its compact rows
+      HIPCHK(sdh_digest_compact(e->pc_rows.p, e->cw, e->r_place_row0, e->r_matches, e->seq_ref, acc.p, e->stream));
+    else
+      HIPCHK(sdh_digest_ratchet(e->d_rmatch.p, e->r_blk_recs, e->r_wide, e->d_blk_count.p, e->d_blk_group.p, e->d_rg.p,
+                                e->r_seq_base, (int)e->r_blk_taken, acc.p, e->stream));
     d2h_sync(e, out, acc.p, 16);
     return SDH_OK;
   });

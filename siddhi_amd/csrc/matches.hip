@@ -113,69 +113,10 @@ __global__ __launch_bounds__(256) void digest_ratchet_kernel(const int64_t* __re
 }
 
 // ---- K_ratchet direct R18 placement (a push whose matches all come from K_ratchet) ----
-// R18 wants per event the queries in receiver-rank order and per query its partials in pending-list
-// order (e1 seq ascending = pop level descending, level 0 the newest partial). K_ratchet's PLACE
-// variant (nfa_ratchet.hip) stored each (event, query rank) cell's match count and each record's
-// pop level; an exclusive scan over the cells gives each cell's first row, and a record of level L
-// goes to
-//   P = row0 + base[cell] + count[cell] - 1 - L = row0 + base[cell + 1] - 1 - L.
-// One pass, no sort: each record becomes its row of the window's COMPACT rows (sdh_matches_compact,
-// `width` int32: query, e2 seq - seq_ref, per slot the trigger seq minus the slot's seq -- e2 - e1,
-// 0 -- then INT32_MIN for slots the engine's wider queries have), one 16-B store for width 4. The
-// ABI columns are built from them only when a poll asks for the full tuples (compact_fill_kernel).
-__global__ __launch_bounds__(256) void ratchet_place_kernel(
-    const int64_t* __restrict__ match, int blk_recs, const int32_t* __restrict__ blk_count,
-    const int32_t* __restrict__ blk_group, int64_t rows, const int32_t* __restrict__ out_rank, int n_streams,
-    int n_ranks, int64_t cells, const int32_t* __restrict__ base, const RatchetGroup* __restrict__ groups,
-    int64_t seq_base, int64_t seq_ref, int64_t row0, int width, int32_t* __restrict__ crow) {
-  __shared__ int32_t s_q[64], s_rank[64];
-  const int b = blockIdx.x;
-  const int n = blk_count[b];
-  const RatchetGroup* G = groups + blk_group[b];
-  if (threadIdx.x < 64) {
-    const int q = threadIdx.x < G->n_lanes ? G->qid[threadIdx.x] : 0;
-    s_q[threadIdx.x] = q;
-    s_rank[threadIdx.x] = out_rank[(int64_t)q * n_streams + G->stream] - 1;
-  }
-  __syncthreads();
-  const uint4* R = reinterpret_cast<const uint4*>(match) + (size_t)b * blk_recs;
-  // U records per thread in flight: their record loads, then their (dependent) count loads, issue
-  // back to back
-  constexpr int U = 4;
-  for (int i0 = threadIdx.x; i0 < n; i0 += U * blockDim.x) {
-    uint4 r[U];
-    int64_t next[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * blockDim.x;
-      r[u] = i < n ? R[i] : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t cell = (int64_t)r[u].x * n_ranks + s_rank[r[u].y & 63];
-      next[u] = cell + 1 < cells ? (int64_t)base[cell + 1] : rows;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (i0 + u * blockDim.x >= n) break;
-      const uint32_t off = r[u].x, lane = r[u].y & 63, q1 = r[u].z, level = r[u].w;
-      const int64_t P = row0 + next[u] - 1 - (int64_t)level;
-      const int64_t s = seq_base + (int64_t)off;
-      const int32_t d0 = (int32_t)((uint32_t)s - q1);  // e2 - e1 (< 2^31: the kernel's aged check)
-      const int32_t rel = (int32_t)(s - seq_ref);
-      int32_t* o = crow + P * width;
-      if (width == 4) {
-        *reinterpret_cast<int4*>(o) = make_int4(s_q[lane], rel, d0, 0);
-      } else {
-        o[0] = s_q[lane];
-        o[1] = rel;
-        o[2] = d0;
-        o[3] = 0;
-        for (int k = 4; k < width; ++k) o[k] = INT32_MIN;
-      }
-    }
-  }
-}
+// nfa_ratchet.hip's COUNT pass stores each (event, group) match total, an exclusive scan over them
+// (sdh_place_scan) gives each cell's first row, and the WRITE pass writes every match as its
+// COMPACT row (sdh_matches_compact) at its R18 row: no records, no sort. The ABI columns are built
+// from the compact rows only when a poll asks for the full tuples (compact_fill_kernel).
 
 // compact rows of a placed window (K_ratchet: two one-event slots) -> the ABI columns of rows
 // [0, rows): words {1, e1, 1, e2} per row, ts from the window's event-time log (ts_log[seq - seq_ref])
@@ -457,29 +398,42 @@ extern "C" hipError_t sdh_digest_ratchet(const int64_t* match, int blk_recs, int
   return hipGetLastError();
 }
 
-// Direct R18 placement of the last push's K_ratchet blocks at rows row0.. of the ABI outputs (see
-// ratchet_place_kernel). cnt: n_events * n_ranks int32 (zeroed here, scanned in place).
+// the same order-independent digest over placed compact rows [row0, row0 + n) (a placed push)
+__global__ __launch_bounds__(256) void digest_compact_kernel(const int32_t* __restrict__ crow, int width, int64_t row0,
+                                                             int64_t n, int64_t seq_ref, unsigned long long* acc) {
+  unsigned long long h = 0, c = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t* r = crow + (row0 + i) * width;
+    const int64_t s = seq_ref + (int64_t)r[1], s1 = s - (int64_t)r[2];
+    h += sdh::mix64(sdh::mix64((uint64_t)s * 0x9E3779B97F4A7C15ull ^ (uint64_t)(int64_t)r[0]) ^ (uint64_t)s1);
+    ++c;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    h += __shfl_down(h, o);
+    c += __shfl_down(c, o);
+  }
+  if ((threadIdx.x & 63) == 0 && c) {
+    atomicAdd(&acc[0], c);
+    atomicAdd(&acc[1], h);
+  }
+}
+extern "C" hipError_t sdh_digest_compact(const int32_t* crow, int width, int64_t row0, int64_t n, int64_t seq_ref,
+                                         unsigned long long* acc, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(digest_compact_kernel, dim3(1024), dim3(256), 0, s, crow, width, row0, n, seq_ref, acc);
+  return hipGetLastError();
+}
+
+// Direct R18 placement: scratch bytes of the scan over `cells` (event, group) counts, and the
+// exclusive scan itself (in place)
 extern "C" size_t sdh_place_temp_bytes(int64_t cells) {
   size_t b = 0;
   (void)hipcub::DeviceScan::ExclusiveSum((void*)nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, (int)cells);
   return b + 256;
 }
-// cnt: the (event, rank) match counts K_ratchet's PLACE variant stored (scanned in place); the
-// records become compact rows row0.. of crow (width int32 each)
-extern "C" hipError_t sdh_place_ratchet(const int64_t* match, int blk_recs, const int32_t* blk_count,
-                                        const int32_t* blk_group, int n_blocks, int64_t rows, const int32_t* out_rank,
-                                        int n_streams, int n_ranks, int64_t n_events, int32_t* cnt, void* temp,
-                                        size_t temp_bytes, const sdh::RatchetGroup* groups, int64_t seq_base,
-                                        int64_t seq_ref, int64_t row0, int width, int32_t* crow, hipStream_t s) {
-  using namespace sdh;
-  if (n_blocks <= 0) return hipSuccess;
-  const int64_t cells = n_events * n_ranks;
+extern "C" hipError_t sdh_place_scan(int32_t* cnt, int64_t cells, void* temp, size_t temp_bytes, hipStream_t s) {
   size_t tb = temp_bytes;
-  hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, tb, cnt, cnt, (int)cells, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(ratchet_place_kernel, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, blk_count, blk_group,
-                     rows, out_rank, n_streams, n_ranks, cells, cnt, groups, seq_base, seq_ref, row0, width, crow);
-  return hipGetLastError();
+  return hipcub::DeviceScan::ExclusiveSum(temp, tb, cnt, cnt, (int)cells, s);
 }
 
 // the ABI columns of a placed window's compact rows (po_* arrays; off has rows + 1 entries)

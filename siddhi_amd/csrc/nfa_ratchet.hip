@@ -416,10 +416,16 @@ __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {  // b >= 0
 // event key against per-lane float bounds, and NaN keys fail every compare by themselves, so the
 // per-event validity bits are not read; an empty deque's top key is NaN, so the match test needs no
 // length check; a non-pushing lane writes its LDS entry to a dummy row instead of branching.
-// PLACE (normal-mode pushes that qualify for the direct R18 placement, matches.hip): 16-B records
-// carry the record's pop level at its event, and every (event, lane) with matches stores its match
-// count into the (event, receiver rank) count matrix -- one plain store per cell, no atomics
-template <int KK, int XM, bool FULL, int NF, bool SIM = false, bool PLACE = false>
+// PM (normal-mode pushes that qualify for the direct R18 placement; RatchetLaunch): 0 = match
+// records in per-wave blocks; 1 = COUNT, each (event, group) match total only (one coalesced store
+// per 64-event tile); 2 = WRITE, the same step again writing every match as its compact row at its
+// final R18 row. A lane's rows at an event are consecutive and the group's lanes hold consecutive
+// ranks, so a row is base(event, group) + the matches of the lower lanes + the lane's count - 1 -
+// the pop level; the count is known before the first pop: the first round's four compares give it
+// unless a lane popped all four or ran through its LDS entries, and then a walk down the deque
+// counts the rest (keys are monotone along it). The lower lanes' matches are mbcnt over the first
+// round's ballots, a wave scan in the rare walk case.
+template <int KK, int XM, bool FULL, int NF, bool SIM = false, int PM = 0>
 // occupancy: the general forms at 7 waves per SIMD (72 VGPRs), the SIM form at 8 (64 VGPRs, a few
 // spills; the LDS rings allow 8 at ML = 8). SIM at 10K C2 patterns: 7 waves 167.9 ms, 8 waves 156.1
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7))) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
@@ -751,10 +757,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
   // by mbcnt. e2 =
   // batch event `off`; e1 = the partial with low seq bits q1. The common case costs one
   // compare-and-branch of bookkeeping (the record index is block base + fill + rank).
-  int32_t* const pcell = PLACE && active ? L.pcnt + (L.out_rank[(int64_t)G->qid[lane] * L.n_streams + G->stream] - 1)
-                                         : nullptr;
-  uint32_t lv = 0;  // PLACE: the lane's records at the current event so far (the next one's level)
+  const int32_t my_q = active ? G->qid[lane] : 0;
+  const int cell = G->cell;
+  int ev_tot = 0;     // COUNT: the wave's matches at the current event
+  int32_t cntv = 0;   // COUNT: lane k = the matches at tile event k
+  int32_t basev = 0;  // WRITE: lane k = the group's first row at tile event k
+  int64_t pos = 0;    // WRITE: the lane's last row at the current event
+  uint32_t lv = 0;    // WRITE: the lane's rows at the current event so far (the next one's level)
+  auto put_row = [&](int64_t row, uint32_t off, uint32_t q1) {
+    const int64_t s = seq_base + (int64_t)off;
+    int32_t* o = L.crow + row * L.cw;
+    const int32_t rel = (int32_t)(s - L.seq_ref), d0 = (int32_t)((uint32_t)s - q1);
+    if (L.cw == 4) {
+      *reinterpret_cast<int4*>(o) = make_int4(my_q, rel, d0, 0);
+    } else {
+      o[0] = my_q;
+      o[1] = rel;
+      o[2] = d0;
+      o[3] = 0;
+      for (int j = 4; j < L.cw; ++j) o[j] = INT32_MIN;
+    }
+  };
   auto emit = [&](bool mt, uint64_t m, uint32_t off, uint32_t q1) {
+    if constexpr (PM == 1) {
+      ev_tot += __popcll(m);
+      return;
+    }
+    if constexpr (PM == 2) {
+      if (mt) put_row(pos - (int64_t)lv, off, q1);
+      lv += mt ? 1u : 0u;
+      return;
+    }
     const int c = __popcll(m);
     if (fill + c > L.blk_recs) {
       if (mover) return;
@@ -779,10 +812,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     }
     if (mt) {
       const int r = fill + wave_mbcnt(m);
-      if (!PLACE && !L.wide) wb[r] = make_uint2(off | ((uint32_t)lane << 26), q1);
-      else reinterpret_cast<uint4*>(wb)[r] = make_uint4(off, (uint32_t)lane, q1, PLACE ? lv : 0u);
+      if (!L.wide) wb[r] = make_uint2(off | ((uint32_t)lane << 26), q1);
+      else reinterpret_cast<uint4*>(wb)[r] = make_uint4(off, (uint32_t)lane, q1, 0u);
     }
-    if constexpr (PLACE) lv += mt ? 1u : 0u;
     fill += c;
   };
 
@@ -809,6 +841,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     // sequence numbers are kept as their low 32 bits: a live partial must stay < 2^31 events old
     // (checked once per tile against the tile's last event; the bottom only gets younger)
     if (D.n() > 0 && (uint32_t)((uint32_t)(seq_base + t + cnt - 1) - bseq) >= 0x80000000u) aged = true;
+    if constexpr (PM == 1) cntv = 0;
+    if constexpr (PM == 2) basev = lane < cnt ? L.pbase[(int64_t)(t + lane) * L.n_cells + cell] : 0;
 
 #pragma unroll 1
     for (int k = 0; k < cnt; ++k) {
@@ -852,7 +886,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       // ---- 2. matches: the newest partials whose key satisfies `cur OP key` ----
       bool mt = SIM ? xop<KK, XM>(xmask, x, tkey) : (x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey));
       uint64_t m = __ballot(mt);
-      if constexpr (PLACE) lv = 0;
+      if constexpr (PM == 1) ev_tot = 0;
+      if constexpr (PM == 2) lv = 0;
+      bool round1 = true;
       while (m) {
         // the three LDS entries under the top, read unconditionally (in-bounds ring slots)
         const int topl = D.lbot + D.ln - 1;
@@ -865,6 +901,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
         const bool c2 = c1 && D.ln > 2 && xop<KK, XM>(xmask, x, k2);
         const bool c3 = c2 && D.ln > 3 && xop<KK, XM>(xmask, x, k3);
         const uint32_t off = (uint32_t)(t + k);
+        if constexpr (PM == 2) {
+          if (round1) {  // the lane's count at this event, then its last row
+            round1 = false;
+            const int p1 = (int)mt + (int)c1 + (int)c2 + (int)c3;
+            const bool more = mt && ((p1 == 4 && D.ln > 4) || (p1 == D.ln && D.sn > 0));
+            const int64_t base = L.row0 + (int64_t)__builtin_amdgcn_readlane(basev, k);
+            if (__ballot(more) == 0) {
+              const int below = wave_mbcnt(m) + wave_mbcnt(__ballot(c1)) + wave_mbcnt(__ballot(c2)) +
+                                wave_mbcnt(__ballot(c3));
+              pos = base + below + p1 - 1;
+            } else {
+              int cl = p1;
+              if (more) {  // walk on below the first four / into the spill ring
+                for (int d = p1;; ++d) {
+                  U kd;
+                  uint32_t qd;
+                  if (d < D.ln) {
+                    D.lget_ks(D.li(D.lbot + D.ln - 1 - d), kd, qd);
+                  } else if (d - D.ln < D.sn) {
+                    int64_t td;
+                    D.sget(D.si(D.sbot + D.sn - 1 - (d - D.ln)), td, kd, qd);
+                  } else {
+                    break;
+                  }
+                  if (!xop<KK, XM>(xmask, x, kd)) break;
+                  ++cl;
+                }
+              }
+              int incl = cl;  // inclusive scan over the lanes (rank order)
+#pragma unroll
+              for (int dd = 1; dd < WAVE; dd <<= 1) {
+                const int o = __shfl_up(incl, dd, WAVE);
+                incl += lane >= dd ? o : 0;
+              }
+              pos = base + incl - 1;
+            }
+          }
+        }
         emit(mt, m, off, tseq);
         const uint64_t m1 = __ballot(c1);
         if (m1) {
@@ -893,8 +967,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
         mt = SIM ? (fix && xop<KK, XM>(xmask, x, tkey)) : (fix && x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey));
         m = __ballot(mt);
       }
-      if constexpr (PLACE)
-        if (lv) pcell[(int64_t)(t + k) * L.n_ranks] = (int32_t)lv;  // (lanes with matches are active)
+      if constexpr (PM == 1) cntv = lane == k ? ev_tot : cntv;
 
       // ---- 3. start state: every event passing f0 opens a partial (pending from j+1) ----
       bool f;
@@ -929,6 +1002,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       tkey = push ? x : tkey;
       tseq = push ? slo : tseq;
     }
+    if constexpr (PM == 1)
+      if (lane < cnt) L.pcnt[(int64_t)(t + lane) * L.n_cells + cell] = cntv;
   }
 
   // ---- outputs ----
@@ -1030,7 +1105,12 @@ static void launch_one(const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t 
   const size_t lds = (size_t)(ML + (SIM ? 1 : 0)) * 64 * (w64 ? 16 : 8);  // (SIM: + the dummy row)
   if constexpr (!FULL) {
     if (L->pcnt) {
-      hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM, true>), dim3(L->n_items), dim3(64), lds, s, *L,
+      hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM, 1>), dim3(L->n_items), dim3(64), lds, s, *L,
+                         ML, SC);
+      return;
+    }
+    if (L->crow) {
+      hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM, 2>), dim3(L->n_items), dim3(64), lds, s, *L,
                          ML, SC);
       return;
     }

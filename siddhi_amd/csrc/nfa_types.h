@@ -157,6 +157,9 @@ struct RatchetGroup {
   int32_t n_f0;
   int32_t sum_slot;                       // row of the launch's per-tile x-summaries (host-set)
   int32_t sim;                            // the SIM kernel form applies (nfa_ratchet.hip; host-set)
+  int32_t cell;                           // direct placement: the group's position among its stream's
+                                          //   groups in receiver-rank order (host-set; -1: none)
+  int32_t pad_cell;
   RatchetAtom f0[RMAXF0];
   int64_t wmax;                           // max within over lanes (-1: none)
   int32_t qid[64];
@@ -209,11 +212,17 @@ struct RatchetLaunch {
                                 //   written, none is read back); rec_total counts them
   unsigned long long* rec_total;
   int32_t* err;                 // [0] deque overflow, [1] unordered ts, [2] match overflow
-  // direct R18 placement (non-null pcnt; wide records, w = the record's pop level at its event):
-  // pcnt[event * n_ranks + out_rank(query, stream) - 1] = the query's matches at that event
+  // direct R18 placement, two passes over the same items (nfa_ratchet.hip PM; the stream's groups
+  // hold consecutive receiver ranks in lane order, groups in `cell` order): COUNT stores each
+  // (event, group) match total at pcnt[event * n_cells + cell]; WRITE reads their exclusive scan
+  // (pbase, same layout) and writes every match as its compact row (cw int32: query, e2 - seq_ref,
+  // e2 - e1, 0, INT32_MIN...) at row row0 + pbase[cell] + the lane's rank-ordered offset + its
+  // count - 1 - pop level (R18: per event by rank, per query oldest partial first)
   int32_t* pcnt;
-  const int32_t* out_rank;
-  int32_t n_ranks, n_streams;
+  const int32_t* pbase;
+  int32_t* crow;
+  int64_t row0, seq_ref;
+  int32_t n_cells, cw;
 };
 
 // ------------------------------------------------------------------------------------------

@@ -136,11 +136,12 @@ def test_headline_config_golden():
 
 @pytest.mark.parametrize("mixed", [False, True])
 def test_direct_placement_equals_sort(mixed):
-    """Pushes whose matches all come from K_ratchet go straight to their R18 rows (matches.hip
-    ratchet_place_kernel, no sort at poll). Against the same pushes with placement off
-    (SDH_NO_PLACE: the device table + radix sort): identical poll output, over polls after one push
-    and after several (placed windows), and -- `mixed` -- with chain / K_gen queries whose rare
-    matches turn a placed window back into table rows (placed_to_table)."""
+    """Pushes whose matches all come from K_ratchet go straight to their R18 rows (nfa_ratchet.hip
+    COUNT + scan + WRITE passes, compact rows; no sort at poll). Against the same pushes with
+    placement off (SDH_NO_PLACE: match records, the device table + radix sort): identical poll
+    output, over polls after one push and after several (placed windows), and -- `mixed` -- with
+    chain / K_gen queries whose rare matches turn a placed window back into table rows
+    (placed_to_table)."""
     import os
     from siddhi_amd.engine import HipEngine
     from siddhi_amd.workloads import c2_app, stock_events
