@@ -554,13 +554,18 @@ def push_latency(args, sh, K, local):
     Event) / receive(Event[]) chunks, StreamJunction.java:376-389): host-resident events of 1, 64 and
     4,096, normal mode (every match polled to the host in R18 order). Median and p99 over 50 pushes
     after 5 warm-up pushes (4,096: 10 after 2; at 10K C2 patterns such a push carries ~17M matches),
-    continuing one stream."""
+    continuing one stream. A second engine fed the same pushes polls the compact rows instead
+    (sdh_engine_poll_compact to the host: 16 B per match instead of ~72; `compact_*`; workloads whose
+    matches the form cannot express report null)."""
+    from siddhi_amd.engine import EngineError
     from siddhi_amd.workloads import stock_events, txn_events
     eng = make_engine(args.workload, sh, K, local, 0, args.partials)
+    ceng = make_engine(args.workload, sh, K, local, 0, args.partials)
     gen = txn_events if args.workload == "c4" else stock_events
     out, lo = {}, 0
+    compact_ok = True
     for bs in (1, 64, 4096):
-        lat, plat, nm = [], [], 0
+        lat, plat, clat, nm = [], [], [], 0
         warm, reps = (5, 50) if bs < 4096 else (2, 10)
         for i in range(warm + reps):
             ts, a, b, c = gen(lo, bs, K)
@@ -570,19 +575,33 @@ def push_latency(args, sh, K, local):
             eng.push_columns(0, ts, cols)
             t1 = time.perf_counter()
             m = eng.poll()
+            t2 = time.perf_counter()
+            if compact_ok:
+                try:
+                    ceng.push_columns(0, ts, cols)
+                    _, rows = ceng.poll_compact()
+                    if len(rows) != len(m[0]):
+                        raise RuntimeError(f"poll_compact {len(rows)} rows, poll {len(m[0])} matches")
+                except EngineError:
+                    compact_ok = False
+            t3 = time.perf_counter()
             if i >= warm:
-                lat.append((time.perf_counter() - t0) * 1e3)
+                lat.append((t2 - t0) * 1e3)
                 plat.append((t1 - t0) * 1e3)
+                clat.append((t3 - t2) * 1e3)
                 nm += len(m[0])
         lat.sort()
         plat.sort()
+        clat.sort()
         # push: host batch in, NFA step, matches placed in HBM in R18 order; poll: the tuples copied
         # to host arrays (PCIe and host copies, ~72 B per match)
-        out[str(bs)] = {"median_ms": lat[len(lat) // 2], "p99_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))],
-                        "push_median_ms": plat[len(plat) // 2],
-                        "push_p99_ms": plat[min(len(plat) - 1, int(len(plat) * 0.99))],
-                        "matches_per_push": nm / len(lat)}
+        q = lambda v, f: v[min(len(v) - 1, int(len(v) * f))]
+        out[str(bs)] = {"median_ms": q(lat, 0.5), "p99_ms": q(lat, 0.99), "push_median_ms": q(plat, 0.5),
+                        "push_p99_ms": q(plat, 0.99), "matches_per_push": nm / len(lat),
+                        "compact_median_ms": q(clat, 0.5) if compact_ok else None,
+                        "compact_p99_ms": q(clat, 0.99) if compact_ok else None}
     eng.close()
+    ceng.close()
     return out
 
 
