@@ -1477,7 +1477,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     const bool placing = !no_place && ratchet_placeable(e, stream, B.seq_base, n, full);
     const int wide = n > ((int64_t)1 << 26) ? 1 : 0;
     if (n > ((int64_t)1 << 32)) throw Error(SDH_E_INVALID, "batch larger than 2^32 events");
-    e->d_rmatch.ensure((size_t)e->r_blocks * e->r_blk_recs * (wide ? 2 : 1));
+    e->d_rmatch.ensure((size_t)(e->r_blocks + 1) * e->r_blk_recs * (wide ? 2 : 1));  // (+ the spare block)
     e->d_rspillA.ensure((size_t)n_items * e->rSC * WAVE);
     e->d_rlts.ensure((size_t)n_items * e->rML * WAVE);
     bool any64 = false;

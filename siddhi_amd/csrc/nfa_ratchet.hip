@@ -35,6 +35,12 @@
 
 #include "nfa_types.h"
 
+#ifndef SDH_RATCHET_UNROLL
+#define SDH_RATCHET_UNROLL 1
+#endif
+#define SDH_PRAGMA(x) _Pragma(#x)
+#define SDH_UNROLL(n) SDH_PRAGMA(unroll n)
+
 namespace sdh {
 
 namespace {
@@ -416,8 +422,8 @@ __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {  // b >= 0
 // event key against per-lane float bounds, and NaN keys fail every compare by themselves, so the
 // per-event validity bits are not read; an empty deque's top key is NaN, so the match test needs no
 // length check; a non-pushing lane writes its LDS entry to a dummy row instead of branching.
-// PM (normal-mode pushes that qualify for the direct R18 placement; RatchetLaunch): 0 = match
-// records in per-wave blocks; 1 = COUNT, each (event, group) match total only (one coalesced store
+// PM (normal-mode pushes that qualify for the direct R18 placement; RatchetLaunch): 0 / 3 = 8-B /
+// 16-B match records in per-wave blocks; 1 = COUNT, each (event, group) match total only (one coalesced store
 // per 64-event tile); 2 = WRITE, the same step again writing every match as its compact row at its
 // final R18 row. A lane's rows at an event are consecutive and the group's lanes hold consecutive
 // ranks, so a row is base(event, group) + the matches of the lower lanes + the lane's count - 1 -
@@ -778,6 +784,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       for (int j = 4; j < L.cw; ++j) o[j] = INT32_MIN;
     }
   };
+  // record width: compile-time in the chunked forms (PM 3 = 16-B records), read at run time in FULL
+  const bool wide = FULL ? L.wide != 0 : PM == 3;
+  // the next output block, taken when a pop round could overrun the current one (every round pops
+  // at most 4 x 64 records: one check per round instead of one per ballot). Out of blocks, the wave
+  // writes on into the spare block past the last (never read: the host doubles the blocks and re-runs)
+  auto roll = [&]() {
+    if (blk >= 0) {
+      if (lane == 0) L.blk_count[blk] = fill;
+      n_emit += (unsigned long long)fill;
+    }
+    int nb = 0;
+    if (lane == 0) nb = atomicAdd(L.blk_next, 1);
+    nb = __builtin_amdgcn_readfirstlane(nb);
+    if (L.ring) nb = (int)((uint32_t)nb % (uint32_t)L.n_blocks);
+    if (nb >= L.n_blocks) {
+      mover = true;
+      blk = -1;
+      nb = L.n_blocks;
+    } else {
+      if (lane == 0) L.blk_group[nb] = W.g;
+      blk = nb;
+    }
+    fill = 0;
+    wb = reinterpret_cast<uint2*>(L.match) + ((size_t)nb * L.blk_recs << (wide ? 1 : 0));
+  };
+  auto emit_room = [&]() {
+    if constexpr (PM == 0 || PM == 3)
+      if (fill > L.blk_recs - 4 * WAVE) roll();
+  };
   auto emit = [&](bool mt, uint64_t m, uint32_t off, uint32_t q1) {
     if constexpr (PM == 1) {
       ev_tot += __popcll(m);
@@ -788,34 +823,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       lv += mt ? 1u : 0u;
       return;
     }
-    const int c = __popcll(m);
-    if (fill + c > L.blk_recs) {
-      if (mover) return;
-      if (blk >= 0) {
-        if (lane == 0) L.blk_count[blk] = fill;
-        n_emit += (unsigned long long)fill;
-      }
-      int nb = 0;
-      if (lane == 0) nb = atomicAdd(L.blk_next, 1);
-      nb = __builtin_amdgcn_readfirstlane(nb);
-      if (L.ring) nb = (int)((uint32_t)nb % (uint32_t)L.n_blocks);
-      if (nb >= L.n_blocks) {
-        blk = -1;
-        mover = true;
-        fill = FULL_FILL;
-        return;
-      }
-      if (lane == 0) L.blk_group[nb] = W.g;
-      blk = nb;
-      fill = 0;
-      wb = reinterpret_cast<uint2*>(L.match) + ((size_t)blk * L.blk_recs << (L.wide ? 1 : 0));
-    }
     if (mt) {
       const int r = fill + wave_mbcnt(m);
-      if (!L.wide) wb[r] = make_uint2(off | ((uint32_t)lane << 26), q1);
+      if (!wide) wb[r] = make_uint2(off | ((uint32_t)lane << 26), q1);
       else reinterpret_cast<uint4*>(wb)[r] = make_uint4(off, (uint32_t)lane, q1, 0u);
     }
-    fill += c;
+    fill += __popcll(m);
   };
 
   // ---- forward NFA step over the events this item emits for. Fast path: straight-line per
@@ -844,7 +857,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     if constexpr (PM == 1) cntv = 0;
     if constexpr (PM == 2) basev = lane < cnt ? L.pbase[(int64_t)(t + lane) * L.n_cells + cell] : 0;
 
-#pragma unroll 1
+    SDH_UNROLL(SDH_RATCHET_UNROLL)
     for (int k = 0; k < cnt; ++k) {
       const int64_t tt = readlane64(ets, k);
       const int64_t s = seq_base + t + k;
@@ -890,6 +903,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       if constexpr (PM == 2) lv = 0;
       bool round1 = true;
       while (m) {
+        emit_room();
         // the three LDS entries under the top, read unconditionally (in-bounds ring slots)
         const int topl = D.lbot + D.ln - 1;
         U k1, k2, k3;
@@ -1007,7 +1021,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
   }
 
   // ---- outputs ----
-  if (blk >= 0) {
+  if (blk >= 0 && (PM == 0 || PM == 3)) {
     if (lane == 0) L.blk_count[blk] = fill;
     n_emit += (unsigned long long)fill;
   }
@@ -1111,6 +1125,11 @@ static void launch_one(const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t 
     }
     if (L->crow) {
       hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM, 2>), dim3(L->n_items), dim3(64), lds, s, *L,
+                         ML, SC);
+      return;
+    }
+    if (L->wide) {
+      hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM, 3>), dim3(L->n_items), dim3(64), lds, s, *L,
                          ML, SC);
       return;
     }
