@@ -212,23 +212,51 @@ struct WaveOutT {
   // buffer. A call larger than the buffer's free room goes in rounds: each round places the lanes
   // (in lane order) whose words and records fit, then the buffer is flushed. Only a lane whose own
   // records exceed the whole buffer reserves globally, as LaneOut does.
+  // uw: every lane's records have the same, wave-uniform, word count (the word prefixes are then the
+  // record prefixes times it: 10 ballots instead of 23)
   template <class F>
-  __device__ void emit_n(int nl, int words, F&& fill) {
+  __device__ void emit_n(int nl, int words, F&& fill, bool uw = false) {
     const unsigned long long lt = below();
     const bool big = nl * words > CAPW || nl > CAPR;
     const int mtw = big ? 0 : nl * words, mnl = big ? 0 : nl;
     int wpre = 0, wtot = 0, rpre = 0;  // exclusive lane prefixes, total words (ballot bits)
+    if (uw) {
+      int rtot = 0;
 #pragma unroll
-    for (int b = 0; b < 13; ++b) {  // mtw <= CAPW
-      const unsigned long long mb = __ballot((mtw >> b) & 1);
-      wpre += __popcll(mb & lt) << b;
-      wtot += __popcll(mb) << b;
-    }
+      for (int b = 0; b < 10; ++b) {  // mnl <= CAPR
+        const unsigned long long mb = __ballot((mnl >> b) & 1);
+        rpre += __popcll(mb & lt) << b;
+        rtot += __popcll(mb) << b;
+      }
+      wpre = rpre * words;
+      wtot = rtot * words;
+    } else {
 #pragma unroll
-    for (int b = 0; b < 10; ++b) {  // mnl <= CAPR
-      const unsigned long long mb = __ballot((mnl >> b) & 1);
-      rpre += __popcll(mb & lt) << b;
+      for (int b = 0; b < 13; ++b) {  // mtw <= CAPW
+        const unsigned long long mb = __ballot((mtw >> b) & 1);
+        wpre += __popcll(mb & lt) << b;
+        wtot += __popcll(mb) << b;
+      }
+#pragma unroll
+      for (int b = 0; b < 10; ++b) {  // mnl <= CAPR
+        const unsigned long long mb = __ballot((mnl >> b) & 1);
+        rpre += __popcll(mb & lt) << b;
+      }
     }
+    place(nl, words, big, mtw, mnl, wpre, wtot, rpre, fill);
+  }
+  // one record of `words` (wave-uniform) words per active lane: the prefixes are mbcnt
+  template <class F>
+  __device__ void emit_u(int words, F&& fill) {
+    const unsigned long long act = active();
+    const bool big = words > CAPW;
+    const int me = __popcll(act & below()), n = __popcll(act);
+    place(1, words, big, big ? 0 : words, big ? 0 : 1, big ? 0 : me * words, big ? 0 : n * words, big ? 0 : me,
+          fill);
+  }
+  // the placement rounds of a call (see emit_n)
+  template <class F>
+  __device__ void place(int nl, int words, bool big, int mtw, int mnl, int wpre, int wtot, int rpre, F&& fill) {
     int wdone = 0, rdone = 0;  // (uniform) words / records of this call placed so far
     while (wdone < wtot) {
       const int used = ld(sh->used), nr = ld(sh->nrec);

@@ -308,7 +308,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
               const int64_t as = fb ? -1 : seq, bs = fb ? seq : -1;  // words: 7 + 2 + 2 + 1
               o.emit_n(n, 12, [&](int64_t* r0) {
                 tab.each(n, [&](int kk, const auto& e) { put_rec(r0 + kk * 12, 12, kk, e.get(1), as, bs); });
-              });
+              }, true);
             }
             n = 0;
           }
@@ -327,7 +327,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
                 const int64_t bseq = (filled && side == 2) ? e.get(2) : seq;
                 put_rec(r0 + kk * 13, 13, kk, e.get(1), aseq, bseq);
               });
-            });
+            }, true);
           }
           int w = 0;
           tab.each(n, [&](int kk, const auto& e) {

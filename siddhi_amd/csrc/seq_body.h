@@ -113,7 +113,7 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
     ++nrec;
     if (!L.write_records) return;
     const int words = 7 + 2 * S;
-    o.emit(words, [&](int64_t* r) {
+    o.emit_u(words, [&](int64_t* r) {  // (words are the wave's shape's)
       r[0] = words;
       r[1] = qid;
       r[2] = -1;
