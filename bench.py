@@ -264,8 +264,16 @@ def timed_steps(eng, step, warmup, steps, world, dist):
     for i in range(warmup):
         t = time.perf_counter()
         step(i)
-        log(f"warm-up step {i + 1}/{warmup}: {(time.perf_counter() - t) * 1e3:.1f} ms, last kernel "
-            f"{eng.stats().last_kernel_ms:.1f} ms")
+        dt = time.perf_counter() - t
+        mem = ""
+        if torch.cuda.is_available():
+            free, total = torch.cuda.mem_get_info()
+            mem = f", HBM used {(total - free) / 1e9:.1f} GB"
+            lb, rb, db = eng.state_bytes()
+            if rb:
+                mem += f" (slab live {lb / 1e9:.1f} GB, reserved {rb / 1e9:.1f} GB, directory {db / 1e9:.1f} GB)"
+        log(f"warm-up step {i + 1}/{warmup}: {dt * 1e3:.1f} ms, last kernel "
+            f"{eng.stats().last_kernel_ms:.1f} ms{mem}")
     kern_ms, kern_bytes, matches = [], [], 0
     pe0 = eng.stats().pattern_events
     if world > 1:
@@ -281,7 +289,12 @@ def timed_steps(eng, step, warmup, steps, world, dist):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    log(f"{steps} timed steps: {elapsed * 1e3 / steps:.2f} ms/step")
+    mem = ""
+    if torch.cuda.is_available():
+        free, total = torch.cuda.mem_get_info()
+        lb, rb, db = eng.state_bytes()
+        mem = f", HBM used {(total - free) / 1e9:.1f} GB" + (f" (slab live {lb / 1e9:.1f} GB, reserved {rb / 1e9:.1f} GB)" if rb else "")
+    log(f"{steps} timed steps: {elapsed * 1e3 / steps:.2f} ms/step{mem}")
     # (event, pattern) evaluations the engine performed: B x patterns for pattern-set shards, each
     # rank's own keys' events x patterns for key shards (sdh_stats.pattern_events)
     pe = float(eng.stats().pattern_events - pe0)

@@ -1,0 +1,13 @@
+#!/bin/bash
+# The bench lines of a round: the default (driver) command, then C3 / C4 / C5 with their CPU
+# baselines, each under its own time limit; logs in gpurun_out/line_<w>.log (copy to profiles/).
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u bench.py > gpurun_out/line_c2.log 2> gpurun_out/line_c2.err || { tail -20 gpurun_out/line_c2.err; exit 1; }
+tail -1 gpurun_out/line_c2.log | cut -c1-400
+for w in c3 c4; do
+  timeout -k 10 400 python -u bench.py --workload $w > gpurun_out/line_$w.log 2> gpurun_out/line_$w.err || { tail -20 gpurun_out/line_$w.err; exit 1; }
+  tail -1 gpurun_out/line_$w.log | cut -c1-300
+done
+timeout -k 10 600 python -u bench.py --workload c5 --no-expansion --no-latency --no-ingest > gpurun_out/line_c5.log 2> gpurun_out/line_c5.err || { tail -20 gpurun_out/line_c5.err; exit 1; }
+tail -1 gpurun_out/line_c5.log | cut -c1-300
