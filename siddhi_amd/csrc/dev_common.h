@@ -213,9 +213,9 @@ struct WaveOutT {
   // (in lane order) whose words and records fit, then the buffer is flushed. Only a lane whose own
   // records exceed the whole buffer reserves globally, as LaneOut does.
   // uw: every lane's records have the same, wave-uniform, word count (the word prefixes are then the
-  // record prefixes times it: 10 ballots instead of 23)
+  // record prefixes times it: rbits ballots -- nl < 2^rbits -- instead of 23)
   template <class F>
-  __device__ void emit_n(int nl, int words, F&& fill, bool uw = false) {
+  __device__ void emit_n(int nl, int words, F&& fill, bool uw = false, int rbits = 10) {
     const unsigned long long lt = below();
     const bool big = nl * words > CAPW || nl > CAPR;
     const int mtw = big ? 0 : nl * words, mnl = big ? 0 : nl;
@@ -224,6 +224,7 @@ struct WaveOutT {
       int rtot = 0;
 #pragma unroll
       for (int b = 0; b < 10; ++b) {  // mnl <= CAPR
+        if (b >= rbits) break;
         const unsigned long long mb = __ballot((mnl >> b) & 1);
         rpre += __popcll(mb & lt) << b;
         rtot += __popcll(mb) << b;

@@ -108,24 +108,36 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
   Row ra, rb;
   if (lo + lane < rows_end) fetch(lo + lane, ra);
   if (lane < S - 1 && lo + 64 + lane < rows_end) fetch(lo + 64 + lane, rb);
-  auto emit = [&](int s) {
+  const int words = 7 + 2 * S;  // (the wave's shape's)
+  auto put_rec = [&](int64_t* r, int s) {
     const Win wv{win + s * ROW};
+    r[0] = words;
+    r[1] = qid;
+    r[2] = -1;
+    r[3] = wv.base[(S - 1) * ROW];      // ts of the last event
+    r[4] = wv.base[(S - 1) * ROW + 1];  // the triggering event's seq
+    r[5] = 0;                               // one match per event per query
+    r[6] = S | (stream << 16);
+    for (int i = 0; i < S; ++i) {
+      r[7 + 2 * i] = 1;
+      r[8 + 2 * i] = wv.base[i * ROW + 1];
+    }
+  };
+  auto emit = [&](int s) {
     ++nrec;
     if (!L.write_records) return;
-    const int words = 7 + 2 * S;
-    o.emit_u(words, [&](int64_t* r) {  // (words are the wave's shape's)
-      r[0] = words;
-      r[1] = qid;
-      r[2] = -1;
-      r[3] = wv.base[(S - 1) * ROW];      // ts of the last event
-      r[4] = wv.base[(S - 1) * ROW + 1];  // the triggering event's seq
-      r[5] = 0;                               // one match per event per query
-      r[6] = S | (stream << 16);
-      for (int i = 0; i < S; ++i) {
-        r[7 + 2 * i] = 1;
-        r[8 + 2 * i] = wv.base[i * ROW + 1];
-      }
-    });
+    o.emit_u(words, [&](int64_t* r) { put_rec(r, s); });
+  };
+  // a lane's matches among 8 starts (mask m over s0 ..) in one collective call: its records are
+  // contiguous, start order; the record counts take 4 ballots
+  auto emit8 = [&](int s0, uint32_t m) {
+    const int nl = __popc(m);
+    nrec += nl;
+    if (!L.write_records || __ballot(nl > 0) == 0) return;
+    o.emit_n(nl, words, [&](int64_t* r0) {
+      int kk = 0;
+      for (uint32_t mm = m; mm; mm &= mm - 1, ++kk) put_rec(r0 + kk * words, s0 + __builtin_ctz(mm));
+    }, true, 4);
   };
   for (int64_t t0 = lo; t0 < hi; t0 += SEQ_TILE) {
     const int cnt = hi - t0 < SEQ_TILE ? (int)(hi - t0) : SEQ_TILE;
@@ -147,11 +159,7 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
           for (int u = 0; u < 8; ++u)
             m |= (Spec::match(k, q, ql, within, Win{win + (s0 + u) * ROW}) ? 1u : 0u) << u;
           if (cnt - s0 < 8) m &= (1u << (cnt - s0)) - 1u;
-          while (m) {
-            const int u = __builtin_ctz(m);
-            m &= m - 1;
-            emit(s0 + u);
-          }
+          emit8(s0, m);
         }
       } else {
         for (int s = 0; s < cnt; ++s)
