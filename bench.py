@@ -364,8 +364,10 @@ def main():
         if world > C5_NODE:
             raise SystemExit(f"--workload c5 models one {C5_NODE}-GPU node")
         B, K_gen = B * C5_NODE, K * C5_NODE
-        # `within 1 hour` of event time: the untimed warm-up covers an hour (the state's steady size)
-        args.warmup = max(args.warmup, -(-3_600_000 // B) + 1)
+        # `within 1 hour` of event time: the untimed warm-up covers an hour and a half -- the hour of
+        # partials plus the ones that expire lazily (at their key's next event) -- so the state and
+        # its slab rings have reached their steady size when the timed steps start
+        args.warmup = max(args.warmup, -(-5_400_000 // B) + 1)
         args.no_expansion = args.no_ingest = True  # (single-stream helpers)
     else:
         K_gen = K

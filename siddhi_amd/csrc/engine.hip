@@ -40,7 +40,9 @@ extern "C" hipError_t sdh_slab_move(uint64_t* dir, int64_t n_dir, int groups, co
                                     const unsigned long long* src_tail, int src_nsub, const unsigned long long* limit,
                                     const uint8_t* active, uint32_t* const* dst_ring, const int64_t* dst_cap,
                                     unsigned long long* dst_head, const unsigned long long* dst_tail, int dst_nsub,
-                                    int32_t* err, hipStream_t s);
+                                    int32_t* err, uint8_t* ring_err, hipStream_t s);
+extern "C" hipError_t sdh_slab_live_words_ring(const uint64_t* dir, int64_t n_dir, int groups, const int32_t* group_ew,
+                                               int nsub, unsigned long long* acc, hipStream_t s);
 extern "C" hipError_t sdh_slab_live_words(const uint64_t* dir, int64_t n_dir, int groups, const int32_t* group_ew,
                                           unsigned long long* acc, hipStream_t s);
 extern "C" hipError_t sdh_seq_tail(const sdh::StreamBatch* b, int64_t* tail, int32_t tail_len, int32_t new_tail_len,
@@ -1872,7 +1874,7 @@ bool slab_move_raw(sdh_engine* e, sdh_engine::SlabSet& ss, uint64_t* dir, uint32
                    const int64_t* src_cap, const unsigned long long* src_tail, int src_nsub,
                    const std::vector<unsigned long long>& limit, const std::vector<uint8_t>& active,
                    uint32_t* const* dst_ring, const int64_t* dst_cap, unsigned long long* dst_head,
-                   const unsigned long long* dst_tail, int dst_nsub) {
+                   const unsigned long long* dst_tail, int dst_nsub, std::vector<uint8_t>* ring_fail = nullptr) {
   DevBuf<unsigned long long> d_lim;
   DevBuf<uint8_t> d_act;
   d_lim.ensure(limit.size());
@@ -1883,11 +1885,20 @@ bool slab_move_raw(sdh_engine* e, sdh_engine::SlabSet& ss, uint64_t* dir, uint32
   }
   e->d_err.ensure(4);
   HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
+  DevBuf<uint8_t> d_rf;
+  if (ring_fail) {
+    d_rf.ensure(dst_nsub);
+    HIPCHK(hipMemsetAsync(d_rf.p, 0, dst_nsub, e->stream));
+  }
   HIPCHK(sdh_slab_move(dir, ss.key_cap * ss.n_groups, ss.n_groups, ss.d_group_ew.p, src_ring, src_cap, src_tail,
                        src_nsub, d_lim.p, active.empty() ? nullptr : d_act.p, dst_ring, dst_cap, dst_head, dst_tail,
-                       dst_nsub, e->d_err.p, e->stream));
+                       dst_nsub, e->d_err.p, ring_fail ? d_rf.p : nullptr, e->stream));
   int32_t err = 0;
   HIPCHK(hipMemcpyAsync(&err, e->d_err.p, 4, hipMemcpyDeviceToHost, e->stream));
+  if (ring_fail) {
+    ring_fail->assign(dst_nsub, 0);
+    HIPCHK(hipMemcpyAsync(ring_fail->data(), d_rf.p, dst_nsub, hipMemcpyDeviceToHost, e->stream));
+  }
   HIPCHK(hipStreamSynchronize(e->stream));
   return err == 0;
 }
@@ -1896,16 +1907,21 @@ bool slab_move_raw(sdh_engine* e, sdh_engine::SlabSet& ss, uint64_t* dir, uint32
 // so the extra memory is a batch's worth)
 void slab_grow(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int>& which,
                const std::vector<int64_t>& new_cap) {
+  // (up to 32 rings and 8 GB of new buffers at a time: old and new buffers coexist while a batch
+  // moves, and C5's rings reach GBs each -- 32 at a time took tens of GB on top of the state)
   const int BATCH = 32;
-  for (size_t b0 = 0; b0 < which.size(); b0 += BATCH) {
+  const int64_t BATCH_WORDS = (int64_t)2 << 30;
+  for (size_t b0 = 0, b1 = 0; b0 < which.size(); b0 = b1) {
     std::vector<uint32_t*> nring(ss.ring);
     std::vector<int64_t> ncap(ss.cap);
     std::vector<uint8_t> active(ss.nsub, 0);
-    for (size_t k = b0; k < std::min(which.size(), b0 + BATCH); ++k) {
-      const int r = which[k];
-      ncap[r] = (new_cap[k] + 3) & ~3ll;
+    int64_t words = 0;
+    for (b1 = b0; b1 < which.size() && b1 < b0 + BATCH && (b1 == b0 || words + new_cap[b1] <= BATCH_WORDS); ++b1) {
+      const int r = which[b1];
+      ncap[r] = (new_cap[b1] + 3) & ~3ll;
       nring[r] = ring_malloc(ncap[r]);
       active[r] = 1;
+      words += ncap[r];
     }
     DevBuf<uint32_t*> d_nr;
     DevBuf<int64_t> d_nc;
@@ -1935,49 +1951,88 @@ void slab_grow(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int>& w
     slab_upload_rings(ss);
     HIPCHK(hipMemcpy(ss.head.p, ss.h_head.data(), ss.nsub * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ss.tail.p, ss.h_tail.data(), ss.nsub * 8, hipMemcpyHostToDevice));
-    ss.growths += (int64_t)std::min<size_t>(BATCH, which.size() - b0);
+    ss.growths += (int64_t)(b1 - b0);
   }
 }
 
-// Room for the next push in every ring. A ring with less free room than twice what it took in the
-// last push is reclaimed: every block written before that push moves to its head (the blocks of
-// the last push are current, so the ring then holds live blocks only). A ring still short, or more
-// than 3/4 full, grows to 1.5x (or to what it needs).
+// Room for the next push in every ring. The rings are log-structured: a push appends the entries it
+// changes, the old copies die in place. A ring whose free room falls below its live words plus 1.25x
+// what it took in the last push is cleaned in place: every block written before that push moves to
+// its head (the blocks of the last push are current) -- the oldest quarter of it, mostly dead copies
+// -- while the moves still fit. A ring below 2x
+// (live + headroom) words moves its live blocks into a fresh buffer of 2.5x that. A push that still
+// overflows is undone and re-run with room for 1.25x its demand (re-runs cost time, never matches).
+// (C5: cleaning only when a push lacked room never fit in place -- the ring was full by then -- so
+// every cleaning reallocated; growing by the ring's span instead of its live words doubled the
+// reservation every other step and ran out of HBM.)
 // demand: words a failed push tried to take per ring (room for 1.25x that is made instead)
 void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int64_t>* demand = nullptr) {
   std::vector<int64_t> need(ss.nsub);
   std::vector<unsigned long long> limit(ss.nsub);
   std::vector<uint8_t> clean(ss.nsub, 0);
+  // live words per ring (one pass over the directory)
+  std::vector<unsigned long long> live(ss.nsub, 0);
+  {
+    DevBuf<unsigned long long> acc;
+    acc.ensure(ss.nsub);
+    HIPCHK(hipMemsetAsync(acc.p, 0, ss.nsub * 8, e->stream));
+    HIPCHK(sdh_slab_live_words_ring(ss.dir.p, ss.key_cap * ss.n_groups, ss.n_groups, ss.d_group_ew.p, ss.nsub, acc.p,
+                                    e->stream));
+    HIPCHK(hipMemcpyAsync(live.data(), acc.p, ss.nsub * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
   bool any = false;
   for (int r = 0; r < ss.nsub; ++r) {
     const int64_t alloc = (int64_t)(ss.h_head[r] - ss.h_push0[r]);
-    need[r] = std::max<int64_t>(2 * alloc, 4096);
+    need[r] = std::max<int64_t>(alloc + alloc / 4, 4096);
     if (demand) need[r] = std::max<int64_t>(need[r], (*demand)[r] + (*demand)[r] / 4);
     const int64_t used = (int64_t)(ss.h_head[r] - ss.h_tail[r]);
-    if (ss.cap[r] - used >= need[r]) continue;
-    limit[r] = ss.h_push0[r] > ss.h_tail[r] ? ss.h_push0[r] : ss.h_head[r];
+    // clean while the live blocks still fit at the head (the in-place move needs room for them)
+    if (ss.cap[r] - used >= need[r] + (int64_t)live[r]) continue;
+    // the oldest quarter of the ring (at least twice the headroom): mostly dead copies, so the move
+    // is small (SDH_SLAB_CLEAN=all: everything before the last push)
+    const unsigned long long cur = ss.h_push0[r] > ss.h_tail[r] ? ss.h_push0[r] : ss.h_head[r];
+    static const bool all = getenv("SDH_SLAB_CLEAN") && !strcmp(getenv("SDH_SLAB_CLEAN"), "all");
+    const unsigned long long span = (unsigned long long)std::max<int64_t>(2 * need[r], ss.cap[r] / 4);
+    limit[r] = all ? cur : std::min<unsigned long long>(cur, ss.h_tail[r] + span);
     clean[r] = 1;
     any = true;
   }
   std::vector<int> grow;
   std::vector<int64_t> gcap;
   if (any) {
-    const bool ok = slab_move_raw(e, ss, ss.dir.p, ss.d_ring.p, ss.d_cap.p, ss.tail.p, ss.nsub, limit, clean,
-                                  ss.d_ring.p, ss.d_cap.p, ss.head.p, ss.tail.p, ss.nsub);
+    // (a ring's blocks move within that ring, so rings succeed or fail on their own)
+    std::vector<uint8_t> fail;
+    (void)slab_move_raw(e, ss, ss.dir.p, ss.d_ring.p, ss.d_cap.p, ss.tail.p, ss.nsub, limit, clean, ss.d_ring.p,
+                        ss.d_cap.p, ss.head.p, ss.tail.p, ss.nsub, &fail);
     slab_heads(e, ss);
-    if (ok) {
-      for (int r = 0; r < ss.nsub; ++r)
-        if (clean[r]) ss.h_tail[r] = limit[r];
-      HIPCHK(hipMemcpy(ss.tail.p, ss.h_tail.data(), ss.nsub * 8, hipMemcpyHostToDevice));
-      ++ss.cleanings;
-    }
+    for (int r = 0; r < ss.nsub; ++r)
+      if (clean[r] && !fail[r]) ss.h_tail[r] = limit[r];
+    HIPCHK(hipMemcpy(ss.tail.p, ss.h_tail.data(), ss.nsub * 8, hipMemcpyHostToDevice));
+    ++ss.cleanings;
+    // a ring below 2x (live + headroom) cannot clean in place for long: a fresh buffer of 2.5x that
+    // takes its live blocks (slab_grow compacts as it moves; sized from the live words, not the
+    // ring's span, which counts dead blocks: sizing from the span doubled the reservation every
+    // other C5 step and ran out of HBM)
     for (int r = 0; r < ss.nsub; ++r) {
       if (!clean[r]) continue;
       const int64_t used = (int64_t)(ss.h_head[r] - ss.h_tail[r]);
-      if (ok && ss.cap[r] - used >= need[r] && 4 * used <= 3 * ss.cap[r]) continue;
+      const int64_t want = 2 * ((int64_t)live[r] + need[r]);
+      if (!fail[r] && ss.cap[r] - used >= need[r] && ss.cap[r] >= want) continue;
       grow.push_back(r);
-      gcap.push_back(std::max<int64_t>(ss.cap[r] + ss.cap[r] / 2, 3 * (used + need[r]) / 2));
+      gcap.push_back(std::max<int64_t>(ss.cap[r], want + want / 4));
     }
+  }
+  if (getenv("SDH_SLAB_TRACE")) {
+    int64_t c = 0, u = 0, nd = 0, g = 0;
+    for (int r = 0; r < ss.nsub; ++r) {
+      c += ss.cap[r];
+      u += (int64_t)(ss.h_head[r] - ss.h_tail[r]);
+      nd += need[r];
+    }
+    for (int64_t x : gcap) g += x;
+    fprintf(stderr, "[sdh] slab prepare: %d rings, cap %.2f GB, used %.2f GB, need %.2f GB, demand %d, grow %zu rings to %.2f GB\n",
+            ss.nsub, c * 4e-9, u * 4e-9, nd * 4e-9, demand ? 1 : 0, grow.size(), g * 4e-9);
   }
   if (!grow.empty()) slab_grow(e, ss, grow, gcap);
   ss.h_push0 = ss.h_head;

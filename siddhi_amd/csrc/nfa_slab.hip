@@ -20,6 +20,8 @@
 // oldest half to its head (slab_move_kernel), or by moving everything into a larger slab.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdlib>
 
 #include "dev_common.h"
@@ -359,7 +361,7 @@ struct SlabRings {
 };
 __global__ void slab_move_kernel(uint64_t* dir, int64_t n_dir, int groups, const int32_t* __restrict__ group_ew,
                                  SlabRings src, const unsigned long long* limit, const uint8_t* active, SlabRings dst,
-                                 int32_t* err) {
+                                 int32_t* err, uint8_t* ring_err) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (x >= n_dir) return;
   const uint64_t d = dir[x];
@@ -376,6 +378,7 @@ __global__ void slab_move_kernel(uint64_t* dir, int64_t n_dir, int groups, const
   const int64_t o = ring_alloc(dst.head, dst.tail[ds], dst.cap[ds], ds, words);
   if (o < 0) {
     atomicOr(err, 1);
+    if (ring_err) ring_err[ds] = 1;  // (which destination ring ran out of room)
     return;
   }
   const uint32_t* from = src.ring[ss] + rel;
@@ -398,7 +401,35 @@ __global__ void slab_live_words_kernel(const uint64_t* dir, int64_t n_dir, int g
   if ((threadIdx.x & 63) == 0 && w) atomicAdd(acc, w);
 }
 
+// live words per sub-ring (acc[nsub]): a block-local histogram in LDS, one atomic per ring per block
+__global__ __launch_bounds__(256) void slab_live_words_ring_kernel(const uint64_t* dir, int64_t n_dir, int groups,
+                                                                   const int32_t* group_ew, int nsub,
+                                                                   unsigned long long* acc) {
+  extern __shared__ unsigned long long hist[];
+  for (int i = threadIdx.x; i < nsub; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n_dir; x += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t d = dir[x];
+    const int n = (int)((d >> 40) & 0xffff);
+    if (n)
+      atomicAdd(&hist[nsub == 1 ? 0u : sub_of((uint64_t)x, nsub)],
+                (unsigned long long)(((int64_t)n * group_ew[x % groups] + 3) & ~3ll));
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nsub; i += blockDim.x)
+    if (hist[i]) atomicAdd(&acc[i], hist[i]);
+}
+
 }  // namespace sdh
+
+extern "C" hipError_t sdh_slab_live_words_ring(const uint64_t* dir, int64_t n_dir, int groups, const int32_t* group_ew,
+                                               int nsub, unsigned long long* acc, hipStream_t s) {
+  if (n_dir <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>(2048, (n_dir + 255) / 256);
+  hipLaunchKernelGGL(sdh::slab_live_words_ring_kernel, dim3((unsigned)blocks), dim3(256), (size_t)nsub * 8, s, dir,
+                     n_dir, groups, group_ew, nsub, acc);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t sdh_launch_slab(const sdh::SlabLaunch* L, hipStream_t s) {
   if (L->n_items <= 0) return hipSuccess;
@@ -429,12 +460,12 @@ extern "C" hipError_t sdh_slab_move(uint64_t* dir, int64_t n_dir, int groups, co
                                     const unsigned long long* src_tail, int src_nsub, const unsigned long long* limit,
                                     const uint8_t* active, uint32_t* const* dst_ring, const int64_t* dst_cap,
                                     unsigned long long* dst_head, const unsigned long long* dst_tail, int dst_nsub,
-                                    int32_t* err, hipStream_t s) {
+                                    int32_t* err, uint8_t* ring_err, hipStream_t s) {
   if (n_dir <= 0) return hipSuccess;
   const sdh::SlabRings S{src_ring, src_cap, nullptr, src_tail, src_nsub};
   const sdh::SlabRings D{dst_ring, dst_cap, dst_head, dst_tail, dst_nsub};
   hipLaunchKernelGGL(sdh::slab_move_kernel, dim3((unsigned)((n_dir + 255) / 256)), dim3(256), 0, s, dir, n_dir, groups,
-                     group_ew, S, limit, active, D, err);
+                     group_ew, S, limit, active, D, err, ring_err);
   return hipGetLastError();
 }
 
