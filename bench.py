@@ -225,6 +225,17 @@ KERNEL_SOURCES = {  # what a kernel's code and launch configuration are built fr
 }
 
 
+def build_provenance():
+    """The source hash the loaded libsiddhi_hip.so was built from (sdh_build_info) against the hash of
+    the tree's sources (siddhi_amd/csrc/src_hash.py): equal when the library matches this tree."""
+    from siddhi_amd.engine import load_library
+    sys.path.insert(0, os.path.join(ROOT, "siddhi_amd", "csrc"))
+    from src_hash import src_hash
+    info = load_library().sdh_build_info().decode()
+    tree = src_hash(os.path.join(ROOT, "siddhi_amd", "csrc"))
+    return {"lib": info, "tree_src_hash": tree, "lib_matches_tree": info.split()[1] == tree}
+
+
 def source_hash(kernel=None):
     """Hash of the sources `kernel` is built from (all kernel sources when None); a committed profile
     is attached to the bench line only at an equal hash."""
@@ -537,6 +548,7 @@ def main():
         log("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(args.workload, K, args.cpu_seconds)
     if rank == 0:
+        result["build"] = build_provenance()
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

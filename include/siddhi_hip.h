@@ -15,6 +15,9 @@
  *                          query/input/StateMultiProcessStreamReceiver.java:65-72 (hand-off of each
  *                          completed StateEvent to QuerySelector.process)
  *   sdh_engine_poll_device  the same matches left in HBM (device consumers of the matches)
+ *   sdh_engine_poll_compact the same matches as 16-B compact rows (host or HBM)
+ *   sdh_engine_set_strings  <- partition/PartitionStreamReceiver.java:277-281 (String.valueOf of a
+ *                          string key: its hashCode / length, for the fan-out order)
  *   sdh_engine_flush    <- (no reference equivalent: the reference is synchronous)
  *   sdh_engine_snapshot / sdh_engine_restore
  *                       <- state/StreamPreStateProcessor.java:352-367 (currentState/restoreState)
@@ -230,6 +233,9 @@ int sdh_engine_debug_digest(sdh_engine* e, uint64_t* out);
 int sdh_calibrate_hbm(int32_t device, int64_t bytes, int32_t iters, double* copy_gbps, double* read_gbps);
 /* Library version / build info string (static storage). */
 const char* sdh_version(void);
+/* "src <hash> gfx950": the hash of the engine sources the library was built from
+ * (siddhi_amd/csrc/src_hash.py), for checking that a deployed .so matches its source tree. */
+const char* sdh_build_info(void);
 
 #ifdef __cplusplus
 }

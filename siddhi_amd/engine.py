@@ -68,7 +68,7 @@ EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engi
            "sdh_engine_pending_matches", "sdh_engine_start", "sdh_engine_advance_time", "sdh_engine_stats",
            "sdh_engine_snapshot", "sdh_engine_state_bytes",
            "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version",
-           "sdh_engine_debug_digest", "sdh_engine_set_strings", "sdh_calibrate_hbm"]
+           "sdh_engine_debug_digest", "sdh_engine_set_strings", "sdh_calibrate_hbm", "sdh_build_info"]
 
 _lib = None
 
@@ -103,6 +103,7 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_last_error.argtypes = [P]
     lib.sdh_last_error.restype = ctypes.c_char_p
     lib.sdh_version.restype = ctypes.c_char_p
+    lib.sdh_build_info.restype = ctypes.c_char_p
     lib.sdh_engine_debug_digest.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
     lib.sdh_engine_set_strings.argtypes = [P, ctypes.c_int64, P, P, P]
     D = ctypes.POINTER(ctypes.c_double)
