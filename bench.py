@@ -427,9 +427,9 @@ def main():
                         bcast_into(t)
                 engine.push_device(si, B, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
                 if len(per_stream) > 1 or i >= args.warmup:
-                    st = engine.stats()
-                    ms += st.last_kernel_ms
-                    by += st.last_kernel_bytes
+                    kms, kby = engine.push_stats()  # (no device work inside the timed steps)
+                    ms += kms
+                    by += kby
                     nm += engine.pending_matches()
             return ms, by, nm
         return step

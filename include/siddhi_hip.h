@@ -203,6 +203,10 @@ int sdh_engine_pending_matches(sdh_engine* e, int64_t* n);
 int sdh_engine_start(sdh_engine* e, int64_t t);
 int sdh_engine_advance_time(sdh_engine* e, int64_t t);
 int sdh_engine_stats(sdh_engine* e, sdh_stats* out);
+/* The last push's device time and algorithmic bytes (sdh_stats.last_kernel_ms / last_kernel_bytes)
+ * without the rest: no device work and no synchronisation (sdh_engine_stats counts the live partials
+ * on the device), for per-push instrumentation. */
+int sdh_engine_push_stats(sdh_engine* e, double* last_kernel_ms, double* last_kernel_bytes);
 /* Device memory of the sparse per-partial state (K_slab: partitioned distinct-stream patterns,
  * state only for instances that hold partials -- PartitionRuntime.java:257-306 clones per key
  * lazily): live entry bytes, reserved slab bytes, directory bytes. */

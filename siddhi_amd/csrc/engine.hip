@@ -3870,6 +3870,13 @@ int sdh_engine_debug_digest(sdh_engine* e, uint64_t* out) {
   });
 }
 
+int sdh_engine_push_stats(sdh_engine* e, double* last_kernel_ms, double* last_kernel_bytes) {
+  if (!e || !last_kernel_ms || !last_kernel_bytes) return SDH_E_INVALID;
+  *last_kernel_ms = e->stats.last_kernel_ms;  // (host-side values: no device work, no sync)
+  *last_kernel_bytes = e->stats.last_kernel_bytes;
+  return SDH_OK;
+}
+
 int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
   if (!e || !out) return SDH_E_INVALID;
   return guard(e, [&]() {

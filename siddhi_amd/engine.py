@@ -68,7 +68,8 @@ EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engi
            "sdh_engine_pending_matches", "sdh_engine_start", "sdh_engine_advance_time", "sdh_engine_stats",
            "sdh_engine_snapshot", "sdh_engine_state_bytes",
            "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version",
-           "sdh_engine_debug_digest", "sdh_engine_set_strings", "sdh_calibrate_hbm", "sdh_build_info"]
+           "sdh_engine_debug_digest", "sdh_engine_set_strings", "sdh_calibrate_hbm", "sdh_build_info",
+           "sdh_engine_push_stats"]
 
 _lib = None
 
@@ -104,6 +105,7 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_last_error.restype = ctypes.c_char_p
     lib.sdh_version.restype = ctypes.c_char_p
     lib.sdh_build_info.restype = ctypes.c_char_p
+    lib.sdh_engine_push_stats.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
     lib.sdh_engine_debug_digest.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
     lib.sdh_engine_set_strings.argtypes = [P, ctypes.c_int64, P, P, P]
     D = ctypes.POINTER(ctypes.c_double)
@@ -267,6 +269,13 @@ class HipEngine:
         s = SdhStats()
         self._check(self.lib.sdh_engine_stats(self.h, ctypes.byref(s)))
         return s
+
+    def push_stats(self):
+        """(last_kernel_ms, last_kernel_bytes) of the last push, with no device work
+        (sdh_engine_push_stats: stats() also counts the live partials on the device)."""
+        ms, by = ctypes.c_double(), ctypes.c_double()
+        self._check(self.lib.sdh_engine_push_stats(self.h, ctypes.byref(ms), ctypes.byref(by)))
+        return ms.value, by.value
 
     def debug_digest(self):
         """(records, order-independent hash) of the last push's K_ratchet records as written, in either
