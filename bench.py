@@ -14,18 +14,21 @@ B = 8M events; every match record is written to HBM (SDH_FLAG_DEVICE_MATCHES: co
 node's key shards).
 
 Multi-GPU (torchrun, one process per GPU). `--scaling strong` (default) measures the metric as
-defined, the whole node at 10K patterns: the P patterns are split over the N GPUs by pattern set
-(strided: rank r runs patterns r, r+N, ...; c3: the partition keys are split instead, rank r owning
-|String.valueOf(key).hashCode() % N| == r). `--scaling weak` gives every GPU P patterns; a strong N>1
-run appends that as a second line (`weak_scaling`). Rank 0 generates each batch and broadcasts it
-over RCCL (the event broadcast of SURVEY §8(e)) inside the timed region; the other ranks receive
-into zeroed buffers. `value` = pattern-events summed over ranks / the max over ranks of the timed
-region (barrier + device sync on both sides).
+defined, the whole node at 10K patterns: every rank's engine runs the full program as its shard
+(sdh_config.shard_rank / shard_world): the P patterns split by pattern set (rank r runs patterns r,
+r+N, ...; c3: the partition keys are split instead, rank r owning |String.valueOf(key).hashCode() % N|
+== r). `--scaling weak` gives every GPU P patterns of its own; a strong N>1 run appends that as a
+second line (`weak_scaling`). The exchange is the library's (include/siddhi_hip.h): an RCCL
+communicator (sdh_comm_create, its id handed out over torch.distributed's gloo control plane), rank
+0's device batch broadcast to every rank by sdh_engine_push_bcast inside the timed region.
+torch.distributed (gloo) carries only control: barriers, the max over ranks, the communicator id.
+`value` = pattern-events summed over ranks / the max over ranks of the timed region (barrier + device
+sync on both sides).
 
 Match expansion (`expansion` in the JSON line): a second engine in normal mode runs pushes of a
 smaller batch followed by sdh_engine_poll_device -- the device R18 sort and the gather of the ABI
-tuples (query, key, ts, off, words) in HBM; with N GPUs the tuples of every rank are then gathered to
-rank 0 over RCCL and k-way merged there (siddhi_amd/dist.py), timed per matched tuple.
+tuples (query, key, ts, off, words) in HBM; with N GPUs sdh_engine_gather instead: every rank's
+R18-ordered tuples go to rank 0 over RCCL and are merged there on the device, timed per step.
 """
 import argparse
 import glob
@@ -82,34 +85,34 @@ def app_source(workload, n, first, step=1):
 
 
 class Shard:
-    """This rank's share of a workload: the patterns first, first+step, ... (n of them) and, for key
-    sharding, (rank, world) of the partition keys (sdh_config.shard_rank / shard_world)."""
+    """This rank's share of a workload. The engine compiles patterns first, first+step, ... (n_prog of
+    them) and runs the shard (rank, world) of that program (sdh_config.shard_rank / shard_world):
+    patterns q % world == rank, and partition keys with |String.valueOf(key).hashCode() % world| ==
+    rank. `n` = the patterns this GPU evaluates."""
 
     def __init__(self, workload, scaling, P, rank, world):
         self.keyed = (workload == "c5") or (workload == "c3" and scaling == "strong")
+        self.first, self.step, self.n_prog = 0, 1, P
         if workload == "c5":
-            self.first, self.step, self.n, self.key_shard = 0, 1, P, (rank, C5_NODE)
+            self.n, self.key_shard = P, (rank, C5_NODE)
         elif scaling == "weak":
-            self.first, self.step, self.n, self.key_shard = rank * P, 1, P, (0, 1)
+            self.first, self.n, self.key_shard = rank * P, P, (0, 1)
         elif workload == "c3":
-            self.first, self.step, self.n, self.key_shard = 0, 1, P, (rank, world)
-        else:  # pattern-set sharding, strided (balances the threshold / multiplier mix)
-            self.first, self.step, self.n, self.key_shard = rank, world, len(range(rank, P, world)), (0, 1)
-
-    def global_q(self, q):
-        """local query index (tensor) -> the full program's query index"""
-        return self.first + q * self.step
+            self.n, self.key_shard = P, (rank, world)
+        else:  # pattern-set sharding by the engine's rule (strided: balances the threshold mix)
+            self.n, self.key_shard = len(range(rank, P, world)), (rank, world)
 
 
 def make_engine(workload, sh, K, device, flags, partials):
     from siddhi_amd import ql
     from siddhi_amd.engine import HipEngine
     from siddhi_amd.planner import plan
-    blob = plan(ql.parse(app_source(workload, sh.n, sh.first, sh.step))).serialize()
+    blob = plan(ql.parse(app_source(workload, sh.n_prog, sh.first, sh.step))).serialize()
     kr, kw = sh.key_shard
     if workload == "c4":
         # a sequence instance holds at most one partial per state (R8): small pools
-        return HipEngine(blob, device=device, flags=flags, gen_pool_states=8, gen_pool_nodes=32, gen_list_cap=8)
+        return HipEngine(blob, device=device, flags=flags, gen_pool_states=8, gen_pool_nodes=32, gen_list_cap=8,
+                         shard_rank=kr, shard_world=kw)
     if workload == "c5":  # key sharding: every rank runs all patterns over its own accounts (K_slab)
         return HipEngine(blob, device=device, flags=flags, gen_max_keys=max(1024, 2 * K), shard_rank=kr,
                          shard_world=kw)
@@ -117,7 +120,7 @@ def make_engine(workload, sh, K, device, flags, partials):
         pools = [int(x) for x in os.environ.get("SDH_C3_POOLS", "32,128,32").split(",")]
         return HipEngine(blob, device=device, flags=flags, gen_pool_states=pools[0], gen_pool_nodes=pools[1],
                          gen_list_cap=pools[2], gen_max_keys=max(1024, 2 * K), shard_rank=kr, shard_world=kw)
-    return HipEngine(blob, device=device, partials=partials, flags=flags)
+    return HipEngine(blob, device=device, partials=partials, flags=flags, shard_rank=kr, shard_world=kw)
 
 
 def gen_batch(workload, start, n, K, dev):
@@ -325,14 +328,21 @@ def reduce_run(elapsed, matches, pe, live, world, dist, cdev):
 
 
 def launches_per_step(prof, prof_dir):
-    """Launches of the profiled kernel per bench step: its rocprof call count over the profiled run's
-    pushes (warm-up + steps of its recorded bench arguments)."""
+    """Launches of the profiled kernel per bench step: its rocprof call count over the steps the
+    profiled run took (warm-up included), as its own bench line recorded them in meta.json (older
+    profiles: the recorded arguments, with bench.py's defaults and C5's forced warm-up)."""
     if not prof:
         return 1
     try:
-        a = json.load(open(os.path.join(ROOT, prof_dir, "meta.json")))["bench_args"].split()
-        n = int(a[a.index("--steps") + 1]) + int(a[a.index("--warmup") + 1])
-        return max(1, round(prof["calls"] / n))
+        meta = json.load(open(os.path.join(ROOT, prof_dir, "meta.json")))
+        if meta.get("steps") is not None and meta.get("warmup") is not None:
+            return prof["calls"] / (int(meta["steps"]) + int(meta["warmup"]))
+        a = meta["bench_args"].split()
+        steps = int(a[a.index("--steps") + 1]) if "--steps" in a else 12
+        warm = int(a[a.index("--warmup") + 1]) if "--warmup" in a else 2
+        if meta.get("workload") == "c5":
+            warm = max(warm, -(-5_400_000 // meta["batch"]) + 1)  # (batch: node events per stream)
+        return prof["calls"] / (steps + warm)
     except (OSError, ValueError, KeyError, IndexError):
         return 1
 
@@ -346,18 +356,18 @@ def main():
     import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    # rehearsal knobs for a 1-GPU box (not used by the driver): every rank on one device, gloo
-    backend = os.environ.get("SDH_BENCH_BACKEND", "nccl")
-    if "SDH_BENCH_DEVICE" in os.environ:
-        local = int(os.environ["SDH_BENCH_DEVICE"])
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        # control plane only (barriers, the max over ranks, the communicator id); the event broadcast
+        # and the match gather run inside libsiddhi_hip.so over its own RCCL communicator
+        dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    cdev = dev if backend == "nccl" else torch.device("cpu")  # where the collectives run
+    cdev = torch.device("cpu")  # where the control collectives run
+    comm = None
+    if world > 1:
+        from siddhi_amd.engine import Comm
+        uid = [Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = Comm.rccl(uid[0], rank, world, local)
 
     from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES
 
@@ -384,36 +394,29 @@ def main():
         K_gen = K
     log(f"building the engine: {args.workload}, {sh.n} patterns on this GPU, {B} events per step")
     eng = make_engine(args.workload, sh, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials)
+    if comm is not None:
+        eng.set_comm(comm)
     t_build = time.perf_counter() - t_build
     log(f"engine built in {t_build:.1f} s")
 
     n_batches = args.warmup + args.steps
-    # synthetic batches generated on the device before the timed region (rank 0's copy is the
-    # broadcast source in multi-GPU runs; the other ranks receive into zeroed buffers, so a missing
-    # broadcast shows as wrong matches)
+    # synthetic batches generated on the device before the timed region; in multi-GPU runs only rank
+    # 0 holds them (the broadcast source), the other ranks receive every batch through the library
     bcast = world > 1
 
     def local_batch(i):
+        if bcast and rank != 0:
+            return [None] * (4 if c5 else 1)
         cols = gen_batch(args.workload, i * B, B, K_gen, dev)
-        if c5:
-            return cols if rank == 0 or not bcast else [[torch.zeros_like(t) for t in c] for c in cols]
-        return [cols] if rank == 0 or not bcast else [[torch.zeros_like(t) for t in cols]]
+        return cols if c5 else [cols]
 
     pre = [local_batch(i) for i in range(args.warmup, n_batches)]
     torch.cuda.synchronize()
 
-    def bcast_into(t):
-        if backend == "nccl":
-            dist.broadcast(t, src=0)
-        else:  # gloo rehearsal: the collective runs on a host copy, received back into t
-            tc = t.cpu()
-            dist.broadcast(tc, src=0)
-            t.copy_(tc)
-
     def make_step(engine, batches):
         def step(i):
-            """One step: every stream's batch pushed once (broadcast from rank 0 first); returns
-            (kernel ms, algorithmic bytes, matches) summed over the step's pushes."""
+            """One step: every stream's batch pushed once (broadcast from rank 0 by the library in
+            multi-GPU runs); returns (kernel ms, algorithmic bytes, matches) summed over the pushes."""
             if i < args.warmup:  # generated now (torch's stream): complete before the engine reads it
                 per_stream = local_batch(i)
                 torch.cuda.synchronize()
@@ -422,10 +425,12 @@ def main():
             ms = by = 0.0
             nm = 0
             for si, cols in enumerate(per_stream):
-                if bcast:
-                    for t in cols:
-                        bcast_into(t)
-                engine.push_device(si, B, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
+                if not bcast:
+                    engine.push_device(si, B, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
+                elif rank == 0:
+                    engine.push_bcast_device(si, B, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]], root=0)
+                else:
+                    engine.push_bcast_recv(root=0)
                 if len(per_stream) > 1 or i >= args.warmup:
                     kms, kby = engine.push_stats()  # (no device work inside the timed steps)
                     ms += kms
@@ -494,6 +499,14 @@ def main():
                      "launches_per_step": launches,
                      "traffic_per_step": traffic * launches if traffic else None},
     }
+    if args.workload == "c2":
+        # §8(d) prices a match at 32 B; the K_ratchet record is 8 B. frac_design: the design's own
+        # minimum bytes per launch -- E x 16 B per 64-pattern group (ts, price; f0 reads the same
+        # column) + 8 B per match -- over the kernel time, against 8 TB/s
+        m_launch = matches / max(1, args.steps * world)
+        design = avg_bytes - 24.0 * m_launch
+        result["roofline"]["design_bytes_per_launch"] = design
+        result["roofline"]["frac_design"] = design / (avg_ms * 1e-3) / 1e9 / peak
     if prof:
         result["roofline"]["counters"] = {k: v for k, v in prof.items() if k != "traffic_bytes"}
         # issue roofline: the profile's wave-instructions per pattern-event at this run's kernel rate,
@@ -526,6 +539,7 @@ def main():
         eng.close()
         wsh = Shard(args.workload, "weak", P, rank, world)
         weng = make_engine(args.workload, wsh, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials)
+        weng.set_comm(comm)
         wsteps = max(2, args.steps // 3)
         wpre = [local_batch(i) for i in range(args.warmup, args.warmup + wsteps)]
         el, _, _, wm, wpe = timed_steps(weng, make_step(weng, wpre), args.warmup, wsteps, world, dist)
@@ -536,7 +550,7 @@ def main():
         del wpre
     if not args.no_expansion:
         log("expansion leg (normal mode + sdh_engine_poll_device)")
-        result["expansion"] = expansion(args, sh, K, local, dev, world, cdev, dist)
+        result["expansion"] = expansion(args, sh, K, local, dev, world, cdev, dist, comm)
     if not args.no_ingest and world == 1:
         log("host-ingest leg")
         result["host_ingest"] = host_ingest(args, eng, B, K, n_batches)
@@ -551,6 +565,8 @@ def main():
         result["build"] = build_provenance()
         print(json.dumps(result), flush=True)
     if world > 1:
+        eng.close()
+        comm.close()
         dist.destroy_process_group()
 
 
@@ -637,23 +653,21 @@ def eng_patterns(eng):
     return st.pattern_events / max(1, st.events)
 
 
-def expansion(args, sh, K, local, dev, world, cdev, dist):
+def expansion(args, sh, K, local, dev, world, cdev, dist, comm=None):
     """Pushes of a smaller batch in normal mode, each followed by sdh_engine_poll_device (device R18
-    sort + gather of the ABI tuples in HBM): the NFA step with every match expanded. With N GPUs every
-    rank's R18-sorted tuples are then gathered to rank 0 over RCCL and merged there (siddhi_amd/dist.py:
-    a k-way merge of the sorted runs), timed per step."""
+    sort + gather of the ABI tuples in HBM): the NFA step with every match expanded. With N GPUs the
+    pushes are broadcast from rank 0 and every push is followed by sdh_engine_gather: every rank's
+    R18-sorted tuples go to rank 0 over RCCL and are merged there on the device, timed per step."""
     import torch
-    from siddhi_amd import dist as sdist
     # with N GPUs every rank's tuples are gathered to rank 0: C2 at 10K patterns makes ~4,300 matches
     # per event, so the multi-GPU gather runs on 8K-event batches
     E = args.expansion_batch if world == 1 else min(args.expansion_batch, 8192)
     eng = make_engine(args.workload, sh, K, local, 0, args.partials)
+    if comm is not None:
+        eng.set_comm(comm)
     steps, warm = 4, 1
-    bs = [gen_batch(args.workload, s * E, E, K, dev) for s in range(steps + warm)]
-    slog = sdist.StreamLog()
-    # one stream: the receiver rank of a query is its index in the full program (every query of
-    # these families reads the one stream; c3's partition receivers are all multi-processor ones)
-    table = torch.arange((args.patterns or DEFAULTS[args.workload][0]) * world, dtype=torch.int64)
+    root = world == 1 or dist.get_rank() == 0
+    bs = [gen_batch(args.workload, s * E, E, K, dev) if root else None for s in range(steps + warm)]
     torch.cuda.synchronize()
     push_ms, gather_ms, matches, merged = 0.0, 0.0, 0, 0
     for i, cols in enumerate(bs):
@@ -663,23 +677,20 @@ def expansion(args, sh, K, local, dev, world, cdev, dist):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
         t1 = time.perf_counter()
-        eng.push_device(0, E, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
-        slog.push(0, E)
+        if world == 1:
+            eng.push_device(0, E, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
+        elif root:
+            eng.push_bcast_device(0, E, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]], root=0)
+        else:
+            eng.push_bcast_recv(root=0)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         if world > 1:
-            mc = sdist.columns_from_device(eng, dev)
-            mc["q"] = sh.global_q(mc["q"])  # this rank's sub-app numbers its queries from 0
-            if cdev.type != "cuda":  # gloo rehearsal: the collectives take host tensors
-                mc = {k: v.to(cdev) for k, v in mc.items()}
+            n_local = eng.pending_matches()  # this rank's window (one push)
             t3 = time.perf_counter()
-            per_rank = sdist.gather_columns(mc)
-            if dist.get_rank() == 0:
-                out = sdist.merge_columns(None, per_rank, slog, table=table.to(cdev), n_streams=1)
-                if i >= warm:  # (timed pushes only, as `matches`)
-                    merged += int(out["q"].numel())
-            torch.cuda.synchronize()
-            n_local = int(mc["q"].numel())
+            m = eng.gather(device=True)
+            if root and i >= warm:  # (timed pushes only, as `matches`)
+                merged += m.n
             t4 = time.perf_counter()
         else:
             n_local = eng.poll_device().n
@@ -714,7 +725,7 @@ def expansion(args, sh, K, local, dev, world, cdev, dist):
     if world > 1:
         if dist.get_rank() == 0 and merged != matches:
             raise RuntimeError(f"the gather merged {merged} matches, the ranks produced {matches}")
-        r["rccl_gather_merge_ms_per_step"] = gather_ms / steps
+        r["rccl_gather_merge_ms_per_step"] = gather_ms / steps  # (sdh_engine_gather: sort, RCCL, merge)
         r["merged_matches_per_step_rank0"] = merged / steps
         r["gather_merge_ns_per_match"] = gather_ms * 1e6 / max(1, matches)
     return r

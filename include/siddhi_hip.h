@@ -224,6 +224,50 @@ int sdh_engine_restore(sdh_engine* e, const void* blob, size_t len);
 void sdh_free(void* p);
 void sdh_engine_destroy(sdh_engine* e);
 const char* sdh_last_error(sdh_engine* e);
+/* ---- Multi-GPU: one engine per GPU, the exchange inside the library ----
+ * Every rank runs the same program with sdh_config.shard_rank / shard_world = its rank in the
+ * communicator: unpartitioned queries shard by pattern set (q % world), partitions by key
+ * (|String.valueOf(key).hashCode() % world|, PartitionedDistributionStrategy.java:98-109). The
+ * exchange has two steps and no other collective:
+ *   sdh_engine_push_bcast  every rank pushes the same batch, broadcast from `root`'s copy (RCCL over
+ *                          xGMI): StreamJunction.sendEvent reaching every subscriber
+ *                          (stream/StreamJunction.java:179-181) when the subscribers live on N GPUs;
+ *   sdh_engine_gather      every rank's R18-ordered matches since its last poll go to rank 0, which
+ *                          merges the runs on the device (a k-way merge: a receiver's matches of one
+ *                          event come from one rank, so the runs never tie) into exactly the order a
+ *                          single engine would deliver -- the QuerySelector hand-off of sdh_engine_poll.
+ * Communicators:
+ *   sdh_comm_get_id + sdh_comm_create: RCCL, one process per GPU (ncclGetUniqueId on one rank, the
+ *     SDH_COMM_ID_BYTES distributed by the host -- e.g. over the cluster's own control channel -- and
+ *     ncclCommInitRank on every rank; collective: every rank calls it).
+ *   sdh_comm_create_local: `world` ranks inside this process (engines on one or several devices),
+ *     buffers copied device-to-device: the same protocol, for one process driving several engines and
+ *     for testing the exchange on one GPU. Its collectives complete in call order: a broadcast's root
+ *     pushes first and the other ranks after it, before the root's next push; a gather's ranks
+ *     1..world-1 call first and rank 0 last.
+ * sdh_engine_set_comm attaches a communicator (not owned; it must outlive the engine's use of it,
+ * and its device must be the engine's). Both exchange calls are collective over the communicator's
+ * ranks and run on the engine's stream. */
+#define SDH_COMM_ID_BYTES 128
+#define SDH_MAX_RANKS 64
+typedef struct sdh_comm sdh_comm;
+int sdh_comm_get_id(void* id, size_t cap);
+int sdh_comm_create(const void* id, size_t len, int32_t rank, int32_t world, int32_t device, sdh_comm** out);
+int sdh_comm_create_local(int32_t world, const int32_t* devices, sdh_comm** out /* world entries */);
+void sdh_comm_destroy(sdh_comm* c);
+const char* sdh_comm_last_error(void);   /* this thread's last sdh_comm_* failure */
+int sdh_engine_set_comm(sdh_engine* e, sdh_comm* c);
+/* As sdh_engine_push on every rank, with the batch taken from `root`'s `batch` (host or device,
+ * single events or a chunk); the other ranks pass NULL (or any batch: ignored) and receive it into
+ * engine-owned HBM. */
+int sdh_engine_push_bcast(sdh_engine* e, int32_t stream, const sdh_batch* batch, int32_t root);
+/* Collective poll: rank 0's `out` receives the matches of every rank since their last poll, merged
+ * into the single-engine order (the sdh_engine_poll contract; device != 0: HBM pointers as
+ * sdh_engine_poll_device), other ranks get n = 0. Requires shard_rank / shard_world equal to the
+ * communicator's rank / world, and every rank's poll windows in step (the same pushes since the last
+ * gather). */
+int sdh_engine_gather(sdh_engine* e, int32_t device, sdh_matches* out);
+
 /* Diagnostic, no device needed: generate and compile (hiprtc, gfx950) the shape-compiled kernels of
  * representative K_seq / K_part shapes. Returns the number compiled, or -1 with the compiler log. */
 int sdh_spec_selftest(char* log, size_t cap);

@@ -62,7 +62,14 @@ def main(src, dst, kernel, workload, patterns, batch):
         commit = subprocess.check_output(["git", "rev-parse", "--short=12", "HEAD"], text=True).strip()
     except (OSError, subprocess.CalledProcessError):
         commit = ""
+    # the profiled run's own bench line: the steps and the warm-up it really ran (C5 forces a longer
+    # warm-up than its arguments say), so bench.py divides the call count by the real step count
+    line = {}
+    for ln in open(os.path.join(src, "trace.log"), errors="replace"):
+        if ln.startswith('{"metric"'):
+            line = json.loads(ln)
     meta = {"source_hash": open(os.path.join(src, "source_hash")).read().strip(),
+            "steps": line.get("steps"), "warmup": line.get("warmup"),
             "bench_args": open(os.path.join(src, "args")).read().strip(), "commit_base": commit,
             "workload": workload, "patterns": int(patterns), "batch": int(batch),
             "kernels": {kernel: d}}

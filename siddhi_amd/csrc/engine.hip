@@ -23,6 +23,7 @@
 
 #include "../../include/siddhi_hip.h"
 #include "chm_order.h"
+#include "comm.h"
 #include "java_fmt.h"
 #include "gen_lower.h"
 #include "nfa_types.h"
@@ -95,6 +96,12 @@ extern "C" hipError_t sdh_key_segments(const uint32_t* uniq, const int32_t* nrun
 extern "C" hipError_t sdh_digest_compact(const int32_t* crow, int width, int64_t row0, int64_t n, int64_t seq_ref,
                                          unsigned long long* acc, hipStream_t s);
 extern "C" hipError_t sdh_place_scan(int32_t* cnt, int64_t cells, void* temp, size_t temp_bytes, hipStream_t s);
+extern "C" hipError_t sdh_merge_keys_table(sdh::MatchTable T, const int32_t* perm, int64_t n, int chunk_words,
+                                           int lo_words, int chunked, uint64_t* keys, hipStream_t s);
+extern "C" hipError_t sdh_merge_keys_placed(const int32_t* crow, int width, int64_t n, int64_t seq_ref,
+                                            const int32_t* out_rank, const int32_t* qinfo, int n_streams,
+                                            int chunk_words, int lo_words, uint64_t* keys, hipStream_t s);
+extern "C" hipError_t sdh_place_total(const int32_t* cnt, int64_t cells, unsigned long long* tot, hipStream_t s);
 extern "C" hipError_t sdh_compact_fill(const int32_t* crow, int width, int64_t rows, const int64_t* ts_log,
                                        int64_t seq_ref, int64_t* oq, int64_t* okey, int64_t* ots, int64_t* oseq,
                                        int64_t* otb, int64_t* ooff, int64_t* owords, hipStream_t s);
@@ -555,13 +562,21 @@ template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  // grows by at least half its size (a buffer sized per push or per poll would otherwise be freed and
+  // allocated again whenever the count edges up: hipFree synchronises the device, a p99 spike)
   void ensure(size_t want) {
     if (want <= n) return;
+    const size_t cap = std::max(want, n + n / 2);
     if (p) HIPCHK(hipFree(p));
     p = nullptr;
     n = 0;
-    size_t cap = std::max(want, n * 2);
-    HIPCHK(hipMalloc(&p, cap * sizeof(T)));
+    if (hipMalloc(&p, cap * sizeof(T)) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+      HIPCHK(hipMalloc(&p, want * sizeof(T)));
+      n = want;
+      return;
+    }
     n = cap;
   }
   // grow to at least `want` elements keeping the first `keep` (stream-ordered copy)
@@ -652,6 +667,7 @@ struct sdh_engine {
     // [0, ck_n) have theirs, the rest are single-event rows filled at the poll
     DevBuf<uint64_t> chi, clo;
     bool chunked = false;
+    bool chunk_pushed = false;       // a chunk push joined the window (every rank alike: same pushes)
     int64_t ck_n = 0;
     int64_t max_run = 0;             // largest run start / key position a chunk row carries
   } mt;
@@ -859,6 +875,15 @@ struct sdh_engine {
   sdh_stats stats{};
   std::string err;
   std::string broken;                // set when a failed push left the state undefined
+  // ---- multi-GPU exchange (comm.h; sdh_engine_push_bcast / sdh_engine_gather) ----
+  sdh_comm* comm = nullptr;          // not owned
+  DevBuf<uint8_t> x_batch;           // a broadcast batch received from the root
+  DevBuf<uint64_t> x_keys;           // this rank's merge keys, one run
+  // rank 0: every rank's run concatenated, and the merged output
+  DevBuf<int64_t> xg_q, xg_key, xg_ts, xg_seq, xg_tb, xg_off, xg_words;
+  DevBuf<uint64_t> xg_keys;
+  DevBuf<int64_t> go_q, go_key, go_ts, go_seq, go_tb, go_len, go_off, go_src, go_pos, go_words;
+  DevBuf<uint8_t> go_temp;
 };
 
 namespace {
@@ -986,6 +1011,7 @@ void table_clear(sdh_engine* e) {
   e->mt.n_lo = 0;
   e->mt.placed = false;
   e->mt.chunked = false;
+  e->mt.chunk_pushed = false;
   e->mt.ck_n = 0;
   e->mt.max_run = 0;
   e->seq_ref = e->seq;
@@ -1064,6 +1090,20 @@ const int32_t* fan_positions(sdh_engine* e, sdh_engine::Route& rt, const kg::LFa
     f.n = nk;
   }
   return f.pos.p;
+}
+
+// A push on a stream that fans out to every key of a string-keyed partition needs the text hash of
+// every key it will reach (fan_positions). Checked before any kernel runs, so a missing
+// sdh_engine_set_strings (e.g. after sdh_engine_restore) fails the push with SDH_E_INVALID and leaves
+// the engine usable. (A push on the keyed stream creates keys but reaches no fan-out position.)
+void check_fan_strings(const sdh_engine* e, int stream) {
+  for (size_t pi = 0; pi < e->lp.parts.size() && pi < e->routes.size(); ++pi) {
+    const sdh_engine::Route* rt = e->routes[pi].get();
+    if (!rt || !rt->track || rt->kkind != 2 || !e->lp.parts[pi].fan(stream)) continue;
+    for (int64_t k : rt->korder_key)
+      if (e->str_info.find((int32_t)k) == e->str_info.end())
+        throw Error(SDH_E_INVALID, fmt("partition key string id %lld has no text hash (sdh_engine_set_strings)", (long long)k));
+  }
 }
 
 // A normal-mode push places its K_ratchet matches directly (nfa_ratchet.hip PM: COUNT per (event,
@@ -1151,18 +1191,6 @@ int32_t* table_order(sdh_engine* e, int64_t* total_words) {
                        e->po_len.p, e->po_off.p, &perm, total_words, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return perm;
-}
-
-// R18 sort of the table and gather of the ABI arrays in HBM (po_*); returns the match count
-int64_t table_sort(sdh_engine* e, int64_t* total_words) {
-  const int64_t n = e->mt.n;
-  *total_words = 0;
-  if (n == 0) return 0;
-  int32_t* perm = table_order(e, total_words);
-  e->po_words.ensure((size_t)std::max<int64_t>(*total_words, 1));
-  HIPCHK(sdh_poll_words(table_view(e), perm, n, e->po_off.p, e->po_words.p, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
-  return n;
 }
 
 void d2h_sync(sdh_engine* e, void* dst, const void* src, size_t bytes) {
@@ -1421,7 +1449,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     if (ring) want = std::min<int64_t>(want, (int64_t)1 << 30);  // 8 GiB of 8-B records, rewritten in a ring
     e->r_blocks = (want + e->r_blk_recs - 1) / e->r_blk_recs;
   }
-  e->d_rtotal.ensure(1);
+  e->d_rtotal.ensure(2);  // [0] ring-mode records, [1] the placement total
   (void)t01;
   bool no_place = false;
   for (int attempt = 0; attempt < 40; ++attempt) {
@@ -1595,13 +1623,14 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     if (placing) {
       // the (event, cell) counts -> each cell's first row; then the same items again, writing
       e->p_ptemp.ensure(sdh_place_temp_bytes(cells));
+      HIPCHK(sdh_place_total(e->p_cnt.p, cells, e->d_rtotal.p + 1, e->stream));
       HIPCHK(sdh_place_scan(e->p_cnt.p, cells, e->p_ptemp.p, e->p_ptemp.n, e->stream));
-      int32_t tot = 0;
-      HIPCHK(hipMemcpyAsync(&tot, e->p_cnt.p + cells - 1, 4, hipMemcpyDeviceToHost, e->stream));
+      unsigned long long tot = 0;
+      HIPCHK(hipMemcpyAsync(&tot, e->d_rtotal.p + 1, 8, hipMemcpyDeviceToHost, e->stream));
       HIPCHK(hipStreamSynchronize(e->stream));
-      placed_rows = tot;
+      placed_rows = (int64_t)tot;
       const int64_t n0 = e->mt.n;
-      if (tot < 0 || n0 + placed_rows >= INT32_MAX) {  // (rows past 2^31: records for the table)
+      if (tot >= (unsigned long long)INT32_MAX || n0 + placed_rows >= INT32_MAX) {  // (2^31 rows: table records)
         no_place = true;
         continue;
       }
@@ -3178,6 +3207,7 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   if (b->n < 0 || (e->cfg.max_batch > 0 && b->n > e->cfg.max_batch))
     throw Error(SDH_E_INVALID, "batch larger than max_batch");
   if (b->n == 0) return SDH_OK;
+  check_fan_strings(e, stream);
   HIPCHK(hipSetDevice(e->dev));
   // an exact re-run needs the journal of the K_gen blocks the push modifies (gen_journal): a batch
   // whose bound does not fit a third of free HBM is pushed as two halves -- the same events in the
@@ -3339,20 +3369,45 @@ void check_usable(sdh_engine* e) {
 }
 
 // R18-sorted matches since the last poll; host == false leaves them in HBM (sdh_engine_poll_device)
+// The window's matches R18-sorted into the ABI arrays in HBM (po_*; *tw words); with `kw_spec`
+// (chunk words, lo words: sdh_engine_gather) also each row's merge key into x_keys.
+int64_t poll_sorted(sdh_engine* e, int64_t* tw, const int* kw_spec = nullptr) {
+  int64_t n = 0;
+  *tw = 0;
+  const int kw = kw_spec ? 2 * kw_spec[0] + 1 + 3 * kw_spec[1] : 0;
+  if (kw) e->x_keys.ensure((size_t)std::max<int64_t>(1, e->mt.n) * kw);
+  if (e->mt.placed) {  // compact rows already in R18 order (place_ratchet): 4 words per match
+    n = e->mt.n;
+    *tw = 4 * n;
+    poll_reserve(e, n, *tw);
+    HIPCHK(sdh_compact_fill(e->pc_rows.p, e->cw, n, e->ts_log.p, e->seq_ref, e->po_q.p, e->po_key.p, e->po_ts.p,
+                            e->po_seq.p, e->po_tb.p, e->po_off.p, e->po_words.p, e->stream));
+    if (kw)
+      HIPCHK(sdh_merge_keys_placed(e->pc_rows.p, e->cw, n, e->seq_ref, e->d_out_rank.p, e->d_qinfo.p,
+                                   (int)e->prog.stream_types.size(), kw_spec[0], kw_spec[1], e->x_keys.p, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  } else if (e->mt.n > 0) {
+    n = e->mt.n;
+    const int32_t* perm = table_order(e, tw);
+    e->po_words.ensure((size_t)std::max<int64_t>(*tw, 1));
+    HIPCHK(sdh_poll_words(table_view(e), perm, n, e->po_off.p, e->po_words.p, e->stream));
+    if (kw)
+      HIPCHK(sdh_merge_keys_table(table_view(e), perm, n, kw_spec[0], kw_spec[1], e->mt.chunked ? 1 : 0, e->x_keys.p,
+                                  e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  if (n == 0) {
+    e->po_off.ensure(1);
+    HIPCHK(hipMemsetAsync(e->po_off.p, 0, 8, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  return n;
+}
+
 int do_poll(sdh_engine* e, sdh_matches* out, bool host) {
   check_usable(e);
   int64_t tw = 0;
-  int64_t n = 0;
-  if (e->mt.placed) {  // compact rows already in R18 order (place_ratchet): 4 words per match
-    n = e->mt.n;
-    tw = 4 * n;
-    poll_reserve(e, n, tw);
-    HIPCHK(sdh_compact_fill(e->pc_rows.p, e->cw, n, e->ts_log.p, e->seq_ref, e->po_q.p, e->po_key.p, e->po_ts.p,
-                            e->po_seq.p, e->po_tb.p, e->po_off.p, e->po_words.p, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-  } else {
-    n = table_sort(e, &tw);
-  }
+  const int64_t n = poll_sorted(e, &tw);
   if (host) {
     e->ho_q.ensure(std::max<int64_t>(n, 1));
     e->ho_key.ensure(std::max<int64_t>(n, 1));
@@ -3380,11 +3435,6 @@ int do_poll(sdh_engine* e, sdh_matches* out, bool host) {
     out->off = e->ho_off.p;
     out->words = e->ho_words.p;
   } else {
-    if (n == 0) {
-      e->po_off.ensure(1);
-      HIPCHK(hipMemsetAsync(e->po_off.p, 0, 8, e->stream));
-      HIPCHK(hipStreamSynchronize(e->stream));
-    }
     out->query = e->po_q.p;
     out->key = e->po_key.p;
     out->ts = e->po_ts.p;
@@ -3435,6 +3485,215 @@ int do_poll_compact(sdh_engine* e, sdh_matches_compact* out, bool device) {
   return SDH_OK;
 }
 
+// ---- multi-GPU exchange (comm.h) ----
+template <class F>
+void xcall(F f) {
+  try {
+    f();
+  } catch (const Error&) {
+    throw;
+  } catch (const std::invalid_argument& ex) {
+    throw Error(SDH_E_INVALID, ex.what());
+  } catch (const std::runtime_error& ex) {
+    throw Error(SDH_E_DEVICE, ex.what());
+  }
+}
+
+int push_chunk(sdh_engine* e, int32_t stream, const sdh_batch* b);
+
+// sdh_engine_push_bcast: the root's batch (staged into HBM first when it is host-resident) goes to
+// every rank -- a header {n, stream, chunk, null-mask bits}, then ts, the attribute columns and the
+// null masks the header names -- and every rank pushes it from HBM.
+int do_push_bcast(sdh_engine* e, int32_t stream, const sdh_batch* b, int root) {
+  if (!e->comm) throw Error(SDH_E_INVALID, "sdh_engine_push_bcast: no communicator (sdh_engine_set_comm)");
+  HIPCHK(hipSetDevice(e->dev));
+  const bool am_root = xch::rank(e->comm) == root;
+  int64_t hdr[xch::HDR] = {};
+  StreamBatch B{};
+  if (am_root) {
+    if (!b || stream < 0 || stream >= (int)e->prog.stream_types.size() ||
+        b->n_cols != (int)e->prog.stream_types[stream].size() || b->n < 0)
+      throw Error(SDH_E_INVALID, "bad stream or batch");  // (before the collective: every rank then fails
+                                                           //  its own call or waits for the next batch)
+    const int na = b->n_cols;
+    B.n = b->n;
+    B.n_attr = na;
+    for (int a = 0; a < na; ++a) B.width[a] = attr_width(e->prog.stream_types[stream][a]);
+    if (b->n > 0 && !b->on_device) {
+      stage_host_batch(e, b, B);
+    } else {
+      B.ts = b->ts;
+      for (int a = 0; a < na; ++a) {
+        B.col[a] = b->cols[a];
+        B.nul[a] = b->nulls ? b->nulls[a] : nullptr;
+      }
+    }
+    int64_t mask = 0;
+    for (int a = 0; a < na; ++a)
+      if (B.nul[a]) mask |= (int64_t)1 << a;
+    hdr[0] = b->n;
+    hdr[1] = stream;
+    hdr[2] = b->chunk;
+    hdr[3] = mask;
+  }
+  xcall([&] { xch::bcast_hdr(e->comm, hdr, root, e->stream); });
+  const int64_t n = hdr[0];
+  stream = (int32_t)hdr[1];
+  if (stream < 0 || stream >= (int)e->prog.stream_types.size()) throw Error(SDH_E_INVALID, "broadcast: bad stream");
+  const auto& types = e->prog.stream_types[stream];
+  const int na = (int)types.size();
+  if (n == 0) return SDH_OK;
+  // the receivers' layout (256-B aligned parts in x_batch), the root's sources
+  std::vector<xch::Buf> bufs;
+  size_t total = 0;
+  auto add = [&](const void* src, size_t bytes) {
+    total = (total + 255) & ~(size_t)255;
+    bufs.push_back({src, (void*)(uintptr_t)total, bytes});
+    total += bytes;
+  };
+  add(B.ts, (size_t)n * 8);
+  for (int a = 0; a < na; ++a) add(am_root ? B.col[a] : nullptr, (size_t)n * attr_width(types[a]));
+  for (int a = 0; a < na; ++a)
+    if (hdr[3] >> a & 1) add(am_root ? B.nul[a] : nullptr, (size_t)n);
+  if (!am_root) {
+    e->x_batch.ensure(total);
+    for (auto& x : bufs) x.dst = e->x_batch.p + (uintptr_t)x.dst;
+  }
+  xcall([&] { xch::bcast_bufs(e->comm, bufs, root, e->stream); });
+  std::vector<const void*> cols((size_t)na);
+  std::vector<const uint8_t*> nuls((size_t)na, nullptr);
+  auto at = [&](size_t i) -> const void* { return am_root ? bufs[i].src : bufs[i].dst; };
+  size_t k = 1;
+  for (int a = 0; a < na; ++a) cols[(size_t)a] = at(k++);
+  for (int a = 0; a < na; ++a)
+    if (hdr[3] >> a & 1) nuls[(size_t)a] = (const uint8_t*)at(k++);
+  sdh_batch db{};
+  db.n = n;
+  db.ts = (const int64_t*)at(0);
+  db.cols = cols.data();
+  db.nulls = hdr[3] ? nuls.data() : nullptr;
+  db.n_cols = na;
+  db.on_device = 1;
+  db.chunk = (int32_t)hdr[2];
+  if (db.chunk && n > 1) return push_chunk(e, stream, &db);
+  return do_push(e, stream, &db);
+}
+
+// sdh_engine_gather: this rank's sorted run and its merge keys go to rank 0 (a header {n, words,
+// seq_ref, kw, seq} first), which merges the world's runs on the device (comm.hip sdh_merge_runs).
+int do_gather(sdh_engine* e, sdh_matches* out, bool host) {
+  if (!e->comm) throw Error(SDH_E_INVALID, "sdh_engine_gather: no communicator (sdh_engine_set_comm)");
+  const int me = xch::rank(e->comm), W = xch::world(e->comm);
+  if (e->cfg.shard_world != W || e->cfg.shard_rank != me)
+    throw Error(SDH_E_INVALID, fmt("sdh_engine_gather: the engine is shard %d of %d, the communicator's rank %d of %d",
+                                   e->cfg.shard_rank, e->cfg.shard_world, me, W));
+  HIPCHK(hipSetDevice(e->dev));
+  // the key words every rank uses (the same on all: same program, same pushes)
+  const int spec[2] = {e->mt.chunk_pushed ? 1 : 0, e->has_absent ? 1 : 0};
+  const int kw = 2 * spec[0] + 1 + 3 * spec[1];
+  int64_t tw = 0;
+  const int64_t n = poll_sorted(e, &tw, spec);
+  int64_t hdr[xch::HDR] = {n, tw, e->seq_ref, kw, e->seq, 0, 0, 0};
+  std::vector<int64_t> all((size_t)W * xch::HDR);
+  xcall([&] { xch::gather_hdr(e->comm, hdr, all.data(), e->stream); });
+  if (me != 0) {
+    const std::vector<xch::Buf> mine = {
+        {e->po_q.p, nullptr, (size_t)n * 8},    {e->po_key.p, nullptr, (size_t)n * 8},
+        {e->po_ts.p, nullptr, (size_t)n * 8},   {e->po_seq.p, nullptr, (size_t)n * 8},
+        {e->po_tb.p, nullptr, (size_t)n * 8},   {e->po_off.p, nullptr, (size_t)(n + 1) * 8},
+        {e->po_words.p, nullptr, (size_t)tw * 8}, {e->x_keys.p, nullptr, (size_t)n * kw * 8}};
+    xcall([&] { xch::gather_bufs(e->comm, mine, {}, e->stream); });
+    HIPCHK(hipStreamSynchronize(e->stream));  // (the sends drained before the buffers change)
+    table_clear(e);
+    poll_reserve(e, 0, 0);
+    HIPCHK(hipMemsetAsync(e->po_off.p, 0, 8, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    *out = sdh_matches{0, e->po_q.p, e->po_key.p, e->po_ts.p, e->po_off.p, e->po_words.p, e->po_seq.p, e->po_tb.p};
+    return SDH_OK;
+  }
+  std::vector<int64_t> run_off((size_t)W + 1, 0), wbase((size_t)W, 0);
+  int64_t TW = 0;
+  for (int r = 0; r < W; ++r) {
+    run_off[(size_t)r + 1] = run_off[(size_t)r] + all[(size_t)r * xch::HDR];
+    wbase[(size_t)r] = TW;
+    TW += all[(size_t)r * xch::HDR + 1];
+  }
+  const int64_t N = run_off[(size_t)W];
+  const size_t rows = (size_t)std::max<int64_t>(1, N);
+  e->xg_q.ensure(rows);
+  e->xg_key.ensure(rows);
+  e->xg_ts.ensure(rows);
+  e->xg_seq.ensure(rows);
+  e->xg_tb.ensure(rows);
+  e->xg_off.ensure((size_t)N + W);
+  e->xg_words.ensure((size_t)std::max<int64_t>(1, TW));
+  e->xg_keys.ensure(rows * kw);
+  std::vector<std::vector<xch::Buf>> recv((size_t)W);
+  for (int r = 0; r < W; ++r) {
+    const int64_t o = run_off[(size_t)r], nr = all[(size_t)r * xch::HDR], wr = all[(size_t)r * xch::HDR + 1];
+    recv[(size_t)r] = {{nullptr, e->xg_q.p + o, (size_t)nr * 8},          {nullptr, e->xg_key.p + o, (size_t)nr * 8},
+                       {nullptr, e->xg_ts.p + o, (size_t)nr * 8},         {nullptr, e->xg_seq.p + o, (size_t)nr * 8},
+                       {nullptr, e->xg_tb.p + o, (size_t)nr * 8},         {nullptr, e->xg_off.p + o + r, (size_t)(nr + 1) * 8},
+                       {nullptr, e->xg_words.p + wbase[(size_t)r], (size_t)wr * 8},
+                       {nullptr, e->xg_keys.p + o * kw, (size_t)nr * kw * 8}};
+  }
+  // rank 0's own run
+  const std::vector<const void*> own = {e->po_q.p, e->po_key.p, e->po_ts.p, e->po_seq.p,
+                                        e->po_tb.p, e->po_off.p, e->po_words.p, e->x_keys.p};
+  for (size_t i = 0; i < own.size(); ++i)
+    if (recv[0][i].bytes)
+      HIPCHK(hipMemcpyAsync(recv[0][i].dst, own[i], recv[0][i].bytes, hipMemcpyDeviceToDevice, e->stream));
+  xcall([&] { xch::gather_bufs(e->comm, {}, recv, e->stream); });
+  HIPCHK(hipStreamSynchronize(e->stream));
+  table_clear(e);
+  for (int r = 1; r < W; ++r) {  // (checked once every run has been received: no rank waits on a failed root)
+    const int64_t* h = all.data() + (size_t)r * xch::HDR;
+    if (h[2] != hdr[2] || h[3] != kw || h[4] != hdr[4])
+      throw Error(SDH_E_INVALID, fmt("sdh_engine_gather: rank %d's poll window differs from rank 0's (pushes out of step)", r));
+  }
+  e->go_q.ensure(rows);
+  e->go_key.ensure(rows);
+  e->go_ts.ensure(rows);
+  e->go_seq.ensure(rows);
+  e->go_tb.ensure(rows);
+  e->go_len.ensure((size_t)N + 1);
+  e->go_off.ensure((size_t)N + 1);
+  e->go_src.ensure(rows);
+  e->go_pos.ensure(rows);
+  e->go_temp.ensure(sdh_merge_temp_bytes(N));
+  int64_t total = 0;
+  HIPCHK(sdh_merge_runs(e->xg_keys.p, kw, run_off.data(), W, N, e->xg_q.p, e->xg_key.p, e->xg_ts.p, e->xg_seq.p,
+                        e->xg_tb.p, e->xg_off.p, wbase.data(), e->go_pos.p, e->go_q.p, e->go_key.p, e->go_ts.p,
+                        e->go_seq.p, e->go_tb.p, e->go_len.p, e->go_off.p, e->go_src.p, e->go_temp.p, e->go_temp.n,
+                        &total, e->stream));
+  if (total != TW) throw Error(SDH_E_DEVICE, "sdh_engine_gather: merged word count differs from the runs'");
+  e->go_words.ensure((size_t)std::max<int64_t>(1, TW));
+  HIPCHK(sdh_merge_words(e->go_src.p, e->go_off.p, N, e->xg_words.p, e->go_words.p, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (!host) {
+    *out = sdh_matches{N, e->go_q.p, e->go_key.p, e->go_ts.p, e->go_off.p, e->go_words.p, e->go_seq.p, e->go_tb.p};
+    return SDH_OK;
+  }
+  const size_t hn = (size_t)std::max<int64_t>(N, 1);
+  e->ho_q.ensure(hn);
+  e->ho_key.ensure(hn);
+  e->ho_ts.ensure(hn);
+  e->ho_seq.ensure(hn);
+  e->ho_tb.ensure(hn);
+  e->ho_off.ensure((size_t)N + 1);
+  e->ho_words.ensure((size_t)std::max<int64_t>(TW, 1));
+  const std::vector<std::tuple<void*, const void*, size_t>> cp = {
+      {e->ho_q.p, e->go_q.p, (size_t)N * 8},     {e->ho_key.p, e->go_key.p, (size_t)N * 8},
+      {e->ho_ts.p, e->go_ts.p, (size_t)N * 8},   {e->ho_seq.p, e->go_seq.p, (size_t)N * 8},
+      {e->ho_tb.p, e->go_tb.p, (size_t)N * 8},   {e->ho_off.p, e->go_off.p, (size_t)(N + 1) * 8},
+      {e->ho_words.p, e->go_words.p, (size_t)TW * 8}};
+  for (const auto& c : cp)
+    if (std::get<2>(c)) HIPCHK(hipMemcpyAsync(std::get<0>(c), std::get<1>(c), std::get<2>(c), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  *out = sdh_matches{N, e->ho_q.p, e->ho_key.p, e->ho_ts.p, e->ho_off.p, e->ho_words.p, e->ho_seq.p, e->ho_tb.p};
+  return SDH_OK;
+}
+
 // the absent states' timers due by t fire, with the next event's seq (sdh_engine_advance_time, and
 // a chunk push before its first event)
 void time_advance(sdh_engine* e, int64_t t) {
@@ -3450,6 +3709,7 @@ void time_advance(sdh_engine* e, int64_t t) {
   e->device_matches = 0;
   e->r_blocks_used = 0;
   e->r_matches = 0;
+  e->r_placing = false;  // (the digest then reads no stale placed rows)
   e->g_dev_matches = 0;
   e->g_used = 0;
   double ms = 0, bytes = 0;
@@ -3536,6 +3796,7 @@ int push_chunk(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     throw Error(SDH_E_INVALID, "bad stream or batch");
   if (e->cfg.max_batch > 0 && b->n > e->cfg.max_batch) throw Error(SDH_E_INVALID, "batch larger than max_batch");
   if (b->n >= INT32_MAX) throw Error(SDH_E_INVALID, "a chunk of 2^31 events or more");
+  if (b->n > 0) check_fan_strings(e, stream);
   HIPCHK(hipSetDevice(e->dev));
   int64_t t01[2];
   if (b->on_device) {
@@ -3553,6 +3814,7 @@ int push_chunk(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   }
   time_advance(e, t01[1]);
   e->ck.active = true;
+  e->mt.chunk_pushed = true;
   e->ck.first_seq = e->seq;
   e->ck.n = b->n;
   e->ck.stream = stream;
@@ -3741,6 +4003,32 @@ int sdh_engine_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     check_usable(e);
     if (b && b->chunk && b->n > 1) return push_chunk(e, stream, b);
     return do_push(e, stream, b);
+  });
+}
+
+int sdh_engine_set_comm(sdh_engine* e, sdh_comm* c) {
+  if (!e) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    if (c && xch::device(c) != e->dev)
+      throw Error(SDH_E_INVALID, fmt("communicator on device %d, engine on device %d", xch::device(c), e->dev));
+    e->comm = c;
+    return SDH_OK;
+  });
+}
+
+int sdh_engine_push_bcast(sdh_engine* e, int32_t stream, const sdh_batch* b, int32_t root) {
+  if (!e) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    check_usable(e);
+    return do_push_bcast(e, stream, b, root);
+  });
+}
+
+int sdh_engine_gather(sdh_engine* e, int32_t device, sdh_matches* out) {
+  if (!e || !out) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    check_usable(e);
+    return do_gather(e, out, device == 0);
   });
 }
 

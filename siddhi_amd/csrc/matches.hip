@@ -436,6 +436,24 @@ extern "C" hipError_t sdh_place_scan(int32_t* cnt, int64_t cells, void* temp, si
   return hipcub::DeviceScan::ExclusiveSum(temp, tb, cnt, cnt, (int)cells, s);
 }
 
+// the exact int64 total of the (event, cell) counts before the int32 scan: a push with 2^31 matches
+// or more would wrap the scan's offsets (engine.hip then takes the table path)
+__global__ __launch_bounds__(256) void place_total_kernel(const int32_t* __restrict__ cnt, int64_t cells,
+                                                          unsigned long long* __restrict__ tot) {
+  unsigned long long a = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells; i += (int64_t)gridDim.x * blockDim.x)
+    a += (unsigned long long)(uint32_t)cnt[i];
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_down(a, o);
+  if ((threadIdx.x & 63) == 0 && a) atomicAdd(tot, a);
+}
+extern "C" hipError_t sdh_place_total(const int32_t* cnt, int64_t cells, unsigned long long* tot, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(tot, 0, 8, s);
+  if (e != hipSuccess || cells <= 0) return e;
+  const int64_t blocks = std::min<int64_t>(1024, (cells + 255) / 256);
+  hipLaunchKernelGGL(place_total_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cnt, cells, tot);
+  return hipGetLastError();
+}
+
 // the ABI columns of a placed window's compact rows (po_* arrays; off has rows + 1 entries)
 extern "C" hipError_t sdh_compact_fill(const int32_t* crow, int width, int64_t rows, const int64_t* ts_log,
                                        int64_t seq_ref, int64_t* oq, int64_t* okey, int64_t* ots, int64_t* oseq,
@@ -461,6 +479,73 @@ extern "C" hipError_t sdh_table_compact(MatchTable T, const int32_t* perm, int64
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(sdh::table_compact_kernel, dim3(sdh::grid(n, 256)), dim3(256), 0, s, T, perm, n, width, seq_ref,
                      crow, err);
+  return hipGetLastError();
+}
+
+// ---- multi-GPU gather (comm.h): each sorted row's merge key ----
+// The poll's sort key, most significant first: [chi, clo] when the window saw a chunk push, hi, then
+// [lo2, lo1, lo0] when the program has absent states (timer rows of one seq from several ranks are
+// ordered by (tb, query, key)). The words the poll did not sort on are zero in every row, and rows
+// of different ranks never tie on the words used, so per-rank runs merge into the engine's order.
+__device__ __forceinline__ void put_merge_key(uint64_t* w, uint64_t chi, uint64_t clo, uint64_t hi, uint64_t l2,
+                                              uint64_t l1, uint64_t l0, int chunk_words, int lo_words) {
+  int k = 0;
+  if (chunk_words) {
+    w[k++] = chi;
+    w[k++] = clo;
+  }
+  w[k++] = hi;
+  if (lo_words) {
+    w[k++] = l2;
+    w[k++] = l1;
+    w[k++] = l0;
+  }
+}
+
+__global__ __launch_bounds__(256) void merge_keys_table_kernel(MatchTable T, const int32_t* __restrict__ perm,
+                                                               int64_t n, int chunk_words, int lo_words, int chunked,
+                                                               uint64_t* __restrict__ keys) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t p = perm[i];
+  const int kw = 2 * chunk_words + 1 + 3 * lo_words;
+  const uint64_t hi = T.hi[p];
+  const uint64_t chi = chunked ? T.chi[p] : hi & ~((1ull << sdh::RANK_BITS) - 1);
+  const uint64_t clo = chunked ? T.clo[p] : 0ull;
+  put_merge_key(keys + i * kw, chi, clo, hi, T.lo[2][p], T.lo[1][p], T.lo[0][p], chunk_words, lo_words);
+}
+
+// a placed window's compact rows (the keys placed_to_table_kernel would give them)
+__global__ __launch_bounds__(256) void merge_keys_placed_kernel(const int32_t* __restrict__ crow, int width, int64_t n,
+                                                                int64_t seq_ref, const int32_t* __restrict__ out_rank,
+                                                                const int32_t* __restrict__ qinfo, int n_streams,
+                                                                int chunk_words, int lo_words,
+                                                                uint64_t* __restrict__ keys) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t* r = crow + i * width;
+  const int qq = r[0];
+  const int64_t e2 = seq_ref + (int64_t)r[1], e1 = e2 - (int64_t)r[2];
+  const int kw = 2 * chunk_words + 1 + 3 * lo_words;
+  const uint64_t hi = sdh::hi_key(e2, seq_ref, out_rank[(int64_t)qq * n_streams + qinfo[2 * qq + 1]]);
+  put_merge_key(keys + i * kw, hi & ~((1ull << sdh::RANK_BITS) - 1), 0ull, hi, 0ull, 0ull, (uint64_t)e1, chunk_words,
+                lo_words);
+}
+
+extern "C" hipError_t sdh_merge_keys_table(MatchTable T, const int32_t* perm, int64_t n, int chunk_words, int lo_words,
+                                           int chunked, uint64_t* keys, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(merge_keys_table_kernel, dim3(sdh::grid(n, 256)), dim3(256), 0, s, T, perm, n, chunk_words,
+                     lo_words, chunked, keys);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sdh_merge_keys_placed(const int32_t* crow, int width, int64_t n, int64_t seq_ref,
+                                            const int32_t* out_rank, const int32_t* qinfo, int n_streams,
+                                            int chunk_words, int lo_words, uint64_t* keys, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(merge_keys_placed_kernel, dim3(sdh::grid(n, 256)), dim3(256), 0, s, crow, width, n, seq_ref,
+                     out_rank, qinfo, n_streams, chunk_words, lo_words, keys);
   return hipGetLastError();
 }
 

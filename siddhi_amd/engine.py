@@ -69,7 +69,10 @@ EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engi
            "sdh_engine_snapshot", "sdh_engine_state_bytes",
            "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version",
            "sdh_engine_debug_digest", "sdh_engine_set_strings", "sdh_calibrate_hbm", "sdh_build_info",
-           "sdh_engine_push_stats"]
+           "sdh_engine_push_stats", "sdh_comm_get_id", "sdh_comm_create", "sdh_comm_create_local",
+           "sdh_comm_destroy", "sdh_comm_last_error", "sdh_engine_set_comm", "sdh_engine_push_bcast",
+           "sdh_engine_gather"]
+SDH_COMM_ID_BYTES = 128
 
 _lib = None
 
@@ -110,6 +113,15 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_engine_set_strings.argtypes = [P, ctypes.c_int64, P, P, P]
     D = ctypes.POINTER(ctypes.c_double)
     lib.sdh_calibrate_hbm.argtypes = [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, D, D]
+    lib.sdh_comm_get_id.argtypes = [P, ctypes.c_size_t]
+    lib.sdh_comm_create.argtypes = [P, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.POINTER(P)]
+    lib.sdh_comm_create_local.argtypes = [ctypes.c_int32, P, ctypes.POINTER(P)]
+    lib.sdh_comm_destroy.argtypes = [P]
+    lib.sdh_comm_last_error.restype = ctypes.c_char_p
+    lib.sdh_engine_set_comm.argtypes = [P, P]
+    lib.sdh_engine_push_bcast.argtypes = [P, ctypes.c_int32, ctypes.POINTER(SdhBatch), ctypes.c_int32]
+    lib.sdh_engine_gather.argtypes = [P, ctypes.c_int32, ctypes.POINTER(SdhMatches)]
     _lib = lib
     return lib
 
@@ -118,6 +130,23 @@ class EngineError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"{ERRORS.get(code, code)}: {msg}")
         self.code = code
+
+
+def _matches_to_arrays(m: SdhMatches, with_seq: bool):
+    """Host sdh_matches -> (query, key, ts, off, words[, seq, tb]) numpy copies."""
+    n = m.n
+    if n == 0:
+        z = np.zeros(0, np.int64)
+        return (z, z, z, np.zeros(1, np.int64), z) + ((z, z) if with_seq else ())
+    q = np.ctypeslib.as_array(m.query, shape=(n,)).copy()
+    k = np.ctypeslib.as_array(m.key, shape=(n,)).copy()
+    ts = np.ctypeslib.as_array(m.ts, shape=(n,)).copy()
+    off = np.ctypeslib.as_array(m.off, shape=(n + 1,)).copy()
+    words = np.ctypeslib.as_array(m.words, shape=(int(off[-1]),)).copy() if off[-1] else np.zeros(0, np.int64)
+    if with_seq:
+        return (q, k, ts, off, words, np.ctypeslib.as_array(m.seq, shape=(n,)).copy(),
+                np.ctypeslib.as_array(m.tb, shape=(n,)).copy())
+    return q, k, ts, off, words
 
 
 _NP_OF = {T_INT: np.int32, T_LONG: np.int64, T_FLOAT: np.uint32, T_DOUBLE: np.int64, T_BOOL: np.uint8,
@@ -199,19 +228,58 @@ class HipEngine:
         """R18-ordered matches since the last poll as arrays (query, key, ts, off, words[, seq, tb])."""
         m = SdhMatches()
         self._check(self.lib.sdh_engine_poll(self.h, ctypes.byref(m)))
-        n = m.n
-        if n == 0:
-            z = np.zeros(0, np.int64)
-            return (z, z, z, np.zeros(1, np.int64), z) + ((z, z) if with_seq else ())
-        q = np.ctypeslib.as_array(m.query, shape=(n,)).copy()
-        k = np.ctypeslib.as_array(m.key, shape=(n,)).copy()
-        ts = np.ctypeslib.as_array(m.ts, shape=(n,)).copy()
-        off = np.ctypeslib.as_array(m.off, shape=(n + 1,)).copy()
-        words = np.ctypeslib.as_array(m.words, shape=(int(off[-1]),)).copy() if off[-1] else np.zeros(0, np.int64)
-        if with_seq:
-            return (q, k, ts, off, words, np.ctypeslib.as_array(m.seq, shape=(n,)).copy(),
-                    np.ctypeslib.as_array(m.tb, shape=(n,)).copy())
-        return q, k, ts, off, words
+        return _matches_to_arrays(m, with_seq)
+
+    def set_comm(self, comm: Optional["Comm"]):
+        """Attach a communicator (sdh_engine_set_comm); the engine does not own it."""
+        self._comm = comm
+        self._check(self.lib.sdh_engine_set_comm(self.h, comm.h if comm is not None else None))
+
+    def push_bcast_device(self, stream: int, n: int, ts_ptr: int, col_ptrs: Sequence[int], root: int = 0,
+                          chunk: bool = False):
+        """Collective push (sdh_engine_push_bcast): the root's batch, resident in HBM, reaches every
+        rank; the other ranks call push_bcast_recv."""
+        cp = (ctypes.c_void_p * len(col_ptrs))(*col_ptrs)
+        b = SdhBatch(n=n, ts=ts_ptr, cols=cp, nulls=None, n_cols=len(col_ptrs), on_device=1, chunk=int(chunk))
+        self._check(self.lib.sdh_engine_push_bcast(self.h, stream, ctypes.byref(b), root))
+
+    def push_bcast_columns(self, stream: int, ts: np.ndarray, cols: Sequence[np.ndarray],
+                           nulls: Optional[Sequence[Optional[np.ndarray]]] = None, root: int = 0, chunk: bool = False):
+        """Collective push from the root's host columns."""
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        cp = (ctypes.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+        nptr, keep = None, []
+        if nulls is not None:
+            nl = [None if x is None else np.ascontiguousarray(x, dtype=np.uint8) for x in nulls]
+            keep = [x for x in nl if x is not None]
+            nptr = (ctypes.c_void_p * len(cols))(*[0 if x is None else x.ctypes.data for x in nl])
+        b = SdhBatch(n=len(ts), ts=ts.ctypes.data, cols=cp, nulls=nptr, n_cols=len(cols), on_device=0,
+                     chunk=int(chunk))
+        self._check(self.lib.sdh_engine_push_bcast(self.h, stream, ctypes.byref(b), root))
+        del keep
+
+    def push_bcast_recv(self, root: int = 0):
+        """A non-root rank's side of push_bcast_*: the batch comes from the root."""
+        self._check(self.lib.sdh_engine_push_bcast(self.h, 0, None, root))
+
+    def send_bcast(self, stream: int, ts, vals: np.ndarray, nulls: Optional[np.ndarray], root: int = 0,
+                   as_chunk=False):
+        """tests/harness.App interface, as send() but through the broadcast (root side)."""
+        types = self.stream_types[stream]
+        cols = columns_from_words(np.asarray(vals, dtype=np.int64).reshape(len(ts), len(types)), types)
+        nl = None
+        if nulls is not None and np.any(nulls):
+            nl = [np.ascontiguousarray(nulls[:, j]) for j in range(len(types))]
+        self.push_bcast_columns(stream, np.asarray(ts, dtype=np.int64), cols, nl, root=root, chunk=as_chunk)
+
+    def gather(self, device: bool = False):
+        """Collective poll (sdh_engine_gather). Host: (query, key, ts, off, words, seq, tb) arrays
+        on rank 0 (empty elsewhere); device: the SdhMatches struct of HBM pointers."""
+        m = SdhMatches()
+        self._check(self.lib.sdh_engine_gather(self.h, int(device), ctypes.byref(m)))
+        if device:
+            return m
+        return _matches_to_arrays(m, True)
 
     def poll_device(self) -> SdhMatches:
         """R18-sorted matches since the last poll, left in HBM: the SdhMatches fields are device
@@ -305,6 +373,61 @@ class HipEngine:
     def close(self):
         if getattr(self, "h", None) and self.h:
             self.lib.sdh_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class Comm:
+    """A communicator of libsiddhi_hip.so (include/siddhi_hip.h sdh_comm_*): RCCL between processes
+    (one per GPU), or `world` in-process ranks (Comm.local) for engines driven by one process."""
+
+    def __init__(self, handle: ctypes.c_void_p, rank: int, world: int, group=None):
+        self.lib = load_library()
+        self.h, self.rank, self.world = handle, rank, world
+        self._group = group  # (local ranks share their group; destroyed together)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        """ncclGetUniqueId on this rank (sdh_comm_get_id): SDH_COMM_ID_BYTES to hand to every rank."""
+        lib = load_library()
+        buf = ctypes.create_string_buffer(SDH_COMM_ID_BYTES)
+        rc = lib.sdh_comm_get_id(buf, SDH_COMM_ID_BYTES)
+        if rc != SDH_OK:
+            raise EngineError(rc, lib.sdh_comm_last_error().decode())
+        return buf.raw
+
+    @classmethod
+    def rccl(cls, uid: bytes, rank: int, world: int, device: int = 0) -> "Comm":
+        """ncclCommInitRank (collective: every rank calls it with the same id)."""
+        lib = load_library()
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(uid, len(uid))
+        rc = lib.sdh_comm_create(buf, len(uid), rank, world, device, ctypes.byref(h))
+        if rc != SDH_OK:
+            raise EngineError(rc, lib.sdh_comm_last_error().decode())
+        return cls(h, rank, world)
+
+    @classmethod
+    def local(cls, world: int, devices: Optional[Sequence[int]] = None) -> List["Comm"]:
+        """`world` ranks in this process (sdh_comm_create_local)."""
+        lib = load_library()
+        hs = (ctypes.c_void_p * world)()
+        dv = (ctypes.c_int32 * world)(*(devices or [0] * world))
+        rc = lib.sdh_comm_create_local(world, dv, hs)
+        if rc != SDH_OK:
+            raise EngineError(rc, lib.sdh_comm_last_error().decode())
+        group: list = []
+        group.extend(cls(ctypes.c_void_p(hs[r]), r, world, group) for r in range(world))
+        return group
+
+    def close(self):
+        if getattr(self, "h", None) and self.h:
+            self.lib.sdh_comm_destroy(self.h)
             self.h = None
 
     def __del__(self):

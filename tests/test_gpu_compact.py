@@ -117,3 +117,44 @@ def test_compact_unsupported_keeps_window(kind):
     assert len(ga[0]) > 0
     for x, y in zip(ga, gb):
         assert np.array_equal(x, y)
+
+
+def test_compact_rows_when_lanes_walk_their_deques(monkeypatch):
+    """Placed rows whose lane count comes from the deque walk: with 4 LDS entries per lane
+    (SDH_RATCHET_ML=4) and falling runs of 12-40 prices every partial stays pending until one high
+    price matches them all, so a lane pops past its first round's four compares, through the LDS ring
+    into the spill ring. The placed rows must equal the table path's (SDH_NO_PLACE on the second
+    engine), restated from its poll."""
+    import os
+    from siddhi_amd.workloads import TS0, c2_app
+    monkeypatch.setenv("SDH_RATCHET_ML", "4")
+    a, b = _engines(c2_app(64))
+    monkeypatch.delenv("SDH_RATCHET_ML")
+    rng = np.random.default_rng(7)
+    price = []
+    while len(price) < 30000:
+        run = int(rng.integers(12, 41))
+        top = float(rng.uniform(60.0, 99.0))
+        price += list(np.linspace(top, top - rng.uniform(5, 40), run)) + [99.99]
+    price = np.asarray(price[:30000], np.float32)
+    n = len(price)
+    ts = TS0 + np.arange(n, dtype=np.int64)
+    cols = [np.zeros(n, np.int32), price.view(np.uint32), np.ones(n, np.int32)]
+    seq_polled = 0
+    for lo in range(0, n, 5000):
+        sl = slice(lo, lo + 5000)
+        part = [c[sl] for c in cols]
+        a.push_columns(0, ts[sl], part)
+        os.environ["SDH_NO_PLACE"] = "1"
+        try:
+            b.push_columns(0, ts[sl], part)
+        finally:
+            del os.environ["SDH_NO_PLACE"]
+        seq_base, rows = a.poll_compact()
+        q, k, t, off, words, seq, tb = b.poll(with_seq=True)
+        assert seq_base == seq_polled
+        assert len(q) > 1000
+        assert np.array_equal(rows, restate(q, off, words, seq, rows.shape[1], seq_base))
+        seq_polled = lo + 5000
+    assert a.stats().placed_pushes == n // 5000
+    assert b.stats().placed_pushes == 0

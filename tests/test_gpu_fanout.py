@@ -64,3 +64,39 @@ def test_fanout_refused_with_key_shards():
     app = App(fanout_app(0), engine_factory=lambda blob: None)
     with pytest.raises(EngineError):
         HipEngine(app.blob, stream_types=[s.attr_types for s in app.ir.streams], shard_rank=0, shard_world=2)
+
+
+def test_unregistered_string_key_fails_the_push_cleanly():
+    """A fan-out push that reaches a string key whose text hash was never registered
+    (sdh_engine_set_strings; e.g. after a restore) fails with SDH_E_INVALID before any kernel runs:
+    the engine stays usable, and once the strings are registered the same push goes through and the
+    run equals the oracle."""
+    from siddhi_amd.engine import EngineError
+    from siddhi_amd.events import encode_rows
+    src = fanout_app(3, "string")
+    ev = fanout_events(5, n=800, keys=30, key_type="string")
+    o, g = App(src), hip_app(src)
+    _send([o], ev, True)
+    n_slots = lambda q: len(g.ir.queries[q].states)  # noqa: E731
+    got, refused = [], 0
+    i = 0
+    while i < len(ev):
+        j = i + 1
+        while j < len(ev) and ev[j][0] == ev[i][0] and j - i < 64:
+            j += 1
+        si = g.ir.stream_index(ev[i][0])
+        vals, nulls = encode_rows([r for _, r, _ in ev[i:j]], g.ir.streams[si].attr_types, g.dictionary)
+        ts = [t for _, _, t in ev[i:j]]
+        try:
+            g.engine.send(si, ts, vals, nulls)
+        except EngineError as ex:
+            assert ex.code == -1 and "sdh_engine_set_strings" in str(ex)
+            refused += 1
+            ids = list(range(len(g.dictionary)))
+            g.engine.set_strings(ids, [g.dictionary.lookup(k) for k in ids])
+            g.engine.send(si, ts, vals, nulls)
+        got.extend(g.engine.take_matches(n_slots))
+        i = j
+    assert refused >= 1  # (each new string key refuses one push until it is registered)
+    assert len(o.matches) > 20
+    assert got == o.matches
