@@ -124,7 +124,7 @@ struct LaneOut {
 template <int CAPW_>
 struct WaveOutT {
   static constexpr int CAPW = CAPW_;
-  static constexpr int CAPR = CAPW / 7 + 1;    // records (>= 7 words each)
+  static constexpr int CAPR = CAPW / 4 + 1;    // records (>= 4 words each: K_part's narrow ones)
   struct Shared {
     int64_t buf[CAPW];
     int32_t roff[CAPR];

@@ -77,9 +77,13 @@ extern "C" hipError_t sdh_append_chain(const int64_t* src, const int64_t* seg_of
                                        const int64_t* dst_off, int rec_words, int n_items, const int32_t* qinfo,
                                        int64_t seq_ref, const int32_t* out_rank, int n_streams, sdh::MatchTable T,
                                        int64_t row0, int64_t word0, hipStream_t s);
+extern "C" size_t sdh_gen_words_temp_bytes(int64_t n_rec);
+extern "C" hipError_t sdh_gen_words(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t* tw, void* temp,
+                                    size_t temp_bytes, hipStream_t s);
 extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t seq_ref,
-                                     const int32_t* out_rank, const int32_t* fan_rank, int n_streams,
-                                     sdh::MatchTable T, int64_t row0, int64_t word0, hipStream_t s);
+                                     const int32_t* out_rank, const int32_t* fan_rank, int n_streams, sdh::MatchTable T,
+                                     int64_t row0, int64_t word0, const int64_t* woff, const int64_t* bts,
+                                     int64_t seq_base, int bstream, const int64_t* const* qkeys, hipStream_t s);
 extern "C" hipError_t sdh_new_keys(const uint32_t* uniq, const int32_t* nruns, int64_t max_runs, const int32_t* off,
                                    const int32_t* idx_s, const int64_t* key_of_id, int64_t old_n, int64_t new_n,
                                    int64_t* out, hipStream_t s);
@@ -823,7 +827,10 @@ struct sdh_engine {
   int64_t g_out_cap = 0;             // K_gen match record words per push
   DevBuf<unsigned long long> g_out_next;
   DevBuf<unsigned long long> g_nrec;
-  DevBuf<int64_t> g_rec_off;         // word offset of each K_gen / K_seq record of the last push
+  DevBuf<int64_t> g_rec_off;         // word offset of each K_gen / K_seq / K_part record of the last push
+  DevBuf<int64_t> g_tw;              // their table words, scanned (append_gen)
+  DevBuf<uint8_t> g_twtemp;
+  DevBuf<const int64_t*> d_qkeys;    // [query] its partition's key table (narrow K_part records)
   DevBuf<unsigned long long> g_rec_next;
   int64_t g_dev_matches = 0;         // K_gen / K_seq matches of the last push
   int64_t g_used = 0;                // words of the last push's records in g_out (normal mode)
@@ -989,18 +996,34 @@ void append_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base) {
   e->mt.n_lo = std::max(e->mt.n_lo, 1);
 }
 
-// the last push's K_gen / K_seq records -> table (the record words are copied whole)
-void append_gen(sdh_engine* e) {
-  const int64_t n_rec = e->g_dev_matches, used = e->g_used;
+// the last push's K_gen / K_seq / K_part records -> table: each record's table words (narrow K_part
+// records expand), scanned, then the rows. bts / seq_base / stream: the push's batch (narrow records
+// take their trigger's ts from it); null for a time advance (timer records only)
+void append_gen(sdh_engine* e, const int64_t* bts, int64_t seq_base, int stream) {
+  const int64_t n_rec = e->g_dev_matches;
   if (n_rec == 0) return;
-  table_reserve(e, n_rec, used);
-  HIPCHK(hipMemcpyAsync(e->mt.words.p + e->mt.nw, e->g_out.p, (size_t)used * 8, hipMemcpyDeviceToDevice, e->stream));
+  e->g_tw.ensure((size_t)n_rec + 1);
+  e->g_twtemp.ensure(sdh_gen_words_temp_bytes(n_rec));
+  HIPCHK(sdh_gen_words(e->g_out.p, e->g_rec_off.p, n_rec, e->g_tw.p, e->g_twtemp.p, e->g_twtemp.n, e->stream));
+  int64_t words = 0;
+  HIPCHK(hipMemcpyAsync(&words, e->g_tw.p + n_rec, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  table_reserve(e, n_rec, words);
+  // per query its partition's key table (narrow records carry the key's dense id)
+  const size_t nq = std::max<size_t>(1, e->prog.q.size());
+  std::vector<const int64_t*> qk(nq, nullptr);
+  for (const auto& g : e->gq)
+    if (g.partition >= 0 && g.partition < (int)e->routes.size() && e->routes[g.partition] && g.qid >= 0 &&
+        (size_t)g.qid < nq)
+      qk[(size_t)g.qid] = e->routes[g.partition]->key_of_id.p;
+  e->d_qkeys.ensure(nq);
+  HIPCHK(hipMemcpyAsync(e->d_qkeys.p, qk.data(), nq * sizeof(void*), hipMemcpyHostToDevice, e->stream));
   HIPCHK(sdh_append_gen(e->g_out.p, e->g_rec_off.p, n_rec, e->seq_ref, e->d_out_rank.p,
                         e->has_fanout ? e->d_fan_rank.p : nullptr, (int)e->prog.stream_types.size(), table_view(e),
-                        e->mt.n, e->mt.nw, e->stream));
+                        e->mt.n, e->mt.nw, e->g_tw.p, bts, seq_base, stream, e->d_qkeys.p, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   e->mt.n += n_rec;
-  e->mt.nw += used;
+  e->mt.nw += words;
   // timer records: (key, query, time); fan-out records: (position, rank, emission)
   e->mt.n_lo = std::max(e->mt.n_lo, e->has_absent || e->has_fanout ? 3 : 1);
 }
@@ -2488,7 +2511,7 @@ sdh::GenLaunch gen_launch_base(sdh_engine* e, const sdh_engine::GenSet& gs, cons
   L.err = e->d_err.p;
   L.rec_count = e->g_nrec.p;
   L.rec_off = e->g_rec_off.p;
-  L.rec_cap = e->g_out_cap / 7 + 1;
+  L.rec_cap = e->g_out_cap / 4 + 1;
   L.rec_next = e->g_rec_next.p;
   L.write_records = write ? 1 : 2;
   L.start_ts = e->start_ts;
@@ -2606,7 +2629,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
         Q.out_next = e->g_out_next.p;
         Q.rec_count = e->g_nrec.p;
         Q.rec_off = e->g_rec_off.p;
-        Q.rec_cap = e->g_out_cap / 7 + 1;
+        Q.rec_cap = e->g_out_cap / 4 + 1;
         Q.rec_next = e->g_rec_next.p;
         Q.err = e->d_err.p;
         const int64_t starts = n + Q.tail_len;
@@ -2854,7 +2877,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       P.out_next = e->g_out_next.p;
       P.rec_count = e->g_nrec.p;
       P.rec_off = e->g_rec_off.p;
-      P.rec_cap = e->g_out_cap / 7 + 1;
+      P.rec_cap = e->g_out_cap / 4 + 1;
       P.rec_next = e->g_rec_next.p;
       P.write_records = write ? 1 : 2;
       if (!write && getenv("SDH_DEBUG_COUNT_ONLY")) P.write_records = 0;  // (measurement experiments)
@@ -2953,7 +2976,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       S.out_next = e->g_out_next.p;
       S.rec_count = e->g_nrec.p;
       S.rec_off = e->g_rec_off.p;
-      S.rec_cap = e->g_out_cap / 7 + 1;
+      S.rec_cap = e->g_out_cap / 4 + 1;
       S.rec_next = e->g_rec_next.p;
       S.write_records = write ? 1 : 2;
       S.err = e->d_serr.p + 4 * si;
@@ -3027,7 +3050,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   std::vector<int32_t> perr(4 * std::max<size_t>(1, nps), 0);
   for (int attempt = 0;; ++attempt) {
     e->g_out.ensure((size_t)e->g_out_cap);
-    e->g_rec_off.ensure((size_t)(e->g_out_cap / 7 + 1));  // a record has at least 7 words
+    e->g_rec_off.ensure((size_t)(e->g_out_cap / 4 + 1));  // a record has at least 4 words (narrow K_part records)
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
     HIPCHK(hipMemsetAsync(e->d_perr.p, 0, perr.size() * 4, e->stream));
     HIPCHK(hipMemsetAsync(e->d_serr.p, 0, serr.size() * 4, e->stream));
@@ -3342,7 +3365,7 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
       const int64_t n0 = e->mt.n;
       append_chain(e);
       append_ratchet(e, B.ts, B.seq_base);
-      append_gen(e);
+      append_gen(e, B.ts, B.seq_base, stream);
       if (e->ck.active) chunk_rows(e, n0);
     }
   }
@@ -3724,7 +3747,7 @@ void time_advance(sdh_engine* e, int64_t t) {
   e->advance_to = INT64_MIN;
   if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) && e->g_dev_matches) {
     placed_to_table(e);
-    append_gen(e);
+    append_gen(e, nullptr, 0, 0);
   }
 }
 

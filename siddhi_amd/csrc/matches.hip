@@ -232,21 +232,91 @@ __global__ __launch_bounds__(256) void append_chain_kernel(
   }
 }
 
-// K_gen / K_seq records [len, qid, key, ts, seq, idx, S | stream << 16, (count, seqs...) x S] ->
-// table rows; the record words themselves are copied whole into the table's word area (word0 + o)
+// The table words each record of a push takes (tw[n_rec] = 0, for the exclusive scan): a K_gen / K_seq
+// record [len, qid, key, ts, seq, idx, S | stream << 16, (count, seqs...) x S] its slot words, a
+// narrow K_part record (nfa_types.h) its slots expanded to that form
+__device__ __forceinline__ int32_t lo32(int64_t w) { return (int32_t)(uint32_t)(uint64_t)w; }
+__device__ __forceinline__ int32_t hi32(int64_t w) { return (int32_t)(uint32_t)((uint64_t)w >> 32); }
+
+__global__ __launch_bounds__(256) void gen_rec_words_kernel(const int64_t* __restrict__ out,
+                                                            const int64_t* __restrict__ rec_off, int64_t n_rec,
+                                                            int64_t* __restrict__ tw) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n_rec) return;
+  if (i == n_rec) {
+    tw[i] = 0;
+    return;
+  }
+  const int64_t* r = out + rec_off[i];
+  const int32_t l0 = lo32(r[0]);
+  if (l0 >= 0) {
+    tw[i] = r[0] - 7;
+  } else if ((-l0) >> 16) {  // count: (1, e1), (c, chain), (1, trigger)
+    tw[i] = 5 + hi32(r[2]);
+  } else {                   // or / and: (1, e1), then per side (1, seq) or (0)
+    tw[i] = 2 + (hi32(r[2]) == INT32_MIN ? 1 : 2) + (lo32(r[3]) == INT32_MIN ? 1 : 2);
+  }
+}
+
+// the push's records -> table rows, each row's words at word0 + woff[i] (gen_rec_words_kernel, scanned).
+// Narrow records take the trigger's ts from the batch (bts[offset]), their key from the partition's key
+// table (qkeys[query][key id]) and e1's seq as the emission index.
 __global__ __launch_bounds__(256) void append_gen_kernel(const int64_t* __restrict__ out,
                                                          const int64_t* __restrict__ rec_off, int64_t n_rec,
                                                          int64_t seq_ref, const int32_t* __restrict__ out_rank,
                                                          const int32_t* __restrict__ fan_rank, int n_streams,
-                                                         MatchTable T, int64_t row0, int64_t word0) {
+                                                         MatchTable T, int64_t row0, int64_t word0,
+                                                         const int64_t* __restrict__ woff,
+                                                         const int64_t* __restrict__ bts, int64_t seq_base,
+                                                         int bstream, const int64_t* const* __restrict__ qkeys) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_rec) return;
-  const int64_t o = rec_off[i];
-  const int64_t* r = out + o;
-  const int q = (int)r[1], stream = (int)((r[6] >> 16) & 0xFFFF);
+  const int64_t* r = out + rec_off[i];
   const int64_t row = row0 + i;
-  T.seq[row] = r[4];
+  const int64_t wo = word0 + woff[i];
+  int64_t* w = T.words + wo;
+  T.woff[row] = wo;
   static_assert(MAXLO >= 3, "timer tiebreaks");
+  const int32_t l0 = lo32(r[0]);
+  if (l0 < 0) {  // narrow K_part record
+    const bool count = ((-l0) >> 16) != 0;
+    const int q = hi32(r[0]);
+    const int64_t off = (int64_t)(uint32_t)lo32(r[1]);
+    const uint32_t kid = (uint32_t)hi32(r[1]);
+    const int64_t sq = seq_base + off, e1 = sq - lo32(r[2]);
+    T.seq[row] = sq;
+    T.hi[row] = hi_key(sq, seq_ref, out_rank[(int64_t)q * n_streams + bstream]);
+    T.lo[0][row] = (uint64_t)e1;
+    T.lo[1][row] = 0ull;
+    T.lo[2][row] = 0ull;
+    T.q[row] = q;
+    T.key[row] = qkeys[q][kid];
+    T.ts[row] = bts[off];
+    int k = 0;
+    w[k++] = 1;
+    w[k++] = e1;
+    if (count) {
+      const int c = hi32(r[2]);
+      w[k++] = c;
+      for (int j = 0; j < c; ++j) w[k++] = sq - (j & 1 ? hi32(r[3 + j / 2]) : lo32(r[3 + j / 2]));
+      w[k++] = 1;
+      w[k++] = sq;
+    } else {
+      for (int s = 0; s < 2; ++s) {
+        const int32_t d = s == 0 ? hi32(r[2]) : lo32(r[3]);
+        if (d == INT32_MIN) {
+          w[k++] = 0;
+        } else {
+          w[k++] = 1;
+          w[k++] = sq - d;
+        }
+      }
+    }
+    T.wlen[row] = k;
+    return;
+  }
+  const int q = (int)r[1], stream = (int)((r[6] >> 16) & 0xFFFF);
+  T.seq[row] = r[4];
   if (stream == 0xFFFF) {
     // an absent state's timer match (nfa_gen.hip): rank 0, before the trigger event's own matches;
     // then by (timer key, query, partition key) -- later lo passes are more significant -- and one
@@ -271,8 +341,9 @@ __global__ __launch_bounds__(256) void append_gen_kernel(const int64_t* __restri
   T.q[row] = q;
   T.key[row] = r[2];
   T.ts[row] = r[3];
-  T.woff[row] = word0 + o + 7;
-  T.wlen[row] = r[0] - 7;
+  const int64_t len = r[0] - 7;
+  T.wlen[row] = len;
+  for (int64_t k = 0; k < len; ++k) w[k] = r[7 + k];
 }
 
 // Chunk delivery keys (nfa_types.h MatchTable chi / clo) of rows [r0, r1).
@@ -380,12 +451,28 @@ extern "C" hipError_t sdh_append_chain(const int64_t* src, const int64_t* seg_of
   return hipGetLastError();
 }
 
+// table words per record (tw, n_rec + 1 entries) scanned in place (tw[n_rec] = the total), so the
+// host can reserve the table's words before sdh_append_gen
+extern "C" size_t sdh_gen_words_temp_bytes(int64_t n_rec) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum((void*)nullptr, b, (int64_t*)nullptr, (int64_t*)nullptr, (int)(n_rec + 1));
+  return b + 256;
+}
+extern "C" hipError_t sdh_gen_words(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t* tw, void* temp,
+                                    size_t temp_bytes, hipStream_t s) {
+  if (n_rec <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::gen_rec_words_kernel, dim3(sdh::grid(n_rec + 1, 256)), dim3(256), 0, s, out, rec_off, n_rec, tw);
+  size_t tb = temp_bytes;
+  return hipcub::DeviceScan::ExclusiveSum(temp, tb, tw, tw, (int)(n_rec + 1), s);
+}
+
 extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t seq_ref,
                                      const int32_t* out_rank, const int32_t* fan_rank, int n_streams, MatchTable T,
-                                     int64_t row0, int64_t word0, hipStream_t s) {
+                                     int64_t row0, int64_t word0, const int64_t* woff, const int64_t* bts,
+                                     int64_t seq_base, int bstream, const int64_t* const* qkeys, hipStream_t s) {
   if (n_rec <= 0) return hipSuccess;
   hipLaunchKernelGGL(sdh::append_gen_kernel, dim3(sdh::grid(n_rec, 256)), dim3(256), 0, s, out, rec_off, n_rec,
-                     seq_ref, out_rank, fan_rank, n_streams, T, row0, word0);
+                     seq_ref, out_rank, fan_rank, n_streams, T, row0, word0, woff, bts, seq_base, bstream, qkeys);
   return hipGetLastError();
 }
 

@@ -40,6 +40,7 @@ __device__ __forceinline__ bool ev_filter(const kg::GQuery* q, const kg::GQuery*
 // K_part with the shape's filters interpreted (the bytecode walked per event)
 struct PartInterp {
   static constexpr int kRegEntries = 0, kEW = 1;  // the whole table in the global state block
+  static constexpr bool kHotRegs = false;         // (GMAXNA-wide hot rows would not stay in VGPRs)
   static constexpr int kNA = kg::GMAXNA, kOutW = 1536;
   struct K {};
   __device__ static void load(K&, const kg::GQuery*, const PartLaunch&, const int64_t*) {}

@@ -313,6 +313,22 @@ constexpr int PK_CMAX = 8;     // count <min:max> with max <= PK_CMAX on K_part
 // count-kind entry words: ts1, seq1, flags (len | inL3 << 8 | null bits << 16), chain[max], then
 // the captured words the e3 filter reads: e1's, the chain's first event's, its last event's
 
+// K_part's narrow match record (int64 words; beside K_gen-format records in the same buffer -- a
+// K_gen record's first word is its positive length, a narrow one's low half is minus its length):
+//   w0 = (uint32)(-words) | qid << 32
+//   w1 = (uint32)(trigger seq - the batch's seq_base) | key id << 32
+//   then int32 seq distances back from the trigger, two per word:
+//     PK_OR / PK_AND: e1, side A, side B (INT32_MIN: the side is empty), pad      -> 4 words (32 B)
+//     PK_COUNT:       e1, chain length c, the chain's c events (e3 is the trigger) -> 3 + ceil(c / 2)
+// The table append (matches.hip) restores the K_gen row: ts from the batch, the key from the
+// partition's key table, emission index = e1's seq (the pending-list order is the creation order).
+// A match whose distances do not fit int32 goes out as a K_gen record instead.
+constexpr int NREC_ORAND_WORDS = 4;
+__host__ __device__ inline int nrec_count_words(int c) { return 3 + (c + 1) / 2; }
+__host__ __device__ inline int64_t nrec_pack(int64_t lo, int64_t hi) {
+  return (int64_t)(((uint64_t)(uint32_t)(int32_t)lo) | ((uint64_t)(uint32_t)(int32_t)hi << 32));
+}
+
 struct PartLaunch {
   const kg::GQuery* queries;
   const int32_t* lane_q;      // [group][64]

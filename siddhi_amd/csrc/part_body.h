@@ -138,6 +138,20 @@ struct PartTable {
     const GRef d = gref(w);
     for (int x = 0; x < words; ++x) d.set(x, src.get(x));
   }
+  // word x of entry kk
+  __device__ int64_t get(int kk, int x) const {
+    if constexpr (RC > 0) {
+      if (kk < RC) {
+        int64_t v = r[0][0];
+#pragma unroll
+        for (int t = 0; t < RC; ++t)
+#pragma unroll
+          for (int y = 0; y < EW; ++y) v = (kk == t && x == y) ? r[t][y] : v;
+        return v;
+      }
+    }
+    return gref(kk).get(x);
+  }
   // one word of entry w
   __device__ void set(int w, int x, int64_t v) {
     if constexpr (RC > 0) {
@@ -150,6 +164,35 @@ struct PartTable {
       }
     }
     gref(w).set(x, v);
+  }
+};
+
+// A count partial's hot words in registers -- ts, seq, flags, then e1's, the chain's first and last
+// event's captured words (what f3 and the chain updates read) -- with its chain of seqs (written
+// once per appended event, read once by a match) in the lane's global block. get / set take the
+// entry's word index (PartOffs layout), so f3 reads it as PartEnt reads any entry.
+template <int HMAX>
+struct HotRef {
+  int64_t* h;   // [HMAX] registers: word w < 3 at h[w], word o_e1 + j at h[3 + j] (HMAX 0: none, all global)
+  int64_t* g;   // the entry's global words (word w at g[w * 64])
+  int o_e1;
+  __device__ int slot(int w) const { return w < 3 ? w : 3 + (w - o_e1); }
+  __device__ int64_t get(int w) const {
+    if (HMAX == 0 || (w >= 3 && w < o_e1)) return g[(int64_t)w * 64];
+    const int s = slot(w);
+    int64_t v = h[0];
+#pragma unroll
+    for (int x = 1; x < HMAX; ++x) v = (s == x) ? h[x] : v;
+    return v;
+  }
+  __device__ void set(int w, int64_t v) const {
+    if (HMAX == 0 || (w >= 3 && w < o_e1)) {
+      g[(int64_t)w * 64] = v;
+      return;
+    }
+    const int s = slot(w);
+#pragma unroll
+    for (int x = 0; x < HMAX; ++x) h[x] = (s == x) ? v : h[x];
   }
 };
 
@@ -205,7 +248,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
   tab.ew = ew;
   int n = (int)in[0];
   const int64_t hdr1 = in[64];
-  {
+  if constexpr (KIND != PK_COUNT) {  // (the count tables are read entry by entry, count_tile below)
     const GRef src{const_cast<int64_t*>(in) + PK_HDR * 64};
     for (int kk = 0; kk < n; ++kk) {
       const GRef e{src.p + (int64_t)kk * ew * 64};
@@ -233,6 +276,158 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
   const int sA = L.sA;
   int F = (int)(hdr1 & 0xffffffff), side = (int)(hdr1 >> 32);  // logical: filled prefix and its side
 
+  // ---- PK_COUNT, entry-major: each partial is loaded once per event tile, run through the tile's
+  // events in registers (its chain appended to its global slot), and stored once, compacted in
+  // creation order; the partials the tile's events open follow, each from the event after its own.
+  // A partial's fate depends on the events and its own words only (f1 / f2 read the event, f3 the
+  // event and the partial), so this is the event-major walk of the reference (every event visits
+  // the e3 list, then the count list, then e1) reordered, with the same result: a partial matches
+  // at the first event it completes on, and the matches of one event keep the pending-list order
+  // (emission index = e1's seq, increasing along the list). (The OR / AND tables above stay
+  // event-major: their state is small and their output is per event.)
+  const bool nb_ok = L.b.n < (int64_t)INT32_MAX;  // batch offsets fit a narrow record's int32
+  auto count_tile = [&](int cnt, bool first_tile) {
+    // the hot words in registers (shape-compiled kernels), or in the entry's global slot (the
+    // interpreter, whose rows are GMAXNA wide)
+    constexpr int HMAX = Spec::kHotRegs ? 3 + 3 * Spec::kNA : 0;
+    const int nh = 3 + of.n_e1 + of.n_first + of.n_last;
+    auto hot_word = [&](int x) { return x < 3 ? x : of.o_e1() + x - 3; };
+    uint64_t m1 = 0, m2 = 0;  // the tile's events passing f1 / f2 (this lane's query)
+    if (live)
+      for (int te = 0; te < cnt; ++te) {
+        const PartEv ev{&t_w[0][te], t_nul[te]};
+        if (Spec::f1(k, q, ql, L, ev)) m1 |= 1ull << te;
+        if (Spec::f2(k, q, ql, L, ev)) m2 |= 1ull << te;
+      }
+    int wmax = n;
+    for (int o2 = 32; o2 > 0; o2 >>= 1) wmax = max(wmax, __shfl_xor(wmax, o2));
+    const int64_t* __restrict__ src = (first_tile ? in : st) + PK_HDR * 64;
+    int64_t* __restrict__ dst = st + PK_HDR * 64;
+    int wpos = 0;             // entries kept so far: slots 0 .. wpos-1 of dst
+    // one partial per lane and call (collective: the call's record emit): the lane's entry kk held
+    // before the tile (kk >= 0), or the one event tc opens (kk < 0); has: the lane has it
+    auto run = [&](bool has, int kk, int tc) {
+      if (has && wpos >= L.cap) {  // no slot for it: the push re-runs exactly with a larger table
+        cap_over = true;
+        has = false;
+      }
+      int64_t h[HMAX > 0 ? HMAX : 1];
+#pragma unroll
+      for (int x = 0; x < (HMAX > 0 ? HMAX : 1); ++x) h[x] = 0;
+      int64_t* gd = dst + (int64_t)wpos * ew * 64;  // the partial's slot if it survives the tile
+      const HotRef<HMAX> e{h, gd, of.o_e1()};
+      int te0 = cnt, len = 0;
+      bool inL3 = false;
+      int64_t fl = 0;
+      if (has && kk < 0) {  // opened by event tc: in the lists from the next event on
+        const PartEv ev{&t_w[0][tc], t_nul[tc]};
+        e.set(0, t_ts[tc]);
+        e.set(1, t_seq[tc]);
+        for (int j = 0; j < of.n_e1; ++j) e.set(of.o_e1() + j, ev.word(j));
+        fl = (int64_t)(ev.nul & 0xff) << 16;  // e1's null bits
+        te0 = tc + 1;
+      } else if (has) {
+        const int64_t* gs = src + (int64_t)kk * ew * 64;
+        if constexpr (HMAX > 0) {
+#pragma unroll
+          for (int x = 0; x < HMAX; ++x)
+            if (x < nh) h[x] = gs[(int64_t)hot_word(x) * 64];
+        } else if (gs != gd) {
+          for (int x = 0; x < nh; ++x) gd[(int64_t)hot_word(x) * 64] = gs[(int64_t)hot_word(x) * 64];
+        }
+        fl = e.get(2);
+        len = (int)(fl & 0xff);
+        inL3 = (fl >> 8) & 1;
+        if (gs != gd)
+          for (int c = 0; c < len; ++c) gd[(int64_t)(3 + c) * 64] = gs[(int64_t)(3 + c) * 64];
+        te0 = live ? 0 : cnt;
+      }
+      bool alive = has && te0 < cnt;
+      int done = -1;  // the event the partial completes on
+      // (wave-uniform bounds: from the earliest first event of the wave's partials, until none lives)
+      int tstart = alive ? te0 : cnt;
+      for (int o2 = 32; o2 > 0; o2 >>= 1) tstart = min(tstart, __shfl_xor(tstart, o2));
+      for (int te = tstart; te < cnt; ++te) {
+        if (!__ballot(alive)) break;
+        if (!alive || te < te0) continue;
+        const PartEv ev{&t_w[0][te], t_nul[te]};
+        // e3 first: expiry, then f3 over the partial as it is now
+        if (inL3) {
+          if (dev::expired(e.get(0), t_ts[te], within)) {
+            inL3 = false;
+          } else if (Spec::f3(k, q, ql, L, ev, part_ent(e, fl, of))) {
+            done = te;
+            alive = false;
+            continue;
+          }
+        }
+        // count state: a partial with len < max appends every f2-passing event
+        if (len < cmax && ((m2 >> te) & 1)) {
+          gd[(int64_t)(3 + len) * 64] = t_seq[te];
+          const int64_t nb = (int64_t)(ev.nul & 0xff);
+          if (len == 0) {
+            for (int j = 0; j < of.n_first; ++j) e.set(of.o_first() + j, ev.word(j));
+            fl = (fl & ~(0xffll << 24)) | (nb << 24);
+          }
+          for (int j = 0; j < of.n_last; ++j) e.set(of.o_last() + j, ev.word(j));
+          fl = (fl & ~(0xffll << 32)) | (nb << 32);
+          ++len;
+          if (len == cmin) inL3 = true;  // CountPost: next.addState at n == min (visible next event)
+        }
+        if (!inL3 && len >= cmax) alive = false;  // in neither list any more
+      }
+      if (done >= 0) ++nrec;
+      if (L.write_records && __ballot(done >= 0)) {
+        // the narrow record (nfa_types.h) when e1's distance fits int32, else the K_gen record
+        // [words, qid, key, ts, seq, idx, 3 | stream, (1, e1), (len, chain...), (1, seq)]
+        const int64_t sq = done >= 0 ? t_seq[done] : 0;
+        const int64_t e1s = e.get(1);
+        const bool nar = nb_ok && sq - e1s <= (int64_t)INT32_MAX;
+        const int words = nar ? nrec_count_words(len) : 7 + 2 + 1 + len + 2;
+        o.emit_n(done >= 0 ? 1 : 0, words, [&](int64_t* r) {
+          if (nar) {
+            r[0] = nrec_pack(-(words + 0x10000), qid);
+            r[1] = nrec_pack(sq - L.b.seq_base, (int64_t)kid);
+            r[2] = nrec_pack(sq - e1s, len);
+            for (int c = 0; c < len; c += 2)
+              r[3 + c / 2] = nrec_pack(sq - gd[(int64_t)(3 + c) * 64], c + 1 < len ? sq - gd[(int64_t)(4 + c) * 64] : 0);
+            return;
+          }
+          r[0] = words;
+          r[1] = qid;
+          r[2] = key;
+          r[3] = t_ts[done];
+          r[4] = sq;
+          r[5] = e1s;  // emission index: e1's seq (the pending-list order)
+          r[6] = 3 | (stream << 16);
+          r[7] = 1;
+          r[8] = e1s;
+          r[9] = len;
+          for (int c = 0; c < len; ++c) r[10 + c] = gd[(int64_t)(3 + c) * 64];
+          r[10 + len] = 1;
+          r[11 + len] = sq;
+        });
+      }
+      // kept: alive at the tile's end, or not run at all (opened by the tile's last event, or a lane
+      // without a query)
+      if (has && (alive || (done < 0 && te0 >= cnt))) {
+        e.set(2, (fl & ~0x1ffll) | (int64_t)len | ((int64_t)inL3 << 8));
+        if constexpr (HMAX > 0) {
+#pragma unroll
+          for (int x = 0; x < HMAX; ++x)
+            if (x < nh) gd[(int64_t)hot_word(x) * 64] = h[x];
+        }
+        ++wpos;
+      }
+    };
+    // the entries held before the tile all start at its first event; the new ones, grouped by the
+    // event that opens them, start together too (a wave's lanes run the same events)
+    for (int kk = 0; kk < wmax; ++kk) run(kk < n, kk, 0);
+    for (int tc = 0; tc < cnt; ++tc)
+      if (__ballot((m1 >> tc) & 1)) run((m1 >> tc) & 1, -1, tc);
+    n = wpos;
+  };
+
   PPROF_T(c_setup);
   PPROF_ADD(0, c_setup - c_start);
   for (int64_t t0 = e0; t0 < e1; t0 += 64) {
@@ -253,6 +448,9 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
     __syncthreads();
     PPROF_T(c_t1);
     PPROF_ADD(1, c_t1 - c_t0);
+    if constexpr (KIND == PK_COUNT) {
+      count_tile(cnt, t0 == e0);
+    } else {
     for (int te = 0; te < cnt && live; ++te) {
       const int64_t seq = t_seq[te];
       const int64_t ts = t_ts[te];
@@ -296,9 +494,23 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
             }
           }
         };
+        // the narrow record (nfa_types.h): slots by state id, 0 = e1, sA = side A, the other side B
+        auto put_nrec = [&](int64_t* r, int64_t e1seq, int64_t a_seq, int64_t b_seq) {
+          const int64_t s1 = sA == 1 ? a_seq : b_seq, s2 = sA == 1 ? b_seq : a_seq;
+          r[0] = nrec_pack(-NREC_ORAND_WORDS, qid);
+          r[1] = nrec_pack(seq - L.b.seq_base, (int64_t)kid);
+          r[2] = nrec_pack(seq - e1seq, s1 >= 0 ? seq - s1 : (int64_t)INT32_MIN);
+          r[3] = nrec_pack(s2 >= 0 ? seq - s2 : (int64_t)INT32_MIN, 0);
+        };
+        // narrow unless a lane's oldest partial is 2^31 events back (one record width per call: the
+        // collective emit is uniform)
+        auto narrow_ok = [&](int c) {
+          return !__ballot(c > 0 && !(nb_ok && seq - tab.get(0, 1) <= (int64_t)INT32_MAX));
+        };
         // The lane's matches of this event are the first c partials of its list (see the two cases
         // below): their records go out in one collective reservation, record kk at r0 + kk * words
-        // with emission index kk (the pending-list order)
+        // with emission index kk (the pending-list order; the narrow form's index is e1's seq, the
+        // same order)
         (void)idx;
         if constexpr (KIND == PK_OR) {
           // side B first (its processor runs first), then side A; either empties the list
@@ -306,9 +518,14 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
             nrec += n;
             if (L.write_records) {
               const int64_t as = fb ? -1 : seq, bs = fb ? seq : -1;  // words: 7 + 2 + 2 + 1
-              o.emit_n(n, 12, [&](int64_t* r0) {
-                tab.each(n, [&](int kk, const auto& e) { put_rec(r0 + kk * 12, 12, kk, e.get(1), as, bs); });
-              }, true);
+              if (narrow_ok(n))
+                o.emit_n(n, NREC_ORAND_WORDS, [&](int64_t* r0) {
+                  tab.each(n, [&](int kk, const auto& e) { put_nrec(r0 + kk * NREC_ORAND_WORDS, e.get(1), as, bs); });
+                }, true);
+              else
+                o.emit_n(n, 12, [&](int64_t* r0) {
+                  tab.each(n, [&](int kk, const auto& e) { put_rec(r0 + kk * 12, 12, kk, e.get(1), as, bs); });
+                }, true);
             }
             n = 0;
           }
@@ -320,12 +537,15 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
           const int c = (fa && fb) ? n : ((fb && side == 1) || (fa && side == 2)) ? F : 0;
           nrec += c;
           if (L.write_records) {
-            o.emit_n(c, 13, [&](int64_t* r0) {  // words: 7 + 2 + 2 + 2
+            const bool nar = narrow_ok(c);
+            const int words = nar ? NREC_ORAND_WORDS : 13;  // (wide: 7 + 2 + 2 + 2)
+            o.emit_n(c, words, [&](int64_t* r0) {
               tab.each(c, [&](int kk, const auto& e) {
                 const bool filled = kk < F;
                 const int64_t aseq = (filled && side == 1) ? e.get(2) : seq;
                 const int64_t bseq = (filled && side == 2) ? e.get(2) : seq;
-                put_rec(r0 + kk * 13, 13, kk, e.get(1), aseq, bseq);
+                if (nar) put_nrec(r0 + kk * NREC_ORAND_WORDS, e.get(1), aseq, bseq);
+                else put_rec(r0 + kk * 13, 13, kk, e.get(1), aseq, bseq);
               });
             }, true);
           }
@@ -357,74 +577,8 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
             cap_over = true;
           }
         }
-      } else {  // PK_COUNT
-        const bool f2 = Spec::f2(k, q, ql, L, ev);
-        const int ewc = 3 + of.cmax + of.n_e1 + of.n_first + of.n_last;
-        int w = 0;
-        tab.each(n, [&](int kk, const auto& e) {
-          int64_t fl = e.get(2);
-          int len = (int)(fl & 0xff);
-          bool inL3 = (fl >> 8) & 1;
-          // e3 (processed first): expiry, then f3 over the partial as it is now
-          if (inL3) {
-            if (dev::expired(e.get(0), ts, within)) {
-              inL3 = false;
-            } else if (Spec::f3(k, q, ql, L, ev, part_ent(e, fl, of))) {
-              // completed: removed from e3's list now, from the count list at this event
-              ++nrec;
-              if (L.write_records) {
-                const int words = 7 + 2 + 1 + len + 2;
-                const int64_t my_idx = idx++;
-                o.emit(words, [&](int64_t* r) {
-                  r[0] = words;
-                  r[1] = qid;
-                  r[2] = key;
-                  r[3] = ts;
-                  r[4] = seq;
-                  r[5] = my_idx;
-                  r[6] = 3 | (stream << 16);
-                  r[7] = 1;
-                  r[8] = e.get(1);
-                  r[9] = len;
-                  for (int c = 0; c < len; ++c) r[10 + c] = e.get(3 + c);
-                  r[10 + len] = 1;
-                  r[11 + len] = seq;
-                });
-              }
-              return;
-            }
-          }
-          // count state: a partial with len < max appends every f2-passing event
-          if (len < cmax && f2) {
-            e.set(3 + len, seq);
-            const int64_t nb = (int64_t)(ev.nul & 0xff);
-            if (len == 0) {
-              for (int j = 0; j < of.n_first; ++j) e.set(of.o_first() + j, ev.word(j));
-              fl = (fl & ~(0xffll << 24)) | (nb << 24);
-            }
-            for (int j = 0; j < of.n_last; ++j) e.set(of.o_last() + j, ev.word(j));
-            fl = (fl & ~(0xffll << 32)) | (nb << 32);
-            ++len;
-            if (len == cmin) inL3 = true;  // CountPost: next.addState at n == min (visible next event)
-          }
-          if (!inL3 && len >= cmax) return;  // in neither list any more
-          e.set(2, (fl & ~0x1ffll) | (int64_t)len | ((int64_t)inL3 << 8));
-          if (w != kk) tab.put(w, e, ewc);
-          ++w;
-        });
-        n = w;
-        if (f1) {
-          if (n < L.cap) {
-            tab.set(n, 0, ts);
-            tab.set(n, 1, seq);
-            for (int j = 0; j < of.n_e1; ++j) tab.set(n, of.o_e1() + j, ev.word(j));
-            tab.set(n, 2, (int64_t)(ev.nul & 0xff) << 16);  // e1's null bits
-            ++n;
-          } else {
-            cap_over = true;
-          }
-        }
       }
+    }
     }
     __syncthreads();  // the tile is rewritten next
     PPROF_T(c_t2);
@@ -433,7 +587,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
   }
   PPROF_T(c_loop);
   // register entries back to the output block
-  if constexpr (RC > 0) {
+  if constexpr (RC > 0 && KIND != PK_COUNT) {
 #pragma unroll
     for (int kk = 0; kk < RC; ++kk)
       if (kk < n)

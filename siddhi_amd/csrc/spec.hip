@@ -64,6 +64,7 @@ const char* const kPrelude =
     "typedef __hip_internal::int64_t int64_t;\n"
     "typedef __hip_internal::uint64_t uint64_t;\n"
     "#define INT32_MIN (-2147483647 - 1)\n"
+    "#define INT32_MAX 2147483647\n"
     "#define INT64_MIN (-9223372036854775807LL - 1)\n"
     "#define INT64_MAX 9223372036854775807LL\n";
 
@@ -258,6 +259,7 @@ std::string part_source(const kg::GQuery& g, const PartLayout& lay) {
   std::string s = tuning_defines() + header() + "#include \"part_body.h\"\n\nstruct SpecPart {\n";
   int na = 1;  // captured words the tile staging holds
   for (int st = 0; st < kg::GMAXSTREAM; ++st) na = std::max(na, (int)g.n_cap[st]);
+  s += "  static constexpr bool kHotRegs = true;  // count partials' hot words in registers (part_body.h)\n";
   s += fmt("  static constexpr int kRegEntries = %d, kEW = %d, kNA = %d, kOutW = %d;\n", lay.reg_entries, lay.ew,
            std::min(na, kg::GMAXNA), env_int("SDH_KPART_OUTW", lay.out_w > 0 ? lay.out_w : 1536, 256, 4096));
   s += fmt("  __device__ static sdh::PartOffs offs(const sdh::PartLaunch&) { return sdh::PartOffs{%d, %d, %d, %d}; }\n",
