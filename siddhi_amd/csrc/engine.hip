@@ -78,6 +78,9 @@ extern "C" hipError_t sdh_append_chain(const int64_t* src, const int64_t* seg_of
                                        int64_t seq_ref, const int32_t* out_rank, int n_streams, sdh::MatchTable T,
                                        int64_t row0, int64_t word0, hipStream_t s);
 extern "C" size_t sdh_gen_words_temp_bytes(int64_t n_rec);
+extern "C" size_t sdh_sorted_batch_bytes(const sdh::StreamBatch* b);
+extern "C" hipError_t sdh_sort_batch(const sdh::StreamBatch* b, const int32_t* idx, uint8_t* buf, sdh::StreamBatch* o,
+                                     hipStream_t s);
 extern "C" hipError_t sdh_gen_words(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t* tw, void* temp,
                                     size_t temp_bytes, hipStream_t s);
 extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t seq_ref,
@@ -831,6 +834,7 @@ struct sdh_engine {
   DevBuf<int64_t> g_tw;              // their table words, scanned (append_gen)
   DevBuf<uint8_t> g_twtemp;
   DevBuf<const int64_t*> d_qkeys;    // [query] its partition's key table (narrow K_part records)
+  DevBuf<uint8_t> sb_buf;            // a batch in key order (K_part reads; sdh_sort_batch)
   DevBuf<unsigned long long> g_rec_next;
   int64_t g_dev_matches = 0;         // K_gen / K_seq matches of the last push
   int64_t g_used = 0;                // words of the last push's records in g_out (normal mode)
@@ -2840,18 +2844,28 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       any = true;
       bytes += (double)n * ev_bytes * gs.n_groups;  // every group streams its keys' events
     }
+    // K_part reads each key's events as one contiguous run of a key-ordered copy of the batch (the
+    // routing sort's order) instead of gathering them from the batch
+    sdh::StreamBatch SB{};
+    bool sorted = false;
     for (size_t si = 0; si < e->psets.size(); ++si) {
       auto& ps = *e->psets[si];
       if (ps.partition != pi) continue;
       part_grow(e, ps, hv[0]);
+      if (!sorted && !getenv("SDH_KPART_GATHER")) {
+        e->sb_buf.ensure(sdh_sorted_batch_bytes(&B));
+        HIPCHK(sdh_sort_batch(&B, e->r_idx_s.p, e->sb_buf.p, &SB, e->stream));
+        sorted = true;
+      }
       sdh::PartLaunch P{};
+      P.sorted = sorted ? 1 : 0;
       P.xcd = e->xcd;
       P.lconst = e->d_lconst.p;
       P.lc_slots = e->lc_slots;
       P.queries = e->d_gq.p;
       P.lane_q = e->d_lane_q.p;
       P.group_tmpl = e->d_group_tmpl.p;
-      P.b = B;
+      P.b = sorted ? SB : B;
       P.seg_begin = e->r_off.p;
       P.seg_len = e->r_cnt.p;
       P.seg_kid = e->r_uniq.p;

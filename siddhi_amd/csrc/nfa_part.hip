@@ -88,6 +88,21 @@ __global__ __launch_bounds__(64) void nfa_part_kernel(PartLaunch L) {
 
 // live partials (sdh_engine_stats): table entries in each key's current buffer; one thread per
 // (key, group, lane)
+// the batch in key order (position t <- batch event idx[t]): ts, every column, every null mask
+__global__ __launch_bounds__(256) void sort_batch_kernel(StreamBatch b, const int32_t* __restrict__ idx, StreamBatch o) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= b.n) return;
+  const int64_t e = idx[t];
+  const_cast<int64_t*>(o.ts)[t] = b.ts[e];
+  for (int a = 0; a < b.n_attr; ++a) {
+    const int w = b.width[a];
+    if (w == 8) ((int64_t*)o.col[a])[t] = ((const int64_t*)b.col[a])[e];
+    else if (w == 4) ((int32_t*)o.col[a])[t] = ((const int32_t*)b.col[a])[e];
+    else ((uint8_t*)o.col[a])[t] = ((const uint8_t*)b.col[a])[e];
+    if (b.nul[a]) const_cast<uint8_t*>(o.nul[a])[t] = b.nul[a][e];
+  }
+}
+
 __global__ void part_live_kernel(const int64_t* __restrict__ st, const int32_t* __restrict__ cur, int64_t n_keys,
                                  int groups, int64_t blocks, int64_t bw, unsigned long long* acc) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -102,6 +117,35 @@ __global__ void part_live_kernel(const int64_t* __restrict__ st, const int32_t* 
 }
 
 }  // namespace sdh
+
+// bytes the key-ordered copy of a batch takes (256-B aligned parts), and the copy itself: `o` gets
+// the same schema with its pointers into buf
+extern "C" size_t sdh_sorted_batch_bytes(const sdh::StreamBatch* b) {
+  size_t t = ((size_t)b->n * 8 + 255) & ~(size_t)255;
+  for (int a = 0; a < b->n_attr; ++a) {
+    t += ((size_t)b->n * b->width[a] + 255) & ~(size_t)255;
+    if (b->nul[a]) t += ((size_t)b->n + 255) & ~(size_t)255;
+  }
+  return t;
+}
+extern "C" hipError_t sdh_sort_batch(const sdh::StreamBatch* b, const int32_t* idx, uint8_t* buf, sdh::StreamBatch* o,
+                                     hipStream_t s) {
+  *o = *b;
+  size_t t = 0;
+  auto take = [&](size_t bytes) {
+    uint8_t* p = buf + t;
+    t += (bytes + 255) & ~(size_t)255;
+    return p;
+  };
+  o->ts = (const int64_t*)take((size_t)b->n * 8);
+  for (int a = 0; a < b->n_attr; ++a) {
+    o->col[a] = take((size_t)b->n * b->width[a]);
+    o->nul[a] = b->nul[a] ? take((size_t)b->n) : nullptr;
+  }
+  if (b->n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sdh::sort_batch_kernel, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0, s, *b, idx, *o);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t sdh_live_part(const int64_t* st, const int32_t* cur, int64_t n_keys, int groups, int64_t blocks,
                                     int64_t bw, unsigned long long* acc, hipStream_t s) {

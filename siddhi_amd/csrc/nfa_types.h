@@ -362,6 +362,8 @@ struct PartLaunch {
   unsigned long long* rec_next;
   int32_t write_records;
   int32_t xcd;                // items in per-XCD ranges (dev::grid_item; the grid is padded to a multiple of 8)
+  int32_t sorted;             // b holds the batch in key order (position t = ev_idx's t); ev_idx still
+                              // gives each position's batch index (its seq)
   int32_t* err;               // [0] entry capacity, [2] output overflow
   unsigned long long* prof;   // SDH_PART_PROF builds: per-phase clock sums (part_body.h), else null
   const int64_t* lconst;      // [group][lc_slots][64] the lanes' query ids, withins, constants (kg::LaneConsts)

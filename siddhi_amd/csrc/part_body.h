@@ -434,13 +434,14 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
     PPROF_T(c_t0);
     const int cnt = e1 - t0 < 64 ? (int)(e1 - t0) : 64;
     if (lane < cnt) {
-      const int64_t e = L.ev_idx[t0 + lane];
-      t_ts[lane] = L.b.ts[e];
+      // (a key-ordered copy of the batch makes the tile's reads contiguous: L.sorted)
+      const int64_t e = L.ev_idx[t0 + lane], p = L.sorted ? t0 + lane : e;
+      t_ts[lane] = L.b.ts[p];
       t_seq[lane] = L.b.seq_base + e;
       uint32_t nb = 0;
       for (int j = 0; j < ncap; ++j) {
         bool nl = false;
-        if (j < Spec::kNA) t_w[j][lane] = dev::raw_word(L.b, q->cap_attr[stream][j], e, nl);
+        if (j < Spec::kNA) t_w[j][lane] = dev::raw_word(L.b, q->cap_attr[stream][j], p, nl);
         if (nl) nb |= 1u << j;
       }
       t_nul[lane] = nb;
