@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the small-push latency leg")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline sample budget")
+    ap.add_argument("--state-reserve-gb", type=float, default=170.0,
+                    help="c5: HBM reserved up front for the sparse K_slab state (sdh_engine_reserve): the state "
+                         "grows inside it with no device allocation during the run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-calibrate", action="store_true", help="skip the HBM copy / read ceiling measurement")
     return ap.parse_args()
@@ -396,6 +399,8 @@ def main():
     eng = make_engine(args.workload, sh, K, local, SDH_FLAG_DEVICE_MATCHES, args.partials)
     if comm is not None:
         eng.set_comm(comm)
+    if c5 and args.state_reserve_gb > 0:
+        eng.reserve(int(args.state_reserve_gb * 1e9))
     t_build = time.perf_counter() - t_build
     log(f"engine built in {t_build:.1f} s")
 

@@ -193,6 +193,27 @@ typedef struct sdh_matches_compact {
   const int32_t* rows;
 } sdh_matches_compact;
 int sdh_engine_poll_compact(sdh_engine* e, int32_t device, sdh_matches_compact* out);
+/* Compact rows for every match (count-state chains, partition keys and absent-state timer matches
+ * included: StateEvent.getStreamEvent:138-182 resolves a count slot to its chain; the key is
+ * PartitionStreamReceiver.java:270-275's per-key delivery). Row i is rows[i * width .. (i + 1) * width):
+ *   { query, seq_i - seq_base, then per state slot v: v >= 0 one event (seq_i - its seq),
+ *     INT32_MIN an empty slot, v < 0 a chain: chain[-(v + 1)] = its event count c, followed by the c
+ *     distances seq_i - seq (a count slot with one event is a plain distance) },
+ * key[i] the partition key (as sdh_matches.key; NULL when no query is partitioned), tb[i] the timer
+ * tiebreak (as sdh_matches.tb; NULL when no query has absent states). Only seq distances past 2^31
+ * fail (SDH_E_UNSUPPORTED, the matches stay pending). device != 0: engine-owned HBM. */
+typedef struct sdh_matches_compact_ex {
+  int64_t n;
+  int64_t seq_base;
+  int32_t width;
+  int32_t flags;             /* 0 */
+  const int32_t* rows;
+  const int64_t* key;
+  const int64_t* tb;
+  int64_t n_chain;           /* int32 words in chain */
+  const int32_t* chain;
+} sdh_matches_compact_ex;
+int sdh_engine_poll_compact_ex(sdh_engine* e, int32_t device, sdh_matches_compact_ex* out);
 /* Device-resident match count of the last push (no host copy of the matches). */
 int sdh_engine_pending_matches(sdh_engine* e, int64_t* n);
 /* Absent patterns (`not S[..] for T`) and time. The runtime starts at t (SiddhiAppRuntime.start:
@@ -211,6 +232,11 @@ int sdh_engine_push_stats(sdh_engine* e, double* last_kernel_ms, double* last_ke
  * state only for instances that hold partials -- PartitionRuntime.java:257-306 clones per key
  * lazily): live entry bytes, reserved slab bytes, directory bytes. */
 int sdh_engine_state_bytes(sdh_engine* e, int64_t* live_bytes, int64_t* reserved_bytes, int64_t* dir_bytes);
+/* Pre-allocate `bytes` of HBM for that sparse state (split over the engine's K_slab sets), so it grows
+ * inside memory the engine already holds: a state that outgrows it takes more in chunks that double.
+ * (One large device allocation can stall for seconds; a deployment that knows its state size sizes it
+ * once here, before the first push.) No-op for an engine without K_slab sets. */
+int sdh_engine_reserve(sdh_engine* e, int64_t bytes);
 /* The text behind string dictionary ids, as String.hashCode and UTF-16 length per id. Needed only by
  * a partition keyed by a string attribute whose queries also read a stream it does not key: that
  * stream reaches every key's junction in the order of a ConcurrentHashMap of "streamId" +

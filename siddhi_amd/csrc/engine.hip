@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <tuple>
 #include <array>
 #include <cmath>
@@ -82,7 +83,14 @@ extern "C" size_t sdh_sorted_batch_bytes(const sdh::StreamBatch* b);
 extern "C" hipError_t sdh_sort_batch(const sdh::StreamBatch* b, const int32_t* idx, uint8_t* buf, sdh::StreamBatch* o,
                                      hipStream_t s);
 extern "C" hipError_t sdh_gen_words(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t* tw, void* temp,
-                                    size_t temp_bytes, hipStream_t s);
+                                    size_t temp_bytes, unsigned long long* n_wide, hipStream_t s);
+extern "C" size_t sdh_ex_temp_bytes(int64_t n);
+extern "C" hipError_t sdh_ex_chain_words(sdh::MatchTable T, const int32_t* perm, int64_t n, int64_t* cw, void* temp,
+                                         size_t temp_bytes, hipStream_t s);
+extern "C" hipError_t sdh_ex_rows(sdh::MatchTable T, const int32_t* perm, int64_t n, int width, int64_t seq_ref,
+                                  const int64_t* coff, int32_t* rows, int32_t* chain, int64_t* okey, int64_t* otb,
+                                  int32_t* err, hipStream_t s);
+extern "C" hipError_t sdh_fill_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
 extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t seq_ref,
                                      const int32_t* out_rank, const int32_t* fan_rank, int n_streams, sdh::MatchTable T,
                                      int64_t row0, int64_t word0, const int64_t* woff, const int64_t* bts,
@@ -800,9 +808,76 @@ struct sdh_engine {
     DevBuf<int64_t> d_cap;
     DevBuf<unsigned long long> head, tail, head_bak;
     std::vector<unsigned long long> h_head, h_tail, h_push0;  // h_push0: heads before the last push
+    // Ring buffers are carved from an arena of large chunks that are never returned while the engine
+    // lives: a ring that grows takes a new range and gives its old one back to the free list (adjacent
+    // free ranges merge), so growing costs no driver allocation once the arena holds enough. (A
+    // hipMalloc of GBs stalls for seconds from time to time on this driver, whether or not memory
+    // was freed; tools/alloc_probe.py.) sdh_engine_reserve sizes the arena up front.
+    struct Chunk {
+      uint8_t* base;
+      size_t bytes;
+      std::map<size_t, size_t> free;  // offset -> length
+    };
+    std::vector<Chunk> chunks;
+    size_t arena_bytes = 0;
+    bool add_chunk(size_t bytes) {
+      void* p = nullptr;
+      if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+      }
+      chunks.push_back(Chunk{(uint8_t*)p, bytes, {}});
+      chunks.back().free[0] = bytes;
+      arena_bytes += bytes;
+      return true;
+    }
+    uint32_t* take(size_t bytes) {
+      for (auto& c : chunks)
+        for (auto it = c.free.begin(); it != c.free.end(); ++it) {
+          if (it->second < bytes) continue;
+          const size_t off = it->first, len = it->second;
+          c.free.erase(it);
+          if (len > bytes) c.free[off + bytes] = len - bytes;
+          return (uint32_t*)(c.base + off);
+        }
+      return nullptr;
+    }
+    uint32_t* alloc_ring(int64_t words) {
+      const size_t bytes = ((size_t)words * 4 + 4095) & ~(size_t)4095;
+      if (uint32_t* p = take(bytes)) return p;
+      // a new chunk: as large as the arena so far (the chunks double), or what the device still has
+      size_t want = std::max(bytes, std::max(arena_bytes, (size_t)1 << 30));
+      for (;;) {
+        if (add_chunk(want)) return take(bytes);
+        if (want == bytes) return nullptr;
+        want = std::max(bytes, want / 2);
+      }
+    }
+    void free_ring(uint32_t* p, int64_t words) {
+      if (!p) return;
+      const size_t bytes = ((size_t)words * 4 + 4095) & ~(size_t)4095;
+      for (auto& c : chunks) {
+        if ((uint8_t*)p < c.base || (uint8_t*)p >= c.base + c.bytes) continue;
+        size_t off = (size_t)((uint8_t*)p - c.base), len = bytes;
+        auto nx = c.free.lower_bound(off);
+        if (nx != c.free.end() && nx->first == off + len) {
+          len += nx->second;
+          nx = c.free.erase(nx);
+        }
+        if (nx != c.free.begin()) {
+          auto pv = std::prev(nx);
+          if (pv->first + pv->second == off) {
+            off = pv->first;
+            len += pv->second;
+            c.free.erase(pv);
+          }
+        }
+        c.free[off] = len;
+        return;
+      }
+    }
     ~SlabSet() {
-      for (uint32_t* p : ring)
-        if (p) (void)hipFree(p);
+      for (auto& c : chunks) (void)hipFree(c.base);
     }
     DevBuf<long long> live, live_bak;
     DevBuf<unsigned long long> traffic;       // block bytes read + written by the last launch
@@ -833,6 +908,13 @@ struct sdh_engine {
   DevBuf<int64_t> g_rec_off;         // word offset of each K_gen / K_seq / K_part record of the last push
   DevBuf<int64_t> g_tw;              // their table words, scanned (append_gen)
   DevBuf<uint8_t> g_twtemp;
+  DevBuf<unsigned long long> g_nwide;  // K_gen-format (not narrow) records of the last append
+  // sdh_engine_poll_compact_ex outputs
+  DevBuf<int64_t> px_cw, px_key, px_tb;
+  DevBuf<int32_t> px_chain;
+  DevBuf<uint8_t> px_temp;
+  HostBuf<int64_t> hx_key, hx_tb;
+  HostBuf<int32_t> hx_chain;
   DevBuf<const int64_t*> d_qkeys;    // [query] its partition's key table (narrow K_part records)
   DevBuf<uint8_t> sb_buf;            // a batch in key order (K_part reads; sdh_sort_batch)
   DevBuf<unsigned long long> g_rec_next;
@@ -1008,8 +1090,12 @@ void append_gen(sdh_engine* e, const int64_t* bts, int64_t seq_base, int stream)
   if (n_rec == 0) return;
   e->g_tw.ensure((size_t)n_rec + 1);
   e->g_twtemp.ensure(sdh_gen_words_temp_bytes(n_rec));
-  HIPCHK(sdh_gen_words(e->g_out.p, e->g_rec_off.p, n_rec, e->g_tw.p, e->g_twtemp.p, e->g_twtemp.n, e->stream));
+  e->g_nwide.ensure(1);
+  HIPCHK(sdh_gen_words(e->g_out.p, e->g_rec_off.p, n_rec, e->g_tw.p, e->g_twtemp.p, e->g_twtemp.n, e->g_nwide.p,
+                       e->stream));
   int64_t words = 0;
+  unsigned long long n_wide = 0;
+  HIPCHK(hipMemcpyAsync(&n_wide, e->g_nwide.p, 8, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipMemcpyAsync(&words, e->g_tw.p + n_rec, 8, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   table_reserve(e, n_rec, words);
@@ -1028,8 +1114,10 @@ void append_gen(sdh_engine* e, const int64_t* bts, int64_t seq_base, int stream)
   HIPCHK(hipStreamSynchronize(e->stream));
   e->mt.n += n_rec;
   e->mt.nw += words;
-  // timer records: (key, query, time); fan-out records: (position, rank, emission)
-  e->mt.n_lo = std::max(e->mt.n_lo, e->has_absent || e->has_fanout ? 3 : 1);
+  // timer records: (key, query, time); fan-out records: (position, rank, emission). K_part's narrow
+  // records need no tiebreak pass: the matches of one (trigger event, query) come from one lane,
+  // which emits them in list order, so the stable sort on the primary key keeps them in it
+  if (n_wide) e->mt.n_lo = std::max(e->mt.n_lo, e->has_absent || e->has_fanout ? 3 : 1);
 }
 
 void table_clear(sdh_engine* e) {
@@ -1871,23 +1959,24 @@ void slab_upload_rings(sdh_engine::SlabSet& ss) {
   HIPCHK(hipMemcpy(ss.d_cap.p, ss.cap.data(), ss.nsub * 8, hipMemcpyHostToDevice));
 }
 
-uint32_t* ring_malloc(int64_t words) {
-  void* p = nullptr;
-  if (hipMalloc(&p, (size_t)words * 4) != hipSuccess) {
-    (void)hipGetLastError();
-    throw Error(SDH_E_CAPACITY, fmt("device memory exhausted allocating a %.2f GB K_slab ring", words * 4.0 / 1e9));
-  }
-  return (uint32_t*)p;
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+uint32_t* ring_malloc(sdh_engine* e, sdh_engine::SlabSet& ss, int64_t words) {
+  (void)e;
+  uint32_t* p = ss.alloc_ring(words);
+  if (!p) throw Error(SDH_E_CAPACITY, fmt("device memory exhausted allocating a %.2f GB K_slab ring", words * 4.0 / 1e9));
+  return p;
 }
 
 // fresh, empty sub-rings of `cap` words each
 void slab_init(sdh_engine* e, sdh_engine::SlabSet& ss, int64_t cap) {
-  for (uint32_t* p : ss.ring)
-    if (p) HIPCHK(hipFree(p));
+  for (size_t r = 0; r < ss.ring.size(); ++r) ss.free_ring(ss.ring[r], r < ss.cap.size() ? ss.cap[r] : 0);
   cap = (cap + 3) & ~3ll;
   ss.ring.assign(ss.nsub, nullptr);
   ss.cap.assign(ss.nsub, cap);
-  for (auto& p : ss.ring) p = ring_malloc(cap);
+  for (auto& p : ss.ring) p = ring_malloc(e, ss, cap);
   ss.d_ring.ensure(ss.nsub);
   ss.d_cap.ensure(ss.nsub);
   slab_upload_rings(ss);
@@ -1903,7 +1992,6 @@ void slab_init(sdh_engine* e, sdh_engine::SlabSet& ss, int64_t cap) {
   ss.live_bak.ensure(256);
   ss.traffic.ensure(256);
   HIPCHK(hipMemset(ss.live.p, 0, 256 * 8));
-  (void)e;
 }
 
 // directory room for `keys` keys (key-major: the old entries are a prefix; new keys' blocks empty)
@@ -1968,6 +2056,7 @@ void slab_grow(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int>& w
   const int BATCH = 32;
   const int64_t BATCH_WORDS = (int64_t)2 << 30;
   for (size_t b0 = 0, b1 = 0; b0 < which.size(); b0 = b1) {
+    const double t_start = now_ms();
     std::vector<uint32_t*> nring(ss.ring);
     std::vector<int64_t> ncap(ss.cap);
     std::vector<uint8_t> active(ss.nsub, 0);
@@ -1975,7 +2064,7 @@ void slab_grow(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int>& w
     for (b1 = b0; b1 < which.size() && b1 < b0 + BATCH && (b1 == b0 || words + new_cap[b1] <= BATCH_WORDS); ++b1) {
       const int r = which[b1];
       ncap[r] = (new_cap[b1] + 3) & ~3ll;
-      nring[r] = ring_malloc(ncap[r]);
+      nring[r] = ring_malloc(e, ss, ncap[r]);
       active[r] = 1;
       words += ncap[r];
     }
@@ -1986,6 +2075,7 @@ void slab_grow(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int>& w
     d_nc.ensure(ss.nsub);
     nh.ensure(ss.nsub);
     nt.ensure(ss.nsub);
+    const double t_alloc = now_ms();
     HIPCHK(hipMemcpy(d_nr.p, nring.data(), ss.nsub * sizeof(uint32_t*), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d_nc.p, ncap.data(), ss.nsub * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(nh.p, 0, ss.nsub * 8));
@@ -1995,9 +2085,10 @@ void slab_grow(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int>& w
       throw Error(SDH_E_CAPACITY, "K_slab: a ring overflowed while growing");
     std::vector<unsigned long long> moved(ss.nsub);
     HIPCHK(hipMemcpy(moved.data(), nh.p, ss.nsub * 8, hipMemcpyDeviceToHost));
+    const double t_move = now_ms();
     for (int r = 0; r < ss.nsub; ++r) {
       if (!active[r]) continue;
-      HIPCHK(hipFree(ss.ring[r]));
+      ss.free_ring(ss.ring[r], ss.cap[r]);
       ss.ring[r] = nring[r];
       ss.cap[r] = ncap[r];
       ss.h_head[r] = moved[r];
@@ -2008,21 +2099,28 @@ void slab_grow(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int>& w
     HIPCHK(hipMemcpy(ss.head.p, ss.h_head.data(), ss.nsub * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ss.tail.p, ss.h_tail.data(), ss.nsub * 8, hipMemcpyHostToDevice));
     ss.growths += (int64_t)(b1 - b0);
+    if (getenv("SDH_SLAB_TRACE"))
+      fprintf(stderr, "[sdh] slab grow: %zu rings, %.2f GB: alloc %.1f ms, move %.1f ms, free %.1f ms\n", b1 - b0,
+              words * 4e-9, t_alloc - t_start, t_move - t_alloc, now_ms() - t_move);
   }
 }
 
 // Room for the next push in every ring. The rings are log-structured: a push appends the entries it
 // changes, the old copies die in place. A ring whose free room falls below its live words plus 1.25x
 // what it took in the last push is cleaned in place: every block written before that push moves to
-// its head (the blocks of the last push are current) -- the oldest quarter of it, mostly dead copies
-// -- while the moves still fit. A ring below 2x
-// (live + headroom) words moves its live blocks into a fresh buffer of 2.5x that. A push that still
-// overflows is undone and re-run with room for 1.25x its demand (re-runs cost time, never matches).
+// its head (the blocks of the last push are current) -- the oldest 4x the room the next push needs
+// (SDH_SLAB_SPAN), mostly dead copies -- once its free room falls below 5x that need (SDH_SLAB_CLEAN_AT):
+// a few pushes per cleaning, each a directory pass. A ring below 1.4x (live + headroom) words (SDH_SLAB_GROW_AT) moves
+// its live blocks into a fresh buffer of 1.6x that (SDH_SLAB_GROW_TO): the reservation stays
+// under 2x the live words, and the cleaning moves (wave-cooperative, nfa_slab.hip) are cheap enough
+// to run at most pushes. A push that still overflows is undone and re-run with room for 1.25x its
+// demand (re-runs cost time, never matches).
 // (C5: cleaning only when a push lacked room never fit in place -- the ring was full by then -- so
 // every cleaning reallocated; growing by the ring's span instead of its live words doubled the
 // reservation every other step and ran out of HBM.)
 // demand: words a failed push tried to take per ring (room for 1.25x that is made instead)
 void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int64_t>* demand = nullptr) {
+  const double t_prep = now_ms();
   std::vector<int64_t> need(ss.nsub);
   std::vector<unsigned long long> limit(ss.nsub);
   std::vector<uint8_t> clean(ss.nsub, 0);
@@ -2043,13 +2141,20 @@ void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int6
     need[r] = std::max<int64_t>(alloc + alloc / 4, 4096);
     if (demand) need[r] = std::max<int64_t>(need[r], (*demand)[r] + (*demand)[r] / 4);
     const int64_t used = (int64_t)(ss.h_head[r] - ss.h_tail[r]);
-    // clean while the live blocks still fit at the head (the in-place move needs room for them)
-    if (ss.cap[r] - used >= need[r] + (int64_t)live[r]) continue;
+    // clean once the room falls below SDH_SLAB_CLEAN_AT x the push's need (then the live blocks of
+    // the span still fit at the head: the in-place move needs room for them, and a span holds at most
+    // SDH_SLAB_SPAN x need live words)
+    static const double clean_at = getenv("SDH_SLAB_CLEAN_AT") ? atof(getenv("SDH_SLAB_CLEAN_AT")) : 5.0;
+    if ((double)(ss.cap[r] - used) >= clean_at * (double)need[r]) continue;
     // the oldest quarter of the ring (at least twice the headroom): mostly dead copies, so the move
     // is small (SDH_SLAB_CLEAN=all: everything before the last push)
     const unsigned long long cur = ss.h_push0[r] > ss.h_tail[r] ? ss.h_push0[r] : ss.h_head[r];
     static const bool all = getenv("SDH_SLAB_CLEAN") && !strcmp(getenv("SDH_SLAB_CLEAN"), "all");
-    const unsigned long long span = (unsigned long long)std::max<int64_t>(2 * need[r], ss.cap[r] / 4);
+    // (the span a push needs, not a fixed share of the ring: every live block in it moves, and the
+    // oldest blocks of a ring are not all dead -- a quarter of the ring per push moved 15 % of C5's
+    // device time)
+    static const double span_x = getenv("SDH_SLAB_SPAN") ? atof(getenv("SDH_SLAB_SPAN")) : 4.0;
+    const unsigned long long span = (unsigned long long)std::max<int64_t>((int64_t)(span_x * need[r]), 4096);
     limit[r] = all ? cur : std::min<unsigned long long>(cur, ss.h_tail[r] + span);
     clean[r] = 1;
     any = true;
@@ -2070,16 +2175,19 @@ void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int6
     // takes its live blocks (slab_grow compacts as it moves; sized from the live words, not the
     // ring's span, which counts dead blocks: sizing from the span doubled the reservation every
     // other C5 step and ran out of HBM)
+    static const double grow_at = getenv("SDH_SLAB_GROW_AT") ? atof(getenv("SDH_SLAB_GROW_AT")) : 1.4;
+    static const double grow_to = getenv("SDH_SLAB_GROW_TO") ? atof(getenv("SDH_SLAB_GROW_TO")) : 1.6;
     for (int r = 0; r < ss.nsub; ++r) {
       if (!clean[r]) continue;
       const int64_t used = (int64_t)(ss.h_head[r] - ss.h_tail[r]);
-      const int64_t want = 2 * ((int64_t)live[r] + need[r]);
-      if (!fail[r] && ss.cap[r] - used >= need[r] && ss.cap[r] >= want) continue;
+      const double base = (double)((int64_t)live[r] + need[r]);
+      if (!fail[r] && ss.cap[r] - used >= need[r] && (double)ss.cap[r] >= grow_at * base) continue;
       grow.push_back(r);
-      gcap.push_back(std::max<int64_t>(ss.cap[r], want + want / 4));
+      gcap.push_back(std::max<int64_t>(ss.cap[r], (int64_t)(grow_to * base)));
     }
   }
   if (getenv("SDH_SLAB_TRACE")) {
+    fprintf(stderr, "[sdh] slab prepare: live pass + cleaning %.1f ms\n", now_ms() - t_prep);
     int64_t c = 0, u = 0, nd = 0, g = 0;
     for (int r = 0; r < ss.nsub; ++r) {
       c += ss.cap[r];
@@ -3522,6 +3630,75 @@ int do_poll_compact(sdh_engine* e, sdh_matches_compact* out, bool device) {
   return SDH_OK;
 }
 
+// sdh_engine_poll_compact_ex: every match as a compact row, chains in a side array, keys and timer
+// tiebreaks beside the rows
+int do_poll_compact_ex(sdh_engine* e, sdh_matches_compact_ex* out, bool device) {
+  check_usable(e);
+  const int64_t n = e->mt.n;
+  const int w = e->cw;
+  const bool want_key = !e->lp.parts.empty(), want_tb = e->has_absent;
+  int64_t nch = 0;
+  const size_t rows = (size_t)std::max<int64_t>(1, n);
+  if (want_key) e->px_key.ensure(rows);
+  if (want_tb) e->px_tb.ensure(rows);
+  e->px_chain.ensure(1);
+  if (!e->mt.placed && n) {
+    if (e->seq - e->seq_ref >= INT32_MAX) throw Error(SDH_E_UNSUPPORTED, "compact rows: seq span past 2^31");
+    int64_t tw = 0;
+    const int32_t* perm = table_order(e, &tw);
+    e->px_cw.ensure((size_t)n + 1);
+    e->px_temp.ensure(sdh_ex_temp_bytes(n));
+    HIPCHK(sdh_ex_chain_words(table_view(e), perm, n, e->px_cw.p, e->px_temp.p, e->px_temp.n, e->stream));
+    HIPCHK(hipMemcpyAsync(&nch, e->px_cw.p + n, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->pc_rows.ensure((size_t)(n * w));
+    e->px_chain.ensure((size_t)std::max<int64_t>(1, nch));
+    e->pc_err.ensure(1);
+    HIPCHK(hipMemsetAsync(e->pc_err.p, 0, 4, e->stream));
+    HIPCHK(sdh_ex_rows(table_view(e), perm, n, w, e->seq_ref, e->px_cw.p, e->pc_rows.p, e->px_chain.p,
+                       want_key ? e->px_key.p : nullptr, want_tb ? e->px_tb.p : nullptr, e->pc_err.p, e->stream));
+    int32_t bad = 0;
+    d2h_sync(e, &bad, e->pc_err.p, 4);
+    if (bad) throw Error(SDH_E_UNSUPPORTED, "compact rows: a seq distance past 2^31 (poll it with sdh_engine_poll)");
+  } else if (n) {  // placed K_ratchet rows: no key, no timer
+    if (want_key) HIPCHK(sdh_fill_i64(e->px_key.p, n, -1, e->stream));
+    if (want_tb) HIPCHK(sdh_fill_i64(e->px_tb.p, n, INT64_MIN, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  e->pc_rows.ensure(1);
+  out->n = n;
+  out->seq_base = e->seq_ref;
+  out->width = w;
+  out->flags = 0;
+  out->n_chain = nch;
+  if (device) {
+    out->rows = e->pc_rows.p;
+    out->key = want_key ? e->px_key.p : nullptr;
+    out->tb = want_tb ? e->px_tb.p : nullptr;
+    out->chain = e->px_chain.p;
+  } else {
+    e->hc_rows.ensure((size_t)std::max<int64_t>(n * w, 1));
+    e->hx_chain.ensure((size_t)std::max<int64_t>(nch, 1));
+    if (n) HIPCHK(hipMemcpyAsync(e->hc_rows.p, e->pc_rows.p, (size_t)(n * w) * 4, hipMemcpyDeviceToHost, e->stream));
+    if (nch) HIPCHK(hipMemcpyAsync(e->hx_chain.p, e->px_chain.p, (size_t)nch * 4, hipMemcpyDeviceToHost, e->stream));
+    if (want_key) {
+      e->hx_key.ensure(rows);
+      if (n) HIPCHK(hipMemcpyAsync(e->hx_key.p, e->px_key.p, (size_t)n * 8, hipMemcpyDeviceToHost, e->stream));
+    }
+    if (want_tb) {
+      e->hx_tb.ensure(rows);
+      if (n) HIPCHK(hipMemcpyAsync(e->hx_tb.p, e->px_tb.p, (size_t)n * 8, hipMemcpyDeviceToHost, e->stream));
+    }
+    HIPCHK(hipStreamSynchronize(e->stream));
+    out->rows = e->hc_rows.p;
+    out->key = want_key ? e->hx_key.p : nullptr;
+    out->tb = want_tb ? e->hx_tb.p : nullptr;
+    out->chain = e->hx_chain.p;
+  }
+  table_clear(e);
+  return SDH_OK;
+}
+
 // ---- multi-GPU exchange (comm.h) ----
 template <class F>
 void xcall(F f) {
@@ -4041,6 +4218,25 @@ int sdh_engine_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
     if (b && b->chunk && b->n > 1) return push_chunk(e, stream, b);
     return do_push(e, stream, b);
   });
+}
+
+int sdh_engine_reserve(sdh_engine* e, int64_t bytes) {
+  if (!e || bytes < 0) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    check_usable(e);
+    HIPCHK(hipSetDevice(e->dev));
+    if (e->ssets.empty() || bytes == 0) return SDH_OK;
+    const size_t per = (size_t)bytes / e->ssets.size();
+    for (auto& ss : e->ssets)
+      if (ss->arena_bytes < per && !ss->add_chunk(((per - ss->arena_bytes) + 4095) & ~(size_t)4095))
+        throw Error(SDH_E_CAPACITY, fmt("device memory exhausted reserving %.1f GB for the sparse state", bytes / 1e9));
+    return SDH_OK;
+  });
+}
+
+int sdh_engine_poll_compact_ex(sdh_engine* e, int32_t device, sdh_matches_compact_ex* out) {
+  if (!e || !out) return SDH_E_INVALID;
+  return guard(e, [&]() { return do_poll_compact_ex(e, out, device != 0); });
 }
 
 int sdh_engine_set_comm(sdh_engine* e, sdh_comm* c) {

@@ -240,7 +240,7 @@ __device__ __forceinline__ int32_t hi32(int64_t w) { return (int32_t)(uint32_t)(
 
 __global__ __launch_bounds__(256) void gen_rec_words_kernel(const int64_t* __restrict__ out,
                                                             const int64_t* __restrict__ rec_off, int64_t n_rec,
-                                                            int64_t* __restrict__ tw) {
+                                                            int64_t* __restrict__ tw, unsigned long long* n_wide) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i > n_rec) return;
   if (i == n_rec) {
@@ -251,6 +251,7 @@ __global__ __launch_bounds__(256) void gen_rec_words_kernel(const int64_t* __res
   const int32_t l0 = lo32(r[0]);
   if (l0 >= 0) {
     tw[i] = r[0] - 7;
+    atomicAdd(n_wide, 1ull);
   } else if ((-l0) >> 16) {  // count: (1, e1), (c, chain), (1, trigger)
     tw[i] = 5 + hi32(r[2]);
   } else {                   // or / and: (1, e1), then per side (1, seq) or (0)
@@ -459,9 +460,12 @@ extern "C" size_t sdh_gen_words_temp_bytes(int64_t n_rec) {
   return b + 256;
 }
 extern "C" hipError_t sdh_gen_words(const int64_t* out, const int64_t* rec_off, int64_t n_rec, int64_t* tw, void* temp,
-                                    size_t temp_bytes, hipStream_t s) {
+                                    size_t temp_bytes, unsigned long long* n_wide, hipStream_t s) {
   if (n_rec <= 0) return hipSuccess;
-  hipLaunchKernelGGL(sdh::gen_rec_words_kernel, dim3(sdh::grid(n_rec + 1, 256)), dim3(256), 0, s, out, rec_off, n_rec, tw);
+  hipError_t e = hipMemsetAsync(n_wide, 0, 8, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sdh::gen_rec_words_kernel, dim3(sdh::grid(n_rec + 1, 256)), dim3(256), 0, s, out, rec_off, n_rec, tw,
+                     n_wide);
   size_t tb = temp_bytes;
   return hipcub::DeviceScan::ExclusiveSum(temp, tb, tw, tw, (int)(n_rec + 1), s);
 }
@@ -633,6 +637,113 @@ extern "C" hipError_t sdh_merge_keys_placed(const int32_t* crow, int width, int6
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(merge_keys_placed_kernel, dim3(sdh::grid(n, 256)), dim3(256), 0, s, crow, width, n, seq_ref,
                      out_rank, qinfo, n_streams, chunk_words, lo_words, keys);
+  return hipGetLastError();
+}
+
+// ---- sdh_engine_poll_compact_ex: compact rows for every match ----
+// per sorted row the chain words it needs (a slot of >= 2 events: its count, then its distances);
+// cw[n] = 0 for the exclusive scan
+__global__ __launch_bounds__(256) void ex_chain_words_kernel(MatchTable T, const int32_t* __restrict__ perm, int64_t n,
+                                                             int64_t* __restrict__ cw) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  if (i == n) {
+    cw[n] = 0;
+    return;
+  }
+  const int32_t p = perm[i];
+  const int64_t* w = T.words + T.woff[p];
+  const int64_t len = T.wlen[p];
+  int64_t t = 0;
+  for (int64_t j = 0; j < len;) {
+    const int64_t c = w[j];
+    if (c >= 2) t += 1 + c;
+    j += 1 + c;
+  }
+  cw[i] = t;
+}
+
+// the rows (sdh_matches_compact_ex), their chains at coff[i], keys and timer tiebreaks; err = 1 when a
+// distance or a chain offset does not fit int32, or a row has more slots than the width
+__global__ __launch_bounds__(256) void ex_rows_kernel(MatchTable T, const int32_t* __restrict__ perm, int64_t n,
+                                                      int width, int64_t seq_ref, const int64_t* __restrict__ coff,
+                                                      int32_t* __restrict__ rows, int32_t* __restrict__ chain,
+                                                      int64_t* __restrict__ okey, int64_t* __restrict__ otb,
+                                                      int32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t p = perm[i];
+  int32_t* o = rows + i * width;
+  const int64_t sq = T.seq[p];
+  bool bad = sq - seq_ref > INT32_MAX || sq < seq_ref;
+  o[0] = (int32_t)T.q[p];
+  o[1] = (int32_t)(sq - seq_ref);
+  const int64_t* w = T.words + T.woff[p];
+  const int64_t len = T.wlen[p];
+  int64_t ref = coff[i];
+  int slot = 0;
+  for (int64_t j = 0; j < len && !bad; ++slot) {
+    const int64_t c = w[j];
+    if (2 + slot >= width) {
+      bad = true;
+      break;
+    }
+    int32_t v = INT32_MIN;
+    if (c == 1) {
+      const int64_t d = sq - w[j + 1];
+      if (d < 0 || d > INT32_MAX) bad = true;
+      v = (int32_t)d;
+    } else if (c >= 2) {
+      if (ref + c >= INT32_MAX) bad = true;
+      chain[ref] = (int32_t)c;
+      for (int64_t k = 0; k < c; ++k) {
+        const int64_t d = sq - w[j + 1 + k];
+        if (d < 0 || d > INT32_MAX) bad = true;
+        chain[ref + 1 + k] = (int32_t)d;
+      }
+      v = (int32_t)(-(ref + 1));
+      ref += 1 + c;
+    }
+    o[2 + slot] = v;
+    j += 1 + c;
+  }
+  for (int k = 2 + slot; k < width; ++k) o[k] = INT32_MIN;
+  if (okey) okey[i] = T.key[p];
+  if (otb) {
+    const bool timer = (T.hi[p] & ((1ull << sdh::RANK_BITS) - 1)) == 0;
+    otb[i] = timer ? (int64_t)(T.lo[2][p] ^ 0x8000000000000000ull) : INT64_MIN;
+  }
+  if (bad) atomicOr(err, 1);
+}
+
+__global__ void fill_i64_kernel(int64_t* p, int64_t n, int64_t v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+extern "C" size_t sdh_ex_temp_bytes(int64_t n) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum((void*)nullptr, b, (int64_t*)nullptr, (int64_t*)nullptr, (int)(n + 1));
+  return b + 256;
+}
+// chain word offsets of the sorted rows (cw: n + 1 entries, scanned in place; cw[n] = the total)
+extern "C" hipError_t sdh_ex_chain_words(MatchTable T, const int32_t* perm, int64_t n, int64_t* cw, void* temp,
+                                         size_t temp_bytes, hipStream_t s) {
+  hipLaunchKernelGGL(ex_chain_words_kernel, dim3(sdh::grid(n + 1, 256)), dim3(256), 0, s, T, perm, n, cw);
+  size_t tb = temp_bytes;
+  return hipcub::DeviceScan::ExclusiveSum(temp, tb, cw, cw, (int)(n + 1), s);
+}
+extern "C" hipError_t sdh_ex_rows(MatchTable T, const int32_t* perm, int64_t n, int width, int64_t seq_ref,
+                                  const int64_t* coff, int32_t* rows, int32_t* chain, int64_t* okey, int64_t* otb,
+                                  int32_t* err, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ex_rows_kernel, dim3(sdh::grid(n, 256)), dim3(256), 0, s, T, perm, n, width, seq_ref, coff, rows,
+                     chain, okey, otb, err);
+  return hipGetLastError();
+}
+extern "C" hipError_t sdh_fill_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_i64_kernel, dim3(sdh::grid(n, 256)), dim3(256), 0, s, p, n, v);
   return hipGetLastError();
 }
 

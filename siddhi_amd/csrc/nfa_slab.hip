@@ -35,7 +35,8 @@ using SlabWaveOut = dev::WaveOutT<256>;
 namespace {
 
 __device__ __forceinline__ uint32_t sub_of(uint64_t dir_idx, int nsub) {
-  return (uint32_t)(((dir_idx * 0x9E3779B97F4A7C15ull) >> 32) % (uint64_t)nsub);
+  const uint32_t h = (uint32_t)((dir_idx * 0x9E3779B97F4A7C15ull) >> 32);
+  return (nsub & (nsub - 1)) == 0 ? h & (uint32_t)(nsub - 1) : h % (uint32_t)nsub;  // (the same value)
 }
 
 // words [o, o + words) of sub-ring `sub` (o: offset in its buffer), or -1 when the ring is full (a
@@ -359,32 +360,63 @@ struct SlabRings {
   const unsigned long long* tail;
   int32_t nsub;
 };
-__global__ void slab_move_kernel(uint64_t* dir, int64_t n_dir, int groups, const int32_t* __restrict__ group_ew,
-                                 SlabRings src, const unsigned long long* limit, const uint8_t* active, SlabRings dst,
-                                 int32_t* err, uint8_t* ring_err) {
+// One wave per 64 directory entries: each lane decides whether its block moves and takes its
+// destination (one ring_alloc), then copies it in 16-B words (a block is a multiple of 4 uint32 words
+// at a 16-B aligned offset) if it is small -- C5's blocks mostly are: 64 copies in flight -- while the
+// wave copies a large one together, all 64 lanes on it. (A thread copying its own block word by word
+// in 4-B loads read 64 scattered lines per instruction.)
+__global__ __launch_bounds__(256) void slab_move_kernel(uint64_t* dir, int64_t n_dir, int groups,
+                                                        const int32_t* __restrict__ group_ew, SlabRings src,
+                                                        const unsigned long long* limit, const uint8_t* active,
+                                                        SlabRings dst, int32_t* err, uint8_t* ring_err) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= n_dir) return;
-  const uint64_t d = dir[x];
-  const int n = (int)((d >> 40) & 0xffff);
-  if (n == 0) return;
-  const uint32_t ss = src.nsub == 1 ? 0u : sub_of((uint64_t)x, src.nsub);
-  if (active && !active[ss]) return;
-  const int64_t rel = (int64_t)(d & 0xffffffffull) * 4, cap = src.cap[ss];
-  const uint64_t t = src.tail[ss];
-  const uint64_t logical = t + (uint64_t)((rel - (int64_t)(t % (uint64_t)cap) + cap) % cap);
-  if (logical >= limit[ss]) return;
-  const int64_t words = ((int64_t)n * group_ew[x % groups] + 3) & ~3ll;
-  const uint32_t ds = dst.nsub == 1 ? 0u : sub_of((uint64_t)x, dst.nsub);
-  const int64_t o = ring_alloc(dst.head, dst.tail[ds], dst.cap[ds], ds, words);
-  if (o < 0) {
-    atomicOr(err, 1);
-    if (ring_err) ring_err[ds] = 1;  // (which destination ring ran out of room)
-    return;
+  const int lane = threadIdx.x & 63;
+  bool mv = false;
+  uint64_t d = 0;
+  int64_t words = 0, o = -1;
+  const uint32_t* from = nullptr;
+  uint32_t* to = nullptr;
+  if (x < n_dir) {
+    d = dir[x];
+    const int n = (int)((d >> 40) & 0xffff);
+    const uint32_t ss = src.nsub == 1 ? 0u : sub_of((uint64_t)x, src.nsub);
+    if (n != 0 && (!active || active[ss])) {
+      const int64_t rel = (int64_t)(d & 0xffffffffull) * 4, cap = src.cap[ss];
+      const uint64_t t = src.tail[ss];
+      const uint64_t logical = t + (uint64_t)((rel - (int64_t)(t % (uint64_t)cap) + cap) % cap);
+      if (logical < limit[ss]) {
+        const int64_t g = x < (int64_t)UINT32_MAX ? (int64_t)((uint32_t)x % (uint32_t)groups) : x % groups;
+        words = ((int64_t)n * group_ew[g] + 3) & ~3ll;
+        const uint32_t ds = dst.nsub == 1 ? 0u : sub_of((uint64_t)x, dst.nsub);
+        o = ring_alloc(dst.head, dst.tail[ds], dst.cap[ds], ds, words);
+        if (o < 0) {
+          atomicOr(err, 1);
+          if (ring_err) ring_err[ds] = 1;  // (which destination ring ran out of room)
+        } else {
+          mv = true;
+          from = src.ring[ss] + rel;
+          to = dst.ring[ds] + o;
+        }
+      }
+    }
   }
-  const uint32_t* from = src.ring[ss] + rel;
-  uint32_t* to = dst.ring[ds] + o;
-  for (int64_t w = 0; w < words; ++w) to[w] = from[w];
-  dir[x] = (uint64_t)(o / 4) | (d & ~0xffffffffull);
+  // a block of up to 32 16-B words: its lane copies it (64 blocks at a time); a larger one: the whole
+  // wave, one block after another (a block keeps its old place until its directory word moves)
+  const bool own = mv && words <= 4 * 32;
+  if (own) {
+    const uint4* f = reinterpret_cast<const uint4*>(from);
+    uint4* t = reinterpret_cast<uint4*>(to);
+    for (int64_t i = 0; i < words / 4; ++i) t[i] = f[i];
+  }
+  for (unsigned long long m = __ballot(mv && !own); m; m &= m - 1) {
+    const int l = __ffsll((long long)m) - 1;
+    const uint4* f = reinterpret_cast<const uint4*>(
+        (const uint32_t*)__shfl((long long)(uintptr_t)from, l));
+    uint4* t = reinterpret_cast<uint4*>((uint32_t*)__shfl((long long)(uintptr_t)to, l));
+    const int64_t q = __shfl(words, l) / 4;
+    for (int64_t i = lane; i < q; i += 64) t[i] = f[i];
+  }
+  if (mv) dir[x] = (uint64_t)(o / 4) | (d & ~0xffffffffull);
 }
 
 // live words of the blocks (stats: bytes per live partial)

@@ -52,6 +52,13 @@ class SdhMatchesCompact(ctypes.Structure):
                 ("flags", ctypes.c_int32), ("rows", ctypes.POINTER(ctypes.c_int32))]
 
 
+class SdhMatchesCompactEx(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("seq_base", ctypes.c_int64), ("width", ctypes.c_int32),
+                ("flags", ctypes.c_int32), ("rows", ctypes.POINTER(ctypes.c_int32)),
+                ("key", ctypes.POINTER(ctypes.c_int64)), ("tb", ctypes.POINTER(ctypes.c_int64)),
+                ("n_chain", ctypes.c_int64), ("chain", ctypes.POINTER(ctypes.c_int32))]
+
+
 class SdhStats(ctypes.Structure):
     _fields_ = [("events", ctypes.c_int64), ("pattern_events", ctypes.c_int64),
                 ("matches", ctypes.c_int64), ("live_partials", ctypes.c_int64),
@@ -64,14 +71,14 @@ class SdhStats(ctypes.Structure):
 
 
 EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engine_poll", "sdh_engine_poll_device",
-           "sdh_engine_poll_compact",
+           "sdh_engine_poll_compact", "sdh_engine_poll_compact_ex",
            "sdh_engine_pending_matches", "sdh_engine_start", "sdh_engine_advance_time", "sdh_engine_stats",
            "sdh_engine_snapshot", "sdh_engine_state_bytes",
            "sdh_engine_restore", "sdh_free", "sdh_engine_destroy", "sdh_last_error", "sdh_version",
            "sdh_engine_debug_digest", "sdh_engine_set_strings", "sdh_calibrate_hbm", "sdh_build_info",
            "sdh_engine_push_stats", "sdh_comm_get_id", "sdh_comm_create", "sdh_comm_create_local",
            "sdh_comm_destroy", "sdh_comm_last_error", "sdh_engine_set_comm", "sdh_engine_push_bcast",
-           "sdh_engine_gather"]
+           "sdh_engine_gather", "sdh_engine_reserve"]
 SDH_COMM_ID_BYTES = 128
 
 _lib = None
@@ -94,12 +101,14 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_engine_poll.argtypes = [P, ctypes.POINTER(SdhMatches)]
     lib.sdh_engine_poll_device.argtypes = [P, ctypes.POINTER(SdhMatches)]
     lib.sdh_engine_poll_compact.argtypes = [P, ctypes.c_int32, ctypes.POINTER(SdhMatchesCompact)]
+    lib.sdh_engine_poll_compact_ex.argtypes = [P, ctypes.c_int32, ctypes.POINTER(SdhMatchesCompactEx)]
     lib.sdh_engine_pending_matches.argtypes = [P, ctypes.POINTER(ctypes.c_int64)]
     lib.sdh_engine_start.argtypes = [P, ctypes.c_int64]
     lib.sdh_engine_advance_time.argtypes = [P, ctypes.c_int64]
     lib.sdh_engine_stats.argtypes = [P, ctypes.POINTER(SdhStats)]
     I64P = ctypes.POINTER(ctypes.c_int64)
     lib.sdh_engine_state_bytes.argtypes = [P, I64P, I64P, I64P]
+    lib.sdh_engine_reserve.argtypes = [P, ctypes.c_int64]
     lib.sdh_engine_snapshot.argtypes = [P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
     lib.sdh_engine_restore.argtypes = [P, ctypes.c_void_p, ctypes.c_size_t]
     lib.sdh_free.argtypes = [P]
@@ -299,6 +308,20 @@ class HipEngine:
             return m.seq_base, np.zeros((0, m.width), np.int32)
         return m.seq_base, np.ctypeslib.as_array(m.rows, shape=(m.n, m.width)).copy()
 
+    def poll_compact_ex(self, device: bool = False):
+        """Compact rows for every match (sdh_engine_poll_compact_ex): host arrays (seq_base, rows[n, width],
+        key or None, tb or None, chain), or the SdhMatchesCompactEx struct of HBM pointers (device)."""
+        m = SdhMatchesCompactEx()
+        self._check(self.lib.sdh_engine_poll_compact_ex(self.h, int(device), ctypes.byref(m)))
+        if device:
+            return m
+        n, w = m.n, m.width
+        rows = np.ctypeslib.as_array(m.rows, shape=(n, w)).copy() if n else np.zeros((0, w), np.int32)
+        key = np.ctypeslib.as_array(m.key, shape=(n,)).copy() if (m.key and n) else (np.zeros(0, np.int64) if m.key else None)
+        tb = np.ctypeslib.as_array(m.tb, shape=(n,)).copy() if (m.tb and n) else (np.zeros(0, np.int64) if m.tb else None)
+        chain = np.ctypeslib.as_array(m.chain, shape=(m.n_chain,)).copy() if m.n_chain else np.zeros(0, np.int32)
+        return m.seq_base, rows, key, tb, chain
+
     def take_matches(self, n_slots_of):
         q, k, ts, off, words = self.poll()
         out = []
@@ -357,6 +380,10 @@ class HipEngine:
         a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         self._check(self.lib.sdh_engine_state_bytes(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return a.value, b.value, c.value
+
+    def reserve(self, nbytes: int):
+        """Pre-allocate HBM for the sparse K_slab state (sdh_engine_reserve)."""
+        self._check(self.lib.sdh_engine_reserve(self.h, int(nbytes)))
 
     def snapshot(self) -> bytes:
         p = ctypes.c_void_p()

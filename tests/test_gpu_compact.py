@@ -158,3 +158,107 @@ def test_compact_rows_when_lanes_walk_their_deques(monkeypatch):
         seq_polled = lo + 5000
     assert a.stats().placed_pushes == n // 5000
     assert b.stats().placed_pushes == 0
+
+
+def restate_ex(q, k, off, words, seq, tb, width, seq_base, with_key, with_tb):
+    """poll tuples -> what sdh_engine_poll_compact_ex promises: rows with chains in a side array
+    (include/siddhi_hip.h), keys and timer tiebreaks beside them"""
+    rows = np.full((len(q), width), EMPTY, np.int64)
+    chain = []
+    for i in range(len(q)):
+        rows[i, 0] = q[i]
+        rows[i, 1] = seq[i] - seq_base
+        w = words[off[i]:off[i + 1]]
+        j, slot = 0, 0
+        while j < len(w):
+            c = int(w[j])
+            if c == 1:
+                rows[i, 2 + slot] = seq[i] - w[j + 1]
+            elif c >= 2:
+                rows[i, 2 + slot] = -(len(chain) + 1)
+                chain += [c] + [int(seq[i] - x) for x in w[j + 1:j + 1 + c]]
+            j += 1 + c
+            slot += 1
+    return rows.astype(np.int32), (np.asarray(k) if with_key else None), (np.asarray(tb) if with_tb else None), \
+        np.asarray(chain, np.int32)
+
+
+def _ex_equals_poll(a, b, with_key, with_tb):
+    seq_base, rows, key, tb, chain = a.poll_compact_ex()
+    q, k, t, off, words, seq, tbb = b.poll(with_seq=True)
+    want = restate_ex(q, k, off, words, seq, tbb, rows.shape[1], seq_base, with_key, with_tb)
+    assert np.array_equal(rows, want[0])
+    assert (key is None) == (not with_key) and (tb is None) == (not with_tb)
+    if with_key:
+        assert np.array_equal(key, want[1])
+    if with_tb:
+        assert np.array_equal(tb, want[2])
+    assert np.array_equal(chain, want[3])
+    return len(q)
+
+
+@pytest.mark.parametrize("family", ["c3", "c5"])
+def test_compact_ex_equals_poll_partitioned_families(family):
+    """Count chains and partition keys (C3: K_part count / and / or; C5: K_slab over four streams)."""
+    from siddhi_amd.workloads import c3_app, c5_app, c5_events, stock_events
+    src = c3_app(48) if family == "c3" else c5_app(64)
+    a, b = _engines(src)
+    total, lo = 0, 0
+    for i in range(8):
+        if family == "c3":
+            ts, sym, price, vol = stock_events(lo, 3000, 12)
+            cols = [(0, ts, [sym, price.view(np.uint32), vol])]
+            lo += 3000
+        else:
+            cols = []
+            for si in range(4):
+                ts, acct, amt, code = c5_events(si, lo, 1500, 40)
+                cols.append((si, ts, [acct, amt.view(np.uint32), code]))
+            lo += 1500
+        for si, ts, c in cols:
+            a.push_columns(si, ts, c)
+            b.push_columns(si, ts, c)
+        if i % 2:
+            total += _ex_equals_poll(a, b, True, False)
+    assert total > 1000
+
+
+def test_compact_ex_equals_poll_absent_apps():
+    """Timer matches of absent states (tb beside the rows), on the absent-app timelines."""
+    from dist_gpu_child import batches
+    from siddhi_amd.events import encode_rows
+    from siddhi_amd.engine import columns_from_words
+    from test_dist import events, full_src
+    app = App(full_src(absent=True), engine_factory=lambda blob: None)
+    types = [s.attr_types for s in app.ir.streams]
+    a, b = _engines(full_src(absent=True))
+    evs = events()
+    total = 0
+    for i, (stream, rows, ts) in enumerate(batches(evs)):
+        si = app.ir.stream_index(stream)
+        vals, nulls = encode_rows(rows, types[si], app.dictionary)
+        cols = columns_from_words(vals, types[si])
+        a.push_columns(si, np.asarray(ts, np.int64), cols)
+        b.push_columns(si, np.asarray(ts, np.int64), cols)
+        if i % 4 == 3:
+            total += _ex_equals_poll(a, b, True, True)
+    a.advance_time(evs[-1][2] + 100)
+    b.advance_time(evs[-1][2] + 100)
+    total += _ex_equals_poll(a, b, True, True)
+    assert total > 50
+
+
+def test_compact_ex_placed_and_unpartitioned():
+    """A program without partitions or absent states: no key / tb arrays; placed K_ratchet windows and
+    chain windows (a count state in an unpartitioned query) both convert."""
+    from siddhi_amd.workloads import c2_app, stock_events
+    src = c2_app(64) + (" @info(name='n1') from every e1=StockStream[price > 80] -> "
+                        "e2=StockStream[price < 20]<2:4> -> e3=StockStream[price > 50] within 1 sec "
+                        "select e1.price as a insert into O;")
+    for s in (c2_app(64), src):
+        a, b = _engines(s)
+        ts, sym, price, vol = stock_events(0, 20000)
+        cols = [sym, price.view(np.uint32), vol]
+        a.push_columns(0, ts, cols)
+        b.push_columns(0, ts, cols)
+        assert _ex_equals_poll(a, b, False, False) > 1000

@@ -134,6 +134,45 @@ def test_headline_config_golden():
     assert one.debug_digest()[0] == g["n_matches"]
 
 
+@pytest.mark.timeout(600)
+def test_bench_shape_one_push_equals_many():
+    """The bench's exact timed configuration (bench.py's default line): one 8M-event push of the
+    10K-pattern C2 family, from HBM, in SDH_FLAG_DEVICE_MATCHES mode (the record ring wraps, so only
+    its count is readable) counts the same matches as the same events in 64 normal-mode pushes of
+    128K; each of those pushes writes the same records in both output modes (count and
+    order-independent hash, sdh_engine_debug_digest). A full-size property check of the timed step."""
+    import torch
+    from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES, HipEngine
+    from siddhi_amd.workloads import c2_app, stock_events_torch
+    app = App(c2_app(10000), engine_factory=lambda blob: None)
+    types = [s.attr_types for s in app.ir.streams]
+    dev = torch.device("cuda:0")
+    B, parts = 1 << 23, 64
+    ts, sym, price, vol = stock_events_torch(0, B, 100, dev)
+    cols = [sym, price.view(torch.int32), vol]
+    torch.cuda.synchronize()
+    one = HipEngine(app.blob, stream_types=types, flags=SDH_FLAG_DEVICE_MATCHES)
+    one.push_device(0, B, ts.data_ptr(), [c.data_ptr() for c in cols])
+    total = one.pending_matches()
+    one.close()
+    normal = HipEngine(app.blob, stream_types=types)
+    ring = HipEngine(app.blob, stream_types=types, flags=SDH_FLAG_DEVICE_MATCHES)
+    n, acc = B // parts, 0
+    for i in range(parts):
+        ptrs = [c.data_ptr() + i * n * c.element_size() for c in cols]
+        for e in (normal, ring):
+            e.push_device(0, n, ts.data_ptr() + i * n * 8, ptrs)
+        dn, dr = normal.debug_digest(), ring.debug_digest()
+        assert dn == dr and dn[0] > 0, f"push {i}: normal-mode records {dn} != device-match-mode records {dr}"
+        assert ring.pending_matches() == dn[0]
+        acc += dn[0]
+        assert normal.poll_compact(device=True).n == dn[0]  # (drops the window)
+    assert normal.stats().placed_pushes == parts
+    normal.close()
+    ring.close()
+    assert total > 3e10 and acc == total
+
+
 @pytest.mark.parametrize("mixed", [False, True])
 def test_direct_placement_equals_sort(mixed):
     """Pushes whose matches all come from K_ratchet go straight to their R18 rows (nfa_ratchet.hip
