@@ -603,8 +603,7 @@ def push_latency(args, sh, K, local):
     4,096, normal mode (every match polled to the host in R18 order). Median and p99 over 50 pushes
     after 5 warm-up pushes (4,096: 10 after 2; at 10K C2 patterns such a push carries ~17M matches),
     continuing one stream. A second engine fed the same pushes polls the compact rows instead
-    (sdh_engine_poll_compact to the host: 16 B per match instead of ~72; `compact_*`; workloads whose
-    matches the form cannot express report null)."""
+    (sdh_engine_poll_compact_ex to the host: 16 B per C2 match instead of ~72; `compact_*`)."""
     from siddhi_amd.engine import EngineError
     from siddhi_amd.workloads import stock_events, txn_events
     eng = make_engine(args.workload, sh, K, local, 0, args.partials)
@@ -627,7 +626,7 @@ def push_latency(args, sh, K, local):
             if compact_ok:
                 try:
                     ceng.push_columns(0, ts, cols)
-                    _, rows = ceng.poll_compact()
+                    _, rows, _, _, _ = ceng.poll_compact_ex()
                     if len(rows) != len(m[0]):
                         raise RuntimeError(f"poll_compact {len(rows)} rows, poll {len(m[0])} matches")
                 except EngineError:
@@ -727,6 +726,7 @@ def expansion(args, sh, K, local, dev, world, cdev, dist, comm=None):
          "matches_per_step": matches / steps, "pattern_events_per_s": pe_timed / el, "matches_per_s": matches / el}
     if world == 1:
         r["compact"] = compact_leg(args, sh, K, local, bs, E, warm, matches)
+        r["compact"]["pattern_events_per_s"] = pe_timed / (r["compact"]["ms_per_step"] * 1e-3 * steps)
     if world > 1:
         if dist.get_rank() == 0 and merged != matches:
             raise RuntimeError(f"the gather merged {merged} matches, the ranks produced {matches}")
@@ -737,36 +737,36 @@ def expansion(args, sh, K, local, dev, world, cdev, dist, comm=None):
 
 
 def compact_leg(args, sh, K, local, bs, E, warm, want):
-    """The expansion pushes again on a fresh engine, each followed by sdh_engine_poll_compact(device):
+    """The expansion pushes again on a fresh engine, each followed by sdh_engine_poll_compact_ex(device):
     the same R18-ordered matches as compact int32 rows (a window placed by K_ratchet is handed out as
-    it is: no sort, no gather). Workloads whose matches the form cannot express (count chains,
-    partition keys) report why."""
+    it is: no sort, no gather), count chains in a side array, partition keys / timer tiebreaks beside
+    the rows when the program has them."""
     import torch
-    from siddhi_amd.engine import EngineError
     eng = make_engine(args.workload, sh, K, local, 0, args.partials)
-    matches, width = 0, 0
+    matches, width, chain, extra = 0, 0, 0, 0
     try:
         for i, cols in enumerate(bs):
             if i == warm:
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
             eng.push_device(0, E, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]])
-            m = eng.poll_compact(device=True)
+            m = eng.poll_compact_ex(device=True)
             if i >= warm:
                 matches += m.n
                 width = m.width
+                chain += m.n_chain
+                extra = 8 * (bool(m.key) + bool(m.tb))
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-    except EngineError as ex:
-        return {"unsupported": str(ex)}
     finally:
         eng.close()
     if matches != want:
-        raise RuntimeError(f"poll_compact delivered {matches} matches, sdh_engine_poll_device {want}")
+        raise RuntimeError(f"poll_compact_ex delivered {matches} matches, sdh_engine_poll_device {want}")
     steps = len(bs) - warm
     log(f"compact leg: {matches} matches in {el * 1e3:.1f} ms (width {width})")
     return {"ms_per_step": el * 1e3 / steps, "matches_per_s": matches / el, "width": width,
-            "bytes_per_match": 4 * width}
+            "pattern_events_per_s": None,
+            "bytes_per_match": 4 * width + extra + (4.0 * chain / matches if matches else 0.0)}
 
 
 if __name__ == "__main__":

@@ -1270,8 +1270,13 @@ int bits_of(uint64_t v) {
 }
 
 // the ABI output arrays in HBM for n matches of tw words (po_*; off and len have n + 1 entries)
+// (at least 64K rows: a window that edges past the last size would otherwise reallocate -- a
+// device allocation inside the poll, the p99 of small pushes)
+constexpr int64_t POLL_MIN_ROWS = 1 << 16;
 void poll_reserve(sdh_engine* e, int64_t n, int64_t tw) {
-  const size_t m = (size_t)std::max<int64_t>(n, 1);
+  const size_t m = (size_t)std::max<int64_t>(n, POLL_MIN_ROWS);
+  tw = std::max<int64_t>(tw, 4 * POLL_MIN_ROWS);
+  n = std::max<int64_t>(n, POLL_MIN_ROWS);
   e->po_q.ensure(m);
   e->po_key.ensure(m);
   e->po_ts.ensure(m);
@@ -3553,14 +3558,15 @@ int do_poll(sdh_engine* e, sdh_matches* out, bool host) {
   check_usable(e);
   int64_t tw = 0;
   const int64_t n = poll_sorted(e, &tw);
-  if (host) {
-    e->ho_q.ensure(std::max<int64_t>(n, 1));
-    e->ho_key.ensure(std::max<int64_t>(n, 1));
-    e->ho_ts.ensure(std::max<int64_t>(n, 1));
-    e->ho_seq.ensure(std::max<int64_t>(n, 1));
-    e->ho_tb.ensure(std::max<int64_t>(n, 1));
-    e->ho_off.ensure(n + 1);
-    e->ho_words.ensure(std::max<int64_t>(tw, 1));
+  if (host) {  // (pinned; sized like poll_reserve's device arrays)
+    const int64_t hn = std::max<int64_t>(n, POLL_MIN_ROWS);
+    e->ho_q.ensure(hn);
+    e->ho_key.ensure(hn);
+    e->ho_ts.ensure(hn);
+    e->ho_seq.ensure(hn);
+    e->ho_tb.ensure(hn);
+    e->ho_off.ensure(hn + 1);
+    e->ho_words.ensure(std::max<int64_t>(tw, 4 * POLL_MIN_ROWS));
     e->ho_off.p[0] = 0;
     if (n) {
       HIPCHK(hipMemcpyAsync(e->ho_q.p, e->po_q.p, n * 8, hipMemcpyDeviceToHost, e->stream));
@@ -3622,7 +3628,7 @@ int do_poll_compact(sdh_engine* e, sdh_matches_compact* out, bool device) {
   if (device) {
     out->rows = e->pc_rows.p;
   } else {
-    e->hc_rows.ensure((size_t)std::max<int64_t>(n * w, 1));
+    e->hc_rows.ensure((size_t)std::max<int64_t>(n * w, POLL_MIN_ROWS * w));
     if (n) d2h_sync(e, e->hc_rows.p, e->pc_rows.p, (size_t)(n * w) * 4);
     out->rows = e->hc_rows.p;
   }
@@ -3677,7 +3683,7 @@ int do_poll_compact_ex(sdh_engine* e, sdh_matches_compact_ex* out, bool device) 
     out->tb = want_tb ? e->px_tb.p : nullptr;
     out->chain = e->px_chain.p;
   } else {
-    e->hc_rows.ensure((size_t)std::max<int64_t>(n * w, 1));
+    e->hc_rows.ensure((size_t)std::max<int64_t>(n * w, POLL_MIN_ROWS * w));
     e->hx_chain.ensure((size_t)std::max<int64_t>(nch, 1));
     if (n) HIPCHK(hipMemcpyAsync(e->hc_rows.p, e->pc_rows.p, (size_t)(n * w) * 4, hipMemcpyDeviceToHost, e->stream));
     if (nch) HIPCHK(hipMemcpyAsync(e->hx_chain.p, e->px_chain.p, (size_t)nch * 4, hipMemcpyDeviceToHost, e->stream));
