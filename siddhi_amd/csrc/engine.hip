@@ -1573,11 +1573,13 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
   (void)t01;
   bool no_place = false;
   for (int attempt = 0; attempt < 40; ++attempt) {
-    // out-of-order timestamps seen on this stream, or timestamps so extreme that `ts0 + within`
-    // could wrap: exact per-entry expiry scan, no chunking
+    // out-of-order timestamps seen on this stream, timestamps so extreme that `ts0 + within`
+    // could wrap, or a batch spanning 2^31 - 2 ms or more (the lazy forms' 32-bit deadline domain,
+    // nfa_ratchet.hip rel_deadline): exact per-entry expiry scan, no chunking
     const int64_t lim = (int64_t)1 << 61;
     const bool full = e->r_full_expiry[stream] != 0 || t01[0] < -lim || t01[0] > lim || t01[1] < -lim ||
-                      t01[1] > lim || (B.prev_ts != INT64_MIN && (B.prev_ts < -lim || B.prev_ts > lim));
+                      t01[1] > lim || (B.prev_ts != INT64_MIN && (B.prev_ts < -lim || B.prev_ts > lim)) ||
+                      t01[1] - t01[0] > (int64_t)INT32_MAX - 2;
     // ---- chunk planning: chunk c > 0 rebuilds its starting deques by a reverse scan of the
     // `within` window (a few instructions per 64 events), so chunks can be short. Each launch
     // (one key kind x orientation) gets one resident wave per slot of the chip -- CUs x the

@@ -351,6 +351,17 @@ struct Deque {
   }
   __device__ __forceinline__ void top(int64_t& ts, U& key, uint32_t& seq) const { at(n() - 1, ts, key, seq); }
   __device__ __forceinline__ void bottom(int64_t& ts, U& key, uint32_t& seq) const { at(0, ts, key, seq); }
+  // low seq bits of the oldest entry (n() > 0), without its ts0
+  __device__ __forceinline__ uint32_t bottom_seq() const {
+    if (sn > 0) {
+      if constexpr (KT<KK>::W64) return SB[si(sbot)];
+      else return SA[si(sbot)].w;
+    }
+    U k;
+    uint32_t q;
+    lget_ks(li(lbot), k, q);
+    return q;
+  }
   // append the newest entry; returns false on overflow
   __device__ __forceinline__ bool push_back(int64_t ts, U key, uint32_t seq) {
     if (ln == ML) {
@@ -417,6 +428,18 @@ __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {  // b >= 0
   return a > INT64_MAX - b ? INT64_MAX : a + b;
 }
 
+// Expiry deadlines of the lazy (ordered-timestamp) forms live in a 32-bit domain relative to the
+// item's first timestamp T0: the host routes batches whose ts span is 2^31 - 2 or more (or whose
+// timestamps are beyond +-2^61) to the FULL form, so every event's ts - T0 of an ordered batch is in
+// [0, 2^31 - 2]. A deadline (ts0 + within, saturated) maps to ts - T0 clamped to [INT32_MIN,
+// INT32_MAX]: INT32_MAX (never) and INT32_MIN (already passed) keep `tt > deadline` exact. Out-of-order
+// batches produce garbage here but are flagged from the 64-bit timestamps and re-run in FULL form.
+__device__ __forceinline__ int32_t rel_deadline(int64_t d, int64_t T0) {  // |T0| <= 2^61
+  if (d >= T0 + INT32_MAX) return INT32_MAX;
+  if (d <= T0 + INT32_MIN) return INT32_MIN;
+  return (int32_t)(d - T0);
+}
+
 // SIM (the C2 family's form): 32-bit float keys, one start atom on the key's own float column with a
 // plain interval (no negation), no null masks. The start filter is then two float compares of the
 // event key against per-lane float bounds, and NaN keys fail every compare by themselves, so the
@@ -458,6 +481,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
   D.sbase = ((size_t)wid * SC) * WAVE;
   const bool active = lane < G->n_lanes;
   const int64_t within = G->within[lane & 63];
+  const int32_t w32 = within >= INT32_MAX ? INT32_MAX : (int32_t)within;  // (within >= 0)
+  const int64_t T0 = L.b.ts[W.c0];  // the 32-bit deadline domain's origin (rel_deadline)
   const int64_t wmax = G->wmax;
   const bool has_within = wmax >= 0;
   const int n_f0 = G->n_f0;
@@ -732,21 +757,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
   };
   refill();
 
-  // VGPR caches of the deque ends: top key/seq, bottom deadline/seq
+  // VGPR caches of the deque ends: top key/seq, bottom deadline (rel_deadline; INT32_MAX while the
+  // deque is empty, so a push lowers it to the new entry's deadline by a min: with ordered
+  // timestamps every held entry's deadline is <= a newer one's)
   U tkey = 0;
-  uint32_t tseq = 0, bseq = 0;
-  int64_t bdead = INT64_MAX;
+  uint32_t tseq = 0;
+  int32_t bdead = INT32_MAX;
   auto refresh_top = [&]() {
     if (D.ln > 0) D.lget_ks(D.li(D.lbot + D.ln - 1), tkey, tseq);
     else if (SIM) tkey = TSENT;
   };
   auto refresh_bottom = [&]() {
-    bdead = INT64_MAX;
+    bdead = INT32_MAX;
     if (D.n() > 0) {
       U k0;
       int64_t bts;
-      D.bottom(bts, k0, bseq);
-      bdead = sat_add(bts, within);
+      uint32_t q0;
+      D.bottom(bts, k0, q0);
+      bdead = rel_deadline(sat_add(bts, within), T0);
     }
   };
   refresh_top();
@@ -850,16 +878,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     if (lane == 0) pred = prev_tile_ts;
     if (live && ets < pred) unordered = true;
     prev_tile_ts = __shfl(ets, WAVE - 1, WAVE);
+    // the lazy forms compare in the 32-bit deadline domain (rel_deadline)
+    int32_t ets32 = 0;
+    if constexpr (!FULL)
+      ets32 = ets >= T0 + (INT32_MAX - 1) ? INT32_MAX - 1 : ets <= T0 + INT32_MIN ? INT32_MIN : (int32_t)(ets - T0);
     const int cnt = (int)((W.c1 - t) < WAVE ? (W.c1 - t) : WAVE);
     // sequence numbers are kept as their low 32 bits: a live partial must stay < 2^31 events old
     // (checked once per tile against the tile's last event; the bottom only gets younger)
-    if (D.n() > 0 && (uint32_t)((uint32_t)(seq_base + t + cnt - 1) - bseq) >= 0x80000000u) aged = true;
+    if (D.n() > 0 && (uint32_t)((uint32_t)(seq_base + t + cnt - 1) - D.bottom_seq()) >= 0x80000000u) aged = true;
     if constexpr (PM == 1) cntv = 0;
     if constexpr (PM == 2) basev = lane < cnt ? L.pbase[(int64_t)(t + lane) * L.n_cells + cell] : 0;
 
     SDH_UNROLL(SDH_RATCHET_UNROLL)
     for (int k = 0; k < cnt; ++k) {
-      const int64_t tt = readlane64(ets, k);
+      const int64_t tt = FULL ? readlane64(ets, k) : 0;
+      const int32_t tt32 = FULL ? 0 : (int32_t)__builtin_amdgcn_readlane((uint32_t)ets32, k);
       const int64_t s = seq_base + t + k;
       const uint32_t slo = (uint32_t)s;
       const uint32_t vb = SIM ? 1u : __builtin_amdgcn_readlane(vbits, k);
@@ -872,15 +905,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
           // timestamps non-decreasing: expired(bts, tt) <=> tt > bts + within. Lanes without
           // `within` hold within = INT64_MAX, so their deadline saturates and never passes: the
           // check needs no group-level flag (one compare and branch per event)
-          if (__ballot(tt > bdead) != 0) {
+          if (__ballot(tt32 > bdead) != 0) {
             while (true) {
-              const bool ex = D.n() > 0 && tt > bdead;
+              const bool ex = D.n() > 0 && tt32 > bdead;
               if (__ballot(ex) == 0) break;
               if (ex) {
                 D.pop_front();
                 refill();
                 refresh_bottom();
-                if (D.n() == 0) bdead = INT64_MAX;
                 if (SIM && D.ln == 0) tkey = TSENT;
               }
             }
@@ -976,7 +1008,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
             refresh_top();
           }
         }
-        bdead = (p > 0 && D.n() == 0) ? INT64_MAX : bdead;
+        bdead = (p > 0 && D.n() == 0) ? INT32_MAX : bdead;
         // more matches are possible only where four were popped or the top was refilled
         mt = SIM ? (fix && xop<KK, XM>(xmask, x, tkey)) : (fix && x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey));
         m = __ballot(mt);
@@ -1009,9 +1041,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       const bool push = f && D.ln < ML;
       if constexpr (SIM) D.lput_ks(push ? D.li(D.lbot + D.ln) : ML * WAVE + lane, x, slo);  // (dummy row)
       else if (push) D.lput_ks(D.li(D.lbot + D.ln), x, slo);  // ts0 = ts of this batch event
-      const bool first = push && D.n() == 0;
-      bseq = first ? slo : bseq;
-      bdead = first ? sat_add(tt, within) : bdead;
+      if constexpr (!FULL) {  // a push into an empty deque sets its deadline (see bdead)
+        const int32_t dl = __builtin_elementwise_add_sat(tt32, w32);
+        bdead = push ? min(bdead, dl) : bdead;
+      }
       D.ln += push ? 1 : 0;
       tkey = push ? x : tkey;
       tseq = push ? slo : tseq;

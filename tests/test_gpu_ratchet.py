@@ -168,6 +168,40 @@ def test_ratchet_unordered_timestamps_exact():
     assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2)
 
 
+def test_ratchet_wide_timestamp_spans_and_windows():
+    """The lazy forms compare deadlines in a 32-bit domain relative to each item's first timestamp
+    (nfa_ratchet.hip rel_deadline): windows beyond 2^31 ms clamp to `never within this batch`,
+    partials carried from far older batches clamp to `already expired`, and a batch spanning 2^31 ms
+    or more runs in the FULL form. Timestamps far from 0, chunked and unchunked."""
+    src = ("define stream S (v int); "
+           "@info(name='a') from every e1=S[v > 2] -> e2=S[v > e1.v] within 35 days select e1.v as x insert into O; "
+           "@info(name='b') from every e1=S -> e2=S[v < e1.v] within 3 sec select e1.v as x insert into O; "
+           "@info(name='c') from every e1=S[v < 7] -> e2=S[v >= e1.v] within 40 milliseconds "
+           "select e1.v as x insert into O;")
+    rng = np.random.default_rng(21)
+    base = 1 << 40
+    batches = []
+    t = base
+    for n, step_hi in ((4000, 3), (3000, 2_000_000), (2500, 3), (2000, 5_000_000), (3000, 2)):
+        ts = t + np.cumsum(rng.integers(0, step_hi, n)).astype(np.int64)
+        t = int(ts[-1])
+        batches.append((ts, rng.integers(0, 12, n).astype(np.int32)))
+    # a gap of ~30 days between two batches and one batch whose own span is > 2^31 ms
+    batches[2] = (batches[2][0] + 30 * 86_400_000, batches[2][1])
+    t = int(batches[2][0][-1])
+    batches[3] = (t + np.sort(rng.integers(0, 3 << 31, 2000)).astype(np.int64), batches[3][1])
+    t = int(batches[3][0][-1])
+    batches[4] = (t + np.cumsum(rng.integers(0, 2, 3000)).astype(np.int64), batches[4][1])
+    for chunk in (0, 256):
+        o = App(src)
+        g = hip_app(src, chunk_events=chunk)
+        for ts, v in batches:
+            o.engine.send(0, ts, v.astype(np.int64)[:, None], None)
+            g.engine.push_columns(0, ts, [v])
+            assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2)
+        assert g.engine.stats().matches > 10000
+
+
 def test_ratchet_snapshot_restore():
     src = c2_app(66)
     a = hip_app(src)
