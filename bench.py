@@ -602,12 +602,16 @@ def push_latency(args, sh, K, local):
     Event) / receive(Event[]) chunks, StreamJunction.java:376-389): host-resident events of 1, 64 and
     4,096, normal mode (every match polled to the host in R18 order). Median and p99 over 50 pushes
     after 5 warm-up pushes (4,096: 10 after 2; at 10K C2 patterns such a push carries ~17M matches),
-    continuing one stream. A second engine fed the same pushes polls the compact rows instead
+    continuing one stream; keyed workloads reserve their K keys' state first
+    (sdh_engine_reserve_keys). A second engine fed the same pushes polls the compact rows instead
     (sdh_engine_poll_compact_ex to the host: 16 B per C2 match instead of ~72; `compact_*`)."""
     from siddhi_amd.engine import EngineError
     from siddhi_amd.workloads import stock_events, txn_events
     eng = make_engine(args.workload, sh, K, local, 0, args.partials)
     ceng = make_engine(args.workload, sh, K, local, 0, args.partials)
+    if args.workload in ("c3", "c5"):  # per-key state sized for the K keys up front (no growth copy
+        for x in (eng, ceng):          # inside a push while new keys keep appearing)
+            x.reserve_keys(K)
     gen = txn_events if args.workload == "c4" else stock_events
     out, lo = {}, 0
     compact_ok = True

@@ -237,6 +237,13 @@ int sdh_engine_state_bytes(sdh_engine* e, int64_t* live_bytes, int64_t* reserved
  * (One large device allocation can stall for seconds; a deployment that knows its state size sizes it
  * once here, before the first push.) No-op for an engine without K_slab sets. */
 int sdh_engine_reserve(sdh_engine* e, int64_t bytes);
+/* Size every partitioned state (per-key instance blocks of K_gen / K_part, K_slab key directories)
+ * for `keys` distinct partition keys now, so that pushes bringing the first `keys` keys never
+ * reallocate and copy that state (a push that does stalls for the copy: the p99 of small pushes while
+ * keys keep appearing). The reference creates a key's instances lazily on its first event
+ * (partition/PartitionRuntime.java:257-306); results are identical either way. `keys` <=
+ * sdh_config.gen_max_keys; SDH_E_INVALID beyond it. */
+int sdh_engine_reserve_keys(sdh_engine* e, int64_t keys);
 /* The text behind string dictionary ids, as String.hashCode and UTF-16 length per id. Needed only by
  * a partition keyed by a string attribute whose queries also read a stream it does not key: that
  * stream reaches every key's junction in the order of a ConcurrentHashMap of "streamId" +

@@ -573,6 +573,12 @@ RatchetPlan ratchet_plan(const ChainQuery& c) {
   return r;
 }
 
+// SDH_ALLOC_TRACE=1: one stderr line per device buffer (re)allocation (p99 push/poll latency hunts)
+inline void alloc_trace(const char* what, size_t bytes) {
+  static const bool on = getenv("SDH_ALLOC_TRACE") != nullptr;
+  if (on) fprintf(stderr, "[sdh] alloc %s %zu bytes\n", what, bytes);
+}
+
 template <class T>
 struct DevBuf {
   T* p = nullptr;
@@ -582,6 +588,7 @@ struct DevBuf {
   void ensure(size_t want) {
     if (want <= n) return;
     const size_t cap = std::max(want, n + n / 2);
+    alloc_trace("ensure", cap * sizeof(T));
     if (p) HIPCHK(hipFree(p));
     p = nullptr;
     n = 0;
@@ -598,6 +605,7 @@ struct DevBuf {
   void grow_keep(size_t want, size_t keep, hipStream_t s) {
     if (want <= n) return;
     size_t cap = std::max(want, n * 2);
+    alloc_trace("grow_keep", cap * sizeof(T));
     T* q = nullptr;
     if (hipMalloc(&q, cap * sizeof(T)) != hipSuccess)
       throw Error(SDH_E_CAPACITY, fmt("device memory exhausted growing a %zu-byte buffer", cap * sizeof(T)));
@@ -622,6 +630,7 @@ struct HostBuf {
     if (want <= n) return;
     release();
     const size_t cap = std::max(want, n * 2);
+    alloc_trace("host", cap * sizeof(T));
     if (hipHostMalloc((void**)&p, cap * sizeof(T), hipHostMallocDefault) == hipSuccess) {
       pinned = true;
     } else {
@@ -822,6 +831,7 @@ struct sdh_engine {
     size_t arena_bytes = 0;
     bool add_chunk(size_t bytes) {
       void* p = nullptr;
+      alloc_trace("slab_chunk", bytes);
       if (hipMalloc(&p, bytes) != hipSuccess) {
         (void)hipGetLastError();
         return false;
@@ -4238,6 +4248,25 @@ int sdh_engine_reserve(sdh_engine* e, int64_t bytes) {
     for (auto& ss : e->ssets)
       if (ss->arena_bytes < per && !ss->add_chunk(((per - ss->arena_bytes) + 4095) & ~(size_t)4095))
         throw Error(SDH_E_CAPACITY, fmt("device memory exhausted reserving %.1f GB for the sparse state", bytes / 1e9));
+    return SDH_OK;
+  });
+}
+
+int sdh_engine_reserve_keys(sdh_engine* e, int64_t keys) {
+  if (!e || keys < 0) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    check_usable(e);
+    HIPCHK(hipSetDevice(e->dev));
+    if (keys == 0) return SDH_OK;
+    for (auto& r : e->routes)
+      if (r && keys > r->max_keys)
+        throw Error(SDH_E_INVALID, fmt("reserve_keys(%lld) beyond gen_max_keys (%lld)", (long long)keys,
+                                       (long long)r->max_keys));
+    // the same growth calls a push makes when its batch brings new keys (a prefix copy of held state)
+    for (auto& gs : e->gsets)
+      if (gs->partition >= 0 && gs->n_groups > 0) gen_grow(e, *gs, keys);
+    for (auto& ps : e->psets) part_grow(e, *ps, keys);
+    for (auto& ss : e->ssets) slab_grow_keys(e, *ss, keys);
     return SDH_OK;
   });
 }

@@ -78,7 +78,7 @@ EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engi
            "sdh_engine_debug_digest", "sdh_engine_set_strings", "sdh_calibrate_hbm", "sdh_build_info",
            "sdh_engine_push_stats", "sdh_comm_get_id", "sdh_comm_create", "sdh_comm_create_local",
            "sdh_comm_destroy", "sdh_comm_last_error", "sdh_engine_set_comm", "sdh_engine_push_bcast",
-           "sdh_engine_gather", "sdh_engine_reserve"]
+           "sdh_engine_gather", "sdh_engine_reserve", "sdh_engine_reserve_keys"]
 SDH_COMM_ID_BYTES = 128
 
 _lib = None
@@ -109,6 +109,7 @@ def load_library(path: str = LIB_PATH):
     I64P = ctypes.POINTER(ctypes.c_int64)
     lib.sdh_engine_state_bytes.argtypes = [P, I64P, I64P, I64P]
     lib.sdh_engine_reserve.argtypes = [P, ctypes.c_int64]
+    lib.sdh_engine_reserve_keys.argtypes = [P, ctypes.c_int64]
     lib.sdh_engine_snapshot.argtypes = [P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
     lib.sdh_engine_restore.argtypes = [P, ctypes.c_void_p, ctypes.c_size_t]
     lib.sdh_free.argtypes = [P]
@@ -384,6 +385,10 @@ class HipEngine:
     def reserve(self, nbytes: int):
         """Pre-allocate HBM for the sparse K_slab state (sdh_engine_reserve)."""
         self._check(self.lib.sdh_engine_reserve(self.h, int(nbytes)))
+
+    def reserve_keys(self, keys: int):
+        """Size the partitioned state for `keys` partition keys now (sdh_engine_reserve_keys)."""
+        self._check(self.lib.sdh_engine_reserve_keys(self.h, int(keys)))
 
     def snapshot(self) -> bytes:
         p = ctypes.c_void_p()

@@ -134,3 +134,27 @@ def test_c3_family_kpart_equals_kgen():
         for u, v in zip(x, y):
             assert np.array_equal(u, v)
     assert a.engine.stats().matches > 10000
+
+
+def test_reserve_keys_presizes_and_keeps_results():
+    """sdh_engine_reserve_keys sizes the per-key state up front (no growth copy inside later pushes);
+    the matches equal an engine that grows as keys appear, K_gen (FORCE_GEN) and K_part alike, and a
+    reservation beyond gen_max_keys is refused."""
+    from siddhi_amd.engine import EngineError
+    src = _queries(31, n=15)
+    ts, vals, nl = _events(31, 5000, keys=300)
+    o = App(src)
+    nq = lambda q: len(o.ir.queries[q].states)  # noqa: E731
+    o.engine.send(0, ts, vals, nl)
+    want = o.engine.take_matches(nq)
+    assert len(want) > 100
+    for flags in (0, SDH_FLAG_FORCE_GEN):
+        g = _hip_app(src, flags=flags, gen_max_keys=512)
+        g.engine.reserve_keys(300)
+        g.engine.reserve_keys(100)  # (smaller: no-op)
+        with pytest.raises(EngineError):
+            g.engine.reserve_keys(513)
+        for lo in range(0, len(ts), 250):
+            sl = slice(lo, lo + 250)
+            g.engine.send(0, ts[sl], vals[sl], nl[sl])
+        assert g.engine.take_matches(nq) == want
