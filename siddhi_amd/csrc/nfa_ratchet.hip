@@ -45,6 +45,13 @@ namespace sdh {
 
 namespace {
 
+// ballot of a bool (HIP's __ballot takes an int: the bool -> int -> bool round trip costs a v_cndmask
+// and a v_cmp per ballot in the event loop)
+__device__ __forceinline__ uint64_t wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ int wave_mbcnt(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -102,7 +109,7 @@ __device__ int64_t lower_bound_ts(const int64_t* ts, int64_t c0, int64_t target,
   while (hi - lo > 1) {
     const int64_t span = hi - lo;
     const int64_t p = lo + (span * lane) / WAVE;
-    const uint64_t m = __ballot(ts[p] < target);
+    const uint64_t m = wballot(ts[p] < target);
     const int nb = __popcll(m);
     const int64_t nlo = nb == 0 ? lo : lo + (span * (nb - 1)) / WAVE + 1;
     const int64_t nhi = nb == WAVE ? hi : lo + (span * nb) / WAVE;
@@ -620,7 +627,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     return ok;
   };
 
-  bool overflow = false, unordered = false, mover = false, aged = false;
+  // error flags as ints (a bool carried through the loops becomes a lane-mask phi: three SALU ops at
+  // every merge point of the event loop)
+  int overflow = 0, unordered = 0, mover = 0, aged = 0;
   // persisted deques of the group (pending partials at the start of the batch), oldest first
   const size_t gb = (size_t)W.g * L.rsmax * WAVE;
   const int n_in = pick(L.st, W.inb)[W.g].n[lane];
@@ -632,7 +641,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     // ---- first chunk: start from the persisted deques ----
     for (int i = 0; i < n_in; ++i) {
       const size_t o = gb + (size_t)i * WAVE + lane;
-      if (!D.push_back(i_ts[o], (U)i_ky[o], (uint32_t)i_sq[o])) overflow = true;
+      if (!D.push_back(i_ts[o], (U)i_ky[o], (uint32_t)i_sq[o])) overflow = 1;
     }
   } else {
     // ---- later chunk: rebuild the pending partials at c0 by a REVERSE scan (exact, O(1) per
@@ -670,7 +679,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       if (r_has && (!sh || better(r_val, sv))) sv = r_val;
       sh = sh || r_has;
       const bool cand = live && (vb & 1u) && !(sh && xop<KK, XM>(xmask, sv, xk));
-      uint64_t cm = __ballot(cand);
+      uint64_t cm = wballot(cand);
       while (cm) {  // newest candidate first: prepend
         const int k = 63 - __builtin_clzll(cm);
         cm &= ~(1ull << k);
@@ -678,7 +687,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
         const int64_t tk = readlane64(ets, k);
         const U xkk = rlane(xk, k);
         if (f0_pass(k, vbk) && !expired(tk, t_last, within))
-          if (!D.push_front(tk, xkk, (uint32_t)(seq_base + lo + k))) overflow = true;
+          if (!D.push_front(tk, xkk, (uint32_t)(seq_base + lo + k))) overflow = 1;
       }
       const U tv = rlane(vv, 0);
       const bool th = __builtin_amdgcn_readlane((uint32_t)vh, 0) != 0;
@@ -722,7 +731,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       if (r_has && (!rh || better(r_val, rv))) rv = r_val;
       rh = rh || r_has;
       const bool need = tl && shs && !(rh && xop<KK, XM>(xmask, rv, smx));
-      uint64_t nm = __ballot(need);
+      uint64_t nm = wballot(need);
       while (nm) {  // newest tile first
         const int b = 63 - __builtin_clzll(nm);
         nm &= ~(1ull << b);
@@ -734,13 +743,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     }
     if (w0 == 0) {
       // the window reaches the batch start: carried partials survive unless expired or matched
-      if (L.b.prev_ts > L.b.ts[0]) unordered = true;
+      if (L.b.prev_ts > L.b.ts[0]) unordered = 1;
       for (int i = n_in - 1; i >= 0; --i) {
         const size_t o = gb + (size_t)i * WAVE + lane;
         const int64_t t0 = i_ts[o];
         const U ky = (U)i_ky[o];
         if (!expired(t0, t_last, within) && !(r_has && xop<KK, XM>(xmask, r_val, ky)))
-          if (!D.push_front(t0, ky, (uint32_t)i_sq[o])) overflow = true;
+          if (!D.push_front(t0, ky, (uint32_t)i_sq[o])) overflow = 1;
       }
     }
   }
@@ -748,6 +757,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
   // Keep the top of every non-empty deque in LDS (ln >= 1): move the newest spilled entry up.
   auto refill = [&]() {
     if (D.ln == 0 && D.sn > 0) {
+      // (an opaque copy of lbot: the slot address math stays on this rare path instead of being
+      // hoisted into every matching event by loop-invariant code motion)
+      asm volatile("" : "+v"(D.lbot));
       int64_t t0; U k0; uint32_t q0;
       D.sget(D.si(D.sbot + D.sn - 1), t0, k0, q0);
       --D.sn;
@@ -784,7 +796,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
   constexpr int FULL_FILL = 1 << 30;
   int blk = -1, fill = FULL_FILL;
   unsigned long long n_emit = 0;  // records of this wave's closed blocks (ring mode: the blocks wrap)
-  uint2* wb = nullptr;            // the wave's current output block
+  // the wave's current output block as a buffer resource: a record's address is a 32-bit lane offset
+  // from the block base (no 64-bit address arithmetic per record), and the range check covers it
+  __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(L.match, 0, 0, 0x00020000);
   int64_t prev_tile_ts = (W.c0 == 0) ? L.b.prev_ts : L.b.ts[W.c0 - 1];
 
   // one record per lane with `mt` (ballot m): per-wave output blocks (one atomic per block), ranks
@@ -827,7 +841,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     nb = __builtin_amdgcn_readfirstlane(nb);
     if (L.ring) nb = (int)((uint32_t)nb % (uint32_t)L.n_blocks);
     if (nb >= L.n_blocks) {
-      mover = true;
+      mover = 1;
       blk = -1;
       nb = L.n_blocks;
     } else {
@@ -835,7 +849,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       blk = nb;
     }
     fill = 0;
-    wb = reinterpret_cast<uint2*>(L.match) + ((size_t)nb * L.blk_recs << (wide ? 1 : 0));
+    const int rb = wide ? 16 : 8;
+    const uint64_t base = (uint64_t)(reinterpret_cast<char*>(L.match) + (size_t)nb * L.blk_recs * rb);
+    const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)base), bhi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    wrs = __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)bhi << 32) | blo), 0,
+                                            __builtin_amdgcn_readfirstlane(L.blk_recs * rb), 0x00020000);
   };
   auto emit_room = [&]() {
     if constexpr (PM == 0 || PM == 3)
@@ -853,8 +871,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     }
     if (mt) {
       const int r = fill + wave_mbcnt(m);
-      if (!wide) wb[r] = make_uint2(off | ((uint32_t)lane << 26), q1);
-      else reinterpret_cast<uint4*>(wb)[r] = make_uint4(off, (uint32_t)lane, q1, 0u);
+      if (!wide) {
+        const u32x2 v = {off | ((uint32_t)lane << 26), q1};
+        __builtin_amdgcn_raw_buffer_store_b64(v, wrs, r * 8, 0, 0);
+      } else {
+        const u32x4 v = {off, (uint32_t)lane, q1, 0u};
+        __builtin_amdgcn_raw_buffer_store_b128(v, wrs, r * 16, 0, 0);
+      }
     }
     fill += __popcll(m);
   };
@@ -876,7 +899,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     const bool live = cur.live;
     int64_t pred = __shfl_up(ets, 1, WAVE);
     if (lane == 0) pred = prev_tile_ts;
-    if (live && ets < pred) unordered = true;
+    if (live && ets < pred) unordered = 1;
     prev_tile_ts = __shfl(ets, WAVE - 1, WAVE);
     // the lazy forms compare in the 32-bit deadline domain (rel_deadline)
     int32_t ets32 = 0;
@@ -885,7 +908,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     const int cnt = (int)((W.c1 - t) < WAVE ? (W.c1 - t) : WAVE);
     // sequence numbers are kept as their low 32 bits: a live partial must stay < 2^31 events old
     // (checked once per tile against the tile's last event; the bottom only gets younger)
-    if (D.n() > 0 && (uint32_t)((uint32_t)(seq_base + t + cnt - 1) - D.bottom_seq()) >= 0x80000000u) aged = true;
+    if (D.n() > 0 && (uint32_t)((uint32_t)(seq_base + t + cnt - 1) - D.bottom_seq()) >= 0x80000000u) aged = 1;
     if constexpr (PM == 1) cntv = 0;
     if constexpr (PM == 2) basev = lane < cnt ? L.pbase[(int64_t)(t + lane) * L.n_cells + cell] : 0;
 
@@ -905,10 +928,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
           // timestamps non-decreasing: expired(bts, tt) <=> tt > bts + within. Lanes without
           // `within` hold within = INT64_MAX, so their deadline saturates and never passes: the
           // check needs no group-level flag (one compare and branch per event)
-          if (__ballot(tt32 > bdead) != 0) {
+          if (wballot(tt32 > bdead) != 0) {
             while (true) {
               const bool ex = D.n() > 0 && tt32 > bdead;
-              if (__ballot(ex) == 0) break;
+              if (wballot(ex) == 0) break;
               if (ex) {
                 D.pop_front();
                 refill();
@@ -920,7 +943,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
         } else {
           const int n0 = D.n();
           D.compact_expired(tt, within);
-          if (__ballot(D.n() != n0) != 0) {
+          if (wballot(D.n() != n0) != 0) {
             refill();
             refresh_top();
             refresh_bottom();
@@ -930,7 +953,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
 
       // ---- 2. matches: the newest partials whose key satisfies `cur OP key` ----
       bool mt = SIM ? xop<KK, XM>(xmask, x, tkey) : (x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey));
-      uint64_t m = __ballot(mt);
+      uint64_t m = wballot(mt);
       if constexpr (PM == 1) ev_tot = 0;
       if constexpr (PM == 2) lv = 0;
       bool round1 = true;
@@ -953,9 +976,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
             const int p1 = (int)mt + (int)c1 + (int)c2 + (int)c3;
             const bool more = mt && ((p1 == 4 && D.ln > 4) || (p1 == D.ln && D.sn > 0));
             const int64_t base = L.row0 + (int64_t)__builtin_amdgcn_readlane(basev, k);
-            if (__ballot(more) == 0) {
-              const int below = wave_mbcnt(m) + wave_mbcnt(__ballot(c1)) + wave_mbcnt(__ballot(c2)) +
-                                wave_mbcnt(__ballot(c3));
+            if (wballot(more) == 0) {
+              const int below = wave_mbcnt(m) + wave_mbcnt(wballot(c1)) + wave_mbcnt(wballot(c2)) +
+                                wave_mbcnt(wballot(c3));
               pos = base + below + p1 - 1;
             } else {
               int cl = p1;
@@ -986,32 +1009,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
           }
         }
         emit(mt, m, off, tseq);
-        const uint64_t m1 = __ballot(c1);
+        const uint64_t m1 = wballot(c1);
         if (m1) {
           emit(c1, m1, off, q1);
-          const uint64_t m2 = __ballot(c2);
+          const uint64_t m2 = wballot(c2);
           if (m2) {
             emit(c2, m2, off, q2);
-            const uint64_t m3 = __ballot(c3);
+            const uint64_t m3 = wballot(c3);
             if (m3) emit(c3, m3, off, q3);
           }
         }
         const int p = (int)mt + (int)c1 + (int)c2 + (int)c3;
         D.ln -= p;
-        // new top: prefetched unless four popped (then read it) or the LDS part ran dry
-        tkey = p == 1 ? k1 : p == 2 ? k2 : p == 3 ? k3 : tkey;
-        tseq = p == 1 ? q1 : p == 2 ? q2 : p == 3 ? q3 : tseq;
-        const bool fix = (p == 4 && D.ln > 0) || (p > 0 && D.ln == 0);
-        if (__ballot(fix) != 0) {
-          if (fix) {
-            refill();
-            refresh_top();
-          }
+        // new top: prefetched unless four popped (then read it) or the LDS part ran dry. The pop
+        // masks nest (c3 -> c2 -> c1 -> mt), so three selects place the entry under the last pop
+        tkey = mt ? k1 : tkey;
+        tkey = c1 ? k2 : tkey;
+        tkey = c2 ? k3 : tkey;
+        tseq = mt ? q1 : tseq;
+        tseq = c1 ? q2 : tseq;
+        tseq = c2 ? q3 : tseq;
+        const bool fix = (c3 && D.ln > 0) || (mt && D.ln == 0);
+        // (a plain divergent `if`: its exec-mask skip branch is the wave-uniform test; an outer
+        // ballot would re-materialise the mask through a VGPR)
+        if (fix) {
+          refill();
+          refresh_top();
         }
         bdead = (p > 0 && D.n() == 0) ? INT32_MAX : bdead;
         // more matches are possible only where four were popped or the top was refilled
         mt = SIM ? (fix && xop<KK, XM>(xmask, x, tkey)) : (fix && x_ok && D.ln > 0 && xop<KK, XM>(xmask, x, tkey));
-        m = __ballot(mt);
+        m = wballot(mt);
       }
       if constexpr (PM == 1) cntv = lane == k ? ev_tot : cntv;
 
@@ -1023,19 +1051,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       } else {
         f = f0_pass(k, vb);
       }
-      if (__ballot(f && D.ln == ML) != 0) {
+      if (f && D.ln == ML) {
         // LDS ring full: move its oldest entry to the spill ring (rare)
-        if (f && D.ln == ML) {
-          if (D.sn == SC) {
-            overflow = true;
-          } else {
-            int64_t t0; U k0; uint32_t q0;
-            D.lget(D.li(D.lbot), t0, k0, q0);
-            D.sput(D.si(D.sbot + D.sn), t0, k0, q0);
-            ++D.sn;
-            D.lbot = (D.lbot + 1) & D.lmask;
-            --D.ln;
-          }
+        if (D.sn == SC) {
+          overflow = 1;
+        } else {
+          int64_t t0; U k0; uint32_t q0;
+          D.lget(D.li(D.lbot), t0, k0, q0);
+          D.sput(D.si(D.sbot + D.sn), t0, k0, q0);
+          ++D.sn;
+          D.lbot = (D.lbot + 1) & D.lmask;
+          --D.ln;
         }
       }
       const bool push = f && D.ln < ML;
@@ -1058,7 +1084,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     if (lane == 0) L.blk_count[blk] = fill;
     n_emit += (unsigned long long)fill;
   }
-  const uint64_t any_over = __ballot(overflow), any_unord = __ballot(unordered), any_aged = __ballot(aged);
+  const uint64_t any_over = wballot(overflow != 0), any_unord = wballot(unordered != 0), any_aged = wballot(aged != 0);
   if (lane == 0) {
     if (L.ring && n_emit) atomicAdd(L.rec_total, n_emit);
     if (any_over) atomicOr(&L.err[0], 1);
