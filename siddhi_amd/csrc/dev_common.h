@@ -125,8 +125,22 @@ template <int CAPW_>
 struct WaveOutT {
   static constexpr int CAPW = CAPW_;
   static constexpr int CAPR = CAPW / 4 + 1;    // records (>= 4 words each: K_part's narrow ones)
+  // LDS word x of the buffer lives at x ^ ((x >> 4) & 15) (an XOR swizzle inside each 16-word
+  // block): the lanes of one collective emit write records of `words` words at lane-strided offsets,
+  // and a ds_write_b64 serves 16 contiguous lanes per cycle on 16 qword banks, so 4- and 8-word
+  // records would put 4 or 8 lanes on one bank; the swizzle spreads them (a 16-word block's lanes get
+  // distinct banks for any power-of-two stride), and the flush's consecutive reads stay (nearly) free
+  static_assert(CAPW % 16 == 0, "the LDS swizzle works in 16-word blocks");
+  static constexpr int PADW = CAPW;
+  __device__ static int pidx(int x) { return x ^ ((x >> 4) & 15); }
+  struct Rec {  // a record's words in the padded buffer (pointer-like: r[i], r + k)
+    int64_t* b;
+    int off;
+    __device__ int64_t& operator[](int i) const { return b[pidx(off + i)]; }
+    __device__ Rec operator+(int d) const { return Rec{b, off + d}; }
+  };
   struct Shared {
-    int64_t buf[CAPW];
+    int64_t buf[PADW];
     int32_t roff[CAPR];
     int64_t base, rbase;
     int32_t used, nrec;
@@ -197,18 +211,21 @@ struct WaveOutT {
       g.over = true;
     } else if (g.ring) {
       const int64_t rc = g.cap - GEN_RING_MARGIN, b0 = (int64_t)((unsigned long long)base % (unsigned long long)rc);
-      for (int i = me; i < n; i += cnt) g.out[b0 + i < rc ? b0 + i : b0 + i - rc] = sh->buf[i];
+      for (int i = me; i < n; i += cnt) g.out[b0 + i < rc ? b0 + i : b0 + i - rc] = sh->buf[pidx(i)];
     } else {
-      for (int i = me; i < n; i += cnt) g.out[base + i] = sh->buf[i];
+      for (int i = me; i < n; i += cnt) g.out[base + i] = sh->buf[pidx(i)];
       for (int i = me; i < nr; i += cnt) g.rec_off[rbase + i] = base + sh->roff[i];
     }
     wave_fence();
-    st(sh->used, 0);  // (every active lane writes the same values)
-    st(sh->nrec, 0);
+    if (__lane_id() == lead) {  // (one lane: 64 same-address writes serialise as bank conflicts)
+      st(sh->used, 0);
+      st(sh->nrec, 0);
+    }
     wave_fence();
   }
   // `nl` records of `words` words each for this lane (collective over the active lanes: they all
-  // call it at the same point), written by fill(int64_t* r): record i at r + i * words, into the LDS
+  // call it at the same point), written by fill(r) (r: a Rec into the LDS buffer, or an int64_t* into
+  // a global reservation; generic callbacks index both alike): record i at r + i * words, into the LDS
   // buffer. A call larger than the buffer's free room goes in rounds: each round places the lanes
   // (in lane order) whose words and records fit, then the buffer is flushed. Only a lane whose own
   // records exceed the whole buffer reserves globally, as LaneOut does.
@@ -275,9 +292,12 @@ struct WaveOutT {
       if (fits)
         for (int i = 0; i < mnl; ++i) sh->roff[r0 + i] = off + i * words;
       wave_fence();
-      st(sh->used, used + wend - wdone);  // (every active lane writes the same values)
-      st(sh->nrec, nr + rend - rdone);
-      if (fits) fill(sh->buf + off);
+      if (__lane_id() == __ffsll((long long)active()) - 1) {  // (one lane, as in flush)
+        st(sh->used, used + wend - wdone);
+        st(sh->nrec, nr + rend - rdone);
+      }
+      wave_fence();
+      if (fits) fill(Rec{sh->buf, off});
       wdone = wend;
       rdone = rend;
     }
@@ -286,7 +306,7 @@ struct WaveOutT {
       if (r) fill(r);
     }
   }
-  // this lane's record of `words` words, written by fill(int64_t* r)
+  // this lane's record of `words` words, written by fill(r)
   template <class F>
   __device__ void emit(int words, F&& fill) {
     emit_n(1, words, fill);

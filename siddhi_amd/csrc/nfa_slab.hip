@@ -225,7 +225,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
         if (L.write_records && __ballot(em) != 0) {  // (the collective emit only when a lane emits)
           const int words = em ? record_words(sh, e, st) : 0;
           const int64_t idx = (int64_t)pos_of(e, sh.elem[st]);
-          o.emit_n(em ? 1 : 0, words, [&](int64_t* rr) {
+          o.emit_n(em ? 1 : 0, words, [&](auto rr) {
             write_record(sh, e, st, words, qid, key, idx, stream, ev, rr);
           });
         }

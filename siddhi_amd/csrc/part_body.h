@@ -384,7 +384,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
         const int64_t e1s = e.get(1);
         const bool nar = nb_ok && sq - e1s <= (int64_t)INT32_MAX;
         const int words = nar ? nrec_count_words(len) : 7 + 2 + 1 + len + 2;
-        o.emit_n(done >= 0 ? 1 : 0, words, [&](int64_t* r) {
+        o.emit_n(done >= 0 ? 1 : 0, words, [&](auto r) {
           if (nar) {
             r[0] = nrec_pack(-(words + 0x10000), qid);
             r[1] = nrec_pack(sq - L.b.seq_base, (int64_t)kid);
@@ -476,7 +476,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
         }
         // one match record at r: [words, qid, key, ts, seq, idx, 3 | stream, (1, seq) | (0) per slot]
         // (a_seq / b_seq -1: empty slot)
-        auto put_rec = [&](int64_t* r, int words, int64_t my_idx, int64_t e1seq, int64_t a_seq, int64_t b_seq) {
+        auto put_rec = [&](auto r, int words, int64_t my_idx, int64_t e1seq, int64_t a_seq, int64_t b_seq) {
           r[0] = words;
           r[1] = qid;
           r[2] = key;
@@ -496,7 +496,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
           }
         };
         // the narrow record (nfa_types.h): slots by state id, 0 = e1, sA = side A, the other side B
-        auto put_nrec = [&](int64_t* r, int64_t e1seq, int64_t a_seq, int64_t b_seq) {
+        auto put_nrec = [&](auto r, int64_t e1seq, int64_t a_seq, int64_t b_seq) {
           const int64_t s1 = sA == 1 ? a_seq : b_seq, s2 = sA == 1 ? b_seq : a_seq;
           r[0] = nrec_pack(-NREC_ORAND_WORDS, qid);
           r[1] = nrec_pack(seq - L.b.seq_base, (int64_t)kid);
@@ -520,11 +520,11 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
             if (L.write_records) {
               const int64_t as = fb ? -1 : seq, bs = fb ? seq : -1;  // words: 7 + 2 + 2 + 1
               if (narrow_ok(n))
-                o.emit_n(n, NREC_ORAND_WORDS, [&](int64_t* r0) {
+                o.emit_n(n, NREC_ORAND_WORDS, [&](auto r0) {
                   tab.each(n, [&](int kk, const auto& e) { put_nrec(r0 + kk * NREC_ORAND_WORDS, e.get(1), as, bs); });
                 }, true);
               else
-                o.emit_n(n, 12, [&](int64_t* r0) {
+                o.emit_n(n, 12, [&](auto r0) {
                   tab.each(n, [&](int kk, const auto& e) { put_rec(r0 + kk * 12, 12, kk, e.get(1), as, bs); });
                 }, true);
             }
@@ -540,7 +540,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
           if (L.write_records) {
             const bool nar = narrow_ok(c);
             const int words = nar ? NREC_ORAND_WORDS : 13;  // (wide: 7 + 2 + 2 + 2)
-            o.emit_n(c, words, [&](int64_t* r0) {
+            o.emit_n(c, words, [&](auto r0) {
               tab.each(c, [&](int kk, const auto& e) {
                 const bool filled = kk < F;
                 const int64_t aseq = (filled && side == 1) ? e.get(2) : seq;

@@ -109,7 +109,7 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
   if (lo + lane < rows_end) fetch(lo + lane, ra);
   if (lane < S - 1 && lo + 64 + lane < rows_end) fetch(lo + 64 + lane, rb);
   const int words = 7 + 2 * S;  // (the wave's shape's)
-  auto put_rec = [&](int64_t* r, int s) {
+  auto put_rec = [&](auto r, int s) {
     const Win wv{win + s * ROW};
     r[0] = words;
     r[1] = qid;
@@ -126,7 +126,7 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
   auto emit = [&](int s) {
     ++nrec;
     if (!L.write_records) return;
-    o.emit_u(words, [&](int64_t* r) { put_rec(r, s); });
+    o.emit_u(words, [&](auto r) { put_rec(r, s); });
   };
   // a lane's matches among 8 starts (mask m over s0 ..) in one collective call: its records are
   // contiguous, start order; the record counts take 4 ballots
@@ -134,7 +134,7 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
     const int nl = __popc(m);
     nrec += nl;
     if (!L.write_records || __ballot(nl > 0) == 0) return;
-    o.emit_n(nl, words, [&](int64_t* r0) {
+    o.emit_n(nl, words, [&](auto r0) {
       int kk = 0;
       for (uint32_t mm = m; mm; mm &= mm - 1, ++kk) put_rec(r0 + kk * words, s0 + __builtin_ctz(mm));
     }, true, 4);

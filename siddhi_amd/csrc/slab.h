@@ -275,9 +275,9 @@ KG_FN int record_words(const Shape& sh, const uint32_t* e, int st) {
   }
   return w;
 }
-template <class W>
+template <class R>  // R: a word pointer or a pointer-like record (dev::WaveOutT::Rec)
 KG_FN void write_record(const Shape& sh, const uint32_t* e, int st, int words, int64_t qid, int64_t key, int64_t idx,
-                        int stream, const Ev& ev, W* r) {
+                        int stream, const Ev& ev, R r) {
   r[0] = words;
   r[1] = qid;
   r[2] = key;

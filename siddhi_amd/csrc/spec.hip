@@ -186,7 +186,7 @@ std::string seq_source(const kg::GQuery& g, int out_w) {
   for (int st = 0; st < kg::GMAXSTREAM; ++st) na = std::max(na, (int)g.n_cap[st]);
   std::string s = tuning_defines() + header() + "#include \"seq_body.h\"\n\nstruct SpecSeq {\n  static constexpr bool kBranchFree = true;\n";
   s += fmt("  static constexpr int kRow = %d, kOutW = %d;\n", 3 + std::min(na, kg::GMAXNA),
-           env_int("SDH_KSEQ_OUTW", out_w > 0 ? out_w : 1024, 256, 4096));
+           env_int("SDH_KSEQ_OUTW", out_w > 0 ? out_w : 1024, 256, 4096) & ~15);  // (16-word LDS blocks)
   s += K.decl();
   s += K.load();
   s += "  template <class W>\n  __device__ static bool match(const K& k, const sdh::kg::GQuery*, const sdh::kg::GQuery*, "
@@ -261,7 +261,7 @@ std::string part_source(const kg::GQuery& g, const PartLayout& lay) {
   for (int st = 0; st < kg::GMAXSTREAM; ++st) na = std::max(na, (int)g.n_cap[st]);
   s += "  static constexpr bool kHotRegs = true;  // count partials' hot words in registers (part_body.h)\n";
   s += fmt("  static constexpr int kRegEntries = %d, kEW = %d, kNA = %d, kOutW = %d;\n", lay.reg_entries, lay.ew,
-           std::min(na, kg::GMAXNA), env_int("SDH_KPART_OUTW", lay.out_w > 0 ? lay.out_w : 1536, 256, 4096));
+           std::min(na, kg::GMAXNA), env_int("SDH_KPART_OUTW", lay.out_w > 0 ? lay.out_w : 1536, 256, 4096) & ~15);
   s += fmt("  __device__ static sdh::PartOffs offs(const sdh::PartLaunch&) { return sdh::PartOffs{%d, %d, %d, %d}; }\n",
            lay.cmax, lay.n_e1, lay.n_first, lay.n_last);
   s += K.decl();
