@@ -74,9 +74,10 @@ def parse():
     ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the small-push latency leg")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline sample budget")
-    ap.add_argument("--state-reserve-gb", type=float, default=170.0,
+    ap.add_argument("--state-reserve-gb", type=float, default=140.0,
                     help="c5: HBM reserved up front for the sparse K_slab state (sdh_engine_reserve): the state "
-                         "grows inside it with no device allocation during the run")
+                         "grows inside it with no device allocation during the run (the shard's steady state: "
+                         "~72 GB live in ~125 GB of rings)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-calibrate", action="store_true", help="skip the HBM copy / read ceiling measurement")
     return ap.parse_args()

@@ -2161,7 +2161,7 @@ void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int6
     // clean once the room falls below SDH_SLAB_CLEAN_AT x the push's need (then the live blocks of
     // the span still fit at the head: the in-place move needs room for them, and a span holds at most
     // SDH_SLAB_SPAN x need live words)
-    static const double clean_at = getenv("SDH_SLAB_CLEAN_AT") ? atof(getenv("SDH_SLAB_CLEAN_AT")) : 5.0;
+    static const double clean_at = getenv("SDH_SLAB_CLEAN_AT") ? atof(getenv("SDH_SLAB_CLEAN_AT")) : 3.0;
     if ((double)(ss.cap[r] - used) >= clean_at * (double)need[r]) continue;
     // the oldest quarter of the ring (at least twice the headroom): mostly dead copies, so the move
     // is small (SDH_SLAB_CLEAN=all: everything before the last push)
@@ -2169,8 +2169,10 @@ void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int6
     static const bool all = getenv("SDH_SLAB_CLEAN") && !strcmp(getenv("SDH_SLAB_CLEAN"), "all");
     // (the span a push needs, not a fixed share of the ring: every live block in it moves, and the
     // oldest blocks of a ring are not all dead -- a quarter of the ring per push moved 15 % of C5's
-    // device time)
-    static const double span_x = getenv("SDH_SLAB_SPAN") ? atof(getenv("SDH_SLAB_SPAN")) : 4.0;
+    // device time. C5 sweep, CLEAN_AT:SPAN:GROW_TO -> slab_move share of the 24-step run, ms/step,
+    // reserved/live: 5:4:1.6 10.0 %, 457, 1.80; 3:2:1.6 7.8 %, 458, 1.95; 3:2:1.5 8.8 %, 447, 1.75;
+    // 4:3:1.6 9.0 %, 469, 1.96; 5:8:1.6 30 %, 632; 9:8:1.6 42 %, 822; GROW_TO 2.0 at 5:4 5.9 %, 2.13)
+    static const double span_x = getenv("SDH_SLAB_SPAN") ? atof(getenv("SDH_SLAB_SPAN")) : 2.0;
     const unsigned long long span = (unsigned long long)std::max<int64_t>((int64_t)(span_x * need[r]), 4096);
     limit[r] = all ? cur : std::min<unsigned long long>(cur, ss.h_tail[r] + span);
     clean[r] = 1;
@@ -2193,7 +2195,7 @@ void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int6
     // ring's span, which counts dead blocks: sizing from the span doubled the reservation every
     // other C5 step and ran out of HBM)
     static const double grow_at = getenv("SDH_SLAB_GROW_AT") ? atof(getenv("SDH_SLAB_GROW_AT")) : 1.4;
-    static const double grow_to = getenv("SDH_SLAB_GROW_TO") ? atof(getenv("SDH_SLAB_GROW_TO")) : 1.6;
+    static const double grow_to = getenv("SDH_SLAB_GROW_TO") ? atof(getenv("SDH_SLAB_GROW_TO")) : 1.5;
     for (int r = 0; r < ss.nsub; ++r) {
       if (!clean[r]) continue;
       const int64_t used = (int64_t)(ss.h_head[r] - ss.h_tail[r]);
