@@ -422,7 +422,7 @@ def test_gen_output_overflow_reruns_exactly():
     src = c2_app(64)
     o = App(src)
     g = hip_app(src, flags=SDH_FLAG_FORCE_GEN)
-    for lo, hi in ((0, 30000), (30000, 40000)):  # the first push needs ~16M record words (4M buffer)
+    for lo, hi in ((0, 16000), (16000, 22000)):  # the first push needs ~8M record words (4M buffer)
         ts, sym, price, vol = stock_events(lo, hi - lo)
         vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64), vol.astype(np.int64)], 1)
         o.engine.send(0, ts, vals, None)

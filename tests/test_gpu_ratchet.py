@@ -27,18 +27,37 @@ def words(cols):
     return np.stack([c.astype(np.int64) for c in cols], 1)
 
 
+_ORACLE_CACHE = {}
+
+
+def _c2_oracle_batches(n_pat, sizes):
+    """The oracle's matches per batch of the C2 family (computed once per module: both chunk
+    parametrisations check against the same run)."""
+    key = (n_pat, sizes)
+    if key not in _ORACLE_CACHE:
+        o = App(c2_app(n_pat))
+        out, start = [], 0
+        for n in sizes:
+            ts, cols = c2_columns(start, n)
+            start += n
+            o.engine.send(0, ts, words(cols), None)
+            out.append(o.engine.take_matches(lambda q: 2))
+        _ORACLE_CACHE[key] = out
+    return _ORACLE_CACHE[key]
+
+
 @pytest.mark.parametrize("chunk", [0, 512])
 def test_c2_ratchet_vs_oracle_and_chain(chunk):
     src = c2_app(70)  # two wave groups, the second one partial
-    o = App(src)
+    sizes = (3000, 1, 12000, 777)
+    want = _c2_oracle_batches(70, sizes)
     r = hip_app(src, chunk_events=chunk)
     c = hip_app(src, chunk_events=chunk, partials=256, flags=SDH_FLAG_NO_RATCHET)
     start = 0
-    for n in (3000, 1, 12000, 777):
+    for bi, n in enumerate(sizes):
         ts, cols = c2_columns(start, n)
         start += n
-        o.engine.send(0, ts, words(cols), None)
-        om = o.engine.take_matches(lambda q: 2)
+        om = want[bi]
         r.engine.push_columns(0, ts, cols)
         rm = r.engine.take_matches(lambda q: 2)
         c.engine.push_columns(0, ts, cols)
@@ -132,19 +151,20 @@ def test_deque_growth_to_10k_partials():
     n = 12000
     ts = np.arange(n + 1, dtype=np.int64)
     v = np.concatenate([np.arange(n, 0, -1), [10 * n]]).astype(np.int32)
+    o = App(src)  # (one oracle run for both chunk modes)
+    o.engine.send(0, ts[:n], v[:n].astype(np.int64)[:, None], None)
+    assert o.engine.take_matches(lambda q: 2) == []
+    o.engine.send(0, ts[n:], v[n:].astype(np.int64)[:, None], None)
+    want = o.engine.take_matches(lambda q: 2)
     for chunk in (0, 1024):
-        o = App(src)
         g = hip_app(src, chunk_events=chunk)
-        o.engine.send(0, ts[:n], v[:n].astype(np.int64)[:, None], None)
         g.engine.push_columns(0, ts[:n], [v[:n]])
-        assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2) == []
+        assert g.engine.take_matches(lambda q: 2) == []
         assert g.engine.stats().live_partials == n + (n - 5000)
         g.engine.poll()
         snap = g.engine.snapshot()
         b = hip_app(src, chunk_events=chunk)
         b.engine.restore(snap)
-        o.engine.send(0, ts[n:], v[n:].astype(np.int64)[:, None], None)
-        want = o.engine.take_matches(lambda q: 2)
         g.engine.push_columns(0, ts[n:], [v[n:]])
         b.engine.push_columns(0, ts[n:], [v[n:]])
         assert len(want) == n + (n - 5000)
@@ -156,13 +176,13 @@ def test_ratchet_unordered_timestamps_exact():
     src = c2_app(70)
     o = App(src)
     g = hip_app(src, chunk_events=1024)
-    ts, cols = c2_columns(0, 30000)
+    ts, cols = c2_columns(0, 16000)
     ts = ts.copy()
     ts[9000:9050] -= 20000
     o.engine.send(0, ts, words(cols), None)
     g.engine.push_columns(0, ts, cols)
     assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2)
-    ts2, cols2 = c2_columns(30000, 5000)
+    ts2, cols2 = c2_columns(16000, 5000)
     o.engine.send(0, ts2, words(cols2), None)
     g.engine.push_columns(0, ts2, cols2)
     assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2)
