@@ -11,4 +11,6 @@ for w in $*; do
   bash profiles/collect.sh gpurun_out/p_$w "$A" $K || exit 1
   python3 profiles/summarize.py gpurun_out/p_$w gpurun_out/r5_$w $K $w $P $B > gpurun_out/p_$w.sum || exit 1
   grep -E "kernel_ns|traffic|issue|bank" gpurun_out/p_$w.sum
+  cp gpurun_out/p_$w/trace.log gpurun_out/r5_$w/trace.log
+  rm -rf gpurun_out/p_$w  # (the raw per-dispatch CSVs: C5's exceed what a call copies back)
 done
