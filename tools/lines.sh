@@ -1,7 +1,7 @@
 #!/bin/bash
 # The bench lines of a round: the default (driver) command, then C3 / C4 (and C5 with `c5`) with
 # their CPU baselines, each under its own time limit; logs in gpurun_out/line_<w>.log (copy to
-# profiles/r4_runs).
+# profiles/r5_runs).
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 400 python -u bench.py > gpurun_out/line_c2.log 2> gpurun_out/line_c2.err || { tail -20 gpurun_out/line_c2.err; exit 1; }
