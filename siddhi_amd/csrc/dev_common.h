@@ -121,18 +121,20 @@ struct LaneOut {
 #ifndef SDH_RING_CHUNK
 #define SDH_RING_CHUNK 4
 #endif
-template <int CAPW_>
+template <int CAPW_, bool SWZ = false>
 struct WaveOutT {
   static constexpr int CAPW = CAPW_;
   static constexpr int CAPR = CAPW / 4 + 1;    // records (>= 4 words each: K_part's narrow ones)
-  // LDS word x of the buffer lives at x ^ ((x >> 4) & 15) (an XOR swizzle inside each 16-word
-  // block): the lanes of one collective emit write records of `words` words at lane-strided offsets,
-  // and a ds_write_b64 serves 16 contiguous lanes per cycle on 16 qword banks, so 4- and 8-word
-  // records would put 4 or 8 lanes on one bank; the swizzle spreads them (a 16-word block's lanes get
-  // distinct banks for any power-of-two stride), and the flush's consecutive reads stay (nearly) free
-  static_assert(CAPW % 16 == 0, "the LDS swizzle works in 16-word blocks");
+  // SWZ: LDS word x of the buffer lives at x ^ ((x >> 4) & 15) (an XOR swizzle inside each 16-word
+  // block). The lanes of one collective emit write records of `words` words at lane-strided offsets,
+  // and a ds_write_b64 serves 16 contiguous lanes per cycle on 16 qword banks, so K_part's 4- and
+  // 8-word records would put 4 or 8 lanes on one bank; the swizzle spreads them (a 16-word block's
+  // lanes get distinct banks for any power-of-two stride: C3 9.6 % -> 1.3 % of LDS cycles). Odd
+  // record lengths (K_seq's 13 words) are conflict-free unswizzled and keep the plain layout (the
+  // swizzle put C4 at 5.0 % from 0.6 %).
+  static_assert(!SWZ || CAPW % 16 == 0, "the LDS swizzle works in 16-word blocks");
   static constexpr int PADW = CAPW;
-  __device__ static int pidx(int x) { return x ^ ((x >> 4) & 15); }
+  __device__ static int pidx(int x) { return SWZ ? x ^ ((x >> 4) & 15) : x; }
   struct Rec {  // a record's words in the padded buffer (pointer-like: r[i], r + k)
     int64_t* b;
     int off;
@@ -316,7 +318,7 @@ struct WaveOutT {
     over |= g.over;
   }
 };
-using WaveOut = WaveOutT<1536>;    // K_part
+using WaveOut = WaveOutT<1536, true>;  // K_part
 using SeqWaveOut = WaveOutT<1024>; // K_seq
 
 __device__ __forceinline__ bool expired(int64_t ts1, int64_t ts, int64_t within) {

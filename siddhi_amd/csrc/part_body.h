@@ -262,7 +262,7 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
   // read by broadcast: ts, seq, null bits and the captured words
   // (LDS per wave bounds the resident waves: the staging holds the shape's captured words only, and
   // the Spec sizes the output buffer)
-  using Out = dev::WaveOutT<Spec::kOutW>;
+  using Out = dev::WaveOutT<Spec::kOutW, true>;  // (swizzled LDS records: 4- to 8-word records)
   __shared__ int64_t t_ts[64], t_seq[64], t_w[Spec::kNA][64];
   __shared__ uint32_t t_nul[64];
   __shared__ typename Out::Shared out_sh;
