@@ -298,8 +298,11 @@ def timed_steps(eng, step, warmup, steps, world, dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    step_wall = []  # (host clock per step call: a push returns once its step is done)
     for i in range(warmup, warmup + steps):
+        ts = time.perf_counter()
         ms, by, nm = step(i)
+        step_wall.append((time.perf_counter() - ts) * 1e3)
         kern_ms.append(ms)
         kern_bytes.append(by)
         matches += nm
@@ -312,7 +315,9 @@ def timed_steps(eng, step, warmup, steps, world, dist):
         free, total = torch.cuda.mem_get_info()
         lb, rb, db = eng.state_bytes()
         mem = f", HBM used {(total - free) / 1e9:.1f} GB" + (f" (slab live {lb / 1e9:.1f} GB, reserved {rb / 1e9:.1f} GB)" if rb else "")
-    log(f"{steps} timed steps: {elapsed * 1e3 / steps:.2f} ms/step{mem}")
+    sw = sorted(step_wall)
+    log(f"{steps} timed steps: {elapsed * 1e3 / steps:.2f} ms/step{mem}; per step: median "
+        f"{sw[len(sw) // 2]:.1f} ms, max {sw[-1]:.1f} ms")
     # (event, pattern) evaluations the engine performed: B x patterns for pattern-set shards, each
     # rank's own keys' events x patterns for key shards (sdh_stats.pattern_events)
     pe = float(eng.stats().pattern_events - pe0)
@@ -515,16 +520,21 @@ def main():
         result["roofline"]["frac_design"] = design / (avg_ms * 1e-3) / 1e9 / peak
     if prof:
         result["roofline"]["counters"] = {k: v for k, v in prof.items() if k != "traffic_bytes"}
-        # issue roofline: the profile's wave-instructions per pattern-event at this run's kernel rate,
-        # against the issue capacity at the profile's clock (a wave64 VALU op holds a SIMD32 for 2
-        # cycles, 1024 SIMDs; one scalar issue per CU and cycle, 256 CUs; profiles/summarize.py)
+        # issue roofline: the profile's wave-instructions per step of this run's pattern-events, at
+        # this run's kernel rate, against the issue capacity at the profile's clock (a wave64 VALU op
+        # holds a SIMD32 for 2 cycles, 1024 SIMDs; one scalar issue per CU and cycle, 256 CUs;
+        # profiles/summarize.py). The profile normalises one launch's instructions by patterns x batch;
+        # a step runs `launches` of them and evaluates pe / steps pattern-events (routed events only
+        # for key shards)
+        pe_step = pe / max(1, args.steps) / max(1, world)
+        to_run = float(sh.n) * float(B) * launches / max(1.0, pe_step)
         pe_kernel = pe / max(1e-12, sum(kern_ms) * 1e-3) / max(1, world)  # per GPU, per kernel-second
         clk = prof["clock_ghz"] * 1e9
+        vpe, spe = prof["valu_insts_per_pe"] * to_run, prof["salu_insts_per_pe"] * to_run
         result["roofline"]["issue"] = {
-            "valu_frac": prof["valu_insts_per_pe"] * pe_kernel * 2.0 / (1024.0 * clk),
-            "salu_frac": prof["salu_insts_per_pe"] * pe_kernel / (256.0 * clk),
-            "valu_insts_per_pe": prof["valu_insts_per_pe"], "salu_insts_per_pe": prof["salu_insts_per_pe"],
-            "clock_ghz": prof["clock_ghz"]}
+            "valu_frac": vpe * pe_kernel * 2.0 / (1024.0 * clk), "salu_frac": spe * pe_kernel / (256.0 * clk),
+            "valu_insts_per_pe": vpe, "salu_insts_per_pe": spe, "clock_ghz": prof["clock_ghz"],
+            "profile_valu_frac": prof["valu_issue_frac"], "profile_salu_frac": prof["salu_issue_frac"]}
     if rank == 0 and not args.no_calibrate:
         from siddhi_amd.engine import calibrate_hbm
         copy_gbps, read_gbps = calibrate_hbm(local)

@@ -16,8 +16,17 @@
  *                          completed StateEvent to QuerySelector.process)
  *   sdh_engine_poll_device  the same matches left in HBM (device consumers of the matches)
  *   sdh_engine_poll_compact the same matches as 16-B compact rows (host or HBM)
+ *   sdh_engine_poll_compact_ex  every match as compact rows + key ids, timer tiebreaks and count
+ *                          chains (the StateEvent contents of StateEvent.java:138-182)
  *   sdh_engine_set_strings  <- partition/PartitionStreamReceiver.java:277-281 (String.valueOf of a
  *                          string key: its hashCode / length, for the fan-out order)
+ *   sdh_engine_reserve / sdh_engine_reserve_keys
+ *                       <- partition/PartitionRuntime.java:257-306 (per-key clones created lazily):
+ *                          state sized up front, so no push stalls on growth
+ *   sdh_comm_* / sdh_engine_set_comm / sdh_engine_push_bcast / sdh_engine_gather
+ *                       <- stream/StreamJunction.java:179-181 (every subscriber of a junction) when the
+ *                          subscribers are sharded over the GPUs of a node: RCCL broadcast of each
+ *                          batch, gather + device k-way merge of the matches in R18 order
  *   sdh_engine_flush    <- (no reference equivalent: the reference is synchronous)
  *   sdh_engine_snapshot / sdh_engine_restore
  *                       <- state/StreamPreStateProcessor.java:352-367 (currentState/restoreState)
