@@ -124,7 +124,8 @@ struct LaneOut {
 template <int CAPW_, bool SWZ = false>
 struct WaveOutT {
   static constexpr int CAPW = CAPW_;
-  static constexpr int CAPR = CAPW / 4 + 1;    // records (>= 4 words each: K_part's narrow ones)
+  static constexpr int CAPR = CAPW / NREC_MIN_WORDS + 1;  // records (>= 3 words each: the narrow ones)
+  static constexpr int RBITS = CAPR < 1024 ? 10 : 11;       // bits of a record count <= CAPR
   // SWZ: LDS word x of the buffer lives at x ^ ((x >> 4) & 15) (an XOR swizzle inside each 16-word
   // block). The lanes of one collective emit write records of `words` words at lane-strided offsets,
   // and a ds_write_b64 serves 16 contiguous lanes per cycle on 16 qword banks, so K_part's 4- and
@@ -234,7 +235,7 @@ struct WaveOutT {
   // uw: every lane's records have the same, wave-uniform, word count (the word prefixes are then the
   // record prefixes times it: rbits ballots -- nl < 2^rbits -- instead of 23)
   template <class F>
-  __device__ void emit_n(int nl, int words, F&& fill, bool uw = false, int rbits = 10) {
+  __device__ void emit_n(int nl, int words, F&& fill, bool uw = false, int rbits = RBITS) {
     const unsigned long long lt = below();
     const bool big = nl * words > CAPW || nl > CAPR;
     const int mtw = big ? 0 : nl * words, mnl = big ? 0 : nl;
@@ -242,7 +243,7 @@ struct WaveOutT {
     if (uw) {
       int rtot = 0;
 #pragma unroll
-      for (int b = 0; b < 10; ++b) {  // mnl <= CAPR
+      for (int b = 0; b < RBITS; ++b) {  // mnl <= CAPR
         if (b >= rbits) break;
         const unsigned long long mb = __ballot((mnl >> b) & 1);
         rpre += __popcll(mb & lt) << b;
@@ -258,7 +259,7 @@ struct WaveOutT {
         wtot += __popcll(mb) << b;
       }
 #pragma unroll
-      for (int b = 0; b < 10; ++b) {  // mnl <= CAPR
+      for (int b = 0; b < RBITS; ++b) {  // mnl <= CAPR
         const unsigned long long mb = __ballot((mnl >> b) & 1);
         rpre += __popcll(mb & lt) << b;
       }

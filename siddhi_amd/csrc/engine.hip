@@ -2642,7 +2642,7 @@ sdh::GenLaunch gen_launch_base(sdh_engine* e, const sdh_engine::GenSet& gs, cons
   L.err = e->d_err.p;
   L.rec_count = e->g_nrec.p;
   L.rec_off = e->g_rec_off.p;
-  L.rec_cap = e->g_out_cap / 4 + 1;
+  L.rec_cap = e->g_out_cap / NREC_MIN_WORDS + 1;
   L.rec_next = e->g_rec_next.p;
   L.write_records = write ? 1 : 2;
   L.start_ts = e->start_ts;
@@ -2760,7 +2760,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
         Q.out_next = e->g_out_next.p;
         Q.rec_count = e->g_nrec.p;
         Q.rec_off = e->g_rec_off.p;
-        Q.rec_cap = e->g_out_cap / 4 + 1;
+        Q.rec_cap = e->g_out_cap / NREC_MIN_WORDS + 1;
         Q.rec_next = e->g_rec_next.p;
         Q.err = e->d_err.p;
         const int64_t starts = n + Q.tail_len;
@@ -3018,7 +3018,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       P.out_next = e->g_out_next.p;
       P.rec_count = e->g_nrec.p;
       P.rec_off = e->g_rec_off.p;
-      P.rec_cap = e->g_out_cap / 4 + 1;
+      P.rec_cap = e->g_out_cap / NREC_MIN_WORDS + 1;
       P.rec_next = e->g_rec_next.p;
       P.write_records = write ? 1 : 2;
       if (!write && getenv("SDH_DEBUG_COUNT_ONLY")) P.write_records = 0;  // (measurement experiments)
@@ -3117,7 +3117,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       S.out_next = e->g_out_next.p;
       S.rec_count = e->g_nrec.p;
       S.rec_off = e->g_rec_off.p;
-      S.rec_cap = e->g_out_cap / 4 + 1;
+      S.rec_cap = e->g_out_cap / NREC_MIN_WORDS + 1;
       S.rec_next = e->g_rec_next.p;
       S.write_records = write ? 1 : 2;
       S.err = e->d_serr.p + 4 * si;
@@ -3191,7 +3191,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   std::vector<int32_t> perr(4 * std::max<size_t>(1, nps), 0);
   for (int attempt = 0;; ++attempt) {
     e->g_out.ensure((size_t)e->g_out_cap);
-    e->g_rec_off.ensure((size_t)(e->g_out_cap / 4 + 1));  // a record has at least 4 words (narrow K_part records)
+    e->g_rec_off.ensure((size_t)(e->g_out_cap / NREC_MIN_WORDS + 1));  // a record has at least NREC_MIN_WORDS words (the narrow ones)
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
     HIPCHK(hipMemsetAsync(e->d_perr.p, 0, perr.size() * 4, e->stream));
     HIPCHK(hipMemsetAsync(e->d_serr.p, 0, serr.size() * 4, e->stream));

@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256) void append_chain_kernel(
 
 // The table words each record of a push takes (tw[n_rec] = 0, for the exclusive scan): a K_gen / K_seq
 // record [len, qid, key, ts, seq, idx, S | stream << 16, (count, seqs...) x S] its slot words, a
-// narrow K_part record (nfa_types.h) its slots expanded to that form
+// narrow K_part or K_seq record (nfa_types.h) its slots expanded to that form
 __device__ __forceinline__ int32_t lo32(int64_t w) { return (int32_t)(uint32_t)(uint64_t)w; }
 __device__ __forceinline__ int32_t hi32(int64_t w) { return (int32_t)(uint32_t)((uint64_t)w >> 32); }
 
@@ -252,9 +252,11 @@ __global__ __launch_bounds__(256) void gen_rec_words_kernel(const int64_t* __res
   if (l0 >= 0) {
     tw[i] = r[0] - 7;
     atomicAdd(n_wide, 1ull);
-  } else if ((-l0) >> 16) {  // count: (1, e1), (c, chain), (1, trigger)
+  } else if (((-l0) >> 16) == NREC_KIND_COUNT) {  // count: (1, e1), (c, chain), (1, trigger)
     tw[i] = 5 + hi32(r[2]);
-  } else {                   // or / and: (1, e1), then per side (1, seq) or (0)
+  } else if (((-l0) >> 16) == NREC_KIND_SEQ) {    // K_seq window: (1, seq) x S
+    tw[i] = 2 * hi32(r[1]);
+  } else {  // or / and: (1, e1), then per side (1, seq) or (0)
     tw[i] = 2 + (hi32(r[2]) == INT32_MIN ? 1 : 2) + (lo32(r[3]) == INT32_MIN ? 1 : 2);
   }
 }
@@ -279,8 +281,29 @@ __global__ __launch_bounds__(256) void append_gen_kernel(const int64_t* __restri
   T.woff[row] = wo;
   static_assert(MAXLO >= 3, "timer tiebreaks");
   const int32_t l0 = lo32(r[0]);
+  if (l0 < 0 && ((-l0) >> 16) == NREC_KIND_SEQ) {  // narrow K_seq record
+    const int q = hi32(r[0]), S = hi32(r[1]);
+    const int64_t off = (int64_t)(uint32_t)lo32(r[1]);
+    const int64_t sq = seq_base + off;
+    T.seq[row] = sq;
+    T.hi[row] = hi_key(sq, seq_ref, out_rank[(int64_t)q * n_streams + bstream]);
+    T.lo[0][row] = 0ull;  // (one match per event and query)
+    T.lo[1][row] = 0ull;
+    T.lo[2][row] = 0ull;
+    T.q[row] = q;
+    T.key[row] = -1;
+    T.ts[row] = bts[off];
+    for (int j = 0; j < S - 1; ++j) {
+      w[2 * j] = 1;
+      w[2 * j + 1] = sq - (j & 1 ? hi32(r[2 + j / 2]) : lo32(r[2 + j / 2]));
+    }
+    w[2 * S - 2] = 1;
+    w[2 * S - 1] = sq;
+    T.wlen[row] = 2 * S;
+    return;
+  }
   if (l0 < 0) {  // narrow K_part record
-    const bool count = ((-l0) >> 16) != 0;
+    const bool count = ((-l0) >> 16) == NREC_KIND_COUNT;
     const int q = hi32(r[0]);
     const int64_t off = (int64_t)(uint32_t)lo32(r[1]);
     const uint32_t kid = (uint32_t)hi32(r[1]);

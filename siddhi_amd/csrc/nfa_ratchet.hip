@@ -461,10 +461,14 @@ __device__ __forceinline__ int32_t rel_deadline(int64_t d, int64_t T0) {  // |T0
 // unless a lane popped all four or ran through its LDS entries, and then a walk down the deque
 // counts the rest (keys are monotone along it). The lower lanes' matches are mbcnt over the first
 // round's ballots, a wave scan in the rare walk case.
-template <int KK, int XM, bool FULL, int NF, bool SIM = false, int PM = 0>
+template <int KK, int XM, bool FULL, int NF, bool SIM = false, int PM = 0, int MLC = 0>
 // occupancy: the general forms at 7 waves per SIMD (72 VGPRs), the SIM form at 8 (64 VGPRs, a few
 // spills; the LDS rings allow 8 at ML = 8). SIM at 10K C2 patterns: 7 waves 167.9 ms, 8 waves 156.1
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7))) void nfa_ratchet_kernel(RatchetLaunch L, int ML, int SC) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7))) void nfa_ratchet_kernel(RatchetLaunch L, int ML_, int SC) {
+  // MLC > 0: the LDS ring depth as a compile-time constant (the SIM launches at the default 8): the
+  // ring masks and the full-ring test then take no scalar registers, whose spills were reloaded at
+  // every event
+  const int ML = MLC > 0 ? MLC : ML_;
   using U = typename KT<KK>::U;
   constexpr bool W64 = KT<KK>::W64;
   const int lane = threadIdx.x;
@@ -1176,24 +1180,27 @@ template <int KK, int XM, bool FULL, int NF, bool SIM = false>
 static void launch_one(const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t s) {
   const bool w64 = (KK == sdh::KK_F64 || KK == sdh::KK_I64);
   const size_t lds = (size_t)(ML + (SIM ? 1 : 0)) * 64 * (w64 ? 16 : 8);  // (SIM: + the dummy row)
-  if constexpr (!FULL) {
-    if (L->pcnt) {
-      hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM, 1>), dim3(L->n_items), dim3(64), lds, s, *L,
-                         ML, SC);
-      return;
+  auto go = [&](auto pm, auto mlc) {
+    hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM, decltype(pm)::value, decltype(mlc)::value>),
+                       dim3(L->n_items), dim3(64), lds, s, *L, ML, SC);
+  };
+  auto pick_pm = [&](auto mlc) {
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I0 = std::integral_constant<int, 0>;
+    if constexpr (!FULL) {
+      if (L->pcnt) return go(I1{}, mlc);
+      if (L->crow) return go(I2{}, mlc);
+      if (L->wide) return go(I3{}, mlc);
     }
-    if (L->crow) {
-      hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM, 2>), dim3(L->n_items), dim3(64), lds, s, *L,
-                         ML, SC);
-      return;
-    }
-    if (L->wide) {
-      hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM, 3>), dim3(L->n_items), dim3(64), lds, s, *L,
-                         ML, SC);
-      return;
-    }
+    go(I0{}, mlc);
+  };
+  // the SIM form at the default ring depth takes it as a compile-time constant (MLC)
+  if constexpr (SIM) {
+    if (ML == 8) return pick_pm(std::integral_constant<int, 8>{});
   }
-  hipLaunchKernelGGL((sdh::nfa_ratchet_kernel<KK, XM, FULL, NF, SIM>), dim3(L->n_items), dim3(64), lds, s, *L, ML, SC);
+  pick_pm(std::integral_constant<int, 0>{});
 }
 
 template <int KK, int XM, bool FULL, int NF, bool SIM = false>

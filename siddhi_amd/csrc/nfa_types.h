@@ -323,8 +323,18 @@ constexpr int PK_CMAX = 8;     // count <min:max> with max <= PK_CMAX on K_part
 // The table append (matches.hip) restores the K_gen row: ts from the batch, the key from the
 // partition's key table, emission index = e1's seq (the pending-list order is the creation order).
 // A match whose distances do not fit int32 goes out as a K_gen record instead.
+// K_seq's narrow record (kind 2 in w0's low half: -(words + 0x20000)), an unpartitioned window match:
+//   w0 = (uint32)(-(words + 0x20000)) | qid << 32
+//   w1 = (uint32)(trigger seq - the batch's seq_base) | S << 32
+//   then the S - 1 earlier slots' int32 seq distances back from the trigger, two per word
+//                                                                        -> 2 + S / 2 words (24 B at S = 3)
+// restored as [(1, seq) x S] with key -1, ts from the batch, emission index 0 (one match per event
+// and query).
 constexpr int NREC_ORAND_WORDS = 4;
+constexpr int NREC_KIND_COUNT = 1, NREC_KIND_SEQ = 2;
 __host__ __device__ inline int nrec_count_words(int c) { return 3 + (c + 1) / 2; }
+__host__ __device__ inline int nrec_seq_words(int S) { return 2 + S / 2; }
+constexpr int NREC_MIN_WORDS = 3;  // (K_seq's at S <= 3; record-offset capacities are words / 3)
 __host__ __device__ inline int64_t nrec_pack(int64_t lo, int64_t hi) {
   return (int64_t)(((uint64_t)(uint32_t)(int32_t)lo) | ((uint64_t)(uint32_t)(int32_t)hi << 32));
 }

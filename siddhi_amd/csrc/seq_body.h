@@ -123,10 +123,27 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
       r[8 + 2 * i] = wv.base[i * ROW + 1];
     }
   };
+  // the narrow record (nfa_types.h, 24 B at S = 3 instead of 104) unless an offset or a distance
+  // does not fit int32 (one record width per collective call: the emit is uniform)
+  const bool nb_ok = L.b.n < (int64_t)INT32_MAX;
+  const int nwords = nrec_seq_words(S);
+  auto nar_ok = [&](int s) {
+    const Win wv{win + s * ROW};
+    return nb_ok && wv.base[(S - 1) * ROW + 1] - wv.base[1] <= (int64_t)INT32_MAX;
+  };
+  auto put_nrec = [&](auto r, int s) {
+    const Win wv{win + s * ROW};
+    const int64_t sq = wv.base[(S - 1) * ROW + 1];
+    r[0] = nrec_pack(-(nwords + (NREC_KIND_SEQ << 16)), qid);
+    r[1] = nrec_pack(sq - L.b.seq_base, S);
+    for (int i = 0; i < S - 1; i += 2)
+      r[2 + i / 2] = nrec_pack(sq - wv.base[i * ROW + 1], i + 1 < S - 1 ? sq - wv.base[(i + 1) * ROW + 1] : 0);
+  };
   auto emit = [&](int s) {
     ++nrec;
     if (!L.write_records) return;
-    o.emit_u(words, [&](auto r) { put_rec(r, s); });
+    if (!__ballot(!nar_ok(s))) o.emit_u(nwords, [&](auto r) { put_nrec(r, s); });
+    else o.emit_u(words, [&](auto r) { put_rec(r, s); });
   };
   // a lane's matches among 8 starts (mask m over s0 ..) in one collective call: its records are
   // contiguous, start order; the record counts take 4 ballots
@@ -134,10 +151,18 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
     const int nl = __popc(m);
     nrec += nl;
     if (!L.write_records || __ballot(nl > 0) == 0) return;
-    o.emit_n(nl, words, [&](auto r0) {
-      int kk = 0;
-      for (uint32_t mm = m; mm; mm &= mm - 1, ++kk) put_rec(r0 + kk * words, s0 + __builtin_ctz(mm));
-    }, true, 4);
+    bool ok = true;
+    for (uint32_t mm = m; mm; mm &= mm - 1) ok = ok && nar_ok(s0 + __builtin_ctz(mm));
+    if (!__ballot(!ok))
+      o.emit_n(nl, nwords, [&](auto r0) {
+        int kk = 0;
+        for (uint32_t mm = m; mm; mm &= mm - 1, ++kk) put_nrec(r0 + kk * nwords, s0 + __builtin_ctz(mm));
+      }, true, 4);
+    else
+      o.emit_n(nl, words, [&](auto r0) {
+        int kk = 0;
+        for (uint32_t mm = m; mm; mm &= mm - 1, ++kk) put_rec(r0 + kk * words, s0 + __builtin_ctz(mm));
+      }, true, 4);
   };
   for (int64_t t0 = lo; t0 < hi; t0 += SEQ_TILE) {
     const int cnt = hi - t0 < SEQ_TILE ? (int)(hi - t0) : SEQ_TILE;
