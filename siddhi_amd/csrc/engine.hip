@@ -1611,12 +1611,21 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
         const int occ = sdh_ratchet_occupancy(e->rg[order[i0]].key_kind, full, nf, e->rML, lsim(order[i0]));
         slots = (double)e->n_cu * std::max(1, occ);
       }
-      const double len = std::max((double)min_chunk, (double)n * (double)(i1 - i0) / slots);
+      // chunks per chunkable group: as many as keep the launch's items within one resident round
+      // (floor, not ceil: items past the last slot start only when the first round ends, and that
+      // tail then runs nearly alone -- C2 at 10K had 8,321 items for 8,192 slots), at least
+      // min_chunk events each. Groups without `within` cannot chunk (no reverse-scan window) and
+      // hold one slot each for the whole launch.
+      int64_t n_chunkable = 0;
+      for (size_t i = i0; i < i1; ++i) n_chunkable += (!full && e->rg[order[i]].wmax >= 0) ? 1 : 0;
+      const int64_t free_slots = std::max<int64_t>(1, (int64_t)slots - ((int64_t)(i1 - i0) - n_chunkable));
+      const int64_t c_fit = n_chunkable > 0 ? std::max<int64_t>(1, free_slots / n_chunkable) : 1;
+      const int64_t c_min = std::max<int64_t>(1, n / std::max<int64_t>(1, min_chunk));
       for (size_t i = i0; i < i1; ++i) {
         const int g = order[i];
         const RatchetGroup& G = e->rg[g];
         int64_t C = 1;
-        if (!full && G.wmax >= 0) C = std::max<int64_t>(1, (int64_t)std::ceil((double)n / len));
+        if (!full && G.wmax >= 0) C = std::min(c_fit, c_min);
         for (int64_t ch = 0; ch < C; ++ch) {
           RatchetItem it{};
           it.g = g;
