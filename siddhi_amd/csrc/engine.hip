@@ -1606,16 +1606,19 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       size_t i1 = i0;
       int nf = 0;
       while (i1 < order.size() && lkey(order[i1]) == lkey(order[i0])) nf = std::max(nf, ratchet_nf(e->rg[order[i1++]]));
+      // items per launch: 8 rounds of the chip's resident slots (CUs x occupancy). Short chunks
+      // balance the groups' uneven match density, and a chunk's reverse-scan warm-up is cheap (tile
+      // summaries). C2 at 10K patterns, tools/sweep_ratchet.sh (SDH_RATCHET_WAVES): 8,192 items
+      // 117.8 ms/step, 16,384 110.9, 32,768 103.3, 65,536 100.2, 131,072 100.8, 524,288 104.4
       double slots = e->r_waves;
       if (slots <= 0) {
         const int occ = sdh_ratchet_occupancy(e->rg[order[i0]].key_kind, full, nf, e->rML, lsim(order[i0]));
-        slots = (double)e->n_cu * std::max(1, occ);
+        slots = 8.0 * (double)e->n_cu * std::max(1, occ);
       }
-      // chunks per chunkable group: as many as keep the launch's items within one resident round
-      // (floor, not ceil: items past the last slot start only when the first round ends, and that
-      // tail then runs nearly alone -- C2 at 10K had 8,321 items for 8,192 slots), at least
-      // min_chunk events each. Groups without `within` cannot chunk (no reverse-scan window) and
-      // hold one slot each for the whole launch.
+      // chunks per chunkable group: as many as fit the item target (floor, not ceil: a partial
+      // extra round of items runs as a nearly idle tail -- C2 at 10K once had 8,321 items for 8,192
+      // slots, 128.7 ms/step, against 117.7 at 8,164), at least min_chunk events each. Groups
+      // without `within` cannot chunk (no reverse-scan window) and hold one item each.
       int64_t n_chunkable = 0;
       for (size_t i = i0; i < i1; ++i) n_chunkable += (!full && e->rg[order[i]].wmax >= 0) ? 1 : 0;
       const int64_t free_slots = std::max<int64_t>(1, (int64_t)slots - ((int64_t)(i1 - i0) - n_chunkable));
@@ -2773,7 +2776,11 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
         Q.rec_next = e->g_rec_next.p;
         Q.err = e->d_err.p;
         const int64_t starts = n + Q.tail_len;
-        const int64_t target = std::max<int64_t>(1, 8192 / (int64_t)nrows);
+        // items per launch: many short chunks balance the chunks' uneven match density (C4 sweep,
+        // tools/sweep_seq.sh: 4,096 items 25.2 ms/step, 8,192 19.8, 16,384 17.2, 32,768 16.2, 65,536
+        // 15.8, 131,072 15.5)
+        static const int64_t seq_waves = getenv("SDH_SEQ_WAVES") ? atoll(getenv("SDH_SEQ_WAVES")) : 131072;
+        const int64_t target = std::max<int64_t>(1, seq_waves / (int64_t)nrows);
         int64_t clen = std::max<int64_t>(256, (starts + target - 1) / target);
         clen = (clen + 63) / 64 * 64;  // whole LDS tiles
         Q.chunk_len = clen;
