@@ -1594,7 +1594,10 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     // `within` window (a few instructions per 64 events), so chunks can be short. Each launch
     // (one key kind x orientation) gets one resident wave per slot of the chip -- CUs x the
     // kernel's occupancy -- of at least min_chunk emitted events each ----
-    const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : 2048;
+    // (C2 expansion, 64K-event pushes, tools/sweep_minchunk.sh: 2,048 events per chunk at least
+    // 3.66 ms per push / 3.56 compact, 1,024 3.42 / 3.43, 512 3.43 / 3.48, 256 3.68 / 3.68)
+    static const int64_t def_chunk = getenv("SDH_RATCHET_MIN_CHUNK") ? atoll(getenv("SDH_RATCHET_MIN_CHUNK")) : 1024;
+    const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : def_chunk;
     e->ritems.clear();
     std::vector<int> order(gs);
     // launches: one per (key kind, orientation, SIM form); SIM also needs the key column null-free
