@@ -134,7 +134,8 @@ extern "C" hipError_t sdh_live_seq(const int64_t* tail, int tail_len, int stream
 extern "C" hipError_t sdh_live_part(const int64_t* st, const int32_t* cur, int64_t n_keys, int groups, int64_t blocks,
                                     int64_t bw, unsigned long long* acc, hipStream_t s);
 extern "C" hipError_t sdh_digest_ratchet(const int64_t* match, int blk_recs, int wide, const int32_t* blk_count,
-                                         const int32_t* blk_group, const sdh::RatchetGroup* groups, int64_t seq_base,
+                                         const int32_t* blk_group, const int32_t* blk_side,
+                                         const sdh::RatchetGroup* groups, int64_t seq_base,
                                          int n_blocks, unsigned long long* acc, hipStream_t s);
 extern "C" hipError_t sdh_poll_sort(sdh::MatchTable T, int64_t n, int n_lo, int lo_bits, int hi_bits, int clo_bits,
                                     uint64_t* kbuf, int32_t* pbuf, void* temp, size_t temp_bytes, int64_t* oq,
@@ -941,6 +942,8 @@ struct sdh_engine {
   std::vector<RatchetItem> ritems;
   DevBuf<int64_t> d_rmatch;
   DevBuf<int32_t> d_blk_count, d_blk_next, d_blk_group;
+  DevBuf<int32_t> d_blk_side;            // K_ratchet rec4 blocks: side entries (-1: an 8- / 16-B block)
+  bool r_no_rec4 = false;                // a rec4 distance reached 2^26: 8-B records from then on
   DevBuf<unsigned long long> d_rtotal;  // records written in ring mode (SDH_FLAG_DEVICE_MATCHES)
   int r_wide = 0;
   int64_t r_blocks = 0;              // capacity in blocks
@@ -1580,7 +1583,6 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     e->r_blocks = (want + e->r_blk_recs - 1) / e->r_blk_recs;
   }
   e->d_rtotal.ensure(2);  // [0] ring-mode records, [1] the placement total
-  (void)t01;
   bool no_place = false;
   for (int attempt = 0; attempt < 40; ++attempt) {
     // out-of-order timestamps seen on this stream, timestamps so extreme that `ts0 + within`
@@ -1631,7 +1633,18 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
         const int g = order[i];
         const RatchetGroup& G = e->rg[g];
         int64_t C = 1;
-        if (!full && G.wmax >= 0) C = std::min(c_fit, c_min);
+        if (!full && G.wmax >= 0) {
+          C = std::min(c_fit, c_min);
+          // a chunk's warm-up walks its `within` window back from its first event: tiles whose best
+          // key is dominated by the later ones are skipped on their summary, but flat or rising key
+          // runs are walked event by event. Chunks x window events <= max(16 x the batch, 2^24)
+          // bounds that worst case (a 67M-event window spanning the batch: 16 chunks) and binds
+          // nowhere near C2's windows (1-60 s, up to 60K events, in 8M- or 64K-event pushes)
+          const double span = (double)std::max<int64_t>(1, t01[1] - t01[0]);
+          const double win_ev = std::min((double)n, (double)G.wmax * (double)n / span);
+          const double budget = std::max(16.0 * (double)n, 16777216.0);
+          C = std::min<int64_t>(C, std::max<int64_t>(1, (int64_t)(budget / std::max(1.0, win_ev))));
+        }
         for (int64_t ch = 0; ch < C; ++ch) {
           RatchetItem it{};
           it.g = g;
@@ -1662,8 +1675,9 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     if (any64) e->d_rspillB.ensure((size_t)n_items * e->rSC * WAVE);
     e->d_blk_count.ensure((size_t)e->r_blocks);
     e->d_blk_group.ensure((size_t)e->r_blocks);
-    e->d_err.ensure(4);
-    HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
+    e->d_blk_side.ensure((size_t)e->r_blocks);
+    e->d_err.ensure(5);
+    HIPCHK(hipMemsetAsync(e->d_err.p, 0, 20, e->stream));
     HIPCHK(hipMemsetAsync(e->d_blk_next.p, 0, 4, e->stream));
     HIPCHK(hipMemsetAsync(e->d_rtotal.p, 0, 8, e->stream));
     // per-tile x summaries for the warm-up scans (rows of this stream's key specs)
@@ -1698,6 +1712,9 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.spillB = e->d_rspillB.p;
     L.match = e->d_rmatch.p;
     L.blk_count = e->d_blk_count.p;
+    L.blk_side = e->d_blk_side.p;
+    // ring mode (records written, never read back) takes the 4-B rec4 entries where it can
+    L.rec4 = (ring && !wide && !full && !e->r_no_rec4) ? 1 : 0;
     L.blk_group = e->d_blk_group.p;
     L.wide = wide;
     L.blk_next = e->d_blk_next.p;
@@ -1738,16 +1755,16 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     HIPCHK(hipEventRecord(e->ev0, e->stream));
     run(L);
     HIPCHK(hipEventRecord(e->ev1, e->stream));
-    int32_t errs[4], used = 0;
-    HIPCHK(hipMemcpyAsync(errs, e->d_err.p, 16, hipMemcpyDeviceToHost, e->stream));
+    int32_t errs[5], used = 0;
+    HIPCHK(hipMemcpyAsync(errs, e->d_err.p, 20, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&used, e->d_blk_next.p, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
     if (getenv("SDH_TRACE"))
-      fprintf(stderr, "[sdh] ratchet stream %d n %lld attempt %d full %d items %d blocks %d/%lld errs %d %d %d %d: %.2f ms\n",
-              stream, (long long)n, attempt, (int)full, n_items, used, (long long)e->r_blocks, errs[0], errs[1], errs[2],
-              errs[3], ms);
+      fprintf(stderr, "[sdh] ratchet stream %d n %lld attempt %d full %d rec4 %d items %d blocks %d/%lld errs %d %d %d %d %d: %.2f ms\n",
+              stream, (long long)n, attempt, (int)full, L.rec4, n_items, used, (long long)e->r_blocks, errs[0], errs[1],
+              errs[2], errs[3], errs[4], ms);
     if (errs[3]) throw Error(SDH_E_CAPACITY, "a pending partial is more than 2^31 events old");
     if (errs[1] && !full) {  // timestamps out of order: exact re-run with the full expiry scan
       e->r_full_expiry[stream] = 1;
@@ -1764,6 +1781,10 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     }
     if (errs[2]) {
       e->r_blocks *= 2;
+      continue;
+    }
+    if (errs[4] && L.rec4) {  // a rec4 entry's e1 distance reached 2^26: exact re-run with 8-B records
+      e->r_no_rec4 = true;
       continue;
     }
     int64_t placed_rows = 0;
@@ -4442,8 +4463,8 @@ int sdh_engine_debug_digest(sdh_engine* e, uint64_t* out) {
     if (e->r_placing)  // the last push placed its matches: its compact rows
       HIPCHK(sdh_digest_compact(e->pc_rows.p, e->cw, e->r_place_row0, e->r_matches, e->seq_ref, acc.p, e->stream));
     else
-      HIPCHK(sdh_digest_ratchet(e->d_rmatch.p, e->r_blk_recs, e->r_wide, e->d_blk_count.p, e->d_blk_group.p, e->d_rg.p,
-                                e->r_seq_base, (int)e->r_blk_taken, acc.p, e->stream));
+      HIPCHK(sdh_digest_ratchet(e->d_rmatch.p, e->r_blk_recs, e->r_wide, e->d_blk_count.p, e->d_blk_group.p,
+                                e->d_blk_side.p, e->d_rg.p, e->r_seq_base, (int)e->r_blk_taken, acc.p, e->stream));
     d2h_sync(e, out, acc.p, 16);
     return SDH_OK;
   });

@@ -77,16 +77,31 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 __global__ __launch_bounds__(256) void digest_ratchet_kernel(const int64_t* __restrict__ match, int blk_recs, int wide,
                                                              const int32_t* __restrict__ blk_count,
                                                              const int32_t* __restrict__ blk_group,
+                                                             const int32_t* __restrict__ blk_side,
                                                              const RatchetGroup* __restrict__ groups, int64_t seq_base,
                                                              unsigned long long* acc) {
   const int b = blockIdx.x;
   const int n = blk_count[b];
+  const int ns = blk_side[b];  // >= 0: a rec4 block (nfa_types.h RatchetLaunch::rec4)
   const RatchetGroup* G = groups + blk_group[b];
   const uint2* R = reinterpret_cast<const uint2*>(match) + ((size_t)b * blk_recs << (wide ? 1 : 0));
   unsigned long long h = 0, c = 0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     uint32_t off, ln, q1;
-    if (!wide) {
+    if (ns >= 0) {
+      // entry i: {distance | lane << 26}; its event: the last side entry whose first index is <= i
+      const uint32_t* E = reinterpret_cast<const uint32_t*>(R);
+      const uint2* S = reinterpret_cast<const uint2*>(E + blk_recs);
+      int lo = 0, hi = ns - 1;  // S[0].x == 0 <= i
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)S[mid].x <= i) lo = mid;
+        else hi = mid - 1;
+      }
+      off = S[lo].y;
+      ln = E[i] >> 26;
+      q1 = ((uint32_t)seq_base + off) - (E[i] & ((1u << 26) - 1));
+    } else if (!wide) {
       const uint2 r = R[i];
       off = r.x & ((1u << 26) - 1);
       ln = r.x >> 26;
@@ -504,11 +519,12 @@ extern "C" hipError_t sdh_append_gen(const int64_t* out, const int64_t* rec_off,
 }
 
 extern "C" hipError_t sdh_digest_ratchet(const int64_t* match, int blk_recs, int wide, const int32_t* blk_count,
-                                         const int32_t* blk_group, const sdh::RatchetGroup* groups, int64_t seq_base,
+                                         const int32_t* blk_group, const int32_t* blk_side,
+                                         const sdh::RatchetGroup* groups, int64_t seq_base,
                                          int n_blocks, unsigned long long* acc, hipStream_t s) {
   if (n_blocks <= 0) return hipSuccess;
   hipLaunchKernelGGL(sdh::digest_ratchet_kernel, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, wide, blk_count,
-                     blk_group, groups, seq_base, acc);
+                     blk_group, blk_side, groups, seq_base, acc);
   return hipGetLastError();
 }
 

@@ -38,6 +38,9 @@
 #ifndef SDH_RATCHET_UNROLL
 #define SDH_RATCHET_UNROLL 1
 #endif
+#ifndef SDH_RATCHET_NOSTORE
+#define SDH_RATCHET_NOSTORE 0
+#endif
 #define SDH_PRAGMA(x) _Pragma(#x)
 #define SDH_UNROLL(n) SDH_PRAGMA(unroll n)
 
@@ -830,16 +833,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       for (int j = 4; j < L.cw; ++j) o[j] = INT32_MIN;
     }
   };
-  // record width: compile-time in the chunked forms (PM 3 = 16-B records), read at run time in FULL
+  // record width: compile-time in the chunked forms (PM 3 = 16-B records), read at run time in FULL.
+  // PM 4 (ring mode, nfa_types.h rec4): 4-B entries {e1 distance | lane << 26} and one side entry
+  // {first entry, e2 offset} per matching event in the block's upper half
   const bool wide = FULL ? L.wide != 0 : PM == 3;
+  int sfill = 0;                              // PM 4: side entries in the current block
+  bool new_blk = false;                       // PM 4: a block was taken since the last side entry
+  const uint32_t sb32 = (uint32_t)seq_base;   // PM 4: e2 seq low bits = sb32 + off
+  int d4over = 0;                             // PM 4: a distance reached 2^26 (err[4])
   // the next output block, taken when a pop round could overrun the current one (every round pops
   // at most 4 x 64 records: one check per round instead of one per ballot). Out of blocks, the wave
   // writes on into the spare block past the last (never read: the host doubles the blocks and re-runs)
   auto roll = [&]() {
     if (blk >= 0) {
-      if (lane == 0) L.blk_count[blk] = fill;
+      if (lane == 0) {
+        L.blk_count[blk] = fill;
+        L.blk_side[blk] = PM == 4 ? sfill : -1;
+      }
       n_emit += (unsigned long long)fill;
     }
+    sfill = 0;
+    new_blk = true;  // (an event whose matches continue in this block needs a side entry here too)
     int nb = 0;
     if (lane == 0) nb = atomicAdd(L.blk_next, 1);
     nb = __builtin_amdgcn_readfirstlane(nb);
@@ -862,6 +876,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
   auto emit_room = [&]() {
     if constexpr (PM == 0 || PM == 3)
       if (fill > L.blk_recs - 4 * WAVE) roll();
+    if constexpr (PM == 4)
+      if (fill > L.blk_recs - 4 * WAVE || sfill >= (L.blk_recs >> 1)) roll();
   };
   auto emit = [&](bool mt, uint64_t m, uint32_t off, uint32_t q1) {
     if constexpr (PM == 1) {
@@ -873,7 +889,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       lv += mt ? 1u : 0u;
       return;
     }
-    if (mt) {
+    if constexpr (PM == 4) {
+      if (mt && !SDH_RATCHET_NOSTORE)
+        __builtin_amdgcn_raw_buffer_store_b32(((sb32 + off) - q1) | ((uint32_t)lane << 26), wrs,
+                                              (fill + wave_mbcnt(m)) * 4, 0, 0);
+      fill += __popcll(m);
+      return;
+    }
+    if (mt && !SDH_RATCHET_NOSTORE) {  // (NOSTORE: a measurement build without the record stores)
       const int r = fill + wave_mbcnt(m);
       if (!wide) {
         const u32x2 v = {off | ((uint32_t)lane << 26), q1};
@@ -912,7 +935,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     const int cnt = (int)((W.c1 - t) < WAVE ? (W.c1 - t) : WAVE);
     // sequence numbers are kept as their low 32 bits: a live partial must stay < 2^31 events old
     // (checked once per tile against the tile's last event; the bottom only gets younger)
-    if (D.n() > 0 && (uint32_t)((uint32_t)(seq_base + t + cnt - 1) - D.bottom_seq()) >= 0x80000000u) aged = 1;
+    // (PM 4: every distance a rec4 entry holds is below the bottom's, checked likewise against 2^26)
+    if (D.n() > 0) {
+      const uint32_t dist = (uint32_t)(seq_base + t + cnt - 1) - D.bottom_seq();
+      if (dist >= 0x80000000u) aged = 1;
+      if (PM == 4 && dist >= (1u << 26)) d4over = 1;
+    }
     if constexpr (PM == 1) cntv = 0;
     if constexpr (PM == 2) basev = lane < cnt ? L.pbase[(int64_t)(t + lane) * L.n_cells + cell] : 0;
 
@@ -963,6 +991,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       bool round1 = true;
       while (m) {
         emit_room();
+        if constexpr (PM == 4) {  // the event's side entry: its first entry's index and e2 offset
+          if (round1 || new_blk) {  // (again at the head of a block the event's matches spill into)
+            round1 = false;
+            new_blk = false;
+            if (lane == 0) {
+              const u32x2 se = {(uint32_t)fill, (uint32_t)(t + k)};
+              __builtin_amdgcn_raw_buffer_store_b64(se, wrs, L.blk_recs * 4 + sfill * 8, 0, 0);
+            }
+            ++sfill;
+          }
+        }
         // the three LDS entries under the top, read unconditionally (in-bounds ring slots)
         const int topl = D.lbot + D.ln - 1;
         U k1, k2, k3;
@@ -1084,17 +1123,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
   }
 
   // ---- outputs ----
-  if (blk >= 0 && (PM == 0 || PM == 3)) {
-    if (lane == 0) L.blk_count[blk] = fill;
+  if (blk >= 0 && (PM == 0 || PM == 3 || PM == 4)) {
+    if (lane == 0) {
+      L.blk_count[blk] = fill;
+      L.blk_side[blk] = PM == 4 ? sfill : -1;
+    }
     n_emit += (unsigned long long)fill;
   }
   const uint64_t any_over = wballot(overflow != 0), any_unord = wballot(unordered != 0), any_aged = wballot(aged != 0);
+  const uint64_t d4 = wballot(d4over != 0);
   if (lane == 0) {
     if (L.ring && n_emit) atomicAdd(L.rec_total, n_emit);
     if (any_over) atomicOr(&L.err[0], 1);
     if (any_unord) atomicOr(&L.err[1], 1);
     if (mover) atomicOr(&L.err[2], 1);
     if (any_aged) atomicOr(&L.err[3], 1);
+    if (d4) atomicOr(&L.err[4], 1);
   }
   if (W.chunk == W.n_chunks - 1) {  // the last chunk owns the group's final deques
     const int ob = 1 - W.inb;
@@ -1193,6 +1237,8 @@ static void launch_one(const sdh::RatchetLaunch* L, int ML, int SC, hipStream_t 
       if (L->pcnt) return go(I1{}, mlc);
       if (L->crow) return go(I2{}, mlc);
       if (L->wide) return go(I3{}, mlc);
+      if constexpr (SIM)
+        if (L->rec4) return go(std::integral_constant<int, 4>{}, mlc);
     }
     go(I0{}, mlc);
   };

@@ -210,8 +210,16 @@ struct RatchetLaunch {
   int32_t wide;
   int32_t ring;                 // SDH_FLAG_DEVICE_MATCHES: blocks wrap modulo n_blocks (every record is
                                 //   written, none is read back); rec_total counts them
+  // rec4 (ring mode, SIM form, batches of at most 2^26 events): 4-B entries {e1 distance back from e2
+  // (< 2^26) | lane << 26} in the block's first blk_recs * 4 bytes, and per matching event one side
+  // entry {index of the event's first entry, e2 batch offset} (uint2) from byte blk_recs * 4 on, at
+  // most blk_recs / 2 of them (blk_side[block] counts them). A distance >= 2^26 sets err[4]; the
+  // host then re-runs with 8-B records
+  int32_t rec4;
+  int32_t* blk_side;
   unsigned long long* rec_total;
-  int32_t* err;                 // [0] deque overflow, [1] unordered ts, [2] match overflow
+  int32_t* err;                 // [0] deque overflow, [1] unordered ts, [2] match overflow, [3] aged,
+                                //   [4] a rec4 distance past 2^26
   // direct R18 placement, two passes over the same items (nfa_ratchet.hip PM; the stream's groups
   // hold consecutive receiver ranks in lane order, groups in `cell` order): COUNT stores each
   // (event, group) match total at pcnt[event * n_cells + cell]; WRITE reads their exclusive scan

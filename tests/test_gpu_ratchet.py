@@ -308,3 +308,32 @@ def test_wide_records_for_batches_beyond_2_26_events():
     for i in (0, 1, 2, 4):  # query, key, ts, slot words
         assert np.array_equal(x[i], np.concatenate([y0[i], y1[i]]))
     assert np.array_equal(x[3], np.concatenate([y0[3], y1[3][1:] + y0[3][-1]]))
+
+
+def test_ring_rec4_distance_overflow_reruns_with_8b_records():
+    """SDH_FLAG_DEVICE_MATCHES pushes write 4-B K_ratchet entries (an e1 distance below 2^26 and the
+    lane) with one side entry per matching event (nfa_types.h rec4). A partial matched more than 2^26
+    events after it opened sets err[4] and the push re-runs with 8-B records: the ring engine's record
+    digest still equals the normal-mode engine's, in both pushes."""
+    import torch
+    from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES, HipEngine
+    src = ("define stream S (v float); @info(name='q') from every e1=S[v > 2.0] -> e2=S[v > e1.v] "
+           "within 20 hours select e1.v as a insert into O;")  # (SIM form; `within` lets the push chunk)
+    app = App(src, engine_factory=lambda blob: None)
+    types = [s.attr_types for s in app.ir.streams]
+    normal = HipEngine(app.blob, stream_types=types)
+    ring = HipEngine(app.blob, stream_types=types, flags=SDH_FLAG_DEVICE_MATCHES)
+    dev = torch.device("cuda:0")
+    n1 = 1 << 26  # (not past 2^26: the push keeps 8-B / rec4 records)
+    for lo, n, first, last in ((0, n1, 5, 1), (n1, 3, 1, 10)):
+        ts = torch.arange(lo, lo + n, dtype=torch.int64, device=dev)
+        v = torch.ones(n, dtype=torch.float32, device=dev)
+        v[0], v[-1] = first, last
+        for e in (normal, ring):
+            e.push_device(0, n, ts.data_ptr(), [v.data_ptr()])
+        dn, dr = normal.debug_digest(), ring.debug_digest()
+        assert dn == dr, f"push at {lo}: normal {dn} != ring {dr}"
+        del ts, v
+    assert dn[0] == 1  # the first event's partial, matched 2^26 + 2 events later
+    normal.close()
+    ring.close()

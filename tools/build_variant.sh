@@ -9,5 +9,5 @@ name=$1; src=$2; defs=$3
 obj=../../ab/obj/${src%.hip}_$name.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math $defs -c $src -o $obj
 objs=$(ls build/*.o | grep -v "build/${src%.hip}.o")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../../ab/lib_$name.so $objs $obj -lhiprtc
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../../ab/lib_$name.so $objs $obj -lhiprtc -lrccl
 echo ab/lib_$name.so
