@@ -7,13 +7,19 @@ P = 10,000 concurrent 2-state patterns in total
     every e1=StockStream[price > T_p] -> e2=StockStream[price > e1.price] within W_p
 over the seeded synthetic StockStream (20 B/event SoA), generated on the device and resident in HBM
 before the timed region. One step = one NFA-step pass (one sdh_engine_push per GPU) over a batch of
-B = 8M events; every match record is written to HBM (SDH_FLAG_DEVICE_MATCHES: counted, not polled).
+B = 8M events; every match is written to HBM as a device record (SDH_FLAG_DEVICE_MATCHES) and handed
+out by sdh_engine_poll_records after each push (include/siddhi_hip.h documents the formats; a device
+consumer reads them there -- tests/test_gpu_records.py decodes them). The NFA step's output is
+therefore consumable, not discarded; the R18-ordered delivery is the `expansion` leg's figure.
 `--workload c3 | c4 | c5` runs the count/logical partitioned family (1000 patterns x 10K keys), the
 10K fraud-rule sequences, or the C5 family (100K mixed patterns over four joined streams under one
 `partition with` key, `within 1 hour`; one step = one batch per stream; one GPU = one of the 8-GPU
 node's key shards).
 
-Multi-GPU (torchrun, one process per GPU). `--scaling strong` (default) measures the metric as
+Multi-GPU: one process per GPU. `bench.py --gpus N` started without WORLD_SIZE launches its N ranks
+itself (torch.distributed.run on 127.0.0.1, before any GPU call in the parent) and exits with their
+status; under torchrun WORLD_SIZE must equal N. Fewer than N visible GPUs, or WORLD_SIZE != N, fail
+non-zero (never a silent single-rank run). `--scaling strong` (default) measures the metric as
 defined, the whole node at 10K patterns: every rank's engine runs the full program as its shard
 (sdh_config.shard_rank / shard_world): the P patterns split by pattern set (rank r runs patterns r,
 r+N, ...; c3: the partition keys are split instead, rank r owning |String.valueOf(key).hashCode() % N|
@@ -35,6 +41,8 @@ import glob
 import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -46,6 +54,7 @@ import numpy as np  # noqa: E402
 DEFAULTS = {  # workload -> (patterns, events per step, keys); patterns are the node total under strong
     # scaling and per GPU under weak scaling (c5: always per GPU, one of the 8-GPU node's key shards)
     "c2": (10000, 1 << 23, 100),
+    "c2x": (10000, 1 << 22, 100),  # the C2 family with an event-only conjunct on e2 (workloads.c2x_app)
     "c3": (1000, 1 << 20, 10000),
     "c4": (10000, 1 << 20, 100_000),
     "c5": (100_000, 1 << 16, 125_000),  # patterns, events per stream per GPU per step, accounts per GPU
@@ -59,7 +68,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=list(DEFAULTS), default="c2",
-                    help="c2: BASELINE configs[1] at the metric's 10K patterns (headline); c3: configs[2] "
+                    help="c2: BASELINE configs[1] at the metric's 10K patterns (headline); c2x: the same family "
+                         "with an event-only conjunct on e2 (off K_ratchet's plan); c3: configs[2] "
                          "(count/logical, partitioned); c4: configs[3] (10K fraud-rule sequences); c5: configs[4]")
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="strong (default): the workload's patterns (c3: keys) are split over the N GPUs -- "
@@ -80,12 +90,42 @@ def parse():
                          "~72 GB live in ~125 GB of rings)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-calibrate", action="store_true", help="skip the HBM copy / read ceiling measurement")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch check: every rank prints {rank, local_rank, world_size} and exits (no GPU)")
     return ap.parse_args()
 
 
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`--gpus N` without WORLD_SIZE: start the N ranks (torch.distributed.run, one process per GPU) as
+    child processes and return their exit status; None when this process is a rank itself. Nothing
+    here touches the GPU (torch.cuda.device_count() counts devices without initialising HIP)."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}")
+        return None
+    if args.gpus <= 1:
+        return None
+    if not args.dry_run:
+        import torch
+        n = torch.cuda.device_count()
+        if n < args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but {n} GPU(s) visible")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.call(cmd)
+
+
 def app_source(workload, n, first, step=1):
-    from siddhi_amd.workloads import c2_app, c3_app, c4_app, c5_app
-    return {"c2": c2_app, "c3": c3_app, "c4": c4_app, "c5": c5_app}[workload](n, first=first, step=step)
+    from siddhi_amd.workloads import c2_app, c2x_app, c3_app, c4_app, c5_app
+    return {"c2": c2_app, "c2x": c2x_app, "c3": c3_app, "c4": c4_app, "c5": c5_app}[workload](n, first=first, step=step)
 
 
 class Shard:
@@ -217,7 +257,10 @@ def cpu_baseline(workload, n_symbols, budget_s):
                       f"{d1} events (oracle/liboracle.so, matches counted in the library)"}
 
 
+KERNEL_OF_PLAN = {}  # workload -> the kernel its plan launches, where it differs from the default
+
 KERNEL_SOURCES = {  # what a kernel's code and launch configuration are built from
+    "nfa_chain_kernel": ["nfa_chain.hip", "nfa_types.h", "engine.hip"],
     "nfa_ratchet_kernel": ["nfa_ratchet.hip", "nfa_types.h", "engine.hip"],
     "nfa_gen_kernel": ["nfa_gen.hip", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
     "nfa_seq_kernel": ["nfa_gen.hip", "seq_body.h", "dev_common.h", "kgen.h", "gen_lower.h", "nfa_types.h",
@@ -292,7 +335,7 @@ def timed_steps(eng, step, warmup, steps, world, dist):
                 mem += f" (slab live {lb / 1e9:.1f} GB, reserved {rb / 1e9:.1f} GB, directory {db / 1e9:.1f} GB)"
         log(f"warm-up step {i + 1}/{warmup}: {dt * 1e3:.1f} ms, last kernel "
             f"{eng.stats().last_kernel_ms:.1f} ms{mem}")
-    kern_ms, kern_bytes, matches = [], [], 0
+    kern_ms, kern_bytes, rec_bytes, matches = [], [], [], 0
     pe0 = eng.stats().pattern_events
     if world > 1:
         dist.barrier()
@@ -301,10 +344,11 @@ def timed_steps(eng, step, warmup, steps, world, dist):
     step_wall = []  # (host clock per step call: a push returns once its step is done)
     for i in range(warmup, warmup + steps):
         ts = time.perf_counter()
-        ms, by, nm = step(i)
+        ms, by, nm, rb = step(i)
         step_wall.append((time.perf_counter() - ts) * 1e3)
         kern_ms.append(ms)
         kern_bytes.append(by)
+        rec_bytes.append(rb)
         matches += nm
     torch.cuda.synchronize()
     if world > 1:
@@ -321,7 +365,7 @@ def timed_steps(eng, step, warmup, steps, world, dist):
     # (event, pattern) evaluations the engine performed: B x patterns for pattern-set shards, each
     # rank's own keys' events x patterns for key shards (sdh_stats.pattern_events)
     pe = float(eng.stats().pattern_events - pe0)
-    return elapsed, kern_ms, kern_bytes, matches, pe
+    return elapsed, kern_ms, kern_bytes, rec_bytes, matches, pe
 
 
 def reduce_run(elapsed, matches, pe, live, world, dist, cdev):
@@ -358,10 +402,18 @@ def launches_per_step(prof, prof_dir):
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "local_rank": local, "world_size": world, "gpus": args.gpus}), flush=True)
+        return
     import torch
+    if local >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible")
     import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -433,7 +485,7 @@ def main():
                 torch.cuda.synchronize()
             else:
                 per_stream = batches[i - args.warmup]
-            ms = by = 0.0
+            ms = by = rb = 0.0
             nm = 0
             for si, cols in enumerate(per_stream):
                 if not bcast:
@@ -442,28 +494,36 @@ def main():
                     engine.push_bcast_device(si, B, cols[0].data_ptr(), [c.data_ptr() for c in cols[1:]], root=0)
                 else:
                     engine.push_bcast_recv(root=0)
+                # the push's device records go to their consumer (sdh_engine_poll_records: the
+                # descriptor of the records in HBM; no device work)
+                rec = engine.poll_records()
                 if len(per_stream) > 1 or i >= args.warmup:
                     kms, kby = engine.push_stats()  # (no device work inside the timed steps)
                     ms += kms
                     by += kby
-                    nm += engine.pending_matches()
-            return ms, by, nm
+                    nm += rec.n
+                    rb += rec.r_bytes + 8.0 * rec.f_words + 8.0 * rec.c_n * rec.c_words
+            return ms, by, nm, rb
         return step
 
-    elapsed, kern_ms, kern_bytes, matches, pe = timed_steps(eng, make_step(eng, pre), args.warmup, args.steps,
-                                                           world, dist)
+    elapsed, kern_ms, kern_bytes, rec_bytes, matches, pe = timed_steps(eng, make_step(eng, pre), args.warmup,
+                                                                      args.steps, world, dist)
     live = eng.stats().live_partials
     elapsed, matches, pe, live = reduce_run(elapsed, matches, pe, live, world, dist, cdev)
     value = pe / elapsed
     avg_ms = float(np.mean(kern_ms))
-    avg_bytes = float(np.mean(kern_bytes))
-    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
+    avg_bytes = float(np.mean(kern_bytes))  # SURVEY §8(d) accounting bytes per step (32 B per match)
+    avg_rec = float(np.mean(rec_bytes))      # record bytes the kernels wrote per step (device records)
     peak = 8000.0
     per_gpu = "per GPU" if scaling == "weak" else f"in total over {world} GPU(s)"
     if args.workload == "c2":
         wl = (f"C2 at the metric's 10K patterns: {P} concurrent 2-state filter+reference patterns {per_gpu} "
               "(every e1[price>T_p] -> e2[price>e1.price] within W_p)")
         kernel = "nfa_ratchet_kernel"
+    elif args.workload == "c2x":
+        wl = (f"C2x: {P} C2 patterns {per_gpu} with an event-only conjunct on e2 "
+              "(every e1[price>T_p] -> e2[price>e1.price and volume>V_p] within W_p)")
+        kernel = KERNEL_OF_PLAN.get("c2x", "nfa_chain_kernel")
     elif args.workload == "c3":
         wl = (f"C3: {P} count <2:5> + logical and/or patterns, partition with (symbol) over {K} keys, "
               f"within 10 sec; " + (f"key shards x{world}" if sh.keyed else f"{P} patterns per GPU"))
@@ -480,6 +540,23 @@ def main():
     prof, prof_dir = profiled(kernel, args.workload, sh.n, B)
     traffic = prof.get("traffic_bytes") if prof else None
     launches = launches_per_step(prof, prof_dir)
+    # Roofline. `achieved` is what the memory system moved: the committed rocprofv3 PMC
+    # bytes per launch of this kernel at these sources (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) x
+    # launches per step, over this run's kernel time per step (HIP events on the engine's stream).
+    # Without a matching profile it falls back to the design's minimum bytes and says so.
+    m_step = matches / max(1, args.steps * world)
+    design = None
+    if args.workload == "c2":
+        # the design's own minimum per step: every 64-pattern group streams the batch's ts + price
+        # (the start filter reads the same column) once, plus the record bytes the kernel wrote
+        # (rec4: 4 B per match + 8 B per matching event and wave) -- §8(d)'s accounting less its 32 B
+        # per match, plus the records as written
+        design = avg_bytes - 32.0 * m_step + avg_rec
+    if traffic:
+        moved, source = traffic * launches, "pmc"
+    else:
+        moved, source = (design if design is not None else avg_bytes), ("design" if design is not None else "accounting_8d")
+    achieved = moved / (avg_ms * 1e-3) / 1e9
     result = {
         "metric": "events/sec x active patterns (whole node) at 10K patterns; achieved HBM GB/s",
         "value": value,
@@ -498,25 +575,24 @@ def main():
                    "timed_events": B * args.steps * (4 if c5 else 1),
                    "keys": K, "parallelism": (f"key shards x{world}" if sh.keyed else f"pattern-set x{world}") +
                    (" (RCCL event broadcast)" if bcast else ""),
+                   "output": "device records, every match written and handed out per push (sdh_engine_poll_records)",
                    "matches": matches, "matches_per_s": matches / elapsed, "live_partials": live,
+                   "record_bytes_per_step": avg_rec, "record_bytes_per_match": avg_rec / max(1.0, m_step),
                    "source_hash": source_hash(kernel)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                     "frac": achieved / peak, "traffic": traffic, "traffic_source": prof_dir,
+                     "frac": achieved / peak, "achieved_source": source,
+                     "traffic": traffic, "traffic_source": prof_dir,
                      "kernel": kernel, "kernel_ms": avg_ms,
-                     # measured HBM rate: the profile's PMC bytes per launch over its average launch
-                     # time (below `achieved` when the device record is narrower than §8(d)'s 32-B
-                     # match unit); per step: x launches per step
-                     "traffic_gbps": (traffic / (prof["kernel_ns_avg"] * 1e-9) / 1e9) if traffic else None,
                      "launches_per_step": launches,
-                     "traffic_per_step": traffic * launches if traffic else None},
+                     "traffic_per_step": traffic * launches if traffic else None,
+                     # the profiled run's own rate (its PMC bytes over its own launch time)
+                     "traffic_gbps_profiled": (traffic / (prof["kernel_ns_avg"] * 1e-9) / 1e9) if traffic else None,
+                     # SURVEY §8(d)'s work accounting (32 B per match: the tuple the reference hands over),
+                     # not bytes the device moves -- the device record is ~4.6 B
+                     "accounting_8d": {"bytes_per_step": avg_bytes, "per_kernel_second_gbps": avg_bytes / (avg_ms * 1e-3) / 1e9}},
     }
-    if args.workload == "c2":
-        # §8(d) prices a match at 32 B; the K_ratchet record is 8 B. frac_design: the design's own
-        # minimum bytes per launch -- E x 16 B per 64-pattern group (ts, price; f0 reads the same
-        # column) + 8 B per match -- over the kernel time, against 8 TB/s
-        m_launch = matches / max(1, args.steps * world)
-        design = avg_bytes - 24.0 * m_launch
-        result["roofline"]["design_bytes_per_launch"] = design
+    if design is not None:
+        result["roofline"]["design_bytes_per_step"] = design
         result["roofline"]["frac_design"] = design / (avg_ms * 1e-3) / 1e9 / peak
     if prof:
         result["roofline"]["counters"] = {k: v for k, v in prof.items() if k != "traffic_bytes"}
@@ -542,8 +618,6 @@ def main():
         rf["measured_peak"] = {"copy": copy_gbps, "read": read_gbps, "unit": "GB/s",
                                "how": "best of 5 streaming 4 GiB copies / reads (csrc/calib.hip)"}
         rf["frac_measured"] = achieved / copy_gbps
-        if traffic:
-            rf["traffic_frac_measured"] = rf["traffic_gbps"] / copy_gbps
     if c5:  # the sparse state (K_slab): bytes per live partial, engine build time
         lb, rb, db = eng.state_bytes()
         result["config"].update({"state_live_bytes": lb, "state_slab_bytes": rb, "state_dir_bytes": db,
@@ -558,7 +632,7 @@ def main():
         weng.set_comm(comm)
         wsteps = max(2, args.steps // 3)
         wpre = [local_batch(i) for i in range(args.warmup, args.warmup + wsteps)]
-        el, _, _, wm, wpe = timed_steps(weng, make_step(weng, wpre), args.warmup, wsteps, world, dist)
+        el, _, _, _, wm, wpe = timed_steps(weng, make_step(weng, wpre), args.warmup, wsteps, world, dist)
         el, wm, wpe, _ = reduce_run(el, wm, wpe, 0, world, dist, cdev)
         result["weak_scaling"] = {"value": wpe / el, "unit": "pattern-events/s", "patterns_per_gpu": wsh.n,
                                   "steps": wsteps, "ms_per_step": el * 1e3 / wsteps, "matches": wm}

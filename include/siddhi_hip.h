@@ -18,6 +18,8 @@
  *   sdh_engine_poll_compact the same matches as 16-B compact rows (host or HBM)
  *   sdh_engine_poll_compact_ex  every match as compact rows + key ids, timer tiebreaks and count
  *                          chains (the StateEvent contents of StateEvent.java:138-182)
+ *   sdh_engine_poll_records the matches as the kernels wrote them, left in HBM for a device consumer
+ *                          (SDH_FLAG_DEVICE_MATCHES; the formats are documented below)
  *   sdh_engine_set_strings  <- partition/PartitionStreamReceiver.java:277-281 (String.valueOf of a
  *                          string key: its hashCode / length, for the fan-out order)
  *   sdh_engine_reserve / sdh_engine_reserve_keys
@@ -81,11 +83,18 @@ typedef struct sdh_config {
   int32_t gen_list_cap;      /* entries per pending / newAndEvery list                       */
   int32_t gen_pad;
   int64_t gen_max_keys;      /* distinct partition keys per partition                        */
+  /* Tuning / diagnostic overrides, "NAME=VALUE;NAME=VALUE" (NULL: none), copied at create: kernel
+   * A/B knobs, traces, and test hooks that force a code path (DESIGN.md §4 lists them). The library
+   * reads no environment variables, so a host process's environment never changes its behaviour. */
+  const char* debug;
 } sdh_config;
 
-/* Matches of a push that are not polled before the next push are dropped instead of being copied
- * to the host (they stay countable via sdh_engine_pending_matches until then). For consumers that
- * read matches on the device, and for throughput benchmarking of the NFA step. */
+/* Device records: a push leaves its matches in HBM as the kernels wrote them (no R18 sort, no
+ * match table), for consumers on the device: sdh_engine_poll_records hands them out (formats below),
+ * valid until the next push. Every match of the push is written (the record buffers grow and the push
+ * re-runs exactly, as in the normal mode); a push's records that nobody reads are dropped at the next
+ * push (sdh_engine_pending_matches counts them until then). sdh_engine_poll and the compact polls
+ * return nothing in this mode. */
 #define SDH_FLAG_DEVICE_MATCHES 1
 /* Disable the K_ratchet plan (every query of that shape runs on the general chain kernel instead);
  * for differential testing of the two plans. */
@@ -225,6 +234,86 @@ typedef struct sdh_matches_compact_ex {
 int sdh_engine_poll_compact_ex(sdh_engine* e, int32_t device, sdh_matches_compact_ex* out);
 /* Device-resident match count of the last push (no host copy of the matches). */
 int sdh_engine_pending_matches(sdh_engine* e, int64_t* n);
+/* ---- Device records (SDH_FLAG_DEVICE_MATCHES) ----
+ * The last push's matches as the kernels wrote them, in three parts; every pointer is a HIP device
+ * pointer into engine-owned HBM, valid until the next push/restore/destroy. Records are in no
+ * particular order (wave completion order); a consumer that needs the reference's delivery order
+ * sorts them by (trigger seq, receiver rank, ...) -- or polls in the normal mode. Sequence numbers:
+ * the push's event at batch offset k has seq seq_base + k (sdh_matches.seq). The call also marks the
+ * records consumed (sdh_engine_pending_matches returns 0 until the next push).
+ *
+ * 1. K_ratchet blocks (the `every e1=S[f] -> e2=S[cur.a OP e1.a] within T` plan: DESIGN.md §3.1).
+ *    Block b (0 <= b < r_blocks) is r_blk_bytes at (const char*)r_base + b * r_blk_bytes and belongs
+ *    to wave group g = r_group[b]; a record's lane l names query r_lane_query[g * 64 + l]. It holds
+ *    r_count[b] records of format r_format:
+ *      SDH_REC_8:  uint32 pairs {e2 | l << 26, e1lo}: e2 = the trigger's batch offset (bits 0-25),
+ *                  e1lo = the low 32 bits of e1's seq (e1 = s2 - (uint32)((uint32)s2 - e1lo), s2 =
+ *                  seq_base + e2);
+ *      SDH_REC_16: uint32 quads {e2, l, e1lo, 0} (batches of more than 2^26 events);
+ *      SDH_REC_4:  uint32 entries {d | l << 26} from the block's start, d = s2 - e1 (< 2^26), plus
+ *                  r_side[b] side entries, uint32 pairs {first, e2}, from the block's END downwards:
+ *                  side entry j at r_blk_bytes - 8 * (j + 1). Entry i belongs to the trigger e2 of the
+ *                  last side entry whose `first` <= i (side entry 0 has first == 0; `first` ascends).
+ *                  (Only float-keyed queries write rec4 blocks: a block with r_side[b] < 0 in such a
+ *                  push holds SDH_REC_8 records.)
+ *    sdh_engine_records_compact decodes this part into compact rows on the device.
+ * 2. Flat records (the K_gen / K_part / K_seq / K_slab plans): f_words int64 words at f_base, a
+ *    sequence of records, each identified by the low 32 bits of its first word, lo = (int32)w[0]:
+ *      lo >= 0       a full record of lo words: {lo, query, key, ts, trigger seq, emission index,
+ *                    S | stream << 16, then per state slot: c, c event seqs} (stream 0xFFFF: an absent
+ *                    state's timer match; key -1 when unpartitioned, else the raw partition key);
+ *      -lo >> 16 == 0: K_part logical (or / and) match, -lo words (4): w[0] >> 32 = query,
+ *                    w[1] = {trigger batch offset (low 32), partition key id (high 32)}, then int32
+ *                    distances back from the trigger (s2 - seq): e1, side A, side B (INT32_MIN: empty);
+ *      -lo >> 16 == 1: K_part count match, (-lo & 0xFFFF) words: as above, then e1, chain length c and
+ *                    the c chain events' distances (two int32 per word, low half first);
+ *      -lo >> 16 == 2: K_seq window match, (-lo & 0xFFFF) words: w[0] >> 32 = query, w[1] = {trigger
+ *                    batch offset, S}, then the S - 1 earlier slots' int32 distances;
+ *      -lo >> 16 == 4: padding of (-lo & 0xFFFF) words (skip it).
+ *    A K_part record's key id is a dense id: f_query_keys[query][id] is the raw partition key (the
+ *    sdh_matches.key value; f_query_keys[query] is NULL for an unpartitioned query).
+ * 3. K_chain segments (the general chain plan): c_items segments, segment i = c_count[i] records of
+ *    c_words int64 at c_base + c_off[i] * c_words, each {query, ts, seq_0 .. seq_{S-1}}.
+ */
+#define SDH_REC_NONE 0
+#define SDH_REC_8 1
+#define SDH_REC_16 2
+#define SDH_REC_4 3
+typedef struct sdh_records {
+  int64_t n;                  /* matches in all parts                                          */
+  int64_t seq_base;           /* seq of the push's batch offset 0                              */
+  int64_t n_events;           /* events of the push                                            */
+  /* 1. K_ratchet blocks */
+  int64_t r_n;                /* matches in this part                                          */
+  int64_t r_blocks;
+  int64_t r_bytes;            /* bytes of records written (entries + side entries)             */
+  const void* r_base;
+  const int32_t* r_count;
+  const int32_t* r_side;      /* (SDH_REC_4 blocks)                                             */
+  const int32_t* r_group;
+  const int32_t* r_lane_query;
+  int32_t r_format;           /* SDH_REC_*                                                      */
+  int32_t r_blk_bytes;
+  /* 2. flat records */
+  int64_t f_n;
+  int64_t f_words;
+  const int64_t* f_base;
+  const int64_t* const* f_query_keys; /* [queries] device pointers to the key tables (see above)  */
+  /* 3. K_chain segments */
+  int64_t c_n;
+  int64_t c_items;
+  int32_t c_words;
+  int32_t flags;              /* 0 */
+  const int64_t* c_base;
+  const int64_t* c_off;
+  const int64_t* c_count;
+} sdh_records;
+int sdh_engine_poll_records(sdh_engine* e, sdh_records* out);
+/* Part 1 of the last push's device records decoded into compact rows of `width` int32 (>= 4) in HBM,
+ * in block order: { query, e2 - seq_base, e2 - e1, 0, INT32_MIN ... } (the sdh_matches_compact row of
+ * a 2-state match). rows == NULL: *n = the row count only; otherwise rows holds cap rows and
+ * SDH_E_CAPACITY is returned if the part has more. */
+int sdh_engine_records_compact(sdh_engine* e, int32_t* rows, int64_t cap, int32_t width, int64_t* n);
 /* Absent patterns (`not S[..] for T`) and time. The runtime starts at t (SiddhiAppRuntime.start:
  * start states with a 'for' time schedule their first check at t + T); without this call it starts
  * with its first event or advance. sdh_engine_advance_time: time passes to t with no event, and
@@ -284,9 +373,15 @@ const char* sdh_last_error(sdh_engine* e);
  *     ncclCommInitRank on every rank; collective: every rank calls it).
  *   sdh_comm_create_local: `world` ranks inside this process (engines on one or several devices),
  *     buffers copied device-to-device: the same protocol, for one process driving several engines and
- *     for testing the exchange on one GPU. Its collectives complete in call order: a broadcast's root
- *     pushes first and the other ranks after it, before the root's next push; a gather's ranks
- *     1..world-1 call first and rank 0 last.
+ *     for testing the exchange on one GPU. Its collectives are one-sided and complete in call order,
+ *     so its calls must be serialised (one thread, or the caller orders them): a broadcast's root
+ *     pushes first and every other rank receives it before the root's next broadcast; a gather's ranks
+ *     1..world-1 call first and rank 0 last, and a rank that has deposited its matches is not polled
+ *     again until rank 0 has gathered. A call out of this order fails with SDH_E_INVALID. Copies wait
+ *     on the depositing rank's stream (HIP events), so the engines may run on different streams.
+ * An invalid batch at the root of sdh_engine_push_bcast fails the call on every rank (the root
+ * broadcasts an error header). With RCCL every rank receives every rank's gather header and all
+ * refuse an out-of-step window before any table is cleared.
  * sdh_engine_set_comm attaches a communicator (not owned; it must outlive the engine's use of it,
  * and its device must be the engine's). Both exchange calls are collective over the communicator's
  * ranks and run on the engine's stream. */
@@ -314,8 +409,7 @@ int sdh_engine_gather(sdh_engine* e, int32_t device, sdh_matches* out);
  * representative K_seq / K_part shapes. Returns the number compiled, or -1 with the compiler log. */
 int sdh_spec_selftest(char* log, size_t cap);
 /* Test diagnostic: out[0] = the K_ratchet records the last push wrote, out[1] = an order-independent
- * hash of them (e2 seq, query, e1 seq), in either output mode (SDH_FLAG_DEVICE_MATCHES included,
- * unless its record ring wrapped: SDH_E_CAPACITY). */
+ * hash of them (e2 seq, query, e1 seq), in either output mode (device records included). */
 int sdh_engine_debug_digest(sdh_engine* e, uint64_t* out);
 /* Diagnostic: best-of-`iters` HBM bandwidth of a streaming copy (bytes read + written) and a
  * streaming read over `bytes`-sized buffers on `device`, in GB/s -- the measured ceiling the bench

@@ -36,6 +36,7 @@ struct Buf {
 };
 
 int rank(const sdh_comm* c);
+bool is_local(const sdh_comm* c);
 int world(const sdh_comm* c);
 int device(const sdh_comm* c);
 
@@ -46,8 +47,11 @@ int device(const sdh_comm* c);
 void bcast_hdr(sdh_comm* c, int64_t hdr[HDR], int root, hipStream_t s);
 void bcast_bufs(sdh_comm* c, const std::vector<Buf>& bufs, int root, hipStream_t s);
 
-// Gather to rank 0: every rank's header (rank 0 receives world x HDR words into `all`), then every
-// non-root rank's buffers (`mine`: src) into rank 0's destinations (`recv[r]`: dst, r = 1..world-1).
+// Gather to rank 0: every rank's header -- RCCL: an all-gather, every rank receives world x HDR words
+// into `all`; local: rank 0 only --, then the buffers (`mine`: src) into rank 0's destinations
+// (`recv[r]`: dst). RCCL: every rank passes `mine`, rank 0 its own run too (a self send / receive) and
+// recv[0 .. world-1]; local: the non-root ranks pass `mine`, rank 0 recv[1 .. world-1] (its own run
+// it copies itself).
 void gather_hdr(sdh_comm* c, const int64_t hdr[HDR], int64_t* all, hipStream_t s);
 void gather_bufs(sdh_comm* c, const std::vector<Buf>& mine, const std::vector<std::vector<Buf>>& recv, hipStream_t s);
 

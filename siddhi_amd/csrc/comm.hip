@@ -38,8 +38,18 @@ struct LocalGroup {
     bool g_hdr = false, g_bufs = false;
     int64_t ghdr[sdh::xch::HDR] = {};
     std::vector<sdh::xch::Buf> gbufs;
+    // stream order between ranks: the depositing rank records an event on its stream once its buffers
+    // are complete (a broadcast root's batch, a gather deposit), and the copying rank's stream waits on
+    // it before its copies (raw pointers alone carry no ordering)
+    hipEvent_t bev = nullptr, gev = nullptr;
   };
   std::vector<Slot> slots;
+  ~LocalGroup() {
+    for (auto& sl : slots) {
+      if (sl.bev) (void)hipEventDestroy(sl.bev);
+      if (sl.gev) (void)hipEventDestroy(sl.gev);
+    }
+  }
 };
 
 [[noreturn]] void fail(const std::string& m) { throw std::runtime_error(m); }
@@ -48,6 +58,11 @@ struct LocalGroup {
 
 void hipchk(hipError_t e, const char* what) {
   if (e != hipSuccess) fail(std::string(what) + ": " + hipGetErrorString(e));
+}
+// record `ev` (created on first use, on the calling rank's device) on stream s
+void mark(hipEvent_t& ev, hipStream_t s) {
+  if (!ev) hipchk(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  hipchk(hipEventRecord(ev, s), "hipEventRecord");
 }
 void ncclchk(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) fail(std::string(what) + ": " + ncclGetErrorString(r));
@@ -71,6 +86,7 @@ namespace sdh {
 namespace xch {
 
 int rank(const sdh_comm* c) { return c->rank; }
+bool is_local(const sdh_comm* c) { return c->local; }
 int world(const sdh_comm* c) { return c->world; }
 int device(const sdh_comm* c) { return c->device; }
 
@@ -81,6 +97,9 @@ void bcast_hdr(sdh_comm* c, int64_t hdr[HDR], int root, hipStream_t s) {
     auto& R = c->grp->slots[(size_t)root];
     auto& me = c->grp->slots[(size_t)c->rank];
     if (c->rank == root) {
+      for (int r = 0; r < c->world; ++r)  // (the previous batch reached every rank before this one)
+        if (r != root && R.bgen && c->grp->slots[(size_t)r].seen_hdr[(size_t)root] != R.bgen)
+          misuse("local communicator: rank " + std::to_string(r) + " has not received the root's previous batch");
       ++R.bgen;
       std::memcpy(R.bhdr, hdr, sizeof R.bhdr);
       R.bbufs.clear();
@@ -93,7 +112,7 @@ void bcast_hdr(sdh_comm* c, int64_t hdr[HDR], int root, hipStream_t s) {
     me.seen_hdr[(size_t)root] = R.bgen;
     return;
   }
-  if (c->world == 1) return;
+  // (RCCL at world 1 too: the collective runs, copying in place)
   hipchk(hipMemcpyAsync(c->scratch, hdr, HDR * 8, hipMemcpyHostToDevice, s), "broadcast header");
   ncclchk(ncclBroadcast(c->scratch, c->scratch, HDR, ncclInt64, root, c->nc, s), "ncclBroadcast (header)");
   hipchk(hipMemcpyAsync(hdr, c->scratch, HDR * 8, hipMemcpyDeviceToHost, s), "broadcast header");
@@ -108,11 +127,13 @@ void bcast_bufs(sdh_comm* c, const std::vector<Buf>& bufs, int root, hipStream_t
     if (c->rank == root) {
       R.bbufs = bufs;
       R.bbufs_gen = R.bgen;
+      mark(R.bev, s);
       return;
     }
     if (R.bbufs_gen != me.seen_hdr[(size_t)root] || R.bbufs.size() != bufs.size() ||
         me.seen_bufs[(size_t)root] == R.bbufs_gen)
       misuse("local communicator: broadcast buffers out of step with the root");
+    hipchk(hipStreamWaitEvent(s, R.bev, 0), "hipStreamWaitEvent");
     for (size_t i = 0; i < bufs.size(); ++i) {
       if (R.bbufs[i].bytes != bufs[i].bytes) misuse("local communicator: broadcast buffer sizes differ");
       if (bufs[i].bytes)
@@ -121,7 +142,6 @@ void bcast_bufs(sdh_comm* c, const std::vector<Buf>& bufs, int root, hipStream_t
     me.seen_bufs[(size_t)root] = R.bbufs_gen;
     return;
   }
-  if (c->world == 1) return;
   ncclchk(ncclGroupStart(), "ncclGroupStart");
   for (const Buf& b : bufs) {
     if (!b.bytes) continue;
@@ -136,6 +156,7 @@ void gather_hdr(sdh_comm* c, const int64_t hdr[HDR], int64_t* all, hipStream_t s
     std::lock_guard<std::mutex> g(c->grp->mu);
     auto& me = c->grp->slots[(size_t)c->rank];
     if (c->rank != 0) {
+      if (me.g_hdr) misuse("local communicator: rank 0 has not taken this rank's previous gather");
       std::memcpy(me.ghdr, hdr, sizeof me.ghdr);
       me.g_hdr = true;
       me.g_bufs = false;
@@ -149,21 +170,12 @@ void gather_hdr(sdh_comm* c, const int64_t hdr[HDR], int64_t* all, hipStream_t s
     }
     return;
   }
-  if (c->rank == 0) std::memcpy(all, hdr, HDR * 8);
-  if (c->world == 1) return;
-  if (c->rank != 0) {
-    hipchk(hipMemcpyAsync(c->scratch, hdr, HDR * 8, hipMemcpyHostToDevice, s), "gather header");
-    hipchk(hipStreamSynchronize(s), "gather header");
-    ncclchk(ncclSend(c->scratch, HDR, ncclInt64, 0, c->nc, s), "ncclSend (header)");
-    hipchk(hipStreamSynchronize(s), "gather header");
-    return;
-  }
-  ncclchk(ncclGroupStart(), "ncclGroupStart");
-  for (int r = 1; r < c->world; ++r)
-    ncclchk(ncclRecv(c->scratch + (size_t)r * HDR, HDR, ncclInt64, r, c->nc, s), "ncclRecv (header)");
-  ncclchk(ncclGroupEnd(), "ncclGroupEnd");
-  hipchk(hipMemcpyAsync(all + HDR, c->scratch + HDR, (size_t)(c->world - 1) * HDR * 8, hipMemcpyDeviceToHost, s),
-         "gather header");
+  // RCCL: an all-gather, so that every rank sees every header and can refuse an out-of-step window
+  // before any rank clears its table or sends its buffers (world 1 included)
+  int64_t* mine = c->scratch + (size_t)c->world * HDR;
+  hipchk(hipMemcpyAsync(mine, hdr, HDR * 8, hipMemcpyHostToDevice, s), "gather header");
+  ncclchk(ncclAllGather(mine, c->scratch, HDR, ncclInt64, c->nc, s), "ncclAllGather (header)");
+  hipchk(hipMemcpyAsync(all, c->scratch, (size_t)c->world * HDR * 8, hipMemcpyDeviceToHost, s), "gather header");
   hipchk(hipStreamSynchronize(s), "gather header");
 }
 
@@ -174,12 +186,14 @@ void gather_bufs(sdh_comm* c, const std::vector<Buf>& mine, const std::vector<st
       auto& me = c->grp->slots[(size_t)c->rank];
       me.gbufs = mine;
       me.g_bufs = true;
+      mark(me.gev, s);
       return;
     }
     for (int r = 1; r < c->world; ++r) {
       auto& S = c->grp->slots[(size_t)r];
       const auto& want = recv[(size_t)r];
       if (!S.g_bufs || S.gbufs.size() != want.size()) misuse("local communicator: gather buffers out of step");
+      hipchk(hipStreamWaitEvent(s, S.gev, 0), "hipStreamWaitEvent");
       for (size_t i = 0; i < want.size(); ++i) {
         if (S.gbufs[i].bytes != want[i].bytes) misuse("local communicator: gather buffer sizes differ");
         if (want[i].bytes)
@@ -189,16 +203,15 @@ void gather_bufs(sdh_comm* c, const std::vector<Buf>& mine, const std::vector<st
     }
     return;
   }
-  if (c->world == 1) return;
+  // RCCL: every rank sends its run to rank 0 -- rank 0 to itself as well (a self send / receive, so
+  // world 1 runs the same transfers), and rank 0 receives every rank's
   ncclchk(ncclGroupStart(), "ncclGroupStart");
-  if (c->rank != 0) {
-    for (const Buf& b : mine)
-      if (b.bytes) ncclchk(ncclSend(b.src, b.bytes, ncclUint8, 0, c->nc, s), "ncclSend");
-  } else {
-    for (int r = 1; r < c->world; ++r)
+  for (const Buf& b : mine)
+    if (b.bytes) ncclchk(ncclSend(b.src, b.bytes, ncclUint8, 0, c->nc, s), "ncclSend");
+  if (c->rank == 0)
+    for (int r = 0; r < c->world; ++r)
       for (const Buf& b : recv[(size_t)r])
         if (b.bytes) ncclchk(ncclRecv(b.dst, b.bytes, ncclUint8, r, c->nc, s), "ncclRecv");
-  }
   ncclchk(ncclGroupEnd(), "ncclGroupEnd");
 }
 
@@ -369,7 +382,7 @@ int sdh_comm_create(const void* id, size_t len, int32_t rank, int32_t world, int
     c->world = world;
     c->device = device;
     hipchk(hipSetDevice(device), "hipSetDevice");
-    hipchk(hipMalloc(&c->scratch, (size_t)world * sdh::xch::HDR * 8), "hipMalloc");
+    hipchk(hipMalloc(&c->scratch, (size_t)(world + 1) * sdh::xch::HDR * 8), "hipMalloc");
     ncclUniqueId u;
     std::memcpy(&u, id, SDH_COMM_ID_BYTES);
     ncclchk(ncclCommInitRank(&c->nc, world, u, rank), "ncclCommInitRank");

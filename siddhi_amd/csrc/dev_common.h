@@ -46,15 +46,20 @@ __device__ __forceinline__ int64_t raw_word(const StreamBatch& b, int attr, int6
 
 // match output: one flat word buffer; each record is reserved with an atomic add of its length
 // (the backend's atomic optimizer folds a wave's same-address adds into one atomic + a scan).
-// Ring mode (write_records == 2, SDH_FLAG_DEVICE_MATCHES): every record is still written, at its
-// offset modulo the buffer less a one-record margin, because nobody reads it back. In normal mode
-// each record's offset is also listed in rec_off (the device match table finds records by it,
-// matches.hip); a record fits only if its words and its index entry both do.
+// Device records (write_records == 2, SDH_FLAG_DEVICE_MATCHES): the records stay in the buffer for a
+// consumer (sdh_engine_poll_records walks them by their first word's length; include/siddhi_hip.h) and
+// no record index is kept. In normal mode each record's offset is also listed in rec_off (the device
+// match table finds records by it, matches.hip); a record fits only if its words and its index entry
+// both do. Either way a reservation past the buffer sets `over`, and the host grows the buffer and
+// re-runs the push exactly.
+// A pad record (device records: the unused tail of a wave's reserved run, WaveOutT) has first word
+// (uint32)(-(REC_PAD + words)): it spans `words` words, of which only the first is written.
+constexpr int REC_PAD = 4 << 16;
 struct LaneOut {
   int64_t* out;
   int64_t cap;
   unsigned long long* next;
-  bool ring;
+  bool ring;  // device records
   int64_t* rec_off;
   int64_t rec_cap;
   unsigned long long* rec_next;
@@ -64,20 +69,11 @@ struct LaneOut {
   __device__ int64_t* reserve_n(int nl, int words) {
     const int64_t tw = (int64_t)nl * words;
     const unsigned long long o = atomicAdd(next, (unsigned long long)tw);
-    if (ring) {
-      // the margin holds any record the ring wraps; a longer run of records wraps modulo the buffer
-      // less its own length (written, and counted, like any other: ADVICE r2)
-      const int64_t m = cap - (tw > GEN_RING_MARGIN ? tw : GEN_RING_MARGIN);
-      if (m <= 0) {
-        over = true;
-        return nullptr;
-      }
-      return out + (int64_t)(o % (unsigned long long)m);
-    }
     if ((int64_t)(o + tw) > cap) {
       over = true;
       return nullptr;
     }
+    if (ring) return out + o;
     const unsigned long long r = atomicAdd(rec_next, (unsigned long long)nl);
     if ((int64_t)(r + nl) > rec_cap) {
       over = true;
@@ -88,11 +84,11 @@ struct LaneOut {
   }
   __device__ int64_t* reserve(int words) {
     const unsigned long long o = atomicAdd(next, (unsigned long long)words);
-    if (ring) return out + (int64_t)(o % (unsigned long long)(cap - GEN_RING_MARGIN));
     if ((int64_t)(o + words) > cap) {
       over = true;
       return nullptr;
     }
+    if (ring) return out + o;
     const unsigned long long r = atomicAdd(rec_next, 1ull);
     if ((int64_t)r >= rec_cap) {
       over = true;
@@ -100,6 +96,10 @@ struct LaneOut {
     }
     rec_off[r] = (int64_t)o;
     return out + o;
+  }
+  // device records: the words [o, o + words) hold no record
+  __device__ void pad(int64_t o, int64_t words) {
+    if (words > 0 && o < cap) out[o] = (int64_t)(uint64_t)(uint32_t)(-(REC_PAD + (int32_t)words));
   }
 };
 
@@ -115,9 +115,9 @@ struct LaneOut {
 // CAPW_: words in the LDS buffer. Every flush takes two atomics on the chip-wide counters, which
 // serialise once the match rate is high (C3: 512 words -> 42 ms/step, 1536 -> 24), while a larger
 // buffer costs resident waves (4096 -> 38 ms); K_part uses 1536, K_seq 1024 (measured)
-// Ring mode (SDH_FLAG_DEVICE_MATCHES) reserves SDH_RING_CHUNK buffers' worth of the ring per atomic:
-// the flush's round trip on the chip-wide counter stalls the whole wave (C3 ring chunk 1: 23.4
-// ms/step, 4: 20.7, 16: 20.7; C4 27.3 / 25.9 / 26.1)
+// Device records (SDH_FLAG_DEVICE_MATCHES) reserve SDH_RING_CHUNK buffers' worth of the buffer per
+// atomic: the flush's round trip on the chip-wide counter stalls the whole wave (C3 chunk 1: 23.4
+// ms/step, 4: 20.7, 16: 20.7; C4 27.3 / 25.9 / 26.1). The unused tail of a run becomes a pad record.
 #ifndef SDH_RING_CHUNK
 #define SDH_RING_CHUNK 4
 #endif
@@ -147,7 +147,7 @@ struct WaveOutT {
     int32_t roff[CAPR];
     int64_t base, rbase;
     int32_t used, nrec;
-    int64_t cbase, cleft;  // ring mode: the wave's reserved run of the ring (SDH_RING_CHUNK)
+    int64_t cbase, cleft;  // device records: the wave's reserved run of the buffer (SDH_RING_CHUNK)
   };
   // the wave's shared counters: relaxed atomics, so no lane keeps a stale copy in a register (other
   // lanes update them) and, unlike volatile, the accesses stay ds_ operations
@@ -181,11 +181,12 @@ struct WaveOutT {
     if (n == 0) return;
     if (__lane_id() == lead) {
 #if SDH_RING_CHUNK > 1
-      // ring mode: one reservation per SDH_RING_CHUNK buffers' worth of words (the ring is written,
-      // never read back, so the run's unused tail costs nothing)
+      // device records: one reservation per SDH_RING_CHUNK buffers' worth of words (a run's unused
+      // tail becomes a pad record)
       unsigned long long o;
       if (g.ring) {
         if (ld(sh->cleft) < n) {
+          g.pad(ld(sh->cbase), ld(sh->cleft));
           st(sh->cbase, (int64_t)atomicAdd(g.next, (unsigned long long)(SDH_RING_CHUNK * CAPW)));
           st(sh->cleft, (int64_t)(SDH_RING_CHUNK * CAPW));
         }
@@ -199,8 +200,8 @@ struct WaveOutT {
       const unsigned long long o = atomicAdd(g.next, (unsigned long long)n);
 #endif
       int64_t base = (int64_t)o, rbase = 0;
+      if ((int64_t)(o + n) > g.cap) base = -1;
       if (!g.ring) {
-        if ((int64_t)(o + n) > g.cap) base = -1;
         const unsigned long long r = atomicAdd(g.rec_next, (unsigned long long)nr);
         if ((int64_t)(r + nr) > g.rec_cap) base = -1;
         rbase = (int64_t)r;
@@ -213,8 +214,7 @@ struct WaveOutT {
     if (base < 0) {
       g.over = true;
     } else if (g.ring) {
-      const int64_t rc = g.cap - GEN_RING_MARGIN, b0 = (int64_t)((unsigned long long)base % (unsigned long long)rc);
-      for (int i = me; i < n; i += cnt) g.out[b0 + i < rc ? b0 + i : b0 + i - rc] = sh->buf[pidx(i)];
+      for (int i = me; i < n; i += cnt) g.out[base + i] = sh->buf[pidx(i)];
     } else {
       for (int i = me; i < n; i += cnt) g.out[base + i] = sh->buf[pidx(i)];
       for (int i = me; i < nr; i += cnt) g.rec_off[rbase + i] = base + sh->roff[i];
@@ -316,6 +316,10 @@ struct WaveOutT {
   }
   __device__ void close() {
     flush();
+#if SDH_RING_CHUNK > 1
+    if (g.ring && __lane_id() == __ffsll((long long)active()) - 1) g.pad(ld(sh->cbase), ld(sh->cleft));
+    wave_fence();
+#endif
     over |= g.over;
   }
 };

@@ -25,6 +25,7 @@
 #include "../../include/siddhi_hip.h"
 #include "chm_order.h"
 #include "comm.h"
+#include "knobs.h"
 #include "java_fmt.h"
 #include "gen_lower.h"
 #include "nfa_types.h"
@@ -137,6 +138,12 @@ extern "C" hipError_t sdh_digest_ratchet(const int64_t* match, int blk_recs, int
                                          const int32_t* blk_group, const int32_t* blk_side,
                                          const sdh::RatchetGroup* groups, int64_t seq_base,
                                          int n_blocks, unsigned long long* acc, hipStream_t s);
+extern "C" size_t sdh_ratchet_compact_temp(int64_t n_blocks);
+extern "C" hipError_t sdh_ratchet_compact(const int64_t* match, int blk_recs, int wide, const int32_t* blk_count,
+                                          const int32_t* blk_group, const int32_t* blk_side,
+                                          const sdh::RatchetGroup* groups, int64_t seq_base, int n_blocks,
+                                          int64_t* row_off, void* temp, size_t temp_bytes, int width, int32_t* rows,
+                                          hipStream_t s);
 extern "C" hipError_t sdh_poll_sort(sdh::MatchTable T, int64_t n, int n_lo, int lo_bits, int hi_bits, int clo_bits,
                                     uint64_t* kbuf, int32_t* pbuf, void* temp, size_t temp_bytes, int64_t* oq,
                                     int64_t* okey, int64_t* ots, int64_t* oseq, int64_t* otb, int64_t* olen,
@@ -576,7 +583,7 @@ RatchetPlan ratchet_plan(const ChainQuery& c) {
 
 // SDH_ALLOC_TRACE=1: one stderr line per device buffer (re)allocation (p99 push/poll latency hunts)
 inline void alloc_trace(const char* what, size_t bytes) {
-  static const bool on = getenv("SDH_ALLOC_TRACE") != nullptr;
+  const bool on = sdh::knob("SDH_ALLOC_TRACE") != nullptr;
   if (on) fprintf(stderr, "[sdh] alloc %s %zu bytes\n", what, bytes);
 }
 
@@ -930,7 +937,7 @@ struct sdh_engine {
   DevBuf<uint8_t> sb_buf;            // a batch in key order (K_part reads; sdh_sort_batch)
   DevBuf<unsigned long long> g_rec_next;
   int64_t g_dev_matches = 0;         // K_gen / K_seq matches of the last push
-  int64_t g_used = 0;                // words of the last push's records in g_out (normal mode)
+  int64_t g_used = 0;                // words of the last push's records in g_out
   bool g_journal = false;            // the current K_gen pass journals the blocks it modifies
   // ---- K_ratchet groups ----
   std::vector<RatchetGroup> rg;
@@ -943,13 +950,20 @@ struct sdh_engine {
   DevBuf<int64_t> d_rmatch;
   DevBuf<int32_t> d_blk_count, d_blk_next, d_blk_group;
   DevBuf<int32_t> d_blk_side;            // K_ratchet rec4 blocks: side entries (-1: an 8- / 16-B block)
-  bool r_no_rec4 = false;                // a rec4 distance reached 2^26: 8-B records from then on
-  DevBuf<unsigned long long> d_rtotal;  // records written in ring mode (SDH_FLAG_DEVICE_MATCHES)
+  int64_t r_rec4_reruns = 0;             // pushes re-run with 8-B records (a rec4 distance reached 2^26)
+  DevBuf<unsigned long long> d_rtotal;  // device records: [0] entries, [2] bytes written
   int r_wide = 0;
   int64_t r_blocks = 0;              // capacity in blocks
   int r_blk_recs = 8192;
   int r_blocks_used = 0;             // of the last launch
-  int64_t r_blk_taken = 0;           // blocks the last launch took (ring mode: may exceed r_blocks)
+  int64_t r_blk_taken = 0;           // blocks the last launch took
+  double r_rec_bytes = 0;            // device records: bytes the last launch wrote (entries + side entries)
+  int r_rec4 = 0;                    // device records: the last launch wrote rec4 blocks (SIM launches)
+  DevBuf<int32_t> d_rlane_q;         // [group][64] query of each K_ratchet lane (-1 idle; sdh_records)
+  DevBuf<int64_t> d_rrow_off;        // sdh_engine_records_compact: per-block row offsets
+  DevBuf<uint8_t> d_rrow_tmp;
+  bool dev_polled = false;           // the last push's device records were handed out
+  int64_t last_n = 0, last_seq_base = 0;  // the last push's events and first seq
   // direct R18 placement (nfa_ratchet.hip PM): the (event, group cell) match counts, scanned
   DevBuf<int32_t> p_cnt;
   std::vector<int> place_cells;     // [stream] K_ratchet groups reading it (0: not placeable)
@@ -981,6 +995,7 @@ struct sdh_engine {
   sdh_stats stats{};
   std::string err;
   std::string broken;                // set when a failed push left the state undefined
+  std::vector<std::pair<std::string, std::string>> knobs;  // sdh_config.debug (knobs.h)
   // ---- multi-GPU exchange (comm.h; sdh_engine_push_bcast / sdh_engine_gather) ----
   sdh_comm* comm = nullptr;          // not owned
   DevBuf<uint8_t> x_batch;           // a broadcast batch received from the root
@@ -1095,6 +1110,19 @@ void append_ratchet(sdh_engine* e, const int64_t* ts_col, int64_t seq_base) {
   e->mt.n_lo = std::max(e->mt.n_lo, 1);
 }
 
+// per query its partition's key table, on the device (narrow K_part records carry the key's dense id)
+void upload_qkeys(sdh_engine* e) {
+  const size_t nq = std::max<size_t>(1, e->prog.q.size());
+  std::vector<const int64_t*> qk(nq, nullptr);
+  for (const auto& g : e->gq)
+    if (g.partition >= 0 && g.partition < (int)e->routes.size() && e->routes[g.partition] && g.qid >= 0 &&
+        (size_t)g.qid < nq)
+      qk[(size_t)g.qid] = e->routes[g.partition]->key_of_id.p;
+  e->d_qkeys.ensure(nq);
+  HIPCHK(hipMemcpyAsync(e->d_qkeys.p, qk.data(), nq * sizeof(void*), hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+}
+
 // the last push's K_gen / K_seq / K_part records -> table: each record's table words (narrow K_part
 // records expand), scanned, then the rows. bts / seq_base / stream: the push's batch (narrow records
 // take their trigger's ts from it); null for a time advance (timer records only)
@@ -1112,15 +1140,7 @@ void append_gen(sdh_engine* e, const int64_t* bts, int64_t seq_base, int stream)
   HIPCHK(hipMemcpyAsync(&words, e->g_tw.p + n_rec, 8, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   table_reserve(e, n_rec, words);
-  // per query its partition's key table (narrow records carry the key's dense id)
-  const size_t nq = std::max<size_t>(1, e->prog.q.size());
-  std::vector<const int64_t*> qk(nq, nullptr);
-  for (const auto& g : e->gq)
-    if (g.partition >= 0 && g.partition < (int)e->routes.size() && e->routes[g.partition] && g.qid >= 0 &&
-        (size_t)g.qid < nq)
-      qk[(size_t)g.qid] = e->routes[g.partition]->key_of_id.p;
-  e->d_qkeys.ensure(nq);
-  HIPCHK(hipMemcpyAsync(e->d_qkeys.p, qk.data(), nq * sizeof(void*), hipMemcpyHostToDevice, e->stream));
+  upload_qkeys(e);
   HIPCHK(sdh_append_gen(e->g_out.p, e->g_rec_off.p, n_rec, e->seq_ref, e->d_out_rank.p,
                         e->has_fanout ? e->d_fan_rank.p : nullptr, (int)e->prog.stream_types.size(), table_view(e),
                         e->mt.n, e->mt.nw, e->g_tw.p, bts, seq_base, stream, e->d_qkeys.p, e->stream));
@@ -1244,7 +1264,7 @@ bool ratchet_placeable(const sdh_engine* e, int stream, int64_t seq_base, int64_
   return nc > 0 && !(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) && !full && n_events > 0 && !e->ck.active &&
          e->device_matches == 0 && e->g_dev_matches == 0 && (e->mt.n == 0 || e->mt.placed) &&
          (double)n_events * nc < (double)(1 << 30) && seq_base + n_events - e->seq_ref < INT32_MAX &&
-         !getenv("SDH_NO_PLACE");
+         !sdh::knob("SDH_NO_PLACE");
 }
 
 // a placed push joins the window: its rows are already in pc_rows; the compact rows carry seqs
@@ -1451,7 +1471,7 @@ void ratchet_build(sdh_engine* e, std::vector<std::pair<RatchetPlan, int>>& plan
   // lanes: normal mode in receiver-rank order (a wave's lanes are then consecutive ranks, which the
   // direct placement needs: place_cells); SDH_FLAG_DEVICE_MATCHES mode by `within`, so that similar
   // warm-up windows share a wave (SDH_RATCHET_LANES=rank|within overrides)
-  const char* lo = getenv("SDH_RATCHET_LANES");
+  const char* lo = sdh::knob("SDH_RATCHET_LANES");
   const bool by_rank = lo ? strcmp(lo, "rank") == 0 : !(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES);
   const size_t ns = e->prog.stream_types.size();
   auto rank = [&](const std::pair<RatchetPlan, int>& p) { return e->out_rank[(size_t)p.second * ns + p.first.stream]; };
@@ -1555,7 +1575,7 @@ int ratchet_nf(const sdh::RatchetGroup& g) {
 // the SIM form (nfa_ratchet.hip): float keys from a float column, one start atom over that same
 // column compared in the float / double domain against a constant, without negation
 int ratchet_sim(const sdh::RatchetGroup& g) {
-  if (getenv("SDH_RATCHET_NO_SIM")) return 0;
+  if (sdh::knob("SDH_RATCHET_NO_SIM")) return 0;
   if (g.key_kind != sdh::KK_F32 || g.key_conv == sdh::CV_F32_INT || g.key_conv == sdh::CV_F32_LONG || g.n_f0 != 1)
     return 0;
   const sdh::RatchetAtom& A = g.f0[0];
@@ -1569,6 +1589,8 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
   e->r_matches = 0;
   e->r_kernel_ms = 0;
   e->r_kernel_bytes = 0;
+  e->r_rec_bytes = 0;
+  e->r_rec4 = 0;
   std::vector<int> gs;
   for (int g = 0; g < (int)e->rg.size(); ++g)
     if (e->rg[g].stream == stream) gs.push_back(g);
@@ -1576,14 +1598,16 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
   const int64_t n = B.n;
   int64_t lanes = 0;
   for (int g : gs) lanes += e->rg[g].n_lanes;
-  const bool ring = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) != 0;
+  const bool devrec = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) != 0;
   if (e->r_blocks == 0) {
+    // a first guess (at most 8 GiB of blocks): a push that needs more re-runs once with the count of
+    // blocks its waves asked for
     int64_t want = e->cfg.match_capacity > 0 ? e->cfg.match_capacity : std::max<int64_t>(1 << 20, n * lanes * 3 / 4);
-    if (ring) want = std::min<int64_t>(want, (int64_t)1 << 30);  // 8 GiB of 8-B records, rewritten in a ring
+    if (e->cfg.match_capacity <= 0) want = std::min<int64_t>(want, (int64_t)1 << 30);
     e->r_blocks = (want + e->r_blk_recs - 1) / e->r_blk_recs;
   }
-  e->d_rtotal.ensure(2);  // [0] ring-mode records, [1] the placement total
-  bool no_place = false;
+  e->d_rtotal.ensure(3);  // [0] device-record entries, [1] the placement total, [2] device-record bytes
+  bool no_place = false, no_rec4 = false;
   for (int attempt = 0; attempt < 40; ++attempt) {
     // out-of-order timestamps seen on this stream, timestamps so extreme that `ts0 + within`
     // could wrap, or a batch spanning 2^31 - 2 ms or more (the lazy forms' 32-bit deadline domain,
@@ -1598,7 +1622,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     // kernel's occupancy -- of at least min_chunk emitted events each ----
     // (C2 expansion, 64K-event pushes, tools/sweep_minchunk.sh: 2,048 events per chunk at least
     // 3.66 ms per push / 3.56 compact, 1,024 3.42 / 3.43, 512 3.43 / 3.48, 256 3.68 / 3.68)
-    static const int64_t def_chunk = getenv("SDH_RATCHET_MIN_CHUNK") ? atoll(getenv("SDH_RATCHET_MIN_CHUNK")) : 1024;
+    const int64_t def_chunk = sdh::knob("SDH_RATCHET_MIN_CHUNK") ? atoll(sdh::knob("SDH_RATCHET_MIN_CHUNK")) : 1024;
     const int64_t min_chunk = e->cfg.chunk_events > 0 ? e->cfg.chunk_events : def_chunk;
     e->ritems.clear();
     std::vector<int> order(gs);
@@ -1679,7 +1703,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     e->d_err.ensure(5);
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 20, e->stream));
     HIPCHK(hipMemsetAsync(e->d_blk_next.p, 0, 4, e->stream));
-    HIPCHK(hipMemsetAsync(e->d_rtotal.p, 0, 8, e->stream));
+    HIPCHK(hipMemsetAsync(e->d_rtotal.p, 0, 24, e->stream));
     // per-tile x summaries for the warm-up scans (rows of this stream's key specs)
     const int64_t n_tiles = (n + 63) / 64;
     const size_t n_rows = e->r_sum_specs.size();
@@ -1713,14 +1737,14 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     L.match = e->d_rmatch.p;
     L.blk_count = e->d_blk_count.p;
     L.blk_side = e->d_blk_side.p;
-    // ring mode (records written, never read back) takes the 4-B rec4 entries where it can
-    L.rec4 = (ring && !wide && !full && !e->r_no_rec4) ? 1 : 0;
+    // device records take the 4-B rec4 entries where they can
+    L.rec4 = (devrec && !wide && !full && !no_rec4) ? 1 : 0;
     L.blk_group = e->d_blk_group.p;
     L.wide = wide;
     L.blk_next = e->d_blk_next.p;
     L.n_blocks = (int32_t)std::min<int64_t>(e->r_blocks, INT32_MAX);
     L.blk_recs = e->r_blk_recs;
-    L.ring = ring ? 1 : 0;
+    L.dev_records = devrec ? 1 : 0;
     L.rec_total = e->d_rtotal.p;
     L.err = e->d_err.p;
     const int nc = e->place_cells[(size_t)stream];
@@ -1732,6 +1756,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       L.n_cells = nc;
     }
     e->r_placing = false;
+    int any_rec4 = 0;
     // one launch per (key kind, orientation, SIM form)
     auto run = [&](const RatchetLaunch& L0) {
       for (int i0 = 0; i0 < n_items;) {
@@ -1748,6 +1773,8 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
         Ls.spillA = e->d_rspillA.p + (size_t)i0 * e->rSC * WAVE;
         Ls.lds_ts = e->d_rlts.p + (size_t)i0 * e->rML * WAVE;
         Ls.spillB = any64 ? e->d_rspillB.p + (size_t)i0 * e->rSC * WAVE : nullptr;
+        Ls.rec4 = L0.rec4 && sim ? 1 : 0;  // (rec4 blocks come from the SIM form only)
+        any_rec4 |= Ls.rec4;
         HIPCHK(sdh_launch_ratchet(kk, xm, full, nf, full ? 0 : sim, e->rML, e->rSC, &Ls, e->stream));
         i0 = i1;
       }
@@ -1761,7 +1788,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     HIPCHK(hipStreamSynchronize(e->stream));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
-    if (getenv("SDH_TRACE"))
+    if (sdh::knob("SDH_TRACE"))
       fprintf(stderr, "[sdh] ratchet stream %d n %lld attempt %d full %d rec4 %d items %d blocks %d/%lld errs %d %d %d %d %d: %.2f ms\n",
               stream, (long long)n, attempt, (int)full, L.rec4, n_items, used, (long long)e->r_blocks, errs[0], errs[1],
               errs[2], errs[3], errs[4], ms);
@@ -1780,11 +1807,24 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       continue;
     }
     if (errs[2]) {
-      e->r_blocks *= 2;
+      // out of blocks: blk_next ends at the number of blocks the launch's waves asked for (a wave past
+      // the last block writes into the spare one and keeps counting), so one re-run with that many fits
+      const int64_t need = std::max<int64_t>(2 * e->r_blocks, (int64_t)used + used / 64 + 64);
+      const int64_t blk_bytes = (int64_t)e->r_blk_recs * 8 * (wide ? 2 : 1);
+      size_t fr = 0, tot = 0;
+      HIPCHK(hipMemGetInfo(&fr, &tot));
+      const double have = (double)fr + (double)e->d_rmatch.n * 8.0 - (double)(1 << 30);
+      int64_t nb = std::max<int64_t>((int64_t)used + used / 64 + 64, e->r_blocks + 1);
+      if ((double)(need + 1) * blk_bytes <= have) nb = std::max(nb, need);
+      if ((double)(nb + 1) * blk_bytes > have || nb >= INT32_MAX)
+        throw Error(SDH_E_CAPACITY, fmt("the push's match records need %.1f GB of HBM (%.1f GB free): push fewer events "
+                                        "per call", (double)(nb + 1) * blk_bytes / 1e9, have / 1e9));
+      e->r_blocks = nb;
       continue;
     }
     if (errs[4] && L.rec4) {  // a rec4 entry's e1 distance reached 2^26: exact re-run with 8-B records
-      e->r_no_rec4 = true;
+      no_rec4 = true;  // (this push only: the next one tries rec4 again)
+      ++e->r_rec4_reruns;
       continue;
     }
     int64_t placed_rows = 0;
@@ -1826,11 +1866,13 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     if (placing) {
       e->r_blocks_used = 0;
       e->r_matches = placed_rows;
-    } else if (ring) {  // counted, not collected
-      unsigned long long tot = 0;
-      HIPCHK(hipMemcpy(&tot, e->d_rtotal.p, 8, hipMemcpyDeviceToHost));
-      e->r_blocks_used = 0;
-      e->r_matches = (int64_t)tot;
+    } else if (devrec) {  // left on the device for sdh_engine_poll_records: the blocks 0 .. used-1
+      unsigned long long tot[3] = {0, 0, 0};
+      HIPCHK(hipMemcpy(tot, e->d_rtotal.p, 24, hipMemcpyDeviceToHost));
+      e->r_blocks_used = used;
+      e->r_matches = (int64_t)tot[0];
+      e->r_rec_bytes = (double)tot[2];
+      e->r_rec4 = any_rec4;
     } else {
       e->r_blocks_used = std::min<int>(used, (int)e->r_blocks);
       e->r_blk_count.resize(e->r_blocks_used);
@@ -1949,7 +1991,7 @@ KPart kpart_shape(const kg::LProgram& P, int qi, const kg::GQuery& g) {
 // failed compile is an error; default: shapes that fill at least two waves (a compile costs about
 // a second once per process and shape, the interpreted kernel is exact too)
 int spec_mode() {
-  const char* v = getenv("SDH_SPEC");
+  const char* v = sdh::knob("SDH_SPEC");
   if (!v || !*v) return 1;
   if (!strcmp(v, "0")) return 0;
   if (!strcmp(v, "require")) return 3;
@@ -1984,7 +2026,7 @@ void spec_build(sdh_engine* e) {
       // stay in VGPRs across the key's events (C3 instances hold a handful at a time)
       // (C3 at 1000 x 10K keys, or/and entries: 8 26.0 ms/step, 6 25.4, 5 25.1, 4 24.6, 3 24.4, 2 32.8)
       int regs = ps.kind == PK_COUNT ? 3 : 3;
-      if (const char* v = getenv(ps.kind == PK_COUNT ? "SDH_KPART_REGS_COUNT" : "SDH_KPART_REGS")) regs = std::max(0, atoi(v));
+      if (const char* v = sdh::knob(ps.kind == PK_COUNT ? "SDH_KPART_REGS_COUNT" : "SDH_KPART_REGS")) regs = std::max(0, atoi(v));
       sdh::spec::PartLayout lay{ps.kind, ps.sA, ps.sB, ps.cmax, ps.n_e1, ps.n_first, ps.n_last, ps.ew, regs};
       // (C3 ring: 1536 words 20.7 ms/step, 1024 17.5, 768 18.0, 2048 21.8)
       if (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) lay.out_w = 1024;
@@ -2152,7 +2194,7 @@ void slab_grow(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int>& w
     HIPCHK(hipMemcpy(ss.head.p, ss.h_head.data(), ss.nsub * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ss.tail.p, ss.h_tail.data(), ss.nsub * 8, hipMemcpyHostToDevice));
     ss.growths += (int64_t)(b1 - b0);
-    if (getenv("SDH_SLAB_TRACE"))
+    if (sdh::knob("SDH_SLAB_TRACE"))
       fprintf(stderr, "[sdh] slab grow: %zu rings, %.2f GB: alloc %.1f ms, move %.1f ms, free %.1f ms\n", b1 - b0,
               words * 4e-9, t_alloc - t_start, t_move - t_alloc, now_ms() - t_move);
   }
@@ -2197,18 +2239,18 @@ void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int6
     // clean once the room falls below SDH_SLAB_CLEAN_AT x the push's need (then the live blocks of
     // the span still fit at the head: the in-place move needs room for them, and a span holds at most
     // SDH_SLAB_SPAN x need live words)
-    static const double clean_at = getenv("SDH_SLAB_CLEAN_AT") ? atof(getenv("SDH_SLAB_CLEAN_AT")) : 3.0;
+    const double clean_at = sdh::knob("SDH_SLAB_CLEAN_AT") ? atof(sdh::knob("SDH_SLAB_CLEAN_AT")) : 3.0;
     if ((double)(ss.cap[r] - used) >= clean_at * (double)need[r]) continue;
     // the oldest quarter of the ring (at least twice the headroom): mostly dead copies, so the move
     // is small (SDH_SLAB_CLEAN=all: everything before the last push)
     const unsigned long long cur = ss.h_push0[r] > ss.h_tail[r] ? ss.h_push0[r] : ss.h_head[r];
-    static const bool all = getenv("SDH_SLAB_CLEAN") && !strcmp(getenv("SDH_SLAB_CLEAN"), "all");
+    const bool all = sdh::knob("SDH_SLAB_CLEAN") && !strcmp(sdh::knob("SDH_SLAB_CLEAN"), "all");
     // (the span a push needs, not a fixed share of the ring: every live block in it moves, and the
     // oldest blocks of a ring are not all dead -- a quarter of the ring per push moved 15 % of C5's
     // device time. C5 sweep, CLEAN_AT:SPAN:GROW_TO -> slab_move share of the 24-step run, ms/step,
     // reserved/live: 5:4:1.6 10.0 %, 457, 1.80; 3:2:1.6 7.8 %, 458, 1.95; 3:2:1.5 8.8 %, 447, 1.75;
     // 4:3:1.6 9.0 %, 469, 1.96; 5:8:1.6 30 %, 632; 9:8:1.6 42 %, 822; GROW_TO 2.0 at 5:4 5.9 %, 2.13)
-    static const double span_x = getenv("SDH_SLAB_SPAN") ? atof(getenv("SDH_SLAB_SPAN")) : 2.0;
+    const double span_x = sdh::knob("SDH_SLAB_SPAN") ? atof(sdh::knob("SDH_SLAB_SPAN")) : 2.0;
     const unsigned long long span = (unsigned long long)std::max<int64_t>((int64_t)(span_x * need[r]), 4096);
     limit[r] = all ? cur : std::min<unsigned long long>(cur, ss.h_tail[r] + span);
     clean[r] = 1;
@@ -2230,8 +2272,8 @@ void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int6
     // takes its live blocks (slab_grow compacts as it moves; sized from the live words, not the
     // ring's span, which counts dead blocks: sizing from the span doubled the reservation every
     // other C5 step and ran out of HBM)
-    static const double grow_at = getenv("SDH_SLAB_GROW_AT") ? atof(getenv("SDH_SLAB_GROW_AT")) : 1.4;
-    static const double grow_to = getenv("SDH_SLAB_GROW_TO") ? atof(getenv("SDH_SLAB_GROW_TO")) : 1.5;
+    const double grow_at = sdh::knob("SDH_SLAB_GROW_AT") ? atof(sdh::knob("SDH_SLAB_GROW_AT")) : 1.4;
+    const double grow_to = sdh::knob("SDH_SLAB_GROW_TO") ? atof(sdh::knob("SDH_SLAB_GROW_TO")) : 1.5;
     for (int r = 0; r < ss.nsub; ++r) {
       if (!clean[r]) continue;
       const int64_t used = (int64_t)(ss.h_head[r] - ss.h_tail[r]);
@@ -2241,7 +2283,7 @@ void slab_prepare(sdh_engine* e, sdh_engine::SlabSet& ss, const std::vector<int6
       gcap.push_back(std::max<int64_t>(ss.cap[r], (int64_t)(grow_to * base)));
     }
   }
-  if (getenv("SDH_SLAB_TRACE")) {
+  if (sdh::knob("SDH_SLAB_TRACE")) {
     fprintf(stderr, "[sdh] slab prepare: live pass + cleaning %.1f ms\n", now_ms() - t_prep);
     int64_t c = 0, u = 0, nd = 0, g = 0;
     for (int r = 0; r < ss.nsub; ++r) {
@@ -2285,8 +2327,8 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
   std::vector<int> gidx(e->lp.q.size(), -1);
   std::vector<KPart> kpart(e->lp.q.size());
   std::vector<char> is_slab(e->lp.q.size(), 0);
-  const bool use_part = !(e->cfg.flags & SDH_FLAG_FORCE_GEN) && !getenv("SDH_NO_KPART");
-  const bool use_slab = !(e->cfg.flags & SDH_FLAG_FORCE_GEN) && !getenv("SDH_NO_KSLAB");
+  const bool use_part = !(e->cfg.flags & SDH_FLAG_FORCE_GEN) && !sdh::knob("SDH_NO_KPART");
+  const bool use_slab = !(e->cfg.flags & SDH_FLAG_FORCE_GEN) && !sdh::knob("SDH_NO_KSLAB");
   for (int qi : qis) {
     try {
       kg::GQuery g = kg::lower_gen(e->lp, qi, sz);
@@ -2385,7 +2427,7 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
       }
       ps->ew = kind == PK_COUNT ? 3 + ps->cmax + ps->n_e1 + ps->n_first + ps->n_last : 3;
       ps->cap = kind == PK_COUNT ? 8 : 16;
-      if (const char* v = getenv("SDH_KPART_CAP")) ps->cap = std::max(1, atoi(v));
+      if (const char* v = sdh::knob("SDH_KPART_CAP")) ps->cap = std::max(1, atoi(v));
       e->psets.push_back(std::move(ps));
     }
   };
@@ -2432,9 +2474,9 @@ void gen_build(sdh_engine* e, const std::vector<int>& qis) {
     HIPCHK(hipMemcpy(ss->d_group_shape.p, ss->group_shape.data(), ss->n_groups * 4, hipMemcpyHostToDevice));
     ss->d_group_ew.ensure(ss->n_groups);
     HIPCHK(hipMemcpy(ss->d_group_ew.p, ss->group_ew.data(), ss->n_groups * 4, hipMemcpyHostToDevice));
-    if (const char* v = getenv("SDH_SLAB_LDS_WORDS")) ss->lds_words = std::max(64, atoi(v));
+    if (const char* v = sdh::knob("SDH_SLAB_LDS_WORDS")) ss->lds_words = std::max(64, atoi(v));
     int64_t sub = 1 << 16;  // words per sub-ring; grows on demand (slab_prepare)
-    if (const char* v = getenv("SDH_SLAB_SUB_WORDS")) sub = std::max<int64_t>(64, atoll(v));
+    if (const char* v = sdh::knob("SDH_SLAB_SUB_WORDS")) sub = std::max<int64_t>(64, atoll(v));
     slab_init(e, *ss, sub);
     e->ssets.push_back(std::move(ss));
   };
@@ -2803,7 +2845,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
         // items per launch: many short chunks balance the chunks' uneven match density (C4 sweep,
         // tools/sweep_seq.sh: 4,096 items 25.2 ms/step, 8,192 19.8, 16,384 17.2, 32,768 16.2, 65,536
         // 15.8, 131,072 15.5)
-        static const int64_t seq_waves = getenv("SDH_SEQ_WAVES") ? atoll(getenv("SDH_SEQ_WAVES")) : 131072;
+        const int64_t seq_waves = sdh::knob("SDH_SEQ_WAVES") ? atoll(sdh::knob("SDH_SEQ_WAVES")) : 131072;
         const int64_t target = std::max<int64_t>(1, seq_waves / (int64_t)nrows);
         int64_t clen = std::max<int64_t>(256, (starts + target - 1) / target);
         clen = (clen + 63) / 64 * 64;  // whole LDS tiles
@@ -2839,7 +2881,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       int64_t C = 1, clen = n;
       if (look >= 0 && n > 0) {
         int64_t minlen = std::max<int64_t>(256, 8 * look);
-        if (const char* v = getenv("SDH_GEN_CHUNK_LEN")) minlen = std::max<int64_t>(std::max(1, look), atoll(v));
+        if (const char* v = sdh::knob("SDH_GEN_CHUNK_LEN")) minlen = std::max<int64_t>(std::max(1, look), atoll(v));
         const int64_t target = std::max<int64_t>(1, 8192 / (int64_t)gen_groups.size());
         C = std::max<int64_t>(1, std::min<int64_t>((n + minlen - 1) / minlen, target));
         clen = (n + C - 1) / C;
@@ -2893,7 +2935,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
     // an ordered batch takes the indexed sweep (each key walks its own events; its timers fire at the
     // first event whose time reaches them, found by binary search), else every key walks the batch
     auto ordered = [&]() {
-      if (n <= 0 || getenv("SDH_NO_TIMER_INDEX")) return false;
+      if (n <= 0 || sdh::knob("SDH_NO_TIMER_INDEX")) return false;
       e->t_pm.ensure((size_t)n);
       e->t_flag.ensure(1);
       e->t_temp.ensure(sdh_prefix_max_temp_bytes(n));
@@ -3019,7 +3061,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       auto& ps = *e->psets[si];
       if (ps.partition != pi) continue;
       part_grow(e, ps, hv[0]);
-      if (!sorted && !getenv("SDH_KPART_GATHER")) {
+      if (!sorted && !sdh::knob("SDH_KPART_GATHER")) {
         e->sb_buf.ensure(sdh_sorted_batch_bytes(&B));
         HIPCHK(sdh_sort_batch(&B, e->r_idx_s.p, e->sb_buf.p, &SB, e->stream));
         sorted = true;
@@ -3061,9 +3103,9 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       P.rec_cap = e->g_out_cap / NREC_MIN_WORDS + 1;
       P.rec_next = e->g_rec_next.p;
       P.write_records = write ? 1 : 2;
-      if (!write && getenv("SDH_DEBUG_COUNT_ONLY")) P.write_records = 0;  // (measurement experiments)
+      if (!write && sdh::knob("SDH_DEBUG_COUNT_ONLY")) P.write_records = 0;  // (measurement experiments)
       P.err = e->d_perr.p + 4 * si;
-      static const bool prof = getenv("SDH_PART_PROF") != nullptr;
+      const bool prof = sdh::knob("SDH_PART_PROF") != nullptr;
       if (prof) {
         e->d_pprof.ensure(8);
         HIPCHK(hipMemsetAsync(e->d_pprof.p, 0, 8 * 8, e->stream));
@@ -3213,10 +3255,9 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   e->g_rec_next.ensure(1);
   const bool write = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) == 0;
   // the blocks a pass modifies are journaled so that an overflow (match output, K_part tables, K_gen
-  // pools, K_slab space) can be undone and the push re-run exactly at the grown capacity. The
-  // benchmark mode (SDH_FLAG_DEVICE_MATCHES: records wrap in a ring, nothing is polled) skips it
-  // unless K_part / K_slab sets are present; there a K_gen pool overflow fails the push loudly
-  e->g_journal = write || !e->psets.empty() || !e->ssets.empty();
+  // pools, K_slab space) can be undone and the push re-run exactly at the grown capacity, in both
+  // output modes (device records grow like the match table's records: no push drops a match)
+  e->g_journal = true;
   for (auto& up : e->gsets) up->jn = 0;
   for (auto& ss : e->ssets) slab_prepare(e, *ss);
   const size_t nss = e->ssets.size();
@@ -3231,7 +3272,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   std::vector<int32_t> perr(4 * std::max<size_t>(1, nps), 0);
   for (int attempt = 0;; ++attempt) {
     e->g_out.ensure((size_t)e->g_out_cap);
-    e->g_rec_off.ensure((size_t)(e->g_out_cap / NREC_MIN_WORDS + 1));  // a record has at least NREC_MIN_WORDS words (the narrow ones)
+    if (write) e->g_rec_off.ensure((size_t)(e->g_out_cap / NREC_MIN_WORDS + 1));  // a record has at least NREC_MIN_WORDS words (the narrow ones)
     HIPCHK(hipMemsetAsync(e->d_err.p, 0, 16, e->stream));
     HIPCHK(hipMemsetAsync(e->d_perr.p, 0, perr.size() * 4, e->stream));
     HIPCHK(hipMemsetAsync(e->d_serr.p, 0, serr.size() * 4, e->stream));
@@ -3338,7 +3379,7 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
   *bytes_out += (double)nrec * 32.0;  // one (query, ts, seqs) record per match, as for K_ratchet
   e->stats.matches += (int64_t)nrec;
   e->g_dev_matches = (int64_t)nrec;
-  e->g_used = write ? (int64_t)used : 0;
+  e->g_used = (int64_t)used;
 }
 
 // Host-resident batch -> HBM (the StreamJunction -> receiver hand-off of north_star (2)): the
@@ -3416,10 +3457,9 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   // an exact re-run needs the journal of the K_gen blocks the push modifies (gen_journal): a batch
   // whose bound does not fit a third of free HBM is pushed as two halves -- the same events in the
   // same order, so the same matches
-  const bool journaled = (e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) == 0 || !e->psets.empty() || !e->ssets.empty();
-  if (!e->gsets.empty() && journaled && b->n > 1) {
+  if (!e->gsets.empty() && b->n > 1) {
     size_t fr = 0, tot = 0;
-    const char* jb = getenv("SDH_JOURNAL_BUDGET");  // (tests: force the split)
+    const char* jb = sdh::knob("SDH_JOURNAL_BUDGET");  // (tests: force the split)
     if (hipMemGetInfo(&fr, &tot) == hipSuccess && gen_journal_bound(e, b->n) > (jb ? atof(jb) : (double)fr / 3)) {
       std::vector<const void*> c0(na), c1(na);
       std::vector<const uint8_t*> n0(na), n1(na);
@@ -3485,6 +3525,9 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   e->r_matches = 0;
   e->g_dev_matches = 0;
   e->g_used = 0;
+  e->dev_polled = false;
+  e->last_n = b->n;
+  e->last_seq_base = B.seq_base;
   for (auto& k : e->part_kept) k = b->n;
   try {
     if (!qs.empty()) {
@@ -3553,8 +3596,17 @@ int do_push(sdh_engine* e, int32_t stream, const sdh_batch* b) {
   return SDH_OK;
 }
 
+// knobs.h: the knobs of the engine whose ABI call runs on this thread
+thread_local const std::vector<std::pair<std::string, std::string>>* t_knobs = nullptr;
+struct KnobScope {
+  const std::vector<std::pair<std::string, std::string>>* prev;
+  explicit KnobScope(const sdh_engine* e) : prev(t_knobs) { t_knobs = e ? &e->knobs : nullptr; }
+  ~KnobScope() { t_knobs = prev; }
+};
+
 template <class F>
 int guard(sdh_engine* e, F f) {
+  KnobScope ks(e);
   try {
     return f();
   } catch (const Error& ex) {
@@ -3784,11 +3836,15 @@ int do_push_bcast(sdh_engine* e, int32_t stream, const sdh_batch* b, int root) {
   const bool am_root = xch::rank(e->comm) == root;
   int64_t hdr[xch::HDR] = {};
   StreamBatch B{};
+  if (am_root && (!b || stream < 0 || stream >= (int)e->prog.stream_types.size() ||
+                  b->n_cols != (int)e->prog.stream_types[stream].size() || b->n < 0)) {
+    // an invalid batch still takes part in the collective, as an error header: every rank then fails
+    // this call with SDH_E_INVALID (no rank waits on a broadcast the root never makes)
+    hdr[0] = -1;
+    xcall([&] { xch::bcast_hdr(e->comm, hdr, root, e->stream); });
+    throw Error(SDH_E_INVALID, "bad stream or batch");
+  }
   if (am_root) {
-    if (!b || stream < 0 || stream >= (int)e->prog.stream_types.size() ||
-        b->n_cols != (int)e->prog.stream_types[stream].size() || b->n < 0)
-      throw Error(SDH_E_INVALID, "bad stream or batch");  // (before the collective: every rank then fails
-                                                           //  its own call or waits for the next batch)
     const int na = b->n_cols;
     B.n = b->n;
     B.n_attr = na;
@@ -3812,6 +3868,7 @@ int do_push_bcast(sdh_engine* e, int32_t stream, const sdh_batch* b, int root) {
   }
   xcall([&] { xch::bcast_hdr(e->comm, hdr, root, e->stream); });
   const int64_t n = hdr[0];
+  if (n < 0) throw Error(SDH_E_INVALID, "sdh_engine_push_bcast: the root's batch was invalid (bad stream or batch)");
   stream = (int32_t)hdr[1];
   if (stream < 0 || stream >= (int)e->prog.stream_types.size()) throw Error(SDH_E_INVALID, "broadcast: bad stream");
   const auto& types = e->prog.stream_types[stream];
@@ -3870,12 +3927,21 @@ int do_gather(sdh_engine* e, sdh_matches* out, bool host) {
   int64_t hdr[xch::HDR] = {n, tw, e->seq_ref, kw, e->seq, 0, 0, 0};
   std::vector<int64_t> all((size_t)W * xch::HDR);
   xcall([&] { xch::gather_hdr(e->comm, hdr, all.data(), e->stream); });
+  const bool local = xch::is_local(e->comm);
+  // the poll windows must agree (same pushes since the last gather): with RCCL every rank holds every
+  // header and refuses a mismatch before any rank clears its table or sends; the local
+  // communicator's rank 0 checks before it clears its own
+  for (int r = 0; r < W && (!local || me == 0); ++r) {
+    const int64_t* h = all.data() + (size_t)r * xch::HDR;
+    if (h[2] != hdr[2] || h[3] != kw || h[4] != hdr[4])
+      throw Error(SDH_E_INVALID, fmt("sdh_engine_gather: rank %d's poll window differs from rank %d's (pushes out of step)", r, me));
+  }
+  const std::vector<xch::Buf> mine = {
+      {e->po_q.p, nullptr, (size_t)n * 8},    {e->po_key.p, nullptr, (size_t)n * 8},
+      {e->po_ts.p, nullptr, (size_t)n * 8},   {e->po_seq.p, nullptr, (size_t)n * 8},
+      {e->po_tb.p, nullptr, (size_t)n * 8},   {e->po_off.p, nullptr, (size_t)(n + 1) * 8},
+      {e->po_words.p, nullptr, (size_t)tw * 8}, {e->x_keys.p, nullptr, (size_t)n * kw * 8}};
   if (me != 0) {
-    const std::vector<xch::Buf> mine = {
-        {e->po_q.p, nullptr, (size_t)n * 8},    {e->po_key.p, nullptr, (size_t)n * 8},
-        {e->po_ts.p, nullptr, (size_t)n * 8},   {e->po_seq.p, nullptr, (size_t)n * 8},
-        {e->po_tb.p, nullptr, (size_t)n * 8},   {e->po_off.p, nullptr, (size_t)(n + 1) * 8},
-        {e->po_words.p, nullptr, (size_t)tw * 8}, {e->x_keys.p, nullptr, (size_t)n * kw * 8}};
     xcall([&] { xch::gather_bufs(e->comm, mine, {}, e->stream); });
     HIPCHK(hipStreamSynchronize(e->stream));  // (the sends drained before the buffers change)
     table_clear(e);
@@ -3911,20 +3977,18 @@ int do_gather(sdh_engine* e, sdh_matches* out, bool host) {
                        {nullptr, e->xg_words.p + wbase[(size_t)r], (size_t)wr * 8},
                        {nullptr, e->xg_keys.p + o * kw, (size_t)nr * kw * 8}};
   }
-  // rank 0's own run
-  const std::vector<const void*> own = {e->po_q.p, e->po_key.p, e->po_ts.p, e->po_seq.p,
-                                        e->po_tb.p, e->po_off.p, e->po_words.p, e->x_keys.p};
-  for (size_t i = 0; i < own.size(); ++i)
-    if (recv[0][i].bytes)
-      HIPCHK(hipMemcpyAsync(recv[0][i].dst, own[i], recv[0][i].bytes, hipMemcpyDeviceToDevice, e->stream));
-  xcall([&] { xch::gather_bufs(e->comm, {}, recv, e->stream); });
+  if (local) {  // rank 0's own run (RCCL: a self send / receive inside the gather)
+    for (size_t i = 0; i < mine.size(); ++i)
+      if (recv[0][i].bytes)
+        HIPCHK(hipMemcpyAsync(recv[0][i].dst, mine[i].src, recv[0][i].bytes, hipMemcpyDeviceToDevice, e->stream));
+    std::vector<std::vector<xch::Buf>> others(recv);
+    others[0].clear();
+    xcall([&] { xch::gather_bufs(e->comm, {}, others, e->stream); });
+  } else {
+    xcall([&] { xch::gather_bufs(e->comm, mine, recv, e->stream); });
+  }
   HIPCHK(hipStreamSynchronize(e->stream));
   table_clear(e);
-  for (int r = 1; r < W; ++r) {  // (checked once every run has been received: no rank waits on a failed root)
-    const int64_t* h = all.data() + (size_t)r * xch::HDR;
-    if (h[2] != hdr[2] || h[3] != kw || h[4] != hdr[4])
-      throw Error(SDH_E_INVALID, fmt("sdh_engine_gather: rank %d's poll window differs from rank 0's (pushes out of step)", r));
-  }
   e->go_q.ensure(rows);
   e->go_key.ensure(rows);
   e->go_ts.ensure(rows);
@@ -3986,6 +4050,9 @@ void time_advance(sdh_engine* e, int64_t t) {
   e->r_placing = false;  // (the digest then reads no stale placed rows)
   e->g_dev_matches = 0;
   e->g_used = 0;
+  e->dev_polled = false;
+  e->last_n = 0;
+  e->last_seq_base = e->seq;
   double ms = 0, bytes = 0;
   e->advance_to = t;
   try {
@@ -4116,6 +4183,21 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
   sdh_engine* e = new sdh_engine;
   int rc = guard(e, [&]() {
     if (cfg) e->cfg = *cfg;
+    // sdh_config.debug: "NAME=VALUE;..." knobs (knobs.h), copied: the caller's string need not outlive
+    // the call
+    if (e->cfg.debug) {
+      const std::string d(e->cfg.debug);
+      size_t i = 0;
+      while (i < d.size()) {
+        size_t j = d.find(';', i);
+        if (j == std::string::npos) j = d.size();
+        const std::string kv = d.substr(i, j - i);
+        const size_t eq = kv.find('=');
+        if (!kv.empty()) e->knobs.emplace_back(kv.substr(0, eq), eq == std::string::npos ? "1" : kv.substr(eq + 1));
+        i = j + 1;
+      }
+      e->cfg.debug = nullptr;
+    }
     if (e->cfg.shard_world <= 0) e->cfg.shard_world = 1;
     e->dev = e->cfg.device;
     // the program is validated before any device call (a malformed blob is SDH_E_INVALID with or
@@ -4135,10 +4217,10 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
     HIPCHK(hipSetDevice(e->dev));
     HIPCHK(hipDeviceGetAttribute(&e->n_cu, hipDeviceAttributeMultiprocessorCount, e->dev));
     // tuning overrides for kernel experiments: K_ratchet LDS ring depth and waves per launch
-    if (const char* v = getenv("SDH_RATCHET_ML")) e->rML = std::max(4, atoi(v));
-    if (const char* v = getenv("SDH_RATCHET_WAVES")) e->r_waves = atof(v);
-    if (const char* v = getenv("SDH_XCD")) e->xcd = atoi(v) != 0;
-    if (const char* v = getenv("SDH_SLAB_LDS_SMALL")) e->slab_lds_small = std::max(64, atoi(v));
+    if (const char* v = sdh::knob("SDH_RATCHET_ML")) e->rML = std::max(4, atoi(v));
+    if (const char* v = sdh::knob("SDH_RATCHET_WAVES")) e->r_waves = atof(v);
+    if (const char* v = sdh::knob("SDH_XCD")) e->xcd = atoi(v) != 0;
+    if (const char* v = sdh::knob("SDH_SLAB_LDS_SMALL")) e->slab_lds_small = std::max(64, atoi(v));
     e->out_rank = kg::output_ranks(e->lp);
     // plan selection per query: K_ratchet (2-state threshold ratchet) > K_chain (stream-state
     // chains) > K_gen (everything else: count, logical, sequences, partitions, general predicates)
@@ -4381,7 +4463,8 @@ int sdh_engine_advance_time(sdh_engine* e, int64_t t) {
 
 int sdh_engine_pending_matches(sdh_engine* e, int64_t* n) {
   if (!e || !n) return SDH_E_INVALID;
-  *n = e->mt.n + ((e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) ? e->device_matches + e->r_matches + e->g_dev_matches : 0);
+  *n = e->mt.n + ((e->cfg.flags & SDH_FLAG_DEVICE_MATCHES) && !e->dev_polled
+                       ? e->device_matches + e->r_matches + e->g_dev_matches : 0);
   return SDH_OK;
 }
 
@@ -4455,8 +4538,6 @@ int sdh_engine_debug_digest(sdh_engine* e, uint64_t* out) {
   if (!e || !out) return SDH_E_INVALID;
   return guard(e, [&]() {
     out[0] = out[1] = 0;
-    if (e->r_blk_taken > e->r_blocks)
-      throw Error(SDH_E_CAPACITY, "the last push's device-match records wrapped their ring");
     DevBuf<unsigned long long> acc;
     acc.ensure(2);
     HIPCHK(hipMemsetAsync(acc.p, 0, 16, e->stream));
@@ -4466,6 +4547,83 @@ int sdh_engine_debug_digest(sdh_engine* e, uint64_t* out) {
       HIPCHK(sdh_digest_ratchet(e->d_rmatch.p, e->r_blk_recs, e->r_wide, e->d_blk_count.p, e->d_blk_group.p,
                                 e->d_blk_side.p, e->d_rg.p, e->r_seq_base, (int)e->r_blk_taken, acc.p, e->stream));
     d2h_sync(e, out, acc.p, 16);
+    return SDH_OK;
+  });
+}
+
+// The last push's device records (SDH_FLAG_DEVICE_MATCHES; formats: include/siddhi_hip.h sdh_records)
+int sdh_engine_poll_records(sdh_engine* e, sdh_records* out) {
+  if (!e || !out) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    check_usable(e);
+    *out = sdh_records{};
+    if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES))
+      throw Error(SDH_E_INVALID, "sdh_engine_poll_records needs SDH_FLAG_DEVICE_MATCHES (use sdh_engine_poll)");
+    out->seq_base = e->last_seq_base;
+    out->n_events = e->last_n;
+    if (e->r_blocks_used > 0 && !e->r_placing) {
+      if (e->d_rlane_q.n < e->rg.size() * WAVE) {
+        std::vector<int32_t> lq(e->rg.size() * WAVE, -1);
+        for (size_t g = 0; g < e->rg.size(); ++g)
+          for (int l = 0; l < e->rg[g].n_lanes; ++l) lq[g * WAVE + l] = e->rg[g].qid[l];
+        e->d_rlane_q.ensure(lq.size());
+        HIPCHK(hipMemcpy(e->d_rlane_q.p, lq.data(), lq.size() * 4, hipMemcpyHostToDevice));
+      }
+      out->r_n = e->r_matches;
+      out->r_blocks = e->r_blocks_used;
+      out->r_bytes = (int64_t)e->r_rec_bytes;
+      out->r_base = e->d_rmatch.p;
+      out->r_count = e->d_blk_count.p;
+      out->r_side = e->d_blk_side.p;
+      out->r_group = e->d_blk_group.p;
+      out->r_lane_query = e->d_rlane_q.p;
+      out->r_format = e->r_rec4 ? SDH_REC_4 : e->r_wide ? SDH_REC_16 : SDH_REC_8;
+      out->r_blk_bytes = e->r_blk_recs * 8 * (e->r_wide ? 2 : 1);
+    }
+    if (e->g_dev_matches > 0) {
+      upload_qkeys(e);
+      out->f_n = e->g_dev_matches;
+      out->f_words = e->g_used;
+      out->f_base = e->g_out.p;
+      out->f_query_keys = e->d_qkeys.p;
+    }
+    if (e->device_matches > 0) {
+      const int64_t ni = (int64_t)e->work.size();
+      std::vector<int64_t> so(ni);
+      for (int64_t i = 0; i < ni; ++i) so[i] = e->work[i].seg_off;
+      e->d_seg_off.ensure(ni);
+      HIPCHK(hipMemcpy(e->d_seg_off.p, so.data(), ni * 8, hipMemcpyHostToDevice));
+      out->c_n = e->device_matches;
+      out->c_items = ni;
+      out->c_words = e->rec_words;
+      out->c_base = e->d_match.p;
+      out->c_off = e->d_seg_off.p;
+      out->c_count = e->d_seg_count.p;
+    }
+    out->n = out->r_n + out->f_n + out->c_n;
+    e->dev_polled = true;
+    return SDH_OK;
+  });
+}
+
+int sdh_engine_records_compact(sdh_engine* e, int32_t* rows, int64_t cap, int32_t width, int64_t* n) {
+  if (!e || !n || width < 4) return SDH_E_INVALID;
+  return guard(e, [&]() {
+    check_usable(e);
+    *n = 0;
+    if (!(e->cfg.flags & SDH_FLAG_DEVICE_MATCHES))
+      throw Error(SDH_E_INVALID, "sdh_engine_records_compact needs SDH_FLAG_DEVICE_MATCHES");
+    const int nb = e->r_placing ? 0 : e->r_blocks_used;
+    if (nb <= 0) return SDH_OK;
+    *n = e->r_matches;
+    if (!rows) return SDH_OK;
+    if (cap < e->r_matches) throw Error(SDH_E_CAPACITY, fmt("%lld rows need room for %lld", (long long)cap, (long long)e->r_matches));
+    e->d_rrow_off.ensure((size_t)nb + 1);
+    e->d_rrow_tmp.ensure(sdh_ratchet_compact_temp(nb));
+    HIPCHK(sdh_ratchet_compact(e->d_rmatch.p, e->r_blk_recs, e->r_wide, e->d_blk_count.p, e->d_blk_group.p,
+                               e->d_blk_side.p, e->d_rg.p, e->r_seq_base, nb, e->d_rrow_off.p, e->d_rrow_tmp.p,
+                               e->d_rrow_tmp.n, width, rows, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     return SDH_OK;
   });
 }
@@ -4896,3 +5054,11 @@ void sdh_engine_destroy(sdh_engine* e) {
 const char* sdh_last_error(sdh_engine* e) { return e ? e->err.c_str() : g_create_error.c_str(); }
 
 }  // extern "C"
+
+// knobs.h (t_knobs: the engine whose ABI call runs on this thread)
+const char* sdh::knob(const char* name) {
+  if (!t_knobs) return nullptr;
+  for (const auto& kv : *t_knobs)
+    if (kv.first == name) return kv.second.c_str();
+  return nullptr;
+}

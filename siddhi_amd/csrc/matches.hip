@@ -65,10 +65,41 @@ __global__ __launch_bounds__(256) void append_ratchet_kernel(
   }
 }
 
+// One K_ratchet record of block b (nfa_types.h RatchetLaunch; include/siddhi_hip.h sdh_records):
+// its e2 batch offset, lane and the low 32 bits of e1's seq. ns >= 0: a rec4 block of ns side entries
+// (entry i's event is the last side entry whose first index is <= i; side entry j sits at byte
+// blk_recs * 8 - 8 * (j + 1)).
+__device__ __forceinline__ void ratchet_record(const int64_t* match, int blk_recs, int wide, int b, int ns, int i,
+                                               uint32_t sb32, uint32_t& off, uint32_t& ln, uint32_t& q1) {
+  const char* B = reinterpret_cast<const char*>(match) + ((size_t)b * blk_recs * 8 << (wide ? 1 : 0));
+  if (ns >= 0) {
+    const uint32_t* E = reinterpret_cast<const uint32_t*>(B);
+    const uint2* S = reinterpret_cast<const uint2*>(B + (size_t)blk_recs * 8);  // S[-1 - j] = side entry j
+    int lo = 0, hi = ns - 1;  // side entry 0's first index is 0 <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((int)S[-1 - mid].x <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    off = S[-1 - lo].y;
+    ln = E[i] >> 26;
+    q1 = (sb32 + off) - (E[i] & ((1u << 26) - 1));
+  } else if (!wide) {
+    const uint2 r = reinterpret_cast<const uint2*>(B)[i];
+    off = r.x & ((1u << 26) - 1);
+    ln = r.x >> 26;
+    q1 = r.y;
+  } else {
+    const uint4 r = reinterpret_cast<const uint4*>(B)[i];
+    off = r.x;
+    ln = r.y & 63;
+    q1 = r.z;
+  }
+}
+
 // Order-independent digest of the K_ratchet records of the last launch (both output modes write the
-// same per-wave blocks; SDH_FLAG_DEVICE_MATCHES lets the block index wrap): per record
-// mix64(e2 seq, query, e1 seq) summed mod 2^64, and the record count. Test diagnostics
-// (sdh_engine_debug_digest): normal and device-match modes must write the same records.
+// same per-wave blocks): per record mix64(e2 seq, query, e1 seq) summed mod 2^64, and the record count.
+// Test diagnostics (sdh_engine_debug_digest): normal and device-record modes must write the same records.
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -84,34 +115,10 @@ __global__ __launch_bounds__(256) void digest_ratchet_kernel(const int64_t* __re
   const int n = blk_count[b];
   const int ns = blk_side[b];  // >= 0: a rec4 block (nfa_types.h RatchetLaunch::rec4)
   const RatchetGroup* G = groups + blk_group[b];
-  const uint2* R = reinterpret_cast<const uint2*>(match) + ((size_t)b * blk_recs << (wide ? 1 : 0));
   unsigned long long h = 0, c = 0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     uint32_t off, ln, q1;
-    if (ns >= 0) {
-      // entry i: {distance | lane << 26}; its event: the last side entry whose first index is <= i
-      const uint32_t* E = reinterpret_cast<const uint32_t*>(R);
-      const uint2* S = reinterpret_cast<const uint2*>(E + blk_recs);
-      int lo = 0, hi = ns - 1;  // S[0].x == 0 <= i
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((int)S[mid].x <= i) lo = mid;
-        else hi = mid - 1;
-      }
-      off = S[lo].y;
-      ln = E[i] >> 26;
-      q1 = ((uint32_t)seq_base + off) - (E[i] & ((1u << 26) - 1));
-    } else if (!wide) {
-      const uint2 r = R[i];
-      off = r.x & ((1u << 26) - 1);
-      ln = r.x >> 26;
-      q1 = r.y;
-    } else {
-      const uint4 r = reinterpret_cast<const uint4*>(R)[i];
-      off = r.x;
-      ln = r.y & 63;
-      q1 = r.z;
-    }
+    ratchet_record(match, blk_recs, wide, b, ns, i, (uint32_t)seq_base, off, ln, q1);
     const int64_t s = seq_base + (int64_t)off;
     const int64_t s1 = s - (int64_t)(uint32_t)((uint32_t)s - q1);
     h += mix64(mix64((uint64_t)s * 0x9E3779B97F4A7C15ull ^ (uint64_t)G->qid[ln]) ^ (uint64_t)s1);
@@ -124,6 +131,38 @@ __global__ __launch_bounds__(256) void digest_ratchet_kernel(const int64_t* __re
   if ((threadIdx.x & 63) == 0 && c) {
     atomicAdd(&acc[0], c);
     atomicAdd(&acc[1], h);
+  }
+}
+
+// Device records -> compact rows (sdh_engine_records_compact): block b's records at rows
+// row_off[b] .. row_off[b] + blk_count[b] (an exclusive scan of blk_count), each
+// {query, e2 - seq_base, e2 - e1, 0, INT32_MIN...} of `width` int32 (the sdh_matches_compact form)
+__global__ __launch_bounds__(256) void ratchet_compact_kernel(const int64_t* __restrict__ match, int blk_recs, int wide,
+                                                              const int32_t* __restrict__ blk_count,
+                                                              const int32_t* __restrict__ blk_group,
+                                                              const int32_t* __restrict__ blk_side,
+                                                              const RatchetGroup* __restrict__ groups,
+                                                              const int64_t* __restrict__ row_off, int64_t seq_base,
+                                                              int width, int32_t* __restrict__ rows) {
+  const int b = blockIdx.x;
+  const int n = blk_count[b];
+  const int ns = blk_side[b];
+  const RatchetGroup* G = groups + blk_group[b];
+  const int64_t r0 = row_off[b];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t off, ln, q1;
+    ratchet_record(match, blk_recs, wide, b, ns, i, (uint32_t)seq_base, off, ln, q1);
+    int32_t* o = rows + (r0 + i) * width;
+    const int32_t d = (int32_t)((uint32_t)(seq_base + off) - q1);
+    if (width == 4) {
+      *reinterpret_cast<int4*>(o) = make_int4(G->qid[ln], (int32_t)off, d, 0);
+    } else {
+      o[0] = G->qid[ln];
+      o[1] = (int32_t)off;
+      o[2] = d;
+      o[3] = 0;
+      for (int j = 4; j < width; ++j) o[j] = INT32_MIN;
+    }
   }
 }
 
@@ -525,6 +564,34 @@ extern "C" hipError_t sdh_digest_ratchet(const int64_t* match, int blk_recs, int
   if (n_blocks <= 0) return hipSuccess;
   hipLaunchKernelGGL(sdh::digest_ratchet_kernel, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, wide, blk_count,
                      blk_group, blk_side, groups, seq_base, acc);
+  return hipGetLastError();
+}
+
+// device records -> compact rows: the blocks' record counts widened and scanned into row offsets
+// (row_off: n_blocks + 1 int64, the total last), then one workgroup per block
+__global__ void widen_counts_kernel(const int32_t* __restrict__ c, int64_t n, int64_t* __restrict__ o) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= n) o[i] = i < n ? (int64_t)c[i] : 0;
+}
+extern "C" size_t sdh_ratchet_compact_temp(int64_t n_blocks) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum((void*)nullptr, b, (int64_t*)nullptr, (int64_t*)nullptr, (int)(n_blocks + 1));
+  return b;
+}
+extern "C" hipError_t sdh_ratchet_compact(const int64_t* match, int blk_recs, int wide, const int32_t* blk_count,
+                                          const int32_t* blk_group, const int32_t* blk_side,
+                                          const sdh::RatchetGroup* groups, int64_t seq_base, int n_blocks,
+                                          int64_t* row_off, void* temp, size_t temp_bytes, int width, int32_t* rows,
+                                          hipStream_t s) {
+  if (n_blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(widen_counts_kernel, dim3(sdh::grid(n_blocks + 1, 256)), dim3(256), 0, s, blk_count,
+                     (int64_t)n_blocks, row_off);
+  size_t tb = temp_bytes;
+  hipError_t r = hipcub::DeviceScan::ExclusiveSum(temp, tb, row_off, row_off, n_blocks + 1, s);
+  if (r != hipSuccess) return r;
+  if (rows)
+    hipLaunchKernelGGL(sdh::ratchet_compact_kernel, dim3(n_blocks), dim3(256), 0, s, match, blk_recs, wide, blk_count,
+                       blk_group, blk_side, groups, row_off, seq_base, width, rows);
   return hipGetLastError();
 }
 

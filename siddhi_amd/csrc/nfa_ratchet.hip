@@ -802,7 +802,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
   // output block state: fill >= FULL_FILL forces the block check, which also catches a full output
   constexpr int FULL_FILL = 1 << 30;
   int blk = -1, fill = FULL_FILL;
-  unsigned long long n_emit = 0;  // records of this wave's closed blocks (ring mode: the blocks wrap)
+  unsigned long long n_emit = 0;  // records of this wave's closed blocks
+  unsigned long long n_bytes = 0;  // bytes of this wave's closed blocks' records (+ PM 4 side entries)
   // the wave's current output block as a buffer resource: a record's address is a 32-bit lane offset
   // from the block base (no 64-bit address arithmetic per record), and the range check covers it
   __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(L.match, 0, 0, 0x00020000);
@@ -834,8 +835,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
     }
   };
   // record width: compile-time in the chunked forms (PM 3 = 16-B records), read at run time in FULL.
-  // PM 4 (ring mode, nfa_types.h rec4): 4-B entries {e1 distance | lane << 26} and one side entry
-  // {first entry, e2 offset} per matching event in the block's upper half
+  // PM 4 (device records, nfa_types.h rec4): 4-B entries {e1 distance | lane << 26} from the block's
+  // start and one side entry {first entry, e2 offset} per matching event from its end downwards
   const bool wide = FULL ? L.wide != 0 : PM == 3;
   int sfill = 0;                              // PM 4: side entries in the current block
   bool new_blk = false;                       // PM 4: a block was taken since the last side entry
@@ -851,13 +852,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
         L.blk_side[blk] = PM == 4 ? sfill : -1;
       }
       n_emit += (unsigned long long)fill;
+      n_bytes += PM == 4 ? (unsigned long long)fill * 4 + (unsigned long long)sfill * 8
+                         : (unsigned long long)fill * (wide ? 16 : 8);
     }
     sfill = 0;
     new_blk = true;  // (an event whose matches continue in this block needs a side entry here too)
     int nb = 0;
     if (lane == 0) nb = atomicAdd(L.blk_next, 1);
     nb = __builtin_amdgcn_readfirstlane(nb);
-    if (L.ring) nb = (int)((uint32_t)nb % (uint32_t)L.n_blocks);
     if (nb >= L.n_blocks) {
       mover = 1;
       blk = -1;
@@ -876,8 +878,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
   auto emit_room = [&]() {
     if constexpr (PM == 0 || PM == 3)
       if (fill > L.blk_recs - 4 * WAVE) roll();
-    if constexpr (PM == 4)
-      if (fill > L.blk_recs - 4 * WAVE || sfill >= (L.blk_recs >> 1)) roll();
+    if constexpr (PM == 4)  // room for a round's 4 x 64 entries and one side entry between the two ends
+      if (fill > ((L.blk_recs * 8 - 4 * WAVE * 4 - 8 - sfill * 8) >> 2)) roll();  // (fill starts at FULL_FILL)
   };
   auto emit = [&](bool mt, uint64_t m, uint32_t off, uint32_t q1) {
     if constexpr (PM == 1) {
@@ -997,7 +999,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
             new_blk = false;
             if (lane == 0) {
               const u32x2 se = {(uint32_t)fill, (uint32_t)(t + k)};
-              __builtin_amdgcn_raw_buffer_store_b64(se, wrs, L.blk_recs * 4 + sfill * 8, 0, 0);
+              __builtin_amdgcn_raw_buffer_store_b64(se, wrs, L.blk_recs * 8 - (sfill + 1) * 8, 0, 0);
             }
             ++sfill;
           }
@@ -1129,11 +1131,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SIM ? 8 : 7)
       L.blk_side[blk] = PM == 4 ? sfill : -1;
     }
     n_emit += (unsigned long long)fill;
+    n_bytes += PM == 4 ? (unsigned long long)fill * 4 + (unsigned long long)sfill * 8
+                       : (unsigned long long)fill * (wide ? 16 : 8);
   }
   const uint64_t any_over = wballot(overflow != 0), any_unord = wballot(unordered != 0), any_aged = wballot(aged != 0);
   const uint64_t d4 = wballot(d4over != 0);
   if (lane == 0) {
-    if (L.ring && n_emit) atomicAdd(L.rec_total, n_emit);
+    if (L.dev_records && n_emit) atomicAdd(L.rec_total, n_emit);
+    if (L.dev_records && n_bytes) atomicAdd(L.rec_total + 2, n_bytes);
     if (any_over) atomicOr(&L.err[0], 1);
     if (any_unord) atomicOr(&L.err[1], 1);
     if (mover) atomicOr(&L.err[2], 1);

@@ -24,6 +24,7 @@
 
 #include <cstdlib>
 
+#include "knobs.h"
 #include "dev_common.h"
 #include "slab.h"
 
@@ -468,7 +469,7 @@ extern "C" hipError_t sdh_launch_slab(const sdh::SlabLaunch* L, hipStream_t s) {
   const size_t lds = (size_t)L->lds_words * 4;
   const unsigned grid = (unsigned)(L->xcd ? (L->n_items + 7) & ~7 : L->n_items);
   // waves per SIMD the register allocation aims at (SDH_SLAB_WPE; LDS allows ~4 at the small tier)
-  static const int wpe = getenv("SDH_SLAB_WPE") ? atoi(getenv("SDH_SLAB_WPE")) : 4;
+  const int wpe = sdh::knob("SDH_SLAB_WPE") ? atoi(sdh::knob("SDH_SLAB_WPE")) : 4;
   if (L->max_na <= 4) {
     if (wpe >= 6) hipLaunchKernelGGL((sdh::nfa_slab_kernel<4, 6>), dim3(grid), dim3(64), lds, s, *L);
     else if (wpe == 5) hipLaunchKernelGGL((sdh::nfa_slab_kernel<4, 5>), dim3(grid), dim3(64), lds, s, *L);

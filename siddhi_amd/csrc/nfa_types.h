@@ -198,23 +198,26 @@ struct RatchetLaunch {
   int64_t* lds_ts;              // [item][ML][64] ts0 of the LDS ring entries
   uint4* spillA;                // [item][SC][64] deque entries beyond the LDS ring
   uint32_t* spillB;             //   (seq words of 64-bit-key entries)
-  // match records, in per-wave blocks of blk_recs records. Narrow (wide == 0, batches of at most
-  // 2^26 events): 8 B {e2 batch offset | lane << 26, low 32 bits of e1's seq}; wide: 16 B
-  // {e2 batch offset, lane, low 32 bits of e1's seq, pop level (placement) or 0}. The block's group is blk_group[block];
-  // sdh_launch_ratchet_decode expands records to (qid, ts, seq1, seq2)
+  // match records, in per-wave blocks of blk_recs * 8 bytes (16 B per record when wide; the block's
+  // group is blk_group[block], its record count blk_count[block]; include/siddhi_hip.h sdh_records
+  // documents the formats for consumers). Narrow (wide == 0, batches of at most 2^26 events): 8 B
+  // {e2 batch offset | lane << 26, low 32 bits of e1's seq}; wide: 16 B {e2 batch offset, lane, low
+  // 32 bits of e1's seq, pop level (placement) or 0}. A wave takes its blocks with an atomic on
+  // blk_next; past n_blocks it writes into the spare block, sets err[2], and the host re-runs the push
+  // with blk_next's final count of blocks (blocks never wrap)
   int64_t* match;
   int32_t* blk_count;           // records written per block
   int32_t* blk_group;           // group of the wave that owns the block
   int32_t* blk_next;            // [0] next free block
   int32_t n_blocks, blk_recs;
   int32_t wide;
-  int32_t ring;                 // SDH_FLAG_DEVICE_MATCHES: blocks wrap modulo n_blocks (every record is
-                                //   written, none is read back); rec_total counts them
-  // rec4 (ring mode, SIM form, batches of at most 2^26 events): 4-B entries {e1 distance back from e2
-  // (< 2^26) | lane << 26} in the block's first blk_recs * 4 bytes, and per matching event one side
-  // entry {index of the event's first entry, e2 batch offset} (uint2) from byte blk_recs * 4 on, at
-  // most blk_recs / 2 of them (blk_side[block] counts them). A distance >= 2^26 sets err[4]; the
-  // host then re-runs with 8-B records
+  int32_t dev_records;          // SDH_FLAG_DEVICE_MATCHES: records stay on the device for a consumer
+                                //   (sdh_engine_poll_records); rec_total[0] counts them, [2] their bytes
+  // rec4 (device records, SIM form, batches of at most 2^26 events): 4-B entries {e1 distance back
+  // from e2 (< 2^26) | lane << 26} from the block's start, and per matching event one side entry
+  // {index of the event's first entry, e2 batch offset} (uint2) from the block's end downwards (side
+  // entry j at byte blk_recs * 8 - 8 * (j + 1); blk_side[block] counts them). A distance >= 2^26
+  // sets err[4]; the host then re-runs with 8-B records
   int32_t rec4;
   int32_t* blk_side;
   unsigned long long* rec_total;
@@ -240,8 +243,7 @@ namespace kg {
 struct GQuery;
 }
 
-// ring mode (SDH_FLAG_DEVICE_MATCHES) writes a record at its offset modulo (out_cap - margin): the
-// host keeps out_cap > margin and every record (7 + S + pool nodes words) shorter than it
+// the longest K_gen match record (7 + S + pool nodes words); the flat record buffer is at least twice it
 constexpr int64_t GEN_RING_MARGIN = 8192;
 
 struct GenLaunch {

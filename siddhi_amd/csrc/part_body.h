@@ -307,7 +307,11 @@ __device__ __forceinline__ void part_body(const PartLaunch& L) {
     // one partial per lane and call (collective: the call's record emit): the lane's entry kk held
     // before the tile (kk >= 0), or the one event tc opens (kk < 0); has: the lane has it
     auto run = [&](bool has, int kk, int tc) {
-      if (has && wpos >= L.cap) {  // no slot for it: the push re-runs exactly with a larger table
+      // no slot for it: the push re-runs exactly with a larger table. (The entry-major walk counts the
+      // partials that survive the tile, not those alive at the event that opened this one -- the
+      // event-major rule's count -- so the re-run can fire on a different push than it once did;
+      // the matches are the same either way, test_kpart_table_growth_reruns_exactly)
+      if (has && wpos >= L.cap) {
         cap_over = true;
         has = false;
       }

@@ -1,4 +1,5 @@
 // spec.hip -- shape-compiled kernels: source generation and run-time compilation (see spec.h).
+#include "knobs.h"
 #include "spec.h"
 
 #include "nfa_types.h"
@@ -33,13 +34,13 @@ std::string fmt(const char* f, ...) {
 
 // tuning macros the generated kernels see (SDH_RING_CHUNK: ring-mode output reservations)
 std::string tuning_defines() {
-  const char* v = getenv("SDH_RING_CHUNK");
+  const char* v = sdh::knob("SDH_RING_CHUNK");
   return v && *v ? fmt("#define SDH_RING_CHUNK %d\n", atoi(v)) : std::string();
 }
 
 // an integer knob from the environment, clamped (tuning A/Bs of the generated kernels)
 int env_int(const char* env, int dflt, int lo, int hi) {
-  const char* v = getenv(env);
+  const char* v = sdh::knob(env);
   const int n = v && *v ? atoi(v) : dflt;
   return n < lo ? lo : n > hi ? hi : n;
 }
@@ -47,7 +48,7 @@ int env_int(const char* env, int dflt, int lo, int hi) {
 // register budget of a shape-compiled kernel: SDH_SEQ_WPE / SDH_PART_WPE = N asks for N resident
 // waves per SIMD (amdgpu_waves_per_eu); unset or 0 leaves the compiler's choice
 std::string wpe_attr(const char* env, int dflt) {
-  const char* v = getenv(env);
+  const char* v = sdh::knob(env);
   const int n = v && *v ? atoi(v) : dflt;
   return n > 0 ? fmt("__attribute__((amdgpu_waves_per_eu(%d))) ", std::min(n, 8)) : std::string();
 }
@@ -277,7 +278,7 @@ std::string part_source(const kg::GQuery& g, const PartLayout& lay) {
 // hiprtc: src -> code object for `arch` (e.g. "gfx950"); empty and *err on failure
 std::vector<char> compile(const std::string& src_in, const std::string& arch, std::string* err) {
   // measurement builds: SDH_PART_PROF=1 compiles part_body's phase clocks in (engine prints them)
-  const std::string src = getenv("SDH_PART_PROF") ? "#define SDH_PART_PROF 1\n" + src_in : src_in;
+  const std::string src = sdh::knob("SDH_PART_PROF") ? "#define SDH_PART_PROF 1\n" + src_in : src_in;
   hiprtcProgram prog = nullptr;
   if (hiprtcCreateProgram(&prog, src.c_str(), "sdh_spec.hip", k_spec_n_headers, k_spec_headers,
                           k_spec_header_names) != HIPRTC_SUCCESS) {
@@ -303,7 +304,7 @@ std::vector<char> compile(const std::string& src_in, const std::string& arch, st
   std::vector<char> code(n);
   hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
-  if (const char* dir = getenv("SDH_SPEC_DUMP")) {  // inspection: source + code object per kernel
+  if (const char* dir = sdh::knob("SDH_SPEC_DUMP")) {  // inspection: source + code object per kernel
     const size_t h = std::hash<std::string>{}(src);
     const std::string base = std::string(dir) + "/" + fmt("spec_%016zx", h);
     if (FILE* f = fopen((base + ".hip").c_str(), "w")) {

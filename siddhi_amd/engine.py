@@ -31,7 +31,38 @@ class SdhConfig(ctypes.Structure):
                 ("chunk_events", ctypes.c_int32), ("flags", ctypes.c_int32),
                 ("gen_pool_states", ctypes.c_int32), ("gen_pool_nodes", ctypes.c_int32),
                 ("gen_list_cap", ctypes.c_int32), ("gen_pad", ctypes.c_int32),
-                ("gen_max_keys", ctypes.c_int64)]
+                ("gen_max_keys", ctypes.c_int64), ("debug", ctypes.c_char_p)]
+
+
+def debug_string(debug) -> Optional[bytes]:
+    """sdh_config.debug from a {NAME: VALUE} dict or a "NAME=VALUE;..." string. The test / bench harness
+    may also pass knobs through SIDDHI_HIP_DEBUG (the library itself reads no environment)."""
+    parts = []
+    env = os.environ.get("SIDDHI_HIP_DEBUG")
+    if env:
+        parts.append(env)
+    if isinstance(debug, dict):
+        parts.append(";".join(f"{k}={v}" for k, v in debug.items()))
+    elif debug:
+        parts.append(str(debug))
+    return ";".join(parts).encode() if parts else None
+
+
+class SdhRecords(ctypes.Structure):
+    """sdh_records (include/siddhi_hip.h): the last push's device records, three parts."""
+    _fields_ = [("n", ctypes.c_int64), ("seq_base", ctypes.c_int64), ("n_events", ctypes.c_int64),
+                ("r_n", ctypes.c_int64), ("r_blocks", ctypes.c_int64), ("r_bytes", ctypes.c_int64),
+                ("r_base", ctypes.c_void_p), ("r_count", ctypes.c_void_p), ("r_side", ctypes.c_void_p),
+                ("r_group", ctypes.c_void_p), ("r_lane_query", ctypes.c_void_p),
+                ("r_format", ctypes.c_int32), ("r_blk_bytes", ctypes.c_int32),
+                ("f_n", ctypes.c_int64), ("f_words", ctypes.c_int64), ("f_base", ctypes.c_void_p),
+                ("f_query_keys", ctypes.c_void_p),
+                ("c_n", ctypes.c_int64), ("c_items", ctypes.c_int64), ("c_words", ctypes.c_int32),
+                ("flags", ctypes.c_int32), ("c_base", ctypes.c_void_p), ("c_off", ctypes.c_void_p),
+                ("c_count", ctypes.c_void_p)]
+
+
+SDH_REC_NONE, SDH_REC_8, SDH_REC_16, SDH_REC_4 = 0, 1, 2, 3
 
 
 class SdhBatch(ctypes.Structure):
@@ -78,7 +109,8 @@ EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engi
            "sdh_engine_debug_digest", "sdh_engine_set_strings", "sdh_calibrate_hbm", "sdh_build_info",
            "sdh_engine_push_stats", "sdh_comm_get_id", "sdh_comm_create", "sdh_comm_create_local",
            "sdh_comm_destroy", "sdh_comm_last_error", "sdh_engine_set_comm", "sdh_engine_push_bcast",
-           "sdh_engine_gather", "sdh_engine_reserve", "sdh_engine_reserve_keys"]
+           "sdh_engine_gather", "sdh_engine_reserve", "sdh_engine_reserve_keys", "sdh_engine_poll_records",
+           "sdh_engine_records_compact"]
 SDH_COMM_ID_BYTES = 128
 
 _lib = None
@@ -103,6 +135,8 @@ def load_library(path: str = LIB_PATH):
     lib.sdh_engine_poll_compact.argtypes = [P, ctypes.c_int32, ctypes.POINTER(SdhMatchesCompact)]
     lib.sdh_engine_poll_compact_ex.argtypes = [P, ctypes.c_int32, ctypes.POINTER(SdhMatchesCompactEx)]
     lib.sdh_engine_pending_matches.argtypes = [P, ctypes.POINTER(ctypes.c_int64)]
+    lib.sdh_engine_poll_records.argtypes = [P, ctypes.POINTER(SdhRecords)]
+    lib.sdh_engine_records_compact.argtypes = [P, P, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
     lib.sdh_engine_start.argtypes = [P, ctypes.c_int64]
     lib.sdh_engine_advance_time.argtypes = [P, ctypes.c_int64]
     lib.sdh_engine_stats.argtypes = [P, ctypes.POINTER(SdhStats)]
@@ -185,13 +219,14 @@ class HipEngine:
     def __init__(self, blob: bytes, device: int = 0, partials: int = 128, shard_rank: int = 0,
                  shard_world: int = 1, chunk_events: int = 0, stream_types=None, flags: int = 0,
                  gen_pool_states: int = 0, gen_pool_nodes: int = 0, gen_list_cap: int = 0,
-                 gen_max_keys: int = 0):
+                 gen_max_keys: int = 0, debug=None):
         self.lib = load_library()
+        self._debug = debug_string(debug)
         cfg = SdhConfig(device=device, shard_rank=shard_rank, shard_world=shard_world,
                         partials_per_inst=partials, max_batch=0, match_capacity=0,
                         chunk_events=chunk_events, flags=flags, gen_pool_states=gen_pool_states,
                         gen_pool_nodes=gen_pool_nodes, gen_list_cap=gen_list_cap, gen_pad=0,
-                        gen_max_keys=gen_max_keys)
+                        gen_max_keys=gen_max_keys, debug=self._debug)
         self.h = ctypes.c_void_p()
         self._blob = ctypes.create_string_buffer(blob, len(blob))
         rc = self.lib.sdh_engine_create(self._blob, len(blob), ctypes.byref(cfg), ctypes.byref(self.h))
@@ -322,6 +357,21 @@ class HipEngine:
         tb = np.ctypeslib.as_array(m.tb, shape=(n,)).copy() if (m.tb and n) else (np.zeros(0, np.int64) if m.tb else None)
         chain = np.ctypeslib.as_array(m.chain, shape=(m.n_chain,)).copy() if m.n_chain else np.zeros(0, np.int32)
         return m.seq_base, rows, key, tb, chain
+
+    def poll_records(self) -> SdhRecords:
+        """The last push's device records (sdh_engine_poll_records; SDH_FLAG_DEVICE_MATCHES): the
+        SdhRecords struct of HBM pointers, formats in include/siddhi_hip.h."""
+        r = SdhRecords()
+        self._check(self.lib.sdh_engine_poll_records(self.h, ctypes.byref(r)))
+        return r
+
+    def records_compact(self, rows_ptr: int = 0, cap: int = 0, width: int = 4) -> int:
+        """Decode the K_ratchet part of the last push's device records into compact rows at the device
+        pointer rows_ptr (sdh_engine_records_compact); rows_ptr 0: only the row count."""
+        n = ctypes.c_int64()
+        self._check(self.lib.sdh_engine_records_compact(self.h, rows_ptr or None, int(cap), int(width),
+                                                        ctypes.byref(n)))
+        return n.value
 
     def take_matches(self, n_slots_of):
         q, k, ts, off, words = self.poll()

@@ -6,8 +6,9 @@ state id, their next / next-every / within-every / partner / callback links, the
 receivers with their processor registration order, and the inner-state-runtime tree that drives
 ``init``/``reset``/``update``.  Filters and selector outputs are typed postfix bytecode.
 
-Binary layout (little-endian int64 words), consumed by ``siddhi_amd/csrc/program.cpp`` and by
-the CPU oracle (``oracle/oracle.cpp``)::
+Binary layout (little-endian int64 words; the C-ABI's specification is ``include/siddhi_hip_ir.h``),
+consumed by the engine (``siddhi_amd/csrc/engine.hip`` ``read_ir`` and ``siddhi_amd/csrc/gen_lower.h``
+``kg::read_program``) and by the CPU oracle (``oracle/oracle.cpp``)::
 
     'SDHIR001' version
     n_streams  { n_attrs attr_type* }

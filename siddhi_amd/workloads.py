@@ -88,6 +88,23 @@ def c2_app(n_patterns: int, within=None, first: int = 0, step: int = 1) -> str:
     return " ".join(qs)
 
 
+def c2x_volume(p: int) -> int:
+    return 200 + (p % 7) * 100
+
+
+def c2x_app(n_patterns: int, first: int = 0, step: int = 1) -> str:
+    """The C2 family with one more event-only conjunct on e2: `e2=StockStream[price
+    > e1.price and volume > V_p]`, V_p in 200 .. 800. A partial survives an event whose volume fails
+    V_p whatever its price, so the pending keys are no longer monotone (K_ratchet's deque argument,
+    DESIGN.md §3.1) -- the gated form of the ratchet plan (§3.1, "gated e2") handles it."""
+    qs = [STOCK_STREAM]
+    for p in range(first, first + n_patterns * step, step):
+        qs.append(f"@info(name='x{p}') from every e1=StockStream[price > {c2_threshold_text(p)}] -> "
+                  f"e2=StockStream[price > e1.price and volume > {c2x_volume(p)}] within {c2_within_sec(p)} sec "
+                  f"select e1.price as p1, e2.price as p2 insert into OutStream;")
+    return " ".join(qs)
+
+
 def c3_query(p: int, seed: int = PATTERN_SEED) -> str:
     """Pattern p of the C3 family: count <2:5>, logical and, logical or, within 10 sec,
     all inside `partition with (symbol of StockStream)`."""

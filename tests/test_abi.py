@@ -93,3 +93,41 @@ def test_shape_compiled_kernels_build_without_a_device():
     log = ctypes.create_string_buffer(8192)
     n = lib.sdh_spec_selftest(log, len(log))
     assert n == 7, log.value.decode(errors="replace")
+
+
+def _c1_abi():
+    """tests/native/c1_abi: the C host built from include/ alone (make builds it when missing)."""
+    import subprocess
+    here = os.path.dirname(os.path.abspath(__file__))
+    exe = os.path.join(here, "native", "c1_abi")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(here, "native"), "c1_abi"])
+    return exe
+
+
+def test_c_host_builds_the_program_blob_from_the_header(tmp_path):
+    """A C program that sees only include/siddhi_hip.h and include/siddhi_hip_ir.h builds the C1
+    program blob by hand: byte for byte the blob the planner serializes for the same query."""
+    import subprocess
+    from siddhi_amd import ql
+    from siddhi_amd.planner import plan
+    from siddhi_amd.workloads import c1_app
+    out = tmp_path / "c1.blob"
+    subprocess.check_call([_c1_abi(), "blob", str(out)])
+    assert out.read_bytes() == plan(ql.parse(c1_app())).serialize()
+
+
+def test_ir_header_constants_match_the_planner():
+    """include/siddhi_hip_ir.h's constants are the ones siddhi_amd/ir.py writes."""
+    from siddhi_amd import ir
+    text = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                             "siddhi_hip_ir.h")).read()
+    defs = dict((m.group(1), int(m.group(2))) for m in re.finditer(r"#define SDH_(\w+) \(?(-?\d+)\)?", text))
+    for name in ("T_INT", "T_LONG", "T_FLOAT", "T_DOUBLE", "T_BOOL", "T_STRING", "OP_CONST", "OP_ATTR",
+                 "OP_IS_NULL", "OP_STREAM_IS_NULL", "OP_CMP", "OP_AND", "OP_OR", "OP_NOT", "OP_ARITH", "CMP_EQ",
+                 "CMP_NE", "CMP_GT", "CMP_GE", "CMP_LT", "CMP_LE", "AR_ADD", "AR_SUB", "AR_MUL", "AR_DIV", "AR_MOD",
+                 "IDX_CURRENT", "IDX_LAST", "K_STREAM", "K_COUNT", "K_LOGICAL", "K_ABSENT", "L_AND", "L_OR",
+                 "Q_PATTERN", "Q_SEQUENCE", "R_SINGLE", "R_MULTI", "N_STREAM", "N_NEXT", "N_EVERY", "N_LOGICAL",
+                 "N_COUNT"):
+        assert defs[name] == getattr(ir, name), name
+    assert defs["IR_VERSION"] == ir.VERSION
+    assert f'"{ir.MAGIC.decode()}"' in text

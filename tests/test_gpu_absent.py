@@ -118,13 +118,12 @@ def test_absent_partition_indexed_sweep(seed):
     (nfa_gen.hip: each key's clone walks its own routed events; a timer fires at the first batch event
     whose time reaches it, by binary search of the batch's time prefix max). Against the oracle, and
     equal to the whole-batch sweep (SDH_NO_TIMER_INDEX) push for push."""
-    import os
     import numpy as np
     from fuzz_apps import random_events
     src = random_absent_app(seed, partition=True)
     rng = np.random.default_rng(seed)
     ev = [("A" if rng.random() < 0.9 else "B", row, t) for _, row, t in random_events(seed, n=3000, keys=60)]
-    apps = [App(src), App(src, hip_factory(src)), App(src, hip_factory(src))]
+    apps = [App(src), App(src, hip_factory(src)), App(src, hip_factory(src, debug={"SDH_NO_TIMER_INDEX": 1}))]
     try:
         for a in apps:
             a.start(0)
@@ -134,13 +133,8 @@ def test_absent_partition_indexed_sweep(seed):
             while j < len(ev) and ev[j][0] == ev[i][0] and j - i < 500:
                 j += 1
             rows, ts = [r for _, r, _ in ev[i:j]], [t for _, _, t in ev[i:j]]
-            for k, a in enumerate(apps):
-                if k == 2:
-                    os.environ["SDH_NO_TIMER_INDEX"] = "1"
-                try:
-                    a.send(ev[i][0], rows, ts)
-                finally:
-                    os.environ.pop("SDH_NO_TIMER_INDEX", None)
+            for a in apps:
+                a.send(ev[i][0], rows, ts)
             i = j
         for a in apps:
             a.advance_time(ev[-1][2] + 50)

@@ -164,7 +164,7 @@ def test_device_resident_chunk_and_mixed_window():
 def test_chunk_split_by_the_journal_budget(monkeypatch):
     """A chunk whose K_gen journal would pass SDH_JOURNAL_BUDGET is pushed as two halves that still
     act as one chunk (one time move, one run split, one subscriber order)."""
-    monkeypatch.setenv("SDH_JOURNAL_BUDGET", "1")
+    monkeypatch.setenv("SIDDHI_HIP_DEBUG", "SDH_JOURNAL_BUDGET=1")
     src = random_absent_app(3, partition=True)
     o, g = _apps(src)
     ev = random_events(3, n=400)

@@ -119,17 +119,18 @@ def test_compact_unsupported_keeps_window(kind):
         assert np.array_equal(x, y)
 
 
-def test_compact_rows_when_lanes_walk_their_deques(monkeypatch):
+def test_compact_rows_when_lanes_walk_their_deques():
     """Placed rows whose lane count comes from the deque walk: with 4 LDS entries per lane
     (SDH_RATCHET_ML=4) and falling runs of 12-40 prices every partial stays pending until one high
     price matches them all, so a lane pops past its first round's four compares, through the LDS ring
     into the spill ring. The placed rows must equal the table path's (SDH_NO_PLACE on the second
     engine), restated from its poll."""
-    import os
+    from siddhi_amd.engine import HipEngine
     from siddhi_amd.workloads import TS0, c2_app
-    monkeypatch.setenv("SDH_RATCHET_ML", "4")
-    a, b = _engines(c2_app(64))
-    monkeypatch.delenv("SDH_RATCHET_ML")
+    app = App(c2_app(64), engine_factory=lambda blob: None)
+    types = [s.attr_types for s in app.ir.streams]
+    a = HipEngine(app.blob, stream_types=types, debug={"SDH_RATCHET_ML": 4})
+    b = HipEngine(app.blob, stream_types=types, debug={"SDH_RATCHET_ML": 4, "SDH_NO_PLACE": 1})
     rng = np.random.default_rng(7)
     price = []
     while len(price) < 30000:
@@ -145,11 +146,7 @@ def test_compact_rows_when_lanes_walk_their_deques(monkeypatch):
         sl = slice(lo, lo + 5000)
         part = [c[sl] for c in cols]
         a.push_columns(0, ts[sl], part)
-        os.environ["SDH_NO_PLACE"] = "1"
-        try:
-            b.push_columns(0, ts[sl], part)
-        finally:
-            del os.environ["SDH_NO_PLACE"]
+        b.push_columns(0, ts[sl], part)
         seq_base, rows = a.poll_compact()
         q, k, t, off, words, seq, tb = b.poll(with_seq=True)
         assert seq_base == seq_polled

@@ -272,7 +272,7 @@ def test_gen_snapshot_restore_count_and_partition():
 
 def _chunked_pair(src, chunk_len, monkeypatch):
     """Oracle + a K_gen-only engine (SDH_FLAG_FORCE_GEN keeps windowed sequences off K_seq)."""
-    monkeypatch.setenv("SDH_GEN_CHUNK_LEN", str(chunk_len))
+    monkeypatch.setenv("SIDDHI_HIP_DEBUG", f"SDH_GEN_CHUNK_LEN={chunk_len}")
     return App(src), hip_app(src, flags=SDH_FLAG_FORCE_GEN)
 
 
@@ -438,14 +438,12 @@ def test_journal_budget_splits_the_push_exactly():
     to nothing (SDH_JOURNAL_BUDGET) every push of a partitioned K_gen app splits down to single
     events, and with tiny pools every one of those re-runs from the journal: the matches equal the
     oracle's."""
-    import os
     from siddhi_amd.workloads import c3_app, stock_events
     src = c3_app(12)
     o = App(src)
     g = hip_app(src, flags=SDH_FLAG_FORCE_GEN, gen_pool_states=2, gen_pool_nodes=4, gen_list_cap=2,
-                gen_max_keys=1024)
-    os.environ["SDH_JOURNAL_BUDGET"] = "1"
-    try:
+                gen_max_keys=1024, debug={"SDH_JOURNAL_BUDGET": 1})
+    if True:
         for lo, n in ((0, 700), (700, 1300)):
             ts, sym, price, vol = stock_events(lo, n, 40)
             vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64), vol.astype(np.int64)], 1)
@@ -454,6 +452,4 @@ def test_journal_budget_splits_the_push_exactly():
             om = o.engine.take_matches(lambda q: 3)
             gm = g.engine.take_matches(lambda q: 3)
             assert gm == om and len(om) > 50
-    finally:
-        del os.environ["SDH_JOURNAL_BUDGET"]
     assert g.engine.stats().pool_regrows > 0

@@ -92,7 +92,7 @@ def test_kpart_random_apps(seed):
 def test_kpart_table_growth_reruns_exactly(cap, monkeypatch):
     """Tiny initial tables (SDH_KPART_CAP): every overflow is undone and re-run with twice the
     room, in normal and in device-matches mode."""
-    monkeypatch.setenv("SDH_KPART_CAP", str(cap))
+    monkeypatch.setenv("SIDDHI_HIP_DEBUG", f"SDH_KPART_CAP={cap}")
     src = _queries(77, n=12)
     ts, vals, nl = _events(77, 5000, keys=2)
     _run_pair(src, ts, vals, nl, batch=1000)

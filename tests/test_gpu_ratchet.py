@@ -313,10 +313,11 @@ def test_wide_records_for_batches_beyond_2_26_events():
 def test_ring_rec4_distance_overflow_reruns_with_8b_records():
     """SDH_FLAG_DEVICE_MATCHES pushes write 4-B K_ratchet entries (an e1 distance below 2^26 and the
     lane) with one side entry per matching event (nfa_types.h rec4). A partial matched more than 2^26
-    events after it opened sets err[4] and the push re-runs with 8-B records: the ring engine's record
-    digest still equals the normal-mode engine's, in both pushes."""
+    events after it opened sets err[4] and that push re-runs with 8-B records (its records come out as
+    SDH_REC_8); the next push writes rec4 again. The device-record engine's record digest equals the
+    normal-mode engine's in every push."""
     import torch
-    from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES, HipEngine
+    from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES, SDH_REC_4, SDH_REC_8, HipEngine
     src = ("define stream S (v float); @info(name='q') from every e1=S[v > 2.0] -> e2=S[v > e1.v] "
            "within 20 hours select e1.v as a insert into O;")  # (SIM form; `within` lets the push chunk)
     app = App(src, engine_factory=lambda blob: None)
@@ -325,15 +326,26 @@ def test_ring_rec4_distance_overflow_reruns_with_8b_records():
     ring = HipEngine(app.blob, stream_types=types, flags=SDH_FLAG_DEVICE_MATCHES)
     dev = torch.device("cuda:0")
     n1 = 1 << 26  # (not past 2^26: the push keeps 8-B / rec4 records)
-    for lo, n, first, last in ((0, n1, 5, 1), (n1, 3, 1, 10)):
+    fmts = []
+    for lo, vals in ((0, None), (n1, [1, 1, 10]), (n1 + 3, [3, 20, 1])):
+        n = n1 if vals is None else len(vals)
         ts = torch.arange(lo, lo + n, dtype=torch.int64, device=dev)
-        v = torch.ones(n, dtype=torch.float32, device=dev)
-        v[0], v[-1] = first, last
+        if vals is None:
+            v = torch.ones(n, dtype=torch.float32, device=dev)
+            v[0] = 5
+        else:
+            v = torch.tensor(vals, dtype=torch.float32, device=dev)
         for e in (normal, ring):
             e.push_device(0, n, ts.data_ptr(), [v.data_ptr()])
         dn, dr = normal.debug_digest(), ring.debug_digest()
         assert dn == dr, f"push at {lo}: normal {dn} != ring {dr}"
+        rec = ring.poll_records()
+        assert rec.r_n == dn[0]
+        fmts.append(rec.r_format)
         del ts, v
-    assert dn[0] == 1  # the first event's partial, matched 2^26 + 2 events later
+    # push 2: the partial of the first event, matched 2^26 + 2 events later -> the 8-B re-run;
+    # push 3: two short-distance matches -> rec4 again
+    assert fmts[1:] == [SDH_REC_8, SDH_REC_4]
+    assert dn[0] == 2
     normal.close()
     ring.close()

@@ -64,8 +64,7 @@ def test_slab_fuzz_equals_oracle(seed, batch):
 def test_slab_rollback_growth_and_reclaim(seed, monkeypatch):
     """A 64-word LDS staging area and 64-word sub-rings: pushes overflow both, are undone (journal)
     and re-run at doubled capacity; sub-rings fill with superseded blocks and are reclaimed."""
-    monkeypatch.setenv("SDH_SLAB_LDS_WORDS", "64")
-    monkeypatch.setenv("SDH_SLAB_SUB_WORDS", "64")
+    monkeypatch.setenv("SIDDHI_HIP_DEBUG", "SDH_SLAB_LDS_WORDS=64;SDH_SLAB_SUB_WORDS=64")
     src = random_slab_app(seed + 100)
     ev = random_slab_events(seed + 100, n=800, keys=2)
     o = _run(src, ev, 50)
