@@ -257,11 +257,12 @@ def cpu_baseline(workload, n_symbols, budget_s):
                       f"{d1} events (oracle/liboracle.so, matches counted in the library)"}
 
 
-KERNEL_OF_PLAN = {}  # workload -> the kernel its plan launches, where it differs from the default
+KERNEL_OF_PLAN = {"c2x": "nfa_gate_kernel"}  # workload -> the kernel its plan launches
 
 KERNEL_SOURCES = {  # what a kernel's code and launch configuration are built from
     "nfa_chain_kernel": ["nfa_chain.hip", "nfa_types.h", "engine.hip"],
-    "nfa_ratchet_kernel": ["nfa_ratchet.hip", "nfa_types.h", "engine.hip"],
+    "nfa_ratchet_kernel": ["nfa_ratchet.hip", "ratchet_common.h", "nfa_types.h", "engine.hip"],
+    "nfa_gate_kernel": ["nfa_gate.hip", "ratchet_common.h", "nfa_types.h", "engine.hip"],
     "nfa_gen_kernel": ["nfa_gen.hip", "kgen.h", "gen_lower.h", "nfa_types.h", "engine.hip"],
     "nfa_seq_kernel": ["nfa_gen.hip", "seq_body.h", "dev_common.h", "kgen.h", "gen_lower.h", "nfa_types.h",
                        "engine.hip"],
@@ -546,7 +547,7 @@ def main():
     # Without a matching profile it falls back to the design's minimum bytes and says so.
     m_step = matches / max(1, args.steps * world)
     design = None
-    if args.workload == "c2":
+    if args.workload in ("c2", "c2x"):
         # the design's own minimum per step: every 64-pattern group streams the batch's ts + price
         # (the start filter reads the same column) once, plus the record bytes the kernel wrote
         # (rec4: 4 B per match + 8 B per matching event and wave) -- §8(d)'s accounting less its 32 B

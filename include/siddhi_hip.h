@@ -182,6 +182,9 @@ typedef struct sdh_stats {
   int64_t last_slab_items;   /* K_slab work items of the last push: key segments x groups         */
   int64_t placed_pushes;     /* pushes whose matches (all K_ratchet) went straight to their R18   */
                              /* rows (no sort at poll; matches.hip ratchet_place_kernel)          */
+  int64_t plan_queries[8];   /* queries (pattern instances of this shard) per device plan:         */
+                             /* [0] K_ratchet [1] K_gate [2] K_chain [3] K_part [4] K_slab         */
+                             /* [5] K_seq [6] K_gen                                */
 } sdh_stats;
 
 int sdh_engine_create(const void* ir_blob, size_t len, const sdh_config* cfg, sdh_engine** out);

@@ -138,6 +138,9 @@ extern "C" hipError_t sdh_digest_ratchet(const int64_t* match, int blk_recs, int
                                          const int32_t* blk_group, const int32_t* blk_side,
                                          const sdh::RatchetGroup* groups, int64_t seq_base,
                                          int n_blocks, unsigned long long* acc, hipStream_t s);
+extern "C" hipError_t sdh_launch_gate(int key_kind, int xmask, int full, int nf, int ng, int SC,
+                                      const sdh::RatchetLaunch* L, hipStream_t s);
+extern "C" int sdh_gate_occupancy(int nf, int ng);
 extern "C" size_t sdh_ratchet_compact_temp(int64_t n_blocks);
 extern "C" hipError_t sdh_ratchet_compact(const int64_t* match, int blk_recs, int wide, const int32_t* blk_count,
                                           const int32_t* blk_group, const int32_t* blk_side,
@@ -510,22 +513,53 @@ struct RatchetPlan {
   int stream = 0, key_attr = 0, key_conv = 0, key_kind = 0, xmask = 0;
   std::vector<RatchetAtom> f0;
   std::vector<int64_t> f0c;
+  // K_gate (nfa_gate.hip): e2's event-only conjuncts `cur.b OP const` (empty: plain K_ratchet)
+  std::vector<RatchetAtom> g;
+  std::vector<int64_t> gc;
   int64_t within = -1;
   // grouping signature: everything except the per-lane constants and `within`
   std::vector<int64_t> sig() const {
-    std::vector<int64_t> v{stream, key_kind, key_attr, key_conv, xmask, within >= 0, (int64_t)f0.size()};
-    for (const auto& a : f0)
-      v.insert(v.end(), {a.attr, a.conv, a.cur_left, a.mask, a.f64, a.cur2, a.attr2, a.conv2});
+    std::vector<int64_t> v{stream, key_kind, key_attr, key_conv, xmask, within >= 0, (int64_t)f0.size(),
+                           (int64_t)g.size()};
+    for (const auto* atoms : {&f0, &g})
+      for (const auto& a : *atoms)
+        v.insert(v.end(), {a.attr, a.conv, a.cur_left, a.mask, a.f64, a.cur2, a.attr2, a.conv2});
     return v;
   }
 };
+
+// an event-only atom `cur OP const` / `const OP cur` (a start filter's or a gate's) as a RatchetAtom
+// and its constant; false for any other operand shape
+bool const_atom(const ChainQuery& c, const Atom& A, RatchetAtom& ra, int64_t& cst) {
+  ra = RatchetAtom{};
+  ra.mask = A.mask;
+  ra.f64 = A.f64;
+  if (A.lk == OPK_CUR && A.rk == OPK_CONST) {
+    ra.attr = c.col_attr[A.li]; ra.conv = c.col_conv[A.li]; ra.cur_left = 1; cst = A.rc;
+  } else if (A.lk == OPK_CONST && A.rk == OPK_CUR) {
+    ra.attr = c.col_attr[A.ri]; ra.conv = c.col_conv[A.ri]; ra.cur_left = 0; cst = A.lc;
+  } else {
+    return false;
+  }
+  return true;
+}
 
 RatchetPlan ratchet_plan(const ChainQuery& c) {
   RatchetPlan r;
   if (c.n_states != 2 || !c.every || c.state_stream[0] != c.state_stream[1]) return r;
   if (c.n_cap != 1 || c.cap_slot[0] != 0) return r;
-  if (c.atom_begin[2] - c.atom_begin[1] != 1 || c.xa_count[1] != 1 || c.xa_count[0] != 0) return r;
-  const Atom& X = c.atoms[c.xa_atom[c.xa_first[1]]];
+  if (c.xa_count[1] != 1 || c.xa_count[0] != 0) return r;
+  const int x_at = c.xa_atom[c.xa_first[1]];
+  // state 1's other atoms: event-only constant compares gate it (K_gate); none for K_ratchet
+  for (int a = c.atom_begin[1]; a < c.atom_begin[2]; ++a) {
+    if (a == x_at) continue;
+    RatchetAtom ga;
+    int64_t cst = 0;
+    if (!const_atom(c, c.atoms[a], ga, cst) || r.g.size() >= (size_t)RMAXF0) return RatchetPlan();
+    r.g.push_back(ga);
+    r.gc.push_back(cst);
+  }
+  const Atom& X = c.atoms[x_at];
   int mask = X.mask;
   if (mask & CM_NOT) return r;
   if (!(mask & (CM_LT | CM_GT)) || ((mask & CM_LT) && (mask & CM_GT))) return r;  // ordering only
@@ -551,6 +585,7 @@ RatchetPlan ratchet_plan(const ChainQuery& c) {
     default: return r;
   }
   if (r.key_kind < 0) return r;
+  if (!r.g.empty() && r.key_kind != KK_F32 && r.key_kind != KK_I32) return RatchetPlan();  // (K_gate: 32-bit keys)
   const int na0 = c.atom_begin[1] - c.atom_begin[0];
   if (na0 > RMAXF0) return r;
   for (int a = c.atom_begin[0]; a < c.atom_begin[1]; ++a) {
@@ -563,7 +598,7 @@ RatchetPlan ratchet_plan(const ChainQuery& c) {
       ra.attr = c.col_attr[A.li]; ra.conv = c.col_conv[A.li]; ra.cur_left = 1; cst = A.rc;
     } else if (A.lk == OPK_CONST && A.rk == OPK_CUR) {
       ra.attr = c.col_attr[A.ri]; ra.conv = c.col_conv[A.ri]; ra.cur_left = 0; cst = A.lc;
-    } else if (A.lk == OPK_CUR && A.rk == OPK_CUR) {
+    } else if (A.lk == OPK_CUR && A.rk == OPK_CUR && r.g.empty()) {  // (K_gate: constant atoms only)
       ra.attr = c.col_attr[A.li]; ra.conv = c.col_conv[A.li]; ra.cur_left = 1;
       ra.cur2 = 1; ra.attr2 = c.col_attr[A.ri]; ra.conv2 = c.col_conv[A.ri];
     } else {
@@ -1495,7 +1530,9 @@ void ratchet_build(sdh_engine* e, std::vector<std::pair<RatchetPlan, int>>& plan
     g.xmask = P.xmask;
     g.n_f0 = (int)P.f0.size();
     for (int a = 0; a < g.n_f0; ++a) g.f0[a] = P.f0[a];
-    g.sim = ratchet_sim(g);
+    g.n_g = (int)P.g.size();
+    for (int a = 0; a < g.n_g; ++a) g.g[a] = P.g[a];
+    g.sim = g.n_g ? 0 : ratchet_sim(g);
     g.wmax = -1;
     for (int l = 0; l < 64; ++l) {
       const size_t k = i + std::min<size_t>(l, j - i - 1);  // idle lanes mirror the last pattern
@@ -1504,6 +1541,7 @@ void ratchet_build(sdh_engine* e, std::vector<std::pair<RatchetPlan, int>>& plan
       g.within[l] = Q.within < 0 ? INT64_MAX : Q.within;
       if (l < g.n_lanes) g.wmax = std::max(g.wmax, Q.within);
       for (int a = 0; a < g.n_f0; ++a) g.f0c[a][l] = Q.f0c[a];
+      for (int a = 0; a < g.n_g; ++a) g.gc[a][l] = Q.gc[a];
     }
     e->rg.push_back(g);
     i = j;
@@ -1629,7 +1667,8 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     // launches: one per (key kind, orientation, SIM form); SIM also needs the key column null-free
     // in this batch
     auto lsim = [&](int g) { return e->rg[g].sim && !B.nul[e->rg[g].key_attr] ? 1 : 0; };
-    auto lkey = [&](int g) { return std::make_tuple(e->rg[g].key_kind, e->rg[g].xmask, lsim(g)); };
+    auto lgate = [&](int g) { return e->rg[g].n_g > 0 ? 1 : 0; };  // K_gate groups (nfa_gate.hip)
+    auto lkey = [&](int g) { return std::make_tuple(lgate(g), e->rg[g].key_kind, e->rg[g].xmask, lsim(g)); };
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return lkey(a) < lkey(b); });
     for (size_t i0 = 0; i0 < order.size();) {
       size_t i1 = i0;
@@ -1641,7 +1680,8 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
       // 117.8 ms/step, 16,384 110.9, 32,768 103.3, 65,536 100.2, 131,072 100.8, 524,288 104.4
       double slots = e->r_waves;
       if (slots <= 0) {
-        const int occ = sdh_ratchet_occupancy(e->rg[order[i0]].key_kind, full, nf, e->rML, lsim(order[i0]));
+        const int occ = lgate(order[i0]) ? sdh_gate_occupancy(nf, nf)
+                                         : sdh_ratchet_occupancy(e->rg[order[i0]].key_kind, full, nf, e->rML, lsim(order[i0]));
         slots = 8.0 * (double)e->n_cu * std::max(1, occ);
       }
       // chunks per chunkable group: as many as fit the item target (floor, not ceil: a partial
@@ -1761,7 +1801,7 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
     auto run = [&](const RatchetLaunch& L0) {
       for (int i0 = 0; i0 < n_items;) {
         const int g0 = e->ritems[i0].g;
-        const int kk = e->rg[g0].key_kind, xm = e->rg[g0].xmask, sim = lsim(g0);
+        const int kk = e->rg[g0].key_kind, xm = e->rg[g0].xmask, sim = lsim(g0), gate = lgate(g0);
         int i1 = i0;
         while (i1 < n_items && lkey(e->ritems[i1].g) == lkey(g0)) ++i1;
         RatchetLaunch Ls = L0;
@@ -1773,9 +1813,15 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
         Ls.spillA = e->d_rspillA.p + (size_t)i0 * e->rSC * WAVE;
         Ls.lds_ts = e->d_rlts.p + (size_t)i0 * e->rML * WAVE;
         Ls.spillB = any64 ? e->d_rspillB.p + (size_t)i0 * e->rSC * WAVE : nullptr;
-        Ls.rec4 = L0.rec4 && sim ? 1 : 0;  // (rec4 blocks come from the SIM form only)
+        Ls.rec4 = L0.rec4 && sim && !gate ? 1 : 0;  // (rec4 blocks come from the SIM form only)
         any_rec4 |= Ls.rec4;
-        HIPCHK(sdh_launch_ratchet(kk, xm, full, nf, full ? 0 : sim, e->rML, e->rSC, &Ls, e->stream));
+        if (gate) {
+          int ng = 0;
+          for (int i = i0; i < i1; ++i) ng = std::max(ng, e->rg[e->ritems[i].g].n_g);
+          HIPCHK(sdh_launch_gate(kk, xm, full, nf, ng, e->rSC, &Ls, e->stream));
+        } else {
+          HIPCHK(sdh_launch_ratchet(kk, xm, full, nf, full ? 0 : sim, e->rML, e->rSC, &Ls, e->stream));
+        }
         i0 = i1;
       }
     };
@@ -1894,6 +1940,8 @@ void launch_ratchet(sdh_engine* e, int stream, const StreamBatch& B, const int64
         if (G.f0[a].attr != G.key_attr) ev_bytes += B.width[G.f0[a].attr];
         if (G.f0[a].cur2 && G.f0[a].attr2 != G.key_attr) ev_bytes += B.width[G.f0[a].attr2];
       }
+      for (int a = 0; a < G.n_g; ++a)  // (K_gate's gate columns)
+        if (G.g[a].attr != G.key_attr) ev_bytes += B.width[G.g[a].attr];
       bytes += (double)n * ev_bytes;
     }
     bytes += (double)e->r_matches * 32.0;
@@ -4317,9 +4365,13 @@ int sdh_engine_create(const void* ir, size_t len, const sdh_config* cfg, sdh_eng
       for (auto& g : e->rg) g.cell = -1;
       for (size_t st = 0; st < ns; ++st) {
         std::vector<int> gs;
+        bool gated = false;  // (K_gate writes records, not placed rows)
         for (int g = 0; g < (int)e->rg.size(); ++g)
-          if (e->rg[g].stream == (int)st && e->rg[g].n_lanes > 0) gs.push_back(g);
-        if (gs.empty()) continue;
+          if (e->rg[g].stream == (int)st && e->rg[g].n_lanes > 0) {
+            gs.push_back(g);
+            gated |= e->rg[g].n_g > 0;
+          }
+        if (gs.empty() || gated) continue;
         auto rk = [&](int g, int l) { return e->out_rank[(size_t)e->rg[g].qid[l] * ns + st]; };
         std::sort(gs.begin(), gs.end(), [&](int a, int b) { return rk(a, 0) < rk(b, 0); });
         std::vector<int> ranks;
@@ -4659,6 +4711,22 @@ int sdh_engine_stats(sdh_engine* e, sdh_stats* out) {
     e->stats.live_partials = live;
     e->stats.pool_regrows = e->gen_regrows;
     e->stats.last_slab_items = e->slab_items;
+    // queries per plan: K_ratchet, K_gate, K_chain, K_part, K_slab, K_seq, K_gen
+    for (auto& c : e->stats.plan_queries) c = 0;
+    for (const auto& g : e->rg) e->stats.plan_queries[g.n_g ? 1 : 0] += g.n_lanes;
+    e->stats.plan_queries[2] = (int64_t)e->lq.size();
+    auto lanes = [&](int g) {
+      int64_t c = 0;
+      for (int l = 0; l < WAVE; ++l) c += e->lane_q[(size_t)g * WAVE + l] >= 0 ? 1 : 0;
+      return c;
+    };
+    for (const auto& ps : e->psets)
+      for (int g = ps->group_base; g < ps->group_base + ps->n_groups; ++g) e->stats.plan_queries[3] += lanes(g);
+    for (const auto& ss : e->ssets)
+      for (int g = ss->group_base; g < ss->group_base + ss->n_groups; ++g) e->stats.plan_queries[4] += lanes(g);
+    for (const auto& gs : e->gsets)
+      for (int g = gs->group_base; g < gs->group_base + gs->n_groups; ++g)
+        e->stats.plan_queries[(size_t)g < e->group_seq.size() && e->group_seq[g] > 0 ? 5 : 6] += lanes(g);
     *out = e->stats;
     return SDH_OK;
   });

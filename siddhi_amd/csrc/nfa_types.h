@@ -165,6 +165,12 @@ struct RatchetGroup {
   int32_t qid[64];
   int64_t within[64];                     // per lane; INT64_MAX = none
   int64_t f0c[RMAXF0][64];                // per lane constant key of each f0 atom
+  // K_gate (nfa_gate.hip): e2's event-only conjuncts `g` (constant atoms, per-lane constants as f0's);
+  // n_g > 0 makes the group gated
+  int32_t n_g;
+  int32_t pad_g;
+  RatchetAtom g[RMAXF0];
+  int64_t gc[RMAXF0][64];
 };
 
 struct RatchetItem {

@@ -145,24 +145,26 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
     if (!__ballot(!nar_ok(s))) o.emit_u(nwords, [&](auto r) { put_nrec(r, s); });
     else o.emit_u(words, [&](auto r) { put_rec(r, s); });
   };
-  // a lane's matches among 8 starts (mask m over s0 ..) in one collective call: its records are
-  // contiguous, start order; the record counts take 4 ballots
-  auto emit8 = [&](int s0, uint32_t m) {
-    const int nl = __popc(m);
+  // a lane's matches among the tile's starts (mask m) in one collective call: its records are
+  // contiguous, start order; the record counts take 7 ballots. (One call per 64 starts instead of per
+  // 8: the call's wave-uniform bookkeeping -- ballots, the LDS buffer's counters, placement rounds --
+  // ran on the scalar unit once per 8 starts, which bound C4 at 78 % SALU issue.)
+  auto emit_tile = [&](uint64_t m) {
+    const int nl = __popcll(m);
     nrec += nl;
     if (!L.write_records || __ballot(nl > 0) == 0) return;
     bool ok = true;
-    for (uint32_t mm = m; mm; mm &= mm - 1) ok = ok && nar_ok(s0 + __builtin_ctz(mm));
+    for (uint64_t mm = m; mm; mm &= mm - 1) ok = ok && nar_ok(__builtin_ctzll(mm));
     if (!__ballot(!ok))
       o.emit_n(nl, nwords, [&](auto r0) {
         int kk = 0;
-        for (uint32_t mm = m; mm; mm &= mm - 1, ++kk) put_nrec(r0 + kk * nwords, s0 + __builtin_ctz(mm));
-      }, true, 4);
+        for (uint64_t mm = m; mm; mm &= mm - 1, ++kk) put_nrec(r0 + kk * nwords, __builtin_ctzll(mm));
+      }, true, 7);
     else
       o.emit_n(nl, words, [&](auto r0) {
         int kk = 0;
-        for (uint32_t mm = m; mm; mm &= mm - 1, ++kk) put_rec(r0 + kk * words, s0 + __builtin_ctz(mm));
-      }, true, 4);
+        for (uint64_t mm = m; mm; mm &= mm - 1, ++kk) put_rec(r0 + kk * words, __builtin_ctzll(mm));
+      }, true, 7);
   };
   for (int64_t t0 = lo; t0 < hi; t0 += SEQ_TILE) {
     const int cnt = hi - t0 < SEQ_TILE ? (int)(hi - t0) : SEQ_TILE;
@@ -178,14 +180,16 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
       if constexpr (Spec::kBranchFree) {
         // 8 starts at a time, every state of each evaluated: their LDS reads overlap; starts past
         // cnt read rows of the LDS window that are stale or unset, and are masked off
+        uint64_t m = 0;
         for (int s0 = 0; s0 < cnt; s0 += 8) {
-          uint32_t m = 0;
+          uint32_t m8 = 0;
 #pragma unroll
           for (int u = 0; u < 8; ++u)
-            m |= (Spec::match(k, q, ql, within, Win{win + (s0 + u) * ROW}) ? 1u : 0u) << u;
-          if (cnt - s0 < 8) m &= (1u << (cnt - s0)) - 1u;
-          emit8(s0, m);
+            m8 |= (Spec::match(k, q, ql, within, Win{win + (s0 + u) * ROW}) ? 1u : 0u) << u;
+          m |= (uint64_t)m8 << s0;
         }
+        if (cnt < 64) m &= (1ull << cnt) - 1ull;
+        emit_tile(m);
       } else {
         for (int s = 0; s < cnt; ++s)
           if (Spec::match(k, q, ql, within, Win{win + s * ROW})) emit(s);

@@ -98,7 +98,9 @@ class SdhStats(ctypes.Structure):
                 ("last_part_items", ctypes.c_int64), ("last_ingest_ms", ctypes.c_double),
                 ("ingest_bytes", ctypes.c_int64), ("spec_kernels", ctypes.c_int64),
                 ("pool_regrows", ctypes.c_int64), ("last_slab_items", ctypes.c_int64),
-                ("placed_pushes", ctypes.c_int64)]
+                ("placed_pushes", ctypes.c_int64), ("plan_queries", ctypes.c_int64 * 8)]
+
+PLANS = ("K_ratchet", "K_gate", "K_chain", "K_part", "K_slab", "K_seq", "K_gen")
 
 
 EXPORTS = ["sdh_engine_create", "sdh_engine_push", "sdh_engine_flush", "sdh_engine_poll", "sdh_engine_poll_device",

@@ -102,7 +102,7 @@ def run(cfg_name, n_events, threads, stride, log=True):
                 return raw_matches(apps[i])
             parts = list(ex.map(one, range(T)))
             dig.update(*merge(parts, bounds[:T], rank))
-            if log and (lo // B) % 4 == 0:
+            if log and (lo // B) % (1 if cfg_name == "c2x" else 4) == 0:
                 print(f"  {cfg_name}: {lo + n}/{n_events} events, {dig.n} matches, {time.time() - t0:.0f} s",
                       flush=True)
     return dig

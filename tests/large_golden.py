@@ -16,6 +16,7 @@ seed 7):
   c4: 10,000 C4 fraud sequences x 200K Txn events, 100K accounts
   c2h: the headline configuration itself -- 10,000 C2 patterns (the metric's 10K) x 200K events,
        ~860M matches (tests/test_gpu_golden.py pushes it in 100K-event batches and in one 200K push)
+  c2x: 10,000 patterns of the C2 family with an event-only conjunct on e2 (`volume > V_p`) x 200K events
 """
 from __future__ import annotations
 
@@ -33,17 +34,19 @@ CONFIGS = {
     "c3": dict(patterns=1000, events=200_000, keys=10_000, batch=1 << 15, stream="stock", sample_stride=50_000),
     "c4": dict(patterns=10_000, events=200_000, keys=100_000, batch=1 << 15, stream="txn", sample_stride=200_000),
     "c2h": dict(patterns=10_000, events=200_000, keys=100, batch=1 << 13, stream="stock", sample_stride=2_000_000),
+    # the C2 family with an event-only conjunct on e2 (workloads.c2x_app), off K_ratchet
+    "c2x": dict(patterns=10_000, events=200_000, keys=100, batch=1 << 13, stream="stock", sample_stride=2_000_000),
 }
 SAMPLE_FIRST = 500
 SAMPLE_MAX_STRIDED = 500
 
 
 def app_source(cfg_name: str, n_patterns: int, first: int = 0) -> str:
-    from siddhi_amd.workloads import c1_app, c2_app, c3_app, c4_app
+    from siddhi_amd.workloads import c1_app, c2_app, c2x_app, c3_app, c4_app
     if cfg_name == "c1":
         assert first == 0 and n_patterns == 1
         return c1_app()
-    return {"c2": c2_app, "c2h": c2_app, "c3": c3_app, "c4": c4_app}[cfg_name](n_patterns, first=first)
+    return {"c2": c2_app, "c2h": c2_app, "c2x": c2x_app, "c3": c3_app, "c4": c4_app}[cfg_name](n_patterns, first=first)
 
 
 def events(cfg_name: str, start: int, n: int):

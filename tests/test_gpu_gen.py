@@ -394,25 +394,27 @@ def test_seq_windows_snapshot_restore():
 
 @pytest.mark.gpu
 def test_device_matches_ring_counts_every_record():
-    """SDH_FLAG_DEVICE_MATCHES (benchmark mode) writes every K_gen record into a device ring that
-    wraps when a push's records exceed the buffer; the match count equals the normal mode's over
-    the same stream (pushed in batches small enough for the normal output buffer)."""
+    """SDH_FLAG_DEVICE_MATCHES writes every K_gen record into the flat device-record buffer, which grows
+    and re-runs the push when its records exceed it (no wrap); the records handed out
+    (sdh_engine_poll_records) number the normal mode's matches over the same stream (pushed in
+    batches small enough for the normal output buffer)."""
     from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES, HipEngine
     from siddhi_amd.workloads import c2_app, stock_events
 
     app = App(c2_app(64), engine_factory=lambda blob: None)
     types = [s.attr_types for s in app.ir.streams]
-    ts, sym, price, vol = stock_events(0, 100_000)
+    ts, sym, price, vol = stock_events(0, 60_000)
     vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64), vol.astype(np.int64)], 1)
     ring = HipEngine(app.blob, stream_types=types, flags=SDH_FLAG_FORCE_GEN | SDH_FLAG_DEVICE_MATCHES)
-    ring.send(0, ts, vals, None)  # ~3M records x 11 words: wraps the 6.4M-word buffer
+    ring.send(0, ts, vals, None)  # ~1.8M records x 11 words: past the initial 4M-word buffer
+    rec = ring.poll_records()
     normal = HipEngine(app.blob, stream_types=types, flags=SDH_FLAG_FORCE_GEN)
-    for b in range(0, len(ts), 5000):
-        normal.send(0, ts[b:b + 5000], vals[b:b + 5000], None)
+    for b in range(0, len(ts), 10000):
+        normal.send(0, ts[b:b + 10000], vals[b:b + 10000], None)
         normal.poll()
     n = ring.stats().matches
     assert n > 1_000_000
-    assert n == normal.stats().matches
+    assert n == normal.stats().matches == rec.f_n
 
 
 def test_gen_output_overflow_reruns_exactly():

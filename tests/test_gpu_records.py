@@ -211,7 +211,7 @@ def _slots(r, sq, kind):
 def walk_flat(rec):
     """Part 2 (flat records) walked by the first word's length -> [(query, key, trigger seq, slot words)]."""
     words = _host(rec.f_base, rec.f_words, np.int64)
-    qk_ptrs = None
+    qk_ptrs = {}
     keys = {}
     out, i, pads = [], 0, 0
     while i < len(words):
@@ -237,10 +237,10 @@ def walk_flat(rec):
         key = -1
         if kind != 2:
             kid = (int(r[1]) >> 32) & 0xFFFFFFFF
-            if qk_ptrs is None:
-                qk_ptrs = _host(rec.f_query_keys, q + 1 + 4096, np.uint64)
+            if q not in qk_ptrs:  # f_query_keys[q]: the query's key table (device pointer)
+                qk_ptrs[q] = int(_host(rec.f_query_keys + 8 * q, 1, np.uint64)[0])
             if (q, kid) not in keys:
-                keys[(q, kid)] = int(_host(int(qk_ptrs[q]) + kid * 8, 1, np.int64)[0])
+                keys[(q, kid)] = int(_host(qk_ptrs[q] + kid * 8, 1, np.int64)[0])
             key = keys[(q, kid)]
         out.append((q, key, sq, tuple(_slots(r, sq, kind))))
         i += nw

@@ -17,6 +17,7 @@ ap.add_argument("--n", type=int, default=120)
 ap.add_argument("--compact", action="store_true", help="poll compact_ex rows instead of tuples")
 ap.add_argument("--reserve", action="store_true", help="sdh_engine_reserve_keys(K) before the first push")
 a = ap.parse_args()
+print("cmd: " + " ".join([sys.executable] + sys.argv), file=sys.stderr, flush=True)  # (the log names its run)
 
 import torch  # noqa: E402,F401
 
