@@ -40,13 +40,21 @@
 
 namespace sdh {
 
-constexpr int GML = 16;  // LDS entries per lane
+// LDS entries per lane: occupancy outweighs the spill (C2x at 10K patterns, 4M-event steps: GML 4
+// 515 ms/step, 8 341, 16 404, 32 670; waves per SIMD aimed at 4 / 6: same, 8: 525 -- register spills)
+#ifndef SDH_GATE_GML
+#define SDH_GATE_GML 8
+#endif
+constexpr int GML = SDH_GATE_GML;  // LDS entries per lane (a power of two)
+#ifndef SDH_GATE_WPE
+#define SDH_GATE_WPE 4  // resident waves per SIMD the register allocation aims at
+#endif
 
-extern __shared__ uint2 gate_lds[];  // [GML][64] {key, seq}, then [GML][64] int64 ts0
+extern __shared__ uint2 gate_lds[];  // [GML][64] {key, seq}, then [GML][64] expiry words (int32 / FULL: int64)
 
 // FULL: out-of-order timestamps (eager expiry at every event); otherwise the lazy form
 template <int KK, int XM, int NF, int NG, int PM, bool FULL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void nfa_gate_kernel(RatchetLaunch L,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDH_GATE_WPE))) void nfa_gate_kernel(RatchetLaunch L,
                                                                                             int SC) {
   static_assert(!KT<KK>::W64, "K_gate holds 32-bit keys");
   using U = uint32_t;
@@ -138,13 +146,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void nf
 
   // ---- the lane's pending set: LDS slots [0, ln) (the best keys), spill slots [0, sn) (the rest) ----
   uint2* __restrict__ KQ = gate_lds;
+  // an LDS entry's expiry word: the lazy form's 32-bit deadline relative to the item's first
+  // timestamp (nfa_ratchet.hip rel_deadline; its ts0 is the batch's ts at its seq, since only this
+  // batch's partials enter LDS -- carried ones stay in the spill), FULL's 64-bit ts0
+  int32_t* __restrict__ DL = reinterpret_cast<int32_t*>(gate_lds + GML * WAVE);
   int64_t* __restrict__ TS = reinterpret_cast<int64_t*>(gate_lds + GML * WAVE);
   uint4* __restrict__ SP = L.spillA + (size_t)wid * SC * WAVE;
+  const int64_t T0 = L.b.ts[W.c0];
   int lbot = 0, ln = 0, sn = 0;     // LDS ring slots lbot .. lbot + ln - 1, best key first
+  U tk = 0;                         // the LDS ring's best key (valid while ln > 0)
   bool shas = false;                // best key of the spill part
   U sext = 0;
   uint32_t oq = 0;                  // low seq bits of the oldest held partial (a bound: removals keep it)
   const uint32_t llo = (uint32_t)(seq_base + W.c1 - 1);
+  const int64_t slast = seq_base + W.c1 - 1;
+  auto full_seq = [&](uint32_t q) { return slast - (int64_t)(uint32_t)(llo - q); };
   int overflow = 0, unordered = 0, mover = 0, aged = 0;
   auto li = [&](int slot) { return (slot & (GML - 1)) * WAVE + lane; };
   auto si = [&](int slot) { return (size_t)slot * WAVE + lane; };
@@ -157,23 +173,50 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void nf
     key = a.z;
     seq = a.w;
   };
+  // LDS entries as {key, seq, x}: x the expiry word (lazy: deadline; FULL: ts0)
   auto lput = [&](int slot, int64_t ts, U key, uint32_t seq) {
     KQ[li(slot)] = make_uint2(key, seq);
-    TS[li(slot)] = ts;
+    if constexpr (FULL) TS[li(slot)] = ts;
+    else DL[li(slot)] = rel_deadline(sat_add(ts, within), T0);
   };
-  auto lget = [&](int slot, int64_t& ts, U& key, uint32_t& seq) {
+  auto lgetx = [&](int slot, int64_t& xw, U& key, uint32_t& seq) {
     const uint2 a = KQ[li(slot)];
     key = a.x;
     seq = a.y;
-    ts = TS[li(slot)];
+    if constexpr (FULL) xw = TS[li(slot)];
+    else xw = DL[li(slot)];
+  };
+  auto lputx = [&](int slot, int64_t xw, U key, uint32_t seq) {
+    KQ[li(slot)] = make_uint2(key, seq);
+    if constexpr (FULL) TS[li(slot)] = xw;
+    else DL[li(slot)] = (int32_t)xw;
+  };
+  auto ts_of = [&](int64_t xw, uint32_t seq) -> int64_t {  // an LDS entry's ts0
+    if constexpr (FULL) return xw;
+    else return L.b.ts[full_seq(seq) - seq_base];
+  };
+  // (ts0, key, seq) of an LDS entry
+  auto lget = [&](int slot, int64_t& ts, U& key, uint32_t& seq) {
+    int64_t xw;
+    lgetx(slot, xw, key, seq);
+    ts = ts_of(xw, seq);
   };
   auto lmove = [&](int to, int from) {
     KQ[li(to)] = KQ[li(from)];
-    TS[li(to)] = TS[li(from)];
+    if constexpr (FULL) TS[li(to)] = TS[li(from)];
+    else DL[li(to)] = DL[li(from)];
   };
   auto dead = [&](int64_t t0, int64_t tt) {  // (ordered: tt >= t0; FULL: |tt - t0|, isExpired)
     if constexpr (FULL) return expired(t0, tt, within);
     else return tt > sat_add(t0, within);
+  };
+  // an LDS entry (expiry word xw) expired at tt (tt32: tt in the deadline domain)
+  auto ldead = [&](int64_t xw, int64_t tt, int32_t tt32) {
+    if constexpr (FULL) return expired(xw, tt, within);
+    else return tt32 > (int32_t)xw;
+  };
+  auto rel32 = [&](int64_t tt) {
+    return tt >= T0 + (INT32_MAX - 1) ? INT32_MAX - 1 : tt <= T0 + INT32_MIN ? INT32_MIN : (int32_t)(tt - T0);
   };
   auto add_ext = [&](bool& has, U& ext, U key) {
     ext = (!has || ext_better(key, ext)) ? key : ext;
@@ -210,6 +253,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void nf
   // is no better than every LDS key.
   auto push = [&](int64_t ts, U key, uint32_t seq, int64_t tt) {
     note_seq(seq);
+    if (!FULL && full_seq(seq) < seq_base) {  // a carried partial: its ts0 is not in this batch
+      spill_push(ts, key, seq, tt);
+      return;
+    }
     if (ln == GML) {
       int64_t t0; U k0; uint32_t q0;
       lget(lbot + GML - 1, t0, k0, q0);
@@ -220,14 +267,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void nf
       spill_push(t0, k0, q0, tt);
       --ln;
     }
-    // rank p: the entries strictly better than the key (binary search over the ring)
-    int lo = 0, hi = ln;
-    while (lo < hi) {
-      const int m = (lo + hi) >> 1;
-      if (ext_better(KQ[li(lbot + m)].x, key)) lo = m + 1;
-      else hi = m;
+    // rank p: the entries strictly better than the key -- 0 when it is at least as good as the best
+    // (every push at an event that matched), else by binary search over the ring
+    int p = 0;
+    if (ln > 0 && ext_better(tk, key)) {
+      int lo = 1, hi = ln;
+      while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (ext_better(KQ[li(lbot + m)].x, key)) lo = m + 1;
+        else hi = m;
+      }
+      p = lo;
     }
-    const int p = lo;
     if (p <= ln - p) {  // the better side moves one slot toward the front
       lbot = (lbot - 1) & (GML - 1);
       for (int i = 0; i < p; ++i) lmove(lbot + i, lbot + i + 1);
@@ -236,6 +287,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void nf
     }
     lput(lbot + p, ts, key, seq);
     ++ln;
+    tk = p == 0 ? key : tk;
   };
 
   // ---- output blocks (K_ratchet's: one atomic per block, mbcnt ranks inside) ----
@@ -397,34 +449,39 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void nf
       const U x = (U)__builtin_amdgcn_readlane(xk, k);
       const int64_t tt = readlane64(ets, k);
       const uint32_t off = (uint32_t)(t + k);
+      const int32_t tt32 = FULL ? 0 : rel32(tt);
       if constexpr (FULL) {  // out-of-order timestamps: every expired partial leaves before the event (eager)
         int w = 0;
         for (int i = 0; i < ln; ++i) {
-          int64_t t0; U ky; uint32_t q;
-          lget(lbot + i, t0, ky, q);
-          if (dead(t0, tt)) continue;
-          if (w != i) lput(lbot + w, t0, ky, q);  // (order kept)
+          int64_t xw; U ky; uint32_t q;
+          lgetx(lbot + i, xw, ky, q);
+          if (ldead(xw, tt, tt32)) continue;
+          if (w != i) lputx(lbot + w, xw, ky, q);  // (order kept)
           ++w;
         }
         ln = w;
+        if (ln > 0) tk = KQ[li(lbot)].x;
         spill_compact(tt);
       }
       // ---- matches: an event passing g matches every pending partial with `x OP key` ----
       const bool gate = g_pass(k, vbk);
       // the LDS part: its matches are a prefix (best keys first); an expired entry there leaves
       // unmatched
-      bool pop = gate && ln > 0 && xop<KK, XM>(xmask, x, KQ[li(lbot)].x);
+      // (one entry per round: a round of four, reading the next three unconditionally as K_ratchet
+      // does, measured 363 ms per C2x step against 341 -- a lane pops one or two entries per match)
+      bool pop = gate && ln > 0 && xop<KK, XM>(xmask, x, tk);
       while (wballot(pop) != 0) {
-        int64_t t0 = 0;
+        int64_t xw = 0;
         U ky = 0;
         uint32_t q = 0;
-        if (pop) lget(lbot, t0, ky, q);
-        const bool mt = pop && !dead(t0, tt);
+        if (pop) lgetx(lbot, xw, ky, q);
+        const bool mt = pop && !ldead(xw, tt, tt32);
         emit(mt, wballot(mt), off, q);
         if (pop) {
           lbot = (lbot + 1) & (GML - 1);
           --ln;
-          pop = ln > 0 && xop<KK, XM>(xmask, x, KQ[li(lbot)].x);
+          tk = KQ[li(lbot)].x;  // (a stale slot when ln reaches 0: tk is then unused)
+          pop = ln > 0 && xop<KK, XM>(xmask, x, tk);
         }
       }
       const bool scan_s = gate && shas && xop<KK, XM>(xmask, x, sext);
@@ -480,7 +537,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void nf
   if (W.chunk == W.n_chunks - 1) {  // the last chunk owns the group's lists: the pending set after its last event
     const int64_t t_end = L.b.ts[W.c1 - 1];
     const int ob = 1 - W.inb;
-    const int64_t slast = seq_base + W.c1 - 1;
     int64_t* __restrict__ o_ts = pick(L.ent_ts, ob);
     int64_t* __restrict__ o_sq = pick(L.ent_seq, ob);
     int64_t* __restrict__ o_ky = pick(L.ent_key, ob);
@@ -516,7 +572,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void nf
 
 template <int KK, int XM, int NF, int PM, bool FULL>
 static void gate_launch_one(const sdh::RatchetLaunch* L, int SC, hipStream_t s) {
-  const size_t lds = (size_t)sdh::GML * 64 * 16;
+  const size_t lds = (size_t)sdh::GML * 64 * (FULL ? 16 : 12);
   hipLaunchKernelGGL((sdh::nfa_gate_kernel<KK, XM, NF, NF, PM, FULL>), dim3(L->n_items), dim3(64), lds, s, *L, SC);
 }
 
@@ -565,7 +621,7 @@ extern "C" hipError_t sdh_launch_gate(int key_kind, int xmask, int full, int nf,
 // resident waves per CU of the K_gate instantiation
 extern "C" int sdh_gate_occupancy(int nf, int ng) {
   int nb = 0;
-  const size_t lds = (size_t)sdh::GML * 64 * 16;
+  const size_t lds = (size_t)sdh::GML * 64 * 12;
   const hipError_t r = (nf <= 1 && ng <= 1)
                            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
                                  &nb, sdh::nfa_gate_kernel<sdh::KK_F32, 0, 1, 1, 0, false>, 64, lds)
