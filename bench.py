@@ -749,7 +749,8 @@ def eng_patterns(eng):
 
 def expansion(args, sh, K, local, dev, world, cdev, dist, comm=None):
     """Pushes of a smaller batch in normal mode, each followed by sdh_engine_poll_device (device R18
-    sort + gather of the ABI tuples in HBM): the NFA step with every match expanded. With N GPUs the
+    sort + gather of the ABI tuples in HBM): the NFA step with every match expanded. One GPU: 12 timed
+    pushes after 3 warm-up pushes, keyed workloads with their K keys' state reserved first. With N GPUs the
     pushes are broadcast from rank 0 and every push is followed by sdh_engine_gather: every rank's
     R18-sorted tuples go to rank 0 over RCCL and are merged there on the device, timed per step."""
     import torch
@@ -757,9 +758,11 @@ def expansion(args, sh, K, local, dev, world, cdev, dist, comm=None):
     # per event, so the multi-GPU gather runs on 8K-event batches
     E = args.expansion_batch if world == 1 else min(args.expansion_batch, 8192)
     eng = make_engine(args.workload, sh, K, local, 0, args.partials)
+    if args.workload in ("c3", "c5"):  # per-key state sized up front, as the latency leg does
+        eng.reserve_keys(K)
     if comm is not None:
         eng.set_comm(comm)
-    steps, warm = 4, 1
+    steps, warm = (12, 3) if world == 1 else (4, 1)
     root = world == 1 or dist.get_rank() == 0
     bs = [gen_batch(args.workload, s * E, E, K, dev) if root else None for s in range(steps + warm)]
     torch.cuda.synchronize()
@@ -833,6 +836,8 @@ def compact_leg(args, sh, K, local, bs, E, warm, want):
     the rows when the program has them."""
     import torch
     eng = make_engine(args.workload, sh, K, local, 0, args.partials)
+    if args.workload in ("c3", "c5"):
+        eng.reserve_keys(K)
     matches, width, chain, extra = 0, 0, 0, 0
     try:
         for i, cols in enumerate(bs):

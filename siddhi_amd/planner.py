@@ -553,6 +553,11 @@ def java_string_hash(s: str) -> int:
 
 def plan(app: ql.App) -> ProgramIR:
     """Lower a parsed app to the pattern IR."""
+    with ql.no_gc():
+        return _plan(app)
+
+
+def _plan(app: ql.App) -> ProgramIR:
     pb = _ProgramBuilder(app)
     queries: List[QueryIR] = []
     partitions: List[PartitionIR] = []
@@ -611,7 +616,10 @@ def plan(app: ql.App) -> ProgramIR:
             # ConcurrentHashMap keyed by query name (:177), holding every query of the partition
             names = [q.name for q in obj.queries]
             pos = chm.positions([java_string_hash(nm) for nm in names])
-            qidx.sort(key=lambda i: pos[names.index(queries[i].name)])
+            first = {}
+            for j, nm in enumerate(names):
+                first.setdefault(nm, j)
+            qidx.sort(key=lambda i: pos[first[queries[i].name]])
             partitions.append(PartitionIR(keys, qidx, fanout))
     names = [q.name for q in queries]
     if len(set(names)) != len(names):

@@ -26,7 +26,9 @@ raise :class:`SiddhiParserException`.
 """
 from __future__ import annotations
 
+import gc
 import re
+from contextlib import contextmanager
 from dataclasses import dataclass, field
 from typing import List, Optional, Tuple, Union
 
@@ -225,7 +227,7 @@ _TIME_UNITS = [
 ]
 
 
-@dataclass
+@dataclass(slots=True)
 class Tok:
     kind: str   # 'id','kw','num','str','op','eof'
     text: str
@@ -234,26 +236,29 @@ class Tok:
 
 def tokenize(src: str) -> List[Tok]:
     toks: List[Tok] = []
+    add = toks.append
+    kws = _KEYWORDS
     i = 0
-    while i < len(src):
-        m = _TOKEN_RE.match(src, i)
-        if not m:
-            raise SiddhiParserException(f"unexpected character {src[i]!r} at {i}")
-        kind = m.lastgroup
-        text = m.group(kind)
-        if kind != "ws":
-            if kind == "id":
-                if text.startswith("`"):
-                    toks.append(Tok("id", text[1:-1], i))
-                elif text.lower() in _KEYWORDS:
-                    toks.append(Tok("kw", text.lower(), i))
-                else:
-                    toks.append(Tok("id", text, i))
-            elif kind == "str":
-                toks.append(Tok("str", text[1:-1], i))
-            else:
-                toks.append(Tok(kind, text, i))
+    for m in _TOKEN_RE.finditer(src):
+        if m.start() != i:  # finditer skipped a character no token matches
+            break
         i = m.end()
+        kind = m.lastgroup
+        if kind == "ws":
+            continue
+        text = m.group(kind)
+        if kind == "id":
+            if text[0] == "`":
+                add(Tok("id", text[1:-1], m.start()))
+            else:
+                low = text.lower()
+                add(Tok("kw", low, m.start()) if low in kws else Tok("id", text, m.start()))
+        elif kind == "str":
+            add(Tok("str", text[1:-1], m.start()))
+        else:
+            add(Tok(kind, text, m.start()))
+    if i < len(src):
+        raise SiddhiParserException(f"unexpected character {src[i]!r} at {i}")
     toks.append(Tok("eof", "", len(src)))
     return toks
 
@@ -271,16 +276,19 @@ def _time_unit_ms(word: str) -> Optional[int]:
 class Parser:
     def __init__(self, src: str):
         self.toks = tokenize(src)
+        self._n = len(self.toks)
         self.i = 0
         self.query_counter = 0
 
     # token helpers -------------------------------------------------------------------------
     def peek(self, k: int = 0) -> Tok:
-        return self.toks[min(self.i + k, len(self.toks) - 1)]
+        j = self.i + k
+        return self.toks[j] if j < self._n else self.toks[-1]
 
     def at(self, text: str, k: int = 0) -> bool:
-        t = self.peek(k)
-        return t.kind in ("op", "kw") and t.text == text
+        j = self.i + k
+        t = self.toks[j] if j < self._n else self.toks[-1]
+        return t.text == text and (t.kind == "op" or t.kind == "kw")
 
     def accept(self, text: str) -> bool:
         if self.at(text):
@@ -822,6 +830,20 @@ class Parser:
         return Const("double", sign * float(txt))
 
 
+@contextmanager
+def no_gc():
+    """Parsing and planning build millions of small acyclic objects for a 100K-pattern app (C5): the
+    cyclic collector's passes over them are pure overhead there."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
+
+
 def parse(src: str) -> App:
     """Parse a SiddhiQL app string (``SiddhiCompiler.parse`` equivalent for the subset)."""
-    return Parser(src).parse_app()
+    with no_gc():
+        return Parser(src).parse_app()

@@ -30,6 +30,17 @@ def _pushes(g):
     return pushes({"events": g["prefix_events_per_stream"], "batch": g["batch"], "key_mod": g["key_mod"]})
 
 
+_APPS = {}
+
+
+def _app(patterns):
+    """c5 and c5deep run the same 100K-pattern app: plan it once per session."""
+    from siddhi_amd.workloads import c5_app
+    if patterns not in _APPS:
+        _APPS[patterns] = App(c5_app(patterns), engine_factory=lambda blob: None)
+    return _APPS[patterns]
+
+
 @pytest.mark.timeout(1200)
 @pytest.mark.parametrize("name", ["c5", "c5deep"])
 def test_c5_golden_full_config(name):
@@ -37,9 +48,8 @@ def test_c5_golden_full_config(name):
         pytest.skip(f"{golden_path(name)} not generated")
     from siddhi_amd.engine import HipEngine, columns_from_words
     from siddhi_amd.ir import T_FLOAT, T_INT
-    from siddhi_amd.workloads import c5_app
     g = load(name)
-    app = App(c5_app(g["patterns"]), engine_factory=lambda blob: None)
+    app = _app(g["patterns"])
     types = [[T_INT, T_FLOAT, T_INT]] * 4
     eng = HipEngine(app.blob, stream_types=types, gen_max_keys=1 << 20)
     dig = Digest(g["sample_stride"])

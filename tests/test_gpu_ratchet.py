@@ -319,7 +319,7 @@ def test_ring_rec4_distance_overflow_reruns_with_8b_records():
     import torch
     from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES, SDH_REC_4, SDH_REC_8, HipEngine
     src = ("define stream S (v float); @info(name='q') from every e1=S[v > 2.0] -> e2=S[v > e1.v] "
-           "within 20 hours select e1.v as a insert into O;")  # (SIM form; `within` lets the push chunk)
+           "select e1.v as a insert into O;")  # (SIM form; no `within`: one unchunked item per push)
     app = App(src, engine_factory=lambda blob: None)
     types = [s.attr_types for s in app.ir.streams]
     normal = HipEngine(app.blob, stream_types=types)
