@@ -84,7 +84,7 @@ typedef struct sdh_config {
   int32_t gen_pad;
   int64_t gen_max_keys;      /* distinct partition keys per partition                        */
   /* Tuning / diagnostic overrides, "NAME=VALUE;NAME=VALUE" (NULL: none), copied at create: kernel
-   * A/B knobs, traces, and test hooks that force a code path (DESIGN.md §4 lists them). The library
+   * A/B knobs, traces, and test hooks that force a code path (DESIGN.md §8 lists them). The library
    * reads no environment variables, so a host process's environment never changes its behaviour. */
   const char* debug;
 } sdh_config;

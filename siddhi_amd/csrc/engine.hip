@@ -3224,7 +3224,9 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       S.ev_idx = e->r_idx_s.p;
       S.glist = ss.d_glist[stream].p;
       S.n_glist = (int32_t)gl.size();
-      S.n_items = (int32_t)items;
+      // runs of groups per wave (nfa_slab.hip); SDH_SLAB_RUN 1: one wave per item
+      S.run = std::max(1, std::min(64, sdh::knob("SDH_SLAB_RUN") ? atoi(sdh::knob("SDH_SLAB_RUN")) : 64));
+      S.n_items = (int32_t)((int64_t)hv[1] * ((S.n_glist + S.run - 1) / S.run));
       S.groups = ss.n_groups;
       S.group_base = ss.group_base;
       S.dir = ss.dir.p;

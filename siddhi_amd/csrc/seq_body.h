@@ -16,20 +16,6 @@ namespace sdh {
 constexpr int SEQ_TILE = 64;
 constexpr int SEQ_ROW = 3 + kg::GMAXNA;  // ts, seq, null bits, raw words (the widest row)
 
-// SDH_SEQ_VGPR: a window word read from LDS is wave-uniform (every lane tests the same start), so the
-// compiler moves the work on it -- timestamp differences, null bits, the event-only compares -- to the
-// scalar unit, which one CU's four SIMDs share (C4: SALU issue 78 %, VALU 22 %). Passing the words
-// through an opaque VGPR copy keeps that work on the SIMDs.
-#ifndef SDH_SEQ_VGPR
-#define SDH_SEQ_VGPR 0
-#endif
-__device__ __forceinline__ int64_t seq_word(int64_t x) {
-#if SDH_SEQ_VGPR
-  asm volatile("" : "+v"(x));
-#endif
-  return x;
-}
-
 // a window over LDS rows of ROW words; a Spec sets kRow = 3 + the attributes its shape captures (the
 // LDS a wave takes bounds the resident waves: C4's rows are 5 words, not 11)
 template <int ROW>
@@ -37,9 +23,9 @@ struct LdsWinT {
   static constexpr bool kStagedConsts = false;
   const int64_t* base;  // row of window event 0
   __device__ int64_t lane_const(int) const { return 0; }
-  __device__ int64_t ts(int p) const { return seq_word(base[p * ROW]); }
-  __device__ int64_t raw(int p, int j, bool = false) const { return seq_word(base[p * ROW + 3 + j]); }
-  __device__ bool null(int p, int j, bool = false) const { return (seq_word(base[p * ROW + 2]) >> j) & 1; }
+  __device__ int64_t ts(int p) const { return base[p * ROW]; }
+  __device__ int64_t raw(int p, int j, bool = false) const { return base[p * ROW + 3 + j]; }
+  __device__ bool null(int p, int j, bool = false) const { return (base[p * ROW + 2] >> j) & 1; }
 };
 using LdsWin = LdsWinT<SEQ_ROW>;
 

@@ -32,12 +32,10 @@ std::string fmt(const char* f, ...) {
   return buf;
 }
 
-// tuning macros the generated kernels see (SDH_RING_CHUNK: device-record output reservations;
-// SDH_SEQ_VGPR: K_seq's window words in VGPRs, seq_body.h)
+// tuning macros the generated kernels see (SDH_RING_CHUNK: device-record output reservations)
 std::string tuning_defines() {
   std::string d;
   if (const char* v = sdh::knob("SDH_RING_CHUNK")) d += fmt("#define SDH_RING_CHUNK %d\n", atoi(v));
-  if (const char* v = sdh::knob("SDH_SEQ_VGPR")) d += fmt("#define SDH_SEQ_VGPR %d\n", atoi(v));
   return d;
 }
 

@@ -17,7 +17,7 @@ from large_golden import CONFIGS, Digest, app_source, events, load
 pytestmark = pytest.mark.gpu
 
 # push sizes on the device (the digest does not depend on how the stream is cut)
-PUSH = {"c1": 1 << 18, "c2": 1 << 17, "c3": 1 << 16, "c4": 1 << 16}
+PUSH = {"c1": 1 << 18, "c2": 1 << 17, "c3": 1 << 16, "c4": 1 << 16, "c2x": 1 << 17}
 
 
 def _engine(name, blob, types):
@@ -132,6 +132,48 @@ def test_headline_config_golden():
     one.push_device(0, cfg["events"], t_ts.data_ptr(), [c.data_ptr() for c in t_cols])
     assert one.pending_matches() == g["n_matches"]
     assert one.debug_digest()[0] == g["n_matches"]
+
+
+@pytest.mark.timeout(900)
+def test_c2x_config_golden():
+    """The C2x family (bench.py --workload c2x; workloads.c2x_app: C2 with an event-only conjunct
+    `volume > V_p` on e2, off K_ratchet) at its 10,000 patterns over 200K events, on K_gate
+    (nfa_gate.hip), against the oracle's golden (tests/golden/large_c2x.json): the R18-ordered
+    tuples of every push (sdh_engine_poll_device) reproduce the golden digest and samples, and the
+    same pushes in SDH_FLAG_DEVICE_MATCHES mode write the same records (count and hash)."""
+    import os
+    import torch
+    from large_golden import golden_path
+    from siddhi_amd.engine import SDH_FLAG_DEVICE_MATCHES, HipEngine
+    if not os.path.exists(golden_path("c2x")):
+        pytest.skip("tests/golden/large_c2x.json not generated")
+    cfg = CONFIGS["c2x"]
+    g = load("c2x")
+    app = App(app_source("c2x", cfg["patterns"]), engine_factory=lambda blob: None)
+    types = [s.attr_types for s in app.ir.streams]
+    dev = torch.device("cuda:0")
+    normal = HipEngine(app.blob, stream_types=types)
+    ring = HipEngine(app.blob, stream_types=types, flags=SDH_FLAG_DEVICE_MATCHES)
+    assert normal.stats().plan_queries[1] == cfg["patterns"]  # (every query on K_gate)
+    dig = Digest(g["sample_stride"])
+    B = PUSH["c2x"]
+    for lo in range(0, cfg["events"], B):
+        n = min(B, cfg["events"] - lo)
+        ts, cols, _ = events("c2x", lo, n)
+        t_ts = torch.from_numpy(ts).to(dev)
+        t_cols = [torch.from_numpy(np.ascontiguousarray(c).view(np.int32)).to(dev) for c in cols]
+        for e in (normal, ring):
+            e.push_device(0, n, t_ts.data_ptr(), [c.data_ptr() for c in t_cols])
+        dn, dr = normal.debug_digest(), ring.debug_digest()
+        assert dn == dr and dn[0] > 0, f"normal-mode records {dn} != device-match-mode records {dr}"
+        assert _digest_device_matches(normal, dig) == dn[0]
+    ring.close()
+    normal.close()
+    assert dig.n == g["n_matches"], f"c2x: {dig.n} matches, golden {g['n_matches']}"
+    assert dig.first == g["sample_first"]
+    assert dig.strided == g["sample_strided"]
+    assert dig.n_words == g["n_words"]
+    assert dig.hexdigest() == g["digest"]
 
 
 @pytest.mark.timeout(600)

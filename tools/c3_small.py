@@ -43,10 +43,10 @@ def main():
         elif args.mode == "device":
             n = eng.poll_device().n
         else:
-            n = eng.poll_records().r_n
+            n = eng.poll_records().n
         torch.cuda.synchronize()
         t2 = time.perf_counter()
-        kms = eng.stats().last_kernel_ms
+        kms = eng.push_stats()[0]
         print(f"push {i}: {n} matches, push {(t1 - t0) * 1e3:.3f} ms (kernels {kms:.3f}), "
               f"poll {(t2 - t1) * 1e3:.3f} ms", flush=True)
         if i >= 3:
