@@ -3224,9 +3224,7 @@ bool gen_pass(sdh_engine* e, int stream, const StreamBatch& B, bool write, doubl
       S.ev_idx = e->r_idx_s.p;
       S.glist = ss.d_glist[stream].p;
       S.n_glist = (int32_t)gl.size();
-      // runs of groups per wave (nfa_slab.hip); SDH_SLAB_RUN 1: one wave per item
-      S.run = std::max(1, std::min(64, sdh::knob("SDH_SLAB_RUN") ? atoi(sdh::knob("SDH_SLAB_RUN")) : 64));
-      S.n_items = (int32_t)((int64_t)hv[1] * ((S.n_glist + S.run - 1) / S.run));
+      S.n_items = (int32_t)items;
       S.groups = ss.n_groups;
       S.group_base = ss.group_base;
       S.dir = ss.dir.p;
@@ -3351,6 +3349,10 @@ void launch_gen(sdh_engine* e, int stream, const StreamBatch& B, double* ms_out,
     }
     kg::Sizing grown;
     const bool pools_over = errs[0] != 0 && gen_grown_sizing(e, errs[0], &grown);
+    if (sdh::knob("SDH_TRACE"))
+      fprintf(stderr, "[sdh] gen pass stream %d n %lld attempt %d: out %d part %d pools %d slab %d, %llu of %lld words, %.2f ms\n",
+              stream, (long long)n, attempt, (int)out_over, (int)part_over, (int)pools_over, (int)slab_over, used,
+              (long long)e->g_out_cap, ms);
     if ((out_over || part_over || pools_over || slab_over) && e->g_journal && attempt < 24 &&
         (!errs[0] || pools_over) && !errs[1] && !errs[3]) {
       // undo the pass (K_gen blocks from the journal; K_part tables are double-buffered and their

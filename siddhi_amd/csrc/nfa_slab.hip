@@ -66,55 +66,21 @@ __device__ __forceinline__ int wave_prefix(int v, int bits, int* total) {
 
 // NAX: the captured words the event staging holds (the launch's widest shape); LDS bounds the resident
 // waves of this kernel
-// A wave takes a RUN of up to L.run groups of one key segment (L.item_list: one deferred item): the
-// run's directory words come in with one coalesced load, a group whose state list is empty costs no
-// memory access at all, and the key's event tile staged for one group serves the next groups of the
-// same template. (One wave per (segment, group) launched ~1.4e8 waves per C5 push, most of them only to
-// read one directory word and leave.) Items keep their ids seg * n_glist + j (journal, deferral).
 template <int NAX, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void nfa_slab_kernel(SlabLaunch L) {
   using namespace slab;
   const int lane = threadIdx.x;
-  const int wv = (int)dev::grid_item(L.xcd);
-  if (wv >= L.n_items) return;
-  int seg, j0, j1;
-  if (L.item_list) {
-    const int it = L.item_list[wv];
-    seg = it / L.n_glist;
-    j0 = it % L.n_glist;
-    j1 = j0 + 1;
-  } else {
-    const int rps = (L.n_glist + L.run - 1) / L.run;  // runs per segment
-    seg = wv / rps;
-    j0 = (wv % rps) * L.run;
-    j1 = j0 + L.run < L.n_glist ? j0 + L.run : L.n_glist;
-  }
+  const int gi = (int)dev::grid_item(L.xcd);
+  if (gi >= L.n_items) return;
+  const int item = L.item_list ? L.item_list[gi] : gi;
+  const int seg = item / L.n_glist, g = L.glist[item % L.n_glist];
   const uint32_t kid = L.seg_kid[seg];
   if (kid == 0xFFFFFFFFu) return;  // null / foreign partition keys
-  const int stream = L.b.stream;
-  const int64_t e0 = L.seg_begin[seg], e1 = e0 + L.seg_len[seg];
-
-  extern __shared__ uint32_t slab_lds[];  // [lcap][EW] entries: the old block, then new partials
-  __shared__ int64_t t_ts[64], t_seq[64], t_w[NAX][64];
-  __shared__ uint32_t t_nul[64];
-  __shared__ SlabWaveOut::Shared out_sh;
-  __shared__ int64_t sh_base;
-  __shared__ uint64_t sh_dir[64];  // the run's directory words
-  uint32_t* ent = slab_lds;
-  if (lane < j1 - j0) sh_dir[lane] = L.dir[(uint64_t)kid * (uint64_t)L.groups + (uint64_t)L.glist[j0 + lane]];
-  __syncthreads();
-  SlabWaveOut o;
-  o.g = dev::LaneOut{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
-  o.sh = &out_sh;
-  o.init();
-  unsigned long long nrec = 0;
-  const int64_t key = L.key_of_id[kid];
-  int64_t staged_t0 = -1;  // the event tile in t_* (its first event and the template it was staged for)
-  const kg::GQuery* staged_q = nullptr;
-  auto one = [&](const int item, const int g, const uint64_t d0) {
   const Shape& sh = L.shapes[L.group_shape[g]];  // wave-uniform
+  const int stream = L.b.stream;
   const int st = sh.proc[stream];
   const uint64_t dir_idx = (uint64_t)kid * (uint64_t)L.groups + (uint64_t)g;
+  const uint64_t d0 = L.dir[dir_idx];
   const int n_old = (int)((d0 >> 40) & 0xffff);
   const uint32_t lists = (uint32_t)(d0 >> 56);
   if (st > 0 && !((lists >> st) & 1u)) return;  // no partial waits in this state's list
@@ -125,8 +91,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
   // lane-constant table (a lane reading its own GQuery instead touched 64 scattered lines per value)
   const kg::LaneConsts lk{nullptr, L.lconst + ((int64_t)(L.group_base + g) * L.lc_slots) * 64 + lane};
   const int EW = sh.EW;
+  const int64_t e0 = L.seg_begin[seg], e1 = e0 + L.seg_len[seg];
   const int ncap = q->n_cap[stream];
-  __syncthreads();  // (the previous group's reads of ent are done)
+
+  extern __shared__ uint32_t slab_lds[];  // [lcap][EW] entries: the old block, then new partials
+  __shared__ int64_t t_ts[64], t_seq[64], t_w[NAX][64];
+  __shared__ uint32_t t_nul[64];
+  __shared__ SlabWaveOut::Shared out_sh;
+  __shared__ int64_t sh_base;
+  uint32_t* ent = slab_lds;
   const int cap_ent = L.lds_words / EW;  // entries this shape's rows fit in the launch's LDS
   // a block that outgrows this launch's rows: deferred to the large-LDS launch (two tiers keep most
   // waves small, so more of them are resident), or, in that launch, the push re-runs with more LDS.
@@ -168,8 +141,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     }
     e_l = lo;
   }
+  SlabWaveOut o;
+  o.g = dev::LaneOut{L.out, L.out_cap, L.out_next, L.write_records == 2, L.rec_off, L.rec_cap, L.rec_next};
+  o.sh = &out_sh;
+  o.init();
   const int64_t within = lk.within();
   const int64_t qid = lk.qid();
+  const int64_t key = L.key_of_id[kid];
+  unsigned long long nrec = 0;
   bool changed = false, lds_over = false;
   int n_new = 0;  // wave-uniform: new entries appended after the old block
   // e1: armed unless a non-`every` start has fired (marker); new partials' position in element 1
@@ -197,7 +176,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
 
   for (int64_t t0 = e0; t0 < e1 && !lds_over; t0 += 64) {
     const int cnt = e1 - t0 < 64 ? (int)(e1 - t0) : 64;
-    if (t0 != staged_t0 || q != staged_q) {  // (a run's next group of the same template reuses it)
     if (lane < cnt) {
       const int64_t ev = L.ev_idx[t0 + lane];
       t_ts[lane] = L.b.ts[ev];
@@ -210,10 +188,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
       }
       t_nul[lane] = nb;
     }
-    staged_t0 = t0;
-    staged_q = q;
     __syncthreads();
-    }
     for (int te = 0; te < cnt; ++te) {
       const Ev ev{t_ts[te], t_seq[te], &t_w[0][te], 64, t_nul[te]};
       if (st == 0) {  // e1: every passing lane opens a partial (and a non-every start disarms)
@@ -292,11 +267,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     }
     __syncthreads();  // the tile is rewritten next
   }
+  o.close();
   if (lds_over) {  // only e1 items grow (they emit nothing)
     outgrown();
     return;
   }
   if (lane == 0 && n_old) atomicAdd(&L.traffic[item & 255], (unsigned long long)n_old * EW * 4);
+  if (nrec) atomicAdd(L.rec_count, nrec);
+  if (o.over) atomicOr(&L.err[2], 1);
   if (!__ballot(changed)) return;
   // write-back: the lane's surviving entries (old ones still in a list, markers) then its new ones
   int m_l = 0, parts_old = 0, parts_new = 0;
@@ -359,11 +337,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     L.dir[dir_idx] = dnew;
     if (pn != po) atomicAdd((unsigned long long*)&L.live[item & 255], (unsigned long long)(long long)(pn - po));
   }
-  };
-  for (int j = j0; j < j1; ++j) one(seg * L.n_glist + j, L.glist[j], sh_dir[j - j0]);
-  o.close();
-  if (nrec) atomicAdd(L.rec_count, nrec);
-  if (o.over) atomicOr(&L.err[2], 1);
 }
 
 // A failed push: every directory entry the kernel replaced gets its old value back (the old blocks

@@ -451,9 +451,7 @@ struct SlabLaunch {
   int32_t defer_cap;          // two-tier LDS: room in defer (0: no deferral, an oversized block sets err[0])
   int32_t* defer;             // items whose block outgrew this launch's LDS rows (re-run with more LDS)
   int32_t* defer_n;
-  const int32_t* item_list;   // the deferred launch: its items, one per wave (nullptr: runs)
-  int32_t run;                // groups per wave: wave w takes segment w / ceil(n_glist / run), its run
-                              // w % ceil(n_glist / run) of glist (n_items counts waves)
+  const int32_t* item_list;   // the deferred launch: its items (nullptr: items 0 .. n_items-1)
 };
 
 // ------------------------------------------------------------------------------------------

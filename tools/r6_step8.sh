@@ -9,3 +9,4 @@ for w in c5 c3; do
     python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], sys.argv[3], d['ms_per_step'], d['roofline']['kernel_ms'])" gpurun_out/r5vs6/${w}_$run.json $w $run
   done
 done
+bash tools/ab_knob.sh c5 "" "SDH_SLAB_PREFETCH=1"
