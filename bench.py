@@ -382,15 +382,19 @@ def reduce_run(elapsed, matches, pe, live, world, dist, cdev):
 
 
 def launches_per_step(prof, prof_dir):
-    """Launches of the profiled kernel per bench step: its rocprof call count over the steps the
-    profiled run took (warm-up included), as its own bench line recorded them in meta.json (older
-    profiles: the recorded arguments, with bench.py's defaults and C5's forced warm-up)."""
+    """Launches of the profiled kernel per bench step: its rocprof call count over the pushes the
+    profiled run made (warm-up included, as its own bench line recorded them in meta.json) plus the
+    passes it re-ran (meta `reruns`: a push whose output or state outgrew its buffers is undone and
+    launched again -- in the warm-up, as the buffers grow once), times the pushes per step (C5: one per
+    stream). Older profiles: the recorded arguments, with bench.py's defaults and C5's forced warm-up."""
     if not prof:
         return 1
     try:
         meta = json.load(open(os.path.join(ROOT, prof_dir, "meta.json")))
         if meta.get("steps") is not None and meta.get("warmup") is not None:
-            return prof["calls"] / (int(meta["steps"]) + int(meta["warmup"]))
+            per = 4 if meta.get("workload") == "c5" else 1
+            pushes = (int(meta["steps"]) + int(meta["warmup"])) * per
+            return prof["calls"] * per / (pushes + int(meta.get("reruns", 0)))
         a = meta["bench_args"].split()
         steps = int(a[a.index("--steps") + 1]) if "--steps" in a else 12
         warm = int(a[a.index("--warmup") + 1]) if "--warmup" in a else 2

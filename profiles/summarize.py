@@ -20,6 +20,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import os
 import shutil
 import subprocess
@@ -64,12 +65,16 @@ def main(src, dst, kernel, workload, patterns, batch):
         commit = ""
     # the profiled run's own bench line: the steps and the warm-up it really ran (C5 forces a longer
     # warm-up than its arguments say), so bench.py divides the call count by the real step count
-    line = {}
+    # and the passes it re-ran (an output / capacity overflow undoes a pass and launches it again:
+    # SDH_TRACE prints one line per attempt), so that re-run launches are not counted as per-step work
+    line, reruns = {}, 0
     for ln in open(os.path.join(src, "trace.log"), errors="replace"):
         if ln.startswith('{"metric"'):
             line = json.loads(ln)
+        elif re.match(r"\[sdh\] (ratchet|gen pass) .*attempt [1-9]", ln):
+            reruns += 1
     meta = {"source_hash": open(os.path.join(src, "source_hash")).read().strip(),
-            "steps": line.get("steps"), "warmup": line.get("warmup"),
+            "steps": line.get("steps"), "warmup": line.get("warmup"), "reruns": reruns,
             "bench_args": open(os.path.join(src, "args")).read().strip(), "commit_base": commit,
             "workload": workload, "patterns": int(patterns), "batch": int(batch),
             "kernels": {kernel: d}}

@@ -36,3 +36,17 @@ def test_gpus_n_without_gpus_fails():
 def test_world_size_must_equal_gpus():
     r = _run(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_launches_per_step_leaves_reruns_out(tmp_path):
+    """A profiled run's re-run passes (SDH_TRACE attempt lines, counted into meta.json by
+    profiles/summarize.py) are not per-step work: C2 2 + 1 pushes with one re-run launch -> 1 launch
+    per step; C5 4 pushes per step with 2 launches each and one re-run pass."""
+    import json
+    import bench
+    (tmp_path / "meta.json").write_text(json.dumps({"steps": 2, "warmup": 1, "reruns": 1, "workload": "c2"}))
+    assert bench.launches_per_step({"calls": 4}, str(tmp_path)) == 1.0
+    (tmp_path / "meta.json").write_text(json.dumps({"steps": 2, "warmup": 1, "reruns": 1, "workload": "c5"}))
+    assert bench.launches_per_step({"calls": 26}, str(tmp_path)) == 8.0
+    (tmp_path / "meta.json").write_text(json.dumps({"steps": 3, "warmup": 1, "workload": "c3"}))
+    assert bench.launches_per_step({"calls": 12}, str(tmp_path)) == 3.0

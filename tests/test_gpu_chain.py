@@ -31,7 +31,7 @@ def test_c2_synthetic_parity(chunk):
     src = c2_app(24)
     o = App(src)
     g = hip_app(src, chunk_events=chunk, partials=256)
-    for start, n in ((0, 7000), (7000, 30000)):
+    for start, n in ((0, 7000), (7000, 14000)):
         ts, cols = c2_columns(start, n)
         vals = np.stack([c.astype(np.int64) if c.dtype != np.uint32 else c.astype(np.int64) for c in cols], 1)
         o.engine.send(0, ts, vals, None)

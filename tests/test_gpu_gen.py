@@ -403,17 +403,17 @@ def test_device_matches_ring_counts_every_record():
 
     app = App(c2_app(64), engine_factory=lambda blob: None)
     types = [s.attr_types for s in app.ir.streams]
-    ts, sym, price, vol = stock_events(0, 60_000)
+    ts, sym, price, vol = stock_events(0, 40_000)
     vals = np.stack([sym.astype(np.int64), price.view(np.uint32).astype(np.int64), vol.astype(np.int64)], 1)
     ring = HipEngine(app.blob, stream_types=types, flags=SDH_FLAG_FORCE_GEN | SDH_FLAG_DEVICE_MATCHES)
-    ring.send(0, ts, vals, None)  # ~1.8M records x 11 words: past the initial 4M-word buffer
+    ring.send(0, ts, vals, None)  # ~1.2M records x 11 words: past the initial 4M-word buffer
     rec = ring.poll_records()
     normal = HipEngine(app.blob, stream_types=types, flags=SDH_FLAG_FORCE_GEN)
     for b in range(0, len(ts), 10000):
         normal.send(0, ts[b:b + 10000], vals[b:b + 10000], None)
         normal.poll()
     n = ring.stats().matches
-    assert n > 1_000_000
+    assert n > 500_000
     assert n == normal.stats().matches == rec.f_n
 
 

@@ -49,7 +49,7 @@ def _c2_oracle_batches(n_pat, sizes):
 @pytest.mark.parametrize("chunk", [0, 512])
 def test_c2_ratchet_vs_oracle_and_chain(chunk):
     src = c2_app(70)  # two wave groups, the second one partial
-    sizes = (3000, 1, 12000, 777)
+    sizes = (3000, 1, 7000, 777)
     want = _c2_oracle_batches(70, sizes)
     r = hip_app(src, chunk_events=chunk)
     c = hip_app(src, chunk_events=chunk, partials=256, flags=SDH_FLAG_NO_RATCHET)
@@ -176,13 +176,13 @@ def test_ratchet_unordered_timestamps_exact():
     src = c2_app(70)
     o = App(src)
     g = hip_app(src, chunk_events=1024)
-    ts, cols = c2_columns(0, 16000)
+    ts, cols = c2_columns(0, 12000)
     ts = ts.copy()
     ts[9000:9050] -= 20000
     o.engine.send(0, ts, words(cols), None)
     g.engine.push_columns(0, ts, cols)
     assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2)
-    ts2, cols2 = c2_columns(16000, 5000)
+    ts2, cols2 = c2_columns(12000, 5000)
     o.engine.send(0, ts2, words(cols2), None)
     g.engine.push_columns(0, ts2, cols2)
     assert g.engine.take_matches(lambda q: 2) == o.engine.take_matches(lambda q: 2)

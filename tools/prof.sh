@@ -1,6 +1,8 @@
 # rocprofv3 kernel trace + PMC passes of one bench workload (profiles/collect.sh), summarised into
 # gpurun_out/<tag>_<w> (copied to profiles/<tag>_<w> when committed). Usage: tools/prof.sh <tag> c2 c3 c4 c5 c2x
 set -o pipefail
+# one stderr line per launch attempt, so summarize.py can leave re-run launches out of the per-step count
+export SIDDHI_HIP_DEBUG="SDH_TRACE=1"
 tag=$1; shift
 for w in $*; do
   case $w in
