@@ -118,10 +118,11 @@ struct LaneOut {
 // Device records (SDH_FLAG_DEVICE_MATCHES) reserve SDH_RING_CHUNK buffers' worth of the buffer per
 // atomic: the flush's round trip on the chip-wide counter stalls the whole wave (C3 chunk 1: 23.4
 // ms/step, 4: 20.7, 16: 20.7; C4 27.3 / 25.9 / 26.1). The unused tail of a run becomes a pad record.
+// CHUNK 1 (K_slab: a wave flushes about once, a few records) reserves exactly what each flush needs.
 #ifndef SDH_RING_CHUNK
 #define SDH_RING_CHUNK 4
 #endif
-template <int CAPW_, bool SWZ = false>
+template <int CAPW_, bool SWZ = false, int CHUNK = SDH_RING_CHUNK>
 struct WaveOutT {
   static constexpr int CAPW = CAPW_;
   static constexpr int CAPR = CAPW / NREC_MIN_WORDS + 1;  // records (>= 3 words each: the narrow ones)
@@ -180,15 +181,14 @@ struct WaveOutT {
     const int n = ld(sh->used), nr = ld(sh->nrec);
     if (n == 0) return;
     if (__lane_id() == lead) {
-#if SDH_RING_CHUNK > 1
-      // device records: one reservation per SDH_RING_CHUNK buffers' worth of words (a run's unused
-      // tail becomes a pad record)
+      // device records: one reservation per CHUNK buffers' worth of words (a run's unused tail
+      // becomes a pad record)
       unsigned long long o;
-      if (g.ring) {
+      if (CHUNK > 1 && g.ring) {
         if (ld(sh->cleft) < n) {
           g.pad(ld(sh->cbase), ld(sh->cleft));
-          st(sh->cbase, (int64_t)atomicAdd(g.next, (unsigned long long)(SDH_RING_CHUNK * CAPW)));
-          st(sh->cleft, (int64_t)(SDH_RING_CHUNK * CAPW));
+          st(sh->cbase, (int64_t)atomicAdd(g.next, (unsigned long long)(CHUNK * CAPW)));
+          st(sh->cleft, (int64_t)(CHUNK * CAPW));
         }
         o = (unsigned long long)ld(sh->cbase);
         st(sh->cbase, ld(sh->cbase) + n);
@@ -196,9 +196,6 @@ struct WaveOutT {
       } else {
         o = atomicAdd(g.next, (unsigned long long)n);
       }
-#else
-      const unsigned long long o = atomicAdd(g.next, (unsigned long long)n);
-#endif
       int64_t base = (int64_t)o, rbase = 0;
       if ((int64_t)(o + n) > g.cap) base = -1;
       if (!g.ring) {
@@ -316,10 +313,10 @@ struct WaveOutT {
   }
   __device__ void close() {
     flush();
-#if SDH_RING_CHUNK > 1
-    if (g.ring && __lane_id() == __ffsll((long long)active()) - 1) g.pad(ld(sh->cbase), ld(sh->cleft));
-    wave_fence();
-#endif
+    if (CHUNK > 1) {
+      if (g.ring && __lane_id() == __ffsll((long long)active()) - 1) g.pad(ld(sh->cbase), ld(sh->cleft));
+      wave_fence();
+    }
     over |= g.over;
   }
 };

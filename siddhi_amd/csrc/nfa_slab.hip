@@ -30,8 +30,10 @@
 
 namespace sdh {
 
-// (C5 emits ~0.6 records per work item: a small output buffer leaves LDS for resident waves)
-using SlabWaveOut = dev::WaveOutT<256>;
+// (C5 emits ~0.6 records per work item: a small output buffer leaves LDS for resident waves, and
+// device records take exact reservations -- a 4-buffer chunk per emitting wave left ~490 B of pad
+// per C5 match in the flat record buffer)
+using SlabWaveOut = dev::WaveOutT<256, false, 1>;
 
 namespace {
 

@@ -11,6 +11,6 @@ for w in c3 c4 c2x; do
   tail -1 gpurun_out/line_$w.log | cut -c1-300
 done
 if [ "$1" = c5 ]; then
-  timeout -k 10 700 python -u bench.py --workload c5 > gpurun_out/line_c5.log 2> gpurun_out/line_c5.err || { tail -20 gpurun_out/line_c5.err; exit 1; }
+  timeout -k 10 900 python -u bench.py --workload c5 > gpurun_out/line_c5.log 2> gpurun_out/line_c5.err || { tail -20 gpurun_out/line_c5.err; exit 1; }
   tail -1 gpurun_out/line_c5.log | cut -c1-300
 fi
