@@ -1340,8 +1340,13 @@ int bits_of(uint64_t v) {
 // the ABI output arrays in HBM for n matches of tw words (po_*; off and len have n + 1 entries)
 // (at least 64K rows: a window that edges past the last size would otherwise reallocate -- a
 // device allocation inside the poll, the p99 of small pushes)
+// An eighth more than asked: the first window sizes the buffers exactly otherwise, and the next one
+// a few matches larger reallocated them inside the poll (C2's 64K-push leg: one poll of 226 ms among
+// 4.7-ms ones, a hipFree + hipMalloc of ~20 GB)
 constexpr int64_t POLL_MIN_ROWS = 1 << 16;
 void poll_reserve(sdh_engine* e, int64_t n, int64_t tw) {
+  n += n / 8;
+  tw += tw / 8;
   const size_t m = (size_t)std::max<int64_t>(n, POLL_MIN_ROWS);
   tw = std::max<int64_t>(tw, 4 * POLL_MIN_ROWS);
   n = std::max<int64_t>(n, POLL_MIN_ROWS);
@@ -3697,7 +3702,7 @@ int64_t poll_sorted(sdh_engine* e, int64_t* tw, const int* kw_spec = nullptr) {
   } else if (e->mt.n > 0) {
     n = e->mt.n;
     const int32_t* perm = table_order(e, tw);
-    e->po_words.ensure((size_t)std::max<int64_t>(*tw, 1));
+    e->po_words.ensure((size_t)std::max<int64_t>(*tw + *tw / 8, 1));  // (headroom: poll_reserve)
     HIPCHK(sdh_poll_words(table_view(e), perm, n, e->po_off.p, e->po_words.p, e->stream));
     if (kw)
       HIPCHK(sdh_merge_keys_table(table_view(e), perm, n, kw_spec[0], kw_spec[1], e->mt.chunked ? 1 : 0, e->x_keys.p,

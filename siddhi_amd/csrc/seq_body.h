@@ -17,17 +17,33 @@ constexpr int SEQ_TILE = 64;
 constexpr int SEQ_ROW = 3 + kg::GMAXNA;  // ts, seq, null bits, raw words (the widest row)
 
 // a window over LDS rows of ROW words; a Spec sets kRow = 3 + the attributes its shape captures (the
-// LDS a wave takes bounds the resident waves: C4's rows are 5 words, not 11)
-template <int ROW>
+// LDS a wave takes bounds the resident waves: C4's rows are 5 words, not 11).
+// CLEAN: the tile has no null attribute and its timestamps are ordered and span no more than any
+// lane's `within` -- no null test and no expiry test can fail, so both fold away. The window rows
+// are wave-uniform, so those tests ran on the scalar unit (per start: a 64-bit |ts_i - ts_0| and a
+// bit test per attribute read), which bound K_seq at ~78 % SALU issue.
+template <int ROW, bool CLEAN = false>
 struct LdsWinT {
   static constexpr bool kStagedConsts = false;
   const int64_t* base;  // row of window event 0
   __device__ int64_t lane_const(int) const { return 0; }
   __device__ int64_t ts(int p) const { return base[p * ROW]; }
   __device__ int64_t raw(int p, int j, bool = false) const { return base[p * ROW + 3 + j]; }
-  __device__ bool null(int p, int j, bool = false) const { return (base[p * ROW + 2] >> j) & 1; }
+  __device__ bool null(int p, int j, bool = false) const {
+    if constexpr (CLEAN) return false;
+    else return (base[p * ROW + 2] >> j) & 1;
+  }
+  // state i's event more than `within` from the start event (StreamPreStateProcessor.isExpired)
+  __device__ bool exp(int i, int64_t within) const {
+    if constexpr (CLEAN) return false;
+    else return dev::expired(ts(0), ts(i), within);
+  }
 };
 using LdsWin = LdsWinT<SEQ_ROW>;
+template <bool B>
+struct SeqClean {
+  static constexpr bool value = B;
+};
 
 template <class Spec>
 __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
@@ -49,6 +65,12 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
   const int na = q->n_cap[stream];
   const int64_t within = ql->within;
   const int64_t qid = ql->qid;  // (a per-lane load in the loop would wait for the record stores)
+  // the smallest `within` of the wave's live lanes (none: INT64_MAX), for the clean-tile test
+  int64_t wmin = (qi >= 0 && within >= 0) ? within : INT64_MAX;
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t y = __shfl_xor(wmin, o);
+    wmin = y < wmin ? y : wmin;
+  }
   // window index w: tail rows 0 .. tail_len-1, then batch event w - tail_len. Start s is evaluated
   // by the batch holding its last event s + S - 1.
   const int64_t W = L.tail_len + L.b.n;
@@ -170,7 +192,18 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
     const int cnt = hi - t0 < SEQ_TILE ? (int)(hi - t0) : SEQ_TILE;
     if (t0 + lane < rows_end) put(lane, ra);
     if (lane < S - 1 && t0 + 64 + lane < rows_end) put(64 + lane, rb);
+    // a clean tile (LdsWinT): no null bit in the rows its starts read, timestamps ordered, span <= wmin
+    const bool nulls = __ballot((t0 + lane < rows_end && ra.nb != 0) ||
+                                (lane < S - 1 && t0 + 64 + lane < rows_end && rb.nb != 0)) != 0;
     __syncthreads();
+    const int nrows = cnt + S - 1;  // (rows_end bounds them: the chunk's starts read up to hi + S - 2)
+    bool clean = false;
+    if (!nulls) {
+      bool bad = false;
+      for (int p = lane; p + 1 < nrows; p += 64) bad |= win[(p + 1) * ROW] < win[p * ROW];
+      // (ordered rows: last >= first, so the difference is exact as unsigned)
+      clean = __ballot(bad) == 0 && (uint64_t)win[(nrows - 1) * ROW] - (uint64_t)win[0] <= (uint64_t)wmin;
+    }
     const int64_t t1 = t0 + SEQ_TILE;  // prefetch the next tile's rows
     if (t1 < hi) {
       if (t1 + lane < rows_end) fetch(t1 + lane, ra);
@@ -180,16 +213,20 @@ __device__ __forceinline__ void seq_body(const SeqLaunch& L) {
       if constexpr (Spec::kBranchFree) {
         // 8 starts at a time, every state of each evaluated: their LDS reads overlap; starts past
         // cnt read rows of the LDS window that are stale or unset, and are masked off
-        uint64_t m = 0;
-        for (int s0 = 0; s0 < cnt; s0 += 8) {
-          uint32_t m8 = 0;
+        auto tile = [&](auto c) {
+          using W = LdsWinT<ROW, decltype(c)::value>;
+          uint64_t m = 0;
+          for (int s0 = 0; s0 < cnt; s0 += 8) {
+            uint32_t m8 = 0;
 #pragma unroll
-          for (int u = 0; u < 8; ++u)
-            m8 |= (Spec::match(k, q, ql, within, Win{win + (s0 + u) * ROW}) ? 1u : 0u) << u;
-          m |= (uint64_t)m8 << s0;
-        }
-        if (cnt < 64) m &= (1ull << cnt) - 1ull;
-        emit_tile(m);
+            for (int u = 0; u < 8; ++u)
+              m8 |= (Spec::match(k, q, ql, within, W{win + (s0 + u) * ROW}) ? 1u : 0u) << u;
+            m |= (uint64_t)m8 << s0;
+          }
+          if (cnt < 64) m &= (1ull << cnt) - 1ull;
+          return m;
+        };
+        emit_tile(clean ? tile(SeqClean<true>{}) : tile(SeqClean<false>{}));
       } else {
         for (int s = 0; s < cnt; ++s)
           if (Spec::match(k, q, ql, within, Win{win + s * ROW})) emit(s);

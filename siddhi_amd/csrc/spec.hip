@@ -168,7 +168,7 @@ std::string seq_source(const kg::GQuery& g, int out_w) {
   std::string body;
   for (int i = 0; i < g.n_states; ++i) {
     body += fmt("    // state %d\n", i);
-    if (i >= 1 && g.within >= 0) body += fmt("    ok = ok & !sdh::dev::expired(w.ts(0), w.ts(%d), within);\n", i);
+    if (i >= 1 && g.within >= 0) body += fmt("    ok = ok & !w.exp(%d, within);\n", i);
     const kg::GState& st = g.st[i];
     for (int f = 0; f < st.n_filt; ++f) {
       auto here = [i](const kg::GInsn& in) { return in.a <= i && (in.b == 0 || in.b == -1); };

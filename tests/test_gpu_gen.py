@@ -455,3 +455,40 @@ def test_journal_budget_splits_the_push_exactly():
             gm = g.engine.take_matches(lambda q: 3)
             assert gm == om and len(om) > 50
     assert g.engine.stats().pool_regrows > 0
+
+
+def test_seq_windows_compiled_unclean_tiles():
+    """The shape-compiled K_seq kernel (>= 2 waves of one shape) on tiles that are not clean
+    (seq_body.h LdsWinT: a clean tile has no null, ordered timestamps and a span within every lane's
+    `within`, and skips those tests): null amounts, windows of a few ms shorter than a tile's span,
+    out-of-order timestamps, and clean tiles between them (the first wave's lanes wait an hour),
+    against the oracle push by push."""
+    from siddhi_amd.workloads import TXN_STREAM, txn_events
+    qs = [TXN_STREAM]
+    for p in range(130):
+        w = "1 hour" if p < 64 else f"{(2, 3, 5)[p % 3]} milliseconds"
+        qs.append(f"@info(name='s{p}') from every e1=Txn[amount > {100 + p % 700}], e2=Txn[amount > e1.amount * 1.05], "
+                  f"e3=Txn[amount > e2.amount and risk > {p % 50}] within {w} select e1.amount as a1 insert into Alerts;")
+    src = " ".join(qs)
+    o, g = App(src), hip_app(src)
+    st = g.engine.stats()
+    assert st.spec_kernels > 0 and st.plan_queries[5] == 130  # (every query on K_seq, compiled)
+    rng = np.random.default_rng(5)
+    lo, t, total = 0, 1_000_000, 0
+    for n, nullp, unord in ((4000, 0.0, False), (3000, 0.02, False), (5000, 0.0, True), (3000, 0.0, False)):
+        _, acc, amt, risk = txn_events(lo, n, n_accounts=500)
+        lo += n
+        ts = t + np.cumsum(rng.integers(0, 3, n)).astype(np.int64)
+        if unord:
+            ts[1000:1010] -= 7
+        t = int(ts.max())
+        an = (rng.random(n) < nullp).astype(np.uint8)
+        vals = np.stack([acc.astype(np.int64), amt.view(np.uint32).astype(np.int64), risk.astype(np.int64)], 1)
+        nulls = np.zeros((n, 3), np.uint8)
+        nulls[:, 1] = an
+        o.engine.send(0, ts, vals, nulls)
+        g.engine.push_columns(0, ts, [acc, amt.view(np.uint32), risk], [None, an, None])
+        om = o.engine.take_matches(lambda q: 3)
+        assert g.engine.take_matches(lambda q: 3) == om
+        total += len(om)
+    assert total > 5000
