@@ -628,9 +628,12 @@ struct DevBuf {
   size_t n = 0;
   // grows by at least half its size (a buffer sized per push or per poll would otherwise be freed and
   // allocated again whenever the count edges up: hipFree synchronises the device, a p99 spike)
+  // The first allocation takes an eighth more than asked: a buffer sized exactly by its first push
+  // or poll reallocated at the next one a few elements larger (C2's 64K-push leg: a 1.1-s poll, eight
+  // ~4-GB hipFree + hipMalloc pairs)
   void ensure(size_t want) {
     if (want <= n) return;
-    const size_t cap = std::max(want, n + n / 2);
+    const size_t cap = std::max(want + want / 8, n + n / 2);
     alloc_trace("ensure", cap * sizeof(T));
     if (p) HIPCHK(hipFree(p));
     p = nullptr;
@@ -647,11 +650,15 @@ struct DevBuf {
   // grow to at least `want` elements keeping the first `keep` (stream-ordered copy)
   void grow_keep(size_t want, size_t keep, hipStream_t s) {
     if (want <= n) return;
-    size_t cap = std::max(want, n * 2);
+    size_t cap = std::max(want + want / 8, n * 2);  // (an eighth more on the first allocation: ensure)
     alloc_trace("grow_keep", cap * sizeof(T));
     T* q = nullptr;
-    if (hipMalloc(&q, cap * sizeof(T)) != hipSuccess)
-      throw Error(SDH_E_CAPACITY, fmt("device memory exhausted growing a %zu-byte buffer", cap * sizeof(T)));
+    if (hipMalloc(&q, cap * sizeof(T)) != hipSuccess) {
+      (void)hipGetLastError();
+      cap = want;
+      if (hipMalloc(&q, cap * sizeof(T)) != hipSuccess)
+        throw Error(SDH_E_CAPACITY, fmt("device memory exhausted growing a %zu-byte buffer", cap * sizeof(T)));
+    }
     if (p && keep) HIPCHK(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
     if (p) HIPCHK(hipFree(p));
@@ -1340,13 +1347,8 @@ int bits_of(uint64_t v) {
 // the ABI output arrays in HBM for n matches of tw words (po_*; off and len have n + 1 entries)
 // (at least 64K rows: a window that edges past the last size would otherwise reallocate -- a
 // device allocation inside the poll, the p99 of small pushes)
-// An eighth more than asked: the first window sizes the buffers exactly otherwise, and the next one
-// a few matches larger reallocated them inside the poll (C2's 64K-push leg: one poll of 226 ms among
-// 4.7-ms ones, a hipFree + hipMalloc of ~20 GB)
 constexpr int64_t POLL_MIN_ROWS = 1 << 16;
 void poll_reserve(sdh_engine* e, int64_t n, int64_t tw) {
-  n += n / 8;
-  tw += tw / 8;
   const size_t m = (size_t)std::max<int64_t>(n, POLL_MIN_ROWS);
   tw = std::max<int64_t>(tw, 4 * POLL_MIN_ROWS);
   n = std::max<int64_t>(n, POLL_MIN_ROWS);
@@ -3702,7 +3704,7 @@ int64_t poll_sorted(sdh_engine* e, int64_t* tw, const int* kw_spec = nullptr) {
   } else if (e->mt.n > 0) {
     n = e->mt.n;
     const int32_t* perm = table_order(e, tw);
-    e->po_words.ensure((size_t)std::max<int64_t>(*tw + *tw / 8, 1));  // (headroom: poll_reserve)
+    e->po_words.ensure((size_t)std::max<int64_t>(*tw, 1));
     HIPCHK(sdh_poll_words(table_view(e), perm, n, e->po_off.p, e->po_words.p, e->stream));
     if (kw)
       HIPCHK(sdh_merge_keys_table(table_view(e), perm, n, kw_spec[0], kw_spec[1], e->mt.chunked ? 1 : 0, e->x_keys.p,
