@@ -691,7 +691,7 @@ def push_latency(args, sh, K, local):
     """Latency of one small push + poll, the JNI seam's granularity (StreamJunction.Receiver.receive(
     Event) / receive(Event[]) chunks, StreamJunction.java:376-389): host-resident events of 1, 64 and
     4,096, normal mode (every match polled to the host in R18 order). Median and p99 over 50 pushes
-    after 5 warm-up pushes (4,096: 10 after 2; at 10K C2 patterns such a push carries ~17M matches),
+    after 5 warm-up pushes (64: 10; 4,096: 10 after 2; at 10K C2 patterns such a push carries ~17M matches),
     continuing one stream; keyed workloads reserve their K keys' state first
     (sdh_engine_reserve_keys). A second engine fed the same pushes polls the compact rows instead
     (sdh_engine_poll_compact_ex to the host: 16 B per C2 match instead of ~72; `compact_*`)."""
@@ -707,7 +707,9 @@ def push_latency(args, sh, K, local):
     compact_ok = True
     for bs in (1, 64, 4096):
         lat, plat, clat, nm = [], [], [], 0
-        warm, reps = (5, 50) if bs < 4096 else (2, 10)
+        # (warm-up: the poll buffers grow to the push size's match counts -- C2's 64-event pushes carry
+        # 0.2-0.4M matches each -- before the timed pushes)
+        warm, reps = (5, 50) if bs == 1 else (10, 50) if bs < 4096 else (2, 10)
         for i in range(warm + reps):
             ts, a, b, c = gen(lo, bs, K)
             lo += bs
@@ -726,6 +728,8 @@ def push_latency(args, sh, K, local):
                 except EngineError:
                     compact_ok = False
             t3 = time.perf_counter()
+            if os.environ.get("BENCH_TRACE_PUSHES"):  # (diagnostics: one stderr line per push)
+                log(f"latency push bs {bs} #{i}: push {(t1 - t0) * 1e3:.3f} ms, poll {(t2 - t1) * 1e3:.3f} ms")
             if i >= warm:
                 lat.append((t2 - t0) * 1e3)
                 plat.append((t1 - t0) * 1e3)

@@ -650,7 +650,9 @@ struct DevBuf {
   // grow to at least `want` elements keeping the first `keep` (stream-ordered copy)
   void grow_keep(size_t want, size_t keep, hipStream_t s) {
     if (want <= n) return;
-    size_t cap = std::max(want + want / 8, n * 2);  // (an eighth more on the first allocation: ensure)
+    // (an eighth more on the first allocation, as ensure; and at least 1 MB: growing state tables of a
+    // few hundred KB doubled inside small pushes -- C2's 1-event pushes, a 1.1-ms p99)
+    size_t cap = std::max(std::max(want + want / 8, n * 2), ((size_t)1 << 20) / sizeof(T));
     alloc_trace("grow_keep", cap * sizeof(T));
     T* q = nullptr;
     if (hipMalloc(&q, cap * sizeof(T)) != hipSuccess) {
@@ -679,7 +681,7 @@ struct HostBuf {
   void ensure(size_t want) {
     if (want <= n) return;
     release();
-    const size_t cap = std::max(want, n * 2);
+    const size_t cap = std::max(want + want / 8, n * 2);  // (an eighth of headroom, as DevBuf)
     alloc_trace("host", cap * sizeof(T));
     if (hipHostMalloc((void**)&p, cap * sizeof(T), hipHostMallocDefault) == hipSuccess) {
       pinned = true;
